@@ -1,0 +1,229 @@
+"""ctypes binding of the CPU ORACLE (oracle/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, as the checker or the timed CPU baseline -- never by the product
+(ransac_amd/).  See oracle/usac_oracle.h for what it restates and how it is pinned.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+
+LINE2D, HOMOGRAPHY, FUNDAMENTAL, ESSENTIAL = 1, 2, 3, 4
+DLT_THIN, DLT_NULLSPACE = 0, 1
+
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i32p = ctypes.POINTER(ctypes.c_int)
+_u32p = ctypes.POINTER(ctypes.c_uint)
+
+
+class OrcResult(ctypes.Structure):
+    _fields_ = [
+        ("model", ctypes.c_float * 9),
+        ("inliers", ctypes.c_int),
+        ("iters", ctypes.c_uint),
+        ("n_records", ctypes.c_int),
+        ("polish_passes", ctypes.c_int),
+        ("minimal_model", ctypes.c_float * 9),
+        ("minimal_inliers", ctypes.c_int),
+    ]
+
+
+def build():
+    """Compile the oracle with its own Makefile (plain gcc)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.orc_random.restype = ctypes.c_long
+        L.orc_uniform_new.restype = ctypes.c_void_p
+        L.orc_uniform_new.argtypes = [ctypes.c_uint, ctypes.c_uint]
+        L.orc_uniform_free.argtypes = [ctypes.c_void_p]
+        L.orc_uniform_samples.argtypes = [ctypes.c_void_p, _i32p, ctypes.c_int]
+        L.orc_est_new.restype = ctypes.c_void_p
+        L.orc_est_new.argtypes = [ctypes.c_int, _f32p, ctypes.c_uint, ctypes.c_int]
+        L.orc_est_free.argtypes = [ctypes.c_void_p]
+        L.orc_est_estimate.argtypes = [ctypes.c_void_p, _i32p, _f32p]
+        L.orc_est_nonminimal.argtypes = [ctypes.c_void_p, _i32p, ctypes.c_uint, _f32p]
+        L.orc_est_set_model.argtypes = [ctypes.c_void_p, _f32p]
+        L.orc_est_error.argtypes = [ctypes.c_void_p, ctypes.c_uint]
+        L.orc_est_error.restype = ctypes.c_float
+        L.orc_inv3x3.argtypes = [_f32p, _f32p]
+        L.orc_quality.argtypes = [ctypes.c_void_p, _f32p, ctypes.c_float, _i32p, _f32p, _i32p]
+        L.orc_score_models.argtypes = [ctypes.c_void_p, _f32p, ctypes.c_int, ctypes.c_float, _i32p, _f32p]
+        L.orc_estimate_batch.argtypes = [ctypes.c_void_p, _i32p, ctypes.c_int, _f32p, _i32p]
+        L.orc_gt_inliers_homography.argtypes = [_f32p, ctypes.c_uint, _f32p, ctypes.c_float]
+        L.orc_std_termination.argtypes = [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, ctypes.c_float, ctypes.c_uint]
+        L.orc_std_termination.restype = ctypes.c_uint
+        L.orc_ransac_run.argtypes = [ctypes.c_int, _f32p, ctypes.c_uint, ctypes.c_float, ctypes.c_float,
+                                     ctypes.c_uint, ctypes.c_uint, ctypes.c_int, ctypes.POINTER(OrcResult),
+                                     _i32p, _u32p, _i32p, _f32p, ctypes.c_int]
+        L.orc_hypothesis_loop.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_float, _f32p]
+        L.orc_generate_line2d.argtypes = [ctypes.c_uint, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, _f32p, _f32p]
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def glibc_stream(seed, n):
+    L = lib()
+    L.orc_srandom(ctypes.c_uint(seed))
+    return np.array([L.orc_random() for _ in range(n)], dtype=np.int64)
+
+
+def uniform_samples(seed, n_points, m, count):
+    """glibc-seeded UniformSampler stream: count x m int32."""
+    L = lib()
+    L.orc_srandom(ctypes.c_uint(seed))
+    s = L.orc_uniform_new(n_points, m)
+    out = np.zeros((count, m), dtype=np.int32)
+    L.orc_uniform_samples(s, _p(out, _i32p), count)
+    L.orc_uniform_free(s)
+    return out
+
+
+class Estimator:
+    def __init__(self, kind, points, dlt_mode=DLT_THIN):
+        self.points = np.ascontiguousarray(points, dtype=np.float32)
+        self.kind = kind
+        self.n = self.points.shape[0]
+        self._h = lib().orc_est_new(kind, _p(self.points, _f32p), self.n, dlt_mode)
+        if not self._h:
+            raise ValueError("oracle: unsupported estimator %r" % kind)
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            lib().orc_est_free(self._h)
+            self._h = None
+
+    @property
+    def m(self):
+        return 2 if self.kind == LINE2D else 4
+
+    def estimate(self, sample):
+        sample = np.ascontiguousarray(sample, dtype=np.int32)
+        out = np.zeros(27, dtype=np.float32)
+        k = lib().orc_est_estimate(self._h, _p(sample, _i32p), _p(out, _f32p))
+        return out[: 9 * k].reshape(k, 9)
+
+    def estimate_batch(self, samples):
+        samples = np.ascontiguousarray(samples, dtype=np.int32)
+        B = samples.shape[0]
+        models = np.zeros((B, 9), dtype=np.float32)
+        nm = np.zeros(B, dtype=np.int32)
+        lib().orc_estimate_batch(self._h, _p(samples, _i32p), B, _p(models, _f32p), _p(nm, _i32p))
+        return models, nm
+
+    def nonminimal(self, idx):
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        out = np.zeros(9, dtype=np.float32)
+        ok = lib().orc_est_nonminimal(self._h, _p(idx, _i32p), len(idx), _p(out, _f32p))
+        return out if ok else None
+
+    def errors(self, model):
+        model = np.ascontiguousarray(model, dtype=np.float32).reshape(-1)
+        full = np.zeros(9, dtype=np.float32)
+        full[: model.size] = model
+        L = lib()
+        L.orc_est_set_model(self._h, _p(full, _f32p))
+        return np.array([L.orc_est_error(self._h, i) for i in range(self.n)], dtype=np.float32)
+
+    def quality(self, model, thr, with_inliers=False):
+        model = np.ascontiguousarray(model, dtype=np.float32).reshape(-1)
+        full = np.zeros(9, dtype=np.float32)
+        full[: model.size] = model
+        cnt = ctypes.c_int(0)
+        s = ctypes.c_float(0)
+        inl = np.zeros(max(self.n, 1), dtype=np.int32) if with_inliers else None
+        lib().orc_quality(self._h, _p(full, _f32p), ctypes.c_float(thr), ctypes.byref(cnt), ctypes.byref(s),
+                          _p(inl, _i32p) if inl is not None else None)
+        if with_inliers:
+            return cnt.value, s.value, inl[: cnt.value].copy()
+        return cnt.value, s.value
+
+    def score_models(self, models, thr):
+        models = np.ascontiguousarray(models, dtype=np.float32).reshape(-1, 9)
+        n = models.shape[0]
+        c = np.zeros(n, dtype=np.int32)
+        s = np.zeros(n, dtype=np.float32)
+        lib().orc_score_models(self._h, _p(models, _f32p), n, ctypes.c_float(thr), _p(c, _i32p), _p(s, _f32p))
+        return c, s
+
+
+def inv3x3(m):
+    m = np.ascontiguousarray(m, dtype=np.float32).reshape(9)
+    out = np.zeros(9, dtype=np.float32)
+    ok = lib().orc_inv3x3(_p(m, _f32p), _p(out, _f32p))
+    return out, bool(ok)
+
+
+def gt_inliers_homography(points, model, thr):
+    points = np.ascontiguousarray(points, dtype=np.float32)
+    model = np.ascontiguousarray(model, dtype=np.float32).reshape(9)
+    return lib().orc_gt_inliers_homography(_p(points, _f32p), points.shape[0], _p(model, _f32p),
+                                           ctypes.c_float(thr))
+
+
+def std_termination(inliers, n, m, p, max_iters=10000):
+    return lib().orc_std_termination(inliers, n, m, ctypes.c_float(p), max_iters)
+
+
+def ransac_run(kind, points, thr, p, seed, max_iters=10000, dlt_mode=DLT_THIN, rec_cap=4096):
+    points = np.ascontiguousarray(points, dtype=np.float32)
+    n = points.shape[0]
+    res = OrcResult()
+    inl = np.zeros(max(n, 1), dtype=np.int32)
+    ri = np.zeros(rec_cap, dtype=np.uint32)
+    rc = np.zeros(rec_cap, dtype=np.int32)
+    rs = np.zeros(rec_cap, dtype=np.float32)
+    ret = lib().orc_ransac_run(kind, _p(points, _f32p), n, ctypes.c_float(thr), ctypes.c_float(p), max_iters,
+                               seed, dlt_mode, ctypes.byref(res), _p(inl, _i32p), _p(ri, _u32p), _p(rc, _i32p),
+                               _p(rs, _f32p), rec_cap)
+    k = min(res.n_records, rec_cap)
+    return {
+        "ret": ret,
+        "model": np.array(res.model[:], dtype=np.float32),
+        "inliers": res.inliers,
+        "iters": res.iters,
+        "polish_passes": res.polish_passes,
+        "minimal_model": np.array(res.minimal_model[:], dtype=np.float32),
+        "minimal_inliers": res.minimal_inliers,
+        "inlier_idx": inl[: res.inliers].copy() if ret == 0 else np.zeros(0, np.int32),
+        "records": list(zip(ri[:k].tolist(), rc[:k].tolist(), rs[:k].tolist())),
+    }
+
+
+def hypothesis_loop(kind, points, thr, seed, count, dlt_mode=DLT_THIN):
+    """Reference-style sample+solve+score loop for `count` hypotheses (CPU baseline)."""
+    est = Estimator(kind, points, dlt_mode)
+    L = lib()
+    L.orc_srandom(ctypes.c_uint(seed))
+    s = L.orc_uniform_new(est.n, est.m)
+    best_sum = ctypes.c_float(0)
+    best = L.orc_hypothesis_loop(est._h, s, count, ctypes.c_float(thr), ctypes.byref(best_sum))
+    L.orc_uniform_free(s)
+    return best, best_sum.value
+
+
+def generate_line2d(seed, noise, inliers, outliers, border_x, border_y):
+    pts = np.zeros((inliers + outliers, 2), dtype=np.float32)
+    gt = np.zeros(3, dtype=np.float32)
+    lib().orc_generate_line2d(seed, ctypes.c_float(noise), inliers, outliers, border_x, border_y,
+                              _p(pts, _f32p), _p(gt, _f32p))
+    return pts, gt

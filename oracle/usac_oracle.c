@@ -1,0 +1,704 @@
+/*
+ * usac_oracle.c -- CPU ORACLE (test infrastructure only; see usac_oracle.h header).
+ *
+ * Plain-C restatement of the reference hot path.  Build: oracle/Makefile
+ * (gcc -O2 -ffp-contract=off, no -march: x86-64 SSE2 scalar fp32/fp64, no FMA,
+ * matching the reference's CMake build which sets no optimisation/arch flags,
+ * CMakeLists.txt:102-107).
+ *
+ * Floating-point conventions restated from the reference's C++ (g++/libstdc++):
+ *  - unqualified sqrt()/log() on float arguments resolve to the C library's
+ *    double overloads (only <cmath> is included, usac/precomp.hpp:12; no
+ *    `using namespace std`), so e.g. homography_estimator.hpp:97-98 sums two
+ *    double square roots before rounding to float;
+ *  - every fp32 expression is evaluated left to right, one rounding per operation.
+ */
+#define _DEFAULT_SOURCE
+#include "usac_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ glibc stream */
+/* The reference draws with glibc random() (uniform_sampler.hpp:83) and seeds with
+ * srand() (uniform_sampler.hpp:24); glibc's rand/srand share random()'s state. */
+void orc_srandom(unsigned int seed) { srandom(seed); }
+long orc_random(void) { return random(); }
+void orc_random_n(long *out, int n) {
+    for (int i = 0; i < n; i++) out[i] = random();
+}
+
+/* ------------------------------------------------------------ UniformSampler */
+struct orc_uniform {
+    unsigned int *pool;
+    int max;
+    unsigned int points_size, sample_size;
+};
+
+/* uniform_sampler.hpp:32-39 setPointsSize */
+orc_uniform *orc_uniform_new(unsigned int points_size, unsigned int sample_size) {
+    orc_uniform *s = (orc_uniform *)calloc(1, sizeof(*s));
+    s->pool = (unsigned int *)malloc(sizeof(unsigned int) * (points_size ? points_size : 1));
+    for (unsigned int i = 0; i < points_size; i++) s->pool[i] = i;
+    s->max = (int)points_size;
+    s->points_size = points_size;
+    s->sample_size = sample_size;
+    return s;
+}
+void orc_uniform_free(orc_uniform *s) {
+    if (!s) return;
+    free(s->pool);
+    free(s);
+}
+/* uniform_sampler.hpp:42-54 generateSample: persistent pool; `max` refills to N when it
+ * reaches 0, also in the middle of a sample. */
+void orc_uniform_sample(orc_uniform *s, int *sample) {
+    for (unsigned int i = 0; i < s->sample_size; i++) {
+        if (s->max == 0) s->max = (int)s->points_size;
+        unsigned int idx = (unsigned int)random() % (unsigned int)s->max;
+        unsigned int v = s->pool[idx];
+        s->max--;
+        s->pool[idx] = s->pool[s->max];
+        s->pool[s->max] = v;
+        sample[i] = (int)v;
+    }
+}
+void orc_uniform_samples(orc_uniform *s, int *out, int count) {
+    for (int c = 0; c < count; c++) orc_uniform_sample(s, out + (size_t)c * s->sample_size);
+}
+
+/* ------------------------------------------------------------ small linear algebra */
+
+/* cv::Mat::inv() on a CV_32F 3x3 (DECOMP_LU closed form of cv::invert): determinant and
+ * cofactors from exact float*float products in fp64, scaled by 1/det in fp64, cast to
+ * float once.  Singular (det == 0) => zero matrix, returns 0.  Used by
+ * homography_estimator.hpp:35 (setModelParameters), normalized_dlt.cpp:18 (T2.inv()). */
+int orc_inv3x3(const float *m, float *dst) {
+#define M_(r, c) ((double)m[3 * (r) + (c)])
+    double d = M_(0, 0) * (M_(1, 1) * M_(2, 2) - M_(1, 2) * M_(2, 1)) -
+               M_(0, 1) * (M_(1, 0) * M_(2, 2) - M_(1, 2) * M_(2, 0)) +
+               M_(0, 2) * (M_(1, 0) * M_(2, 1) - M_(1, 1) * M_(2, 0));
+    if (d == 0.0) {
+        for (int i = 0; i < 9; i++) dst[i] = 0.f;
+        return 0;
+    }
+    d = 1.0 / d;
+    double t[9];
+    t[0] = (M_(1, 1) * M_(2, 2) - M_(1, 2) * M_(2, 1)) * d;
+    t[1] = (M_(0, 2) * M_(2, 1) - M_(0, 1) * M_(2, 2)) * d;
+    t[2] = (M_(0, 1) * M_(1, 2) - M_(0, 2) * M_(1, 1)) * d;
+    t[3] = (M_(1, 2) * M_(2, 0) - M_(1, 0) * M_(2, 2)) * d;
+    t[4] = (M_(0, 0) * M_(2, 2) - M_(0, 2) * M_(2, 0)) * d;
+    t[5] = (M_(0, 2) * M_(1, 0) - M_(0, 0) * M_(1, 2)) * d;
+    t[6] = (M_(1, 0) * M_(2, 1) - M_(1, 1) * M_(2, 0)) * d;
+    t[7] = (M_(0, 1) * M_(2, 0) - M_(0, 0) * M_(2, 1)) * d;
+    t[8] = (M_(0, 0) * M_(1, 1) - M_(0, 1) * M_(1, 0)) * d;
+#undef M_
+    for (int i = 0; i < 9; i++) dst[i] = (float)t[i];
+    return 1;
+}
+
+/* One-sided (Hestenes) Jacobi on the ROWS of an r x 9 matrix, r <= 9, fp64.
+ * Restates the row space part of cv::SVD::compute (thin, default flags) used by
+ * dlt.cpp:43 / dlt.cpp:92: after convergence the rows are mutually orthogonal,
+ * row_i = sigma_i * v_i^T, so the thin vt's last row (smallest sigma) is the row of
+ * smallest norm.  Fixed algorithm (shared by the GPU kernel's spec):
+ *   sweeps s < 30; pairs p < q in row-major order; alpha, beta, gamma accumulated over
+ *   k = 0..8 in order; skip when |gamma| <= 1e-14 * sqrt(alpha*beta);
+ *   zeta = (beta-alpha)/(2 gamma); t = sign(zeta)/(|zeta| + sqrt(1+zeta^2));
+ *   c = 1/sqrt(1+t^2); s = c*t; row_p <- c*row_p - s*row_q; row_q <- s*row_p + c*row_q;
+ *   stop after a sweep with no rotation. */
+#define ORC_JAC_SWEEPS 30
+#define ORC_JAC_EPS 1e-14
+static void row_jacobi(double W[][9], int r) {
+    for (int sweep = 0; sweep < ORC_JAC_SWEEPS; sweep++) {
+        int rotated = 0;
+        for (int p = 0; p < r - 1; p++) {
+            for (int q = p + 1; q < r; q++) {
+                double a = 0.0, b = 0.0, g = 0.0;
+                for (int k = 0; k < 9; k++) {
+                    a += W[p][k] * W[p][k];
+                    b += W[q][k] * W[q][k];
+                    g += W[p][k] * W[q][k];
+                }
+                if (fabs(g) <= ORC_JAC_EPS * sqrt(a * b)) continue;
+                rotated = 1;
+                double zeta = (b - a) / (2.0 * g);
+                double t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                double c = 1.0 / sqrt(1.0 + t * t);
+                double s = c * t;
+                for (int k = 0; k < 9; k++) {
+                    double wp = W[p][k], wq = W[q][k];
+                    W[p][k] = c * wp - s * wq;
+                    W[q][k] = s * wp + c * wq;
+                }
+            }
+        }
+        if (!rotated) break;
+    }
+}
+
+/* From converged orthogonal rows pick the model vector:
+ *  thin      -> row of smallest squared norm (first on ties) = vt.row(vt.rows-1)
+ *  nullspace -> unit vector orthogonal to every non-zero row (two Gram-Schmidt passes
+ *               starting from the least-represented coordinate axis).
+ * Writes h (9 doubles, unnormalised). */
+static void pick_vector(double W[][9], int r, int mode, double *h) {
+    double n2[9];
+    for (int i = 0; i < r; i++) {
+        double a = 0.0;
+        for (int k = 0; k < 9; k++) a += W[i][k] * W[i][k];
+        n2[i] = a;
+    }
+    if (mode == ORC_DLT_THIN) {
+        int best = 0;
+        for (int i = 1; i < r; i++)
+            if (n2[i] < n2[best]) best = i;
+        for (int k = 0; k < 9; k++) h[k] = W[best][k];
+        return;
+    }
+    double U[9][9];
+    int nu = 0;
+    for (int i = 0; i < r; i++) {
+        if (n2[i] > 0.0) {
+            double inv = 1.0 / sqrt(n2[i]);
+            for (int k = 0; k < 9; k++) U[nu][k] = W[i][k] * inv;
+            nu++;
+        }
+    }
+    int ks = 0;
+    double bestc = 0.0;
+    for (int k = 0; k < 9; k++) {
+        double c = 0.0;
+        for (int i = 0; i < nu; i++) c += U[i][k] * U[i][k];
+        if (k == 0 || c < bestc) {
+            bestc = c;
+            ks = k;
+        }
+    }
+    for (int k = 0; k < 9; k++) h[k] = (k == ks) ? 1.0 : 0.0;
+    for (int pass = 0; pass < 2; pass++) {
+        for (int i = 0; i < nu; i++) {
+            double d = 0.0;
+            for (int k = 0; k < 9; k++) d += U[i][k] * h[k];
+            for (int k = 0; k < 9; k++) h[k] -= d * U[i][k];
+        }
+    }
+}
+
+/* Cyclic two-sided Jacobi eigen-decomposition of a symmetric 9x9 (fp64); returns the
+ * eigenvector of the smallest eigenvalue in v.  Restates cv::SVD::compute's last vt row
+ * for a tall (2n > 9) DLT system via the normal matrix (dlt.cpp:92-98,
+ * eight_points.cpp:38-44). */
+static void sym_eig_min(double A[9][9], double *v) {
+    double V[9][9];
+    for (int i = 0; i < 9; i++)
+        for (int j = 0; j < 9; j++) V[i][j] = (i == j) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 50; sweep++) {
+        double off = 0.0, diag = 0.0;
+        for (int p = 0; p < 9; p++) {
+            diag += A[p][p] * A[p][p];
+            for (int q = p + 1; q < 9; q++) off += A[p][q] * A[p][q];
+        }
+        if (off <= 1e-30 * diag || off == 0.0) break;
+        for (int p = 0; p < 8; p++) {
+            for (int q = p + 1; q < 9; q++) {
+                double apq = A[p][q];
+                if (apq == 0.0) continue;
+                double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
+                double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                for (int k = 0; k < 9; k++) {
+                    double akp = A[k][p], akq = A[k][q];
+                    A[k][p] = c * akp - s * akq;
+                    A[k][q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < 9; k++) {
+                    double apk = A[p][k], aqk = A[q][k];
+                    A[p][k] = c * apk - s * aqk;
+                    A[q][k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < 9; k++) {
+                    double vkp = V[k][p], vkq = V[k][q];
+                    V[k][p] = c * vkp - s * vkq;
+                    V[k][q] = s * vkp + c * vkq;
+                }
+            }
+        }
+    }
+    int m = 0;
+    for (int i = 1; i < 9; i++)
+        if (A[i][i] < A[m][m]) m = i;
+    for (int k = 0; k < 9; k++) v[k] = V[k][m];
+}
+
+/* ------------------------------------------------------------ estimators */
+struct orc_est {
+    int kind;
+    const float *pts;
+    unsigned int n;
+    int dlt_mode;
+    /* cached model parameters (setModelParameters) */
+    float a, b, c;        /* line2d_estimator.hpp:162-164 */
+    float h[9], hi[9];    /* homography_estimator.hpp:33-45 */
+};
+
+orc_est *orc_est_new(int kind, const float *points, unsigned int n, int dlt_mode) {
+    if (kind != ORC_LINE2D && kind != ORC_HOMOGRAPHY) return NULL;
+    orc_est *e = (orc_est *)calloc(1, sizeof(*e));
+    e->kind = kind;
+    e->pts = points;
+    e->n = n;
+    e->dlt_mode = dlt_mode;
+    return e;
+}
+void orc_est_free(orc_est *e) { free(e); }
+int orc_est_sample_size(const orc_est *e) { return e->kind == ORC_LINE2D ? 2 : 4; }
+
+/* DLt::DLT4p (usac/estimator/dlt/dlt.cpp:7-52): rows of A built in fp32 exactly as
+ * dlt.cpp:24-41, SVD restated by row_jacobi; H = v / v[8] rounded once to float. */
+static int dlt_rows_solve(double W[][9], int r, int mode, float *H) {
+    double v[9];
+    row_jacobi(W, r);
+    pick_vector(W, r, mode, v);
+    for (int k = 0; k < 9; k++) H[k] = (float)(v[k] / v[8]);
+    return 1;
+}
+
+static void dlt_fill_rows(float x1, float y1, float x2, float y2, double *r0, double *r1) {
+    float a[9] = {-x1, -y1, -1.f, 0.f, 0.f, 0.f, x2 * x1, x2 * y1, x2};
+    float b[9] = {0.f, 0.f, 0.f, -x1, -y1, -1.f, y2 * x1, y2 * y1, y2};
+    for (int k = 0; k < 9; k++) {
+        r0[k] = (double)a[k];
+        r1[k] = (double)b[k];
+    }
+}
+
+static int homography_dlt4(const orc_est *e, const int *sample, float *H) {
+    double W[8][9];
+    for (int i = 0; i < 4; i++) {
+        const float *p = e->pts + 4 * (size_t)sample[i];
+        dlt_fill_rows(p[0], p[1], p[2], p[3], W[2 * i], W[2 * i + 1]);
+    }
+    return dlt_rows_solve(W, 8, e->dlt_mode, H);
+}
+
+/* GetNormalizingTransformation (normalizing_transformation.cpp:7-113): fp32 sums in
+ * sample order; the distance accumulation adds a double sqrt into a float (:45-46);
+ * scale = M_SQRT2 / (avg / n) in double, rounded to float (:50-51). */
+static void normalizing_transform(const float *pts, const int *sample, unsigned int n, float *T1, float *T2,
+                                  float *norm /* n x 4 */) {
+    float m1x = 0, m1y = 0, m2x = 0, m2y = 0;
+    for (unsigned int i = 0; i < n; i++) {
+        const float *p = pts + 4 * (size_t)sample[i];
+        m1x += p[0];
+        m1y += p[1];
+        m2x += p[2];
+        m2y += p[3];
+    }
+    m1x /= (float)n;
+    m1y /= (float)n;
+    m2x /= (float)n;
+    m2y /= (float)n;
+    float d1 = 0, d2 = 0;
+    for (unsigned int i = 0; i < n; i++) {
+        const float *p = pts + 4 * (size_t)sample[i];
+        float x1m = p[0] - m1x, y1m = p[1] - m1y, x2m = p[2] - m2x, y2m = p[3] - m2y;
+        d1 = (float)((double)d1 + sqrt((double)(x1m * x1m + y1m * y1m)));
+        d2 = (float)((double)d2 + sqrt((double)(x2m * x2m + y2m * y2m)));
+    }
+    float s1 = (float)(M_SQRT2 / (double)(d1 / (float)n));
+    float s2 = (float)(M_SQRT2 / (double)(d2 / (float)n));
+    float t1[9] = {s1, 0.f, -m1x * s1, 0.f, s1, -m1y * s1, 0.f, 0.f, 1.f};
+    float t2[9] = {s2, 0.f, -m2x * s2, 0.f, s2, -m2y * s2, 0.f, 0.f, 1.f};
+    memcpy(T1, t1, sizeof(t1));
+    memcpy(T2, t2, sizeof(t2));
+    for (unsigned int i = 0; i < n; i++) {
+        const float *p = pts + 4 * (size_t)sample[i];
+        norm[4 * i + 0] = T1[0] * p[0] + T1[2];
+        norm[4 * i + 1] = T1[4] * p[1] + T1[5];
+        norm[4 * i + 2] = T2[0] * p[2] + T2[2];
+        norm[4 * i + 3] = T2[4] * p[3] + T2[5];
+    }
+}
+
+/* DLt::NormalizedDLT (normalized_dlt.cpp:7-23): DLT (dlt.cpp:55-101) on the normalised
+ * points, then H = T2^-1 * H * T1, H /= H33.  2n <= 8 rows keep the thin-SVD semantics
+ * (SURVEY Q2); 2n >= 10 rows take the smallest right singular vector via the fp64
+ * normal matrix. */
+static int homography_normalized_dlt(const orc_est *e, const int *sample, unsigned int n, float *H) {
+    if (n == 0) return 0;
+    float T1[9], T2[9], T2i[9];
+    float *norm = (float *)malloc(sizeof(float) * 4 * n);
+    normalizing_transform(e->pts, sample, n, T1, T2, norm);
+    double v[9];
+    if (2 * n <= 9) {
+        double W[9][9];
+        for (unsigned int i = 0; i < n; i++)
+            dlt_fill_rows(norm[4 * i], norm[4 * i + 1], norm[4 * i + 2], norm[4 * i + 3], W[2 * i], W[2 * i + 1]);
+        row_jacobi(W, (int)(2 * n));
+        pick_vector(W, (int)(2 * n), ORC_DLT_THIN, v);
+    } else {
+        double AtA[9][9];
+        memset(AtA, 0, sizeof(AtA));
+        for (unsigned int i = 0; i < n; i++) {
+            double r0[9], r1[9];
+            dlt_fill_rows(norm[4 * i], norm[4 * i + 1], norm[4 * i + 2], norm[4 * i + 3], r0, r1);
+            for (int j = 0; j < 9; j++)
+                for (int k = j; k < 9; k++) AtA[j][k] += r0[j] * r0[k] + r1[j] * r1[k];
+        }
+        for (int j = 0; j < 9; j++)
+            for (int k = 0; k < j; k++) AtA[j][k] = AtA[k][j];
+        sym_eig_min(AtA, v);
+    }
+    free(norm);
+    orc_inv3x3(T2, T2i);
+    /* H = T2i * Hn * T1 in fp64 */
+    double Hn[9], tmp[9], Hd[9];
+    for (int k = 0; k < 9; k++) Hn[k] = v[k];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) {
+            double s = 0.0;
+            for (int k = 0; k < 3; k++) s += Hn[3 * r + k] * (double)T1[3 * k + c];
+            tmp[3 * r + c] = s;
+        }
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) {
+            double s = 0.0;
+            for (int k = 0; k < 3; k++) s += (double)T2i[3 * r + k] * tmp[3 * k + c];
+            Hd[3 * r + c] = s;
+        }
+    for (int k = 0; k < 9; k++) H[k] = (float)(Hd[k] / Hd[8]);
+    return 1;
+}
+
+/* Line2DEstimator::EstimateModel (line2d_estimator.hpp:36-54) */
+static int line2d_estimate(const orc_est *e, const int *sample, float *m) {
+    const float *p1 = e->pts + 2 * (size_t)sample[0];
+    const float *p2 = e->pts + 2 * (size_t)sample[1];
+    float a = p1[1] - p2[1];
+    float b = p2[0] - p1[0];
+    float mag = (float)sqrt((double)(a * a + b * b));
+    a /= mag;
+    b /= mag;
+    float c = (p1[0] * p2[1] - p2[0] * p1[1]) / mag;
+    m[0] = a;
+    m[1] = b;
+    m[2] = c;
+    for (int k = 3; k < 9; k++) m[k] = 0.f;
+    return 1;
+}
+
+/* Line2DEstimator::EstimateModelNonMinimalSample (line2d_estimator.hpp:59-107): PCA
+ * with fp32 moments (sum_xy initialised to 0: SURVEY Q12), cv::eigen of the 2x2
+ * covariance restated in closed form (fp64); the line normal is the eigenvector of the
+ * smaller eigenvalue (sign is irrelevant to |ax+by+c|). */
+static int line2d_nonminimal(const orc_est *e, const int *sample, unsigned int n, float *m) {
+    if (n == 0) return 0;
+    float sx = 0, sy = 0, sxy = 0, sx2 = 0, sy2 = 0;
+    for (unsigned int i = 0; i < n; i++) {
+        const float *p = e->pts + 2 * (size_t)sample[i];
+        float x = p[0], y = p[1];
+        sx += x;
+        sy += y;
+        sxy += x * y;
+        sx2 += x * x;
+        sy2 += y * y;
+    }
+    float fn = (float)n;
+    float mx = sx / fn, my = sy / fn;
+    float c00 = sx2 - 2.f * sx * mx + fn * mx * mx;
+    float c01 = sxy - sx * my - sy * mx + fn * mx * my;
+    float c11 = sy2 - 2.f * sy * my + fn * my * my;
+    double p = c00, q = c11, r = c01;
+    double half = 0.5 * (p - q);
+    double rad = sqrt(half * half + r * r);
+    double lmin = 0.5 * (p + q) - rad;
+    double vx, vy;
+    if (r == 0.0) {
+        if (p <= q) { vx = 1.0; vy = 0.0; } else { vx = 0.0; vy = 1.0; }
+    } else if (fabs(lmin - p) > fabs(lmin - q)) {
+        vx = r; vy = lmin - p;
+    } else {
+        vx = lmin - q; vy = r;
+    }
+    double nrm = sqrt(vx * vx + vy * vy);
+    float a = (float)(vx / nrm), b = (float)(vy / nrm);
+    m[0] = a;
+    m[1] = b;
+    m[2] = -a * mx - b * my;
+    for (int k = 3; k < 9; k++) m[k] = 0.f;
+    return 1;
+}
+
+int orc_est_estimate(orc_est *e, const int *sample, float *models) {
+    if (e->kind == ORC_LINE2D) return line2d_estimate(e, sample, models);
+    return homography_dlt4(e, sample, models);
+}
+
+int orc_est_nonminimal(orc_est *e, const int *sample, unsigned int n, float *model) {
+    if (e->kind == ORC_LINE2D) return line2d_nonminimal(e, sample, n, model);
+    return homography_normalized_dlt(e, sample, n, model);
+}
+
+void orc_est_set_model(orc_est *e, const float *m) {
+    if (e->kind == ORC_LINE2D) {
+        e->a = m[0];
+        e->b = m[1];
+        e->c = m[2];
+    } else {
+        memcpy(e->h, m, sizeof(float) * 9);
+        orc_inv3x3(m, e->hi);
+    }
+}
+
+/* HomographyEstimator::GetError (homography_estimator.hpp:85-110): symmetric transfer
+ * error; fp32 projections (no z guard: SURVEY Q19), the two distances are double
+ * sqrt()s summed in double and rounded to float, then halved. */
+static inline float homography_error(const orc_est *e, unsigned int pidx) {
+    const float *p = e->pts + 4 * (size_t)pidx;
+    const float x1 = p[0], y1 = p[1], x2 = p[2], y2 = p[3];
+    const float *h = e->h, *hi = e->hi;
+    float ex2 = h[0] * x1 + h[1] * y1 + h[2];
+    float ey2 = h[3] * x1 + h[4] * y1 + h[5];
+    float ez2 = h[6] * x1 + h[7] * y1 + h[8];
+    ex2 /= ez2;
+    ey2 /= ez2;
+    float ex1 = hi[0] * x2 + hi[1] * y2 + hi[2];
+    float ey1 = hi[3] * x2 + hi[4] * y2 + hi[5];
+    float ez1 = hi[6] * x2 + hi[7] * y2 + hi[8];
+    ex1 /= ez1;
+    ey1 /= ez1;
+    float d2 = (x2 - ex2) * (x2 - ex2) + (y2 - ey2) * (y2 - ey2);
+    float d1 = (x1 - ex1) * (x1 - ex1) + (y1 - ey1) * (y1 - ey1);
+    float error = (float)(sqrt((double)d2) + sqrt((double)d1));
+    return error / 2;
+}
+
+/* Line2DEstimator::GetError (line2d_estimator.hpp:154-156) */
+static inline float line2d_error(const orc_est *e, unsigned int pidx) {
+    const float *p = e->pts + 2 * (size_t)pidx;
+    return fabsf(e->a * p[0] + e->b * p[1] + e->c);
+}
+
+float orc_est_error(const orc_est *e, unsigned int pidx) {
+    return e->kind == ORC_LINE2D ? line2d_error(e, pidx) : homography_error(e, pidx);
+}
+
+/* ------------------------------------------------------------ quality */
+/* Quality::getNumberInliers (quality.hpp:60-101): points in order; err < thr strict;
+ * Σ err sequential fp32. */
+void orc_quality(orc_est *e, const float *model, float thr, int *count, float *sum, int *inliers) {
+    orc_est_set_model(e, model);
+    int cnt = 0;
+    float s = 0.f;
+    if (e->kind == ORC_LINE2D) {
+        for (unsigned int p = 0; p < e->n; p++) {
+            float err = line2d_error(e, p);
+            if (err < thr) {
+                if (inliers) inliers[cnt] = (int)p;
+                cnt++;
+                s += err;
+            }
+        }
+    } else {
+        for (unsigned int p = 0; p < e->n; p++) {
+            float err = homography_error(e, p);
+            if (err < thr) {
+                if (inliers) inliers[cnt] = (int)p;
+                cnt++;
+                s += err;
+            }
+        }
+    }
+    *count = cnt;
+    *sum = s;
+}
+
+void orc_score_models(orc_est *e, const float *models, int n_models, float thr, int *counts, float *sums) {
+    for (int i = 0; i < n_models; i++) orc_quality(e, models + 9 * (size_t)i, thr, &counts[i], &sums[i], NULL);
+}
+
+void orc_estimate_batch(orc_est *e, const int *samples, int n_samples, float *models, int *n_models) {
+    int m = orc_est_sample_size(e);
+    for (int i = 0; i < n_samples; i++) n_models[i] = orc_est_estimate(e, samples + (size_t)i * m, models + 9 * (size_t)i);
+}
+
+/* dataset/GetImage.h:209-231: Quality::getInliers with the model and with model.inv(),
+ * keep the larger. */
+int orc_gt_inliers_homography(const float *points, unsigned int n, const float *model, float thr) {
+    orc_est *e = orc_est_new(ORC_HOMOGRAPHY, points, n, ORC_DLT_THIN);
+    int c1, c2;
+    float s;
+    float inv[9];
+    orc_quality(e, model, thr, &c1, &s, NULL);
+    orc_inv3x3(model, inv);
+    orc_quality(e, inv, thr, &c2, &s, NULL);
+    orc_est_free(e);
+    return c2 > c1 ? c2 : c1;
+}
+
+/* ------------------------------------------------------------ termination */
+/* StandardTerminationCriteria (standard_termination_criteria.hpp:24-31, 52-62):
+ * log_1_p = (float) log(1 - p) (double log), fp32 inlier ratio power, EPSILON 0.0005f,
+ * k = log_1_p / log(1 - q) in double, truncated to unsigned. */
+unsigned int orc_std_termination(unsigned int inliers, unsigned int points_size, unsigned int sample_size,
+                                 float desired_prob, unsigned int max_iterations) {
+    float log_1_p = (float)log((double)(1 - desired_prob));
+    float inl_ratio = (float)inliers / (float)points_size;
+    float inl_prob = inl_ratio * inl_ratio;
+    int k = (int)sample_size;
+    while (k > 2) {
+        inl_prob *= inl_ratio;
+        k--;
+    }
+    if (inl_prob < 0.0005f) return max_iterations;
+    double r = (double)log_1_p / log((double)(1 - inl_prob));
+    return (unsigned int)r;
+}
+
+/* ------------------------------------------------------------ Ransac::run */
+static int score_bigger(int c1, float s1, int c2, float s2) {
+    /* Score::bigger (quality.hpp:22-26) */
+    if (c1 > c2) return 1;
+    if (c1 == c2) return s1 > s2;
+    return 0;
+}
+
+int orc_ransac_run(int kind, const float *points, unsigned int n, float threshold, float desired_prob,
+                   unsigned int max_iterations, unsigned int seed, int dlt_mode, orc_result *out,
+                   int *inliers_out, unsigned int *rec_iter, int *rec_count, float *rec_score, int rec_cap) {
+    orc_est *e = orc_est_new(kind, points, n, dlt_mode);
+    if (!e) return -1;
+    const int m = orc_est_sample_size(e);
+    orc_srandom(seed);
+    orc_uniform *smp = orc_uniform_new(n, (unsigned int)m);
+    int *inl = (int *)malloc(sizeof(int) * (n ? n : 1));
+    int sample[9];
+    float models[27], best_model[9];
+    memset(best_model, 0, sizeof(best_model));
+    int best_cnt = 0, nrec = 0;
+    float best_sum = 0.f;
+    unsigned int iters = 0, max_iters = max_iterations;
+
+    /* ransac.cpp:58-139 */
+    while (iters < max_iters) {
+        orc_uniform_sample(smp, sample);
+        int nm = orc_est_estimate(e, sample, models);
+        for (int i = 0; i < nm; i++) {
+            int cnt;
+            float sum;
+            orc_quality(e, models + 9 * i, threshold, &cnt, &sum, NULL);
+            if (score_bigger(cnt, sum, best_cnt, best_sum)) {
+                best_cnt = cnt;
+                best_sum = sum;
+                memcpy(best_model, models + 9 * i, sizeof(best_model));
+                max_iters = orc_std_termination((unsigned int)best_cnt, n, (unsigned int)m, desired_prob, max_iterations);
+                if (nrec < rec_cap) {
+                    if (rec_iter) rec_iter[nrec] = iters;
+                    if (rec_count) rec_count[nrec] = cnt;
+                    if (rec_score) rec_score[nrec] = sum;
+                }
+                nrec++;
+            }
+        }
+        iters++;
+    }
+    int rc = 0;
+    out->iters = iters;
+    out->n_records = nrec;
+    out->polish_passes = 0;
+    memcpy(out->minimal_model, best_model, sizeof(best_model));
+    out->minimal_inliers = best_cnt;
+    if (best_cnt == 0) {
+        rc = -111; /* ransac.cpp:143-147 */
+    } else {
+        /* ransac.cpp:157-207: <= 4 non-minimal passes */
+        float nm_model[9];
+        int prev = 0, cnt;
+        float sum;
+        orc_quality(e, best_model, threshold, &cnt, &sum, inl); /* getInliers */
+        for (int norm = 0; norm < 4; norm++) {
+            if (!orc_est_nonminimal(e, inl, (unsigned int)best_cnt, nm_model)) break;
+            orc_quality(e, nm_model, threshold, &cnt, &sum, inl);
+            if ((double)((float)cnt / (float)best_cnt) < 0.8) break;
+            if (cnt <= prev) break;
+            prev = cnt;
+            best_cnt = cnt;
+            best_sum = sum;
+            memcpy(best_model, nm_model, sizeof(best_model));
+            out->polish_passes++;
+        }
+        /* ransac.cpp:214 final inliers of the best model */
+        orc_quality(e, best_model, threshold, &cnt, &sum, inliers_out ? inliers_out : inl);
+    }
+    memcpy(out->model, best_model, sizeof(best_model));
+    out->inliers = best_cnt;
+    free(inl);
+    orc_uniform_free(smp);
+    orc_est_free(e);
+    return rc;
+}
+
+int orc_hypothesis_loop(orc_est *e, orc_uniform *s, int count, float thr, float *best_score_sum) {
+    int m = orc_est_sample_size(e);
+    int sample[9];
+    float models[27];
+    int best_cnt = 0;
+    float best_sum = 0.f;
+    for (int it = 0; it < count; it++) {
+        orc_uniform_sample(s, sample);
+        int nm = orc_est_estimate(e, sample, models);
+        (void)m;
+        for (int i = 0; i < nm; i++) {
+            int cnt;
+            float sum;
+            orc_quality(e, models + 9 * i, thr, &cnt, &sum, NULL);
+            if (score_bigger(cnt, sum, best_cnt, best_sum)) {
+                best_cnt = cnt;
+                best_sum = sum;
+            }
+        }
+    }
+    if (best_score_sum) *best_score_sum = best_sum;
+    return best_cnt;
+}
+
+/* ------------------------------------------------------------ generator */
+/* Generate2DLinePoints (generator/generator.cpp:98-148), SURVEY Q25: fp32 arithmetic on
+ * glibc rand(); sin/cos/sqrt are the C double functions. */
+void orc_generate_line2d(unsigned int seed, float noise, int inliers, int outliers, int border_x, int border_y,
+                         float *pts, float *gt) {
+    srand(seed);
+    const float RM = (float)RAND_MAX;
+    float alpha = (float)(M_PI * (double)(float)rand() / (double)RAND_MAX);
+    float nx = (float)sin((double)alpha);
+    float ny = (float)cos((double)alpha);
+    float tx = -ny, ty = nx;
+    float cx = (float)(border_x / 2), cy = (float)(border_y / 2);
+    float c = -(nx * cx + ny * cy);
+    gt[0] = nx;
+    gt[1] = ny;
+    gt[2] = c;
+    for (int i = 0; i < outliers; i++) {
+        pts[2 * i] = (float)border_x * (float)rand() / RM;
+        pts[2 * i + 1] = (float)border_y * (float)rand() / RM;
+    }
+    float diag = (float)sqrt((double)(border_x * border_x + border_y * border_y));
+    for (int i = outliers; i < inliers + outliers; i++) {
+        for (;;) {
+            float t = (float)rand() / RM - 0.5f;
+            float x = cx + t * tx * diag;
+            if (x < 0 || x > (float)border_x) continue;
+            float y = cy + t * ty * diag;
+            if (y < 0 || y > (float)border_y) continue;
+            x = x + nx * noise * (float)rand() / RM - noise / 2;
+            y = y + ny * noise * (float)rand() / RM - noise / 2;
+            pts[2 * i] = x;
+            pts[2 * i + 1] = y;
+            break;
+        }
+    }
+}

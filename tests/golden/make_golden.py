@@ -1,0 +1,118 @@
+"""Regenerate the committed golden fixtures from the reference's own data files.
+
+Run in the build container (needs /root/reference, read-only):  python tests/golden/make_golden.py
+
+Fixtures are DATA only -- inputs and expected outputs the reference already holds:
+  * homography_scenes.npz : the 12 SIFT correspondence sets the reference's homography
+    experiments use (dataset/homography/sift_update/<scene>_pts.txt, loaded as
+    Reader::LoadPointsFromFile does -- detector/Reader.cpp:182-213, istream >> float,
+    i.e. strtof) and their GT models (dataset/homography/<scene>_model.txt,
+    Reader::getMatrix3x3, detector/Reader.cpp:129-145);
+  * homography_gt.json    : the reference's published GT inlier counts for those scenes
+    at threshold 2 ("GT Inl" column of results/homography/uniform_gc_Grid_c_sz_50.csv),
+    derived by dataset/GetImage.h:209-231 from the GT model;
+  * line2d_scenes.npz     : the synthetic line sets dataset/line2d/<name>.txt
+    (format dataset/GetImage.h:85-116) and GT lines;
+  * line2d_stats.json     : the published 50-run statistics of Uniform sampling on them
+    (results/line2d/uniform_000.csv, thr 10, p 0.99, no LO/SPRT).
+"""
+import csv
+import ctypes
+import json
+import os
+
+import numpy as np
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+_libc = ctypes.CDLL("libc.so.6")
+_libc.strtof.restype = ctypes.c_float
+_libc.strtof.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p)]
+
+
+def strtof(tok):
+    return _libc.strtof(tok.encode(), None)
+
+
+def load_pts(path):
+    with open(path) as f:
+        lines = f.read().splitlines()
+    n = int(lines[0])
+    rows = []
+    for ln in lines[1:]:
+        toks = ln.split()
+        if len(toks) < 4:
+            continue
+        rows.append([strtof(t) for t in toks[:4]])
+    arr = np.array(rows, dtype=np.float32)
+    assert arr.shape[0] == n, (path, arr.shape, n)
+    return arr
+
+
+def load_model(path):
+    with open(path) as f:
+        toks = f.read().split()
+    return np.array([strtof(t) for t in toks[:9]], dtype=np.float32)
+
+
+def homography():
+    csv_path = os.path.join(REF, "results/homography/uniform_gc_Grid_c_sz_50.csv")
+    gt = {}
+    with open(csv_path) as f:
+        for row in csv.reader(f):
+            if len(row) > 2 and row[0] and row[0] != "Filename" and row[1].strip().isdigit():
+                gt[row[0]] = int(row[1])
+    arrays = {}
+    for scene in sorted(gt):
+        arrays[scene + "_pts"] = load_pts(os.path.join(REF, "dataset/homography/sift_update", scene + "_pts.txt"))
+        arrays[scene + "_model"] = load_model(os.path.join(REF, "dataset/homography", scene + "_model.txt"))
+    np.savez_compressed(os.path.join(OUT, "homography_scenes.npz"), **arrays)
+    with open(os.path.join(OUT, "homography_gt.json"), "w") as f:
+        json.dump({"source": "results/homography/uniform_gc_Grid_c_sz_50.csv (GT Inl)", "threshold": 2.0,
+                   "gt_inliers": gt}, f, indent=1, sort_keys=True)
+
+
+def line2d():
+    arrays = {}
+    names = []
+    d = os.path.join(REF, "dataset/line2d")
+    for fn in sorted(os.listdir(d)):
+        if not fn.endswith(".txt") or fn == "dataset.txt":
+            continue
+        name = fn[:-4]
+        with open(os.path.join(d, fn)) as f:
+            toks = f.read().split()
+        w, h, noise = int(toks[0]), int(toks[1]), int(toks[2])
+        a, b, c = (strtof(t) for t in toks[3:6])
+        n = int(toks[6])
+        vals = np.array([strtof(t) for t in toks[7:7 + 2 * n]], dtype=np.float32).reshape(n, 2)
+        arrays[name + "_pts"] = vals
+        arrays[name + "_model"] = np.array([a, b, c], dtype=np.float32)
+        names.append(name)
+    np.savez_compressed(os.path.join(OUT, "line2d_scenes.npz"), **arrays)
+    stats = {}
+    with open(os.path.join(REF, "results/line2d/uniform_000.csv")) as f:
+        rows = list(csv.reader(f))
+    header = None
+    for row in rows:
+        if row and row[0] == "Filename":
+            header = row
+            continue
+        if header and row and row[0] in names:
+            rec = dict(zip(header, row))
+            stats[row[0]] = {
+                "avg_inliers": float(rec["Avg num inl/gt"].split("/")[0]),
+                "std_inliers": float(rec["Std dev num inl"]),
+                "avg_iters": float(rec["Avg num iters"]),
+                "std_iters": float(rec["Std dev num iters"]),
+                "med_iters": float(rec["Med num iters"]),
+            }
+    with open(os.path.join(OUT, "line2d_stats.json"), "w") as f:
+        json.dump({"source": "results/line2d/uniform_000.csv", "runs": 50, "threshold": 10.0,
+                   "desired_prob": 0.99, "stats": stats}, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    homography()
+    line2d()
+    print("golden fixtures written to", OUT)
