@@ -1,0 +1,159 @@
+/*
+ * usac_gpu.h -- C-ABI of the MI355X-native USAC hypothesize-and-verify engine
+ * (libransac_amd.so).  Plain pointers and sizes, opaque handles, int status
+ * (0 = ok, < 0 = error, message via usac_last_error), never exit().
+ *
+ * Each entry point replaces one reference interface (MathsionYang/Ransac paths):
+ *
+ *   usac_create / usac_destroy     Ransac(Model*, cv::InputArray) estimator+quality init
+ *                                  (usac/ransac/ransac.hpp:41-93, init.cpp:3-20)
+ *   usac_estimate_models           Estimator::EstimateModel, batched
+ *                                  (usac/estimator/estimator.hpp:19; homography
+ *                                  homography_estimator.hpp:47-56 -> dlt.cpp:7-52;
+ *                                  line2d line2d_estimator.hpp:36-54)
+ *   usac_score_models              Quality::getNumberInliers(score, model), batched over
+ *                                  models (usac/quality/quality.hpp:60-101)
+ *   usac_get_inliers               Quality::getNumberInliers(..., get_inliers=true, inliers)
+ *                                  / Quality::getInliers (quality.hpp:80-87, 108-121)
+ *   usac_nonminimal                Estimator::EstimateModelNonMinimalSample
+ *                                  (estimator.hpp:21; normalized_dlt.cpp:7-23;
+ *                                  line2d_estimator.hpp:59-107)
+ *   usac_hypothesize_score         Sampler::generateSample + Estimator::EstimateModel +
+ *                                  Quality::getNumberInliers + Score::bigger, fused over a
+ *                                  batch (the body of ransac.cpp:58-139)
+ *   usac_std_termination           StandardTerminationCriteria::getUpBoundIterations
+ *                                  (standard_termination_criteria.hpp:52-62)
+ *   usac_ransac_run                Ransac::run + RansacOutput (ransac.cpp:14-238,
+ *                                  ransac_output.hpp:29-97), Uniform sampler
+ *   usac_comm_*                    new: one RCCL all-gather of best records per batch
+ *
+ * Threading: a context is bound to one device and one HIP stream and is not
+ * thread-safe (one host thread / process per GPU).  Calls are synchronous with respect
+ * to their outputs unless named *_async.
+ */
+#ifndef USAC_GPU_H
+#define USAC_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define USAC_ABI_VERSION 1
+
+/* = enum ESTIMATOR (usac/model.hpp:10) */
+enum { USAC_LINE2D = 1, USAC_HOMOGRAPHY = 2, USAC_FUNDAMENTAL = 3, USAC_ESSENTIAL = 4 };
+/* = enum SAMPLER (usac/model.hpp:11); only Uniform in ABI v1 */
+enum { USAC_SAMPLER_UNIFORM = 1 };
+/* 4-pt DLT: THIN = reference semantics (vt.row(7) of the thin 8x9 SVD, dlt.cpp:43-48);
+ * NULLSPACE = true null vector. */
+enum { USAC_DLT_THIN = 0, USAC_DLT_NULLSPACE = 1 };
+
+enum {
+    USAC_OK = 0,
+    USAC_ERR_ARG = -1,
+    USAC_ERR_HIP = -2,
+    USAC_ERR_UNSUPPORTED = -3,
+    USAC_ERR_NO_MODEL = -111 /* best score 0, ransac.cpp:143-147 (reference exit(111)) */
+};
+
+typedef struct usac_ctx usac_ctx;
+
+/* A hypothesis record: Score {inlier_number, score} (quality.hpp:16-37) of model
+ * `model` produced by hypothesis `hyp_index` (global sample index). */
+typedef struct usac_record {
+    uint64_t hyp_index;
+    int32_t inliers;
+    float score;
+    float model[9];
+    int32_t valid;
+} usac_record;
+
+/* Model (usac/model.hpp:15-45) fields the Uniform/no-LO/no-SPRT loop reads. */
+typedef struct usac_params {
+    float threshold;            /* model.hpp:17 (default 2) */
+    float desired_prob;         /* model.hpp:18 (0.95) */
+    uint32_t max_iterations;    /* model.hpp:22 (10000) */
+    uint32_t seed;              /* glibc srandom(seed): ResetRandomGenerator(false) semantics */
+    int32_t dlt_mode;           /* USAC_DLT_* */
+    uint32_t batch;             /* hypotheses per device batch (0 = default) */
+} usac_params;
+
+/* RansacOutput getters (ransac_output.hpp:57-97) */
+typedef struct usac_run_output {
+    float model[9];
+    int32_t inliers;            /* getNumberOfInliers */
+    uint32_t iters;             /* getNumberOfMainIterations */
+    int64_t time_us;            /* getTimeMicroSeconds (loop + polish, as ransac.cpp:15,209) */
+    int32_t n_records;          /* best-score updates in the main loop */
+    int32_t polish_passes;
+    float minimal_model[9];     /* best model before the non-minimal polish */
+    int32_t minimal_inliers;
+    uint32_t batches;           /* device batches launched */
+} usac_run_output;
+
+/* ---- lifetime ----------------------------------------------------------------- */
+/* pts: n rows of `cols` floats (2: line [x y]; 4: two-view [x1 y1 x2 y2]), host memory,
+ * copied to the device at create (the caller may free it). */
+int usac_create(usac_ctx **out, int device, int estimator, const float *pts, uint32_t n, uint32_t cols);
+void usac_destroy(usac_ctx *ctx);
+const char *usac_last_error(const usac_ctx *ctx);
+int usac_abi_version(void);
+int usac_set_dlt_mode(usac_ctx *ctx, int mode);
+uint32_t usac_sample_size(const usac_ctx *ctx);
+uint32_t usac_num_points(const usac_ctx *ctx);
+
+/* ---- plugin operators ----------------------------------------------------------- */
+/* samples: B x m int32 (host) -> models: B x 9 floats, n_models[B] (0/1 per sample). */
+int usac_estimate_models(usac_ctx *ctx, const int32_t *samples, uint32_t B, float *models, int32_t *n_models);
+/* models: n_models x 9 floats (host); counts/sums (host, sums nullable).  Counts are
+ * exact; sums are the sequential fp32 sums of quality.hpp:89-96. */
+int usac_score_models(usac_ctx *ctx, const float *models, uint32_t n_models, float thr, int32_t *counts,
+                      float *sums);
+/* One model: ascending inlier indices (idx capacity >= n points), count and sum. */
+int usac_get_inliers(usac_ctx *ctx, const float *model, float thr, int32_t *idx, uint32_t *n, float *sum);
+/* Non-minimal least squares on the listed points; returns USAC_OK and writes model. */
+int usac_nonminimal(usac_ctx *ctx, const int32_t *idx, uint32_t n, float *model);
+
+/* Fused batch: samples (B x m host int32) or NULL => device xorshift sampler keyed by
+ * (seed, first_hyp + i).  Per-hypothesis counts/sums (host, nullable) and the batch best
+ * under Score::bigger with the earliest index on exact ties (best, nullable). */
+int usac_hypothesize_score(usac_ctx *ctx, const int32_t *samples, uint32_t B, uint64_t seed, uint64_t first_hyp,
+                           float thr, int32_t *counts, float *sums, usac_record *best);
+/* Asynchronous device-sampled batch for throughput runs: enqueues sample+solve+score+
+ * argmax on the context stream; usac_fetch_best waits and returns the batch best. */
+int usac_hypothesize_async(usac_ctx *ctx, uint32_t B, uint64_t seed, uint64_t first_hyp, float thr);
+int usac_fetch_best(usac_ctx *ctx, usac_record *best);
+int usac_sync(usac_ctx *ctx);
+/* Device time of the last async batch's kernels, measured with HIP events on the
+ * context stream: [0] whole batch, [1] score kernel, [2] solve kernel (ms). */
+int usac_last_timings(usac_ctx *ctx, float *ms3);
+/* Score-kernel split factor (point chunks per hypothesis tile, 1 = exact sequential sums). */
+int usac_set_score_chunks(usac_ctx *ctx, int chunks);
+
+/* ---- loop --------------------------------------------------------------------- */
+uint32_t usac_std_termination(uint32_t inliers, uint32_t points_size, uint32_t sample_size, float desired_prob,
+                              uint32_t max_iterations);
+/* Ransac::run with the Uniform sampler (glibc random() stream), no LO / SPRT.
+ * inliers_out (capacity n, nullable): final inliers ascending.  records (nullable,
+ * capacity rec_cap): best-score updates in loop order (hyp_index = iteration). */
+int usac_ransac_run(usac_ctx *ctx, const usac_params *params, usac_run_output *out, int32_t *inliers_out,
+                    usac_record *records, uint32_t rec_cap);
+/* Host glibc-compatible UniformSampler stream (uniform_sampler.hpp:42-54): count x m
+ * samples after srandom(seed).  Exposed for parity tests. */
+int usac_uniform_samples(uint32_t seed, uint32_t n_points, uint32_t m, uint32_t count, int32_t *out);
+
+/* ---- multi-GPU (RCCL over xGMI) --------------------------------------------------- */
+/* 128-byte RCCL unique id (rank 0 creates, everyone receives it out of band). */
+int usac_comm_unique_id(uint8_t *id128);
+int usac_comm_init(usac_ctx *ctx, int nranks, int rank, const uint8_t *id128);
+/* All-gather of one usac_record per rank on the context stream: all[nranks]. */
+int usac_allgather_records(usac_ctx *ctx, const usac_record *local, usac_record *all);
+/* Merge n records by Score::bigger, earliest hyp_index on exact ties. */
+int usac_merge_records(const usac_record *recs, uint32_t n, usac_record *best);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -341,13 +341,22 @@ static int homography_normalized_dlt(const orc_est *e, const int *sample, unsign
         row_jacobi(W, (int)(2 * n));
         pick_vector(W, (int)(2 * n), ORC_DLT_THIN, v);
     } else {
+        /* A^T A summation order (no reference order exists -- OpenCV's SVD hides it):
+         * 64-point blocks summed in point order, block partials summed in block order. */
         double AtA[9][9];
         memset(AtA, 0, sizeof(AtA));
-        for (unsigned int i = 0; i < n; i++) {
-            double r0[9], r1[9];
-            dlt_fill_rows(norm[4 * i], norm[4 * i + 1], norm[4 * i + 2], norm[4 * i + 3], r0, r1);
+        for (unsigned int b0 = 0; b0 < n; b0 += 64) {
+            double P[9][9];
+            memset(P, 0, sizeof(P));
+            unsigned int b1 = b0 + 64 < n ? b0 + 64 : n;
+            for (unsigned int i = b0; i < b1; i++) {
+                double r0[9], r1[9];
+                dlt_fill_rows(norm[4 * i], norm[4 * i + 1], norm[4 * i + 2], norm[4 * i + 3], r0, r1);
+                for (int j = 0; j < 9; j++)
+                    for (int k = j; k < 9; k++) P[j][k] += r0[j] * r0[k] + r1[j] * r1[k];
+            }
             for (int j = 0; j < 9; j++)
-                for (int k = j; k < 9; k++) AtA[j][k] += r0[j] * r0[k] + r1[j] * r1[k];
+                for (int k = j; k < 9; k++) AtA[j][k] += P[j][k];
         }
         for (int j = 0; j < 9; j++)
             for (int k = 0; k < j; k++) AtA[j][k] = AtA[k][j];

@@ -1,0 +1,438 @@
+"""ransac_amd -- MI355X-native USAC hypothesize-and-verify engine.
+
+Python host mirror of the reference's plugin surface (MathsionYang/Ransac ``usac/``):
+``Model`` (usac/model.hpp), ``Ransac`` + ``RansacOutput`` (usac/ransac/ransac.hpp,
+ransac_output.hpp), ``Score`` (usac/quality/quality.hpp), and the operator level
+``Context`` (Estimator::EstimateModel, Quality::getNumberInliers, ... batched).  All
+compute goes through the C-ABI of ``libransac_amd.so`` (include/usac_gpu.h) into the HIP
+kernels; there is no Python or CPU compute fallback -- if the library or a GPU is
+missing, the calls raise.
+"""
+import ctypes
+import enum
+import os
+import subprocess
+
+import numpy as np
+
+__all__ = ["ESTIMATOR", "SAMPLER", "DLT", "Model", "Ransac", "RansacOutput", "Score", "Context", "Record",
+           "build", "lib", "std_termination", "uniform_samples", "UsacError"]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libransac_amd.so")
+
+
+class ESTIMATOR(enum.IntEnum):  # usac/model.hpp:10
+    NullE = 0
+    Line2d = 1
+    Homography = 2
+    Fundamental = 3
+    Essential = 4
+
+
+class SAMPLER(enum.IntEnum):  # usac/model.hpp:11
+    NullS = 0
+    Uniform = 1
+    ProgressiveNAPSAC = 2
+    Napsac = 3
+    Prosac = 4
+    Evsac = 5
+    ProsacNapsac = 6
+
+
+class DLT(enum.IntEnum):
+    THIN = 0        # reference semantics: vt.row(7) of the thin 8x9 SVD (dlt.cpp:43-48)
+    NULLSPACE = 1   # true null vector
+
+
+class UsacError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("usac error %d: %s" % (code, msg))
+        self.code = code
+
+
+class Record(ctypes.Structure):
+    _fields_ = [("hyp_index", ctypes.c_uint64), ("inliers", ctypes.c_int32), ("score", ctypes.c_float),
+                ("model", ctypes.c_float * 9), ("valid", ctypes.c_int32)]
+
+    def as_dict(self):
+        return {"hyp_index": int(self.hyp_index), "inliers": int(self.inliers), "score": float(self.score),
+                "model": np.array(self.model[:], dtype=np.float32), "valid": bool(self.valid)}
+
+
+class _Params(ctypes.Structure):
+    _fields_ = [("threshold", ctypes.c_float), ("desired_prob", ctypes.c_float), ("max_iterations", ctypes.c_uint32),
+                ("seed", ctypes.c_uint32), ("dlt_mode", ctypes.c_int32), ("batch", ctypes.c_uint32)]
+
+
+class _RunOutput(ctypes.Structure):
+    _fields_ = [("model", ctypes.c_float * 9), ("inliers", ctypes.c_int32), ("iters", ctypes.c_uint32),
+                ("time_us", ctypes.c_int64), ("n_records", ctypes.c_int32), ("polish_passes", ctypes.c_int32),
+                ("minimal_model", ctypes.c_float * 9), ("minimal_inliers", ctypes.c_int32),
+                ("batches", ctypes.c_uint32)]
+
+
+# every symbol include/usac_gpu.h declares (checked by tests/test_abi.py)
+ABI_SYMBOLS = [
+    "usac_create", "usac_destroy", "usac_last_error", "usac_abi_version", "usac_set_dlt_mode", "usac_sample_size",
+    "usac_num_points", "usac_estimate_models", "usac_score_models", "usac_get_inliers", "usac_nonminimal",
+    "usac_hypothesize_score", "usac_hypothesize_async", "usac_fetch_best", "usac_sync", "usac_last_timings",
+    "usac_set_score_chunks", "usac_std_termination", "usac_ransac_run", "usac_uniform_samples",
+    "usac_comm_unique_id", "usac_comm_init", "usac_allgather_records", "usac_merge_records",
+]
+
+
+def build(jobs=8):
+    """Compile libransac_amd.so for gfx950 in-tree (hipcc via ransac_amd/Makefile)."""
+    subprocess.run(["make", "-s", "-C", _HERE, "-j%d" % jobs], check=True)
+
+
+_lib = None
+_P = ctypes.POINTER
+_vp = ctypes.c_void_p
+
+
+def lib():
+    """Load libransac_amd.so (raises if it is missing: no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("ransac_amd: %s is missing -- run ransac_amd.build() (hipcc, gfx950)" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    f32p, i32p, u32p, u8p = _P(ctypes.c_float), _P(ctypes.c_int32), _P(ctypes.c_uint32), _P(ctypes.c_uint8)
+    sig = {
+        "usac_create": (ctypes.c_int, [_P(_vp), ctypes.c_int, ctypes.c_int, f32p, ctypes.c_uint32, ctypes.c_uint32]),
+        "usac_destroy": (None, [_vp]),
+        "usac_last_error": (ctypes.c_char_p, [_vp]),
+        "usac_abi_version": (ctypes.c_int, []),
+        "usac_set_dlt_mode": (ctypes.c_int, [_vp, ctypes.c_int]),
+        "usac_set_score_chunks": (ctypes.c_int, [_vp, ctypes.c_int]),
+        "usac_sample_size": (ctypes.c_uint32, [_vp]),
+        "usac_num_points": (ctypes.c_uint32, [_vp]),
+        "usac_estimate_models": (ctypes.c_int, [_vp, i32p, ctypes.c_uint32, f32p, i32p]),
+        "usac_score_models": (ctypes.c_int, [_vp, f32p, ctypes.c_uint32, ctypes.c_float, i32p, f32p]),
+        "usac_get_inliers": (ctypes.c_int, [_vp, f32p, ctypes.c_float, i32p, u32p, f32p]),
+        "usac_nonminimal": (ctypes.c_int, [_vp, i32p, ctypes.c_uint32, f32p]),
+        "usac_hypothesize_score": (ctypes.c_int, [_vp, i32p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
+                                                  ctypes.c_float, i32p, f32p, _P(Record)]),
+        "usac_hypothesize_async": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
+                                                  ctypes.c_float]),
+        "usac_fetch_best": (ctypes.c_int, [_vp, _P(Record)]),
+        "usac_sync": (ctypes.c_int, [_vp]),
+        "usac_last_timings": (ctypes.c_int, [_vp, f32p]),
+        "usac_std_termination": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                   ctypes.c_float, ctypes.c_uint32]),
+        "usac_ransac_run": (ctypes.c_int, [_vp, _P(_Params), _P(_RunOutput), i32p, _P(Record), ctypes.c_uint32]),
+        "usac_uniform_samples": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                                i32p]),
+        "usac_comm_unique_id": (ctypes.c_int, [u8p]),
+        "usac_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, u8p]),
+        "usac_allgather_records": (ctypes.c_int, [_vp, _P(Record), _P(Record)]),
+        "usac_merge_records": (ctypes.c_int, [_P(Record), ctypes.c_uint32, _P(Record)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _ptr(a, t):
+    return a.ctypes.data_as(_P(t)) if a is not None else None
+
+
+def std_termination(inliers, points_size, sample_size, desired_prob, max_iterations=10000):
+    """StandardTerminationCriteria::getUpBoundIterations (standard_termination_criteria.hpp:52-62)."""
+    return int(lib().usac_std_termination(inliers, points_size, sample_size, ctypes.c_float(desired_prob),
+                                          max_iterations))
+
+
+def uniform_samples(seed, n_points, m, count):
+    """UniformSampler stream after srandom(seed) (uniform_sampler.hpp:42-54): count x m int32."""
+    out = np.zeros((count, m), dtype=np.int32)
+    rc = lib().usac_uniform_samples(seed, n_points, m, count, _ptr(out, ctypes.c_int32))
+    if rc:
+        raise UsacError(rc, "usac_uniform_samples")
+    return out
+
+
+class Context:
+    """One device + estimator + resident correspondence set (operator-level API)."""
+
+    def __init__(self, estimator, points, device=0):
+        L = lib()
+        self.points = np.ascontiguousarray(points, dtype=np.float32)
+        if self.points.ndim != 2:
+            raise ValueError("points must be N x cols")
+        self.estimator = ESTIMATOR(estimator)
+        self.n, self.cols = self.points.shape
+        h = _vp()
+        rc = L.usac_create(ctypes.byref(h), device, int(self.estimator), _ptr(self.points, ctypes.c_float), self.n,
+                           self.cols)
+        if rc != 0:
+            raise UsacError(rc, "usac_create(device=%d, estimator=%s, n=%d, cols=%d) failed (no usable GPU?)"
+                            % (device, self.estimator.name, self.n, self.cols))
+        self._h = h
+        self.m = int(L.usac_sample_size(h))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().usac_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = lib().usac_last_error(self._h)
+            raise UsacError(rc, "%s: %s" % (what, msg.decode() if msg else ""))
+
+    def set_dlt_mode(self, mode):
+        self._check(lib().usac_set_dlt_mode(self._h, int(mode)), "set_dlt_mode")
+
+    def set_score_chunks(self, chunks):
+        self._check(lib().usac_set_score_chunks(self._h, int(chunks)), "set_score_chunks")
+
+    def estimate_models(self, samples):
+        """Estimator::EstimateModel over a batch of minimal samples -> (B x 9 models, n_models)."""
+        s = np.ascontiguousarray(samples, dtype=np.int32).reshape(-1, self.m)
+        B = s.shape[0]
+        models = np.zeros((B, 9), dtype=np.float32)
+        nm = np.zeros(B, dtype=np.int32)
+        self._check(lib().usac_estimate_models(self._h, _ptr(s, ctypes.c_int32), B, _ptr(models, ctypes.c_float),
+                                               _ptr(nm, ctypes.c_int32)), "estimate_models")
+        return models, nm
+
+    def score_models(self, models, thr):
+        """Quality::getNumberInliers for each model -> (counts, sums)."""
+        m = np.ascontiguousarray(models, dtype=np.float32)
+        if m.ndim == 1:
+            m = m.reshape(1, -1)
+        full = np.zeros((m.shape[0], 9), dtype=np.float32)
+        full[:, : m.shape[1]] = m
+        c = np.zeros(full.shape[0], dtype=np.int32)
+        s = np.zeros(full.shape[0], dtype=np.float32)
+        self._check(lib().usac_score_models(self._h, _ptr(full, ctypes.c_float), full.shape[0], ctypes.c_float(thr),
+                                            _ptr(c, ctypes.c_int32), _ptr(s, ctypes.c_float)), "score_models")
+        return c, s
+
+    def get_inliers(self, model, thr):
+        """Quality::getNumberInliers(get_inliers=true) -> (count, sum, ascending indices)."""
+        full = np.zeros(9, dtype=np.float32)
+        mm = np.asarray(model, dtype=np.float32).reshape(-1)
+        full[: mm.size] = mm
+        idx = np.zeros(self.n, dtype=np.int32)
+        n = ctypes.c_uint32(0)
+        s = ctypes.c_float(0)
+        self._check(lib().usac_get_inliers(self._h, _ptr(full, ctypes.c_float), ctypes.c_float(thr),
+                                           _ptr(idx, ctypes.c_int32), ctypes.byref(n), ctypes.byref(s)),
+                    "get_inliers")
+        return n.value, s.value, idx[: n.value].copy()
+
+    def nonminimal(self, idx):
+        """Estimator::EstimateModelNonMinimalSample on the listed points."""
+        i = np.ascontiguousarray(idx, dtype=np.int32)
+        out = np.zeros(9, dtype=np.float32)
+        self._check(lib().usac_nonminimal(self._h, _ptr(i, ctypes.c_int32), i.size, _ptr(out, ctypes.c_float)),
+                    "nonminimal")
+        return out
+
+    def hypothesize_score(self, B=None, samples=None, seed=0, first_hyp=0, thr=2.0, per_hypothesis=True):
+        """Fused sample + solve + score (+ batch best).  samples=None -> device sampler."""
+        L = lib()
+        if samples is not None:
+            s = np.ascontiguousarray(samples, dtype=np.int32).reshape(-1, self.m)
+            B = s.shape[0]
+        else:
+            s = None
+        c = np.zeros(B, dtype=np.int32) if per_hypothesis else None
+        sm = np.zeros(B, dtype=np.float32) if per_hypothesis else None
+        best = Record()
+        self._check(L.usac_hypothesize_score(self._h, _ptr(s, ctypes.c_int32), B, seed, first_hyp,
+                                             ctypes.c_float(thr), _ptr(c, ctypes.c_int32), _ptr(sm, ctypes.c_float),
+                                             ctypes.byref(best)), "hypothesize_score")
+        return c, sm, best.as_dict()
+
+    def hypothesize_async(self, B, seed, first_hyp, thr):
+        self._check(lib().usac_hypothesize_async(self._h, B, seed, first_hyp, ctypes.c_float(thr)),
+                    "hypothesize_async")
+
+    def fetch_best(self):
+        r = Record()
+        self._check(lib().usac_fetch_best(self._h, ctypes.byref(r)), "fetch_best")
+        return r
+
+    def sync(self):
+        self._check(lib().usac_sync(self._h), "sync")
+
+    def last_timings(self):
+        ms = np.zeros(3, dtype=np.float32)
+        self._check(lib().usac_last_timings(self._h, _ptr(ms, ctypes.c_float)), "last_timings")
+        return {"batch_ms": float(ms[0]), "score_ms": float(ms[1]), "solve_ms": float(ms[2])}
+
+    # ---- multi-GPU
+    @staticmethod
+    def comm_unique_id():
+        buf = (ctypes.c_uint8 * 128)()
+        rc = lib().usac_comm_unique_id(buf)
+        if rc:
+            raise UsacError(rc, "usac_comm_unique_id")
+        return bytes(buf)
+
+    def comm_init(self, nranks, rank, uid):
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        self._check(lib().usac_comm_init(self._h, nranks, rank, buf), "comm_init")
+        self.nranks = nranks
+
+    def allgather_record(self, rec):
+        allr = (Record * self.nranks)()
+        self._check(lib().usac_allgather_records(self._h, ctypes.byref(rec), allr), "allgather_records")
+        return list(allr)
+
+
+def merge_records(records):
+    """Score::bigger over records, earliest hyp_index on exact ties."""
+    arr = (Record * len(records))(*records)
+    out = Record()
+    rc = lib().usac_merge_records(arr, len(records), ctypes.byref(out))
+    if rc:
+        raise UsacError(rc, "usac_merge_records")
+    return out
+
+
+# --------------------------------------------------------------------------- plugin API
+class Score:
+    """usac/quality/quality.hpp:16-37"""
+
+    def __init__(self, inlier_number=0, score=0.0):
+        self.inlier_number = int(inlier_number)
+        self.score = float(np.float32(score))
+
+    def bigger(self, other):
+        if self.inlier_number > other.inlier_number:
+            return True
+        if self.inlier_number == other.inlier_number:
+            return self.score > other.score
+        return False
+
+
+class Model:
+    """usac/model.hpp:15-139 (fields and setters the ported loop reads)."""
+
+    def __init__(self, threshold, sample_number, desired_prob, knn, estimator, sampler):
+        self.threshold = float(threshold)
+        self.sample_size = int(sample_number)
+        self.desired_prob = float(desired_prob)
+        self.k_nearest_neighbors = int(knn)
+        self.estimator = ESTIMATOR(estimator)
+        self.sampler = SAMPLER(sampler)
+        self.max_iterations = 10000
+        self.min_iterations = 20
+        self.reset_random_generator = True
+        self.sprt = False
+        self.lo = 0
+        self.seed = 0
+        self.dlt_mode = DLT.THIN
+        self.batch = 0
+        self.device = 0
+
+    def ResetRandomGenerator(self, reset):
+        self.reset_random_generator = bool(reset)
+
+    def setSeed(self, seed):
+        """Seed of the glibc sampler stream (srandom(seed)); replaces srand(time(NULL))."""
+        self.seed = int(seed)
+
+    def setThreshold(self, thr):
+        self.threshold = float(thr)
+
+    def setDesiredProbability(self, p):
+        self.desired_prob = float(p)
+
+    def setSprt(self, sprt):
+        if sprt:
+            raise NotImplementedError("SPRT is not in ABI v1 (SURVEY §8 a15, next round)")
+        self.sprt = False
+
+    def setDLTMode(self, mode):
+        self.dlt_mode = DLT(mode)
+
+
+class RansacOutput:
+    """usac/ransac/ransac_output.hpp:11-99 getters."""
+
+    def __init__(self, model, inliers, time_us, n_inliers, iters, raw):
+        self._model = model
+        self._inliers = inliers
+        self._time = time_us
+        self._n = n_inliers
+        self._iters = iters
+        self.raw = raw
+
+    def getModel(self):
+        return self._model
+
+    def getInliers(self):
+        return self._inliers
+
+    def getTimeMicroSeconds(self):
+        return self._time
+
+    def getNumberOfInliers(self):
+        return self._n
+
+    def getNumberOfMainIterations(self):
+        return self._iters
+
+    def getLOIters(self):
+        return 0
+
+
+class Ransac:
+    """usac/ransac/ransac.hpp:41-115 -- Ransac(model, points); run(); getRansacOutput()."""
+
+    def __init__(self, model, points):
+        if model.sampler != SAMPLER.Uniform:
+            raise NotImplementedError("sampler %s is not in ABI v1 (Uniform only)" % model.sampler.name)
+        self.model = model
+        self.ctx = Context(model.estimator, points, device=model.device)
+        self._out = None
+        self.records = []
+
+    def run(self, rec_cap=4096):
+        L = lib()
+        m = self.model
+        seed = m.seed
+        if m.reset_random_generator and seed == 0:
+            seed = int.from_bytes(os.urandom(4), "little") or 1
+        p = _Params(m.threshold, m.desired_prob, m.max_iterations, seed, int(m.dlt_mode), m.batch)
+        out = _RunOutput()
+        inl = np.zeros(self.ctx.n, dtype=np.int32)
+        recs = (Record * rec_cap)()
+        rc = L.usac_ransac_run(self.ctx._h, ctypes.byref(p), ctypes.byref(out), _ptr(inl, ctypes.c_int32), recs,
+                               rec_cap)
+        if rc == -111:
+            raise UsacError(rc, "best score is 0 (ransac.cpp:143-147)")
+        self.ctx._check(rc, "ransac_run")
+        k = min(out.n_records, rec_cap)
+        self.records = [(int(recs[i].hyp_index), int(recs[i].inliers), float(recs[i].score)) for i in range(k)]
+        raw = {"minimal_model": np.array(out.minimal_model[:], dtype=np.float32),
+               "minimal_inliers": out.minimal_inliers, "polish_passes": out.polish_passes,
+               "n_records": out.n_records, "batches": out.batches}
+        self._out = RansacOutput(np.array(out.model[:], dtype=np.float32), inl[: out.inliers].copy(), out.time_us,
+                                 out.inliers, out.iters, raw)
+
+    def getRansacOutput(self):
+        return self._out

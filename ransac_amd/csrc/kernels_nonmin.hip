@@ -1,0 +1,285 @@
+// kernels_nonmin.hip -- non-minimal (least-squares) model fits on the device, used by the
+// post-loop polish (ransac.cpp:157-207):
+//   homography: DLt::NormalizedDLT (normalized_dlt.cpp:7-23) with
+//               GetNormalizingTransformation (normalizing_transformation.cpp:7-113);
+//   line2d    : Line2DEstimator::EstimateModelNonMinimalSample PCA (line2d_estimator.hpp:59-107).
+// The reference's fp32 moment sums are sequential in sample order and stay sequential
+// here (one lane per accumulator).  The DLT normal matrix A^T A (fp64) has no reference
+// order (OpenCV's SVD hides it); its order is fixed by this build's spec: 64-point
+// blocks summed in order, block partials summed in block order -- shared with the oracle.
+#include <hip/hip_runtime.h>
+
+#include "usac_device.hpp"
+#include "usac_kernels.h"
+
+namespace usac {
+
+constexpr uint32_t kAtaBlock = 64;
+
+// gather q[i] = pts[idx[i]] so the sequential passes read contiguous memory
+__global__ __launch_bounds__(256) void k_gather4(const float4 *__restrict__ pts, const int32_t *__restrict__ idx,
+                                                 uint32_t n, float4 *__restrict__ q) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) q[i] = pts[idx[i]];
+}
+__global__ __launch_bounds__(256) void k_gather2(const float2 *__restrict__ pts, const int32_t *__restrict__ idx,
+                                                 uint32_t n, float2 *__restrict__ q) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) q[i] = pts[idx[i]];
+}
+
+// normalizing transformation: lanes 0..3 = the four coordinate means, lanes 0..1 = the
+// two distance sums; then every lane normalises a strided share of the points.
+// ws layout (floats): [0..8] T1, [9..17] T2.
+__global__ __launch_bounds__(256) void k_normalize(float4 *__restrict__ q, uint32_t n, float *ws) {
+    __shared__ float s_mean[4];
+    __shared__ float s_scale[2];
+    const uint32_t t = threadIdx.x;
+    if (t < 4) {
+        float acc = 0.f;
+        for (uint32_t i = 0; i < n; i++) {
+            const float4 p = q[i];
+            acc += (t == 0 ? p.x : t == 1 ? p.y : t == 2 ? p.z : p.w);
+        }
+        s_mean[t] = acc / (float)n;
+    }
+    __syncthreads();
+    if (t < 2) {
+        const float mx = s_mean[2 * t], my = s_mean[2 * t + 1];
+        float d = 0.f;
+        for (uint32_t i = 0; i < n; i++) {
+            const float4 p = q[i];
+            const float xm = (t == 0 ? p.x : p.z) - mx;
+            const float ym = (t == 0 ? p.y : p.w) - my;
+            d = (float)((double)d + sqrt((double)(xm * xm + ym * ym)));
+        }
+        s_scale[t] = (float)(M_SQRT2 / (double)(d / (float)n));
+    }
+    __syncthreads();
+    const float s1 = s_scale[0], s2 = s_scale[1];
+    const float t1[9] = {s1, 0.f, -s_mean[0] * s1, 0.f, s1, -s_mean[1] * s1, 0.f, 0.f, 1.f};
+    const float t2[9] = {s2, 0.f, -s_mean[2] * s2, 0.f, s2, -s_mean[3] * s2, 0.f, 0.f, 1.f};
+    if (t < 9) {
+        ws[t] = t1[t];
+        ws[9 + t] = t2[t];
+    }
+    __syncthreads();
+    for (uint32_t i = t; i < n; i += 256) {
+        float4 p = q[i];
+        float4 o;
+        o.x = t1[0] * p.x + t1[2];
+        o.y = t1[4] * p.y + t1[5];
+        o.z = t2[0] * p.z + t2[2];
+        o.w = t2[4] * p.w + t2[5];
+        q[i] = o;
+    }
+}
+
+__device__ __forceinline__ double sel9(const double *r, int j) {
+    double v = r[0];
+#pragma unroll
+    for (int k = 1; k < 9; k++) v = (j == k) ? r[k] : v;
+    return v;
+}
+
+// block partials of A^T A: block c, lane e < 45 -> upper-triangle entry e (row-major j<=k)
+__global__ __launch_bounds__(64) void k_ata_partial(const float4 *__restrict__ q, uint32_t n,
+                                                    double *__restrict__ partial) {
+    const uint32_t e = threadIdx.x;
+    if (e >= 45) return;
+    int j = 0, k = e, rem = (int)e;
+    for (int r = 0; r < 9; r++) {
+        if (rem < 9 - r) {
+            j = r;
+            k = r + rem;
+            break;
+        }
+        rem -= 9 - r;
+    }
+    const uint32_t b0 = blockIdx.x * kAtaBlock;
+    const uint32_t b1 = b0 + kAtaBlock < n ? b0 + kAtaBlock : n;
+    double acc = 0.0;
+    for (uint32_t i = b0; i < b1; i++) {
+        const float4 p = q[i];
+        double r0[9], r1[9];
+        dlt_rows(p.x, p.y, p.z, p.w, r0, r1);
+        acc += sel9(r0, j) * sel9(r0, k) + sel9(r1, j) * sel9(r1, k);
+    }
+    partial[(size_t)blockIdx.x * 45 + e] = acc;
+}
+
+// Final DLT solve, one wave: A^T A from the partials (lane e), cyclic Jacobi eigen on 9
+// lanes (LDS), smallest-eigenvalue vector; or the thin row-Jacobi for 2n <= 8 rows;
+// then H = T2^-1 * Hn * T1 (fp64), H /= H33, cast to float.
+template <int R>
+__device__ void thin_solve(const float4 *q, double *v) {
+    double W[R][9];
+#pragma unroll
+    for (int i = 0; i < R / 2; i++) {
+        const float4 p = q[i];
+        dlt_rows(p.x, p.y, p.z, p.w, W[2 * i], W[2 * i + 1]);
+    }
+    row_jacobi<R>(W);
+    pick_vector<R>(W, 0, v);
+}
+
+__global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q, uint32_t n,
+                                                   const double *__restrict__ partial, uint32_t nblocks,
+                                                   const float *ws, float *model_out, int32_t *ok) {
+    __shared__ double A[9][9];
+    __shared__ double V[9][9];
+    __shared__ double s_v[9];
+    const uint32_t t = threadIdx.x;
+    if (2 * n <= 9) {
+        if (t == 0) {
+            double v[9];
+            if (n == 1) thin_solve<2>(q, v);
+            else if (n == 2) thin_solve<4>(q, v);
+            else if (n == 3) thin_solve<6>(q, v);
+            else thin_solve<8>(q, v);
+            for (int k = 0; k < 9; k++) s_v[k] = v[k];
+        }
+        __syncthreads();
+    } else {
+        if (t < 45) {
+            int j = 0, k = t, rem = (int)t;
+            for (int r = 0; r < 9; r++) {
+                if (rem < 9 - r) {
+                    j = r;
+                    k = r + rem;
+                    break;
+                }
+                rem -= 9 - r;
+            }
+            double acc = 0.0;
+            for (uint32_t c = 0; c < nblocks; c++) acc += partial[(size_t)c * 45 + t];
+            A[j][k] = acc;
+            A[k][j] = acc;
+        }
+        if (t < 9)
+            for (int j = 0; j < 9; j++) V[j][t] = (j == (int)t) ? 1.0 : 0.0;
+        __syncthreads();
+        for (int sweep = 0; sweep < 50; sweep++) {
+            double off = 0.0, diag = 0.0;
+            for (int p = 0; p < 9; p++) {
+                diag += A[p][p] * A[p][p];
+                for (int qq = p + 1; qq < 9; qq++) off += A[p][qq] * A[p][qq];
+            }
+            if (off <= 1e-30 * diag || off == 0.0) break;
+            for (int p = 0; p < 8; p++) {
+                for (int qq = p + 1; qq < 9; qq++) {
+                    const double apq = A[p][qq];
+                    if (apq == 0.0) continue;
+                    const double theta = (A[qq][qq] - A[p][p]) / (2.0 * apq);
+                    const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                    const double c = 1.0 / sqrt(tt * tt + 1.0), s = tt * c;
+                    __syncthreads();
+                    if (t < 9) {
+                        const double akp = A[t][p], akq = A[t][qq];
+                        A[t][p] = c * akp - s * akq;
+                        A[t][qq] = s * akp + c * akq;
+                    }
+                    __syncthreads();
+                    if (t < 9) {
+                        const double apk = A[p][t], aqk = A[qq][t];
+                        A[p][t] = c * apk - s * aqk;
+                        A[qq][t] = s * apk + c * aqk;
+                        const double vkp = V[t][p], vkq = V[t][qq];
+                        V[t][p] = c * vkp - s * vkq;
+                        V[t][qq] = s * vkp + c * vkq;
+                    }
+                    __syncthreads();
+                }
+            }
+        }
+        if (t == 0) {
+            int m = 0;
+            for (int i = 1; i < 9; i++)
+                if (A[i][i] < A[m][m]) m = i;
+            for (int k = 0; k < 9; k++) s_v[k] = V[k][m];
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        float T1[9], T2[9], T2i[9];
+        for (int k = 0; k < 9; k++) {
+            T1[k] = ws[k];
+            T2[k] = ws[9 + k];
+        }
+        inv3x3(T2, T2i);
+        double tmp[9], Hd[9];
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) {
+                double s = 0.0;
+                for (int k = 0; k < 3; k++) s += s_v[3 * r + k] * (double)T1[3 * k + c];
+                tmp[3 * r + c] = s;
+            }
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) {
+                double s = 0.0;
+                for (int k = 0; k < 3; k++) s += (double)T2i[3 * r + k] * tmp[3 * k + c];
+                Hd[3 * r + c] = s;
+            }
+        for (int k = 0; k < 9; k++) model_out[k] = (float)(Hd[k] / Hd[8]);
+        *ok = 1;
+    }
+}
+
+// Line PCA: one lane, sequential fp32 moments (sum_xy = 0 initialised),
+// closed-form eigenvector of the smaller eigenvalue of the 2x2 covariance (fp64).
+__global__ __launch_bounds__(64) void k_line_pca(const float2 *__restrict__ q, uint32_t n, float *model_out,
+                                                 int32_t *ok) {
+    if (threadIdx.x != 0) return;
+    float sx = 0, sy = 0, sxy = 0, sx2 = 0, sy2 = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const float2 p = q[i];
+        sx += p.x;
+        sy += p.y;
+        sxy += p.x * p.y;
+        sx2 += p.x * p.x;
+        sy2 += p.y * p.y;
+    }
+    const float fn = (float)n;
+    const float mx = sx / fn, my = sy / fn;
+    const float c00 = sx2 - 2.f * sx * mx + fn * mx * mx;
+    const float c01 = sxy - sx * my - sy * mx + fn * mx * my;
+    const float c11 = sy2 - 2.f * sy * my + fn * my * my;
+    const double p = c00, qq = c11, r = c01;
+    const double half = 0.5 * (p - qq);
+    const double rad = sqrt(half * half + r * r);
+    const double lmin = 0.5 * (p + qq) - rad;
+    double vx, vy;
+    if (r == 0.0) {
+        if (p <= qq) { vx = 1.0; vy = 0.0; } else { vx = 0.0; vy = 1.0; }
+    } else if (fabs(lmin - p) > fabs(lmin - qq)) {
+        vx = r; vy = lmin - p;
+    } else {
+        vx = lmin - qq; vy = r;
+    }
+    const double nrm = sqrt(vx * vx + vy * vy);
+    const float a = (float)(vx / nrm), b = (float)(vy / nrm);
+    model_out[0] = a;
+    model_out[1] = b;
+    model_out[2] = -a * mx - b * my;
+    for (int k = 3; k < 9; k++) model_out[k] = 0.f;
+    *ok = 1;
+}
+
+hipError_t launch_nonminimal_h(hipStream_t st, const float4 *pts, const int32_t *idx, uint32_t n, float4 *q,
+                               double *partial, float *ws, float *model_out, int32_t *ok) {
+    hipLaunchKernelGGL(k_gather4, dim3((n + 255) / 256), dim3(256), 0, st, pts, idx, n, q);
+    hipLaunchKernelGGL(k_normalize, dim3(1), dim3(256), 0, st, q, n, ws);
+    const uint32_t nb = (n + kAtaBlock - 1) / kAtaBlock;
+    if (2 * n > 9) hipLaunchKernelGGL(k_ata_partial, dim3(nb), dim3(64), 0, st, q, n, partial);
+    hipLaunchKernelGGL(k_dlt_finish, dim3(1), dim3(64), 0, st, q, n, partial, nb, ws, model_out, ok);
+    return hipGetLastError();
+}
+
+hipError_t launch_nonminimal_line(hipStream_t st, const float2 *pts, const int32_t *idx, uint32_t n, float2 *q,
+                                  float *model_out, int32_t *ok) {
+    hipLaunchKernelGGL(k_gather2, dim3((n + 255) / 256), dim3(256), 0, st, pts, idx, n, q);
+    hipLaunchKernelGGL(k_line_pca, dim3(1), dim3(64), 0, st, q, n, model_out, ok);
+    return hipGetLastError();
+}
+
+}  // namespace usac

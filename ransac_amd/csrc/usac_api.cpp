@@ -1,0 +1,557 @@
+// usac_api.cpp -- C-ABI (include/usac_gpu.h) over the HIP kernels, plus the batched
+// Ransac::run replay.  Host code only; every model estimation and every residual runs on
+// the device -- there is no CPU compute path (a context without a usable GPU fails at
+// usac_create with USAC_ERR_HIP).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "../../include/usac_gpu.h"
+#include "usac_host.hpp"
+#include "usac_kernels.h"
+
+namespace {
+
+constexpr uint32_t kDefaultBatch = 8192;
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    hipError_t reserve(size_t b) {
+        if (b <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, b);
+        if (e == hipSuccess) bytes = b;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T *as() const {
+        return static_cast<T *>(p);
+    }
+};
+
+}  // namespace
+
+struct usac_ctx {
+    int device = 0;
+    int estimator = 0;
+    uint32_t n = 0, cols = 0, m = 0;
+    int dlt_mode = USAC_DLT_THIN;
+    int chunks = 4;
+    hipStream_t stream = nullptr;
+    DevBuf pts;
+    // batch buffers
+    DevBuf samples, models, counts, sums, best, hostmodels;
+    // single-model / polish buffers
+    DevBuf one_model, inl_idx, inl_cnt, inl_sum, q, partial, ws, nm_model, nm_ok;
+    // comm
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    DevBuf rec_send, rec_all;
+    // timing
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    float last_ms[3] = {0, 0, 0};
+    bool timed_pending = false;
+    std::string err;
+};
+
+namespace {
+
+int fail(usac_ctx *c, int code, const std::string &msg) {
+    if (c) c->err = msg;
+    return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                      \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return fail((ctx), USAC_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define NCCL_TRY(ctx, expr)                                                                        \
+    do {                                                                                           \
+        ncclResult_t r_ = (expr);                                                                  \
+        if (r_ != ncclSuccess)                                                                     \
+            return fail((ctx), USAC_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+bool two_view(const usac_ctx *c) { return c->estimator == USAC_HOMOGRAPHY; }
+int ncomp(const usac_ctx *c) { return c->estimator == USAC_HOMOGRAPHY ? 9 : 3; }
+int ncomp_dev(const usac_ctx *c) { return c->estimator == USAC_HOMOGRAPHY ? 18 : 3; }
+
+int ensure_batch(usac_ctx *c, uint32_t B) {
+    HIP_TRY(c, c->samples.reserve(sizeof(int32_t) * (size_t)B * c->m));
+    HIP_TRY(c, c->models.reserve(sizeof(float) * (size_t)B * ncomp_dev(c)));
+    HIP_TRY(c, c->counts.reserve(sizeof(int32_t) * (size_t)B));
+    HIP_TRY(c, c->sums.reserve(sizeof(float) * (size_t)B));
+    HIP_TRY(c, c->best.reserve(sizeof(usac_record)));
+    HIP_TRY(c, c->hostmodels.reserve(sizeof(float) * 9 * (size_t)B));
+    return USAC_OK;
+}
+
+int ensure_single(usac_ctx *c) {
+    HIP_TRY(c, c->one_model.reserve(sizeof(float) * 9));
+    HIP_TRY(c, c->inl_idx.reserve(sizeof(int32_t) * (size_t)std::max<uint32_t>(c->n, 1)));
+    HIP_TRY(c, c->inl_cnt.reserve(sizeof(int32_t)));
+    HIP_TRY(c, c->inl_sum.reserve(sizeof(float)));
+    HIP_TRY(c, c->q.reserve(sizeof(float) * 4 * (size_t)std::max<uint32_t>(c->n, 1)));
+    HIP_TRY(c, c->partial.reserve(sizeof(double) * 45 * ((size_t)c->n / 64 + 2)));
+    HIP_TRY(c, c->ws.reserve(sizeof(float) * 32));
+    HIP_TRY(c, c->nm_model.reserve(sizeof(float) * 9));
+    HIP_TRY(c, c->nm_ok.reserve(sizeof(int32_t)));
+    return USAC_OK;
+}
+
+// solve (samples on device, or device RNG when samples_dev == nullptr) into c->models
+hipError_t enqueue_solve(usac_ctx *c, const int32_t *samples_dev, uint32_t B, uint64_t seed, uint64_t first_hyp,
+                         int32_t *samples_out) {
+    if (two_view(c))
+        return usac::launch_solve_h4(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, seed,
+                                     first_hyp, c->dlt_mode == USAC_DLT_NULLSPACE, c->models.as<float>());
+    return usac::launch_solve_line(c->stream, c->pts.as<float2>(), c->n, samples_dev, samples_out, B, seed, first_hyp,
+                                   c->models.as<float>());
+}
+
+hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
+    if (two_view(c))
+        return usac::launch_score_h(c->stream, chunks, c->pts.as<float4>(), c->n, c->models.as<float>(), B, thr,
+                                    c->counts.as<int32_t>(), c->sums.as<float>());
+    return usac::launch_score_line(c->stream, chunks, c->pts.as<float2>(), c->n, c->models.as<float>(), B, thr,
+                                   c->counts.as<int32_t>(), c->sums.as<float>());
+}
+
+// exact single-model inliers into c->inl_idx / inl_cnt / inl_sum (device)
+hipError_t enqueue_inliers(usac_ctx *c, const float *model_dev, float thr) {
+    if (two_view(c))
+        return usac::launch_inliers_h(c->stream, c->pts.as<float4>(), c->n, model_dev, thr, c->inl_idx.as<int32_t>(),
+                                      c->inl_cnt.as<int32_t>(), c->inl_sum.as<float>());
+    return usac::launch_inliers_line(c->stream, c->pts.as<float2>(), c->n, model_dev, thr, c->inl_idx.as<int32_t>(),
+                                     c->inl_cnt.as<int32_t>(), c->inl_sum.as<float>());
+}
+
+hipError_t enqueue_nonminimal(usac_ctx *c, const int32_t *idx_dev, uint32_t n) {
+    if (two_view(c))
+        return usac::launch_nonminimal_h(c->stream, c->pts.as<float4>(), idx_dev, n, c->q.as<float4>(),
+                                         c->partial.as<double>(), c->ws.as<float>(), c->nm_model.as<float>(),
+                                         c->nm_ok.as<int32_t>());
+    return usac::launch_nonminimal_line(c->stream, c->pts.as<float2>(), idx_dev, n, c->q.as<float2>(),
+                                        c->nm_model.as<float>(), c->nm_ok.as<int32_t>());
+}
+
+bool rec_better(const usac_record &a, const usac_record &b) {
+    if (!a.valid) return false;
+    if (!b.valid) return true;
+    if (a.inliers != b.inliers) return a.inliers > b.inliers;
+    if (a.score != b.score) return a.score > b.score;
+    return a.hyp_index < b.hyp_index;
+}
+
+}  // namespace
+
+extern "C" {
+
+int usac_abi_version(void) { return USAC_ABI_VERSION; }
+
+int usac_create(usac_ctx **out, int device, int estimator, const float *pts, uint32_t n, uint32_t cols) {
+    if (!out) return USAC_ERR_ARG;
+    *out = nullptr;
+    if (estimator != USAC_LINE2D && estimator != USAC_HOMOGRAPHY) return USAC_ERR_UNSUPPORTED;
+    if ((estimator == USAC_LINE2D && cols != 2) || (estimator == USAC_HOMOGRAPHY && cols != 4)) return USAC_ERR_ARG;
+    if (n == 0 || !pts) return USAC_ERR_ARG;
+    usac_ctx *c = new usac_ctx();
+    c->device = device;
+    c->estimator = estimator;
+    c->n = n;
+    c->cols = cols;
+    c->m = estimator == USAC_LINE2D ? 2 : 4;
+    int rc = USAC_OK;
+    do {
+        hipError_t e = hipSetDevice(device);
+        if (e != hipSuccess) { rc = fail(c, USAC_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e)); break; }
+        e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) { rc = fail(c, USAC_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e)); break; }
+        for (auto &ev : c->ev) {
+            e = hipEventCreate(&ev);
+            if (e != hipSuccess) break;
+        }
+        if (e != hipSuccess) { rc = fail(c, USAC_ERR_HIP, "hipEventCreate failed"); break; }
+        e = c->pts.reserve(sizeof(float) * (size_t)n * cols);
+        if (e != hipSuccess) { rc = fail(c, USAC_ERR_HIP, "hipMalloc points failed"); break; }
+        e = hipMemcpy(c->pts.p, pts, sizeof(float) * (size_t)n * cols, hipMemcpyHostToDevice);
+        if (e != hipSuccess) { rc = fail(c, USAC_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e)); break; }
+    } while (0);
+    if (rc != USAC_OK) {
+        // keep the message reachable for the caller through a static copy
+        static thread_local std::string last;
+        last = c->err;
+        usac_destroy(c);
+        fprintf(stderr, "usac_create: %s\n", last.c_str());
+        return rc;
+    }
+    *out = c;
+    return USAC_OK;
+}
+
+void usac_destroy(usac_ctx *c) {
+    if (!c) return;
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm) ncclCommDestroy(c->comm);
+    for (DevBuf *b : {&c->pts, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels, &c->one_model,
+                      &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok,
+                      &c->rec_send, &c->rec_all})
+        b->release();
+    for (auto &ev : c->ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char *usac_last_error(const usac_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int usac_set_dlt_mode(usac_ctx *c, int mode) {
+    if (!c || (mode != USAC_DLT_THIN && mode != USAC_DLT_NULLSPACE)) return USAC_ERR_ARG;
+    c->dlt_mode = mode;
+    return USAC_OK;
+}
+
+int usac_set_score_chunks(usac_ctx *c, int chunks) {
+    if (!c || (chunks != 1 && chunks != 2 && chunks != 4 && chunks != 8)) return USAC_ERR_ARG;
+    c->chunks = chunks;
+    return USAC_OK;
+}
+
+uint32_t usac_sample_size(const usac_ctx *c) { return c ? c->m : 0; }
+uint32_t usac_num_points(const usac_ctx *c) { return c ? c->n : 0; }
+
+int usac_estimate_models(usac_ctx *c, const int32_t *samples, uint32_t B, float *models, int32_t *n_models) {
+    if (!c || !samples || !models || B == 0) return USAC_ERR_ARG;
+    for (uint64_t i = 0; i < (uint64_t)B * c->m; i++)
+        if (samples[i] < 0 || (uint32_t)samples[i] >= c->n) return fail(c, USAC_ERR_ARG, "sample index out of range");
+    int rc = ensure_batch(c, B);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipMemcpyAsync(c->samples.p, samples, sizeof(int32_t) * (size_t)B * c->m, hipMemcpyHostToDevice,
+                              c->stream));
+    HIP_TRY(c, enqueue_solve(c, c->samples.as<int32_t>(), B, 0, 0, nullptr));
+    std::vector<float> soa((size_t)ncomp(c) * B);
+    HIP_TRY(c, hipMemcpyAsync(soa.data(), c->models.p, sizeof(float) * soa.size(), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    const int nc = ncomp(c);
+    for (uint32_t h = 0; h < B; h++) {
+        for (int k = 0; k < 9; k++) models[9 * (size_t)h + k] = k < nc ? soa[(size_t)k * B + h] : 0.f;
+        if (n_models) n_models[h] = 1;
+    }
+    return USAC_OK;
+}
+
+int usac_score_models(usac_ctx *c, const float *models, uint32_t nm, float thr, int32_t *counts, float *sums) {
+    if (!c || !models || !counts || nm == 0) return USAC_ERR_ARG;
+    int rc = ensure_batch(c, nm);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipMemcpyAsync(c->hostmodels.p, models, sizeof(float) * 9 * (size_t)nm, hipMemcpyHostToDevice, c->stream));
+    if (two_view(c))
+        HIP_TRY(c, usac::launch_prepare_h(c->stream, c->hostmodels.as<float>(), nm, c->models.as<float>()));
+    else
+        HIP_TRY(c, usac::launch_prepare_line(c->stream, c->hostmodels.as<float>(), nm, c->models.as<float>()));
+    HIP_TRY(c, enqueue_score(c, nm, thr, 1));
+    HIP_TRY(c, hipMemcpyAsync(counts, c->counts.p, sizeof(int32_t) * nm, hipMemcpyDeviceToHost, c->stream));
+    if (sums) HIP_TRY(c, hipMemcpyAsync(sums, c->sums.p, sizeof(float) * nm, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return USAC_OK;
+}
+
+int usac_get_inliers(usac_ctx *c, const float *model, float thr, int32_t *idx, uint32_t *n, float *sum) {
+    if (!c || !model) return USAC_ERR_ARG;
+    int rc = ensure_single(c);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipMemcpyAsync(c->one_model.p, model, sizeof(float) * 9, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, enqueue_inliers(c, c->one_model.as<float>(), thr));
+    int32_t cnt = 0;
+    float s = 0.f;
+    HIP_TRY(c, hipMemcpyAsync(&cnt, c->inl_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(&s, c->inl_sum.p, sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (idx && cnt > 0)
+        HIP_TRY(c, hipMemcpy(idx, c->inl_idx.p, sizeof(int32_t) * (size_t)cnt, hipMemcpyDeviceToHost));
+    if (n) *n = (uint32_t)cnt;
+    if (sum) *sum = s;
+    return USAC_OK;
+}
+
+int usac_nonminimal(usac_ctx *c, const int32_t *idx, uint32_t n, float *model) {
+    if (!c || !idx || !model) return USAC_ERR_ARG;
+    if (n == 0) return fail(c, USAC_ERR_ARG, "empty sample");
+    for (uint32_t i = 0; i < n; i++)
+        if (idx[i] < 0 || (uint32_t)idx[i] >= c->n) return fail(c, USAC_ERR_ARG, "index out of range");
+    int rc = ensure_single(c);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, c->inl_idx.reserve(sizeof(int32_t) * std::max<size_t>(n, c->n)));
+    HIP_TRY(c, c->q.reserve(sizeof(float) * 4 * (size_t)n));
+    HIP_TRY(c, c->partial.reserve(sizeof(double) * 45 * ((size_t)n / 64 + 2)));
+    HIP_TRY(c, hipMemcpyAsync(c->inl_idx.p, idx, sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, enqueue_nonminimal(c, c->inl_idx.as<int32_t>(), n));
+    int32_t ok = 0;
+    HIP_TRY(c, hipMemcpyAsync(model, c->nm_model.p, sizeof(float) * 9, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(&ok, c->nm_ok.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return ok ? USAC_OK : fail(c, USAC_ERR_NO_MODEL, "non-minimal estimation failed");
+}
+
+int usac_hypothesize_score(usac_ctx *c, const int32_t *samples, uint32_t B, uint64_t seed, uint64_t first_hyp,
+                           float thr, int32_t *counts, float *sums, usac_record *best) {
+    if (!c || B == 0) return USAC_ERR_ARG;
+    if (samples)
+        for (uint64_t i = 0; i < (uint64_t)B * c->m; i++)
+            if (samples[i] < 0 || (uint32_t)samples[i] >= c->n) return fail(c, USAC_ERR_ARG, "sample index out of range");
+    int rc = ensure_batch(c, B);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (samples)
+        HIP_TRY(c, hipMemcpyAsync(c->samples.p, samples, sizeof(int32_t) * (size_t)B * c->m, hipMemcpyHostToDevice,
+                                  c->stream));
+    HIP_TRY(c, enqueue_solve(c, samples ? c->samples.as<int32_t>() : nullptr, B, seed, first_hyp,
+                             samples ? nullptr : c->samples.as<int32_t>()));
+    // per-hypothesis outputs requested -> exact sequential sums (one chunk)
+    const int chunks = (counts || sums) ? 1 : c->chunks;
+    HIP_TRY(c, enqueue_score(c, B, thr, chunks));
+    HIP_TRY(c, usac::launch_argmax(c->stream, c->counts.as<int32_t>(), c->sums.as<float>(), B, c->models.as<float>(),
+                                   ncomp(c), first_hyp, c->best.as<usac_record>()));
+    if (counts) HIP_TRY(c, hipMemcpyAsync(counts, c->counts.p, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
+    if (sums) HIP_TRY(c, hipMemcpyAsync(sums, c->sums.p, sizeof(float) * B, hipMemcpyDeviceToHost, c->stream));
+    if (best) HIP_TRY(c, hipMemcpyAsync(best, c->best.p, sizeof(usac_record), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return USAC_OK;
+}
+
+int usac_hypothesize_async(usac_ctx *c, uint32_t B, uint64_t seed, uint64_t first_hyp, float thr) {
+    if (!c || B == 0) return USAC_ERR_ARG;
+    int rc = ensure_batch(c, B);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
+    HIP_TRY(c, enqueue_solve(c, nullptr, B, seed, first_hyp, nullptr));
+    HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
+    HIP_TRY(c, enqueue_score(c, B, thr, c->chunks));
+    HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
+    HIP_TRY(c, usac::launch_argmax(c->stream, c->counts.as<int32_t>(), c->sums.as<float>(), B, c->models.as<float>(),
+                                   ncomp(c), first_hyp, c->best.as<usac_record>()));
+    HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
+    c->timed_pending = true;
+    return USAC_OK;
+}
+
+int usac_fetch_best(usac_ctx *c, usac_record *best) {
+    if (!c || !best) return USAC_ERR_ARG;
+    HIP_TRY(c, hipMemcpyAsync(best, c->best.p, sizeof(usac_record), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return USAC_OK;
+}
+
+int usac_sync(usac_ctx *c) {
+    if (!c) return USAC_ERR_ARG;
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return USAC_OK;
+}
+
+int usac_last_timings(usac_ctx *c, float *ms3) {
+    if (!c || !ms3) return USAC_ERR_ARG;
+    if (c->timed_pending) {
+        HIP_TRY(c, hipEventSynchronize(c->ev[3]));
+        HIP_TRY(c, hipEventElapsedTime(&c->last_ms[0], c->ev[0], c->ev[3]));
+        HIP_TRY(c, hipEventElapsedTime(&c->last_ms[1], c->ev[1], c->ev[2]));
+        HIP_TRY(c, hipEventElapsedTime(&c->last_ms[2], c->ev[0], c->ev[1]));
+        c->timed_pending = false;
+    }
+    memcpy(ms3, c->last_ms, sizeof(c->last_ms));
+    return USAC_OK;
+}
+
+uint32_t usac_std_termination(uint32_t inliers, uint32_t points_size, uint32_t sample_size, float desired_prob,
+                              uint32_t max_iterations) {
+    usac::StandardTerminationCriteria t(desired_prob, sample_size, points_size, max_iterations);
+    return t.getUpBoundIterations(inliers);
+}
+
+int usac_uniform_samples(uint32_t seed, uint32_t n_points, uint32_t m, uint32_t count, int32_t *out) {
+    if (!out || n_points == 0 || m == 0) return USAC_ERR_ARG;
+    usac::UniformSampler s(seed, n_points, m);
+    for (uint32_t i = 0; i < count; i++) s.generateSample(out + (size_t)i * m);
+    return USAC_OK;
+}
+
+// Ransac::run (ransac.cpp:14-238), Uniform sampler, no LO/SPRT.  Samples are drawn on the
+// host from the glibc stream in loop order and shipped in batches; the device solves and
+// scores a whole batch (exact counts, exact sequential sums); the host replays the
+// sequential loop over the batch's (count, sum) list -- Score::bigger, termination
+// update at each new best, `while (iters < max_iters)` -- which reproduces the reference's
+// iteration sequence exactly because max_iters changes only at best-score updates
+// (SURVEY Q24).  Then the <= 4-pass non-minimal polish on the device.
+int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, int32_t *inliers_out,
+                    usac_record *records, uint32_t rec_cap) {
+    if (!c || !prm || !out) return USAC_ERR_ARG;
+    memset(out, 0, sizeof(*out));
+    const auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY(c, hipSetDevice(c->device));
+    const uint32_t batch = prm->batch ? prm->batch : kDefaultBatch;
+    int rc = ensure_batch(c, batch);
+    if (rc) return rc;
+    rc = ensure_single(c);
+    if (rc) return rc;
+    const int saved_mode = c->dlt_mode;
+    c->dlt_mode = prm->dlt_mode;
+
+    usac::UniformSampler sampler(prm->seed, c->n, c->m);
+    usac::StandardTerminationCriteria term(prm->desired_prob, c->m, c->n, prm->max_iterations);
+    std::vector<int32_t> hs((size_t)batch * c->m), hc(batch);
+    std::vector<float> hsum(batch), hmod((size_t)ncomp(c) * batch);
+    usac::Score best;
+    float best_model[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t iters = 0, max_iters = prm->max_iterations;
+    int32_t nrec = 0;
+    uint32_t batches = 0;
+    while (iters < max_iters) {
+        const uint32_t B = std::min(batch, max_iters - iters);
+        for (uint32_t j = 0; j < B; j++) sampler.generateSample(hs.data() + (size_t)j * c->m);
+        HIP_TRY(c, hipMemcpyAsync(c->samples.p, hs.data(), sizeof(int32_t) * (size_t)B * c->m, hipMemcpyHostToDevice,
+                                  c->stream));
+        HIP_TRY(c, enqueue_solve(c, c->samples.as<int32_t>(), B, 0, iters, nullptr));
+        HIP_TRY(c, enqueue_score(c, B, prm->threshold, 1));
+        HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(hsum.data(), c->sums.p, sizeof(float) * B, hipMemcpyDeviceToHost, c->stream));
+        for (int k = 0; k < ncomp(c); k++)
+            HIP_TRY(c, hipMemcpyAsync(hmod.data() + (size_t)k * batch, c->models.as<float>() + (size_t)k * B,
+                                      sizeof(float) * B, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        batches++;
+        for (uint32_t j = 0; j < B && iters < max_iters; j++, iters++) {
+            usac::Score cur;
+            cur.inlier_number = hc[j];
+            cur.score = hsum[j];
+            if (cur.bigger(best)) {
+                best = cur;
+                for (int k = 0; k < 9; k++) best_model[k] = k < ncomp(c) ? hmod[(size_t)k * batch + j] : 0.f;
+                max_iters = term.getUpBoundIterations((uint32_t)best.inlier_number);
+                if (records && (uint32_t)nrec < rec_cap) {
+                    usac_record &r = records[nrec];
+                    r.hyp_index = iters;
+                    r.inliers = cur.inlier_number;
+                    r.score = cur.score;
+                    memcpy(r.model, best_model, sizeof(best_model));
+                    r.valid = 1;
+                }
+                nrec++;
+            }
+        }
+    }
+    out->iters = iters;
+    out->n_records = nrec;
+    out->batches = batches;
+    memcpy(out->minimal_model, best_model, sizeof(best_model));
+    out->minimal_inliers = best.inlier_number;
+    c->dlt_mode = saved_mode;
+    if (best.inlier_number == 0) {
+        memcpy(out->model, best_model, sizeof(best_model));
+        return fail(c, USAC_ERR_NO_MODEL, "best score is 0 (ransac.cpp:143-147)");
+    }
+
+    // ---- polish (ransac.cpp:157-207) on the device
+    const float thr = prm->threshold;
+    int32_t cnt = 0, ok = 0;
+    float s = 0.f;
+    auto score_inliers = [&](const float *model_host) -> int {
+        HIP_TRY(c, hipMemcpyAsync(c->one_model.p, model_host, sizeof(float) * 9, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, enqueue_inliers(c, c->one_model.as<float>(), thr));
+        HIP_TRY(c, hipMemcpyAsync(&cnt, c->inl_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(&s, c->inl_sum.p, sizeof(float), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        return USAC_OK;
+    };
+    if ((rc = score_inliers(best_model))) return rc;  // quality->getInliers(best_model)
+    int prev = 0;
+    float nm_model[9];
+    for (int norm = 0; norm < 4; norm++) {
+        HIP_TRY(c, enqueue_nonminimal(c, c->inl_idx.as<int32_t>(), (uint32_t)best.inlier_number));
+        HIP_TRY(c, hipMemcpyAsync(nm_model, c->nm_model.p, sizeof(float) * 9, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(&ok, c->nm_ok.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        if (!ok) break;
+        if ((rc = score_inliers(nm_model))) return rc;
+        if ((double)((float)cnt / (float)best.inlier_number) < 0.8) break;
+        if (cnt <= prev) break;
+        prev = cnt;
+        best.inlier_number = cnt;
+        best.score = s;
+        memcpy(best_model, nm_model, sizeof(best_model));
+        out->polish_passes++;
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    if ((rc = score_inliers(best_model))) return rc;  // ransac.cpp:214
+    if (inliers_out && cnt > 0)
+        HIP_TRY(c, hipMemcpy(inliers_out, c->inl_idx.p, sizeof(int32_t) * (size_t)cnt, hipMemcpyDeviceToHost));
+    memcpy(out->model, best_model, sizeof(best_model));
+    out->inliers = best.inlier_number;
+    out->time_us = std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
+    return USAC_OK;
+}
+
+// ---------------------------------------------------------------- multi-GPU
+int usac_comm_unique_id(uint8_t *id128) {
+    if (!id128) return USAC_ERR_ARG;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return USAC_ERR_HIP;
+    memcpy(id128, &id, sizeof(id) < 128 ? sizeof(id) : 128);
+    return USAC_OK;
+}
+
+int usac_comm_init(usac_ctx *c, int nranks, int rank, const uint8_t *id128) {
+    if (!c || !id128 || nranks < 1 || rank < 0 || rank >= nranks) return USAC_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    ncclUniqueId id;
+    memcpy(&id, id128, sizeof(id) < 128 ? sizeof(id) : 128);
+    NCCL_TRY(c, ncclCommInitRank(&c->comm, nranks, id, rank));
+    c->nranks = nranks;
+    c->rank = rank;
+    HIP_TRY(c, c->rec_send.reserve(sizeof(usac_record)));
+    HIP_TRY(c, c->rec_all.reserve(sizeof(usac_record) * (size_t)nranks));
+    return USAC_OK;
+}
+
+int usac_allgather_records(usac_ctx *c, const usac_record *local, usac_record *all) {
+    if (!c || !local || !all) return USAC_ERR_ARG;
+    if (!c->comm) return fail(c, USAC_ERR_ARG, "usac_comm_init not called");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipMemcpyAsync(c->rec_send.p, local, sizeof(usac_record), hipMemcpyHostToDevice, c->stream));
+    NCCL_TRY(c, ncclAllGather(c->rec_send.p, c->rec_all.p, sizeof(usac_record), ncclUint8, c->comm, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(all, c->rec_all.p, sizeof(usac_record) * (size_t)c->nranks, hipMemcpyDeviceToHost,
+                              c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return USAC_OK;
+}
+
+int usac_merge_records(const usac_record *recs, uint32_t n, usac_record *best) {
+    if (!recs || !best || n == 0) return USAC_ERR_ARG;
+    usac_record b = recs[0];
+    for (uint32_t i = 1; i < n; i++)
+        if (rec_better(recs[i], b)) b = recs[i];
+    *best = b;
+    return USAC_OK;
+}
+
+}  // extern "C"

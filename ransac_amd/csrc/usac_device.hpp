@@ -1,0 +1,234 @@
+// usac_device.hpp -- per-hypothesis device math of the hot path (gfx950, wave64).
+//
+// Every routine states the reference code it computes and the exact floating-point
+// recipe (DESIGN.md "Numerics"); the CPU oracle (oracle/usac_oracle.c) restates the same
+// reference independently, and the parity tests compare the two bit for bit.
+// Compiled with -ffp-contract=off: no FMA contraction, IEEE fp32/fp64 division and
+// square root (hipcc's default correctly-rounded lowering), denormals kept.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace usac {
+
+// ---------------------------------------------------------------- counter-based sampler
+// Throughput-mode sampler: one SplitMix64 stream per hypothesis keyed by
+// (seed, global hypothesis index), xorshift-style mixing, Lemire multiply-shift into
+// [0, N), duplicates rejected (a minimal sample has distinct points).
+__device__ __forceinline__ uint64_t splitmix64(uint64_t &s) {
+    uint64_t z = (s += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+template <int M>
+__device__ __forceinline__ void draw_sample(uint64_t seed, uint64_t hyp, uint32_t n, int32_t (&s)[M]) {
+    uint64_t st = seed ^ (hyp * 0xD1B54A32D192ED03ull);
+#pragma unroll
+    for (int i = 0; i < M; i++) {
+        int32_t v;
+        bool dup;
+        do {
+            uint64_t r = splitmix64(st);
+            v = (int32_t)(((r >> 32) * (uint64_t)n) >> 32);
+            dup = false;
+#pragma unroll
+            for (int j = 0; j < i; j++) dup |= (s[j] == v);
+        } while (dup);
+        s[i] = v;
+    }
+}
+
+// ---------------------------------------------------------------- 3x3 inverse
+// cv::Mat::inv() of a CV_32F 3x3 (homography_estimator.hpp:35): fp64 determinant and
+// cofactors from exact float*float products, times (1/det) in fp64, one cast to float;
+// det == 0 -> zero matrix.
+__device__ __forceinline__ void inv3x3(const float *m, float *dst) {
+#define M_(r, c) ((double)m[3 * (r) + (c)])
+    double d = M_(0, 0) * (M_(1, 1) * M_(2, 2) - M_(1, 2) * M_(2, 1)) -
+               M_(0, 1) * (M_(1, 0) * M_(2, 2) - M_(1, 2) * M_(2, 0)) +
+               M_(0, 2) * (M_(1, 0) * M_(2, 1) - M_(1, 1) * M_(2, 0));
+    if (d == 0.0) {
+#pragma unroll
+        for (int i = 0; i < 9; i++) dst[i] = 0.f;
+        return;
+    }
+    d = 1.0 / d;
+    dst[0] = (float)((M_(1, 1) * M_(2, 2) - M_(1, 2) * M_(2, 1)) * d);
+    dst[1] = (float)((M_(0, 2) * M_(2, 1) - M_(0, 1) * M_(2, 2)) * d);
+    dst[2] = (float)((M_(0, 1) * M_(1, 2) - M_(0, 2) * M_(1, 1)) * d);
+    dst[3] = (float)((M_(1, 2) * M_(2, 0) - M_(1, 0) * M_(2, 2)) * d);
+    dst[4] = (float)((M_(0, 0) * M_(2, 2) - M_(0, 2) * M_(2, 0)) * d);
+    dst[5] = (float)((M_(0, 2) * M_(1, 0) - M_(0, 0) * M_(1, 2)) * d);
+    dst[6] = (float)((M_(1, 0) * M_(2, 1) - M_(1, 1) * M_(2, 0)) * d);
+    dst[7] = (float)((M_(0, 1) * M_(2, 0) - M_(0, 0) * M_(2, 1)) * d);
+    dst[8] = (float)((M_(0, 0) * M_(1, 1) - M_(0, 1) * M_(1, 0)) * d);
+#undef M_
+}
+
+// ---------------------------------------------------------------- 4-pt DLT
+// Rows of the DLT system exactly as dlt.cpp:24-41 (fp32 products), widened to fp64.
+__device__ __forceinline__ void dlt_rows(float x1, float y1, float x2, float y2, double *r0, double *r1) {
+    r0[0] = (double)(-x1); r0[1] = (double)(-y1); r0[2] = -1.0;
+    r0[3] = 0.0; r0[4] = 0.0; r0[5] = 0.0;
+    r0[6] = (double)(x2 * x1); r0[7] = (double)(x2 * y1); r0[8] = (double)x2;
+    r1[0] = 0.0; r1[1] = 0.0; r1[2] = 0.0;
+    r1[3] = (double)(-x1); r1[4] = (double)(-y1); r1[5] = -1.0;
+    r1[6] = (double)(y2 * x1); r1[7] = (double)(y2 * y1); r1[8] = (double)y2;
+}
+
+// One-sided (Hestenes) Jacobi on the R rows of W (fp64), the row-space part of the thin
+// cv::SVD::compute of dlt.cpp:43.  Spec (identical in the oracle): sweeps < 30, pairs
+// p < q row-major, sums over k = 0..8 in order, skip when |g| <= 1e-14*sqrt(a*b),
+// zeta = (b-a)/(2g), t = sign(zeta)/(|zeta|+sqrt(1+zeta^2)), c = 1/sqrt(1+t^2), s = c*t,
+// stop after a sweep without rotation.  Fully unrolled so W stays in VGPRs.
+template <int R>
+__device__ __forceinline__ void row_jacobi(double (&W)[R][9]) {
+    for (int sweep = 0; sweep < 30; sweep++) {
+        bool rotated = false;
+#pragma unroll
+        for (int p = 0; p < R - 1; p++) {
+#pragma unroll
+            for (int q = p + 1; q < R; q++) {
+                double a = 0.0, b = 0.0, g = 0.0;
+#pragma unroll
+                for (int k = 0; k < 9; k++) {
+                    a += W[p][k] * W[p][k];
+                    b += W[q][k] * W[q][k];
+                    g += W[p][k] * W[q][k];
+                }
+                if (!(fabs(g) <= 1e-14 * sqrt(a * b))) {
+                    rotated = true;
+                    double zeta = (b - a) / (2.0 * g);
+                    double t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                    double c = 1.0 / sqrt(1.0 + t * t);
+                    double s = c * t;
+#pragma unroll
+                    for (int k = 0; k < 9; k++) {
+                        double wp = W[p][k], wq = W[q][k];
+                        W[p][k] = c * wp - s * wq;
+                        W[q][k] = s * wp + c * wq;
+                    }
+                }
+            }
+        }
+        if (!rotated) break;
+    }
+}
+
+// Model vector from the converged rows (oracle pick_vector):
+//  thin      -> row of smallest squared norm, first on ties  (vt.row(vt.rows-1))
+//  nullspace -> unit vector orthogonal to all non-zero rows: rows normalised in place,
+//               start axis = least represented coordinate, two Gram-Schmidt passes.
+template <int R>
+__device__ __forceinline__ void pick_vector(double (&W)[R][9], int nullspace, double *h) {
+    double n2[R];
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+        double a = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) a += W[i][k] * W[i][k];
+        n2[i] = a;
+    }
+    if (!nullspace) {
+        double bestn = n2[0];
+#pragma unroll
+        for (int k = 0; k < 9; k++) h[k] = W[0][k];
+#pragma unroll
+        for (int i = 1; i < R; i++) {
+            if (n2[i] < bestn) {
+                bestn = n2[i];
+#pragma unroll
+                for (int k = 0; k < 9; k++) h[k] = W[i][k];
+            }
+        }
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < R; i++) {
+        if (n2[i] > 0.0) {
+            double inv = 1.0 / sqrt(n2[i]);
+#pragma unroll
+            for (int k = 0; k < 9; k++) W[i][k] = W[i][k] * inv;
+        }
+    }
+    int ks = 0;
+    double bestc = 0.0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        double c = 0.0;
+#pragma unroll
+        for (int i = 0; i < R; i++)
+            if (n2[i] > 0.0) c += W[i][k] * W[i][k];
+        if (k == 0 || c < bestc) {
+            bestc = c;
+            ks = k;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 9; k++) h[k] = (k == ks) ? 1.0 : 0.0;
+#pragma unroll
+    for (int pass = 0; pass < 2; pass++) {
+#pragma unroll
+        for (int i = 0; i < R; i++) {
+            if (n2[i] > 0.0) {
+                double d = 0.0;
+#pragma unroll
+                for (int k = 0; k < 9; k++) d += W[i][k] * h[k];
+#pragma unroll
+                for (int k = 0; k < 9; k++) h[k] -= d * W[i][k];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- residuals
+// HomographyEstimator::GetError (homography_estimator.hpp:85-110): fp32 projections
+// evaluated left to right, IEEE divisions, the two distances are double square roots
+// summed in double and rounded to float, halved.  No z guard: inf/NaN -> outlier.
+__device__ __forceinline__ float homography_error(const float *h, const float *hi, float x1, float y1, float x2,
+                                                  float y2) {
+    float ex2 = h[0] * x1 + h[1] * y1 + h[2];
+    float ey2 = h[3] * x1 + h[4] * y1 + h[5];
+    float ez2 = h[6] * x1 + h[7] * y1 + h[8];
+    ex2 = ex2 / ez2;
+    ey2 = ey2 / ez2;
+    float ex1 = hi[0] * x2 + hi[1] * y2 + hi[2];
+    float ey1 = hi[3] * x2 + hi[4] * y2 + hi[5];
+    float ez1 = hi[6] * x2 + hi[7] * y2 + hi[8];
+    ex1 = ex1 / ez1;
+    ey1 = ey1 / ez1;
+    float d2 = (x2 - ex2) * (x2 - ex2) + (y2 - ey2) * (y2 - ey2);
+    float d1 = (x1 - ex1) * (x1 - ex1) + (y1 - ey1) * (y1 - ey1);
+    float error = (float)(sqrt((double)d2) + sqrt((double)d1));
+    return error / 2;
+}
+
+// Line2DEstimator::GetError (line2d_estimator.hpp:154-156)
+__device__ __forceinline__ float line2d_error(float a, float b, float c, float x, float y) {
+    return fabsf(a * x + b * y + c);
+}
+
+// Line2DEstimator::EstimateModel (line2d_estimator.hpp:36-54)
+__device__ __forceinline__ void line2d_estimate(float x1, float y1, float x2, float y2, float *m) {
+    float a = y1 - y2;
+    float b = x2 - x1;
+    float mag = (float)sqrt((double)(a * a + b * b));
+    a = a / mag;
+    b = b / mag;
+    float c = (x1 * y2 - x2 * y1) / mag;
+    m[0] = a;
+    m[1] = b;
+    m[2] = c;
+}
+
+// Score::bigger (quality.hpp:22-26) extended to a strict total order with the earliest
+// hypothesis index winning exact ties (the sequential loop keeps the first).
+__device__ __forceinline__ bool record_better(int c1, float s1, uint32_t i1, int c2, float s2, uint32_t i2) {
+    if (c1 != c2) return c1 > c2;
+    if (s1 != s2) return s1 > s2;
+    return i1 < i2;
+}
+
+}  // namespace usac

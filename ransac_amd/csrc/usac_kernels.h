@@ -1,0 +1,38 @@
+// usac_kernels.h -- internal launchers (kernels.hip, kernels_nonmin.hip) used by the host
+// side of the C-ABI (usac_api.cpp).  Every launcher enqueues on `st` and returns the
+// launch status; none synchronises.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/usac_gpu.h"
+
+namespace usac {
+
+hipError_t launch_solve_h4(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
+                           int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, int nullspace,
+                           float *models);
+hipError_t launch_prepare_h(hipStream_t st, const float *in, uint32_t B, float *models);
+hipError_t launch_score_h(hipStream_t st, int chunks, const float4 *pts, uint32_t n, const float *models, uint32_t B,
+                          float thr, int32_t *counts, float *sums);
+
+hipError_t launch_solve_line(hipStream_t st, const float2 *pts, uint32_t n, const int32_t *samples_in,
+                             int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, float *models);
+hipError_t launch_prepare_line(hipStream_t st, const float *in, uint32_t B, float *models);
+hipError_t launch_score_line(hipStream_t st, int chunks, const float2 *pts, uint32_t n, const float *models,
+                             uint32_t B, float thr, int32_t *counts, float *sums);
+
+hipError_t launch_argmax(hipStream_t st, const int32_t *counts, const float *sums, uint32_t B, const float *models,
+                         int ncomp, uint64_t first_hyp, usac_record *out);
+
+hipError_t launch_inliers_h(hipStream_t st, const float4 *pts, uint32_t n, const float *model, float thr,
+                            int32_t *idx, int32_t *count, float *sum);
+hipError_t launch_inliers_line(hipStream_t st, const float2 *pts, uint32_t n, const float *model, float thr,
+                               int32_t *idx, int32_t *count, float *sum);
+
+hipError_t launch_nonminimal_h(hipStream_t st, const float4 *pts, const int32_t *idx, uint32_t n, float4 *q,
+                               double *partial, float *ws, float *model_out, int32_t *ok);
+hipError_t launch_nonminimal_line(hipStream_t st, const float2 *pts, const int32_t *idx, uint32_t n, float2 *q,
+                                  float *model_out, int32_t *ok);
+
+}  // namespace usac

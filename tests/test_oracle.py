@@ -1,0 +1,97 @@
+"""The CPU oracle against the reference's own golden data (runs without a GPU).
+
+Pins (see oracle/usac_oracle.h):
+  * glibc random() KAT (the reference sampler's RNG);
+  * the homography residual + cv::Mat::inv restatement reproduces the reference's
+    published GT inlier counts on all 12 scenes (results/homography/*.csv, GT Inl);
+  * the line2d loop (Uniform sampler, 2-pt estimator, standard termination, PCA polish)
+    reproduces the published 50-run statistics (results/line2d/uniform_000.csv).
+"""
+import numpy as np
+import pytest
+
+from ransac_amd import synthetic
+
+
+def test_glibc_random_kat(oracle):
+    # glibc srandom(1) TYPE_3 stream (what the reference's random() yields with no srand)
+    assert list(oracle.glibc_stream(1, 5)) == [1804289383, 846930886, 1681692777, 1714636915, 1957747793]
+
+
+def test_uniform_sampler_pool_semantics(oracle):
+    n, m = 7, 4
+    s = oracle.uniform_samples(3, n, m, 50)
+    assert s.min() >= 0 and s.max() < n
+    # every n consecutive draws of the persistent pool are a permutation (uniform_sampler.hpp:42-54)
+    flat = s.reshape(-1)
+    for k in range(0, (flat.size // n) * n, n):
+        assert sorted(flat[k:k + n].tolist()) == list(range(n))
+
+
+def test_homography_gt_inliers_match_reference(oracle, homography_scenes):
+    for scene, (pts, model, gt) in homography_scenes.items():
+        assert oracle.gt_inliers_homography(pts, model, 2.0) == gt, scene
+
+
+def test_inverse_matches_numpy(oracle, homography_scenes):
+    for scene, (pts, model, gt) in homography_scenes.items():
+        inv, ok = oracle.inv3x3(model)
+        assert ok
+        ref = np.linalg.inv(model.astype(np.float64).reshape(3, 3)).reshape(9)
+        np.testing.assert_allclose(inv, ref, rtol=1e-5, atol=1e-9)
+    z, ok = oracle.inv3x3(np.zeros(9, np.float32))
+    assert not ok and not z.any()
+
+
+def test_termination_kat(oracle):
+    # SURVEY §8 a13 table (N=10k, m=4, p=.95) and the epsilon floor
+    assert oracle.std_termination(2000, 10000, 4, 0.95) == 1870
+    assert oracle.std_termination(3000, 10000, 4, 0.95) == 368
+    assert oracle.std_termination(5000, 10000, 4, 0.95) == 46
+    assert oracle.std_termination(1000, 10000, 4, 0.95) == 10000
+    assert oracle.std_termination(10000, 10000, 4, 0.95) == 0
+
+
+def test_dlt_nullspace_fits_exact_samples(oracle):
+    pts, H, inl = synthetic.homography_points(n=200, inlier_ratio=1.0, noise=0.0, seed=5)
+    est = oracle.Estimator(oracle.HOMOGRAPHY, pts, oracle.DLT_NULLSPACE)
+    for k in range(20):
+        sample = np.arange(4 * k, 4 * k + 4)
+        m = est.estimate(sample)[0].reshape(3, 3)
+        np.testing.assert_allclose(m / m[2, 2], H / H[2, 2], rtol=2e-3, atol=2e-5)
+    # the reference's thin-SVD row is NOT the null vector
+    thin = oracle.Estimator(oracle.HOMOGRAPHY, pts, oracle.DLT_THIN).estimate(np.arange(4))[0]
+    assert not np.allclose(thin.reshape(3, 3), H / H[2, 2], rtol=1e-2)
+
+
+def test_line2d_statistics_match_reference(oracle, line2d_scenes):
+    """50 seeded runs per scene vs the reference's published 50-run averages."""
+    for name, (pts, gt, st) in sorted(line2d_scenes.items())[:4]:
+        inl, its = [], []
+        for seed in range(1, 51):
+            r = oracle.ransac_run(oracle.LINE2D, pts, 10.0, 0.99, seed)
+            assert r["ret"] == 0
+            inl.append(r["inliers"])
+            its.append(r["iters"])
+        se_inl = max(st["std_inliers"], 1.0) / np.sqrt(50)
+        se_it = st["std_iters"] / np.sqrt(50)
+        assert abs(np.mean(inl) - st["avg_inliers"]) < 4 * se_inl + 1.5, (name, np.mean(inl), st)
+        assert abs(np.mean(its) - st["avg_iters"]) < 4 * se_it + 0.02 * st["avg_iters"], (name, np.mean(its), st)
+
+
+def test_homography_run_real_scene(oracle, homography_scenes):
+    pts, model, gt = homography_scenes["adam"]
+    for mode in (oracle.DLT_THIN, oracle.DLT_NULLSPACE):
+        r = oracle.ransac_run(oracle.HOMOGRAPHY, pts, 2.0, 0.95, 7, dlt_mode=mode)
+        assert r["ret"] == 0
+        # the reference reports 123-134 inliers after the polish on adam
+        assert 115 <= r["inliers"] <= 140, r["inliers"]
+        assert len(r["inlier_idx"]) == r["inliers"]
+
+
+def test_line2d_generator(oracle):
+    pts, gt = oracle.generate_line2d(11, 3.0, 100, 900, 1000, 1000)
+    assert pts.shape == (1000, 2)
+    assert abs(float(np.hypot(gt[0], gt[1])) - 1.0) < 1e-6
+    d = np.abs(pts[900:] @ gt[:2] + gt[2])
+    assert d.max() < 3.0 * 1.5
