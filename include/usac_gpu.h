@@ -131,6 +131,9 @@ int usac_sync(usac_ctx *ctx);
 int usac_last_timings(usac_ctx *ctx, float *ms3);
 /* Score-kernel split factor (point chunks per hypothesis tile, 1 = exact sequential sums). */
 int usac_set_score_chunks(usac_ctx *ctx, int chunks);
+/* Homography score kernel: 0 = guard-band fast path (default), 1 = exact reference
+ * expression for every pair (A/B and debugging; same results). */
+int usac_set_score_variant(usac_ctx *ctx, int variant);
 
 /* ---- loop --------------------------------------------------------------------- */
 uint32_t usac_std_termination(uint32_t inliers, uint32_t points_size, uint32_t sample_size, float desired_prob,

@@ -77,7 +77,7 @@ ABI_SYMBOLS = [
     "usac_create", "usac_destroy", "usac_last_error", "usac_abi_version", "usac_set_dlt_mode", "usac_sample_size",
     "usac_num_points", "usac_estimate_models", "usac_score_models", "usac_get_inliers", "usac_nonminimal",
     "usac_hypothesize_score", "usac_hypothesize_async", "usac_fetch_best", "usac_sync", "usac_last_timings",
-    "usac_set_score_chunks", "usac_std_termination", "usac_ransac_run", "usac_uniform_samples",
+    "usac_set_score_chunks", "usac_set_score_variant", "usac_std_termination", "usac_ransac_run", "usac_uniform_samples",
     "usac_comm_unique_id", "usac_comm_init", "usac_allgather_records", "usac_merge_records",
 ]
 
@@ -108,6 +108,7 @@ def lib():
         "usac_abi_version": (ctypes.c_int, []),
         "usac_set_dlt_mode": (ctypes.c_int, [_vp, ctypes.c_int]),
         "usac_set_score_chunks": (ctypes.c_int, [_vp, ctypes.c_int]),
+        "usac_set_score_variant": (ctypes.c_int, [_vp, ctypes.c_int]),
         "usac_sample_size": (ctypes.c_uint32, [_vp]),
         "usac_num_points": (ctypes.c_uint32, [_vp]),
         "usac_estimate_models": (ctypes.c_int, [_vp, i32p, ctypes.c_uint32, f32p, i32p]),
@@ -204,6 +205,10 @@ class Context:
 
     def set_score_chunks(self, chunks):
         self._check(lib().usac_set_score_chunks(self._h, int(chunks)), "set_score_chunks")
+
+    def set_score_variant(self, variant):
+        """0 = guard-band fast path (default), 1 = exact reference expression for every pair."""
+        self._check(lib().usac_set_score_variant(self._h, int(variant)), "set_score_variant")
 
     def estimate_models(self, samples):
         """Estimator::EstimateModel over a batch of minimal samples -> (B x 9 models, n_models)."""

@@ -129,6 +129,109 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_h(const float4 *__restric
     }
 }
 
+// ------------------------------------------------------------------------ score (H), fast path
+// Point records for the fast kernel: 32 B per point, rec[2i] = {x1, x2, y1, y2} (pairs
+// the two directions' coordinates for packed fp32 math), rec[2i+1].x = guard band for the
+// current threshold.  Built once per context (+ once per new threshold).
+__global__ __launch_bounds__(256) void k_prepare_rec(const float4 *__restrict__ pts, uint32_t n, float T,
+                                                     float4 *__restrict__ rec) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float4 p = pts[i];
+    const float mp = fabsf(p.x) + fabsf(p.y) + fabsf(p.z) + fabsf(p.w);
+    rec[2 * i] = make_float4(p.x, p.z, p.y, p.w);
+    rec[2 * i + 1] = make_float4(kBandMp * mp + kBandT * T, 0.f, 0.f, 0.f);
+}
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+// Lanes = hypotheses, points wave-uniform (scalar loads).  Per point and wave: the six
+// projections as three packed fp32 pairs (forward, backward), two v_rcp, two packed
+// quotient products, packed differences, two v_sqrt -- ~30 VALU issue slots for 64
+// (hypothesis, point) pairs -- then the guard-band test; lanes inside the band (or with
+// a non-finite fast value) re-evaluate the exact reference expression.  EXACT_SUM also
+// routes every inlier through the exact expression so Σerr is the reference's
+// sequential fp32 sum (parity mode); otherwise Σerr accumulates the fast values
+// (throughput mode; counts are exact either way).
+template <int CHUNKS, bool EXACT_SUM>
+__global__ __launch_bounds__(64 * CHUNKS) void k_score_hf(const float4 *__restrict__ rec, uint32_t n,
+                                                          const float *__restrict__ models, uint32_t B, float thr,
+                                                          int32_t *__restrict__ counts, float *__restrict__ sums) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t h = blockIdx.x * 64 + lane;
+    const uint32_t hc = h < B ? h : B - 1;
+    f2 P[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) P[k] = f2{models[(size_t)k * B + hc], models[(size_t)(9 + k) * B + hc]};
+    const float T = 2.0f * thr;
+    const uint32_t per = (n + CHUNKS - 1) / CHUNKS;
+    const uint32_t begin = wave * per;
+    const uint32_t end = begin + per < n ? begin + per : n;
+    int cnt = 0;
+    float sum = 0.f;
+#pragma unroll 2
+    for (uint32_t i = begin; i < end; ++i) {
+        const float4 a = rec[2 * i];
+        const float band = rec[2 * i + 1].x;
+        const f2 X = f2{a.x, a.y};   // (x1, x2)
+        const f2 Y = f2{a.z, a.w};   // (y1, y2)
+        // (forward, backward) projections, reference operation order, no contraction
+        const f2 NX = (P[0] * X + P[1] * Y) + P[2];
+        const f2 NY = (P[3] * X + P[4] * Y) + P[5];
+        const f2 NZ = (P[6] * X + P[7] * Y) + P[8];
+        const f2 R = f2{__builtin_amdgcn_rcpf(NZ.x), __builtin_amdgcn_rcpf(NZ.y)};
+        const f2 DX = X.yx - NX * R;  // (x2 - q2x, x1 - q1x)
+        const f2 DY = Y.yx - NY * R;
+        const f2 D = DX * DX + DY * DY;
+        const float S = __builtin_amdgcn_sqrtf(D.x) + __builtin_amdgcn_sqrtf(D.y);
+        const float diff = S - T;
+        const bool sure = (fabsf(diff) > band) & (S < INFINITY);
+        bool inl = sure & (diff < 0.f);
+        float add = S;
+        const bool need = EXACT_SUM ? (!sure || inl) : !sure;
+        if (need) {
+            float Hh[9], Hi[9];
+#pragma unroll
+            for (int k = 0; k < 9; k++) {
+                Hh[k] = P[k].x;
+                Hi[k] = P[k].y;
+            }
+            const float e = homography_error(Hh, Hi, a.x, a.z, a.y, a.w);
+            inl = e < thr;
+            add = EXACT_SUM ? e : e + e;
+        }
+        if (inl) {
+            cnt++;
+            sum += add;
+        }
+    }
+    if (!EXACT_SUM) sum *= 0.5f;
+    if constexpr (CHUNKS == 1) {
+        if (h < B) {
+            counts[h] = cnt;
+            sums[h] = sum;
+        }
+    } else {
+        __shared__ int s_cnt[CHUNKS][64];
+        __shared__ float s_sum[CHUNKS][64];
+        s_cnt[wave][lane] = cnt;
+        s_sum[wave][lane] = sum;
+        __syncthreads();
+        if (wave == 0 && h < B) {
+            int c = s_cnt[0][lane];
+            float s = s_sum[0][lane];
+#pragma unroll
+            for (int w = 1; w < CHUNKS; w++) {
+                c += s_cnt[w][lane];
+                s += s_sum[w][lane];
+            }
+            counts[h] = c;
+            sums[h] = s;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------ line2d
 __global__ __launch_bounds__(256) void k_solve_line(const float2 *__restrict__ pts, uint32_t n,
                                                     const int32_t *__restrict__ samples_in, int32_t *samples_out,
@@ -364,6 +467,36 @@ hipError_t launch_score_h(hipStream_t st, int chunks, const float4 *pts, uint32_
         case 8: hipLaunchKernelGGL(k_score_h<8>, grid, dim3(512), 0, st, pts, n, models, B, thr, counts, sums); break;
         default: return hipErrorInvalidValue;
     }
+    return LAUNCH_CHECK();
+}
+
+hipError_t launch_prepare_rec(hipStream_t st, const float4 *pts, uint32_t n, float thr, float4 *rec) {
+    hipLaunchKernelGGL(k_prepare_rec, dim3((n + 255) / 256), dim3(256), 0, st, pts, n, 2.0f * thr, rec);
+    return LAUNCH_CHECK();
+}
+
+hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const float4 *rec, uint32_t n,
+                           const float *models, uint32_t B, float thr, int32_t *counts, float *sums) {
+    dim3 grid((B + 63) / 64);
+#define SHF(C, E) hipLaunchKernelGGL((k_score_hf<C, E>), grid, dim3(64 * C), 0, st, rec, n, models, B, thr, counts, sums)
+    if (exact_sum) {
+        switch (chunks) {
+            case 1: SHF(1, true); break;
+            case 2: SHF(2, true); break;
+            case 4: SHF(4, true); break;
+            case 8: SHF(8, true); break;
+            default: return hipErrorInvalidValue;
+        }
+    } else {
+        switch (chunks) {
+            case 1: SHF(1, false); break;
+            case 2: SHF(2, false); break;
+            case 4: SHF(4, false); break;
+            case 8: SHF(8, false); break;
+            default: return hipErrorInvalidValue;
+        }
+    }
+#undef SHF
     return LAUNCH_CHECK();
 }
 

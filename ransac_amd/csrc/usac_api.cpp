@@ -51,8 +51,11 @@ struct usac_ctx {
     uint32_t n = 0, cols = 0, m = 0;
     int dlt_mode = USAC_DLT_THIN;
     int chunks = 4;
+    int score_variant = 0;  // 0 = guard-band fast path, 1 = exact reference expression only
     hipStream_t stream = nullptr;
     DevBuf pts;
+    DevBuf rec;             // fast-kernel point records (32 B / point)
+    float rec_thr = -1.f;   // threshold the record bands were built for
     // batch buffers
     DevBuf samples, models, counts, sums, best, hostmodels;
     // single-model / polish buffers
@@ -126,10 +129,23 @@ hipError_t enqueue_solve(usac_ctx *c, const int32_t *samples_dev, uint32_t B, ui
                                    c->models.as<float>());
 }
 
+// chunks == 1 is the parity configuration: per-hypothesis sums are the exact sequential
+// fp32 sums of the reference.  chunks > 1 re-associates Σerr across chunks (counts exact).
 hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
-    if (two_view(c))
-        return usac::launch_score_h(c->stream, chunks, c->pts.as<float4>(), c->n, c->models.as<float>(), B, thr,
-                                    c->counts.as<int32_t>(), c->sums.as<float>());
+    if (two_view(c)) {
+        if (c->score_variant == 1)
+            return usac::launch_score_h(c->stream, chunks, c->pts.as<float4>(), c->n, c->models.as<float>(), B, thr,
+                                        c->counts.as<int32_t>(), c->sums.as<float>());
+        if (c->rec_thr != thr) {
+            hipError_t e = c->rec.reserve(sizeof(float) * 8 * (size_t)c->n);
+            if (e != hipSuccess) return e;
+            e = usac::launch_prepare_rec(c->stream, c->pts.as<float4>(), c->n, thr, c->rec.as<float4>());
+            if (e != hipSuccess) return e;
+            c->rec_thr = thr;
+        }
+        return usac::launch_score_hf(c->stream, chunks, chunks == 1, c->rec.as<float4>(), c->n,
+                                     c->models.as<float>(), B, thr, c->counts.as<int32_t>(), c->sums.as<float>());
+    }
     return usac::launch_score_line(c->stream, chunks, c->pts.as<float2>(), c->n, c->models.as<float>(), B, thr,
                                    c->counts.as<int32_t>(), c->sums.as<float>());
 }
@@ -210,7 +226,7 @@ void usac_destroy(usac_ctx *c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
-    for (DevBuf *b : {&c->pts, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels, &c->one_model,
+    for (DevBuf *b : {&c->pts, &c->rec, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels, &c->one_model,
                       &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok,
                       &c->rec_send, &c->rec_all})
         b->release();
@@ -231,6 +247,12 @@ int usac_set_dlt_mode(usac_ctx *c, int mode) {
 int usac_set_score_chunks(usac_ctx *c, int chunks) {
     if (!c || (chunks != 1 && chunks != 2 && chunks != 4 && chunks != 8)) return USAC_ERR_ARG;
     c->chunks = chunks;
+    return USAC_OK;
+}
+
+int usac_set_score_variant(usac_ctx *c, int variant) {
+    if (!c || (variant != 0 && variant != 1)) return USAC_ERR_ARG;
+    c->score_variant = variant;
     return USAC_OK;
 }
 

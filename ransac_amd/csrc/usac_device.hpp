@@ -205,6 +205,18 @@ __device__ __forceinline__ float homography_error(const float *h, const float *h
     return error / 2;
 }
 
+// ---------------------------------------------------------------- fast decision path
+// The score kernel decides `err < thr` with approximate fp32 reciprocal / square root and
+// falls back to homography_error() (the exact reference expression) whenever the fast
+// value is within a guard band of the threshold or not finite.  Error analysis
+// (DESIGN.md "Guard band"): the projections X, Y, Z are computed with the exact
+// reference operation sequence; q0 = X*rcp(Z) is within 2^-21|q0| of fl(X/Z)
+// (v_rcp_f32 1 ulp); the fast sum S = sqrt~(dx2^2+dy2^2) + sqrt~(dx1^2+dy1^2) then
+// differs from the reference's fp32 `error` by at most 2^-21*Mp + 2^-18*S near S = 2 thr,
+// Mp = |x1|+|y1|+|x2|+|y2|.  The band uses 8x that: 2^-18*Mp + 2^-15*(2 thr).
+constexpr float kBandMp = 3.814697265625e-06f;  // 2^-18
+constexpr float kBandT = 3.0517578125e-05f;     // 2^-15
+
 // Line2DEstimator::GetError (line2d_estimator.hpp:154-156)
 __device__ __forceinline__ float line2d_error(float a, float b, float c, float x, float y) {
     return fabsf(a * x + b * y + c);

@@ -16,6 +16,10 @@ hipError_t launch_prepare_h(hipStream_t st, const float *in, uint32_t B, float *
 hipError_t launch_score_h(hipStream_t st, int chunks, const float4 *pts, uint32_t n, const float *models, uint32_t B,
                           float thr, int32_t *counts, float *sums);
 
+hipError_t launch_prepare_rec(hipStream_t st, const float4 *pts, uint32_t n, float thr, float4 *rec);
+hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const float4 *rec, uint32_t n,
+                           const float *models, uint32_t B, float thr, int32_t *counts, float *sums);
+
 hipError_t launch_solve_line(hipStream_t st, const float2 *pts, uint32_t n, const int32_t *samples_in,
                              int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, float *models);
 hipError_t launch_prepare_line(hipStream_t st, const float *in, uint32_t B, float *models);

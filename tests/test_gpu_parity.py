@@ -99,19 +99,28 @@ def test_fused_batch_matches_oracle(usac, oracle):
 
 # ----------------------------------------------------------------------------- inliers / LSQ
 def test_get_inliers_exact(usac, oracle, homography_scenes):
-    pts, model, gt = homography_scenes["Boston"]
-    est = oracle.Estimator(oracle.HOMOGRAPHY, pts)
-    oc, os_, oidx = est.quality(model, 2.0, with_inliers=True)
-    with usac.Context(usac.ESTIMATOR.Homography, pts) as ctx:
-        c, s, idx = ctx.get_inliers(model, 2.0)
-    assert c == oc and np.float32(s) == np.float32(os_)
-    np.testing.assert_array_equal(idx, oidx)
+    est = oracle.Estimator(oracle.HOMOGRAPHY, homography_scenes["Boston"][0])
+    with usac.Context(usac.ESTIMATOR.Homography, homography_scenes["Boston"][0]) as ctx:
+        for scene in ("Boston", "Boston", "graf", "city"):
+            pts, model, gt = homography_scenes[scene]
+            if scene != "Boston":
+                ctx.close()
+                ctx = usac.Context(usac.ESTIMATOR.Homography, pts)
+                est = oracle.Estimator(oracle.HOMOGRAPHY, pts)
+            for m in (model, oracle.inv3x3(model)[0]):
+                oc, os_, oidx = est.quality(m, 2.0, with_inliers=True)
+                c, s, idx = ctx.get_inliers(m, 2.0)
+                assert c == oc and np.float32(s) == np.float32(os_)
+                np.testing.assert_array_equal(idx, oidx)
 
 
 def test_nonminimal_matches_oracle(usac, oracle, homography_scenes):
     pts, model, gt = homography_scenes["Boston"]
     est = oracle.Estimator(oracle.HOMOGRAPHY, pts)
-    _, _, idx = est.quality(model, 2.0, with_inliers=True)
+    inv, _ = oracle.inv3x3(model)
+    cands = [est.quality(m, 2.0, with_inliers=True) for m in (model, inv)]
+    idx = max(cands, key=lambda r: r[0])[2]
+    assert len(idx) == gt
     with usac.Context(usac.ESTIMATOR.Homography, pts) as ctx:
         for sub in (idx, idx[:4], idx[:3], idx[:57], idx[:200]):
             g = ctx.nonminimal(sub)
@@ -166,6 +175,59 @@ def test_ransac_run_line2d_identical(usac, oracle, line2d_scenes, seed):
     np.testing.assert_array_equal(out.getInliers(), o["inlier_idx"])
 
 
+# ----------------------------------------------------------------------------- guard band
+def test_fast_kernel_equals_exact_kernel_full_size(usac):
+    """Guard-band fast path vs the exact-expression kernel on every (hypothesis, point)
+    pair of a BASELINE-size batch (N = 10k, B = 65536): identical counts (chunked and
+    sequential), identical sequential sums."""
+    pts, _ = _cfg2(10000, seed=2)
+    with usac.Context(usac.ESTIMATOR.Homography, pts) as ctx:
+        for mode in (0, 1):
+            ctx.set_dlt_mode(mode)
+            ctx.set_score_variant(1)
+            ce, se, be = ctx.hypothesize_score(B=65536, seed=99, first_hyp=0, thr=2.0)
+            ctx.set_score_variant(0)
+            cf, sf, bf = ctx.hypothesize_score(B=65536, seed=99, first_hyp=0, thr=2.0)
+            np.testing.assert_array_equal(cf, ce)
+            np.testing.assert_array_equal(sf.view(np.int32), se.view(np.int32))
+            assert bf["hyp_index"] == be["hyp_index"]
+            for chunks in (2, 4, 8):
+                ctx.set_score_chunks(chunks)
+                ctx.hypothesize_async(65536, 99, 0, 2.0)
+                rec = ctx.fetch_best()
+                assert rec.inliers == be["inliers"]
+
+
+def test_fast_kernel_adversarial_models(usac, oracle):
+    """Models built to put pairs on the threshold, near-zero denominators, huge entries."""
+    rng = np.random.default_rng(0)
+    pts, Hgt = _cfg2(2000, seed=4)
+    est = oracle.Estimator(oracle.HOMOGRAPHY, pts)
+    base = (Hgt / Hgt[2, 2]).reshape(9).astype(np.float32)
+    models = [base]
+    for scale in (1e-6, 1e-4, 1e-2, 1.0):
+        models += [base * (1 + scale * rng.standard_normal(9).astype(np.float32)) for _ in range(40)]
+    models += [rng.standard_normal(9).astype(np.float32) * 10 ** rng.uniform(-20, 20) for _ in range(100)]
+    tiny = base.copy(); tiny[6:] = [1e-30, -1e-30, 1e-38]
+    models += [tiny, base * np.float32(1e30), base * np.float32(1e-30), np.full(9, np.nan, np.float32)]
+    models = np.stack(models).astype(np.float32)
+    thresholds = [2.0, 0.5, 7.3]
+    with usac.Context(usac.ESTIMATOR.Homography, pts) as ctx:
+        for thr in thresholds:
+            gc, gs = ctx.score_models(models, thr)
+            oc, os_ = est.score_models(models, thr)
+            np.testing.assert_array_equal(gc, oc)
+            np.testing.assert_array_equal(gs.view(np.int32), os_.view(np.int32))
+            # put points exactly on the threshold: thr := the exact error of some pairs
+            errs = est.errors(base)
+            for e in np.sort(errs[np.isfinite(errs)])[::97][:8]:
+                t = float(e)
+                for tt in (t, float(np.nextafter(np.float32(t), np.float32(np.inf)))):
+                    gc, _ = ctx.score_models(base[None], tt)
+                    oc, _ = est.score_models(base[None], tt)
+                    assert gc[0] == oc[0], tt
+
+
 # ----------------------------------------------------------------------------- full size
 def test_full_size_device_sampler_properties(usac, oracle):
     """BASELINE cfg2 size (N = 10k, B = 65536), device sampler: size-independent checks."""
@@ -178,7 +240,7 @@ def test_full_size_device_sampler_properties(usac, oracle):
         ab = ctx.fetch_best()
         n, ssum, idx = ctx.get_inliers(best["model"], 2.0)
     np.testing.assert_array_equal(c, c2)                         # deterministic sampler
-    assert best == best2 or best["hyp_index"] == best2["hyp_index"]
+    assert best["hyp_index"] == best2["hyp_index"] and best["inliers"] == best2["inliers"]
     assert (c >= 0).all() and (c <= len(pts)).all()
     assert best["inliers"] == c.max() == n                       # argmax + exact recount
     assert ab.inliers == best["inliers"]                         # chunked kernel: same counts
