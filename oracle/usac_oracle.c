@@ -105,36 +105,68 @@ int orc_inv3x3(const float *m, float *dst) {
  * dlt.cpp:43 / dlt.cpp:92: after convergence the rows are mutually orthogonal,
  * row_i = sigma_i * v_i^T, so the thin vt's last row (smallest sigma) is the row of
  * smallest norm.  Fixed algorithm (shared by the GPU kernel's spec):
- *   sweeps s < 30; pairs p < q in row-major order; alpha, beta, gamma accumulated over
- *   k = 0..8 in order; skip when |gamma| <= 1e-14 * sqrt(alpha*beta);
- *   zeta = (beta-alpha)/(2 gamma); t = sign(zeta)/(|zeta| + sqrt(1+zeta^2));
- *   c = 1/sqrt(1+t^2); s = c*t; row_p <- c*row_p - s*row_q; row_q <- s*row_p + c*row_q;
- *   stop after a sweep with no rotation. */
+ *   sweeps s < 30; pairs in round-robin (tournament) order -- circle method over rows
+ *   0..r-1 (odd r gets a bye slot), R-1 rounds of disjoint pairs, each pair as (min, max);
+ *   row norms n_i = sum_k W[i][k]^2 (k = 0..8 in order) recomputed at each sweep start;
+ *   per pair: a = n_p, b = n_q, g = sum_k W[p][k] W[q][k]; skip when g*g <= 1e-28*(a*b);
+ *   d = b - a, t = 2g / (|d| + sqrt(d*d + (2g)^2)), negated when d < 0;
+ *   c = 1/sqrt(1+t*t); s = c*t; row_p <- c*row_p - s*row_q; row_q <- s*row_p + c*row_q;
+ *   n_p <- a - t*g, n_q <- b + t*g;  stop after a sweep with no rotation. */
 #define ORC_JAC_SWEEPS 30
-#define ORC_JAC_EPS 1e-14
+#define ORC_JAC_EPS2 1e-28 /* skip when g^2 <= 1e-28 a b  (|g| <= 1e-14 sqrt(a b)) */
+static int tournament_pairs(int r, int pairs[][2]) {
+    int m = (r % 2) ? r + 1 : r; /* bye slot for odd r */
+    int arr[10], np = 0;
+    for (int i = 0; i < m; i++) arr[i] = i;
+    for (int round = 0; round < m - 1; round++) {
+        for (int i = 0; i < m / 2; i++) {
+            int p = arr[i], q = arr[m - 1 - i];
+            if (p >= r || q >= r) continue;
+            pairs[np][0] = p < q ? p : q;
+            pairs[np][1] = p < q ? q : p;
+            np++;
+        }
+        int last = arr[m - 1];
+        for (int i = m - 1; i > 1; i--) arr[i] = arr[i - 1];
+        arr[1] = last;
+    }
+    return np;
+}
+
 static void row_jacobi(double W[][9], int r) {
+    int pairs[45][2];
+    int np = tournament_pairs(r, pairs);
     for (int sweep = 0; sweep < ORC_JAC_SWEEPS; sweep++) {
         int rotated = 0;
-        for (int p = 0; p < r - 1; p++) {
-            for (int q = p + 1; q < r; q++) {
-                double a = 0.0, b = 0.0, g = 0.0;
-                for (int k = 0; k < 9; k++) {
-                    a += W[p][k] * W[p][k];
-                    b += W[q][k] * W[q][k];
-                    g += W[p][k] * W[q][k];
-                }
-                if (fabs(g) <= ORC_JAC_EPS * sqrt(a * b)) continue;
-                rotated = 1;
-                double zeta = (b - a) / (2.0 * g);
-                double t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-                double c = 1.0 / sqrt(1.0 + t * t);
-                double s = c * t;
-                for (int k = 0; k < 9; k++) {
-                    double wp = W[p][k], wq = W[q][k];
-                    W[p][k] = c * wp - s * wq;
-                    W[q][k] = s * wp + c * wq;
-                }
+        /* row norms recomputed once per sweep, updated exactly-in-theory within it:
+         * a' = a - t g, b' = b + t g */
+        double nrm[9];
+        for (int i = 0; i < r; i++) {
+            double a = 0.0;
+            for (int k = 0; k < 9; k++) a += W[i][k] * W[i][k];
+            nrm[i] = a;
+        }
+        for (int pi = 0; pi < np; pi++) {
+            const int p = pairs[pi][0], q = pairs[pi][1];
+            const double a = nrm[p], b = nrm[q];
+            double g = 0.0;
+            for (int k = 0; k < 9; k++) g += W[p][k] * W[q][k];
+            if (g * g <= ORC_JAC_EPS2 * (a * b)) continue;
+            rotated = 1;
+            /* t = sign(zeta)/(|zeta| + sqrt(1+zeta^2)), zeta = (b-a)/(2g), written as
+             * t = sign(d) 2g / (|d| + sqrt(d^2 + 4g^2)), d = b - a */
+            const double d = b - a, g2 = 2.0 * g;
+            double t = g2 / (fabs(d) + sqrt(d * d + g2 * g2));
+            if (d < 0.0) t = -t;
+            const double c = 1.0 / sqrt(1.0 + t * t);
+            const double s = c * t;
+            for (int k = 0; k < 9; k++) {
+                double wp = W[p][k], wq = W[q][k];
+                W[p][k] = c * wp - s * wq;
+                W[q][k] = s * wp + c * wq;
             }
+            nrm[p] = a - t * g;
+            nrm[q] = b + t * g;
         }
         if (!rotated) break;
     }

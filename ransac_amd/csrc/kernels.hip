@@ -130,80 +130,171 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_h(const float4 *__restric
 }
 
 // ------------------------------------------------------------------------ score (H), fast path
-// Point records for the fast kernel: 32 B per point, rec[2i] = {x1, x2, y1, y2} (pairs
-// the two directions' coordinates for packed fp32 math), rec[2i+1].x = guard band for the
-// current threshold.  Built once per context (+ once per new threshold).
+// Point records for the fast kernel, in groups of 4 points (128 B per group):
+//   float4 [0..3] = {x1, x2, y1, y2} of points 4g..4g+3,
+//   float4 [4]    = guard bands for the current threshold          band_i
+//   float4 [5]    = forward-rejection radii (T + band_i)(1 + 2^-18), T = 2 thr
+//   float4 [6..7] = padding.
+// One s_load_dwordx16 + one s_load_dwordx8 bring four points into SGPRs.  The tail group
+// is padded with NaN points, which are never inliers (NaN < thr is false in every path).
+// Built once per context and threshold.
 __global__ __launch_bounds__(256) void k_prepare_rec(const float4 *__restrict__ pts, uint32_t n, float T,
                                                      float4 *__restrict__ rec) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const float4 p = pts[i];
-    const float mp = fabsf(p.x) + fabsf(p.y) + fabsf(p.z) + fabsf(p.w);
-    rec[2 * i] = make_float4(p.x, p.z, p.y, p.w);
-    rec[2 * i + 1] = make_float4(kBandMp * mp + kBandT * T, 0.f, 0.f, 0.f);
+    const uint32_t ngroups = (n + 3) / 4;
+    if (i >= 4 * ngroups) return;
+    const uint32_t g = i >> 2, j = i & 3;
+    float4 out;
+    float band, tr;
+    if (i < n) {
+        const float4 p = pts[i];
+        const float mp = fabsf(p.x) + fabsf(p.y) + fabsf(p.z) + fabsf(p.w);
+        out = make_float4(p.x, p.z, p.y, p.w);
+        band = kBandMp * mp + kBandT * T;
+        tr = (T + band) * 1.000003814697265625f;  // (1 + 2^-18)
+    } else {
+        out = make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
+        band = 0.f;
+        tr = __builtin_nanf("");
+    }
+    rec[8 * g + j] = out;
+    reinterpret_cast<float *>(rec + 8 * g + 4)[j] = band;
+    reinterpret_cast<float *>(rec + 8 * g + 5)[j] = tr;
+    if (j < 2) rec[8 * g + 6 + j] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
-typedef float f2 __attribute__((ext_vector_type(2)));
+// Model registers of a lane: h[9] = H, hi[9] = H^-1; plus the lane's stage-A error
+// bounds dZ, E (below).
+struct HModel {
+    float h[9], hi[9];
+    float dZ, E;
+};
 
-// Lanes = hypotheses, points wave-uniform (scalar loads).  Per point and wave: the six
-// projections as three packed fp32 pairs (forward, backward), two v_rcp, two packed
-// quotient products, packed differences, two v_sqrt -- ~30 VALU issue slots for 64
-// (hypothesis, point) pairs -- then the guard-band test; lanes inside the band (or with
-// a non-finite fast value) re-evaluate the exact reference expression.  EXACT_SUM also
-// routes every inlier through the exact expression so Σerr is the reference's
-// sequential fp32 sum (parity mode); otherwise Σerr accumulates the fast values
-// (throughput mode; counts are exact either way).
+// Stage-A bounds of one hypothesis over the dataset box |x1| <= c.x, |y1| <= c.y,
+// |x2| <= c.z, |y2| <= c.w:  K_X = |h0| c.x + |h1| c.y + |h2| bounds every magnitude in the
+// reference's X = (h0 x1 + h1 y1) + h2 and in the FMA chain below, so the two differ by at
+// most 2^-21 K_X; dX = 2^-20 K_X (2x slack), likewise dY, dZ;
+// E = ((c.z dZ + dX) + (c.w dZ + dY)) (1 + 2^-18).
+__device__ __forceinline__ void stage_a_bounds(HModel &M, float4 c) {
+    const float kx = fabsf(M.h[0]) * c.x + fabsf(M.h[1]) * c.y + fabsf(M.h[2]);
+    const float ky = fabsf(M.h[3]) * c.x + fabsf(M.h[4]) * c.y + fabsf(M.h[5]);
+    const float kz = fabsf(M.h[6]) * c.x + fabsf(M.h[7]) * c.y + fabsf(M.h[8]);
+    const float s = 9.5367431640625e-07f;  // 2^-20
+    const float dx = s * kx, dy = s * ky, dz = s * kz;
+    M.dZ = dz;
+    M.E = ((c.z * dz + dx) + (c.w * dz + dy)) * 1.000003814697265625f;
+}
+
+// Stage A -- forward-only rejection, 14 VALU ops, no rcp / sqrt.  X, Y, Z by FMA chains,
+// e = (x2 Z - X, y2 Z - Y); with r = tr (|Z| + dZ) + E:
+//   |e|^2 > r^2   ==>   the reference's forward distance exceeds T + band >= 2 thr,
+// so its error is not below the threshold: a sure outlier, whatever the backward term.
+// (DESIGN.md "Guard band" derives it: |Z_ref u_ref - e| <= E, |Z_ref| <= |Z| + dZ; the
+// (1 + 2^-18) factors dominate every rounding of the test itself; NaN -> not rejected.)
+__device__ __forceinline__ bool stage_a_reject(const HModel &M, float x1, float y1, float x2, float y2, float tr) {
+    const float X = __builtin_fmaf(M.h[1], y1, __builtin_fmaf(M.h[0], x1, M.h[2]));
+    const float Y = __builtin_fmaf(M.h[4], y1, __builtin_fmaf(M.h[3], x1, M.h[5]));
+    const float Z = __builtin_fmaf(M.h[7], y1, __builtin_fmaf(M.h[6], x1, M.h[8]));
+    const float ex = __builtin_fmaf(x2, Z, -X);
+    const float ey = __builtin_fmaf(y2, Z, -Y);
+    const float lhs = __builtin_fmaf(ex, ex, ey * ey);
+    const float r = __builtin_fmaf(tr, fabsf(Z) + M.dZ, M.E);
+    return lhs > r * r;
+}
+
+// Stage B -- both directions with the reference's projection order, v_rcp, v_sqrt, and the
+// guard-band test; lanes inside the band / non-finite / (EXACT_SUM) inliers re-evaluate the
+// exact reference expression.  Adds to (cnt, sum): the exact err (EXACT_SUM, so Σ is the
+// reference's sequential fp32 sum) or S ~= 2 err (throughput mode, halved at the end).
+template <bool EXACT_SUM>
+__device__ __forceinline__ void stage_b(const HModel &M, float x1, float y1, float x2, float y2, float band, float T,
+                                        float thr, int &cnt, float &sum) {
+    const float X = M.h[0] * x1 + M.h[1] * y1 + M.h[2];
+    const float Y = M.h[3] * x1 + M.h[4] * y1 + M.h[5];
+    const float Z = M.h[6] * x1 + M.h[7] * y1 + M.h[8];
+    const float r2 = __builtin_amdgcn_rcpf(Z);
+    const float dx2 = __builtin_fmaf(-X, r2, x2);
+    const float dy2 = __builtin_fmaf(-Y, r2, y2);
+    const float X1 = M.hi[0] * x2 + M.hi[1] * y2 + M.hi[2];
+    const float Y1 = M.hi[3] * x2 + M.hi[4] * y2 + M.hi[5];
+    const float Z1 = M.hi[6] * x2 + M.hi[7] * y2 + M.hi[8];
+    const float r1 = __builtin_amdgcn_rcpf(Z1);
+    const float dx1 = __builtin_fmaf(-X1, r1, x1);
+    const float dy1 = __builtin_fmaf(-Y1, r1, y1);
+    const float d2 = __builtin_fmaf(dx2, dx2, dy2 * dy2);
+    const float d1 = __builtin_fmaf(dx1, dx1, dy1 * dy1);
+    const float S = __builtin_amdgcn_sqrtf(d2) + __builtin_amdgcn_sqrtf(d1);
+    const float diff = S - T;
+    const bool sure = (fabsf(diff) > band) & (S < INFINITY);
+    bool inl = sure & (diff < 0.f);
+    float add = S;
+    if (EXACT_SUM ? (!sure || inl) : !sure) {
+        const float e = homography_error(M.h, M.hi, x1, y1, x2, y2);
+        inl = e < thr;
+        add = EXACT_SUM ? e : e + e;
+    }
+    if (inl) {
+        cnt++;
+        sum += add;
+    }
+}
+
+// Four points of a group: stage A for all four first (independent chains), then stage B
+// per point behind a branch that the wave skips unless one of its 64 hypotheses survived.
+template <bool EXACT_SUM>
+__device__ __forceinline__ void score_group(const HModel &M, float4 a0, float4 a1, float4 a2, float4 a3, float4 bd,
+                                            float4 tr, float T, float thr, int &cnt, float &sum) {
+    const bool k0 = stage_a_reject(M, a0.x, a0.z, a0.y, a0.w, tr.x);
+    const bool k1 = stage_a_reject(M, a1.x, a1.z, a1.y, a1.w, tr.y);
+    const bool k2 = stage_a_reject(M, a2.x, a2.z, a2.y, a2.w, tr.z);
+    const bool k3 = stage_a_reject(M, a3.x, a3.z, a3.y, a3.w, tr.w);
+    if (!k0) stage_b<EXACT_SUM>(M, a0.x, a0.z, a0.y, a0.w, bd.x, T, thr, cnt, sum);
+    if (!k1) stage_b<EXACT_SUM>(M, a1.x, a1.z, a1.y, a1.w, bd.y, T, thr, cnt, sum);
+    if (!k2) stage_b<EXACT_SUM>(M, a2.x, a2.z, a2.y, a2.w, bd.z, T, thr, cnt, sum);
+    if (!k3) stage_b<EXACT_SUM>(M, a3.x, a3.z, a3.y, a3.w, bd.w, T, thr, cnt, sum);
+}
+
+// Lanes = hypotheses (64 per wave), point groups wave-uniform (scalar loads, double-
+// buffered one group ahead).  CHUNKS waves of a workgroup split the groups of the same 64
+// hypotheses and combine (count, Σ) in chunk order.  ext = dataset box (see above).
 template <int CHUNKS, bool EXACT_SUM>
-__global__ __launch_bounds__(64 * CHUNKS) void k_score_hf(const float4 *__restrict__ rec, uint32_t n,
+__global__ __launch_bounds__(64 * CHUNKS) void k_score_hf(const float4 *__restrict__ rec, uint32_t n, float4 ext,
                                                           const float *__restrict__ models, uint32_t B, float thr,
                                                           int32_t *__restrict__ counts, float *__restrict__ sums) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t h = blockIdx.x * 64 + lane;
     const uint32_t hc = h < B ? h : B - 1;
-    f2 P[9];
+    HModel M;
 #pragma unroll
-    for (int k = 0; k < 9; k++) P[k] = f2{models[(size_t)k * B + hc], models[(size_t)(9 + k) * B + hc]};
+    for (int k = 0; k < 9; k++) {
+        M.h[k] = models[(size_t)k * B + hc];
+        M.hi[k] = models[(size_t)(9 + k) * B + hc];
+    }
+    stage_a_bounds(M, ext);
     const float T = 2.0f * thr;
-    const uint32_t per = (n + CHUNKS - 1) / CHUNKS;
-    const uint32_t begin = wave * per;
-    const uint32_t end = begin + per < n ? begin + per : n;
+    const uint32_t ngroups = (n + 3) / 4;
+    const uint32_t per = (ngroups + CHUNKS - 1) / CHUNKS;
+    const uint32_t gbeg = wave * per < ngroups ? wave * per : ngroups;
+    const uint32_t gend = gbeg + per < ngroups ? gbeg + per : ngroups;
     int cnt = 0;
     float sum = 0.f;
-#pragma unroll 2
-    for (uint32_t i = begin; i < end; ++i) {
-        const float4 a = rec[2 * i];
-        const float band = rec[2 * i + 1].x;
-        const f2 X = f2{a.x, a.y};   // (x1, x2)
-        const f2 Y = f2{a.z, a.w};   // (y1, y2)
-        // (forward, backward) projections, reference operation order, no contraction
-        const f2 NX = (P[0] * X + P[1] * Y) + P[2];
-        const f2 NY = (P[3] * X + P[4] * Y) + P[5];
-        const f2 NZ = (P[6] * X + P[7] * Y) + P[8];
-        const f2 R = f2{__builtin_amdgcn_rcpf(NZ.x), __builtin_amdgcn_rcpf(NZ.y)};
-        const f2 DX = X.yx - NX * R;  // (x2 - q2x, x1 - q1x)
-        const f2 DY = Y.yx - NY * R;
-        const f2 D = DX * DX + DY * DY;
-        const float S = __builtin_amdgcn_sqrtf(D.x) + __builtin_amdgcn_sqrtf(D.y);
-        const float diff = S - T;
-        const bool sure = (fabsf(diff) > band) & (S < INFINITY);
-        bool inl = sure & (diff < 0.f);
-        float add = S;
-        const bool need = EXACT_SUM ? (!sure || inl) : !sure;
-        if (need) {
-            float Hh[9], Hi[9];
-#pragma unroll
-            for (int k = 0; k < 9; k++) {
-                Hh[k] = P[k].x;
-                Hi[k] = P[k].y;
-            }
-            const float e = homography_error(Hh, Hi, a.x, a.z, a.y, a.w);
-            inl = e < thr;
-            add = EXACT_SUM ? e : e + e;
-        }
-        if (inl) {
-            cnt++;
-            sum += add;
+    if (gbeg < gend) {
+        const float4 *p = rec + 8 * (size_t)gbeg;
+        float4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], ab = p[4], at = p[5];
+        float4 b0, b1, b2, b3, bb, bt;
+        uint32_t g = gbeg;
+        for (;;) {
+            // buffer B <- group g+1 (clamped), evaluate buffer A = group g
+            p = rec + 8 * (size_t)(g + 1 < gend ? g + 1 : g);
+            b0 = p[0]; b1 = p[1]; b2 = p[2]; b3 = p[3]; bb = p[4]; bt = p[5];
+            score_group<EXACT_SUM>(M, a0, a1, a2, a3, ab, at, T, thr, cnt, sum);
+            if (++g >= gend) break;
+            // buffer A <- group g+1 (clamped), evaluate buffer B = group g
+            p = rec + 8 * (size_t)(g + 1 < gend ? g + 1 : g);
+            a0 = p[0]; a1 = p[1]; a2 = p[2]; a3 = p[3]; ab = p[4]; at = p[5];
+            score_group<EXACT_SUM>(M, b0, b1, b2, b3, bb, bt, T, thr, cnt, sum);
+            if (++g >= gend) break;
         }
     }
     if (!EXACT_SUM) sum *= 0.5f;
@@ -313,48 +404,74 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_line(const float2 *__rest
 }
 
 // ------------------------------------------------------------------------ batch argmax
-// One workgroup: strided scan + LDS tree under record_better (a strict total order, so
-// the reduction order does not change the result).
-__global__ __launch_bounds__(1024) void k_argmax(const int32_t *__restrict__ counts, const float *__restrict__ sums,
-                                                 uint32_t B, const float *__restrict__ models, int ncomp,
-                                                 uint64_t first_hyp, usac_record *out) {
-    __shared__ int s_c[1024];
-    __shared__ float s_s[1024];
-    __shared__ uint32_t s_i[1024];
-    const uint32_t t = threadIdx.x;
-    int bc = -1;
-    float bs = 0.f;
-    uint32_t bi = 0xFFFFFFFFu;
-    for (uint32_t i = t; i < B; i += 1024) {
-        int c = counts[i];
-        float s = sums[i];
-        if (bc < 0 || record_better(c, s, i, bc, bs, bi)) {
-            bc = c;
-            bs = s;
-            bi = i;
-        }
-    }
-    s_c[t] = bc;
-    s_s[t] = bs;
-    s_i[t] = bi;
-    __syncthreads();
-    for (uint32_t w = 512; w > 0; w >>= 1) {
+// Two launches: k_argmax_part reduces 2048 hypotheses per workgroup (8 independent loads
+// per lane in flight, LDS tree), k_argmax_final reduces the partials and gathers the
+// model.  record_better is a strict total order, so the tree shape does not change the
+// result (= the sequential first-best under Score::bigger).
+struct BestEntry {
+    int c;
+    float s;
+    uint32_t i;
+};
+
+__device__ __forceinline__ void tree_best(BestEntry *sh, uint32_t t, uint32_t width) {
+    for (uint32_t w = width / 2; w > 0; w >>= 1) {
         if (t < w) {
-            int c2 = s_c[t + w];
-            if (c2 >= 0 && (s_c[t] < 0 || record_better(c2, s_s[t + w], s_i[t + w], s_c[t], s_s[t], s_i[t]))) {
-                s_c[t] = c2;
-                s_s[t] = s_s[t + w];
-                s_i[t] = s_i[t + w];
-            }
+            const BestEntry o = sh[t + w];
+            if (o.c >= 0 && (sh[t].c < 0 || record_better(o.c, o.s, o.i, sh[t].c, sh[t].s, sh[t].i))) sh[t] = o;
         }
         __syncthreads();
     }
+}
+
+__global__ __launch_bounds__(256) void k_argmax_part(const int32_t *__restrict__ counts,
+                                                     const float *__restrict__ sums, uint32_t B,
+                                                     BestEntry *__restrict__ part) {
+    __shared__ BestEntry sh[256];
+    const uint32_t t = threadIdx.x;
+    const uint32_t base = blockIdx.x * 2048 + t;
+    int c[8];
+    float s[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const uint32_t i = base + 256 * j;
+        c[j] = i < B ? counts[i] : -1;
+        s[j] = i < B ? sums[i] : 0.f;
+    }
+    BestEntry b{-1, 0.f, 0xFFFFFFFFu};
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const uint32_t i = base + 256 * j;
+        if (c[j] >= 0 && (b.c < 0 || record_better(c[j], s[j], i, b.c, b.s, b.i))) b = BestEntry{c[j], s[j], i};
+    }
+    sh[t] = b;
+    __syncthreads();
+    tree_best(sh, t, 256);
+    if (t == 0) part[blockIdx.x] = sh[0];
+}
+
+__global__ __launch_bounds__(256) void k_argmax_final(const BestEntry *__restrict__ part, uint32_t nparts, uint32_t B,
+                                                      const float *__restrict__ models, int ncomp, uint64_t first_hyp,
+                                                      usac_record *out) {
+    __shared__ BestEntry sh[256];
+    const uint32_t t = threadIdx.x;
+    BestEntry b{-1, 0.f, 0xFFFFFFFFu};
+    for (uint32_t k = t; k < nparts; k += 256) {
+        const BestEntry o = part[k];
+        if (o.c >= 0 && (b.c < 0 || record_better(o.c, o.s, o.i, b.c, b.s, b.i))) b = o;
+    }
+    sh[t] = b;
+    __syncthreads();
+    tree_best(sh, t, 256);
     if (t == 0) {
         usac_record r;
-        const uint32_t i = s_i[0];
-        r.valid = s_c[0] >= 0 ? 1 : 0;
-        r.inliers = s_c[0] < 0 ? 0 : s_c[0];
-        r.score = s_s[0];
+        const BestEntry best = sh[0];
+        const int sc0 = best.c;
+        const float ss0 = best.s;
+        const uint32_t i = best.i;
+        r.valid = sc0 >= 0 ? 1 : 0;
+        r.inliers = sc0 < 0 ? 0 : sc0;
+        r.score = ss0;
         r.hyp_index = first_hyp + (i == 0xFFFFFFFFu ? 0 : i);
         for (int k = 0; k < 9; k++) r.model[k] = (k < ncomp && r.valid) ? models[(size_t)k * B + i] : 0.f;
         *out = r;
@@ -471,14 +588,16 @@ hipError_t launch_score_h(hipStream_t st, int chunks, const float4 *pts, uint32_
 }
 
 hipError_t launch_prepare_rec(hipStream_t st, const float4 *pts, uint32_t n, float thr, float4 *rec) {
-    hipLaunchKernelGGL(k_prepare_rec, dim3((n + 255) / 256), dim3(256), 0, st, pts, n, 2.0f * thr, rec);
+    const uint32_t total = 4 * ((n + 3) / 4);
+    hipLaunchKernelGGL(k_prepare_rec, dim3((total + 255) / 256), dim3(256), 0, st, pts, n, 2.0f * thr, rec);
     return LAUNCH_CHECK();
 }
 
-hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const float4 *rec, uint32_t n,
+hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const float4 *rec, uint32_t n, float4 ext,
                            const float *models, uint32_t B, float thr, int32_t *counts, float *sums) {
     dim3 grid((B + 63) / 64);
-#define SHF(C, E) hipLaunchKernelGGL((k_score_hf<C, E>), grid, dim3(64 * C), 0, st, rec, n, models, B, thr, counts, sums)
+#define SHF(C, E) \
+    hipLaunchKernelGGL((k_score_hf<C, E>), grid, dim3(64 * C), 0, st, rec, n, ext, models, B, thr, counts, sums)
     if (exact_sum) {
         switch (chunks) {
             case 1: SHF(1, true); break;
@@ -526,8 +645,11 @@ hipError_t launch_score_line(hipStream_t st, int chunks, const float2 *pts, uint
 }
 
 hipError_t launch_argmax(hipStream_t st, const int32_t *counts, const float *sums, uint32_t B, const float *models,
-                         int ncomp, uint64_t first_hyp, usac_record *out) {
-    hipLaunchKernelGGL(k_argmax, dim3(1), dim3(1024), 0, st, counts, sums, B, models, ncomp, first_hyp, out);
+                         int ncomp, uint64_t first_hyp, void *scratch, usac_record *out) {
+    const uint32_t nparts = (B + 2047) / 2048;
+    BestEntry *part = static_cast<BestEntry *>(scratch);
+    hipLaunchKernelGGL(k_argmax_part, dim3(nparts), dim3(256), 0, st, counts, sums, B, part);
+    hipLaunchKernelGGL(k_argmax_final, dim3(1), dim3(256), 0, st, part, nparts, B, models, ncomp, first_hyp, out);
     return LAUNCH_CHECK();
 }
 

@@ -4,6 +4,7 @@
 // usac_create with USAC_ERR_HIP).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <math.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -56,8 +57,9 @@ struct usac_ctx {
     DevBuf pts;
     DevBuf rec;             // fast-kernel point records (32 B / point)
     float rec_thr = -1.f;   // threshold the record bands were built for
+    float4 ext = {0, 0, 0, 0};  // dataset box: max |x1|, |y1|, |x2|, |y2| (fast-kernel bounds)
     // batch buffers
-    DevBuf samples, models, counts, sums, best, hostmodels;
+    DevBuf samples, models, counts, sums, best, hostmodels, argmax_part;
     // single-model / polish buffers
     DevBuf one_model, inl_idx, inl_cnt, inl_sum, q, partial, ws, nm_model, nm_ok;
     // comm
@@ -102,6 +104,7 @@ int ensure_batch(usac_ctx *c, uint32_t B) {
     HIP_TRY(c, c->counts.reserve(sizeof(int32_t) * (size_t)B));
     HIP_TRY(c, c->sums.reserve(sizeof(float) * (size_t)B));
     HIP_TRY(c, c->best.reserve(sizeof(usac_record)));
+    HIP_TRY(c, c->argmax_part.reserve(16 * ((size_t)B / 2048 + 1)));
     HIP_TRY(c, c->hostmodels.reserve(sizeof(float) * 9 * (size_t)B));
     return USAC_OK;
 }
@@ -137,13 +140,13 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
             return usac::launch_score_h(c->stream, chunks, c->pts.as<float4>(), c->n, c->models.as<float>(), B, thr,
                                         c->counts.as<int32_t>(), c->sums.as<float>());
         if (c->rec_thr != thr) {
-            hipError_t e = c->rec.reserve(sizeof(float) * 8 * (size_t)c->n);
+            hipError_t e = c->rec.reserve(sizeof(float) * 32 * (((size_t)c->n + 3) / 4));
             if (e != hipSuccess) return e;
             e = usac::launch_prepare_rec(c->stream, c->pts.as<float4>(), c->n, thr, c->rec.as<float4>());
             if (e != hipSuccess) return e;
             c->rec_thr = thr;
         }
-        return usac::launch_score_hf(c->stream, chunks, chunks == 1, c->rec.as<float4>(), c->n,
+        return usac::launch_score_hf(c->stream, chunks, chunks == 1, c->rec.as<float4>(), c->n, c->ext,
                                      c->models.as<float>(), B, thr, c->counts.as<int32_t>(), c->sums.as<float>());
     }
     return usac::launch_score_line(c->stream, chunks, c->pts.as<float2>(), c->n, c->models.as<float>(), B, thr,
@@ -208,6 +211,15 @@ int usac_create(usac_ctx **out, int device, int estimator, const float *pts, uin
         e = c->pts.reserve(sizeof(float) * (size_t)n * cols);
         if (e != hipSuccess) { rc = fail(c, USAC_ERR_HIP, "hipMalloc points failed"); break; }
         e = hipMemcpy(c->pts.p, pts, sizeof(float) * (size_t)n * cols, hipMemcpyHostToDevice);
+        if (cols == 4) {  // dataset box for the score kernel's error bounds (NaN rows skipped)
+            float mx[4] = {0, 0, 0, 0};
+            for (uint32_t i = 0; i < n; i++)
+                for (int k = 0; k < 4; k++) {
+                    const float v = fabsf(pts[4 * (size_t)i + k]);
+                    if (v > mx[k]) mx[k] = v;
+                }
+            c->ext = make_float4(mx[0], mx[1], mx[2], mx[3]);
+        }
         if (e != hipSuccess) { rc = fail(c, USAC_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e)); break; }
     } while (0);
     if (rc != USAC_OK) {
@@ -226,7 +238,7 @@ void usac_destroy(usac_ctx *c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
-    for (DevBuf *b : {&c->pts, &c->rec, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels, &c->one_model,
+    for (DevBuf *b : {&c->pts, &c->rec, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels, &c->argmax_part, &c->one_model,
                       &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok,
                       &c->rec_send, &c->rec_all})
         b->release();
@@ -354,7 +366,7 @@ int usac_hypothesize_score(usac_ctx *c, const int32_t *samples, uint32_t B, uint
     const int chunks = (counts || sums) ? 1 : c->chunks;
     HIP_TRY(c, enqueue_score(c, B, thr, chunks));
     HIP_TRY(c, usac::launch_argmax(c->stream, c->counts.as<int32_t>(), c->sums.as<float>(), B, c->models.as<float>(),
-                                   ncomp(c), first_hyp, c->best.as<usac_record>()));
+                                   ncomp(c), first_hyp, c->argmax_part.p, c->best.as<usac_record>()));
     if (counts) HIP_TRY(c, hipMemcpyAsync(counts, c->counts.p, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
     if (sums) HIP_TRY(c, hipMemcpyAsync(sums, c->sums.p, sizeof(float) * B, hipMemcpyDeviceToHost, c->stream));
     if (best) HIP_TRY(c, hipMemcpyAsync(best, c->best.p, sizeof(usac_record), hipMemcpyDeviceToHost, c->stream));
@@ -373,7 +385,7 @@ int usac_hypothesize_async(usac_ctx *c, uint32_t B, uint64_t seed, uint64_t firs
     HIP_TRY(c, enqueue_score(c, B, thr, c->chunks));
     HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
     HIP_TRY(c, usac::launch_argmax(c->stream, c->counts.as<int32_t>(), c->sums.as<float>(), B, c->models.as<float>(),
-                                   ncomp(c), first_hyp, c->best.as<usac_record>()));
+                                   ncomp(c), first_hyp, c->argmax_part.p, c->best.as<usac_record>()));
     HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
     c->timed_pending = true;
     return USAC_OK;

@@ -78,39 +78,76 @@ __device__ __forceinline__ void dlt_rows(float x1, float y1, float x2, float y2,
     r1[6] = (double)(y2 * x1); r1[7] = (double)(y2 * y1); r1[8] = (double)y2;
 }
 
+// Round-robin (tournament) pair schedule, circle method, as (min, max) pairs; R-1 rounds
+// of R/2 disjoint pairs (odd R: bye slot).  Consecutive pairs of a round touch disjoint
+// rows, so their rotations are independent dependency chains (ILP for one lane).
+template <int R>
+struct Tournament {
+    static constexpr int M = (R % 2) ? R + 1 : R;
+    static constexpr int NP = R * (R - 1) / 2;
+    int p[NP > 0 ? NP : 1], q[NP > 0 ? NP : 1];
+    constexpr Tournament() : p(), q() {
+        int arr[M] = {};
+        for (int i = 0; i < M; i++) arr[i] = i;
+        int np = 0;
+        for (int round = 0; round < M - 1; round++) {
+            for (int i = 0; i < M / 2; i++) {
+                const int a = arr[i], b = arr[M - 1 - i];
+                if (a >= R || b >= R) continue;
+                p[np] = a < b ? a : b;
+                q[np] = a < b ? b : a;
+                np++;
+            }
+            const int last = arr[M - 1];
+            for (int i = M - 1; i > 1; i--) arr[i] = arr[i - 1];
+            arr[1] = last;
+        }
+    }
+};
+
 // One-sided (Hestenes) Jacobi on the R rows of W (fp64), the row-space part of the thin
-// cv::SVD::compute of dlt.cpp:43.  Spec (identical in the oracle): sweeps < 30, pairs
-// p < q row-major, sums over k = 0..8 in order, skip when |g| <= 1e-14*sqrt(a*b),
-// zeta = (b-a)/(2g), t = sign(zeta)/(|zeta|+sqrt(1+zeta^2)), c = 1/sqrt(1+t^2), s = c*t,
-// stop after a sweep without rotation.  Fully unrolled so W stays in VGPRs.
+// cv::SVD::compute of dlt.cpp:43.  Spec (identical in the oracle): sweeps < 30, pairs in
+// tournament order (above); row norms n_i (sum over k = 0..8 in order) recomputed at
+// each sweep start; per pair a = n_p, b = n_q, g = sum_k W[p][k] W[q][k], skip when
+// g*g <= 1e-28*(a*b); d = b - a, t = 2g/(|d| + sqrt(d*d + (2g)^2)) negated when d < 0
+// (= sign(zeta)/(|zeta|+sqrt(1+zeta^2)), zeta = d/2g), c = 1/sqrt(1+t*t), s = c*t;
+// n_p <- a - t g, n_q <- b + t g; stop after a sweep without rotation.  Fully unrolled
+// so W stays in VGPRs.
 template <int R>
 __device__ __forceinline__ void row_jacobi(double (&W)[R][9]) {
+    constexpr Tournament<R> T{};
     for (int sweep = 0; sweep < 30; sweep++) {
         bool rotated = false;
+        double nrm[R];
 #pragma unroll
-        for (int p = 0; p < R - 1; p++) {
+        for (int i = 0; i < R; i++) {
+            double a = 0.0;
 #pragma unroll
-            for (int q = p + 1; q < R; q++) {
-                double a = 0.0, b = 0.0, g = 0.0;
+            for (int k = 0; k < 9; k++) a += W[i][k] * W[i][k];
+            nrm[i] = a;
+        }
+#pragma unroll
+        for (int pi = 0; pi < Tournament<R>::NP; pi++) {
+            const int p = T.p[pi], q = T.q[pi];
+            const double a = nrm[p], b = nrm[q];
+            double g = 0.0;
+#pragma unroll
+            for (int k = 0; k < 9; k++) g += W[p][k] * W[q][k];
+            if (!(g * g <= 1e-28 * (a * b))) {
+                rotated = true;
+                const double d = b - a, g2 = 2.0 * g;
+                double t = g2 / (fabs(d) + sqrt(d * d + g2 * g2));
+                if (d < 0.0) t = -t;
+                const double c = 1.0 / sqrt(1.0 + t * t);
+                const double s = c * t;
 #pragma unroll
                 for (int k = 0; k < 9; k++) {
-                    a += W[p][k] * W[p][k];
-                    b += W[q][k] * W[q][k];
-                    g += W[p][k] * W[q][k];
+                    double wp = W[p][k], wq = W[q][k];
+                    W[p][k] = c * wp - s * wq;
+                    W[q][k] = s * wp + c * wq;
                 }
-                if (!(fabs(g) <= 1e-14 * sqrt(a * b))) {
-                    rotated = true;
-                    double zeta = (b - a) / (2.0 * g);
-                    double t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
-                    double c = 1.0 / sqrt(1.0 + t * t);
-                    double s = c * t;
-#pragma unroll
-                    for (int k = 0; k < 9; k++) {
-                        double wp = W[p][k], wq = W[q][k];
-                        W[p][k] = c * wp - s * wq;
-                        W[q][k] = s * wp + c * wq;
-                    }
-                }
+                nrm[p] = a - t * g;
+                nrm[q] = b + t * g;
             }
         }
         if (!rotated) break;

@@ -17,7 +17,8 @@ hipError_t launch_score_h(hipStream_t st, int chunks, const float4 *pts, uint32_
                           float thr, int32_t *counts, float *sums);
 
 hipError_t launch_prepare_rec(hipStream_t st, const float4 *pts, uint32_t n, float thr, float4 *rec);
-hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const float4 *rec, uint32_t n,
+// ext = dataset box {max|x1|, max|y1|, max|x2|, max|y2|} (stage-A error bounds)
+hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const float4 *rec, uint32_t n, float4 ext,
                            const float *models, uint32_t B, float thr, int32_t *counts, float *sums);
 
 hipError_t launch_solve_line(hipStream_t st, const float2 *pts, uint32_t n, const int32_t *samples_in,
@@ -27,7 +28,8 @@ hipError_t launch_score_line(hipStream_t st, int chunks, const float2 *pts, uint
                              uint32_t B, float thr, int32_t *counts, float *sums);
 
 hipError_t launch_argmax(hipStream_t st, const int32_t *counts, const float *sums, uint32_t B, const float *models,
-                         int ncomp, uint64_t first_hyp, usac_record *out);
+                         int ncomp, uint64_t first_hyp, void *scratch /* 12 B x ceil(B/2048) */,
+                         usac_record *out);
 
 hipError_t launch_inliers_h(hipStream_t st, const float4 *pts, uint32_t n, const float *model, float thr,
                             int32_t *idx, int32_t *count, float *sum);

@@ -1,0 +1,33 @@
+"""Summarise a tools/profile.sh output directory into profiles/<tag>_summary.json.
+
+Per kernel: rocprofv3 --kernel-trace --stats average duration, and the PMC passes'
+per-dispatch averages.  HBM traffic per launch = FETCH_SIZE*1024*2 (gfx950 reports half
+the bytes of wide coalesced reads: MI355X_MICROARCH.md §HBM) + WRITE_SIZE*1024.
+"""
+import csv, collections, json, os, sys
+
+src, tag = sys.argv[1], sys.argv[2]
+out = {"source": src, "kernels": {}}
+stats = os.path.join(src, "trace", "run_kernel_stats.csv")
+for r in csv.DictReader(open(stats)):
+    out["kernels"].setdefault(r["Name"], {})["trace"] = {
+        "calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "min_ns": float(r["MinNs"]),
+        "max_ns": float(r["MaxNs"]), "percent": float(r["Percentage"])}
+for d in sorted(os.listdir(src)):
+    if not d.startswith("pmc_"):
+        continue
+    f = os.path.join(src, d, "run_counter_collection.csv")
+    if not os.path.exists(f):
+        continue
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(f)):
+        agg[(r["Kernel_Name"], r["Counter_Name"])].append(float(r["Counter_Value"]))
+    for (k, c), v in agg.items():
+        out["kernels"].setdefault(k, {}).setdefault("pmc", {})[c] = sum(v) / len(v)
+for k, v in out["kernels"].items():
+    p = v.get("pmc", {})
+    if "FETCH_SIZE" in p or "WRITE_SIZE" in p:
+        v["hbm_bytes_per_launch"] = p.get("FETCH_SIZE", 0.0) * 1024 * 2 + p.get("WRITE_SIZE", 0.0) * 1024
+with open(os.path.join("profiles", "%s_summary.json" % tag), "w") as f:
+    json.dump(out, f, indent=1, sort_keys=True)
+print(json.dumps({k[:60]: (v.get("trace", {}).get("avg_ns"), v.get("hbm_bytes_per_launch")) for k, v in out["kernels"].items()}, indent=1))
