@@ -30,6 +30,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--estimator", choices=["homography", "fundamental"], default="homography",
+                    help="homography = cfg2 (the BASELINE metric's config); fundamental = cfg3 without SPRT")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=65536)
@@ -42,36 +44,51 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(pts, thr, dlt_mode, seconds):
-    """The CPU oracle's reference-style loop (glibc pool sampler, per-hypothesis 4-pt DLT,
-    per-model 3x3 inverse, full sequential score) on one host core, bounded sample."""
+def cpu_baseline(kind, pts, thr, dlt_mode, seconds):
+    """The CPU oracle's reference-style loop (glibc pool sampler, per-hypothesis minimal
+    solve, full sequential score of every model) on one host core, bounded sample."""
     from oracle import oracle as O
 
     O.lib()
+    okind = O.FUNDAMENTAL if kind == "fundamental" else O.HOMOGRAPHY
     t0 = time.perf_counter()
-    O.hypothesis_loop(O.HOMOGRAPHY, pts, thr, 1, 50, dlt_mode)
+    O.hypothesis_loop(okind, pts, thr, 1, 50, dlt_mode)
     per = max((time.perf_counter() - t0) / 50, 1e-6)
     count = max(100, int(seconds / per))
     t0 = time.perf_counter()
-    O.hypothesis_loop(O.HOMOGRAPHY, pts, thr, 2, count, dlt_mode)
+    O.hypothesis_loop(okind, pts, thr, 2, count, dlt_mode)
     dt = time.perf_counter() - t0
+    what = "7-pt solve+oriented filter+Sampson score" if kind == "fundamental" else "DLT4+inverse+score"
     return {"value": count / dt, "unit": "hypotheses/s", "cores": 1, "kind": "port",
-            "sample": "%d hypotheses of the same workload (N=%d, sample+DLT4+inverse+score, glibc sampler), "
-                      "%.1f s on 1 core of %s" % (count, len(pts), dt, platform.processor() or platform.machine())}
+            "sample": "%d hypotheses of the same workload (N=%d, sample+%s, glibc sampler), "
+                      "%.1f s on 1 core of %s" % (count, len(pts), what, dt,
+                                                  platform.processor() or platform.machine())}
 
 
-def parity_check(usac, pts, thr, dlt_mode):
+def parity_check(usac, kind, pts, thr, dlt_mode):
     """Inlier-count match vs the reference path (CPU oracle) on 256 host-drawn samples."""
     from oracle import oracle as O
 
-    samples = O.uniform_samples(77, len(pts), 4, 256)
-    est = O.Estimator(O.HOMOGRAPHY, pts, dlt_mode)
-    om, _ = est.estimate_batch(samples)
-    oc, osum = est.score_models(om, thr)
-    with usac.Context(usac.ESTIMATOR.Homography, pts, device=usac_device()) as ctx:
+    fund = kind == "fundamental"
+    m = 7 if fund else 4
+    samples = O.uniform_samples(77, len(pts), m, 256)
+    est = O.Estimator(O.FUNDAMENTAL if fund else O.HOMOGRAPHY, pts, dlt_mode)
+    om, onm = est.estimate_batch(samples)
+    if fund:
+        slots = om.reshape(-1, 9)
+        oc, osum = est.score_models(slots, thr)
+        occupied = (np.arange(3)[None, :] < onm[:, None]).reshape(-1)
+        oc = np.where(occupied, oc, -1)
+        osum = np.where(occupied, osum, 0).astype(np.float32)
+    else:
+        oc, osum = est.score_models(om, thr)
+        occupied = np.ones(len(oc), bool)
+    est_id = usac.ESTIMATOR.Fundamental if fund else usac.ESTIMATOR.Homography
+    with usac.Context(est_id, pts, device=usac_device()) as ctx:
         ctx.set_dlt_mode(dlt_mode)
         c, s, _ = ctx.hypothesize_score(samples=samples, thr=thr)
-    return {"hypotheses": 256, "inlier_counts_equal": bool((c == oc).all()),
+    s = np.where(occupied, s, 0).astype(np.float32)
+    return {"hypotheses": 256, "models": int(occupied.sum()), "inlier_counts_equal": bool((c == oc).all()),
             "scores_bit_equal": bool((s.view(np.int32) == osum.view(np.int32)).all())}
 
 
@@ -119,9 +136,13 @@ def main():
 
     if world > 1:
         dist.init_process_group("gloo")
-    pts, _, _ = synthetic.homography_points(n=args.points, inlier_ratio=0.3, seed=args.seed)
+    fund = args.estimator == "fundamental"
+    if fund:
+        pts, _, _ = synthetic.fundamental_points(n=args.points, inlier_ratio=0.3, seed=args.seed)
+    else:
+        pts, _, _ = synthetic.homography_points(n=args.points, inlier_ratio=0.3, seed=args.seed)
     dlt_mode = 0 if args.dlt == "thin" else 1
-    ctx = usac.Context(usac.ESTIMATOR.Homography, pts, device=local_rank)
+    ctx = usac.Context(usac.ESTIMATOR.Fundamental if fund else usac.ESTIMATOR.Homography, pts, device=local_rank)
     ctx.set_dlt_mode(dlt_mode)
     ctx.set_score_chunks(args.chunks)
     if world > 1:
@@ -129,6 +150,10 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(world, rank, uid[0])
     B = args.batch
+    models_per_hyp = 1.0
+    if fund:  # occupied model slots per sample of the device sampler's stream (one batch)
+        c0, _, _ = ctx.hypothesize_score(B=B, seed=args.seed + 1000, first_hyp=0, thr=args.threshold)
+        models_per_hyp = float((c0 >= 0).sum()) / B
 
     def sync():
         ctx.sync()
@@ -172,11 +197,13 @@ def main():
         total = world * args.steps * B
         value = total / elapsed
         n = args.points
-        bytes_per_hyp = 16 * n + 4 * 4 + 1 * (36 + 8)  # N*S + m*4 + k*(36+8)
+        m = 7 if fund else 4
+        # N*S per scored model + m*4 + k*(36+8)
+        bytes_per_hyp = models_per_hyp * 16 * n + m * 4 + models_per_hyp * (36 + 8)
         avg_score_ms = float(np.mean(score_ms))
         achieved = bytes_per_hyp * B / (avg_score_ms * 1e-3) / 1e9
-        kname = "void usac::k_score_hf<%d, false>" % args.chunks
-        traffic = measured_traffic(kname, n, B)
+        kname = ("void usac::k_score_f<%d>" if fund else "void usac::k_score_hf<%d, false>") % args.chunks
+        traffic = measured_traffic(kname, n, B) if not fund else None
         out = {
             "metric": "model hypotheses/sec (sample+solve+score) and inlier-count match vs ref",
             "value": value,
@@ -189,15 +216,20 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (SURVEY §8(d) cfg2 generator: 30% inliers, 1 px noise, 70% uniform outliers)",
-            "config": {"workload": "cfg2: Homography_estimator (4-pt DLT, %s) + Uniform sampler (device "
-                                   "xorshift), %d correspondences, %d-hypothesis batch per GPU" % (args.dlt, n, B),
+            "data": ("synthetic (SURVEY §8(d) cfg3 generator: two views, 30% inliers, 0.5 px noise)" if fund else
+                     "synthetic (SURVEY §8(d) cfg2 generator: 30% inliers, 1 px noise, 70% uniform outliers)"),
+            "config": {"workload": ("cfg3 without SPRT: Fundamental_estimator (7-pt, oriented filter, Sampson) + "
+                                    "Uniform sampler (device xorshift), %d correspondences, %d-hypothesis batch per "
+                                    "GPU, %.3f models/sample" % (n, B, models_per_hyp)) if fund else
+                                   ("cfg2: Homography_estimator (4-pt DLT, %s) + Uniform sampler (device "
+                                    "xorshift), %d correspondences, %d-hypothesis batch per GPU" % (args.dlt, n, B)),
                        "n_points": n, "batch_per_gpu": B, "threshold": args.threshold,
                        "score_chunks": args.chunks, "parallelism": "hypothesis-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
                          "traffic_unit": "bytes/launch", "traffic_source": traffic[1] if traffic else None,
-                         "kernel": "k_score_hf<%d,false>" % args.chunks, "kernel_ms": avg_score_ms,
+                         "kernel": ("k_score_f<%d>" if fund else "k_score_hf<%d,false>") % args.chunks,
+                         "kernel_ms": avg_score_ms, "models_per_hypothesis": models_per_hyp,
                          "algorithmic_bytes_per_hypothesis": bytes_per_hyp,
                          "hypotheses_per_launch": B,
                          "note": "achieved = algorithmic bytes (16 B x N points per hypothesis, the bytes the "
@@ -208,9 +240,9 @@ def main():
             "best": {"inliers": int(best.inliers), "hyp_index": int(best.hyp_index)},
         }
         if world == 1:
-            out["parity"] = parity_check(usac, pts, args.threshold, dlt_mode)
+            out["parity"] = parity_check(usac, args.estimator, pts, args.threshold, dlt_mode)
             if args.cpu_seconds > 0:
-                out["cpu_baseline"] = cpu_baseline(pts, args.threshold, dlt_mode, args.cpu_seconds)
+                out["cpu_baseline"] = cpu_baseline(args.estimator, pts, args.threshold, dlt_mode, args.cpu_seconds)
                 out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
         print(json.dumps(out), flush=True)
     ctx.close()

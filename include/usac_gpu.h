@@ -10,6 +10,8 @@
  *   usac_estimate_models           Estimator::EstimateModel, batched
  *                                  (usac/estimator/estimator.hpp:19; homography
  *                                  homography_estimator.hpp:47-56 -> dlt.cpp:7-52;
+ *                                  fundamental fundamental_estimator.hpp:48-63 ->
+ *                                  seven_points.cpp:49-156;
  *                                  line2d line2d_estimator.hpp:36-54)
  *   usac_score_models              Quality::getNumberInliers(score, model), batched over
  *                                  models (usac/quality/quality.hpp:60-101)
@@ -17,6 +19,7 @@
  *                                  / Quality::getInliers (quality.hpp:80-87, 108-121)
  *   usac_nonminimal                Estimator::EstimateModelNonMinimalSample
  *                                  (estimator.hpp:21; normalized_dlt.cpp:7-23;
+ *                                  eight_points.cpp:4-100;
  *                                  line2d_estimator.hpp:59-107)
  *   usac_hypothesize_score         Sampler::generateSample + Estimator::EstimateModel +
  *                                  Quality::getNumberInliers + Score::bigger, fused over a
@@ -105,7 +108,10 @@ uint32_t usac_sample_size(const usac_ctx *ctx);
 uint32_t usac_num_points(const usac_ctx *ctx);
 
 /* ---- plugin operators ----------------------------------------------------------- */
-/* samples: B x m int32 (host) -> models: B x 9 floats, n_models[B] (0/1 per sample). */
+/* samples: B x m int32 (host) -> models: B x S x 9 floats, n_models[B] valid models per
+ * sample, S = model slots per sample (3 for USAC_FUNDAMENTAL -- SevenPointsAlgorithm returns
+ * <= 3 F that pass the oriented constraint, fundamental_estimator.hpp:48-63 -- else 1);
+ * empty slots are zero-filled. */
 int usac_estimate_models(usac_ctx *ctx, const int32_t *samples, uint32_t B, float *models, int32_t *n_models);
 /* models: n_models x 9 floats (host); counts/sums (host, sums nullable).  Counts are
  * exact; sums are the sequential fp32 sums of quality.hpp:89-96. */
@@ -117,8 +123,10 @@ int usac_get_inliers(usac_ctx *ctx, const float *model, float thr, int32_t *idx,
 int usac_nonminimal(usac_ctx *ctx, const int32_t *idx, uint32_t n, float *model);
 
 /* Fused batch: samples (B x m host int32) or NULL => device xorshift sampler keyed by
- * (seed, first_hyp + i).  Per-hypothesis counts/sums (host, nullable) and the batch best
- * under Score::bigger with the earliest index on exact ties (best, nullable). */
+ * (seed, first_hyp + i).  Per-model counts/sums (host, nullable, B x S entries: slot
+ * b*S + j = j-th valid model of sample b, count -1 on an empty slot) and the batch best
+ * under Score::bigger with the earliest (sample, slot) on exact ties (best, nullable;
+ * best->hyp_index = first_hyp + sample). */
 int usac_hypothesize_score(usac_ctx *ctx, const int32_t *samples, uint32_t B, uint64_t seed, uint64_t first_hyp,
                            float thr, int32_t *counts, float *sums, usac_record *best);
 /* Asynchronous device-sampled batch for throughput runs: enqueues sample+solve+score+

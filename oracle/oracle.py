@@ -63,6 +63,8 @@ def lib():
         L.orc_inv3x3.argtypes = [_f32p, _f32p]
         L.orc_quality.argtypes = [ctypes.c_void_p, _f32p, ctypes.c_float, _i32p, _f32p, _i32p]
         L.orc_score_models.argtypes = [ctypes.c_void_p, _f32p, ctypes.c_int, ctypes.c_float, _i32p, _f32p]
+        L.orc_est_max_models.argtypes = [ctypes.c_void_p]
+        L.orc_cubic_roots.argtypes = [ctypes.c_double] * 4 + [ctypes.POINTER(ctypes.c_double)]
         L.orc_estimate_batch.argtypes = [ctypes.c_void_p, _i32p, ctypes.c_int, _f32p, _i32p]
         L.orc_gt_inliers_homography.argtypes = [_f32p, ctypes.c_uint, _f32p, ctypes.c_float]
         L.orc_std_termination.argtypes = [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, ctypes.c_float, ctypes.c_uint]
@@ -114,7 +116,11 @@ class Estimator:
 
     @property
     def m(self):
-        return 2 if self.kind == LINE2D else 4
+        return {LINE2D: 2, FUNDAMENTAL: 7}.get(self.kind, 4)
+
+    @property
+    def max_models(self):
+        return 3 if self.kind == FUNDAMENTAL else 1
 
     def estimate(self, sample):
         sample = np.ascontiguousarray(sample, dtype=np.int32)
@@ -125,10 +131,11 @@ class Estimator:
     def estimate_batch(self, samples):
         samples = np.ascontiguousarray(samples, dtype=np.int32)
         B = samples.shape[0]
-        models = np.zeros((B, 9), dtype=np.float32)
+        km = self.max_models
+        models = np.zeros((B, km, 9), dtype=np.float32)
         nm = np.zeros(B, dtype=np.int32)
         lib().orc_estimate_batch(self._h, _p(samples, _i32p), B, _p(models, _f32p), _p(nm, _i32p))
-        return models, nm
+        return (models[:, 0] if km == 1 else models), nm
 
     def nonminimal(self, idx):
         idx = np.ascontiguousarray(idx, dtype=np.int32)
@@ -164,6 +171,12 @@ class Estimator:
         s = np.zeros(n, dtype=np.float32)
         lib().orc_score_models(self._h, _p(models, _f32p), n, ctypes.c_float(thr), _p(c, _i32p), _p(s, _f32p))
         return c, s
+
+
+def cubic_roots(c0, c1, c2, c3):
+    r = (ctypes.c_double * 3)()
+    k = lib().orc_cubic_roots(c0, c1, c2, c3, r)
+    return [r[i] for i in range(k)]
 
 
 def inv3x3(m):

@@ -275,10 +275,11 @@ struct orc_est {
     /* cached model parameters (setModelParameters) */
     float a, b, c;        /* line2d_estimator.hpp:162-164 */
     float h[9], hi[9];    /* homography_estimator.hpp:33-45 */
+    float f[9];           /* fundamental_estimator.hpp:36-46 */
 };
 
 orc_est *orc_est_new(int kind, const float *points, unsigned int n, int dlt_mode) {
-    if (kind != ORC_LINE2D && kind != ORC_HOMOGRAPHY) return NULL;
+    if (kind != ORC_LINE2D && kind != ORC_HOMOGRAPHY && kind != ORC_FUNDAMENTAL) return NULL;
     orc_est *e = (orc_est *)calloc(1, sizeof(*e));
     e->kind = kind;
     e->pts = points;
@@ -287,7 +288,10 @@ orc_est *orc_est_new(int kind, const float *points, unsigned int n, int dlt_mode
     return e;
 }
 void orc_est_free(orc_est *e) { free(e); }
-int orc_est_sample_size(const orc_est *e) { return e->kind == ORC_LINE2D ? 2 : 4; }
+int orc_est_sample_size(const orc_est *e) {
+    return e->kind == ORC_LINE2D ? 2 : e->kind == ORC_FUNDAMENTAL ? 7 : 4;
+}
+int orc_est_max_models(const orc_est *e) { return e->kind == ORC_FUNDAMENTAL ? 3 : 1; }
 
 /* DLt::DLT4p (usac/estimator/dlt/dlt.cpp:7-52): rows of A built in fp32 exactly as
  * dlt.cpp:24-41, SVD restated by row_jacobi; H = v / v[8] rounded once to float. */
@@ -474,14 +478,304 @@ static int line2d_nonminimal(const orc_est *e, const int *sample, unsigned int n
     return 1;
 }
 
+/* ------------------------------------------------------------ fundamental */
+
+/* Orthonormal complement of the converged Jacobi rows (the FULL_UV null-space rows of
+ * cv::SVDecomp, seven_points.cpp:88-90): rows normalised (zero rows skipped); for each
+ * complement vector j: start axis = argmin_k (sum_i U[i][k]^2 + sum_{l<j} N[l][k]^2) (first
+ * minimum), two Gram-Schmidt passes against U then N[0..j-1], normalise (x_k / |x|). */
+static void null_complement(double W[][9], int r, int count, double N[][9]) {
+    double U[9][9];
+    int nu = 0;
+    for (int i = 0; i < r; i++) {
+        double a = 0.0;
+        for (int k = 0; k < 9; k++) a += W[i][k] * W[i][k];
+        if (a > 0.0) {
+            double inv = 1.0 / sqrt(a);
+            for (int k = 0; k < 9; k++) U[nu][k] = W[i][k] * inv;
+            nu++;
+        }
+    }
+    for (int j = 0; j < count; j++) {
+        int ks = 0;
+        double bestc = 0.0;
+        for (int k = 0; k < 9; k++) {
+            double c = 0.0;
+            for (int i = 0; i < nu; i++) c += U[i][k] * U[i][k];
+            for (int l = 0; l < j; l++) c += N[l][k] * N[l][k];
+            if (k == 0 || c < bestc) {
+                bestc = c;
+                ks = k;
+            }
+        }
+        double x[9];
+        for (int k = 0; k < 9; k++) x[k] = (k == ks) ? 1.0 : 0.0;
+        for (int pass = 0; pass < 2; pass++) {
+            for (int i = 0; i < nu; i++) {
+                double d = 0.0;
+                for (int k = 0; k < 9; k++) d += U[i][k] * x[k];
+                for (int k = 0; k < 9; k++) x[k] -= d * U[i][k];
+            }
+            for (int l = 0; l < j; l++) {
+                double d = 0.0;
+                for (int k = 0; k < 9; k++) d += N[l][k] * x[k];
+                for (int k = 0; k < 9; k++) x[k] -= d * N[l][k];
+            }
+        }
+        double nrm = 0.0;
+        for (int k = 0; k < 9; k++) nrm += x[k] * x[k];
+        nrm = sqrt(nrm);
+        for (int k = 0; k < 9; k++) N[j][k] = x[k] / nrm;
+    }
+}
+
+/* Real roots of c0 x^3 + c1 x^2 + c2 x + c3, ascending -- restates the contract of
+ * cv::solveCubic (seven_points.cpp:131) with IEEE basic operations only (OpenCV's
+ * closed form uses acos/cos/pow, which are not correctly rounded; this spec is shared
+ * bit-for-bit with the device).  Monic form a, b, c; Cauchy bound R = 1 + max(|a|,|b|,|c|);
+ * critical points from a^2 - 3b; each sign-changing bracket refined by bisection
+ * (midpoint 0.5*(lo+hi), stop when it equals an end, <= 200 steps). */
+static double cubic_eval(double a, double b, double c, double x) { return ((x + a) * x + b) * x + c; }
+
+static double cubic_bisect(double a, double b, double c, double lo, double hi) {
+    double flo = cubic_eval(a, b, c, lo);
+    for (int it = 0; it < 200; it++) {
+        double mid = 0.5 * (lo + hi);
+        if (!(mid > lo && mid < hi)) break;
+        double fm = cubic_eval(a, b, c, mid);
+        if (fm == 0.0) return mid;
+        if ((fm < 0.0) == (flo < 0.0)) {
+            lo = mid;
+            flo = fm;
+        } else {
+            hi = mid;
+        }
+    }
+    return 0.5 * (lo + hi);
+}
+
+static int cubic_roots(double c0, double c1, double c2, double c3, double *r) {
+    if (c0 == 0.0) {
+        if (c1 == 0.0) {
+            if (c2 == 0.0) return 0;
+            r[0] = -c3 / c2;
+            return 1;
+        }
+        double D = c2 * c2 - 4.0 * c1 * c3;
+        if (D < 0.0) return 0;
+        if (D == 0.0) {
+            r[0] = -c2 / (2.0 * c1);
+            return 1;
+        }
+        double s = sqrt(D);
+        double q = -0.5 * (c2 + (c2 >= 0.0 ? s : -s));
+        double x1 = q / c1, x2 = c3 / q;
+        r[0] = x1 < x2 ? x1 : x2;
+        r[1] = x1 < x2 ? x2 : x1;
+        return 2;
+    }
+    const double a = c1 / c0, b = c2 / c0, c = c3 / c0;
+    double R = fabs(a);
+    if (fabs(b) > R) R = fabs(b);
+    if (fabs(c) > R) R = fabs(c);
+    R = R + 1.0;
+    const double D = a * a - 3.0 * b;
+    int n = 0;
+    if (!(D > 0.0)) {
+        r[n++] = cubic_bisect(a, b, c, -R, R);
+        return n;
+    }
+    const double s = sqrt(D);
+    const double m1 = (-a - s) / 3.0, m2 = (-a + s) / 3.0;
+    const double v1 = cubic_eval(a, b, c, m1), v2 = cubic_eval(a, b, c, m2);
+    if (v1 >= 0.0) r[n++] = cubic_bisect(a, b, c, -R, m1);
+    if (v1 > 0.0 && v2 < 0.0) r[n++] = cubic_bisect(a, b, c, m1, m2);
+    if (v2 <= 0.0) r[n++] = cubic_bisect(a, b, c, m2, R);
+    return n;
+}
+
+/* FundamentalEstimator oriented constraint (fundamental_estimator.hpp:189-231), fp32:
+ * epipole = row0 x row2 (row1 x row2 when all |e_i| <= 1.9984e-15), then the sign of
+ * (F0 x2 + F3 y2 + F6)(e1 - e2 y1) must agree over the 7 sample points. */
+static int fund_is_valid(const float *pts, const float *F, const int *sample) {
+    float e0 = F[1] * F[8] - F[2] * F[7];
+    float e1 = F[2] * F[6] - F[0] * F[8];
+    float e2 = F[0] * F[7] - F[1] * F[6];
+    if (!((e0 > 1.9984e-15 || e0 < -1.9984e-15) || (e1 > 1.9984e-15 || e1 < -1.9984e-15) ||
+          (e2 > 1.9984e-15 || e2 < -1.9984e-15))) {
+        e0 = F[4] * F[8] - F[5] * F[7];
+        e1 = F[5] * F[6] - F[3] * F[8];
+        e2 = F[3] * F[7] - F[4] * F[6];
+    }
+    float sig1 = 0.f;
+    for (int i = 0; i < 7; i++) {
+        const float *p = pts + 4 * (size_t)sample[i];
+        float s1 = F[0] * p[2] + F[3] * p[3] + F[6];
+        float s2 = e1 - e2 * p[1];
+        float sig = s1 * s2;
+        if (i == 0) sig1 = sig;
+        else if (sig1 * sig < 0) return 0;
+    }
+    return 1;
+}
+
+/* FundamentalSolver::SevenPointsAlgorithm (seven_points.cpp:49-156) + the validity filter
+ * of FundamentalEstimator::EstimateModel (fundamental_estimator.hpp:48-63): 7x9 fp32
+ * rows, fp64 row Jacobi + null complement (f1, f2 = the two null rows, cast to float),
+ * fp32 cubic coefficients exactly as :98-128, roots (cubic_roots) cast to float, fp32
+ * F assembly with F33 normalisation (:138-154); valid models kept in root order. */
+static int fundamental_7pt(const orc_est *e, const int *sample, float *models) {
+    double W[7][9];
+    for (int i = 0; i < 7; i++) {
+        const float *p = e->pts + 4 * (size_t)sample[i];
+        float x1 = p[0], y1 = p[1], x2 = p[2], y2 = p[3];
+        float row[9] = {x2 * x1, x2 * y1, x2, y2 * x1, y2 * y1, y2, x1, y1, 1.f};
+        for (int k = 0; k < 9; k++) W[i][k] = (double)row[k];
+    }
+    row_jacobi(W, 7);
+    double N[2][9];
+    null_complement(W, 7, 2, N);
+    float f1[9], f2[9];
+    for (int k = 0; k < 9; k++) {
+        f1[k] = (float)N[0][k];
+        f2[k] = (float)N[1][k];
+    }
+    for (int i = 0; i < 9; i++) f1[i] -= f2[i];
+    float t0 = f2[4] * f2[8] - f2[5] * f2[7];
+    float t1 = f2[3] * f2[8] - f2[5] * f2[6];
+    float t2 = f2[3] * f2[7] - f2[4] * f2[6];
+    float c[4];
+    c[3] = f2[0] * t0 - f2[1] * t1 + f2[2] * t2;
+    c[2] = f1[0] * t0 - f1[1] * t1 + f1[2] * t2 - f1[3] * (f2[1] * f2[8] - f2[2] * f2[7]) +
+           f1[4] * (f2[0] * f2[8] - f2[2] * f2[6]) - f1[5] * (f2[0] * f2[7] - f2[1] * f2[6]) +
+           f1[6] * (f2[1] * f2[5] - f2[2] * f2[4]) - f1[7] * (f2[0] * f2[5] - f2[2] * f2[3]) +
+           f1[8] * (f2[0] * f2[4] - f2[1] * f2[3]);
+    t0 = f1[4] * f1[8] - f1[5] * f1[7];
+    t1 = f1[3] * f1[8] - f1[5] * f1[6];
+    t2 = f1[3] * f1[7] - f1[4] * f1[6];
+    c[1] = f2[0] * t0 - f2[1] * t1 + f2[2] * t2 - f2[3] * (f1[1] * f1[8] - f1[2] * f1[7]) +
+           f2[4] * (f1[0] * f1[8] - f1[2] * f1[6]) - f2[5] * (f1[0] * f1[7] - f1[1] * f1[6]) +
+           f2[6] * (f1[1] * f1[5] - f1[2] * f1[4]) - f2[7] * (f1[0] * f1[5] - f1[2] * f1[3]) +
+           f2[8] * (f1[0] * f1[4] - f1[1] * f1[3]);
+    c[0] = f1[0] * t0 - f1[1] * t1 + f1[2] * t2;
+    double rd[3];
+    int nroots = cubic_roots((double)c[0], (double)c[1], (double)c[2], (double)c[3], rd);
+    int valid = 0;
+    for (int k = 0; k < nroots; k++) {
+        float r = (float)rd[k];
+        float F[9];
+        float lambda = r, mu = 1.f;
+        float s = f1[8] * r + f2[8];
+        if ((double)fabsf(s) > DBL_EPSILON) {
+            mu = 1.f / s;
+            lambda *= mu;
+            F[8] = 1.f;
+        } else {
+            F[8] = 0.f;
+        }
+        for (int i = 0; i < 8; i++) F[i] = f1[i] * lambda + f2[i] * mu;
+        if (fund_is_valid(e->pts, F, sample)) {
+            memcpy(models + 9 * valid, F, sizeof(F));
+            valid++;
+        }
+    }
+    return valid;
+}
+
+/* FundamentalSolver::EightPointsAlgorithm (eight_points.cpp:4-100): normalising transform,
+ * n x 9 rows in fp32; thin last row for n <= 8, fp64 normal-matrix smallest
+ * eigenvector otherwise (blocked order as the DLT); F = T2^T F T1 (fp64), F /= F33 when
+ * |F33| > FLT_EPSILON (:76-99). */
+static int fundamental_8pt(const orc_est *e, const int *sample, unsigned int n, float *F) {
+    if (n == 0) return 0;
+    float T1[9], T2[9];
+    float *norm = (float *)malloc(sizeof(float) * 4 * n);
+    normalizing_transform(e->pts, sample, n, T1, T2, norm);
+    double v[9];
+    if (n <= 8) {
+        double W[9][9];
+        for (unsigned int i = 0; i < n; i++) {
+            float x1 = norm[4 * i], y1 = norm[4 * i + 1], x2 = norm[4 * i + 2], y2 = norm[4 * i + 3];
+            float row[9] = {x2 * x1, x2 * y1, x2, y2 * x1, y2 * y1, y2, x1, y1, 1.f};
+            for (int k = 0; k < 9; k++) W[i][k] = (double)row[k];
+        }
+        row_jacobi(W, (int)n);
+        pick_vector(W, (int)n, ORC_DLT_THIN, v);
+    } else {
+        double AtA[9][9];
+        memset(AtA, 0, sizeof(AtA));
+        for (unsigned int b0 = 0; b0 < n; b0 += 64) {
+            double P[9][9];
+            memset(P, 0, sizeof(P));
+            unsigned int b1 = b0 + 64 < n ? b0 + 64 : n;
+            for (unsigned int i = b0; i < b1; i++) {
+                float x1 = norm[4 * i], y1 = norm[4 * i + 1], x2 = norm[4 * i + 2], y2 = norm[4 * i + 3];
+                float row[9] = {x2 * x1, x2 * y1, x2, y2 * x1, y2 * y1, y2, x1, y1, 1.f};
+                double rd[9];
+                for (int k = 0; k < 9; k++) rd[k] = (double)row[k];
+                for (int j = 0; j < 9; j++)
+                    for (int k = j; k < 9; k++) P[j][k] += rd[j] * rd[k];
+            }
+            for (int j = 0; j < 9; j++)
+                for (int k = j; k < 9; k++) AtA[j][k] += P[j][k];
+        }
+        for (int j = 0; j < 9; j++)
+            for (int k = 0; k < j; k++) AtA[j][k] = AtA[k][j];
+        sym_eig_min(AtA, v);
+    }
+    free(norm);
+    /* T2^T = [s2 0 0; 0 s2 0; t2_13 t2_23 1] */
+    double T2t[9] = {T2[0], 0.0, 0.0, 0.0, T2[4], 0.0, T2[2], T2[5], 1.0};
+    double tmp[9], Fd[9];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) {
+            double s = 0.0;
+            for (int k = 0; k < 3; k++) s += v[3 * r + k] * (double)T1[3 * k + c];
+            tmp[3 * r + c] = s;
+        }
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) {
+            double s = 0.0;
+            for (int k = 0; k < 3; k++) s += T2t[3 * r + k] * tmp[3 * k + c];
+            Fd[3 * r + c] = s;
+        }
+    if (fabs(Fd[8]) > (double)FLT_EPSILON) {
+        for (int k = 0; k < 9; k++) F[k] = (float)(Fd[k] / Fd[8]);
+    } else {
+        for (int k = 0; k < 9; k++) F[k] = (float)Fd[k];
+    }
+    return 1;
+}
+
+/* FundamentalEstimator::GetError (fundamental_estimator.hpp:101-134): Sampson error, fp32,
+ * left-to-right sums, one IEEE division (threshold in px^2). */
+static inline float fundamental_error(const orc_est *e, unsigned int pidx) {
+    const float *p = e->pts + 4 * (size_t)pidx;
+    const float x1 = p[0], y1 = p[1], x2 = p[2], y2 = p[3];
+    const float *f = e->f;
+    float Fx = f[0] * x1 + f[1] * y1 + f[2];
+    float Fy = f[3] * x1 + f[4] * y1 + f[5];
+    float Gx = f[0] * x2 + f[3] * y2 + f[6];
+    float Gy = f[1] * x2 + f[4] * y2 + f[7];
+    float s = x2 * Fx + y2 * Fy + f[6] * x1 + f[7] * y1 + f[8];
+    return (s * s) / (Fx * Fx + Fy * Fy + Gx * Gx + Gy * Gy);
+}
+
 int orc_est_estimate(orc_est *e, const int *sample, float *models) {
     if (e->kind == ORC_LINE2D) return line2d_estimate(e, sample, models);
+    if (e->kind == ORC_FUNDAMENTAL) return fundamental_7pt(e, sample, models);
     return homography_dlt4(e, sample, models);
 }
 
 int orc_est_nonminimal(orc_est *e, const int *sample, unsigned int n, float *model) {
     if (e->kind == ORC_LINE2D) return line2d_nonminimal(e, sample, n, model);
+    if (e->kind == ORC_FUNDAMENTAL) return fundamental_8pt(e, sample, n, model);
     return homography_normalized_dlt(e, sample, n, model);
+}
+
+/* test hook: the cubic solver spec */
+int orc_cubic_roots(double c0, double c1, double c2, double c3, double *roots) {
+    return cubic_roots(c0, c1, c2, c3, roots);
 }
 
 void orc_est_set_model(orc_est *e, const float *m) {
@@ -489,6 +783,8 @@ void orc_est_set_model(orc_est *e, const float *m) {
         e->a = m[0];
         e->b = m[1];
         e->c = m[2];
+    } else if (e->kind == ORC_FUNDAMENTAL) {
+        memcpy(e->f, m, sizeof(float) * 9);
     } else {
         memcpy(e->h, m, sizeof(float) * 9);
         orc_inv3x3(m, e->hi);
@@ -525,7 +821,9 @@ static inline float line2d_error(const orc_est *e, unsigned int pidx) {
 }
 
 float orc_est_error(const orc_est *e, unsigned int pidx) {
-    return e->kind == ORC_LINE2D ? line2d_error(e, pidx) : homography_error(e, pidx);
+    if (e->kind == ORC_LINE2D) return line2d_error(e, pidx);
+    if (e->kind == ORC_FUNDAMENTAL) return fundamental_error(e, pidx);
+    return homography_error(e, pidx);
 }
 
 /* ------------------------------------------------------------ quality */
@@ -538,6 +836,15 @@ void orc_quality(orc_est *e, const float *model, float thr, int *count, float *s
     if (e->kind == ORC_LINE2D) {
         for (unsigned int p = 0; p < e->n; p++) {
             float err = line2d_error(e, p);
+            if (err < thr) {
+                if (inliers) inliers[cnt] = (int)p;
+                cnt++;
+                s += err;
+            }
+        }
+    } else if (e->kind == ORC_FUNDAMENTAL) {
+        for (unsigned int p = 0; p < e->n; p++) {
+            float err = fundamental_error(e, p);
             if (err < thr) {
                 if (inliers) inliers[cnt] = (int)p;
                 cnt++;
@@ -562,9 +869,11 @@ void orc_score_models(orc_est *e, const float *models, int n_models, float thr, 
     for (int i = 0; i < n_models; i++) orc_quality(e, models + 9 * (size_t)i, thr, &counts[i], &sums[i], NULL);
 }
 
+/* models: n_samples x (9 * max_models) floats (max_models = 3 for F, else 1) */
 void orc_estimate_batch(orc_est *e, const int *samples, int n_samples, float *models, int *n_models) {
-    int m = orc_est_sample_size(e);
-    for (int i = 0; i < n_samples; i++) n_models[i] = orc_est_estimate(e, samples + (size_t)i * m, models + 9 * (size_t)i);
+    int m = orc_est_sample_size(e), km = orc_est_max_models(e);
+    for (int i = 0; i < n_samples; i++)
+        n_models[i] = orc_est_estimate(e, samples + (size_t)i * m, models + 9 * (size_t)km * i);
 }
 
 /* dataset/GetImage.h:209-231: Quality::getInliers with the model and with model.inv(),

@@ -47,6 +47,10 @@ typedef struct orc_est orc_est;
 orc_est *orc_est_new(int kind, const float *points, unsigned int n, int dlt_mode);
 void orc_est_free(orc_est *e);
 int orc_est_sample_size(const orc_est *e);
+/* models per EstimateModel call: 3 for the 7-point fundamental solver, else 1 */
+int orc_est_max_models(const orc_est *e);
+/* real roots (ascending) of c0 x^3 + c1 x^2 + c2 x + c3: the shared cubic spec of the 7-pt solver */
+int orc_cubic_roots(double c0, double c1, double c2, double c3, double *roots);
 /* EstimateModel: writes <= 3 models of 9 floats; returns number of models */
 int orc_est_estimate(orc_est *e, const int *sample, float *models);
 /* EstimateModelNonMinimalSample: returns 1 on success */

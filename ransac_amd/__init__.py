@@ -177,6 +177,8 @@ class Context:
                             % (device, self.estimator.name, self.n, self.cols))
         self._h = h
         self.m = int(L.usac_sample_size(h))
+        # model slots per minimal sample: the 7-point solver returns up to 3 models
+        self.spk = 3 if self.estimator == ESTIMATOR.Fundamental else 1
 
     def close(self):
         if getattr(self, "_h", None):
@@ -211,14 +213,16 @@ class Context:
         self._check(lib().usac_set_score_variant(self._h, int(variant)), "set_score_variant")
 
     def estimate_models(self, samples):
-        """Estimator::EstimateModel over a batch of minimal samples -> (B x 9 models, n_models)."""
+        """Estimator::EstimateModel over a batch of minimal samples -> (models, n_models):
+        models is B x 9, or B x 3 x 9 for the fundamental 7-point solver (valid models first,
+        zero-filled)."""
         s = np.ascontiguousarray(samples, dtype=np.int32).reshape(-1, self.m)
         B = s.shape[0]
-        models = np.zeros((B, 9), dtype=np.float32)
+        models = np.zeros((B, self.spk, 9), dtype=np.float32)
         nm = np.zeros(B, dtype=np.int32)
         self._check(lib().usac_estimate_models(self._h, _ptr(s, ctypes.c_int32), B, _ptr(models, ctypes.c_float),
                                                _ptr(nm, ctypes.c_int32)), "estimate_models")
-        return models, nm
+        return (models[:, 0] if self.spk == 1 else models), nm
 
     def score_models(self, models, thr):
         """Quality::getNumberInliers for each model -> (counts, sums)."""
@@ -255,15 +259,17 @@ class Context:
         return out
 
     def hypothesize_score(self, B=None, samples=None, seed=0, first_hyp=0, thr=2.0, per_hypothesis=True):
-        """Fused sample + solve + score (+ batch best).  samples=None -> device sampler."""
+        """Fused sample + solve + score (+ batch best).  samples=None -> device sampler.
+        Per-model outputs have B * spk entries (slot 3b + j = j-th valid model of sample b
+        for the fundamental solver; count -1 marks an empty slot)."""
         L = lib()
         if samples is not None:
             s = np.ascontiguousarray(samples, dtype=np.int32).reshape(-1, self.m)
             B = s.shape[0]
         else:
             s = None
-        c = np.zeros(B, dtype=np.int32) if per_hypothesis else None
-        sm = np.zeros(B, dtype=np.float32) if per_hypothesis else None
+        c = np.zeros(B * self.spk, dtype=np.int32) if per_hypothesis else None
+        sm = np.zeros(B * self.spk, dtype=np.float32) if per_hypothesis else None
         best = Record()
         self._check(L.usac_hypothesize_score(self._h, _ptr(s, ctypes.c_int32), B, seed, first_hyp,
                                              ctypes.c_float(thr), _ptr(c, ctypes.c_int32), _ptr(sm, ctypes.c_float),

@@ -452,7 +452,7 @@ __global__ __launch_bounds__(256) void k_argmax_part(const int32_t *__restrict__
 
 __global__ __launch_bounds__(256) void k_argmax_final(const BestEntry *__restrict__ part, uint32_t nparts, uint32_t B,
                                                       const float *__restrict__ models, int ncomp, uint64_t first_hyp,
-                                                      usac_record *out) {
+                                                      uint32_t spk, usac_record *out) {
     __shared__ BestEntry sh[256];
     const uint32_t t = threadIdx.x;
     BestEntry b{-1, 0.f, 0xFFFFFFFFu};
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(256) void k_argmax_final(const BestEntry *__restric
         r.valid = sc0 >= 0 ? 1 : 0;
         r.inliers = sc0 < 0 ? 0 : sc0;
         r.score = ss0;
-        r.hyp_index = first_hyp + (i == 0xFFFFFFFFu ? 0 : i);
+        r.hyp_index = first_hyp + (i == 0xFFFFFFFFu ? 0 : i / spk);  // spk model slots per hypothesis
         for (int k = 0; k < 9; k++) r.model[k] = (k < ncomp && r.valid) ? models[(size_t)k * B + i] : 0.f;
         *out = r;
     }
@@ -645,11 +645,12 @@ hipError_t launch_score_line(hipStream_t st, int chunks, const float2 *pts, uint
 }
 
 hipError_t launch_argmax(hipStream_t st, const int32_t *counts, const float *sums, uint32_t B, const float *models,
-                         int ncomp, uint64_t first_hyp, void *scratch, usac_record *out) {
+                         int ncomp, uint64_t first_hyp, uint32_t spk, void *scratch, usac_record *out) {
     const uint32_t nparts = (B + 2047) / 2048;
     BestEntry *part = static_cast<BestEntry *>(scratch);
     hipLaunchKernelGGL(k_argmax_part, dim3(nparts), dim3(256), 0, st, counts, sums, B, part);
-    hipLaunchKernelGGL(k_argmax_final, dim3(1), dim3(256), 0, st, part, nparts, B, models, ncomp, first_hyp, out);
+    hipLaunchKernelGGL(k_argmax_final, dim3(1), dim3(256), 0, st, part, nparts, B, models, ncomp, first_hyp, spk,
+                       out);
     return LAUNCH_CHECK();
 }
 

@@ -82,7 +82,9 @@ __device__ __forceinline__ double sel9(const double *r, int j) {
     return v;
 }
 
-// block partials of A^T A: block c, lane e < 45 -> upper-triangle entry e (row-major j<=k)
+// block partials of A^T A: block c, lane e < 45 -> upper-triangle entry e (row-major j<=k).
+// FUND: one 8-point row per correspondence (eight_points.cpp:26-45), else two DLT rows.
+template <bool FUND>
 __global__ __launch_bounds__(64) void k_ata_partial(const float4 *__restrict__ q, uint32_t n,
                                                     double *__restrict__ partial) {
     const uint32_t e = threadIdx.x;
@@ -101,28 +103,47 @@ __global__ __launch_bounds__(64) void k_ata_partial(const float4 *__restrict__ q
     double acc = 0.0;
     for (uint32_t i = b0; i < b1; i++) {
         const float4 p = q[i];
-        double r0[9], r1[9];
-        dlt_rows(p.x, p.y, p.z, p.w, r0, r1);
-        acc += sel9(r0, j) * sel9(r0, k) + sel9(r1, j) * sel9(r1, k);
+        if (FUND) {
+            double r[9];
+            fund_row(p.x, p.y, p.z, p.w, r);
+            acc += sel9(r, j) * sel9(r, k);
+        } else {
+            double r0[9], r1[9];
+            dlt_rows(p.x, p.y, p.z, p.w, r0, r1);
+            acc += sel9(r0, j) * sel9(r0, k) + sel9(r1, j) * sel9(r1, k);
+        }
     }
     partial[(size_t)blockIdx.x * 45 + e] = acc;
 }
 
-// Final DLT solve, one wave: A^T A from the partials (lane e), cyclic Jacobi eigen on 9
-// lanes (LDS), smallest-eigenvalue vector; or the thin row-Jacobi for 2n <= 8 rows;
-// then H = T2^-1 * Hn * T1 (fp64), H /= H33, cast to float.
-template <int R>
+// Final solve, one wave: A^T A from the partials (lane e), cyclic Jacobi eigen on 9
+// lanes (LDS), smallest-eigenvalue vector; or the thin row-Jacobi when the system has
+// <= 8 rows (homography 2n <= 8, fundamental n <= 8: SURVEY Q1/Q2); then
+//   homography : H = T2^-1 * Hn * T1 (fp64), H /= H33 (normalized_dlt.cpp:18-22);
+//   fundamental: F = T2^T * Fn * T1 (fp64), F /= F33 when |F33| > FLT_EPSILON
+//                (eight_points.cpp:76-99);
+// cast to float.
+template <int R, bool FUND>
 __device__ void thin_solve(const float4 *q, double *v) {
     double W[R][9];
+    if (FUND) {
 #pragma unroll
-    for (int i = 0; i < R / 2; i++) {
-        const float4 p = q[i];
-        dlt_rows(p.x, p.y, p.z, p.w, W[2 * i], W[2 * i + 1]);
+        for (int i = 0; i < R; i++) {
+            const float4 p = q[i];
+            fund_row(p.x, p.y, p.z, p.w, W[i]);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < R / 2; i++) {
+            const float4 p = q[i];
+            dlt_rows(p.x, p.y, p.z, p.w, W[2 * i], W[2 * i + 1]);
+        }
     }
     row_jacobi<R>(W);
     pick_vector<R>(W, 0, v);
 }
 
+template <bool FUND>
 __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q, uint32_t n,
                                                    const double *__restrict__ partial, uint32_t nblocks,
                                                    const float *ws, float *model_out, int32_t *ok) {
@@ -130,13 +151,26 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q,
     __shared__ double V[9][9];
     __shared__ double s_v[9];
     const uint32_t t = threadIdx.x;
-    if (2 * n <= 9) {
+    if (FUND ? n <= 8 : 2 * n <= 9) {
         if (t == 0) {
             double v[9];
-            if (n == 1) thin_solve<2>(q, v);
-            else if (n == 2) thin_solve<4>(q, v);
-            else if (n == 3) thin_solve<6>(q, v);
-            else thin_solve<8>(q, v);
+            if (FUND) {
+                switch (n) {
+                    case 1: thin_solve<1, true>(q, v); break;
+                    case 2: thin_solve<2, true>(q, v); break;
+                    case 3: thin_solve<3, true>(q, v); break;
+                    case 4: thin_solve<4, true>(q, v); break;
+                    case 5: thin_solve<5, true>(q, v); break;
+                    case 6: thin_solve<6, true>(q, v); break;
+                    case 7: thin_solve<7, true>(q, v); break;
+                    default: thin_solve<8, true>(q, v); break;
+                }
+            } else {
+                if (n == 1) thin_solve<2, false>(q, v);
+                else if (n == 2) thin_solve<4, false>(q, v);
+                else if (n == 3) thin_solve<6, false>(q, v);
+                else thin_solve<8, false>(q, v);
+            }
             for (int k = 0; k < 9; k++) s_v[k] = v[k];
         }
         __syncthreads();
@@ -200,7 +234,29 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q,
         }
         __syncthreads();
     }
-    if (t == 0) {
+    if (t == 0 && FUND) {
+        double T1[9], tmp[9], Fd[9];
+        for (int k = 0; k < 9; k++) T1[k] = (double)ws[k];
+        const double T2t[9] = {(double)ws[9], 0.0, 0.0, 0.0, (double)ws[13], 0.0, (double)ws[11], (double)ws[14], 1.0};
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) {
+                double s = 0.0;
+                for (int k = 0; k < 3; k++) s += s_v[3 * r + k] * T1[3 * k + c];
+                tmp[3 * r + c] = s;
+            }
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) {
+                double s = 0.0;
+                for (int k = 0; k < 3; k++) s += T2t[3 * r + k] * tmp[3 * k + c];
+                Fd[3 * r + c] = s;
+            }
+        if (fabs(Fd[8]) > (double)1.1920928955078125e-07f) {
+            for (int k = 0; k < 9; k++) model_out[k] = (float)(Fd[k] / Fd[8]);
+        } else {
+            for (int k = 0; k < 9; k++) model_out[k] = (float)Fd[k];
+        }
+        *ok = 1;
+    } else if (t == 0) {
         float T1[9], T2[9], T2i[9];
         for (int k = 0; k < 9; k++) {
             T1[k] = ws[k];
@@ -270,8 +326,20 @@ hipError_t launch_nonminimal_h(hipStream_t st, const float4 *pts, const int32_t 
     hipLaunchKernelGGL(k_gather4, dim3((n + 255) / 256), dim3(256), 0, st, pts, idx, n, q);
     hipLaunchKernelGGL(k_normalize, dim3(1), dim3(256), 0, st, q, n, ws);
     const uint32_t nb = (n + kAtaBlock - 1) / kAtaBlock;
-    if (2 * n > 9) hipLaunchKernelGGL(k_ata_partial, dim3(nb), dim3(64), 0, st, q, n, partial);
-    hipLaunchKernelGGL(k_dlt_finish, dim3(1), dim3(64), 0, st, q, n, partial, nb, ws, model_out, ok);
+    if (2 * n > 9) hipLaunchKernelGGL(k_ata_partial<false>, dim3(nb), dim3(64), 0, st, q, n, partial);
+    hipLaunchKernelGGL(k_dlt_finish<false>, dim3(1), dim3(64), 0, st, q, n, partial, nb, ws, model_out, ok);
+    return hipGetLastError();
+}
+
+// FundamentalEstimator::EstimateModelNonMinimalSample -> EightPointsAlgorithm
+// (fundamental_estimator.hpp:65-76, eight_points.cpp:4-100)
+hipError_t launch_nonminimal_f(hipStream_t st, const float4 *pts, const int32_t *idx, uint32_t n, float4 *q,
+                               double *partial, float *ws, float *model_out, int32_t *ok) {
+    hipLaunchKernelGGL(k_gather4, dim3((n + 255) / 256), dim3(256), 0, st, pts, idx, n, q);
+    hipLaunchKernelGGL(k_normalize, dim3(1), dim3(256), 0, st, q, n, ws);
+    const uint32_t nb = (n + kAtaBlock - 1) / kAtaBlock;
+    if (n > 8) hipLaunchKernelGGL(k_ata_partial<true>, dim3(nb), dim3(64), 0, st, q, n, partial);
+    hipLaunchKernelGGL(k_dlt_finish<true>, dim3(1), dim3(64), 0, st, q, n, partial, nb, ws, model_out, ok);
     return hipGetLastError();
 }
 

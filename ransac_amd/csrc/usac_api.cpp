@@ -60,6 +60,8 @@ struct usac_ctx {
     float4 ext = {0, 0, 0, 0};  // dataset box: max |x1|, |y1|, |x2|, |y2| (fast-kernel bounds)
     // batch buffers
     DevBuf samples, models, counts, sums, best, hostmodels, argmax_part;
+    DevBuf list, list_n;    // fundamental: occupied model slots (compacted) and their number
+    uint32_t spk = 1;       // model slots per hypothesis (3 for the 7-point solver)
     // single-model / polish buffers
     DevBuf one_model, inl_idx, inl_cnt, inl_sum, q, partial, ws, nm_model, nm_ok;
     // comm
@@ -94,18 +96,26 @@ int fail(usac_ctx *c, int code, const std::string &msg) {
             return fail((ctx), USAC_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
     } while (0)
 
-bool two_view(const usac_ctx *c) { return c->estimator == USAC_HOMOGRAPHY; }
-int ncomp(const usac_ctx *c) { return c->estimator == USAC_HOMOGRAPHY ? 9 : 3; }
-int ncomp_dev(const usac_ctx *c) { return c->estimator == USAC_HOMOGRAPHY ? 18 : 3; }
+bool is_h(const usac_ctx *c) { return c->estimator == USAC_HOMOGRAPHY; }
+bool is_f(const usac_ctx *c) { return c->estimator == USAC_FUNDAMENTAL; }
+bool two_view(const usac_ctx *c) { return c->cols == 4; }
+int ncomp(const usac_ctx *c) { return two_view(c) ? 9 : 3; }
+int ncomp_dev(const usac_ctx *c) { return is_h(c) ? 18 : ncomp(c); }
 
+// B = hypotheses (minimal samples); every per-model buffer holds B * spk slots
 int ensure_batch(usac_ctx *c, uint32_t B) {
+    const size_t S = (size_t)B * c->spk;
     HIP_TRY(c, c->samples.reserve(sizeof(int32_t) * (size_t)B * c->m));
-    HIP_TRY(c, c->models.reserve(sizeof(float) * (size_t)B * ncomp_dev(c)));
-    HIP_TRY(c, c->counts.reserve(sizeof(int32_t) * (size_t)B));
-    HIP_TRY(c, c->sums.reserve(sizeof(float) * (size_t)B));
+    HIP_TRY(c, c->models.reserve(sizeof(float) * S * ncomp_dev(c)));
+    HIP_TRY(c, c->counts.reserve(sizeof(int32_t) * S));
+    HIP_TRY(c, c->sums.reserve(sizeof(float) * S));
     HIP_TRY(c, c->best.reserve(sizeof(usac_record)));
-    HIP_TRY(c, c->argmax_part.reserve(16 * ((size_t)B / 2048 + 1)));
-    HIP_TRY(c, c->hostmodels.reserve(sizeof(float) * 9 * (size_t)B));
+    HIP_TRY(c, c->argmax_part.reserve(16 * (S / 2048 + 1)));
+    HIP_TRY(c, c->hostmodels.reserve(sizeof(float) * 9 * S));
+    if (is_f(c)) {
+        HIP_TRY(c, c->list.reserve(sizeof(uint32_t) * S));
+        HIP_TRY(c, c->list_n.reserve(sizeof(uint32_t)));
+    }
     return USAC_OK;
 }
 
@@ -125,7 +135,11 @@ int ensure_single(usac_ctx *c) {
 // solve (samples on device, or device RNG when samples_dev == nullptr) into c->models
 hipError_t enqueue_solve(usac_ctx *c, const int32_t *samples_dev, uint32_t B, uint64_t seed, uint64_t first_hyp,
                          int32_t *samples_out) {
-    if (two_view(c))
+    if (is_f(c))
+        return usac::launch_solve_f7(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, seed,
+                                     first_hyp, c->models.as<float>(), c->counts.as<int32_t>(),
+                                     c->list.as<uint32_t>(), c->list_n.as<uint32_t>());
+    if (is_h(c))
         return usac::launch_solve_h4(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, seed,
                                      first_hyp, c->dlt_mode == USAC_DLT_NULLSPACE, c->models.as<float>());
     return usac::launch_solve_line(c->stream, c->pts.as<float2>(), c->n, samples_dev, samples_out, B, seed, first_hyp,
@@ -135,7 +149,11 @@ hipError_t enqueue_solve(usac_ctx *c, const int32_t *samples_dev, uint32_t B, ui
 // chunks == 1 is the parity configuration: per-hypothesis sums are the exact sequential
 // fp32 sums of the reference.  chunks > 1 re-associates Σerr across chunks (counts exact).
 hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
-    if (two_view(c)) {
+    if (is_f(c))  // the occupied slots of the last solve
+        return usac::launch_score_f(c->stream, chunks, c->pts.as<float4>(), c->n, c->models.as<float>(), 3 * (size_t)B,
+                                    c->list.as<uint32_t>(), c->list_n.as<uint32_t>(), 3 * B, thr,
+                                    c->counts.as<int32_t>(), c->sums.as<float>());
+    if (is_h(c)) {
         if (c->score_variant == 1)
             return usac::launch_score_h(c->stream, chunks, c->pts.as<float4>(), c->n, c->models.as<float>(), B, thr,
                                         c->counts.as<int32_t>(), c->sums.as<float>());
@@ -155,7 +173,10 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
 
 // exact single-model inliers into c->inl_idx / inl_cnt / inl_sum (device)
 hipError_t enqueue_inliers(usac_ctx *c, const float *model_dev, float thr) {
-    if (two_view(c))
+    if (is_f(c))
+        return usac::launch_inliers_f(c->stream, c->pts.as<float4>(), c->n, model_dev, thr, c->inl_idx.as<int32_t>(),
+                                      c->inl_cnt.as<int32_t>(), c->inl_sum.as<float>());
+    if (is_h(c))
         return usac::launch_inliers_h(c->stream, c->pts.as<float4>(), c->n, model_dev, thr, c->inl_idx.as<int32_t>(),
                                       c->inl_cnt.as<int32_t>(), c->inl_sum.as<float>());
     return usac::launch_inliers_line(c->stream, c->pts.as<float2>(), c->n, model_dev, thr, c->inl_idx.as<int32_t>(),
@@ -163,7 +184,11 @@ hipError_t enqueue_inliers(usac_ctx *c, const float *model_dev, float thr) {
 }
 
 hipError_t enqueue_nonminimal(usac_ctx *c, const int32_t *idx_dev, uint32_t n) {
-    if (two_view(c))
+    if (is_f(c))
+        return usac::launch_nonminimal_f(c->stream, c->pts.as<float4>(), idx_dev, n, c->q.as<float4>(),
+                                         c->partial.as<double>(), c->ws.as<float>(), c->nm_model.as<float>(),
+                                         c->nm_ok.as<int32_t>());
+    if (is_h(c))
         return usac::launch_nonminimal_h(c->stream, c->pts.as<float4>(), idx_dev, n, c->q.as<float4>(),
                                          c->partial.as<double>(), c->ws.as<float>(), c->nm_model.as<float>(),
                                          c->nm_ok.as<int32_t>());
@@ -188,15 +213,17 @@ int usac_abi_version(void) { return USAC_ABI_VERSION; }
 int usac_create(usac_ctx **out, int device, int estimator, const float *pts, uint32_t n, uint32_t cols) {
     if (!out) return USAC_ERR_ARG;
     *out = nullptr;
-    if (estimator != USAC_LINE2D && estimator != USAC_HOMOGRAPHY) return USAC_ERR_UNSUPPORTED;
-    if ((estimator == USAC_LINE2D && cols != 2) || (estimator == USAC_HOMOGRAPHY && cols != 4)) return USAC_ERR_ARG;
+    if (estimator != USAC_LINE2D && estimator != USAC_HOMOGRAPHY && estimator != USAC_FUNDAMENTAL)
+        return USAC_ERR_UNSUPPORTED;
+    if ((estimator == USAC_LINE2D) != (cols == 2) || (cols != 2 && cols != 4)) return USAC_ERR_ARG;
     if (n == 0 || !pts) return USAC_ERR_ARG;
     usac_ctx *c = new usac_ctx();
     c->device = device;
     c->estimator = estimator;
     c->n = n;
     c->cols = cols;
-    c->m = estimator == USAC_LINE2D ? 2 : 4;
+    c->m = estimator == USAC_LINE2D ? 2 : estimator == USAC_FUNDAMENTAL ? 7 : 4;
+    c->spk = estimator == USAC_FUNDAMENTAL ? 3 : 1;
     int rc = USAC_OK;
     do {
         hipError_t e = hipSetDevice(device);
@@ -238,7 +265,8 @@ void usac_destroy(usac_ctx *c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
-    for (DevBuf *b : {&c->pts, &c->rec, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels, &c->argmax_part, &c->one_model,
+    for (DevBuf *b : {&c->pts, &c->rec, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
+                      &c->argmax_part, &c->list, &c->list_n, &c->one_model,
                       &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok,
                       &c->rec_send, &c->rec_all})
         b->release();
@@ -281,14 +309,24 @@ int usac_estimate_models(usac_ctx *c, const int32_t *samples, uint32_t B, float 
     HIP_TRY(c, hipMemcpyAsync(c->samples.p, samples, sizeof(int32_t) * (size_t)B * c->m, hipMemcpyHostToDevice,
                               c->stream));
     HIP_TRY(c, enqueue_solve(c, c->samples.as<int32_t>(), B, 0, 0, nullptr));
-    std::vector<float> soa((size_t)ncomp(c) * B);
+    const size_t S = (size_t)B * c->spk;
+    std::vector<float> soa((size_t)ncomp(c) * S);
+    std::vector<int32_t> slot_cnt(S, 0);
     HIP_TRY(c, hipMemcpyAsync(soa.data(), c->models.p, sizeof(float) * soa.size(), hipMemcpyDeviceToHost, c->stream));
+    if (c->spk > 1)
+        HIP_TRY(c, hipMemcpyAsync(slot_cnt.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     const int nc = ncomp(c);
-    for (uint32_t h = 0; h < B; h++) {
-        for (int k = 0; k < 9; k++) models[9 * (size_t)h + k] = k < nc ? soa[(size_t)k * B + h] : 0.f;
-        if (n_models) n_models[h] = 1;
+    for (size_t sl = 0; sl < S; sl++) {
+        const bool ok = slot_cnt[sl] >= 0;
+        for (int k = 0; k < 9; k++) models[9 * sl + k] = (k < nc && ok) ? soa[(size_t)k * S + sl] : 0.f;
     }
+    if (n_models)
+        for (uint32_t h = 0; h < B; h++) {
+            int32_t k = 0;
+            for (uint32_t j = 0; j < c->spk; j++) k += slot_cnt[(size_t)h * c->spk + j] >= 0;
+            n_models[h] = k;
+        }
     return USAC_OK;
 }
 
@@ -298,11 +336,17 @@ int usac_score_models(usac_ctx *c, const float *models, uint32_t nm, float thr, 
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipMemcpyAsync(c->hostmodels.p, models, sizeof(float) * 9 * (size_t)nm, hipMemcpyHostToDevice, c->stream));
-    if (two_view(c))
-        HIP_TRY(c, usac::launch_prepare_h(c->stream, c->hostmodels.as<float>(), nm, c->models.as<float>()));
-    else
-        HIP_TRY(c, usac::launch_prepare_line(c->stream, c->hostmodels.as<float>(), nm, c->models.as<float>()));
-    HIP_TRY(c, enqueue_score(c, nm, thr, 1));
+    if (is_f(c)) {
+        HIP_TRY(c, usac::launch_prepare_f(c->stream, c->hostmodels.as<float>(), nm, c->models.as<float>()));
+        HIP_TRY(c, usac::launch_score_f(c->stream, 1, c->pts.as<float4>(), c->n, c->models.as<float>(), nm, nullptr,
+                                        nullptr, nm, thr, c->counts.as<int32_t>(), c->sums.as<float>()));
+    } else {
+        if (is_h(c))
+            HIP_TRY(c, usac::launch_prepare_h(c->stream, c->hostmodels.as<float>(), nm, c->models.as<float>()));
+        else
+            HIP_TRY(c, usac::launch_prepare_line(c->stream, c->hostmodels.as<float>(), nm, c->models.as<float>()));
+        HIP_TRY(c, enqueue_score(c, nm, thr, 1));
+    }
     HIP_TRY(c, hipMemcpyAsync(counts, c->counts.p, sizeof(int32_t) * nm, hipMemcpyDeviceToHost, c->stream));
     if (sums) HIP_TRY(c, hipMemcpyAsync(sums, c->sums.p, sizeof(float) * nm, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -365,10 +409,11 @@ int usac_hypothesize_score(usac_ctx *c, const int32_t *samples, uint32_t B, uint
     // per-hypothesis outputs requested -> exact sequential sums (one chunk)
     const int chunks = (counts || sums) ? 1 : c->chunks;
     HIP_TRY(c, enqueue_score(c, B, thr, chunks));
-    HIP_TRY(c, usac::launch_argmax(c->stream, c->counts.as<int32_t>(), c->sums.as<float>(), B, c->models.as<float>(),
-                                   ncomp(c), first_hyp, c->argmax_part.p, c->best.as<usac_record>()));
-    if (counts) HIP_TRY(c, hipMemcpyAsync(counts, c->counts.p, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
-    if (sums) HIP_TRY(c, hipMemcpyAsync(sums, c->sums.p, sizeof(float) * B, hipMemcpyDeviceToHost, c->stream));
+    const uint32_t S = B * c->spk;
+    HIP_TRY(c, usac::launch_argmax(c->stream, c->counts.as<int32_t>(), c->sums.as<float>(), S, c->models.as<float>(),
+                                   ncomp(c), first_hyp, c->spk, c->argmax_part.p, c->best.as<usac_record>()));
+    if (counts) HIP_TRY(c, hipMemcpyAsync(counts, c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
+    if (sums) HIP_TRY(c, hipMemcpyAsync(sums, c->sums.p, sizeof(float) * S, hipMemcpyDeviceToHost, c->stream));
     if (best) HIP_TRY(c, hipMemcpyAsync(best, c->best.p, sizeof(usac_record), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     return USAC_OK;
@@ -384,8 +429,9 @@ int usac_hypothesize_async(usac_ctx *c, uint32_t B, uint64_t seed, uint64_t firs
     HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
     HIP_TRY(c, enqueue_score(c, B, thr, c->chunks));
     HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
-    HIP_TRY(c, usac::launch_argmax(c->stream, c->counts.as<int32_t>(), c->sums.as<float>(), B, c->models.as<float>(),
-                                   ncomp(c), first_hyp, c->argmax_part.p, c->best.as<usac_record>()));
+    HIP_TRY(c, usac::launch_argmax(c->stream, c->counts.as<int32_t>(), c->sums.as<float>(), B * c->spk,
+                                   c->models.as<float>(), ncomp(c), first_hyp, c->spk, c->argmax_part.p,
+                                   c->best.as<usac_record>()));
     HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
     c->timed_pending = true;
     return USAC_OK;
@@ -453,8 +499,10 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
 
     usac::UniformSampler sampler(prm->seed, c->n, c->m);
     usac::StandardTerminationCriteria term(prm->desired_prob, c->m, c->n, prm->max_iterations);
-    std::vector<int32_t> hs((size_t)batch * c->m), hc(batch);
-    std::vector<float> hsum(batch), hmod((size_t)ncomp(c) * batch);
+    const uint32_t spk = c->spk;
+    const size_t SB = (size_t)batch * spk;  // slot stride of the host copies
+    std::vector<int32_t> hs((size_t)batch * c->m), hc(SB);
+    std::vector<float> hsum(SB), hmod((size_t)ncomp(c) * SB);
     usac::Score best;
     float best_model[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t iters = 0, max_iters = prm->max_iterations;
@@ -467,30 +515,36 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
                                   c->stream));
         HIP_TRY(c, enqueue_solve(c, c->samples.as<int32_t>(), B, 0, iters, nullptr));
         HIP_TRY(c, enqueue_score(c, B, prm->threshold, 1));
-        HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * B, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipMemcpyAsync(hsum.data(), c->sums.p, sizeof(float) * B, hipMemcpyDeviceToHost, c->stream));
+        const size_t S = (size_t)B * spk;
+        HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(hsum.data(), c->sums.p, sizeof(float) * S, hipMemcpyDeviceToHost, c->stream));
         for (int k = 0; k < ncomp(c); k++)
-            HIP_TRY(c, hipMemcpyAsync(hmod.data() + (size_t)k * batch, c->models.as<float>() + (size_t)k * B,
-                                      sizeof(float) * B, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(c, hipMemcpyAsync(hmod.data() + (size_t)k * SB, c->models.as<float>() + (size_t)k * S,
+                                      sizeof(float) * S, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         batches++;
         for (uint32_t j = 0; j < B && iters < max_iters; j++, iters++) {
-            usac::Score cur;
-            cur.inlier_number = hc[j];
-            cur.score = hsum[j];
-            if (cur.bigger(best)) {
-                best = cur;
-                for (int k = 0; k < 9; k++) best_model[k] = k < ncomp(c) ? hmod[(size_t)k * batch + j] : 0.f;
-                max_iters = term.getUpBoundIterations((uint32_t)best.inlier_number);
-                if (records && (uint32_t)nrec < rec_cap) {
-                    usac_record &r = records[nrec];
-                    r.hyp_index = iters;
-                    r.inliers = cur.inlier_number;
-                    r.score = cur.score;
-                    memcpy(r.model, best_model, sizeof(best_model));
-                    r.valid = 1;
+            // the sample's models in solver order (empty slots carry count -1)
+            for (uint32_t q = 0; q < spk; q++) {
+                const size_t sl = (size_t)j * spk + q;
+                if (hc[sl] < 0) break;
+                usac::Score cur;
+                cur.inlier_number = hc[sl];
+                cur.score = hsum[sl];
+                if (cur.bigger(best)) {
+                    best = cur;
+                    for (int k = 0; k < 9; k++) best_model[k] = k < ncomp(c) ? hmod[(size_t)k * SB + sl] : 0.f;
+                    max_iters = term.getUpBoundIterations((uint32_t)best.inlier_number);
+                    if (records && (uint32_t)nrec < rec_cap) {
+                        usac_record &r = records[nrec];
+                        r.hyp_index = iters;
+                        r.inliers = cur.inlier_number;
+                        r.score = cur.score;
+                        memcpy(r.model, best_model, sizeof(best_model));
+                        r.valid = 1;
+                    }
+                    nrec++;
                 }
-                nrec++;
             }
         }
     }

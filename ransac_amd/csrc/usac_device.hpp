@@ -220,6 +220,223 @@ __device__ __forceinline__ void pick_vector(double (&W)[R][9], int nullspace, do
     }
 }
 
+// ---------------------------------------------------------------- fundamental (7-pt / 8-pt)
+// Row of the epipolar system x2^T F x1 = 0 (seven_points.cpp:62-73, eight_points.cpp:26-45):
+// fp32 products, widened to fp64.
+__device__ __forceinline__ void fund_row(float x1, float y1, float x2, float y2, double *r) {
+    r[0] = (double)(x2 * x1); r[1] = (double)(x2 * y1); r[2] = (double)x2;
+    r[3] = (double)(y2 * x1); r[4] = (double)(y2 * y1); r[5] = (double)y2;
+    r[6] = (double)x1; r[7] = (double)y1; r[8] = 1.0;
+}
+
+// The two FULL_UV null-space rows of the 7x9 system (vt rows 7 and 8 of
+// seven_points.cpp:88-90) from the converged Jacobi rows: rows normalised in place (zero
+// rows skipped); vector j starts at the axis least represented by the rows and the
+// earlier vectors (first minimum), two Gram-Schmidt passes (rows, then earlier vectors),
+// normalised as x_k / |x|.  Identical to the oracle's null_complement.
+__device__ __forceinline__ void null_complement7(double (&W)[7][9], double (&N)[2][9]) {
+    double n2[7];
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+        double a = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) a += W[i][k] * W[i][k];
+        n2[i] = a;
+        if (a > 0.0) {
+            const double inv = 1.0 / sqrt(a);
+#pragma unroll
+            for (int k = 0; k < 9; k++) W[i][k] = W[i][k] * inv;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        int ks = 0;
+        double bestc = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            double c = 0.0;
+#pragma unroll
+            for (int i = 0; i < 7; i++)
+                if (n2[i] > 0.0) c += W[i][k] * W[i][k];
+            if (j == 1) c += N[0][k] * N[0][k];
+            if (k == 0 || c < bestc) {
+                bestc = c;
+                ks = k;
+            }
+        }
+        double x[9];
+#pragma unroll
+        for (int k = 0; k < 9; k++) x[k] = (k == ks) ? 1.0 : 0.0;
+#pragma unroll
+        for (int pass = 0; pass < 2; pass++) {
+#pragma unroll
+            for (int i = 0; i < 7; i++) {
+                if (n2[i] > 0.0) {
+                    double d = 0.0;
+#pragma unroll
+                    for (int k = 0; k < 9; k++) d += W[i][k] * x[k];
+#pragma unroll
+                    for (int k = 0; k < 9; k++) x[k] -= d * W[i][k];
+                }
+            }
+            if (j == 1) {
+                double d = 0.0;
+#pragma unroll
+                for (int k = 0; k < 9; k++) d += N[0][k] * x[k];
+#pragma unroll
+                for (int k = 0; k < 9; k++) x[k] -= d * N[0][k];
+            }
+        }
+        double nrm = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) nrm += x[k] * x[k];
+        nrm = sqrt(nrm);
+#pragma unroll
+        for (int k = 0; k < 9; k++) N[j][k] = x[k] / nrm;
+    }
+}
+
+// Real roots of c0 x^3 + c1 x^2 + c2 x + c3 (the contract of cv::solveCubic,
+// seven_points.cpp:131) with IEEE basic operations only -- monic form, Cauchy bound,
+// critical-point brackets, bisection.  Identical to the oracle's cubic_roots.
+__device__ __forceinline__ double cubic_eval(double a, double b, double c, double x) {
+    return ((x + a) * x + b) * x + c;
+}
+
+__device__ __noinline__ double cubic_bisect(double a, double b, double c, double lo, double hi) {
+    double flo = cubic_eval(a, b, c, lo);
+    for (int it = 0; it < 200; it++) {
+        const double mid = 0.5 * (lo + hi);
+        if (!(mid > lo && mid < hi)) break;
+        const double fm = cubic_eval(a, b, c, mid);
+        if (fm == 0.0) return mid;
+        if ((fm < 0.0) == (flo < 0.0)) {
+            lo = mid;
+            flo = fm;
+        } else {
+            hi = mid;
+        }
+    }
+    return 0.5 * (lo + hi);
+}
+
+__device__ __forceinline__ int cubic_roots(double c0, double c1, double c2, double c3, double *r) {
+    if (c0 == 0.0) {
+        if (c1 == 0.0) {
+            if (c2 == 0.0) return 0;
+            r[0] = -c3 / c2;
+            return 1;
+        }
+        const double D = c2 * c2 - 4.0 * c1 * c3;
+        if (D < 0.0) return 0;
+        if (D == 0.0) {
+            r[0] = -c2 / (2.0 * c1);
+            return 1;
+        }
+        const double s = sqrt(D);
+        const double q = -0.5 * (c2 + (c2 >= 0.0 ? s : -s));
+        const double x1 = q / c1, x2 = c3 / q;
+        r[0] = x1 < x2 ? x1 : x2;
+        r[1] = x1 < x2 ? x2 : x1;
+        return 2;
+    }
+    const double a = c1 / c0, b = c2 / c0, c = c3 / c0;
+    double R = fabs(a);
+    if (fabs(b) > R) R = fabs(b);
+    if (fabs(c) > R) R = fabs(c);
+    R = R + 1.0;
+    const double D = a * a - 3.0 * b;
+    int n = 0;
+    if (!(D > 0.0)) {
+        r[n++] = cubic_bisect(a, b, c, -R, R);
+        return n;
+    }
+    const double s = sqrt(D);
+    const double m1 = (-a - s) / 3.0, m2 = (-a + s) / 3.0;
+    const double v1 = cubic_eval(a, b, c, m1), v2 = cubic_eval(a, b, c, m2);
+    if (v1 >= 0.0) r[n++] = cubic_bisect(a, b, c, -R, m1);
+    if (v1 > 0.0 && v2 < 0.0) r[n++] = cubic_bisect(a, b, c, m1, m2);
+    if (v2 <= 0.0) r[n++] = cubic_bisect(a, b, c, m2, R);
+    return n;
+}
+
+// det(f1 + lambda f2)-style cubic coefficients exactly as seven_points.cpp:98-128 (fp32,
+// left to right), after f1 -= f2.
+__device__ __forceinline__ void fund_cubic(float (&f1)[9], const float (&f2)[9], float (&c)[4]) {
+#pragma unroll
+    for (int i = 0; i < 9; i++) f1[i] -= f2[i];
+    float t0 = f2[4] * f2[8] - f2[5] * f2[7];
+    float t1 = f2[3] * f2[8] - f2[5] * f2[6];
+    float t2 = f2[3] * f2[7] - f2[4] * f2[6];
+    c[3] = f2[0] * t0 - f2[1] * t1 + f2[2] * t2;
+    c[2] = f1[0] * t0 - f1[1] * t1 + f1[2] * t2 - f1[3] * (f2[1] * f2[8] - f2[2] * f2[7]) +
+           f1[4] * (f2[0] * f2[8] - f2[2] * f2[6]) - f1[5] * (f2[0] * f2[7] - f2[1] * f2[6]) +
+           f1[6] * (f2[1] * f2[5] - f2[2] * f2[4]) - f1[7] * (f2[0] * f2[5] - f2[2] * f2[3]) +
+           f1[8] * (f2[0] * f2[4] - f2[1] * f2[3]);
+    t0 = f1[4] * f1[8] - f1[5] * f1[7];
+    t1 = f1[3] * f1[8] - f1[5] * f1[6];
+    t2 = f1[3] * f1[7] - f1[4] * f1[6];
+    c[1] = f2[0] * t0 - f2[1] * t1 + f2[2] * t2 - f2[3] * (f1[1] * f1[8] - f1[2] * f1[7]) +
+           f2[4] * (f1[0] * f1[8] - f1[2] * f1[6]) - f2[5] * (f1[0] * f1[7] - f1[1] * f1[6]) +
+           f2[6] * (f1[1] * f1[5] - f1[2] * f1[4]) - f2[7] * (f1[0] * f1[5] - f1[2] * f1[3]) +
+           f2[8] * (f1[0] * f1[4] - f1[1] * f1[3]);
+    c[0] = f1[0] * t0 - f1[1] * t1 + f1[2] * t2;
+}
+
+// F for one cubic root (seven_points.cpp:138-154, fp32)
+__device__ __forceinline__ void fund_from_root(const float (&f1)[9], const float (&f2)[9], float r, float (&F)[9]) {
+    float lambda = r, mu = 1.f;
+    const float s = f1[8] * r + f2[8];
+    if ((double)fabsf(s) > 2.220446049250313e-16) {
+        mu = 1.f / s;
+        lambda *= mu;
+        F[8] = 1.f;
+    } else {
+        F[8] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) F[i] = f1[i] * lambda + f2[i] * mu;
+}
+
+// Oriented epipolar constraint (fundamental_estimator.hpp:189-231), fp32: epipole
+// row0 x row2 (row1 x row2 when every |e_i| <= 1.9984e-15), sign of
+// (F0 x2 + F3 y2 + F6)(e1 - e2 y1) consistent over the sample.
+__device__ __forceinline__ bool fund_oriented(const float (&F)[9], const float4 *__restrict__ pts,
+                                              const int32_t (&smp)[7]) {
+    float e1 = F[2] * F[6] - F[0] * F[8];
+    float e2 = F[0] * F[7] - F[1] * F[6];
+    const float e0 = F[1] * F[8] - F[2] * F[7];
+    const bool big = (e0 > 1.9984e-15 || e0 < -1.9984e-15) || (e1 > 1.9984e-15 || e1 < -1.9984e-15) ||
+                     (e2 > 1.9984e-15 || e2 < -1.9984e-15);
+    if (!big) {
+        e1 = F[5] * F[6] - F[3] * F[8];
+        e2 = F[3] * F[7] - F[4] * F[6];
+    }
+    float sig1 = 0.f;
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+        const float4 P = pts[smp[i]];
+        const float s1 = F[0] * P.z + F[3] * P.w + F[6];
+        const float s2 = e1 - e2 * P.y;
+        const float sig = s1 * s2;
+        if (i == 0) sig1 = sig;
+        else ok = ok && !(sig1 * sig < 0);
+    }
+    return ok;
+}
+
+// FundamentalEstimator::GetError (fundamental_estimator.hpp:101-134): Sampson distance,
+// fp32 left to right, one IEEE division.
+__device__ __forceinline__ float fundamental_error(const float *f, float x1, float y1, float x2, float y2) {
+    const float Fx = f[0] * x1 + f[1] * y1 + f[2];
+    const float Fy = f[3] * x1 + f[4] * y1 + f[5];
+    const float Gx = f[0] * x2 + f[3] * y2 + f[6];
+    const float Gy = f[1] * x2 + f[4] * y2 + f[7];
+    const float s = x2 * Fx + y2 * Fy + f[6] * x1 + f[7] * y1 + f[8];
+    return (s * s) / (Fx * Fx + Fy * Fy + Gx * Gx + Gy * Gy);
+}
+
 // ---------------------------------------------------------------- residuals
 // HomographyEstimator::GetError (homography_estimator.hpp:85-110): fp32 projections
 // evaluated left to right, IEEE divisions, the two distances are double square roots

@@ -27,9 +27,25 @@ hipError_t launch_prepare_line(hipStream_t st, const float *in, uint32_t B, floa
 hipError_t launch_score_line(hipStream_t st, int chunks, const float2 *pts, uint32_t n, const float *models,
                              uint32_t B, float thr, int32_t *counts, float *sums);
 
+// B = number of model slots; hyp_index = first_hyp + slot / spk (spk = slots per hypothesis)
 hipError_t launch_argmax(hipStream_t st, const int32_t *counts, const float *sums, uint32_t B, const float *models,
-                         int ncomp, uint64_t first_hyp, void *scratch /* 12 B x ceil(B/2048) */,
+                         int ncomp, uint64_t first_hyp, uint32_t spk, void *scratch /* 12 B x ceil(B/2048) */,
                          usac_record *out);
+
+// fundamental (kernels_fund.hip): slots 3*b + j, counts -1 on empty slots, list/list_n =
+// occupied slots (list_n zeroed by the launcher)
+hipError_t launch_solve_f7(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
+                           int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, float *models,
+                           int32_t *counts, uint32_t *list, uint32_t *list_n);
+hipError_t launch_prepare_f(hipStream_t st, const float *in, uint32_t K, float *models);
+// list == nullptr: lanes = slots 0..kmax-1; else lanes walk list[0 .. *list_n) (<= kmax)
+hipError_t launch_score_f(hipStream_t st, int chunks, const float4 *pts, uint32_t n, const float *models,
+                          size_t stride, const uint32_t *list, const uint32_t *list_n, uint32_t kmax, float thr,
+                          int32_t *counts, float *sums);
+hipError_t launch_inliers_f(hipStream_t st, const float4 *pts, uint32_t n, const float *model, float thr,
+                            int32_t *idx, int32_t *count, float *sum);
+hipError_t launch_nonminimal_f(hipStream_t st, const float4 *pts, const int32_t *idx, uint32_t n, float4 *q,
+                               double *partial, float *ws, float *model_out, int32_t *ok);
 
 hipError_t launch_inliers_h(hipStream_t st, const float4 *pts, uint32_t n, const float *model, float thr,
                             int32_t *idx, int32_t *count, float *sum);

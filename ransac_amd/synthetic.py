@@ -58,3 +58,65 @@ def line_points(n=1000, inlier_ratio=0.1, seed=1, noise=3.0, size=1000.0):
     pts = np.concatenate([np.stack([xs, ys], 1), out], 0)
     perm = rng.permutation(n)
     return np.ascontiguousarray(pts[perm], dtype=np.float32), np.array([nx, ny, c], dtype=np.float32)
+
+
+def _rot_y(deg):
+    a = np.deg2rad(deg)
+    return np.array([[np.cos(a), 0.0, np.sin(a)], [0.0, 1.0, 0.0], [-np.sin(a), 0.0, np.cos(a)]])
+
+
+def _skew(t):
+    return np.array([[0.0, -t[2], t[1]], [t[2], 0.0, -t[0]], [-t[1], t[0], 0.0]])
+
+
+def two_view_geometry():
+    """cfg3/cfg4 cameras: K = [[1000,0,500],[0,1000,500],[0,0,1]], cam1 = K[I|0],
+    cam2 = K[R|t] with R = rotY(10 deg), t = (200, 0, 20).  Returns (K, R, t, E, F) with
+    F = K^-T [t]x R K^-1 scaled so F33 = 1 and E = [t]x R / |t|."""
+    K = np.array([[1000.0, 0.0, 500.0], [0.0, 1000.0, 500.0], [0.0, 0.0, 1.0]])
+    R = _rot_y(10.0)
+    t = np.array([200.0, 0.0, 20.0])
+    E = _skew(t) @ R
+    Ki = np.linalg.inv(K)
+    F = Ki.T @ E @ Ki
+    return K, R, t, E / np.linalg.norm(t), F / F[2, 2]
+
+
+def fundamental_points(n=10000, inlier_ratio=0.3, seed=1, noise=0.5, size=1000.0, prosac_order=True,
+                       normalized=False):
+    """cfg3 (and cfg4 with normalized=True): N x 4 fp32 [x1 y1 x2 y2].
+
+    X ~ U([-500,500]^2 x [1000,3000]) projected through both cameras + N(0, noise^2) px;
+    outliers uniform in both images.  With prosac_order the rows are sorted by the PROSAC
+    quality q = U(0,1) + 0.5 [inlier], descending; otherwise a random
+    permutation.  normalized=True returns K^-1 x (calibrated coordinates, cfg4).
+    Returns (points, F_gt (or E_gt when normalized), is_inlier)."""
+    rng = np.random.default_rng(seed)
+    K, R, t, E, F = two_view_geometry()
+    n_in = int(round(n * inlier_ratio))
+    X = np.stack([rng.uniform(-500, 500, n_in), rng.uniform(-500, 500, n_in), rng.uniform(1000, 3000, n_in)], 1)
+    p1 = X @ K.T
+    x1 = p1[:, :2] / p1[:, 2:3]
+    p2 = (X @ R.T + t) @ K.T
+    x2 = p2[:, :2] / p2[:, 2:3]
+    x1 = x1 + rng.normal(0.0, noise, size=x1.shape)
+    x2 = x2 + rng.normal(0.0, noise, size=x2.shape)
+    o1 = rng.uniform(0.0, size, size=(n - n_in, 2))
+    o2 = rng.uniform(0.0, size, size=(n - n_in, 2))
+    pts = np.concatenate([np.concatenate([x1, x2], 1), np.concatenate([o1, o2], 1)], 0)
+    inl = np.zeros(n, dtype=bool)
+    inl[:n_in] = True
+    if prosac_order:
+        q = rng.uniform(0.0, 1.0, n) + 0.5 * inl
+        order = np.argsort(-q, kind="stable")
+    else:
+        order = rng.permutation(n)
+    pts, inl = pts[order], inl[order]
+    model = F
+    if normalized:
+        Ki = np.linalg.inv(K)
+        h1 = np.c_[pts[:, :2], np.ones(n)] @ Ki.T
+        h2 = np.c_[pts[:, 2:], np.ones(n)] @ Ki.T
+        pts = np.concatenate([h1[:, :2], h2[:, :2]], 1)
+        model = E
+    return np.ascontiguousarray(pts, dtype=np.float32), model.astype(np.float32), inl

@@ -41,3 +41,9 @@ def usac():
     import ransac_amd
     ransac_amd.lib()
     return ransac_amd
+
+
+@pytest.fixture(scope="session")
+def kusvod2_scenes():
+    z = np.load(os.path.join(GOLDEN, "kusvod2_scenes.npz"))
+    return {k[:-4]: (z[k], z[k[:-4] + "_model"]) for k in z.files if k.endswith("_pts")}
