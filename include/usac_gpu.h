@@ -26,6 +26,8 @@
  *                                  batch (the body of ransac.cpp:58-139)
  *   usac_std_termination           StandardTerminationCriteria::getUpBoundIterations
  *                                  (standard_termination_criteria.hpp:52-62)
+ *   usac_prosac_samples            ProsacSampler::generateSample (prosac_sampler.hpp:117-172)
+ *   usac_sprt_pool                 SPRT ctor pool + A0 (sprt.hpp:89-175)
  *   usac_ransac_run                Ransac::run + RansacOutput (ransac.cpp:14-238,
  *                                  ransac_output.hpp:29-97), Uniform sampler
  *   usac_comm_*                    new: one RCCL all-gather of best records per batch
@@ -43,12 +45,12 @@
 extern "C" {
 #endif
 
-#define USAC_ABI_VERSION 1
+#define USAC_ABI_VERSION 2
 
 /* = enum ESTIMATOR (usac/model.hpp:10) */
 enum { USAC_LINE2D = 1, USAC_HOMOGRAPHY = 2, USAC_FUNDAMENTAL = 3, USAC_ESSENTIAL = 4 };
-/* = enum SAMPLER (usac/model.hpp:11); only Uniform in ABI v1 */
-enum { USAC_SAMPLER_UNIFORM = 1 };
+/* = enum SAMPLER (usac/model.hpp:11); Uniform and Prosac in ABI v2 */
+enum { USAC_SAMPLER_UNIFORM = 1, USAC_SAMPLER_PROSAC = 4 };
 /* 4-pt DLT: THIN = reference semantics (vt.row(7) of the thin 8x9 SVD, dlt.cpp:43-48);
  * NULLSPACE = true null vector. */
 enum { USAC_DLT_THIN = 0, USAC_DLT_NULLSPACE = 1 };
@@ -73,14 +75,17 @@ typedef struct usac_record {
     int32_t valid;
 } usac_record;
 
-/* Model (usac/model.hpp:15-45) fields the Uniform/no-LO/no-SPRT loop reads. */
+/* Model (usac/model.hpp:15-45) fields the loop reads. */
 typedef struct usac_params {
     float threshold;            /* model.hpp:17 (default 2) */
     float desired_prob;         /* model.hpp:18 (0.95) */
     uint32_t max_iterations;    /* model.hpp:22 (10000) */
-    uint32_t seed;              /* glibc srandom(seed): ResetRandomGenerator(false) semantics */
+    uint32_t seed;              /* glibc srandom(seed): ResetRandomGenerator(false) semantics;
+                                   also seeds PROSAC's mt19937 (the reference uses random_device) */
     int32_t dlt_mode;           /* USAC_DLT_* */
     uint32_t batch;             /* hypotheses per device batch (0 = default) */
+    int32_t sampler;            /* USAC_SAMPLER_UNIFORM | USAC_SAMPLER_PROSAC (points sorted by quality) */
+    int32_t sprt;               /* Model::setSprt (model.hpp:104): SPRT verification, sprt.hpp */
 } usac_params;
 
 /* RansacOutput getters (ransac_output.hpp:57-97) */
@@ -94,6 +99,10 @@ typedef struct usac_run_output {
     float minimal_model[9];     /* best model before the non-minimal polish */
     int32_t minimal_inliers;
     uint32_t batches;           /* device batches launched */
+    int32_t sprt_rejected;      /* models rejected by SPRT */
+    int32_t sprt_histories;     /* SPRT tests designed (sprt_histories.size()) */
+    uint32_t prosac_term_len;   /* final PROSAC termination_length (n without PROSAC) */
+    uint32_t rollbacks;         /* PROSAC speculative batches cut short by a termination_length change */
 } usac_run_output;
 
 /* ---- lifetime ----------------------------------------------------------------- */
@@ -146,14 +155,23 @@ int usac_set_score_variant(usac_ctx *ctx, int variant);
 /* ---- loop --------------------------------------------------------------------- */
 uint32_t usac_std_termination(uint32_t inliers, uint32_t points_size, uint32_t sample_size, float desired_prob,
                               uint32_t max_iterations);
-/* Ransac::run with the Uniform sampler (glibc random() stream), no LO / SPRT.
- * inliers_out (capacity n, nullable): final inliers ascending.  records (nullable,
- * capacity rec_cap): best-score updates in loop order (hyp_index = iteration). */
+/* Ransac::run (ransac.cpp:14-238) with the Uniform (glibc random() stream) or PROSAC
+ * (prosac_sampler.hpp + prosac_termination_criteria.hpp) sampler, optional SPRT
+ * (sprt.hpp; pool shuffle from the same glibc stream), no LO.  inliers_out (capacity n,
+ * nullable): final inliers ascending.  records (nullable, capacity rec_cap): best-score
+ * updates in loop order (hyp_index = iteration, SPRT double counting included). */
 int usac_ransac_run(usac_ctx *ctx, const usac_params *params, usac_run_output *out, int32_t *inliers_out,
                     usac_record *records, uint32_t rec_cap);
 /* Host glibc-compatible UniformSampler stream (uniform_sampler.hpp:42-54): count x m
  * samples after srandom(seed).  Exposed for parity tests. */
 int usac_uniform_samples(uint32_t seed, uint32_t n_points, uint32_t m, uint32_t count, int32_t *out);
+/* Host ProsacSampler stream (prosac_sampler.hpp:117-172), mt19937 seeded with `seed`,
+ * termination_length held at `termination_length`: count x m samples.  For parity tests. */
+int usac_prosac_samples(uint32_t seed, uint32_t n_points, uint32_t m, uint32_t count, uint32_t termination_length,
+                        int32_t *out);
+/* SPRT random pool after srandom(seed) (sprt.hpp:89-104; n_points glibc draws) and the
+ * first test's threshold A (sprt.hpp:332-355) for `estimator`.  For parity tests. */
+int usac_sprt_pool(uint32_t seed, int estimator, uint32_t n_points, uint32_t m, uint32_t *pool, double *A0);
 
 /* ---- multi-GPU (RCCL over xGMI) --------------------------------------------------- */
 /* 128-byte RCCL unique id (rank 0 creates, everyone receives it out of band). */

@@ -30,7 +30,22 @@ class OrcResult(ctypes.Structure):
         ("polish_passes", ctypes.c_int),
         ("minimal_model", ctypes.c_float * 9),
         ("minimal_inliers", ctypes.c_int),
+        ("sprt_rejected", ctypes.c_int),
+        ("sprt_histories", ctypes.c_int),
+        ("prosac_term_len", ctypes.c_uint),
     ]
+
+
+SAMPLER_UNIFORM, SAMPLER_NAPSAC, SAMPLER_PROSAC = 1, 3, 4  # usac/model.hpp:11
+
+
+class OrcConfig(ctypes.Structure):
+    _fields_ = [("threshold", ctypes.c_float), ("desired_prob", ctypes.c_float), ("max_iterations", ctypes.c_uint),
+                ("seed", ctypes.c_uint), ("dlt_mode", ctypes.c_int), ("sampler", ctypes.c_int), ("sprt", ctypes.c_int)]
+
+
+class OrcMT(ctypes.Structure):
+    _fields_ = [("mt", ctypes.c_uint32 * 624), ("i", ctypes.c_int)]
 
 
 def build():
@@ -72,6 +87,38 @@ def lib():
         L.orc_ransac_run.argtypes = [ctypes.c_int, _f32p, ctypes.c_uint, ctypes.c_float, ctypes.c_float,
                                      ctypes.c_uint, ctypes.c_uint, ctypes.c_int, ctypes.POINTER(OrcResult),
                                      _i32p, _u32p, _i32p, _f32p, ctypes.c_int]
+        L.orc_ransac_run_cfg.argtypes = [ctypes.c_int, _f32p, ctypes.c_uint, ctypes.POINTER(OrcConfig),
+                                         ctypes.POINTER(OrcResult), _i32p, _u32p, _i32p, _f32p, ctypes.c_int]
+        L.orc_mt_seed.argtypes = [ctypes.POINTER(OrcMT), ctypes.c_uint32]
+        L.orc_mt_next.argtypes = [ctypes.POINTER(OrcMT)]
+        L.orc_mt_next.restype = ctypes.c_uint32
+        L.orc_mt_uniform.argtypes = [ctypes.POINTER(OrcMT), ctypes.c_uint]
+        L.orc_prosac_new.restype = ctypes.c_void_p
+        L.orc_prosac_new.argtypes = [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint32]
+        L.orc_prosac_free.argtypes = [ctypes.c_void_p]
+        L.orc_prosac_growth.argtypes = [ctypes.c_void_p]
+        L.orc_prosac_growth.restype = _u32p
+        L.orc_prosac_largest.argtypes = [ctypes.c_void_p]
+        L.orc_prosac_largest.restype = ctypes.c_uint
+        L.orc_prosac_set_term_len.argtypes = [ctypes.c_void_p, ctypes.c_uint]
+        L.orc_prosac_sample.argtypes = [ctypes.c_void_p, _i32p]
+        L.orc_prosac_term_new.restype = ctypes.c_void_p
+        L.orc_prosac_term_new.argtypes = [_u32p, ctypes.c_uint, ctypes.c_uint, ctypes.c_float, ctypes.c_uint]
+        L.orc_prosac_term_free.argtypes = [ctypes.c_void_p]
+        L.orc_prosac_term_length.argtypes = [ctypes.c_void_p]
+        L.orc_prosac_term_length.restype = ctypes.c_uint
+        L.orc_prosac_term_update.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.POINTER(ctypes.c_uint8),
+                                             ctypes.c_uint]
+        L.orc_prosac_term_update.restype = ctypes.c_uint
+        L.orc_sprt_new.restype = ctypes.c_void_p
+        L.orc_sprt_new.argtypes = [ctypes.c_int, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, ctypes.c_int]
+        L.orc_sprt_free.argtypes = [ctypes.c_void_p]
+        L.orc_sprt_pool.argtypes = [ctypes.c_void_p]
+        L.orc_sprt_pool.restype = _u32p
+        L.orc_sprt_A.argtypes = [ctypes.c_void_p]
+        L.orc_sprt_A.restype = ctypes.c_double
+        L.orc_sprt_upper_bound.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.orc_sprt_upper_bound.restype = ctypes.c_uint
         L.orc_hypothesis_loop.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_float, _f32p]
         L.orc_generate_line2d.argtypes = [ctypes.c_uint, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, _f32p, _f32p]
@@ -197,7 +244,8 @@ def std_termination(inliers, n, m, p, max_iters=10000):
     return lib().orc_std_termination(inliers, n, m, ctypes.c_float(p), max_iters)
 
 
-def ransac_run(kind, points, thr, p, seed, max_iters=10000, dlt_mode=DLT_THIN, rec_cap=4096):
+def ransac_run(kind, points, thr, p, seed, max_iters=10000, dlt_mode=DLT_THIN, rec_cap=4096,
+               sampler=SAMPLER_UNIFORM, sprt=False):
     points = np.ascontiguousarray(points, dtype=np.float32)
     n = points.shape[0]
     res = OrcResult()
@@ -205,9 +253,9 @@ def ransac_run(kind, points, thr, p, seed, max_iters=10000, dlt_mode=DLT_THIN, r
     ri = np.zeros(rec_cap, dtype=np.uint32)
     rc = np.zeros(rec_cap, dtype=np.int32)
     rs = np.zeros(rec_cap, dtype=np.float32)
-    ret = lib().orc_ransac_run(kind, _p(points, _f32p), n, ctypes.c_float(thr), ctypes.c_float(p), max_iters,
-                               seed, dlt_mode, ctypes.byref(res), _p(inl, _i32p), _p(ri, _u32p), _p(rc, _i32p),
-                               _p(rs, _f32p), rec_cap)
+    cfg = OrcConfig(thr, p, max_iters, seed, dlt_mode, sampler, 1 if sprt else 0)
+    ret = lib().orc_ransac_run_cfg(kind, _p(points, _f32p), n, ctypes.byref(cfg), ctypes.byref(res), _p(inl, _i32p),
+                                   _p(ri, _u32p), _p(rc, _i32p), _p(rs, _f32p), rec_cap)
     k = min(res.n_records, rec_cap)
     return {
         "ret": ret,
@@ -219,7 +267,48 @@ def ransac_run(kind, points, thr, p, seed, max_iters=10000, dlt_mode=DLT_THIN, r
         "minimal_inliers": res.minimal_inliers,
         "inlier_idx": inl[: res.inliers].copy() if ret == 0 else np.zeros(0, np.int32),
         "records": list(zip(ri[:k].tolist(), rc[:k].tolist(), rs[:k].tolist())),
+        "sprt_rejected": res.sprt_rejected,
+        "sprt_histories": res.sprt_histories,
+        "prosac_term_len": res.prosac_term_len,
     }
+
+
+def mt19937_stream(seed, count):
+    g = OrcMT()
+    lib().orc_mt_seed(ctypes.byref(g), seed)
+    return np.array([lib().orc_mt_next(ctypes.byref(g)) for _ in range(count)], dtype=np.uint64)
+
+
+def mt19937_uniform(seed, max_, count):
+    g = OrcMT()
+    lib().orc_mt_seed(ctypes.byref(g), seed)
+    return np.array([lib().orc_mt_uniform(ctypes.byref(g), max_) for _ in range(count)], dtype=np.int64)
+
+
+def prosac_samples(seed, n_points, m, count, term_len=None):
+    """ProsacSampler stream (termination_length fixed at term_len, default n): count x m."""
+    L = lib()
+    p = L.orc_prosac_new(m, n_points, seed)
+    if term_len is not None:
+        L.orc_prosac_set_term_len(p, term_len)
+    out = np.zeros((count, m), dtype=np.int32)
+    for i in range(count):
+        L.orc_prosac_sample(p, _p(out[i], _i32p))
+    growth = np.ctypeslib.as_array(L.orc_prosac_growth(p), shape=(n_points,)).copy()
+    largest = L.orc_prosac_largest(p)
+    L.orc_prosac_free(p)
+    return out, growth, largest
+
+
+def sprt_pool(seed, kind, n_points, m, max_iters=10000):
+    """The SPRT random pool after srandom(seed) (consumes n_points glibc draws) and A_0."""
+    L = lib()
+    L.orc_srandom(ctypes.c_uint(seed))
+    s = L.orc_sprt_new(kind, n_points, m, max_iters, 20)
+    pool = np.ctypeslib.as_array(L.orc_sprt_pool(s), shape=(n_points,)).copy()
+    A = L.orc_sprt_A(s)
+    L.orc_sprt_free(s)
+    return pool, A
 
 
 def hypothesis_loop(kind, points, thr, seed, count, dlt_mode=DLT_THIN):

@@ -909,6 +909,392 @@ unsigned int orc_std_termination(unsigned int inliers, unsigned int points_size,
     return (unsigned int)r;
 }
 
+/* ------------------------------------------------------------ mt19937 / PROSAC */
+/* std::mt19937 (the PROSAC generator, uniform_random_generator.hpp:16-26).  The reference
+ * seeds it from std::random_device (non-reproducible); this build seeds it with the run
+ * seed.  uniform_int_distribution<int>(0, max) is restated as libstdc++'s classic
+ * downscaling (GCC <= 10, the toolchain of the reference's era): scaling = 0xFFFFFFFF /
+ * (max + 1), reject r >= (max + 1) * scaling, return r / scaling. */
+void orc_mt_seed(orc_mt *g, uint32_t seed) {
+    g->mt[0] = seed;
+    for (int i = 1; i < 624; i++) g->mt[i] = 1812433253u * (g->mt[i - 1] ^ (g->mt[i - 1] >> 30)) + (uint32_t)i;
+    g->i = 624;
+}
+
+uint32_t orc_mt_next(orc_mt *g) {
+    if (g->i >= 624) {
+        for (int k = 0; k < 624; k++) {
+            uint32_t y = (g->mt[k] & 0x80000000u) | (g->mt[(k + 1) % 624] & 0x7fffffffu);
+            g->mt[k] = g->mt[(k + 397) % 624] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        g->i = 0;
+    }
+    uint32_t y = g->mt[g->i++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+int orc_mt_uniform(orc_mt *g, unsigned int max) {
+    const uint64_t urngrange = 0xFFFFFFFFull, urange = (uint64_t)max;
+    if (urange == urngrange) return (int)orc_mt_next(g);
+    const uint64_t uerange = urange + 1, scaling = urngrange / uerange, past = uerange * scaling;
+    uint64_t r;
+    do {
+        r = orc_mt_next(g);
+    } while (r >= past);
+    return (int)(r / scaling);
+}
+
+/* UniformRandomGenerator::generateUniqueRandomSet(sample, k, max): closed <0; max>,
+ * redraw on a repeat (uniform_random_generator.hpp:44-54) */
+static void mt_unique_set(orc_mt *g, int *sample, unsigned int k, unsigned int max) {
+    for (unsigned int i = 0; i < k; i++) {
+        sample[i] = orc_mt_uniform(g, max);
+        for (int j = (int)i - 1; j >= 0; j--) {
+            if (sample[i] == sample[j]) {
+                i--;
+                break;
+            }
+        }
+    }
+}
+
+struct orc_prosac {
+    orc_mt g;
+    unsigned int *growth;
+    unsigned int subset, largest, hyp, m, n, growth_max;
+    unsigned int term_len; /* = ProsacTerminationCriteria::termination_length (shared pointer) */
+};
+
+/* ProsacSampler::initProsacSampler (prosac_sampler.hpp:62-114) */
+orc_prosac *orc_prosac_new(unsigned int sample_size, unsigned int points_size, uint32_t seed) {
+    orc_prosac *p = (orc_prosac *)calloc(1, sizeof(*p));
+    p->m = sample_size;
+    p->n = points_size;
+    p->growth_max = 200000;
+    orc_mt_seed(&p->g, seed);
+    p->growth = (unsigned int *)malloc(sizeof(unsigned int) * points_size);
+    double T_n = p->growth_max;
+    for (unsigned int i = 0; i < sample_size; ++i) T_n *= (double)(sample_size - i) / (points_size - i);
+    unsigned int T_n_prime = 1;
+    for (unsigned int i = 0; i < points_size; ++i) {
+        if (i + 1 <= sample_size) {
+            p->growth[i] = T_n_prime;
+            continue;
+        }
+        double Tn_plus1 = (double)(i + 1) * T_n / (i + 1 - sample_size);
+        p->growth[i] = T_n_prime + (unsigned int)ceil(Tn_plus1 - T_n);
+        T_n = Tn_plus1;
+        T_n_prime = p->growth[i];
+    }
+    p->largest = sample_size;
+    p->subset = sample_size;
+    p->hyp = 1;
+    p->term_len = points_size;
+    return p;
+}
+
+void orc_prosac_free(orc_prosac *p) {
+    if (!p) return;
+    free(p->growth);
+    free(p);
+}
+
+const unsigned int *orc_prosac_growth(const orc_prosac *p) { return p->growth; }
+unsigned int orc_prosac_largest(const orc_prosac *p) { return p->largest; }
+void orc_prosac_set_term_len(orc_prosac *p, unsigned int t) { p->term_len = t; }
+
+/* ProsacSampler::generateSample (prosac_sampler.hpp:117-172).  Reference quirks kept:
+ * both uniform fall-backs draw from the CLOSED range <0; max>. */
+void orc_prosac_sample(orc_prosac *p, int *sample) {
+    if (p->hyp > p->growth_max) {
+        mt_unique_set(&p->g, sample, p->m, p->n);
+        return;
+    }
+    if (p->subset > p->term_len) {
+        mt_unique_set(&p->g, sample, p->m, p->term_len);
+        return;
+    }
+    if (p->hyp > p->growth[p->subset - 1]) {
+        ++p->subset;
+        if (p->subset > p->n) p->subset = p->n;
+        if (p->largest < p->subset) p->largest = p->subset;
+    }
+    mt_unique_set(&p->g, sample, p->m - 1, p->subset - 2);
+    sample[p->m - 1] = (int)p->subset - 1;
+    p->hyp++;
+}
+
+struct orc_prosac_term {
+    unsigned int *maximality, *non_random;
+    const unsigned int *growth;
+    unsigned int term_len, n, m, max_iters;
+    float desired_prob;
+};
+
+/* ProsacTerminationCriteria ctor (prosac_termination_criteria.hpp:44-119) */
+orc_prosac_term *orc_prosac_term_new(const unsigned int *growth, unsigned int points_size, unsigned int sample_size,
+                                     float desired_prob, unsigned int max_iterations) {
+    orc_prosac_term *t = (orc_prosac_term *)calloc(1, sizeof(*t));
+    t->growth = growth;
+    t->n = points_size;
+    t->m = sample_size;
+    t->max_iters = max_iterations;
+    t->desired_prob = desired_prob;
+    t->term_len = points_size;
+    const float non_randomness = 0.95f, beta = 0.05f;
+    t->non_random = (unsigned int *)calloc(points_size, sizeof(unsigned int));
+    double *pn = (double *)malloc(sizeof(double) * points_size);
+    for (size_t n = sample_size + 1; n <= points_size; ++n) {
+        if (n - 1 > 1000) {
+            t->non_random[n - 1] = t->non_random[n - 2];
+            continue;
+        }
+        memset(pn, 0, sizeof(double) * points_size);
+        pn[sample_size] = (beta)*pow((double)1 - beta, (double)n - sample_size - 1) * (n - sample_size);
+        double pn_i = pn[sample_size];
+        for (size_t i = sample_size + 2; i <= n; ++i) {
+            if (i == n) {
+                pn[n - 1] = pow((double)beta, (double)n - sample_size);
+                break;
+            }
+            pn[i - 1] = pn_i * ((beta) / (1 - beta)) * ((double)(n - i) / (i - sample_size + 1));
+            pn_i = pn[i - 1];
+        }
+        double acc = 0.0;
+        unsigned int i_min = 0;
+        for (size_t i = n; i >= sample_size + 1; --i) {
+            acc += pn[i - 1];
+            if (acc < 1 - non_randomness) i_min = (unsigned int)i;
+            else break;
+        }
+        t->non_random[n - 1] = i_min;
+    }
+    free(pn);
+    t->maximality = (unsigned int *)malloc(sizeof(unsigned int) * points_size);
+    for (size_t i = 0; i < points_size; ++i) t->maximality[i] = 10000; /* max_hypotheses, :62 */
+    return t;
+}
+
+void orc_prosac_term_free(orc_prosac_term *t) {
+    if (!t) return;
+    free(t->maximality);
+    free(t->non_random);
+    free(t);
+}
+
+unsigned int orc_prosac_term_length(const orc_prosac_term *t) { return t->term_len; }
+
+/* ProsacTerminationCriteria::getUpBoundIterations(hypCount, model)
+ * (prosac_termination_criteria.hpp:148-201) over the model's inlier flags of the sorted
+ * points (flags[i] = GetError(i) < threshold); largest = the sampler's largest_sample_size
+ * at the call.  Mutates non_random (reference quirk) and maximality. */
+unsigned int orc_prosac_term_update(orc_prosac_term *t, unsigned int hypCount, const unsigned char *flags,
+                                    unsigned int largest) {
+    const unsigned int min_len = 20;
+    unsigned int max_samples = t->maximality[t->term_len - 1];
+    unsigned int inlier_count = 0;
+    for (unsigned int i = 0; i < min_len; i++) inlier_count += flags[i];
+    int in_next = 0, in_i = flags[min_len];
+    for (unsigned int i = min_len; i < t->n; ++i) {
+        if (i != t->n - 1) in_next = flags[i + 1];
+        inlier_count += (unsigned int)in_i;
+        if (t->non_random[i] < inlier_count) {
+            t->non_random[i] = inlier_count;
+            if ((i == t->n - 1) || (in_i && !in_next)) {
+                unsigned int new_samples = orc_std_termination(inlier_count, i + 1, t->m, t->desired_prob, t->max_iters);
+                if (i + 1 < largest) new_samples += hypCount - t->growth[i];
+                if (new_samples < t->maximality[i]) {
+                    t->maximality[i] = new_samples;
+                    if ((new_samples < max_samples) || ((new_samples == max_samples) && (i + 1 >= t->term_len))) {
+                        t->term_len = i + 1;
+                        max_samples = new_samples;
+                    }
+                }
+            }
+        }
+        in_i = in_next;
+    }
+    return max_samples;
+}
+
+/* ------------------------------------------------------------ SPRT */
+typedef struct {
+    double epsilon, delta, A;
+    int k;
+} sprt_hist;
+
+struct orc_sprt {
+    unsigned int *pool;
+    unsigned int idx, n, m, max_iters, cur;
+    int last_update, max_before;
+    double t_M, m_S;
+    sprt_hist *h;
+    unsigned int nh, caph;
+};
+
+/* SPRT::estimateThresholdA (sprt.hpp:332-355) */
+static double sprt_threshold_A(const orc_sprt *s, double epsilon, double delta) {
+    double C = (1 - delta) * log((1 - delta) / (1 - epsilon)) + delta * (log(delta / epsilon));
+    double K = (s->t_M * C) / s->m_S + 1;
+    double An_1 = K, An = K;
+    for (unsigned int i = 0; i < 10; ++i) {
+        An = K + log(An_1);
+        if (fabs(An - An_1) < 1.5e-8) break;
+        An_1 = An;
+    }
+    return An;
+}
+
+static void sprt_push(orc_sprt *s, double eps, double delta, double A, int k) {
+    if (s->nh == s->caph) {
+        s->caph = s->caph ? 2 * s->caph : 16;
+        s->h = (sprt_hist *)realloc(s->h, sizeof(sprt_hist) * s->caph);
+    }
+    s->h[s->nh].epsilon = eps;
+    s->h[s->nh].delta = delta;
+    s->h[s->nh].A = A;
+    s->h[s->nh].k = k;
+    s->nh++;
+}
+
+/* SPRT ctor (sprt.hpp:89-175): the pool shuffle consumes points_size random() draws from
+ * the shared glibc stream; per-estimator (epsilon0, delta0, t_M, m_S). */
+orc_sprt *orc_sprt_new(int kind, unsigned int points_size, unsigned int sample_size, unsigned int max_iterations,
+                       int max_hypothesis_test_before_sprt) {
+    orc_sprt *s = (orc_sprt *)calloc(1, sizeof(*s));
+    s->n = points_size;
+    s->m = sample_size;
+    s->max_iters = max_iterations;
+    s->max_before = max_hypothesis_test_before_sprt;
+    s->pool = (unsigned int *)malloc(sizeof(unsigned int) * points_size);
+    for (unsigned int i = 0; i < points_size; i++) s->pool[i] = i;
+    int max = (int)points_size;
+    for (unsigned int i = 0; i < points_size; i++) {
+        unsigned int r = (unsigned int)random() % (unsigned int)max;
+        unsigned int tmp = s->pool[r];
+        max--;
+        s->pool[r] = s->pool[max];
+        s->pool[max] = tmp;
+    }
+    s->idx = 0;
+    double eps0, delta0;
+    if (kind == ORC_HOMOGRAPHY) {
+        delta0 = 0.01; eps0 = 0.1; s->t_M = 200; s->m_S = 1;
+    } else if (kind == ORC_FUNDAMENTAL) {
+        delta0 = 0.05; eps0 = 0.2; s->t_M = 200; s->m_S = 2.48;
+    } else if (kind == ORC_ESSENTIAL) {
+        delta0 = 0.05; eps0 = 0.2; s->t_M = 300; s->m_S = 4;
+    } else {
+        delta0 = 0.0001; eps0 = 0.001; s->t_M = 100; s->m_S = 1;
+    }
+    sprt_push(s, eps0, delta0, sprt_threshold_A(s, eps0, delta0), 0);
+    s->cur = 0;
+    s->last_update = 0;
+    return s;
+}
+
+void orc_sprt_free(orc_sprt *s) {
+    if (!s) return;
+    free(s->pool);
+    free(s->h);
+    free(s);
+}
+
+const unsigned int *orc_sprt_pool(const orc_sprt *s) { return s->pool; }
+double orc_sprt_A(const orc_sprt *s) { return s->h[s->cur].A; }
+unsigned int orc_sprt_histories(const orc_sprt *s) { return s->nh; }
+
+/* SPRT::verifyModelAndGetModelScore (sprt.hpp:191-317) with the model already set in e.
+ * Returns good (1/0); writes (count, score) when the reference writes them. */
+int orc_sprt_verify(orc_sprt *s, orc_est *e, float thr, int current_hypothese, unsigned int maximum_score,
+                    int *count, float *score, unsigned int *tested_out) {
+    const double epsilon = s->h[s->cur].epsilon, delta = s->h[s->cur].delta, A = s->h[s->cur].A;
+    double lambda_new, lambda = 1;
+    unsigned int tested_point = 0, tested_inliers = 0;
+    int good = 1;
+    for (tested_point = 0; tested_point < s->n; tested_point++) {
+        if (s->idx >= s->n) s->idx = 0;
+        if (orc_est_error(e, s->pool[s->idx]) < thr) {
+            tested_inliers++;
+            lambda_new = lambda * (delta / epsilon);
+        } else {
+            lambda_new = lambda * ((1 - delta) / (1 - epsilon));
+        }
+        s->idx++;
+        if (lambda_new > A) {
+            good = 0;
+            tested_point++;
+            break;
+        }
+        lambda = lambda_new;
+    }
+    if (good) {
+        *count = (int)tested_inliers;
+        *score = (float)*count;
+    } else if (current_hypothese < s->max_before) {
+        unsigned int after = 0;
+        for (unsigned int p = tested_point; p < s->n; p++) {
+            if (s->idx >= s->n) s->idx = 0;
+            if (orc_est_error(e, s->pool[s->idx]) < thr) after++;
+            s->idx++;
+        }
+        *count = (int)(tested_inliers + after);
+        *score = (float)*count;
+    }
+    if (tested_out) *tested_out = tested_point;
+    if (good) {
+        if (tested_inliers > maximum_score) {
+            const double eps_new = (float)tested_inliers / s->n;
+            sprt_push(s, eps_new, delta, sprt_threshold_A(s, eps_new, delta), current_hypothese - s->last_update);
+            s->last_update = current_hypothese;
+            s->cur++;
+        }
+    } else {
+        const float delta_est = (float)tested_inliers / tested_point;
+        if (delta_est > 0 && fabs(delta - delta_est) / delta > 0.05) {
+            sprt_push(s, epsilon, delta_est, sprt_threshold_A(s, epsilon, delta_est), current_hypothese - s->last_update);
+            s->last_update = current_hypothese;
+            s->cur++;
+        }
+    }
+    return good;
+}
+
+/* SPRT::computeExponentH (sprt.hpp:442-491) */
+static double sprt_exponent_h(double epsilon, double epsilon_new, double delta) {
+    double a = log(delta / epsilon);
+    double b = log((1 - delta) / (1 - epsilon));
+    double x0 = log(1 / (1 - epsilon_new)) / b;
+    double v0 = epsilon_new * exp(x0 * a);
+    double x1 = log((1 - 2 * v0) / (1 - epsilon_new)) / b;
+    double v1 = epsilon_new * exp(x1 * a) + (1 - epsilon_new) * exp(x1 * b);
+    double h = x0 - (x0 - x1) / (1 + v0 - v1) * v0;
+    if (isnan(h)) return 0;
+    return h;
+}
+
+/* SPRT::getUpperBoundIterations (sprt.hpp:371-393) */
+unsigned int orc_sprt_upper_bound(const orc_sprt *s, int inliers_size) {
+    double epsilon = (double)inliers_size / s->n;
+    double P_g = pow(epsilon, s->m);
+    double log_eta_l_1 = 0;
+    for (unsigned int test = 0; test < s->cur; test++) {
+        double h = sprt_exponent_h(s->h[test].epsilon, epsilon, s->h[test].delta);
+        log_eta_l_1 += log(1 - P_g * (1 - pow(s->h[test].A, -h))) * s->h[test].k;
+    }
+    double numerator = log(0.05) - log_eta_l_1;
+    if (numerator >= 0) return 0;
+    double denumerator = log(1 - P_g * (1 - 1 / s->h[s->cur].A));
+    if (isnan(denumerator) || fabs(denumerator) < 0.00001) return s->max_iters;
+    double kl = numerator / denumerator;
+    unsigned int k = (unsigned int)kl;
+    return k < s->max_iters ? k : s->max_iters;
+}
+
 /* ------------------------------------------------------------ Ransac::run */
 static int score_bigger(int c1, float s1, int c2, float s2) {
     /* Score::bigger (quality.hpp:22-26) */
@@ -917,35 +1303,73 @@ static int score_bigger(int c1, float s1, int c2, float s2) {
     return 0;
 }
 
-int orc_ransac_run(int kind, const float *points, unsigned int n, float threshold, float desired_prob,
-                   unsigned int max_iterations, unsigned int seed, int dlt_mode, orc_result *out,
-                   int *inliers_out, unsigned int *rec_iter, int *rec_count, float *rec_score, int rec_cap) {
-    orc_est *e = orc_est_new(kind, points, n, dlt_mode);
+int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_config *cfg, orc_result *out,
+                       int *inliers_out, unsigned int *rec_iter, int *rec_count, float *rec_score, int rec_cap) {
+    orc_est *e = orc_est_new(kind, points, n, cfg->dlt_mode);
     if (!e) return -1;
     const int m = orc_est_sample_size(e);
-    orc_srandom(seed);
-    orc_uniform *smp = orc_uniform_new(n, (unsigned int)m);
+    const float threshold = cfg->threshold;
+    const int prosac = cfg->sampler == ORC_SAMPLER_PROSAC;
+    /* Ransac ctor order (ransac.hpp:41-93): sampler, termination, then SPRT (whose pool
+     * shuffle consumes n glibc draws before the Uniform sampler's first). */
+    orc_srandom(cfg->seed);
+    orc_uniform *smp = prosac ? NULL : orc_uniform_new(n, (unsigned int)m);
+    orc_prosac *ps = prosac ? orc_prosac_new((unsigned int)m, n, cfg->seed) : NULL;
+    orc_prosac_term *pt = prosac ? orc_prosac_term_new(orc_prosac_growth(ps), n, (unsigned int)m, cfg->desired_prob,
+                                                       cfg->max_iterations)
+                                 : NULL;
+    orc_sprt *sp = cfg->sprt ? orc_sprt_new(kind, n, (unsigned int)m, cfg->max_iterations, 20) : NULL;
     int *inl = (int *)malloc(sizeof(int) * (n ? n : 1));
-    int sample[9];
+    unsigned char *flags = (unsigned char *)malloc(n ? n : 1);
+    int sample[16];
     float models[27], best_model[9];
     memset(best_model, 0, sizeof(best_model));
     int best_cnt = 0, nrec = 0;
     float best_sum = 0.f;
-    unsigned int iters = 0, max_iters = max_iterations;
+    unsigned int iters = 0, max_iters = cfg->max_iterations;
+    out->sprt_rejected = 0;
 
     /* ransac.cpp:58-139 */
     while (iters < max_iters) {
-        orc_uniform_sample(smp, sample);
+        if (prosac) {
+            orc_prosac_set_term_len(ps, orc_prosac_term_length(pt));
+            orc_prosac_sample(ps, sample);
+        } else {
+            orc_uniform_sample(smp, sample);
+        }
         int nm = orc_est_estimate(e, sample, models);
         for (int i = 0; i < nm; i++) {
-            int cnt;
-            float sum;
-            orc_quality(e, models + 9 * i, threshold, &cnt, &sum, NULL);
+            int cnt = 0;
+            float sum = 0.f;
+            if (sp) {
+                orc_est_set_model(e, models + 9 * i);
+                int good = orc_sprt_verify(sp, e, threshold, (int)iters, (unsigned int)best_cnt, &cnt, &sum, NULL);
+                if (!good) {
+                    out->sprt_rejected++;
+                    if ((int)iters >= 20) { /* max_hypothesis_test_before_sprt, SURVEY Q9 */
+                        iters++;
+                        continue;
+                    }
+                }
+            } else {
+                orc_quality(e, models + 9 * i, threshold, &cnt, &sum, NULL);
+            }
             if (score_bigger(cnt, sum, best_cnt, best_sum)) {
                 best_cnt = cnt;
                 best_sum = sum;
                 memcpy(best_model, models + 9 * i, sizeof(best_model));
-                max_iters = orc_std_termination((unsigned int)best_cnt, n, (unsigned int)m, desired_prob, max_iterations);
+                if (prosac) {
+                    orc_est_set_model(e, best_model);
+                    for (unsigned int p = 0; p < n; p++) flags[p] = orc_est_error(e, p) < threshold;
+                    max_iters = orc_prosac_term_update(pt, iters, flags, orc_prosac_largest(ps));
+                } else {
+                    max_iters = orc_std_termination((unsigned int)best_cnt, n, (unsigned int)m, cfg->desired_prob,
+                                                    cfg->max_iterations);
+                }
+                if (sp) {
+                    unsigned int ub = orc_sprt_upper_bound(sp, best_cnt);
+                    if (ub < max_iters) max_iters = ub;
+                }
                 if (nrec < rec_cap) {
                     if (rec_iter) rec_iter[nrec] = iters;
                     if (rec_count) rec_count[nrec] = cnt;
@@ -960,6 +1384,8 @@ int orc_ransac_run(int kind, const float *points, unsigned int n, float threshol
     out->iters = iters;
     out->n_records = nrec;
     out->polish_passes = 0;
+    out->sprt_histories = sp ? (int)orc_sprt_histories(sp) : 0;
+    out->prosac_term_len = pt ? orc_prosac_term_length(pt) : n;
     memcpy(out->minimal_model, best_model, sizeof(best_model));
     out->minimal_inliers = best_cnt;
     if (best_cnt == 0) {
@@ -987,9 +1413,28 @@ int orc_ransac_run(int kind, const float *points, unsigned int n, float threshol
     memcpy(out->model, best_model, sizeof(best_model));
     out->inliers = best_cnt;
     free(inl);
+    free(flags);
     orc_uniform_free(smp);
+    orc_prosac_free(ps);
+    orc_prosac_term_free(pt);
+    orc_sprt_free(sp);
     orc_est_free(e);
     return rc;
+}
+
+int orc_ransac_run(int kind, const float *points, unsigned int n, float threshold, float desired_prob,
+                   unsigned int max_iterations, unsigned int seed, int dlt_mode, orc_result *out,
+                   int *inliers_out, unsigned int *rec_iter, int *rec_count, float *rec_score, int rec_cap) {
+    orc_config cfg;
+    memset(&cfg, 0, sizeof(cfg));
+    cfg.threshold = threshold;
+    cfg.desired_prob = desired_prob;
+    cfg.max_iterations = max_iterations;
+    cfg.seed = seed;
+    cfg.dlt_mode = dlt_mode;
+    cfg.sampler = ORC_SAMPLER_UNIFORM;
+    cfg.sprt = 0;
+    return orc_ransac_run_cfg(kind, points, n, &cfg, out, inliers_out, rec_iter, rec_count, rec_score, rec_cap);
 }
 
 int orc_hypothesis_loop(orc_est *e, orc_uniform *s, int count, float thr, float *best_score_sum) {

@@ -86,7 +86,63 @@ typedef struct {
     int polish_passes;    /* accepted non-minimal passes */
     float minimal_model[9];
     int minimal_inliers;
+    int sprt_rejected;    /* models SPRT rejected */
+    int sprt_histories;   /* SPRT tests designed (history length) */
+    unsigned int prosac_term_len; /* final PROSAC termination_length (n without PROSAC) */
 } orc_result;
+
+enum { ORC_SAMPLER_UNIFORM = 1, ORC_SAMPLER_NAPSAC = 3, ORC_SAMPLER_PROSAC = 4 }; /* = SAMPLER, usac/model.hpp:11 */
+typedef struct {
+    float threshold, desired_prob;
+    unsigned int max_iterations, seed;
+    int dlt_mode;
+    int sampler; /* ORC_SAMPLER_* */
+    int sprt;    /* Model::setSprt */
+} orc_config;
+
+/* Ransac::run with the sampler / SPRT of cfg (PROSAC: points sorted by quality; its
+ * mt19937 is seeded with cfg->seed instead of std::random_device). */
+int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_config *cfg, orc_result *out,
+                       int *inliers_out, unsigned int *rec_iter, int *rec_count, float *rec_score, int rec_cap);
+
+/* std::mt19937 + uniform_int_distribution<int>(0, max) (libstdc++ downscaling) */
+typedef struct {
+    uint32_t mt[624];
+    int i;
+} orc_mt;
+void orc_mt_seed(orc_mt *g, uint32_t seed);
+uint32_t orc_mt_next(orc_mt *g);
+int orc_mt_uniform(orc_mt *g, unsigned int max);
+
+/* ProsacSampler (usac/sampler/prosac_sampler.hpp) */
+typedef struct orc_prosac orc_prosac;
+orc_prosac *orc_prosac_new(unsigned int sample_size, unsigned int points_size, uint32_t seed);
+void orc_prosac_free(orc_prosac *p);
+const unsigned int *orc_prosac_growth(const orc_prosac *p);
+unsigned int orc_prosac_largest(const orc_prosac *p);
+void orc_prosac_set_term_len(orc_prosac *p, unsigned int t);
+void orc_prosac_sample(orc_prosac *p, int *sample);
+
+/* ProsacTerminationCriteria (usac/termination_criteria/prosac_termination_criteria.hpp) */
+typedef struct orc_prosac_term orc_prosac_term;
+orc_prosac_term *orc_prosac_term_new(const unsigned int *growth, unsigned int points_size, unsigned int sample_size,
+                                     float desired_prob, unsigned int max_iterations);
+void orc_prosac_term_free(orc_prosac_term *t);
+unsigned int orc_prosac_term_length(const orc_prosac_term *t);
+unsigned int orc_prosac_term_update(orc_prosac_term *t, unsigned int hypCount, const unsigned char *flags,
+                                    unsigned int largest);
+
+/* SPRT (usac/sprt.hpp) */
+typedef struct orc_sprt orc_sprt;
+orc_sprt *orc_sprt_new(int kind, unsigned int points_size, unsigned int sample_size, unsigned int max_iterations,
+                       int max_hypothesis_test_before_sprt);
+void orc_sprt_free(orc_sprt *s);
+const unsigned int *orc_sprt_pool(const orc_sprt *s);
+double orc_sprt_A(const orc_sprt *s);
+unsigned int orc_sprt_histories(const orc_sprt *s);
+int orc_sprt_verify(orc_sprt *s, orc_est *e, float thr, int current_hypothese, unsigned int maximum_score,
+                    int *count, float *score, unsigned int *tested_out);
+unsigned int orc_sprt_upper_bound(const orc_sprt *s, int inliers_size);
 
 int orc_ransac_run(int kind, const float *points, unsigned int n, float threshold, float desired_prob,
                    unsigned int max_iterations, unsigned int seed, int dlt_mode, orc_result *out,

@@ -16,7 +16,7 @@ import subprocess
 import numpy as np
 
 __all__ = ["ESTIMATOR", "SAMPLER", "DLT", "Model", "Ransac", "RansacOutput", "Score", "Context", "Record",
-           "build", "lib", "std_termination", "uniform_samples", "UsacError"]
+           "build", "lib", "std_termination", "uniform_samples", "prosac_samples", "sprt_pool", "UsacError"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libransac_amd.so")
@@ -62,14 +62,16 @@ class Record(ctypes.Structure):
 
 class _Params(ctypes.Structure):
     _fields_ = [("threshold", ctypes.c_float), ("desired_prob", ctypes.c_float), ("max_iterations", ctypes.c_uint32),
-                ("seed", ctypes.c_uint32), ("dlt_mode", ctypes.c_int32), ("batch", ctypes.c_uint32)]
+                ("seed", ctypes.c_uint32), ("dlt_mode", ctypes.c_int32), ("batch", ctypes.c_uint32),
+                ("sampler", ctypes.c_int32), ("sprt", ctypes.c_int32)]
 
 
 class _RunOutput(ctypes.Structure):
     _fields_ = [("model", ctypes.c_float * 9), ("inliers", ctypes.c_int32), ("iters", ctypes.c_uint32),
                 ("time_us", ctypes.c_int64), ("n_records", ctypes.c_int32), ("polish_passes", ctypes.c_int32),
                 ("minimal_model", ctypes.c_float * 9), ("minimal_inliers", ctypes.c_int32),
-                ("batches", ctypes.c_uint32)]
+                ("batches", ctypes.c_uint32), ("sprt_rejected", ctypes.c_int32), ("sprt_histories", ctypes.c_int32),
+                ("prosac_term_len", ctypes.c_uint32), ("rollbacks", ctypes.c_uint32)]
 
 
 # every symbol include/usac_gpu.h declares (checked by tests/test_abi.py)
@@ -78,6 +80,7 @@ ABI_SYMBOLS = [
     "usac_num_points", "usac_estimate_models", "usac_score_models", "usac_get_inliers", "usac_nonminimal",
     "usac_hypothesize_score", "usac_hypothesize_async", "usac_fetch_best", "usac_sync", "usac_last_timings",
     "usac_set_score_chunks", "usac_set_score_variant", "usac_std_termination", "usac_ransac_run", "usac_uniform_samples",
+    "usac_prosac_samples", "usac_sprt_pool",
     "usac_comm_unique_id", "usac_comm_init", "usac_allgather_records", "usac_merge_records",
 ]
 
@@ -127,6 +130,10 @@ def lib():
         "usac_ransac_run": (ctypes.c_int, [_vp, _P(_Params), _P(_RunOutput), i32p, _P(Record), ctypes.c_uint32]),
         "usac_uniform_samples": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                 i32p]),
+        "usac_prosac_samples": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
+                                               ctypes.c_uint32, i32p]),
+        "usac_sprt_pool": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, u32p,
+                                          _P(ctypes.c_double)]),
         "usac_comm_unique_id": (ctypes.c_int, [u8p]),
         "usac_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, u8p]),
         "usac_allgather_records": (ctypes.c_int, [_vp, _P(Record), _P(Record)]),
@@ -148,6 +155,26 @@ def std_termination(inliers, points_size, sample_size, desired_prob, max_iterati
     """StandardTerminationCriteria::getUpBoundIterations (standard_termination_criteria.hpp:52-62)."""
     return int(lib().usac_std_termination(inliers, points_size, sample_size, ctypes.c_float(desired_prob),
                                           max_iterations))
+
+
+def prosac_samples(seed, n_points, m, count, termination_length=None):
+    """Host ProsacSampler stream (mt19937 seeded with `seed`), count x m int32."""
+    out = np.zeros((count, m), dtype=np.int32)
+    tl = n_points if termination_length is None else termination_length
+    rc = lib().usac_prosac_samples(seed, n_points, m, count, tl, _ptr(out, ctypes.c_int32))
+    if rc:
+        raise UsacError(rc, "usac_prosac_samples")
+    return out
+
+
+def sprt_pool(seed, estimator, n_points, m):
+    """SPRT random pool after srandom(seed) and the first threshold A."""
+    pool = np.zeros(n_points, dtype=np.uint32)
+    A = ctypes.c_double(0)
+    rc = lib().usac_sprt_pool(seed, int(estimator), n_points, m, _ptr(pool, ctypes.c_uint32), ctypes.byref(A))
+    if rc:
+        raise UsacError(rc, "usac_sprt_pool")
+    return pool, A.value
 
 
 def uniform_samples(seed, n_points, m, count):
@@ -373,9 +400,7 @@ class Model:
         self.desired_prob = float(p)
 
     def setSprt(self, sprt):
-        if sprt:
-            raise NotImplementedError("SPRT is not in ABI v1 (SURVEY §8 a15, next round)")
-        self.sprt = False
+        self.sprt = bool(sprt)
 
     def setDLTMode(self, mode):
         self.dlt_mode = DLT(mode)
@@ -415,8 +440,8 @@ class Ransac:
     """usac/ransac/ransac.hpp:41-115 -- Ransac(model, points); run(); getRansacOutput()."""
 
     def __init__(self, model, points):
-        if model.sampler != SAMPLER.Uniform:
-            raise NotImplementedError("sampler %s is not in ABI v1 (Uniform only)" % model.sampler.name)
+        if model.sampler not in (SAMPLER.Uniform, SAMPLER.Prosac):
+            raise NotImplementedError("sampler %s is not in ABI v2 (Uniform, Prosac)" % model.sampler.name)
         self.model = model
         self.ctx = Context(model.estimator, points, device=model.device)
         self._out = None
@@ -428,7 +453,8 @@ class Ransac:
         seed = m.seed
         if m.reset_random_generator and seed == 0:
             seed = int.from_bytes(os.urandom(4), "little") or 1
-        p = _Params(m.threshold, m.desired_prob, m.max_iterations, seed, int(m.dlt_mode), m.batch)
+        p = _Params(m.threshold, m.desired_prob, m.max_iterations, seed, int(m.dlt_mode), m.batch, int(m.sampler),
+                    1 if m.sprt else 0)
         out = _RunOutput()
         inl = np.zeros(self.ctx.n, dtype=np.int32)
         recs = (Record * rec_cap)()
@@ -441,7 +467,9 @@ class Ransac:
         self.records = [(int(recs[i].hyp_index), int(recs[i].inliers), float(recs[i].score)) for i in range(k)]
         raw = {"minimal_model": np.array(out.minimal_model[:], dtype=np.float32),
                "minimal_inliers": out.minimal_inliers, "polish_passes": out.polish_passes,
-               "n_records": out.n_records, "batches": out.batches}
+               "n_records": out.n_records, "batches": out.batches, "sprt_rejected": out.sprt_rejected,
+               "sprt_histories": out.sprt_histories, "prosac_term_len": out.prosac_term_len,
+               "rollbacks": out.rollbacks}
         self._out = RansacOutput(np.array(out.model[:], dtype=np.float32), inl[: out.inliers].copy(), out.time_us,
                                  out.inliers, out.iters, raw)
 

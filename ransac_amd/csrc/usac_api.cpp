@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -61,6 +62,7 @@ struct usac_ctx {
     // batch buffers
     DevBuf samples, models, counts, sums, best, hostmodels, argmax_part;
     DevBuf list, list_n;    // fundamental: occupied model slots (compacted) and their number
+    DevBuf pool_idx, pool_pts, masks;  // SPRT parity path: pool order, permuted points, flag words
     uint32_t spk = 1;       // model slots per hypothesis (3 for the 7-point solver)
     // single-model / polish buffers
     DevBuf one_model, inl_idx, inl_cnt, inl_sum, q, partial, ws, nm_model, nm_ok;
@@ -266,7 +268,7 @@ void usac_destroy(usac_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
     for (DevBuf *b : {&c->pts, &c->rec, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
-                      &c->argmax_part, &c->list, &c->list_n, &c->one_model,
+                      &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->one_model,
                       &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok,
                       &c->rec_send, &c->rec_all})
         b->release();
@@ -476,91 +478,98 @@ int usac_uniform_samples(uint32_t seed, uint32_t n_points, uint32_t m, uint32_t 
     return USAC_OK;
 }
 
-// Ransac::run (ransac.cpp:14-238), Uniform sampler, no LO/SPRT.  Samples are drawn on the
-// host from the glibc stream in loop order and shipped in batches; the device solves and
-// scores a whole batch (exact counts, exact sequential sums); the host replays the
-// sequential loop over the batch's (count, sum) list -- Score::bigger, termination
-// update at each new best, `while (iters < max_iters)` -- which reproduces the reference's
-// iteration sequence exactly because max_iters changes only at best-score updates
-// (SURVEY Q24).  Then the <= 4-pass non-minimal polish on the device.
+int usac_prosac_samples(uint32_t seed, uint32_t n_points, uint32_t m, uint32_t count, uint32_t termination_length,
+                        int32_t *out) {
+    if (!out || m < 2 || n_points < m || termination_length == 0 || count > usac::ProsacSampler::kGrowthMax)
+        return USAC_ERR_ARG;
+    usac::ProsacSampler s(seed, n_points, m);
+    for (uint32_t i = 0; i < count; i++) s.generateSample(out + (size_t)i * m, termination_length);
+    return USAC_OK;
+}
+
+int usac_sprt_pool(uint32_t seed, int estimator, uint32_t n_points, uint32_t m, uint32_t *pool, double *A0) {
+    if (!pool || n_points == 0) return USAC_ERR_ARG;
+    usac::GlibcRandom g(seed);
+    usac::Sprt s(g, estimator, n_points, m, 10000);
+    memcpy(pool, s.pool().data(), sizeof(uint32_t) * n_points);
+    if (A0) *A0 = s.thresholdA0();
+    return USAC_OK;
+}
+
+// Ransac::run (ransac.cpp:14-238): Uniform (glibc stream) or PROSAC sampler, optional SPRT,
+// no LO.  Samples are drawn on the host in loop order and shipped in batches; the device
+// solves every sample of a batch and either scores every model exactly (count, sequential
+// Σerr) or, with SPRT, produces every model's inlier flags in SPRT-pool order; the host
+// then replays the sequential loop over the batch -- SPRT walk, Score::bigger, termination
+// update at each new best (standard, or PROSAC's scan of the best model's device inlier
+// list), `while (iters < max_iters)` with the reference's SPRT double counting.
+// This reproduces the reference's iteration sequence exactly because the loop state
+// changes only at those points.  PROSAC samples depend on
+// termination_length, which a best update can change: a batch is speculative, and when a
+// change would alter a later sample of the batch the rest of the batch is dropped and the
+// sampler is rewound to just after the current sample.  Then the <= 4-pass non-minimal
+// polish on the device.
 int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, int32_t *inliers_out,
                     usac_record *records, uint32_t rec_cap) {
     if (!c || !prm || !out) return USAC_ERR_ARG;
     memset(out, 0, sizeof(*out));
+    const bool prosac = prm->sampler == USAC_SAMPLER_PROSAC;
+    if (!prosac && prm->sampler != USAC_SAMPLER_UNIFORM && prm->sampler != 0)
+        return fail(c, USAC_ERR_UNSUPPORTED, "sampler not supported (Uniform, Prosac)");
+    if (prosac && c->n <= 20) return fail(c, USAC_ERR_ARG, "PROSAC needs > 20 points (prosac_termination_criteria.hpp:158-163)");
+    if (prosac && prm->max_iterations > usac::ProsacSampler::kGrowthMax)
+        return fail(c, USAC_ERR_ARG, "PROSAC max_iterations > 200000 (reference draws outside the point range)");
     const auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(c, hipSetDevice(c->device));
-    const uint32_t batch = prm->batch ? prm->batch : kDefaultBatch;
+    const uint32_t batch = prm->batch ? prm->batch : (prm->sprt ? 1024u : kDefaultBatch);
     int rc = ensure_batch(c, batch);
     if (rc) return rc;
     rc = ensure_single(c);
     if (rc) return rc;
     const int saved_mode = c->dlt_mode;
     c->dlt_mode = prm->dlt_mode;
+    const uint32_t n = c->n, m = c->m, spk = c->spk;
+    const float thr = prm->threshold;
 
-    usac::UniformSampler sampler(prm->seed, c->n, c->m);
-    usac::StandardTerminationCriteria term(prm->desired_prob, c->m, c->n, prm->max_iterations);
-    const uint32_t spk = c->spk;
+    // Ransac ctor order (ransac.hpp:41-93): sampler, termination criteria, then SPRT -- the
+    // SPRT pool shuffle draws n values of the glibc stream before the Uniform sampler's first.
+    usac::GlibcRandom grng(prm->seed);
+    std::unique_ptr<usac::UniformSampler> uni;
+    std::unique_ptr<usac::ProsacSampler> pro;
+    std::unique_ptr<usac::ProsacTerminationCriteria> pterm;
+    if (prosac) {
+        pro.reset(new usac::ProsacSampler(prm->seed, n, m));
+        pterm.reset(new usac::ProsacTerminationCriteria(pro->growth(), prm->desired_prob, m, n, prm->max_iterations));
+    } else {
+        uni.reset(new usac::UniformSampler(grng, n, m));
+    }
+    usac::StandardTerminationCriteria term(prm->desired_prob, m, n, prm->max_iterations);
+    std::unique_ptr<usac::Sprt> sprt;
+    const uint32_t nw = (n + 31) / 32;
+    if (prm->sprt) {
+        sprt.reset(new usac::Sprt(grng, c->estimator, n, m, prm->max_iterations));
+        HIP_TRY(c, c->pool_idx.reserve(sizeof(uint32_t) * n));
+        HIP_TRY(c, c->pool_pts.reserve(sizeof(float) * c->cols * (size_t)n));
+        HIP_TRY(c, c->masks.reserve(sizeof(uint32_t) * nw * (size_t)batch * spk));
+        HIP_TRY(c, hipMemcpyAsync(c->pool_idx.p, sprt->pool().data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice,
+                                  c->stream));
+        HIP_TRY(c, usac::launch_gather_points(c->stream, c->pts.p, c->cols, c->pool_idx.as<uint32_t>(), n,
+                                              c->pool_pts.p));
+    }
+
     const size_t SB = (size_t)batch * spk;  // slot stride of the host copies
-    std::vector<int32_t> hs((size_t)batch * c->m), hc(SB);
+    std::vector<int32_t> hs((size_t)batch * m), hc(SB), slot_row(SB);
     std::vector<float> hsum(SB), hmod((size_t)ncomp(c) * SB);
+    std::vector<uint32_t> hlist(SB), hmask(sprt ? (size_t)nw * SB : 0);
+    std::vector<uint32_t> subset_at(batch), largest_at(batch);
+    std::vector<uint8_t> flags(prosac ? n : 0);
+    std::vector<int32_t> inl_list(prosac ? n : 0);
     usac::Score best;
     float best_model[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t iters = 0, max_iters = prm->max_iterations;
     int32_t nrec = 0;
-    uint32_t batches = 0;
-    while (iters < max_iters) {
-        const uint32_t B = std::min(batch, max_iters - iters);
-        for (uint32_t j = 0; j < B; j++) sampler.generateSample(hs.data() + (size_t)j * c->m);
-        HIP_TRY(c, hipMemcpyAsync(c->samples.p, hs.data(), sizeof(int32_t) * (size_t)B * c->m, hipMemcpyHostToDevice,
-                                  c->stream));
-        HIP_TRY(c, enqueue_solve(c, c->samples.as<int32_t>(), B, 0, iters, nullptr));
-        HIP_TRY(c, enqueue_score(c, B, prm->threshold, 1));
-        const size_t S = (size_t)B * spk;
-        HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipMemcpyAsync(hsum.data(), c->sums.p, sizeof(float) * S, hipMemcpyDeviceToHost, c->stream));
-        for (int k = 0; k < ncomp(c); k++)
-            HIP_TRY(c, hipMemcpyAsync(hmod.data() + (size_t)k * SB, c->models.as<float>() + (size_t)k * S,
-                                      sizeof(float) * S, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
-        batches++;
-        for (uint32_t j = 0; j < B && iters < max_iters; j++, iters++) {
-            // the sample's models in solver order (empty slots carry count -1)
-            for (uint32_t q = 0; q < spk; q++) {
-                const size_t sl = (size_t)j * spk + q;
-                if (hc[sl] < 0) break;
-                usac::Score cur;
-                cur.inlier_number = hc[sl];
-                cur.score = hsum[sl];
-                if (cur.bigger(best)) {
-                    best = cur;
-                    for (int k = 0; k < 9; k++) best_model[k] = k < ncomp(c) ? hmod[(size_t)k * SB + sl] : 0.f;
-                    max_iters = term.getUpBoundIterations((uint32_t)best.inlier_number);
-                    if (records && (uint32_t)nrec < rec_cap) {
-                        usac_record &r = records[nrec];
-                        r.hyp_index = iters;
-                        r.inliers = cur.inlier_number;
-                        r.score = cur.score;
-                        memcpy(r.model, best_model, sizeof(best_model));
-                        r.valid = 1;
-                    }
-                    nrec++;
-                }
-            }
-        }
-    }
-    out->iters = iters;
-    out->n_records = nrec;
-    out->batches = batches;
-    memcpy(out->minimal_model, best_model, sizeof(best_model));
-    out->minimal_inliers = best.inlier_number;
-    c->dlt_mode = saved_mode;
-    if (best.inlier_number == 0) {
-        memcpy(out->model, best_model, sizeof(best_model));
-        return fail(c, USAC_ERR_NO_MODEL, "best score is 0 (ransac.cpp:143-147)");
-    }
 
-    // ---- polish (ransac.cpp:157-207) on the device
-    const float thr = prm->threshold;
+    // exact inliers of a model on the device -> (cnt, s) and c->inl_idx
     int32_t cnt = 0, ok = 0;
     float s = 0.f;
     auto score_inliers = [&](const float *model_host) -> int {
@@ -571,6 +580,147 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         return USAC_OK;
     };
+
+    while (iters < max_iters) {
+        const uint32_t B = std::min(batch, max_iters - iters);
+        // ---- draw the batch (speculatively for PROSAC)
+        std::unique_ptr<usac::ProsacSampler> snapshot;
+        const uint32_t gen_term = prosac ? pterm->terminationLength() : n;
+        if (prosac) snapshot.reset(new usac::ProsacSampler(*pro));
+        for (uint32_t j = 0; j < B; j++) {
+            int32_t *smp = hs.data() + (size_t)j * m;
+            if (prosac) {
+                subset_at[j] = pro->subset();
+                pro->generateSample(smp, gen_term);
+                largest_at[j] = pro->largest();
+            } else {
+                uni->generateSample(smp);
+            }
+        }
+        // ---- device: solve, then exact scores or pool-order flags
+        const size_t S = (size_t)B * spk;
+        HIP_TRY(c, hipMemcpyAsync(c->samples.p, hs.data(), sizeof(int32_t) * (size_t)B * m, hipMemcpyHostToDevice,
+                                  c->stream));
+        HIP_TRY(c, enqueue_solve(c, c->samples.as<int32_t>(), B, 0, iters, nullptr));
+        const size_t mstride = is_f(c) ? 3 * (size_t)B : (size_t)B;
+        if (sprt) {
+            HIP_TRY(c, usac::launch_pool_mask(c->stream, c->estimator, c->pool_pts.p, n, c->models.as<float>(), mstride,
+                                              is_f(c) ? c->list.as<uint32_t>() : nullptr,
+                                              is_f(c) ? c->list_n.as<uint32_t>() : nullptr, (uint32_t)S, thr,
+                                              c->masks.as<uint32_t>(), (uint32_t)S));
+        } else {
+            HIP_TRY(c, enqueue_score(c, B, thr, 1));
+            HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(c, hipMemcpyAsync(hsum.data(), c->sums.p, sizeof(float) * S, hipMemcpyDeviceToHost, c->stream));
+        }
+        for (int k = 0; k < ncomp(c); k++)
+            HIP_TRY(c, hipMemcpyAsync(hmod.data() + (size_t)k * SB, c->models.as<float>() + (size_t)k * S,
+                                      sizeof(float) * S, hipMemcpyDeviceToHost, c->stream));
+        uint32_t rows = (uint32_t)S;
+        if (sprt) {
+            if (is_f(c)) {  // occupied slots -> mask rows
+                HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
+                HIP_TRY(c, hipMemcpyAsync(&rows, c->list_n.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+                HIP_TRY(c, hipStreamSynchronize(c->stream));
+                if (rows) HIP_TRY(c, hipMemcpyAsync(hlist.data(), c->list.p, sizeof(uint32_t) * rows,
+                                                    hipMemcpyDeviceToHost, c->stream));
+            } else {
+                std::fill(hc.begin(), hc.begin() + S, 0);
+            }
+            for (uint32_t w = 0; w < nw && rows; w++)
+                HIP_TRY(c, hipMemcpyAsync(hmask.data() + (size_t)w * rows, c->masks.as<uint32_t>() + (size_t)w * S,
+                                          sizeof(uint32_t) * rows, hipMemcpyDeviceToHost, c->stream));
+        }
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        if (sprt) {
+            if (is_f(c)) {
+                std::fill(slot_row.begin(), slot_row.begin() + S, -1);
+                for (uint32_t r = 0; r < rows; r++) slot_row[hlist[r]] = (int32_t)r;
+            } else {
+                for (size_t sl = 0; sl < S; sl++) slot_row[sl] = (int32_t)sl;
+            }
+        }
+        out->batches++;
+        // ---- sequential replay
+        std::vector<uint32_t> wbuf(sprt ? nw : 0);
+        uint32_t j = 0;
+        bool rewind = false;
+        for (; j < B && iters < max_iters; j++) {
+            for (uint32_t q = 0; q < spk; q++) {
+                const size_t sl = (size_t)j * spk + q;
+                if (hc[sl] < 0) break;  // empty slot: the sample has no more models
+                usac::Score cur;
+                if (sprt) {
+                    const int32_t r = slot_row[sl];
+                    for (uint32_t w = 0; w < nw; w++) wbuf[w] = hmask[(size_t)w * rows + r];
+                    const bool good = sprt->verify(wbuf.data(), (int)iters, (uint32_t)best.inlier_number,
+                                                   cur.inlier_number, cur.score);
+                    if (!good) {
+                        out->sprt_rejected++;
+                        if ((int)iters >= 20) {  // max_hypothesis_test_before_sprt (model.hpp:40), Q9
+                            iters++;
+                            continue;
+                        }
+                    }
+                } else {
+                    cur.inlier_number = hc[sl];
+                    cur.score = hsum[sl];
+                }
+                if (!cur.bigger(best)) continue;
+                best = cur;
+                for (int k = 0; k < 9; k++) best_model[k] = k < ncomp(c) ? hmod[(size_t)k * SB + sl] : 0.f;
+                if (prosac) {
+                    if ((rc = score_inliers(best_model))) return rc;
+                    if (cnt > 0)
+                        HIP_TRY(c, hipMemcpy(inl_list.data(), c->inl_idx.p, sizeof(int32_t) * (size_t)cnt,
+                                             hipMemcpyDeviceToHost));
+                    std::fill(flags.begin(), flags.end(), 0);
+                    for (int32_t t = 0; t < cnt; t++) flags[inl_list[t]] = 1;
+                    max_iters = pterm->getUpBoundIterations(iters, [&](uint32_t i) { return flags[i] != 0; },
+                                                            largest_at[j]);
+                } else {
+                    max_iters = term.getUpBoundIterations((uint32_t)best.inlier_number);
+                }
+                if (sprt) max_iters = std::min(max_iters, sprt->getUpperBoundIterations(best.inlier_number));
+                if (records && (uint32_t)nrec < rec_cap) {
+                    usac_record &rr = records[nrec];
+                    rr.hyp_index = iters;
+                    rr.inliers = cur.inlier_number;
+                    rr.score = cur.score;
+                    memcpy(rr.model, best_model, sizeof(best_model));
+                    rr.valid = 1;
+                }
+                nrec++;
+            }
+            iters++;
+            if (prosac && pterm->terminationLength() != gen_term) {
+                // would any later sample of the batch be drawn differently?
+                const uint32_t tl = pterm->terminationLength();
+                for (uint32_t k = j + 1; k < B && !rewind; k++)
+                    rewind = (subset_at[k] > gen_term) || (subset_at[k] > tl);
+                if (rewind) break;
+            }
+        }
+        if (rewind) {  // sampler state just after sample j: replay the first j + 1 draws
+            pro = std::move(snapshot);
+            std::vector<int32_t> tmp(m);
+            for (uint32_t k = 0; k <= j; k++) pro->generateSample(tmp.data(), gen_term);
+            out->rollbacks++;
+        }
+    }
+    out->iters = iters;
+    out->n_records = nrec;
+    out->sprt_histories = sprt ? (int32_t)sprt->histories() : 0;
+    out->prosac_term_len = prosac ? pterm->terminationLength() : n;
+    memcpy(out->minimal_model, best_model, sizeof(best_model));
+    out->minimal_inliers = best.inlier_number;
+    c->dlt_mode = saved_mode;
+    if (best.inlier_number == 0) {
+        memcpy(out->model, best_model, sizeof(best_model));
+        return fail(c, USAC_ERR_NO_MODEL, "best score is 0 (ransac.cpp:143-147)");
+    }
+
+    // ---- polish (ransac.cpp:157-207) on the device
     if ((rc = score_inliers(best_model))) return rc;  // quality->getInliers(best_model)
     int prev = 0;
     float nm_model[9];

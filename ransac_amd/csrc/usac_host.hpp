@@ -6,12 +6,17 @@
 //   usac::UniformSampler             uniform_sampler.hpp:49-95 over a private glibc
 //                                    random_r TYPE_3 state (= random()/srandom() stream)
 //   usac::StandardTerminationCriteria standard_termination_criteria.hpp:10-74
-//   usac::Ransac (batched replay)    ransac.cpp:14-238
+//   usac::Mt19937 / UniformIntDist   std::mt19937 + uniform_int_distribution<int>
+//                                    (uniform_random_generator.hpp:16-63)
+//   usac::ProsacSampler              prosac_sampler.hpp:62-172
+//   usac::ProsacTerminationCriteria  prosac_termination_criteria.hpp:44-201
+//   usac::Sprt                       sprt.hpp:89-491 (decisions on device inlier masks)
 #pragma once
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <cmath>
 #include <vector>
 
@@ -50,7 +55,13 @@ class GlibcRandom {
 class UniformSampler {
    public:
     UniformSampler(unsigned int seed, uint32_t points_size, uint32_t sample_size)
-        : rng_(seed), pool_(points_size), max_((int)points_size), n_(points_size), m_(sample_size) {
+        : own_(seed), rng_(own_), pool_(points_size), max_((int)points_size), n_(points_size), m_(sample_size) {
+        for (uint32_t i = 0; i < points_size; i++) pool_[i] = i;
+    }
+    // sampler drawing from a shared stream (the reference's global random(): the SPRT pool
+    // shuffle and the sampler consume the same sequence)
+    UniformSampler(GlibcRandom &shared, uint32_t points_size, uint32_t sample_size)
+        : own_(1), rng_(shared), pool_(points_size), max_((int)points_size), n_(points_size), m_(sample_size) {
         for (uint32_t i = 0; i < points_size; i++) pool_[i] = i;
     }
     // uniform_sampler.hpp:42-54: persistent pool; refill when max reaches 0 (also
@@ -68,7 +79,8 @@ class UniformSampler {
     }
 
    private:
-    GlibcRandom rng_;
+    GlibcRandom own_;
+    GlibcRandom &rng_;
     std::vector<uint32_t> pool_;
     int max_;
     uint32_t n_, m_;
@@ -84,8 +96,10 @@ class StandardTerminationCriteria {
           m_(sample_size),
           n_(points_size),
           max_(max_iterations) {}
-    uint32_t getUpBoundIterations(uint32_t inlier_size) const {
-        float inl_ratio = (float)inlier_size / (float)n_;
+    uint32_t getUpBoundIterations(uint32_t inlier_size) const { return getUpBoundIterations(inlier_size, n_); }
+    // two-argument overload (standard_termination_criteria.hpp:64-74), used by PROSAC
+    uint32_t getUpBoundIterations(uint32_t inlier_size, uint32_t points_size) const {
+        float inl_ratio = (float)inlier_size / (float)points_size;
         float inl_prob = inl_ratio * inl_ratio;
         int k = (int)m_;
         while (k > 2) {
@@ -100,6 +114,329 @@ class StandardTerminationCriteria {
    private:
     float log_1_p_;
     uint32_t m_, n_, max_;
+};
+
+// ---------------------------------------------------------------- PROSAC
+// std::mt19937 (32-bit Mersenne twister, default tempering) -- the reference's PROSAC
+// generator; seeded here with the run seed (the reference uses std::random_device).
+class Mt19937 {
+   public:
+    explicit Mt19937(uint32_t seed) {
+        s_[0] = seed;
+        for (int i = 1; i < kN; i++) s_[i] = 1812433253u * (s_[i - 1] ^ (s_[i - 1] >> 30)) + (uint32_t)i;
+        pos_ = kN;
+    }
+    uint32_t operator()() {
+        if (pos_ == kN) twist();
+        uint32_t y = s_[pos_++];
+        y ^= y >> 11;
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        return y ^ (y >> 18);
+    }
+
+   private:
+    static constexpr int kN = 624, kM = 397;
+    void twist() {
+        for (int k = 0; k < kN; k++) {
+            const uint32_t y = (s_[k] & 0x80000000u) | (s_[(k + 1) % kN] & 0x7fffffffu);
+            s_[k] = s_[(k + kM) % kN] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+        }
+        pos_ = 0;
+    }
+    uint32_t s_[kN];
+    int pos_;
+};
+
+// uniform_int_distribution<int>(0, hi) as libstdc++ implemented it through GCC 10
+// (downscaling by the generator range; the toolchain of the reference's era).
+inline int uniform_int(Mt19937 &g, uint32_t hi) {
+    const uint64_t range = 0xFFFFFFFFull;
+    if ((uint64_t)hi == range) return (int)g();
+    const uint64_t buckets = (uint64_t)hi + 1, scale = range / buckets, limit = buckets * scale;
+    uint64_t r;
+    do r = g(); while (r >= limit);
+    return (int)(r / scale);
+}
+
+// UniformRandomGenerator::generateUniqueRandomSet(sample, k, hi): k distinct draws from
+// the closed range <0; hi>, a repeat is redrawn (uniform_random_generator.hpp:44-54)
+inline void unique_set(Mt19937 &g, int32_t *sample, uint32_t k, uint32_t hi) {
+    for (uint32_t i = 0; i < k; i++) {
+        const int v = uniform_int(g, hi);
+        bool dup = false;
+        for (uint32_t j = 0; j < i; j++) dup |= sample[j] == v;
+        if (dup) i--;
+        else sample[i] = v;
+    }
+}
+
+class ProsacSampler {
+   public:
+    // prosac_sampler.hpp:62-114 (T_N = 200000)
+    ProsacSampler(uint32_t seed, uint32_t points_size, uint32_t sample_size)
+        : rng_(seed), growth_(points_size), n_(points_size), m_(sample_size) {
+        double T_n = kGrowthMax;
+        for (uint32_t i = 0; i < m_; ++i) T_n *= (double)(m_ - i) / (n_ - i);
+        uint32_t T_prime = 1;
+        for (uint32_t i = 0; i < n_; ++i) {
+            if (i + 1 <= m_) {
+                growth_[i] = T_prime;
+                continue;
+            }
+            const double T_next = (double)(i + 1) * T_n / (i + 1 - m_);
+            growth_[i] = T_prime + (uint32_t)std::ceil(T_next - T_n);
+            T_n = T_next;
+            T_prime = growth_[i];
+        }
+        largest_ = subset_ = m_;
+        hyp_ = 1;
+    }
+    // prosac_sampler.hpp:117-172 with the current termination_length
+    void generateSample(int32_t *sample, uint32_t termination_length) {
+        if (hyp_ > kGrowthMax) {
+            unique_set(rng_, sample, m_, n_);  // closed range (reference), guarded by the caller
+            return;
+        }
+        if (subset_ > termination_length) {
+            unique_set(rng_, sample, m_, termination_length);  // closed range, SURVEY Q15
+            return;
+        }
+        if (hyp_ > growth_[subset_ - 1]) {
+            if (++subset_ > n_) subset_ = n_;
+            largest_ = std::max(largest_, subset_);
+        }
+        unique_set(rng_, sample, m_ - 1, subset_ - 2);
+        sample[m_ - 1] = (int32_t)subset_ - 1;
+        hyp_++;
+    }
+    const std::vector<uint32_t> &growth() const { return growth_; }
+    uint32_t largest() const { return largest_; }
+    uint32_t subset() const { return subset_; }
+    static constexpr uint32_t kGrowthMax = 200000;
+
+   private:
+    Mt19937 rng_;
+    std::vector<uint32_t> growth_;
+    uint32_t n_, m_, largest_, subset_, hyp_;
+};
+
+class ProsacTerminationCriteria {
+   public:
+    // prosac_termination_criteria.hpp:44-119: non-random inlier minima (beta 0.05,
+    // Psi 0.05, tabulated up to n = 1001 then held), maximality samples = 10000
+    ProsacTerminationCriteria(const std::vector<uint32_t> &growth, float desired_prob, uint32_t sample_size,
+                              uint32_t points_size, uint32_t max_iterations)
+        : std_(desired_prob, sample_size, points_size, max_iterations),
+          growth_(growth),
+          non_random_(points_size, 0),
+          maximality_(points_size, 10000),
+          n_(points_size),
+          m_(sample_size),
+          term_len_(points_size) {
+        const float psi = 0.95f, beta = 0.05f;
+        std::vector<double> pn(points_size);
+        for (size_t n = m_ + 1; n <= n_; ++n) {
+            if (n - 1 > 1000) {
+                non_random_[n - 1] = non_random_[n - 2];
+                continue;
+            }
+            std::fill(pn.begin(), pn.end(), 0.0);
+            pn[m_] = beta * std::pow((double)1 - beta, (double)n - m_ - 1) * (n - m_);
+            double prev = pn[m_];
+            for (size_t i = m_ + 2; i <= n; ++i) {
+                if (i == n) {
+                    pn[n - 1] = std::pow((double)beta, (double)n - m_);
+                    break;
+                }
+                pn[i - 1] = prev * (beta / (1 - beta)) * ((double)(n - i) / (i - m_ + 1));
+                prev = pn[i - 1];
+            }
+            double acc = 0.0;
+            uint32_t imin = 0;
+            for (size_t i = n; i >= m_ + 1; --i) {
+                acc += pn[i - 1];
+                if (acc < 1 - psi) imin = (uint32_t)i;
+                else break;
+            }
+            non_random_[n - 1] = imin;
+        }
+    }
+    uint32_t terminationLength() const { return term_len_; }
+    // prosac_termination_criteria.hpp:148-201; inlier(i) = error of point i < threshold for
+    // the new best model, largest = the sampler's largest_sample_size at that iteration
+    template <class Flags>
+    uint32_t getUpBoundIterations(uint32_t hypCount, const Flags &inlier, uint32_t largest) {
+        constexpr uint32_t kMin = 20;
+        uint32_t max_samples = maximality_[term_len_ - 1];
+        uint32_t count = 0;
+        for (uint32_t i = 0; i < kMin; i++) count += inlier(i) ? 1 : 0;
+        bool cur = inlier(kMin), nxt = false;
+        for (uint32_t i = kMin; i < n_; ++i) {
+            if (i != n_ - 1) nxt = inlier(i + 1);
+            count += cur ? 1 : 0;
+            if (non_random_[i] < count) {
+                non_random_[i] = count;
+                if (i == n_ - 1 || (cur && !nxt)) {
+                    uint32_t samples = std_.getUpBoundIterations(count, i + 1);
+                    if (i + 1 < largest) samples += hypCount - growth_[i];
+                    if (samples < maximality_[i]) {
+                        maximality_[i] = samples;
+                        if (samples < max_samples || (samples == max_samples && i + 1 >= term_len_)) {
+                            term_len_ = i + 1;
+                            max_samples = samples;
+                        }
+                    }
+                }
+            }
+            cur = nxt;
+        }
+        return max_samples;
+    }
+
+   private:
+    StandardTerminationCriteria std_;
+    std::vector<uint32_t> growth_;  // the sampler's growth function (a copy: samplers are rewound by value)
+    std::vector<uint32_t> non_random_, maximality_;
+    uint32_t n_, m_, term_len_;
+};
+
+// ---------------------------------------------------------------- SPRT
+// sprt.hpp:89-491.  The walk over the random pool runs here, in fp64 with the host libm
+// (as the reference); the device supplies each model's inlier flags in pool order as
+// 32-bit words (bit b of word w = pool position 32 w + b).
+class Sprt {
+   public:
+    struct History {
+        double epsilon, delta, A;
+        int k;
+    };
+    // ctor (sprt.hpp:89-175): pool shuffle with points_size draws of the shared stream
+    Sprt(GlibcRandom &rng, int estimator, uint32_t points_size, uint32_t sample_size, uint32_t max_iterations,
+         int max_hypothesis_test_before_sprt = 20)
+        : pool_(points_size), n_(points_size), m_(sample_size), max_iters_(max_iterations),
+          max_before_(max_hypothesis_test_before_sprt) {
+        for (uint32_t i = 0; i < n_; i++) pool_[i] = i;
+        int max = (int)n_;
+        for (uint32_t i = 0; i < n_; i++) {
+            const uint32_t r = rng.next() % (uint32_t)max;
+            const uint32_t t = pool_[r];
+            max--;
+            pool_[r] = pool_[max];
+            pool_[max] = t;
+        }
+        double eps0, delta0;
+        switch (estimator) {
+            case 2: delta0 = 0.01; eps0 = 0.1; t_M_ = 200; m_S_ = 1; break;        // homography
+            case 3: delta0 = 0.05; eps0 = 0.2; t_M_ = 200; m_S_ = 2.48; break;     // fundamental
+            case 4: delta0 = 0.05; eps0 = 0.2; t_M_ = 300; m_S_ = 4; break;        // essential
+            default: delta0 = 0.0001; eps0 = 0.001; t_M_ = 100; m_S_ = 1; break;   // line2d
+        }
+        hist_.push_back(History{eps0, delta0, thresholdA(eps0, delta0), 0});
+    }
+    const std::vector<uint32_t> &pool() const { return pool_; }
+    size_t histories() const { return hist_.size(); }
+    double thresholdA0() const { return hist_[0].A; }
+
+    // verifyModelAndGetModelScore (sprt.hpp:191-317).  words = the model's pool-order
+    // flags; count/score are written when the reference writes them.
+    bool verify(const uint32_t *words, int current_hypothese, uint32_t maximum_score, int &count, float &score) {
+        const History &h = hist_[cur_];
+        const double epsilon = h.epsilon, delta = h.delta, A = h.A;
+        const double up = delta / epsilon, down = (1 - delta) / (1 - epsilon);
+        double lambda = 1;
+        uint32_t tested = 0, inl = 0;
+        bool good = true;
+        for (tested = 0; tested < n_; tested++) {
+            if (idx_ >= n_) idx_ = 0;
+            const bool in = (words[idx_ >> 5] >> (idx_ & 31)) & 1u;
+            const double next = in ? lambda * up : lambda * down;
+            inl += in ? 1 : 0;
+            idx_++;
+            if (next > A) {
+                good = false;
+                tested++;
+                break;
+            }
+            lambda = next;
+        }
+        if (good) {
+            count = (int)inl;
+            score = (float)count;
+        } else if (current_hypothese < max_before_) {
+            uint32_t after = 0;
+            for (uint32_t p = tested; p < n_; p++) {
+                if (idx_ >= n_) idx_ = 0;
+                after += (words[idx_ >> 5] >> (idx_ & 31)) & 1u;
+                idx_++;
+            }
+            count = (int)(inl + after);
+            score = (float)count;
+        }
+        if (good) {
+            if (inl > maximum_score) {
+                const double eps = (float)inl / n_;
+                push(eps, delta, current_hypothese);
+            }
+        } else {
+            const float dest = (float)inl / tested;
+            if (dest > 0 && std::fabs(delta - dest) / delta > 0.05) push(epsilon, dest, current_hypothese);
+        }
+        return good;
+    }
+
+    // getUpperBoundIterations (sprt.hpp:371-393)
+    uint32_t getUpperBoundIterations(int inliers_size) const {
+        const double epsilon = (double)inliers_size / n_;
+        const double P_g = std::pow(epsilon, m_);
+        double log_eta = 0;
+        for (uint32_t t = 0; t < cur_; t++) {
+            const double h = exponentH(hist_[t].epsilon, epsilon, hist_[t].delta);
+            log_eta += std::log(1 - P_g * (1 - std::pow(hist_[t].A, -h))) * hist_[t].k;
+        }
+        const double num = std::log(0.05) - log_eta;
+        if (num >= 0) return 0;
+        const double den = std::log(1 - P_g * (1 - 1 / hist_[cur_].A));
+        if (std::isnan(den) || std::fabs(den) < 0.00001) return max_iters_;
+        const uint32_t k = (uint32_t)(num / den);
+        return std::min(k, max_iters_);
+    }
+
+   private:
+    void push(double eps, double delta, int current_hypothese) {
+        hist_.push_back(History{eps, delta, thresholdA(eps, delta), current_hypothese - last_update_});
+        last_update_ = current_hypothese;
+        cur_++;
+    }
+    // estimateThresholdA (sprt.hpp:332-355)
+    double thresholdA(double epsilon, double delta) const {
+        const double C = (1 - delta) * std::log((1 - delta) / (1 - epsilon)) + delta * (std::log(delta / epsilon));
+        const double K = (t_M_ * C) / m_S_ + 1;
+        double prev = K, An = K;
+        for (int i = 0; i < 10; ++i) {
+            An = K + std::log(prev);
+            if (std::fabs(An - prev) < 1.5e-8) break;
+            prev = An;
+        }
+        return An;
+    }
+    // computeExponentH (sprt.hpp:442-491)
+    static double exponentH(double epsilon, double epsilon_new, double delta) {
+        const double a = std::log(delta / epsilon);
+        const double b = std::log((1 - delta) / (1 - epsilon));
+        const double x0 = std::log(1 / (1 - epsilon_new)) / b;
+        const double v0 = epsilon_new * std::exp(x0 * a);
+        const double x1 = std::log((1 - 2 * v0) / (1 - epsilon_new)) / b;
+        const double v1 = epsilon_new * std::exp(x1 * a) + (1 - epsilon_new) * std::exp(x1 * b);
+        const double h = x0 - (x0 - x1) / (1 + v0 - v1) * v0;
+        return std::isnan(h) ? 0 : h;
+    }
+
+    std::vector<uint32_t> pool_;
+    std::vector<History> hist_;
+    uint32_t n_, m_, max_iters_, idx_ = 0, cur_ = 0;
+    int max_before_, last_update_ = 0;
+    double t_M_ = 0, m_S_ = 0;
 };
 
 }  // namespace usac

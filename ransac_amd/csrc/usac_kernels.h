@@ -47,6 +47,14 @@ hipError_t launch_inliers_f(hipStream_t st, const float4 *pts, uint32_t n, const
 hipError_t launch_nonminimal_f(hipStream_t st, const float4 *pts, const int32_t *idx, uint32_t n, float4 *q,
                                double *partial, float *ws, float *model_out, int32_t *ok);
 
+// SPRT parity support (kernels_sprt.hip): points permuted into pool order, and per-model
+// pool-order inlier words (words[w * row_stride + row], bit b = position 32 w + b)
+hipError_t launch_gather_points(hipStream_t st, const void *pts, uint32_t cols, const uint32_t *idx, uint32_t n,
+                                void *out);
+hipError_t launch_pool_mask(hipStream_t st, int estimator, const void *pool_pts, uint32_t n, const float *models,
+                            size_t stride, const uint32_t *list, const uint32_t *list_n, uint32_t kmax, float thr,
+                            uint32_t *words, uint32_t row_stride);
+
 hipError_t launch_inliers_h(hipStream_t st, const float4 *pts, uint32_t n, const float *model, float thr,
                             int32_t *idx, int32_t *count, float *sum);
 hipError_t launch_inliers_line(hipStream_t st, const float2 *pts, uint32_t n, const float *model, float thr,
