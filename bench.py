@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--threshold", type=float, default=2.0)
     ap.add_argument("--chunks", type=int, default=8)
     ap.add_argument("--dlt", choices=["thin", "nullspace"], default="thin")
+    ap.add_argument("--sprt", action="store_true",
+                    help="batch SPRT verification (reference initial epsilon/delta for the estimator)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--seed", type=int, default=1)
     return ap.parse_args()
@@ -150,10 +152,15 @@ def main():
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(world, rank, uid[0])
     B = args.batch
+    if args.sprt:
+        ctx.set_sprt(True, seed=args.seed)
     models_per_hyp = 1.0
     if fund:  # occupied model slots per sample of the device sampler's stream (one batch)
+        ctx.set_sprt(False)
         c0, _, _ = ctx.hypothesize_score(B=B, seed=args.seed + 1000, first_hyp=0, thr=args.threshold)
         models_per_hyp = float((c0 >= 0).sum()) / B
+        if args.sprt:
+            ctx.set_sprt(True, seed=args.seed)
 
     def sync():
         ctx.sync()
@@ -188,6 +195,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    tested_per_batch = ctx.sprt_tested() if args.sprt else None
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -199,11 +207,16 @@ def main():
         n = args.points
         m = 7 if fund else 4
         # N*S per scored model + m*4 + k*(36+8)
-        bytes_per_hyp = models_per_hyp * 16 * n + m * 4 + models_per_hyp * (36 + 8)
+        if args.sprt:  # with SPRT, the bytes actually tested (16 B x tested points)
+            bytes_per_hyp = 16.0 * tested_per_batch / B + m * 4 + models_per_hyp * (36 + 8)
+        else:
+            bytes_per_hyp = models_per_hyp * 16 * n + m * 4 + models_per_hyp * (36 + 8)
         avg_score_ms = float(np.mean(score_ms))
         achieved = bytes_per_hyp * B / (avg_score_ms * 1e-3) / 1e9
         kname = ("void usac::k_score_f<%d>" if fund else "void usac::k_score_hf<%d, false>") % args.chunks
-        traffic = measured_traffic(kname, n, B) if not fund else None
+        traffic = measured_traffic(kname, n, B) if not (fund or args.sprt) else None
+        kshort = ("k_score_sprt<%d>" % (3 if fund else 2)) if args.sprt else \
+            (("k_score_f<%d>" if fund else "k_score_hf<%d,false>") % args.chunks)
         out = {
             "metric": "model hypotheses/sec (sample+solve+score) and inlier-count match vs ref",
             "value": value,
@@ -218,17 +231,20 @@ def main():
             "dtype": "f32",
             "data": ("synthetic (SURVEY §8(d) cfg3 generator: two views, 30% inliers, 0.5 px noise)" if fund else
                      "synthetic (SURVEY §8(d) cfg2 generator: 30% inliers, 1 px noise, 70% uniform outliers)"),
-            "config": {"workload": ("cfg3 without SPRT: Fundamental_estimator (7-pt, oriented filter, Sampson) + "
+            "config": {"workload": ("cfg3%s: Fundamental_estimator (7-pt, oriented filter, Sampson) + "
                                     "Uniform sampler (device xorshift), %d correspondences, %d-hypothesis batch per "
-                                    "GPU, %.3f models/sample" % (n, B, models_per_hyp)) if fund else
-                                   ("cfg2: Homography_estimator (4-pt DLT, %s) + Uniform sampler (device "
-                                    "xorshift), %d correspondences, %d-hypothesis batch per GPU" % (args.dlt, n, B)),
+                                    "GPU, %.3f models/sample" % (" + batch SPRT" if args.sprt else " without SPRT", n, B,
+                                                                 models_per_hyp)) if fund else
+                                   ("cfg2%s: Homography_estimator (4-pt DLT, %s) + Uniform sampler (device "
+                                    "xorshift), %d correspondences, %d-hypothesis batch per GPU" %
+                                    (" + batch SPRT" if args.sprt else "", args.dlt, n, B)),
                        "n_points": n, "batch_per_gpu": B, "threshold": args.threshold,
                        "score_chunks": args.chunks, "parallelism": "hypothesis-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
                          "traffic_unit": "bytes/launch", "traffic_source": traffic[1] if traffic else None,
-                         "kernel": ("k_score_f<%d>" if fund else "k_score_hf<%d,false>") % args.chunks,
+                         "kernel": kshort, "sprt": bool(args.sprt),
+                         "sprt_points_tested_per_batch": tested_per_batch,
                          "kernel_ms": avg_score_ms, "models_per_hypothesis": models_per_hyp,
                          "algorithmic_bytes_per_hypothesis": bytes_per_hyp,
                          "hypotheses_per_launch": B,

@@ -26,6 +26,8 @@
  *                                  batch (the body of ransac.cpp:58-139)
  *   usac_std_termination           StandardTerminationCriteria::getUpBoundIterations
  *                                  (standard_termination_criteria.hpp:52-62)
+ *   usac_set_sprt / usac_sprt_tested  SPRT::verifyModelAndGetModelScore as a batch test
+ *                                  (sprt.hpp:191-317, 332-355)
  *   usac_prosac_samples            ProsacSampler::generateSample (prosac_sampler.hpp:117-172)
  *   usac_sprt_pool                 SPRT ctor pool + A0 (sprt.hpp:89-175)
  *   usac_ransac_run                Ransac::run + RansacOutput (ransac.cpp:14-238,
@@ -151,6 +153,17 @@ int usac_set_score_chunks(usac_ctx *ctx, int chunks);
 /* Homography score kernel: 0 = guard-band fast path (default), 1 = exact reference
  * expression for every pair (A/B and debugging; same results). */
 int usac_set_score_variant(usac_ctx *ctx, int variant);
+
+/* Throughput SPRT (sprt.hpp:191-317 as a batch test): with enable != 0 every later
+ * batch (usac_hypothesize_score / _async) verifies each model by the SPRT with fixed
+ * (epsilon, delta) -- <= 0 selects the reference's initial values for the estimator
+ * (sprt.hpp:106-150) -- and threshold A = estimateThresholdA(epsilon, delta), over the
+ * SPRT pool of srandom(seed) (sprt.hpp:93-104).  Rejected models get count -1; accepted
+ * ones count = inliers over all points, score = (float)count (sprt.hpp:276-281).
+ * usac_ransac_run always replays the exact sequential SPRT instead. */
+int usac_set_sprt(usac_ctx *ctx, int enable, uint32_t seed, double epsilon, double delta);
+/* pool points the SPRT tested in the last batch (the scoring work actually done) */
+int usac_sprt_tested(usac_ctx *ctx, uint64_t *points_tested);
 
 /* ---- loop --------------------------------------------------------------------- */
 uint32_t usac_std_termination(uint32_t inliers, uint32_t points_size, uint32_t sample_size, float desired_prob,

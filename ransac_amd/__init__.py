@@ -80,7 +80,7 @@ ABI_SYMBOLS = [
     "usac_num_points", "usac_estimate_models", "usac_score_models", "usac_get_inliers", "usac_nonminimal",
     "usac_hypothesize_score", "usac_hypothesize_async", "usac_fetch_best", "usac_sync", "usac_last_timings",
     "usac_set_score_chunks", "usac_set_score_variant", "usac_std_termination", "usac_ransac_run", "usac_uniform_samples",
-    "usac_prosac_samples", "usac_sprt_pool",
+    "usac_prosac_samples", "usac_sprt_pool", "usac_set_sprt", "usac_sprt_tested",
     "usac_comm_unique_id", "usac_comm_init", "usac_allgather_records", "usac_merge_records",
 ]
 
@@ -134,6 +134,8 @@ def lib():
                                                ctypes.c_uint32, i32p]),
         "usac_sprt_pool": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, u32p,
                                           _P(ctypes.c_double)]),
+        "usac_set_sprt": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_double, ctypes.c_double]),
+        "usac_sprt_tested": (ctypes.c_int, [_vp, _P(ctypes.c_uint64)]),
         "usac_comm_unique_id": (ctypes.c_int, [u8p]),
         "usac_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, u8p]),
         "usac_allgather_records": (ctypes.c_int, [_vp, _P(Record), _P(Record)]),
@@ -302,6 +304,16 @@ class Context:
                                              ctypes.c_float(thr), _ptr(c, ctypes.c_int32), _ptr(sm, ctypes.c_float),
                                              ctypes.byref(best)), "hypothesize_score")
         return c, sm, best.as_dict()
+
+    def set_sprt(self, enable, seed=1, epsilon=0.0, delta=0.0):
+        """Batch SPRT verification for the throughput entry points (reference defaults when
+        epsilon / delta are 0)."""
+        self._check(lib().usac_set_sprt(self._h, 1 if enable else 0, seed, epsilon, delta), "set_sprt")
+
+    def sprt_tested(self):
+        t = ctypes.c_uint64(0)
+        self._check(lib().usac_sprt_tested(self._h, ctypes.byref(t)), "sprt_tested")
+        return int(t.value)
 
     def hypothesize_async(self, B, seed, first_hyp, thr):
         self._check(lib().usac_hypothesize_async(self._h, B, seed, first_hyp, ctypes.c_float(thr)),

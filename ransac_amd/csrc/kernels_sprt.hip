@@ -102,3 +102,201 @@ hipError_t launch_pool_mask(hipStream_t st, int estimator, const void *pool_pts,
 }
 
 }  // namespace usac
+
+namespace usac {
+
+// Throughput SPRT ("batch-native"): every model of a batch is verified with
+// the same test (log A, log(delta/eps), log((1-delta)/(1-eps)) fixed for the batch, from
+// the host's current SPRT history), walking the pool-ordered points from a wave-uniform
+// start (pool position (block * 7919) mod n, wrapping) -- the reference's rolling pool
+// index places each model's test at an arbitrary pool position too.  The log-likelihood
+// ratio L is accumulated in fp32; a model is rejected at the first point where L > log A
+// (count -1, never a best).  A model that passes all n points is accepted: count = its
+// inliers over all points (the reference's `tested_inliers`), score = (float)count
+// (sprt.hpp:276-281).
+//
+// Two phases, because nearly every model is rejected within a few dozen points while the
+// few good ones must walk all n:
+//   phase 1 (lanes = models): the first kHead pool points, wave exit once all lanes
+//            decided; lanes still undecided are appended to a survivor list with (L, count);
+//   phase 2 (a workgroup per survivor, lanes = points): the remaining points split into
+//            256 contiguous chunks; each thread reduces its chunk to (count, ΣΔL, max prefix
+//            of ΔL); thread 0 combines the chunks in pool order -- rejected iff some prefix
+//            exceeds log A, the sequential test re-associated (fp32).
+constexpr uint32_t kHead = 256;
+
+template <int EST>
+__device__ __forceinline__ float sprt_error(const float *m, const void *pts, uint32_t p) {
+    if constexpr (EST == 1) {
+        const float2 q = static_cast<const float2 *>(pts)[p];
+        return line2d_error(m[0], m[1], m[2], q.x, q.y);
+    } else if constexpr (EST == 2) {
+        const float4 q = static_cast<const float4 *>(pts)[p];
+        return homography_error(m, m + 9, q.x, q.y, q.z, q.w);
+    } else {
+        const float4 q = static_cast<const float4 *>(pts)[p];
+        return fundamental_error(m, q.x, q.y, q.z, q.w);
+    }
+}
+
+struct SprtSurvivor {
+    uint32_t slot, start;  // model slot, pool position where phase 2 begins
+    float L;
+    int cnt;
+};
+
+template <int EST>
+__global__ __launch_bounds__(64) void k_sprt_head(const void *__restrict__ pool_pts, uint32_t n,
+                                                  const float *__restrict__ models, size_t stride,
+                                                  const uint32_t *__restrict__ list,
+                                                  const uint32_t *__restrict__ list_n, uint32_t kmax, float thr,
+                                                  float log_up, float log_down, float log_A,
+                                                  int32_t *__restrict__ counts, float *__restrict__ sums,
+                                                  uint32_t *__restrict__ tested_total, SprtSurvivor *__restrict__ surv,
+                                                  uint32_t *__restrict__ surv_n) {
+    constexpr int NC = EST == 1 ? 3 : EST == 2 ? 18 : 9;
+    const uint32_t K = list ? __builtin_amdgcn_readfirstlane(*list_n) : kmax;
+    const uint32_t i0 = blockIdx.x * 64;
+    if (i0 >= K) return;
+    const uint32_t row = i0 + threadIdx.x;
+    const uint32_t rc = row < K ? row : K - 1;
+    const uint32_t slot = list ? list[rc] : rc;
+    float m[NC];
+#pragma unroll
+    for (int k = 0; k < NC; k++) m[k] = models[(size_t)k * stride + slot];
+    const uint32_t start = (uint32_t)(((uint64_t)blockIdx.x * 7919u) % n);
+    const uint32_t head = n < kHead ? n : kHead;
+    float L = 0.f;
+    int cnt = 0;
+    bool live = row < K;
+    uint32_t tested = 0;
+    uint32_t p = start;
+    for (uint32_t t = 0; t < head; t += 4) {
+        // four independent residuals per step (pool positions wave-uniform: scalar loads)
+        float e[4];
+        uint32_t q = p;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            e[u] = t + u < head ? sprt_error<EST>(m, pool_pts, q) : __builtin_nanf("");
+            if (++q == n) q = 0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (live && t + u < head) {
+                const bool in = e[u] < thr;
+                cnt += in ? 1 : 0;
+                L += in ? log_up : log_down;
+                tested++;
+                if (L > log_A) live = false;
+            }
+        }
+        p = q;
+        if (!__any(live)) break;
+    }
+    if (row < K) {
+        if (!live) {
+            counts[slot] = -1;
+            sums[slot] = 0.f;
+        } else if (head == n) {
+            counts[slot] = cnt;
+            sums[slot] = (float)cnt;
+        } else {
+            const uint32_t k = atomicAdd(surv_n, 1u);
+            surv[k] = SprtSurvivor{slot, (start + head) % n, L, cnt};
+        }
+    }
+    uint32_t v = row < K ? tested : 0;
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (threadIdx.x == 0 && tested_total) atomicAdd(tested_total, v);
+}
+
+template <int EST>
+__global__ __launch_bounds__(256) void k_sprt_tail(const void *__restrict__ pool_pts, uint32_t n,
+                                                   const float *__restrict__ models, size_t stride, float thr,
+                                                   float log_up, float log_down, float log_A,
+                                                   const SprtSurvivor *__restrict__ surv,
+                                                   const uint32_t *__restrict__ surv_n, int32_t *__restrict__ counts,
+                                                   float *__restrict__ sums, uint32_t *__restrict__ tested_total) {
+    constexpr int NC = EST == 1 ? 3 : EST == 2 ? 18 : 9;
+    __shared__ int s_cnt[256];
+    __shared__ float s_sum[256], s_max[256];
+    const uint32_t ns = *surv_n;
+    const uint32_t rest = n - kHead;  // launched only when n > kHead
+    const uint32_t per = (rest + 255) / 256;
+    for (uint32_t k = blockIdx.x; k < ns; k += gridDim.x) {
+        const SprtSurvivor sv = surv[k];
+        float m[NC];
+#pragma unroll
+        for (int c = 0; c < NC; c++) m[c] = models[(size_t)c * stride + sv.slot];
+        const uint32_t b = threadIdx.x * per;
+        const uint32_t e = b + per < rest ? b + per : rest;
+        int cnt = 0;
+        float acc = 0.f, mx = -INFINITY;
+        uint32_t p = sv.start + (b < rest ? b : rest);
+        if (p >= n) p -= n;
+        for (uint32_t t = b; t < e; t++) {
+            const bool in = sprt_error<EST>(m, pool_pts, p) < thr;
+            cnt += in ? 1 : 0;
+            acc += in ? log_up : log_down;
+            mx = fmaxf(mx, acc);
+            if (++p == n) p = 0;
+        }
+        s_cnt[threadIdx.x] = cnt;
+        s_sum[threadIdx.x] = acc;
+        s_max[threadIdx.x] = mx;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float L = sv.L;
+            int c = sv.cnt;
+            bool good = true;
+            uint32_t tested = kHead;
+            for (int j = 0; j < 256; j++) {
+                const uint32_t cb = j * per, ce = cb + per < rest ? cb + per : rest;
+                if (cb >= ce) break;
+                if (L + s_max[j] > log_A) {  // rejected inside chunk j
+                    good = false;
+                    tested += ce - cb;  // upper bound of the points the sequential test reads
+                    break;
+                }
+                L += s_sum[j];
+                c += s_cnt[j];
+                tested += ce - cb;
+            }
+            counts[sv.slot] = good ? c : -1;
+            sums[sv.slot] = good ? (float)c : 0.f;
+            if (tested_total) atomicAdd(tested_total, tested - kHead);
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_score_sprt(hipStream_t st, int estimator, const void *pool_pts, uint32_t n, const float *models,
+                             size_t stride, const uint32_t *list, const uint32_t *list_n, uint32_t kmax, float thr,
+                             float log_up, float log_down, float log_A, int32_t *counts, float *sums,
+                             uint32_t *tested_total, void *surv, uint32_t *surv_n) {
+    hipError_t err = hipMemsetAsync(surv_n, 0, sizeof(uint32_t), st);
+    if (err != hipSuccess) return err;
+    const dim3 grid((kmax + 63) / 64);
+    SprtSurvivor *sv = static_cast<SprtSurvivor *>(surv);
+    const dim3 tgrid(kmax < 2048 ? (kmax ? kmax : 1) : 2048);
+#define SS(E)                                                                                                         \
+    do {                                                                                                              \
+        hipLaunchKernelGGL(k_sprt_head<E>, grid, dim3(64), 0, st, pool_pts, n, models, stride, list, list_n, kmax, thr, \
+                           log_up, log_down, log_A, counts, sums, tested_total, sv, surv_n);                          \
+        if (n > kHead)                                                                                                \
+            hipLaunchKernelGGL(k_sprt_tail<E>, tgrid, dim3(256), 0, st, pool_pts, n, models, stride, thr, log_up,    \
+                               log_down, log_A, sv, surv_n, counts, sums, tested_total);                             \
+    } while (0)
+    switch (estimator) {
+        case USAC_LINE2D: SS(1); break;
+        case USAC_HOMOGRAPHY: SS(2); break;
+        case USAC_FUNDAMENTAL: SS(3); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef SS
+    return hipGetLastError();
+}
+
+size_t sprt_survivor_bytes() { return sizeof(SprtSurvivor); }
+
+}  // namespace usac

@@ -63,6 +63,11 @@ struct usac_ctx {
     DevBuf samples, models, counts, sums, best, hostmodels, argmax_part;
     DevBuf list, list_n;    // fundamental: occupied model slots (compacted) and their number
     DevBuf pool_idx, pool_pts, masks;  // SPRT parity path: pool order, permuted points, flag words
+    // throughput SPRT (usac_set_sprt): batch-fixed test on the pool-ordered points
+    bool sprt_on = false;
+    float sprt_log_up = 0.f, sprt_log_down = 0.f, sprt_log_A = 0.f;
+    double sprt_A = 0.0;
+    DevBuf sprt_pts, sprt_tested, sprt_surv, sprt_surv_n;
     uint32_t spk = 1;       // model slots per hypothesis (3 for the 7-point solver)
     // single-model / polish buffers
     DevBuf one_model, inl_idx, inl_cnt, inl_sum, q, partial, ws, nm_model, nm_ok;
@@ -151,6 +156,18 @@ hipError_t enqueue_solve(usac_ctx *c, const int32_t *samples_dev, uint32_t B, ui
 // chunks == 1 is the parity configuration: per-hypothesis sums are the exact sequential
 // fp32 sums of the reference.  chunks > 1 re-associates Σerr across chunks (counts exact).
 hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
+    if (c->sprt_on) {
+        hipError_t e = hipMemsetAsync(c->sprt_tested.p, 0, sizeof(uint32_t), c->stream);
+        if (e != hipSuccess) return e;
+        const uint32_t S = B * c->spk;
+        e = c->sprt_surv.reserve(usac::sprt_survivor_bytes() * (size_t)S);
+        if (e != hipSuccess) return e;
+        return usac::launch_score_sprt(c->stream, c->estimator, c->sprt_pts.p, c->n, c->models.as<float>(),
+                                       is_f(c) ? 3 * (size_t)B : (size_t)B, is_f(c) ? c->list.as<uint32_t>() : nullptr,
+                                       is_f(c) ? c->list_n.as<uint32_t>() : nullptr, S, thr, c->sprt_log_up,
+                                       c->sprt_log_down, c->sprt_log_A, c->counts.as<int32_t>(), c->sums.as<float>(),
+                                       c->sprt_tested.as<uint32_t>(), c->sprt_surv.p, c->sprt_surv_n.as<uint32_t>());
+    }
     if (is_f(c))  // the occupied slots of the last solve
         return usac::launch_score_f(c->stream, chunks, c->pts.as<float4>(), c->n, c->models.as<float>(), 3 * (size_t)B,
                                     c->list.as<uint32_t>(), c->list_n.as<uint32_t>(), 3 * B, thr,
@@ -268,7 +285,8 @@ void usac_destroy(usac_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
     for (DevBuf *b : {&c->pts, &c->rec, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
-                      &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->one_model,
+                      &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
+                      &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->one_model,
                       &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok,
                       &c->rec_send, &c->rec_all})
         b->release();
@@ -478,6 +496,46 @@ int usac_uniform_samples(uint32_t seed, uint32_t n_points, uint32_t m, uint32_t 
     return USAC_OK;
 }
 
+int usac_set_sprt(usac_ctx *c, int enable, uint32_t seed, double epsilon, double delta) {
+    if (!c) return USAC_ERR_ARG;
+    if (!enable) {
+        c->sprt_on = false;
+        return USAC_OK;
+    }
+    if (c->estimator == USAC_ESSENTIAL) return fail(c, USAC_ERR_UNSUPPORTED, "SPRT: estimator not supported");
+    HIP_TRY(c, hipSetDevice(c->device));
+    usac::GlibcRandom g(seed);
+    usac::Sprt sp(g, c->estimator, c->n, c->m, 10000);
+    const double eps = epsilon > 0 ? epsilon : sp.epsilon0(), del = delta > 0 ? delta : sp.delta0();
+    if (!(eps < 1.0) || !(del < 1.0)) return fail(c, USAC_ERR_ARG, "SPRT: epsilon and delta must be in (0, 1)");
+    c->sprt_A = sp.thresholdA(eps, del);
+    c->sprt_log_up = (float)log(del / eps);
+    c->sprt_log_down = (float)log((1 - del) / (1 - eps));
+    c->sprt_log_A = (float)log(c->sprt_A);
+    HIP_TRY(c, c->pool_idx.reserve(sizeof(uint32_t) * c->n));
+    HIP_TRY(c, c->sprt_pts.reserve(sizeof(float) * c->cols * (size_t)c->n));
+    HIP_TRY(c, c->sprt_tested.reserve(sizeof(uint32_t)));
+    HIP_TRY(c, c->sprt_surv_n.reserve(sizeof(uint32_t)));
+    HIP_TRY(c, hipMemcpyAsync(c->pool_idx.p, sp.pool().data(), sizeof(uint32_t) * c->n, hipMemcpyHostToDevice,
+                              c->stream));
+    HIP_TRY(c, usac::launch_gather_points(c->stream, c->pts.p, c->cols, c->pool_idx.as<uint32_t>(), c->n,
+                                          c->sprt_pts.p));
+    HIP_TRY(c, hipMemsetAsync(c->sprt_tested.p, 0, sizeof(uint32_t), c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    c->sprt_on = true;
+    return USAC_OK;
+}
+
+int usac_sprt_tested(usac_ctx *c, uint64_t *points_tested) {
+    if (!c || !points_tested) return USAC_ERR_ARG;
+    if (!c->sprt_on) return fail(c, USAC_ERR_ARG, "SPRT not enabled");
+    uint32_t t = 0;
+    HIP_TRY(c, hipMemcpyAsync(&t, c->sprt_tested.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    *points_tested = t;
+    return USAC_OK;
+}
+
 int usac_prosac_samples(uint32_t seed, uint32_t n_points, uint32_t m, uint32_t count, uint32_t termination_length,
                         int32_t *out) {
     if (!out || m < 2 || n_points < m || termination_length == 0 || count > usac::ProsacSampler::kGrowthMax)
@@ -528,6 +586,17 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
     if (rc) return rc;
     const int saved_mode = c->dlt_mode;
     c->dlt_mode = prm->dlt_mode;
+    const bool saved_sprt = c->sprt_on;  // the replay verifies exactly; the batch test is off
+    c->sprt_on = false;
+    struct Restore {
+        usac_ctx *c;
+        int mode;
+        bool sprt;
+        ~Restore() {
+            c->dlt_mode = mode;
+            c->sprt_on = sprt;
+        }
+    } restore{c, saved_mode, saved_sprt};
     const uint32_t n = c->n, m = c->m, spk = c->spk;
     const float thr = prm->threshold;
 
@@ -714,7 +783,6 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
     out->prosac_term_len = prosac ? pterm->terminationLength() : n;
     memcpy(out->minimal_model, best_model, sizeof(best_model));
     out->minimal_inliers = best.inlier_number;
-    c->dlt_mode = saved_mode;
     if (best.inlier_number == 0) {
         memcpy(out->model, best_model, sizeof(best_model));
         return fail(c, USAC_ERR_NO_MODEL, "best score is 0 (ransac.cpp:143-147)");

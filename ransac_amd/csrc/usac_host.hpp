@@ -337,6 +337,8 @@ class Sprt {
     const std::vector<uint32_t> &pool() const { return pool_; }
     size_t histories() const { return hist_.size(); }
     double thresholdA0() const { return hist_[0].A; }
+    double epsilon0() const { return hist_[0].epsilon; }
+    double delta0() const { return hist_[0].delta; }
 
     // verifyModelAndGetModelScore (sprt.hpp:191-317).  words = the model's pool-order
     // flags; count/score are written when the reference writes them.
@@ -402,12 +404,6 @@ class Sprt {
         return std::min(k, max_iters_);
     }
 
-   private:
-    void push(double eps, double delta, int current_hypothese) {
-        hist_.push_back(History{eps, delta, thresholdA(eps, delta), current_hypothese - last_update_});
-        last_update_ = current_hypothese;
-        cur_++;
-    }
     // estimateThresholdA (sprt.hpp:332-355)
     double thresholdA(double epsilon, double delta) const {
         const double C = (1 - delta) * std::log((1 - delta) / (1 - epsilon)) + delta * (std::log(delta / epsilon));
@@ -419,6 +415,13 @@ class Sprt {
             prev = An;
         }
         return An;
+    }
+
+   private:
+    void push(double eps, double delta, int current_hypothese) {
+        hist_.push_back(History{eps, delta, thresholdA(eps, delta), current_hypothese - last_update_});
+        last_update_ = current_hypothese;
+        cur_++;
     }
     // computeExponentH (sprt.hpp:442-491)
     static double exponentH(double epsilon, double epsilon_new, double delta) {

@@ -55,6 +55,15 @@ hipError_t launch_pool_mask(hipStream_t st, int estimator, const void *pool_pts,
                             size_t stride, const uint32_t *list, const uint32_t *list_n, uint32_t kmax, float thr,
                             uint32_t *words, uint32_t row_stride);
 
+// throughput SPRT (batch-fixed test): counts -1 for rejected models, tested_total (nullable)
+// accumulates the pool points tested
+// surv: kmax * sprt_survivor_bytes() scratch, surv_n: one uint32 (zeroed by the launcher)
+hipError_t launch_score_sprt(hipStream_t st, int estimator, const void *pool_pts, uint32_t n, const float *models,
+                             size_t stride, const uint32_t *list, const uint32_t *list_n, uint32_t kmax, float thr,
+                             float log_up, float log_down, float log_A, int32_t *counts, float *sums,
+                             uint32_t *tested_total, void *surv, uint32_t *surv_n);
+size_t sprt_survivor_bytes();
+
 hipError_t launch_inliers_h(hipStream_t st, const float4 *pts, uint32_t n, const float *model, float thr,
                             int32_t *idx, int32_t *count, float *sum);
 hipError_t launch_inliers_line(hipStream_t st, const float2 *pts, uint32_t n, const float *model, float thr,

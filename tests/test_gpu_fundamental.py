@@ -141,3 +141,35 @@ def test_throughput_batch_full_size(usac, oracle):
     assert oc == best["inliers"] == c.max()
     # chunked Σ may reorder exact count ties; the count of the batch best is exact
     assert rec.inliers == best["inliers"]
+
+
+@pytest.mark.parametrize("kind", ["F", "H"])
+def test_batch_sprt_accepts_exact_counts(usac, oracle, kind):
+    """Throughput SPRT: accepted models carry their exact full inlier count (score = count),
+    rejected ones -1; good all-inlier samples survive, most random models are rejected."""
+    if kind == "F":
+        pts, M, inl = _cfg3(n=4000, seed=6)
+        est_id, okind, m = usac.ESTIMATOR.Fundamental, oracle.FUNDAMENTAL, 7
+    else:
+        pts, M, inl = synthetic.homography_points(n=4000, inlier_ratio=0.3, seed=6)
+        est_id, okind, m = usac.ESTIMATOR.Homography, oracle.HOMOGRAPHY, 4
+    rng = np.random.default_rng(1)
+    idx = np.where(inl)[0]
+    good = np.stack([rng.choice(idx, m, replace=False) for _ in range(64)]).astype(np.int32)
+    samples = np.concatenate([oracle.uniform_samples(21, len(pts), m, 4096), good])
+    est = oracle.Estimator(okind, pts)
+    with usac.Context(est_id, pts) as ctx:
+        ctx.set_sprt(True, seed=1)
+        c, s, best = ctx.hypothesize_score(samples=samples, thr=2.0)
+        tested = ctx.sprt_tested()
+        ctx.set_sprt(False)
+        cf, sf, _ = ctx.hypothesize_score(samples=samples, thr=2.0)
+    acc = c >= 0
+    occupied = cf >= 0
+    assert (acc <= occupied).all()
+    assert (c[acc] == cf[acc]).all() and (s[acc] == c[acc].astype(np.float32)).all()
+    assert acc.sum() >= 1 and acc.sum() <= 0.2 * occupied.sum()
+    assert best["valid"] and best["inliers"] == c.max()
+    oc, _ = est.quality(best["model"], 2.0)
+    assert oc == best["inliers"]
+    assert tested < 0.2 * occupied.sum() * len(pts)
