@@ -80,6 +80,8 @@ def lib():
         L.orc_score_models.argtypes = [ctypes.c_void_p, _f32p, ctypes.c_int, ctypes.c_float, _i32p, _f32p]
         L.orc_est_max_models.argtypes = [ctypes.c_void_p]
         L.orc_cubic_roots.argtypes = [ctypes.c_double] * 4 + [ctypes.POINTER(ctypes.c_double)]
+        L.orc_real_roots.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+        L.orc_e5_candidates.argtypes = [ctypes.c_void_p, _i32p, _f32p, _i32p]
         L.orc_estimate_batch.argtypes = [ctypes.c_void_p, _i32p, ctypes.c_int, _f32p, _i32p]
         L.orc_gt_inliers_homography.argtypes = [_f32p, ctypes.c_uint, _f32p, ctypes.c_float]
         L.orc_std_termination.argtypes = [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, ctypes.c_float, ctypes.c_uint]
@@ -163,7 +165,7 @@ class Estimator:
 
     @property
     def m(self):
-        return {LINE2D: 2, FUNDAMENTAL: 7}.get(self.kind, 4)
+        return {LINE2D: 2, FUNDAMENTAL: 7, ESSENTIAL: 5}.get(self.kind, 4)
 
     @property
     def max_models(self):
@@ -174,6 +176,13 @@ class Estimator:
         out = np.zeros(27, dtype=np.float32)
         k = lib().orc_est_estimate(self._h, _p(sample, _i32p), _p(out, _f32p))
         return out[: 9 * k].reshape(k, 9)
+
+    def e5_candidates(self, sample):
+        sample = np.ascontiguousarray(sample, dtype=np.int32)
+        cand = np.zeros((10, 9), dtype=np.float32)
+        ok = np.zeros(10, dtype=np.int32)
+        k = lib().orc_e5_candidates(self._h, _p(sample, _i32p), _p(cand, _f32p), _p(ok, _i32p))
+        return cand[:k].copy(), ok[:k].astype(bool)
 
     def estimate_batch(self, samples):
         samples = np.ascontiguousarray(samples, dtype=np.int32)
@@ -218,6 +227,15 @@ class Estimator:
         s = np.zeros(n, dtype=np.float32)
         lib().orc_score_models(self._h, _p(models, _f32p), n, ctypes.c_float(thr), _p(c, _i32p), _p(s, _f32p))
         return c, s
+
+
+def real_roots(coeffs):
+    """real roots (ascending) of sum coeffs[i] z^i (the 5-pt solver's root finder)"""
+    a = np.ascontiguousarray(coeffs, dtype=np.float64)
+    r = np.zeros(max(len(a) - 1, 1), dtype=np.float64)
+    k = lib().orc_real_roots(a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), len(a) - 1,
+                             r.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    return r[:k].copy()
 
 
 def cubic_roots(c0, c1, c2, c3):

@@ -279,7 +279,7 @@ struct orc_est {
 };
 
 orc_est *orc_est_new(int kind, const float *points, unsigned int n, int dlt_mode) {
-    if (kind != ORC_LINE2D && kind != ORC_HOMOGRAPHY && kind != ORC_FUNDAMENTAL) return NULL;
+    if (kind != ORC_LINE2D && kind != ORC_HOMOGRAPHY && kind != ORC_FUNDAMENTAL && kind != ORC_ESSENTIAL) return NULL;
     orc_est *e = (orc_est *)calloc(1, sizeof(*e));
     e->kind = kind;
     e->pts = points;
@@ -289,7 +289,7 @@ orc_est *orc_est_new(int kind, const float *points, unsigned int n, int dlt_mode
 }
 void orc_est_free(orc_est *e) { free(e); }
 int orc_est_sample_size(const orc_est *e) {
-    return e->kind == ORC_LINE2D ? 2 : e->kind == ORC_FUNDAMENTAL ? 7 : 4;
+    return e->kind == ORC_LINE2D ? 2 : e->kind == ORC_FUNDAMENTAL ? 7 : e->kind == ORC_ESSENTIAL ? 5 : 4;
 }
 int orc_est_max_models(const orc_est *e) { return e->kind == ORC_FUNDAMENTAL ? 3 : 1; }
 
@@ -761,15 +761,513 @@ static inline float fundamental_error(const orc_est *e, unsigned int pidx) {
     return (s * s) / (Fx * Fx + Fy * Fy + Gx * Gx + Gy * Gy);
 }
 
+/* ------------------------------------------------------------ essential (5-pt) */
+/* EssentialSolver::FivePoints / Solve5PointEssential (five_points.cpp:13-274), restated
+ * with IEEE basic operations only so that the device follows it bit for bit (OpenCV's
+ * SVD, determinant, inv and rpoly are not reproducible here -- parity vs the reference is
+ * end-to-end tolerance):
+ *   1. 5 rows [x1x2, x2y1, x2, x1y2, y1y2, y2, x1, y1, 1] in fp64 (:45-59); row Jacobi +
+ *      null complement -> basis N0..N3 (vt rows 5..8 of the FULL_UV SVD, :65-104);
+ *   2. E(x,y,z) = x N0 + y N1 + z N2 + N3 and its ten cubic constraints -- the nine
+ *      entries of 2 E E^T E - tr(E E^T) E (row-major) and det E -- as the 10 x 10 matrix
+ *      M(z) over the monomials [x^3, y^3, x^2y, xy^2, x^2, y^2, xy, x, y, 1] (mblock.hpp);
+ *   3. det M(z) at z = -5..5 (LU, partial pivoting), Newton divided differences ->
+ *      degree-10 coefficients (:113-136 interpolates at the same nodes);
+ *   4. real roots, ascending: derivative-recursion isolation (Gauss-Lucas: every
+ *      derivative's roots lie inside the Cauchy bound) + bisection (:139-158);
+ *   5. per root: null vector of M(z) by elimination with partial pivoting (v9 = 1):
+ *      x = v7, y = v8 (:180-187); E assembled as :190-200;
+ *   6. cheirality (:202-262): 3x3 SVD (row Jacobi with accumulated rotations), the four
+ *      projections, linear triangulation (4x4 row Jacobi, null vector), CalcDepth; the
+ *      first root whose E puts all five points in front of both cameras is returned. */
+
+/* row Jacobi on r rows of `cols` (<= 4) columns, same rules as row_jacobi; J (nullable,
+ * r x r) accumulates the rotations applied to the rows */
+static void row_jacobi_small(double W[][4], int r, int cols, double J[][4]) {
+    int pairs[6][2];
+    int np = tournament_pairs(r, pairs);
+    for (int sweep = 0; sweep < ORC_JAC_SWEEPS; sweep++) {
+        int rotated = 0;
+        double nrm[4];
+        for (int i = 0; i < r; i++) {
+            double a = 0.0;
+            for (int k = 0; k < cols; k++) a += W[i][k] * W[i][k];
+            nrm[i] = a;
+        }
+        for (int pi = 0; pi < np; pi++) {
+            const int p = pairs[pi][0], q = pairs[pi][1];
+            const double a = nrm[p], b = nrm[q];
+            double g = 0.0;
+            for (int k = 0; k < cols; k++) g += W[p][k] * W[q][k];
+            if (g * g <= ORC_JAC_EPS2 * (a * b)) continue;
+            rotated = 1;
+            const double d = b - a, g2 = 2.0 * g;
+            double t = g2 / (fabs(d) + sqrt(d * d + g2 * g2));
+            if (d < 0.0) t = -t;
+            const double c = 1.0 / sqrt(1.0 + t * t);
+            const double sn = c * t;
+            for (int k = 0; k < cols; k++) {
+                double wp = W[p][k], wq = W[q][k];
+                W[p][k] = c * wp - sn * wq;
+                W[q][k] = sn * wp + c * wq;
+            }
+            if (J) {
+                for (int k = 0; k < r; k++) {
+                    double jp = J[p][k], jq = J[q][k];
+                    J[p][k] = c * jp - sn * jq;
+                    J[q][k] = sn * jp + c * jq;
+                }
+            }
+            nrm[p] = a - t * g;
+            nrm[q] = b + t * g;
+        }
+        if (!rotated) break;
+    }
+}
+
+/* ----- bivariate cubic algebra over [x^3, y^3, x^2y, xy^2, x^2, y^2, xy, x, y, 1] */
+typedef struct { double a, b, c; } lin3;         /* a x + b y + c */
+typedef struct { double x2, y2, xy, x, y, k; } quad3;
+
+static quad3 q_mul(lin3 u, lin3 v) {
+    quad3 q;
+    q.x2 = u.a * v.a;
+    q.y2 = u.b * v.b;
+    q.xy = u.a * v.b + u.b * v.a;
+    q.x = u.a * v.c + u.c * v.a;
+    q.y = u.b * v.c + u.c * v.b;
+    q.k = u.c * v.c;
+    return q;
+}
+static quad3 q_add(quad3 p, quad3 q) {
+    quad3 r = {p.x2 + q.x2, p.y2 + q.y2, p.xy + q.xy, p.x + q.x, p.y + q.y, p.k + q.k};
+    return r;
+}
+static quad3 q_sub(quad3 p, quad3 q) {
+    quad3 r = {p.x2 - q.x2, p.y2 - q.y2, p.xy - q.xy, p.x - q.x, p.y - q.y, p.k - q.k};
+    return r;
+}
+/* cubic = Q * L into c[10] */
+static void c_mul(quad3 q, lin3 l, double *c) {
+    c[0] = q.x2 * l.a;
+    c[1] = q.y2 * l.b;
+    c[2] = q.x2 * l.b + q.xy * l.a;
+    c[3] = q.y2 * l.a + q.xy * l.b;
+    c[4] = q.x2 * l.c + q.x * l.a;
+    c[5] = q.y2 * l.c + q.y * l.b;
+    c[6] = q.xy * l.c + q.x * l.b + q.y * l.a;
+    c[7] = q.x * l.c + q.k * l.a;
+    c[8] = q.y * l.c + q.k * l.b;
+    c[9] = q.k * l.c;
+}
+
+/* M(z): rows 0..8 = 2 (E E^T E)_ij - tr(E E^T) E_ij (row-major), row 9 = det E */
+static void e5_matrix(const double N[4][9], double z, double M[10][10]) {
+    lin3 E[9];
+    for (int k = 0; k < 9; k++) {
+        E[k].a = N[0][k];
+        E[k].b = N[1][k];
+        E[k].c = z * N[2][k] + N[3][k];
+    }
+    quad3 EEt[3][3];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            quad3 acc = q_mul(E[3 * i], E[3 * j]);
+            acc = q_add(acc, q_mul(E[3 * i + 1], E[3 * j + 1]));
+            acc = q_add(acc, q_mul(E[3 * i + 2], E[3 * j + 2]));
+            EEt[i][j] = acc;
+        }
+    quad3 tr = q_add(q_add(EEt[0][0], EEt[1][1]), EEt[2][2]);
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double t0[10], t1[10], t2[10], tt[10];
+            c_mul(EEt[i][0], E[j], t0);
+            c_mul(EEt[i][1], E[3 + j], t1);
+            c_mul(EEt[i][2], E[6 + j], t2);
+            c_mul(tr, E[3 * i + j], tt);
+            for (int m = 0; m < 10; m++) M[3 * i + j][m] = 2.0 * (t0[m] + t1[m] + t2[m]) - tt[m];
+        }
+    {
+        double d0[10], d1[10], d2[10];
+        c_mul(q_sub(q_mul(E[4], E[8]), q_mul(E[5], E[7])), E[0], d0);
+        c_mul(q_sub(q_mul(E[3], E[8]), q_mul(E[5], E[6])), E[1], d1);
+        c_mul(q_sub(q_mul(E[3], E[7]), q_mul(E[4], E[6])), E[2], d2);
+        for (int m = 0; m < 10; m++) M[9][m] = d0[m] - d1[m] + d2[m];
+    }
+}
+
+/* determinant by LU with partial pivoting (first maximal |pivot|) */
+static double det10(double A[10][10]) {
+    double det = 1.0;
+    for (int k = 0; k < 10; k++) {
+        int p = k;
+        double best = fabs(A[k][k]);
+        for (int i = k + 1; i < 10; i++)
+            if (fabs(A[i][k]) > best) {
+                best = fabs(A[i][k]);
+                p = i;
+            }
+        if (A[p][k] == 0.0) return 0.0;
+        if (p != k) {
+            for (int j = 0; j < 10; j++) {
+                double t = A[k][j];
+                A[k][j] = A[p][j];
+                A[p][j] = t;
+            }
+            det = -det;
+        }
+        for (int i = k + 1; i < 10; i++) {
+            const double f = A[i][k] / A[k][k];
+            for (int j = k + 1; j < 10; j++) A[i][j] -= f * A[k][j];
+        }
+    }
+    for (int k = 0; k < 10; k++) det *= A[k][k];
+    return det;
+}
+
+/* null vector of M(z) with v9 = 1 by elimination over columns 0..8; returns 0 if singular */
+static int null10(double A[10][10], double *v) {
+    for (int k = 0; k < 9; k++) {
+        int p = k;
+        double best = fabs(A[k][k]);
+        for (int i = k + 1; i < 10; i++)
+            if (fabs(A[i][k]) > best) {
+                best = fabs(A[i][k]);
+                p = i;
+            }
+        if (A[p][k] == 0.0) return 0;
+        if (p != k)
+            for (int j = 0; j < 10; j++) {
+                double t = A[k][j];
+                A[k][j] = A[p][j];
+                A[p][j] = t;
+            }
+        for (int i = k + 1; i < 10; i++) {
+            const double f = A[i][k] / A[k][k];
+            for (int j = k + 1; j < 10; j++) A[i][j] -= f * A[k][j];
+        }
+    }
+    v[9] = 1.0;
+    for (int k = 8; k >= 0; k--) {
+        double sum = A[k][9];
+        for (int j = k + 1; j < 9; j++) sum += A[k][j] * v[j];
+        v[k] = -sum / A[k][k];
+    }
+    return 1;
+}
+
+static double poly_eval(const double *c, int deg, double x) {
+    double r = c[deg];
+    for (int i = deg - 1; i >= 0; i--) r = r * x + c[i];
+    return r;
+}
+
+static double poly_bisect(const double *c, int deg, double lo, double hi, double flo) {
+    for (int it = 0; it < 200; it++) {
+        const double mid = 0.5 * (lo + hi);
+        if (!(mid > lo && mid < hi)) break;
+        const double fm = poly_eval(c, deg, mid);
+        if (fm == 0.0) return mid;
+        if ((fm < 0.0) == (flo < 0.0)) {
+            lo = mid;
+            flo = fm;
+        } else {
+            hi = mid;
+        }
+    }
+    return 0.5 * (lo + hi);
+}
+
+/* real roots of a[0] + a[1] z + ... + a[n] z^n, ascending (<= n) */
+static int real_roots(const double *a_in, int n, double *roots) {
+    while (n > 0 && a_in[n] == 0.0) n--;
+    if (n == 0) return 0;
+    double R = 0.0;
+    for (int i = 0; i < n; i++) {
+        double q = fabs(a_in[i] / a_in[n]);
+        if (q > R) R = q;
+    }
+    R = R + 1.0;
+    double crit[10], next[10];
+    int ncrit = 0;
+    for (int d = n - 1; d >= 0; d--) {
+        /* coefficients of the d-th derivative: a[j+d] (j+d)!/j! */
+        double c[11];
+        const int deg = n - d;
+        for (int j = 0; j <= deg; j++) {
+            double f = 1.0;
+            for (int m = j + d; m > j; m--) f *= (double)m;
+            c[j] = a_in[j + d] * f;
+        }
+        int nn = 0;
+        double lo = -R, flo = poly_eval(c, deg, lo);
+        for (int k = 0; k <= ncrit; k++) {
+            const double hi = k < ncrit ? crit[k] : R;
+            const double fhi = poly_eval(c, deg, hi);
+            if (hi > lo && ((flo < 0.0) != (fhi < 0.0))) next[nn++] = poly_bisect(c, deg, lo, hi, flo);
+            lo = hi;
+            flo = fhi;
+        }
+        for (int k = 0; k < nn; k++) crit[k] = next[k];
+        ncrit = nn;
+    }
+    for (int k = 0; k < ncrit; k++) roots[k] = crit[k];
+    return ncrit;
+}
+
+/* null vector of a 4x4 system: rows Jacobi-orthogonalised, the smallest row dropped, unit
+ * complement of the other three (least represented axis, two Gram-Schmidt passes) */
+static void null4(double A[4][4], double *X) {
+    row_jacobi_small(A, 4, 4, NULL);
+    double n2[4];
+    int m = 0;
+    for (int i = 0; i < 4; i++) {
+        double a = 0.0;
+        for (int k = 0; k < 4; k++) a += A[i][k] * A[i][k];
+        n2[i] = a;
+        if (i > 0 && a < n2[m]) m = i;
+    }
+    double U[3][4];
+    int nu = 0;
+    for (int i = 0; i < 4; i++) {
+        if (i == m || !(n2[i] > 0.0)) continue;
+        const double inv = 1.0 / sqrt(n2[i]);
+        for (int k = 0; k < 4; k++) U[nu][k] = A[i][k] * inv;
+        nu++;
+    }
+    int ks = 0;
+    double bestc = 0.0;
+    for (int k = 0; k < 4; k++) {
+        double cc = 0.0;
+        for (int i = 0; i < nu; i++) cc += U[i][k] * U[i][k];
+        if (k == 0 || cc < bestc) {
+            bestc = cc;
+            ks = k;
+        }
+    }
+    double x[4];
+    for (int k = 0; k < 4; k++) x[k] = k == ks ? 1.0 : 0.0;
+    for (int pass = 0; pass < 2; pass++)
+        for (int i = 0; i < nu; i++) {
+            double d = 0.0;
+            for (int k = 0; k < 4; k++) d += U[i][k] * x[k];
+            for (int k = 0; k < 4; k++) x[k] -= d * U[i][k];
+        }
+    double nrm = 0.0;
+    for (int k = 0; k < 4; k++) nrm += x[k] * x[k];
+    nrm = sqrt(nrm);
+    for (int k = 0; k < 4; k++) X[k] = x[k] / nrm;
+}
+
+static double det3d(const double P[3][4]) {
+    return P[0][0] * (P[1][1] * P[2][2] - P[1][2] * P[2][1]) - P[0][1] * (P[1][0] * P[2][2] - P[1][2] * P[2][0]) +
+           P[0][2] * (P[1][0] * P[2][1] - P[1][1] * P[2][0]);
+}
+
+/* CalcDepth (five_points.cpp:278-302) */
+static double calc_depth(const double *X, const double P[3][4]) {
+    double w = 0.0;
+    for (int k = 0; k < 4; k++) w += P[2][k] * X[k];
+    const double det = det3d(P);
+    const double a = P[0][2], b = P[1][2], c = P[2][2];
+    const double m3 = sqrt(a * a + b * b + c * c);
+    const double sign = det > 0 ? 1.0 : -1.0;
+    return (w / X[3]) * (sign / m3);
+}
+
+/* TriangulatePoint (five_points.cpp:304-334) */
+static void triangulate(double x1, double y1, double x2, double y2, const double P1[3][4], const double P2[3][4],
+                        double *X) {
+    double A[4][4];
+    for (int c = 0; c < 4; c++) {
+        A[0][c] = x1 * P1[2][c] - P1[0][c];
+        A[1][c] = y1 * P1[2][c] - P1[1][c];
+        A[2][c] = x2 * P2[2][c] - P2[0][c];
+        A[3][c] = y2 * P2[2][c] - P2[1][c];
+    }
+    null4(A, X);
+}
+
+/* ProjectionsFromEssential (five_points.cpp:336-371): P[j] = [R | t], R in {U W V^T, U W^T V^T},
+ * t = +/- u3; U, V from the 3x3 SVD (rows Jacobi with accumulated rotations, singular values
+ * descending, v3 = v1 x v2). */
+static void projections(const double E[9], double P[4][3][4]) {
+    double B[4][4], J[4][4];
+    memset(B, 0, sizeof(B));
+    memset(J, 0, sizeof(J));
+    for (int i = 0; i < 3; i++) {
+        for (int k = 0; k < 3; k++) B[i][k] = E[3 * i + k];
+        J[i][i] = 1.0;
+    }
+    row_jacobi_small(B, 3, 3, J);
+    double sg[3];
+    for (int i = 0; i < 3; i++) {
+        double a = 0.0;
+        for (int k = 0; k < 3; k++) a += B[i][k] * B[i][k];
+        sg[i] = sqrt(a);
+    }
+    int o[3] = {0, 1, 2};
+    for (int i = 0; i < 3; i++)
+        for (int j = i + 1; j < 3; j++)
+            if (sg[o[j]] > sg[o[i]]) {
+                int t = o[i];
+                o[i] = o[j];
+                o[j] = t;
+            }
+    double U[3][3], V[3][3]; /* columns */
+    for (int k = 0; k < 3; k++)
+        for (int r = 0; r < 3; r++) U[r][k] = J[o[k]][r];
+    for (int k = 0; k < 2; k++)
+        for (int r = 0; r < 3; r++) V[r][k] = B[o[k]][r] / sg[o[k]];
+    V[0][2] = V[1][0] * V[2][1] - V[2][0] * V[1][1];
+    V[1][2] = V[2][0] * V[0][1] - V[0][0] * V[2][1];
+    V[2][2] = V[0][0] * V[1][1] - V[1][0] * V[0][1];
+    static const double Wm[3][3] = {{0, -1, 0}, {1, 0, 0}, {0, 0, 1}};
+    for (int w = 0; w < 2; w++) {
+        double T[3][3], R[3][3];
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) {
+                double sum = 0.0;
+                for (int k = 0; k < 3; k++) sum += U[r][k] * (w == 0 ? Wm[k][c] : Wm[c][k]);
+                T[r][c] = sum;
+            }
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) {
+                double sum = 0.0;
+                for (int k = 0; k < 3; k++) sum += T[r][k] * V[c][k];
+                R[r][c] = sum;
+            }
+        for (int sgn = 0; sgn < 2; sgn++) {
+            double(*Pj)[4] = P[2 * w + sgn];
+            for (int r = 0; r < 3; r++) {
+                for (int c = 0; c < 3; c++) Pj[r][c] = R[r][c];
+                Pj[r][3] = sgn == 0 ? U[r][2] : -U[r][2];
+            }
+        }
+    }
+}
+
+/* returns 1 and writes E (9 floats) when a root passes the cheirality test; with
+ * cand != NULL every root's E (10 x 9) and cheirality flag are reported (test hook) */
+static int essential_5pt_all(const orc_est *e, const int *sample, float *Eout, float *cand, int *cand_ok,
+                             int *ncand) {
+    double W[9][9];
+    double p1[5][2], p2[5][2];
+    for (int i = 0; i < 5; i++) {
+        const float *p = e->pts + 4 * (size_t)sample[i];
+        const double x1 = p[0], y1 = p[1], x2 = p[2], y2 = p[3];
+        p1[i][0] = x1;
+        p1[i][1] = y1;
+        p2[i][0] = x2;
+        p2[i][1] = y2;
+        const double row[9] = {x1 * x2, x2 * y1, x2, x1 * y2, y1 * y2, y2, x1, y1, 1.0};
+        for (int k = 0; k < 9; k++) W[i][k] = row[k];
+    }
+    row_jacobi(W, 5);
+    double N[4][9];
+    null_complement(W, 5, 4, N);
+    double Mz[10][10], dets[11], z[11];
+    for (int k = 0; k < 11; k++) {
+        z[k] = (double)(k - 5);
+        e5_matrix((const double(*)[9])N, z[k], Mz);
+        dets[k] = det10(Mz);
+    }
+    /* Newton divided differences, then monomial coefficients */
+    double c[11], a[11];
+    for (int k = 0; k < 11; k++) c[k] = dets[k];
+    for (int j = 1; j < 11; j++)
+        for (int i = 10; i >= j; i--) c[i] = (c[i] - c[i - 1]) / (z[i] - z[i - j]);
+    for (int i = 0; i < 11; i++) a[i] = 0.0;
+    a[0] = c[10];
+    int deg = 0;
+    for (int k = 9; k >= 0; k--) {
+        a[deg + 1] = 0.0;
+        for (int i = deg + 1; i >= 1; i--) a[i] = a[i - 1] - z[k] * a[i];
+        a[0] = c[k] - z[k] * a[0];
+        deg++;
+    }
+    double roots[10];
+    const int nr = real_roots(a, 10, roots);
+    static const double Pref[3][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}};
+    for (int r = 0; r < nr; r++) {
+        const double zz = roots[r];
+        e5_matrix((const double(*)[9])N, zz, Mz);
+        double v[10];
+        if (!null10(Mz, v)) continue;
+        const double x = v[7], y = v[8];
+        double E[9];
+        for (int k = 0; k < 9; k++) E[k] = N[0][k] * x + N[1][k] * y + N[2][k] * zz + N[3][k];
+        double P[4][3][4];
+        projections(E, P);
+        int found = 0;
+        for (int j = 0; j < 4 && !found; j++) {
+            double X[4];
+            triangulate(p1[0][0], p1[0][1], p2[0][0], p2[0][1], Pref, P[j], X);
+            if (!(calc_depth(X, Pref) > 0 && calc_depth(X, P[j]) > 0)) continue;
+            int inl = 1;
+            for (int k = 1; k < 5; k++) {
+                triangulate(p1[k][0], p1[k][1], p2[k][0], p2[k][1], Pref, P[j], X);
+                if (calc_depth(X, Pref) > 0 && calc_depth(X, P[j]) > 0) inl++;
+            }
+            if (inl >= 5) found = 1;
+        }
+        if (cand) {
+            for (int k = 0; k < 9; k++) cand[9 * *ncand + k] = (float)E[k];
+            cand_ok[*ncand] = found;
+            (*ncand)++;
+            continue;
+        }
+        if (found) {
+            for (int k = 0; k < 9; k++) Eout[k] = (float)E[k];
+            return 1;
+        }
+    }
+    return 0;
+}
+
+static int essential_5pt(const orc_est *e, const int *sample, float *Eout) {
+    return essential_5pt_all(e, sample, Eout, NULL, NULL, NULL);
+}
+
+int orc_e5_candidates(orc_est *e, const int *sample, float *cand, int *cand_ok) {
+    int n = 0;
+    float dummy[9];
+    essential_5pt_all(e, sample, dummy, cand, cand_ok, &n);
+    return n;
+}
+
+/* EssentialEstimator::GetError (essential_estimator.hpp:76-107): mean of the two
+ * point-to-epipolar-line distances, fp32 (sqrt of a float: C double sqrt, rounded). */
+static inline float essential_error(const orc_est *e, unsigned int pidx) {
+    const float *p = e->pts + 4 * (size_t)pidx;
+    const float x1 = p[0], y1 = p[1], x2 = p[2], y2 = p[3];
+    const float *E = e->f;
+    const float l1 = E[0] * x2 + E[3] * y2 + E[6];
+    const float l2 = E[1] * x2 + E[4] * y2 + E[7];
+    const float l3 = E[2] * x2 + E[5] * y2 + E[8];
+    const float t1 = E[0] * x1 + E[1] * y1 + E[2];
+    const float t2 = E[3] * x1 + E[4] * y1 + E[5];
+    const float t3 = E[6] * x1 + E[7] * y1 + E[8];
+    const float a1 = l1 * x1 + l2 * y1 + l3;
+    const float a2 = (float)sqrt((double)(l1 * l1 + l2 * l2));
+    const float b1 = t1 * x2 + t2 * y2 + t3;
+    const float b2 = (float)sqrt((double)(t1 * t1 + t2 * t2));
+    return (fabsf(a1 / a2) + fabsf(b1 / b2)) / 2;
+}
+
+/* test hook: real roots of a polynomial (ascending) by the 5-pt solver's spec */
+int orc_real_roots(const double *a, int n, double *roots) { return real_roots(a, n, roots); }
+
 int orc_est_estimate(orc_est *e, const int *sample, float *models) {
     if (e->kind == ORC_LINE2D) return line2d_estimate(e, sample, models);
     if (e->kind == ORC_FUNDAMENTAL) return fundamental_7pt(e, sample, models);
+    if (e->kind == ORC_ESSENTIAL) return essential_5pt(e, sample, models);
     return homography_dlt4(e, sample, models);
 }
 
 int orc_est_nonminimal(orc_est *e, const int *sample, unsigned int n, float *model) {
     if (e->kind == ORC_LINE2D) return line2d_nonminimal(e, sample, n, model);
-    if (e->kind == ORC_FUNDAMENTAL) return fundamental_8pt(e, sample, n, model);
+    if (e->kind == ORC_FUNDAMENTAL || e->kind == ORC_ESSENTIAL) return fundamental_8pt(e, sample, n, model);
     return homography_normalized_dlt(e, sample, n, model);
 }
 
@@ -783,7 +1281,7 @@ void orc_est_set_model(orc_est *e, const float *m) {
         e->a = m[0];
         e->b = m[1];
         e->c = m[2];
-    } else if (e->kind == ORC_FUNDAMENTAL) {
+    } else if (e->kind == ORC_FUNDAMENTAL || e->kind == ORC_ESSENTIAL) {
         memcpy(e->f, m, sizeof(float) * 9);
     } else {
         memcpy(e->h, m, sizeof(float) * 9);
@@ -823,6 +1321,7 @@ static inline float line2d_error(const orc_est *e, unsigned int pidx) {
 float orc_est_error(const orc_est *e, unsigned int pidx) {
     if (e->kind == ORC_LINE2D) return line2d_error(e, pidx);
     if (e->kind == ORC_FUNDAMENTAL) return fundamental_error(e, pidx);
+    if (e->kind == ORC_ESSENTIAL) return essential_error(e, pidx);
     return homography_error(e, pidx);
 }
 
@@ -842,9 +1341,10 @@ void orc_quality(orc_est *e, const float *model, float thr, int *count, float *s
                 s += err;
             }
         }
-    } else if (e->kind == ORC_FUNDAMENTAL) {
+    } else if (e->kind == ORC_FUNDAMENTAL || e->kind == ORC_ESSENTIAL) {
+        const int ess = e->kind == ORC_ESSENTIAL;
         for (unsigned int p = 0; p < e->n; p++) {
-            float err = fundamental_error(e, p);
+            float err = ess ? essential_error(e, p) : fundamental_error(e, p);
             if (err < thr) {
                 if (inliers) inliers[cnt] = (int)p;
                 cnt++;

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include "usac_device.hpp"
+#include "usac_device_e5.hpp"
 #include "usac_kernels.h"
 
 namespace usac {
@@ -99,7 +100,14 @@ __global__ __launch_bounds__(256) void k_prepare_f(const float *__restrict__ in,
 // results land at the listed slots; without it lane i is slot i < kmax.  Points are
 // wave-uniform scalar loads; per lane the count and the Σerr are accumulated in point
 // order (exact sequential sums with CHUNKS == 1).
-template <int CHUNKS>
+// EST = USAC_FUNDAMENTAL (Sampson) or USAC_ESSENTIAL (mean epipolar distance)
+template <int EST>
+__device__ __forceinline__ float two_view_error(const float *f, float x1, float y1, float x2, float y2) {
+    if constexpr (EST == USAC_ESSENTIAL) return essential_error(f, x1, y1, x2, y2);
+    else return fundamental_error(f, x1, y1, x2, y2);
+}
+
+template <int CHUNKS, int EST>
 __global__ __launch_bounds__(64 * CHUNKS) void k_score_f(const float4 *__restrict__ pts, uint32_t n,
                                                          const float *__restrict__ models, size_t stride,
                                                          const uint32_t *__restrict__ list,
@@ -124,10 +132,10 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_f(const float4 *__restric
     uint32_t p = begin;
     for (; p + 4 <= end; p += 4) {
         const float4 a0 = pts[p], a1 = pts[p + 1], a2 = pts[p + 2], a3 = pts[p + 3];
-        const float e0 = fundamental_error(f, a0.x, a0.y, a0.z, a0.w);
-        const float e1 = fundamental_error(f, a1.x, a1.y, a1.z, a1.w);
-        const float e2 = fundamental_error(f, a2.x, a2.y, a2.z, a2.w);
-        const float e3 = fundamental_error(f, a3.x, a3.y, a3.z, a3.w);
+        const float e0 = two_view_error<EST>(f, a0.x, a0.y, a0.z, a0.w);
+        const float e1 = two_view_error<EST>(f, a1.x, a1.y, a1.z, a1.w);
+        const float e2 = two_view_error<EST>(f, a2.x, a2.y, a2.z, a2.w);
+        const float e3 = two_view_error<EST>(f, a3.x, a3.y, a3.z, a3.w);
         if (e0 < thr) { cnt++; sum += e0; }
         if (e1 < thr) { cnt++; sum += e1; }
         if (e2 < thr) { cnt++; sum += e2; }
@@ -135,7 +143,7 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_f(const float4 *__restric
     }
     for (; p < end; p++) {
         const float4 a = pts[p];
-        const float e = fundamental_error(f, a.x, a.y, a.z, a.w);
+        const float e = two_view_error<EST>(f, a.x, a.y, a.z, a.w);
         if (e < thr) { cnt++; sum += e; }
     }
     if constexpr (CHUNKS == 1) {
@@ -163,7 +171,8 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_f(const float4 *__restric
     }
 }
 
-// Quality::getNumberInliers(get_inliers=true) for one F (exact, ascending, sequential Σ)
+// Quality::getNumberInliers(get_inliers=true) for one F / E (exact, ascending, sequential Σ)
+template <int EST>
 __global__ __launch_bounds__(256) void k_inliers_f(const float4 *__restrict__ pts, uint32_t n, const float *model,
                                                    float thr, int32_t *idx, int32_t *count, float *sum) {
     __shared__ float s_err[256];
@@ -177,7 +186,7 @@ __global__ __launch_bounds__(256) void k_inliers_f(const float4 *__restrict__ pt
         float e = 0.f;
         if (i < n) {
             const float4 p = pts[i];
-            e = fundamental_error(f, p.x, p.y, p.z, p.w);
+            e = two_view_error<EST>(f, p.x, p.y, p.z, p.w);
         }
         s_err[threadIdx.x] = e;
         __syncthreads();
@@ -214,26 +223,147 @@ hipError_t launch_prepare_f(hipStream_t st, const float *in, uint32_t K, float *
     return hipGetLastError();
 }
 
-hipError_t launch_score_f(hipStream_t st, int chunks, const float4 *pts, uint32_t n, const float *models,
-                          size_t stride, const uint32_t *list, const uint32_t *list_n, uint32_t kmax, float thr,
-                          int32_t *counts, float *sums) {
+hipError_t launch_score_f(hipStream_t st, int estimator, int chunks, const float4 *pts, uint32_t n,
+                          const float *models, size_t stride, const uint32_t *list, const uint32_t *list_n,
+                          uint32_t kmax, float thr, int32_t *counts, float *sums) {
     const dim3 grid((kmax + 63) / 64);
-#define SF(C) \
-    hipLaunchKernelGGL(k_score_f<C>, grid, dim3(64 * C), 0, st, pts, n, models, stride, list, list_n, kmax, thr, counts, sums)
+#define SF(C, E)                                                                                                   \
+    hipLaunchKernelGGL((k_score_f<C, E>), grid, dim3(64 * C), 0, st, pts, n, models, stride, list, list_n, kmax, thr, \
+                       counts, sums)
+    const bool ess = estimator == USAC_ESSENTIAL;
     switch (chunks) {
-        case 1: SF(1); break;
-        case 2: SF(2); break;
-        case 4: SF(4); break;
-        case 8: SF(8); break;
+        case 1: if (ess) SF(1, USAC_ESSENTIAL); else SF(1, USAC_FUNDAMENTAL); break;
+        case 2: if (ess) SF(2, USAC_ESSENTIAL); else SF(2, USAC_FUNDAMENTAL); break;
+        case 4: if (ess) SF(4, USAC_ESSENTIAL); else SF(4, USAC_FUNDAMENTAL); break;
+        case 8: if (ess) SF(8, USAC_ESSENTIAL); else SF(8, USAC_FUNDAMENTAL); break;
         default: return hipErrorInvalidValue;
     }
 #undef SF
     return hipGetLastError();
 }
 
-hipError_t launch_inliers_f(hipStream_t st, const float4 *pts, uint32_t n, const float *model, float thr,
-                            int32_t *idx, int32_t *count, float *sum) {
-    hipLaunchKernelGGL(k_inliers_f, dim3(1), dim3(256), 0, st, pts, n, model, thr, idx, count, sum);
+hipError_t launch_inliers_f(hipStream_t st, int estimator, const float4 *pts, uint32_t n, const float *model,
+                            float thr, int32_t *idx, int32_t *count, float *sum) {
+    if (estimator == USAC_ESSENTIAL)
+        hipLaunchKernelGGL(k_inliers_f<USAC_ESSENTIAL>, dim3(1), dim3(256), 0, st, pts, n, model, thr, idx, count, sum);
+    else
+        hipLaunchKernelGGL(k_inliers_f<USAC_FUNDAMENTAL>, dim3(1), dim3(256), 0, st, pts, n, model, thr, idx, count,
+                           sum);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------ essential (5-pt)
+// One lane per sample: 5 x 9 fp64 rows -> Jacobi -> four null-space rows -> det M(z) at
+// z = -5..5 -> degree-10 coefficients -> real roots -> per root: null vector of M(z), E,
+// cheirality over the sample; the first root that puts all five points in front of both
+// cameras gives the sample's (single) model (five_points.cpp:30-34, 239-273).  Slot layout
+// as the fundamental path with one slot per sample: models [9][B], counts 0 / -1, list.
+__global__ __launch_bounds__(64) void k_solve_e5(const float4 *__restrict__ pts, uint32_t n,
+                                                 const int32_t *__restrict__ samples_in, int32_t *samples_out,
+                                                 uint32_t B, uint64_t seed, uint64_t first_hyp,
+                                                 float *__restrict__ models, int32_t *__restrict__ counts,
+                                                 uint32_t *__restrict__ list, uint32_t *__restrict__ list_n) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t h = blockIdx.x * 64 + lane;
+    const bool active = h < B;
+    int nvalid = 0;
+    if (active) {
+        int32_t s[5];
+        if (samples_in) {
+#pragma unroll
+            for (int i = 0; i < 5; i++) s[i] = samples_in[5 * (size_t)h + i];
+        } else {
+            draw_sample<5>(seed, first_hyp + h, n, s);
+            if (samples_out) {
+#pragma unroll
+                for (int i = 0; i < 5; i++) samples_out[5 * (size_t)h + i] = s[i];
+            }
+        }
+        double N[4][9];
+        {
+            double W[5][9];
+#pragma unroll
+            for (int i = 0; i < 5; i++) {
+                const float4 p = pts[s[i]];
+                const double x1 = p.x, y1 = p.y, x2 = p.z, y2 = p.w;
+                W[i][0] = x1 * x2; W[i][1] = x2 * y1; W[i][2] = x2;
+                W[i][3] = x1 * y2; W[i][4] = y1 * y2; W[i][5] = y2;
+                W[i][6] = x1; W[i][7] = y1; W[i][8] = 1.0;
+            }
+            row_jacobi<5>(W);
+            e5::null_basis4(W, N);
+        }
+        double c[11], z[11];
+        for (int k = 0; k < 11; k++) {
+            z[k] = (double)(k - 5);
+            double M[10][10];
+            e5::matrix(N, z[k], M);
+            c[k] = e5::det10(M);
+        }
+        for (int j = 1; j < 11; j++)
+            for (int i = 10; i >= j; i--) c[i] = (c[i] - c[i - 1]) / (z[i] - z[i - j]);
+        double a[11];
+        for (int i = 0; i < 11; i++) a[i] = 0.0;
+        a[0] = c[10];
+        int deg = 0;
+        for (int k = 9; k >= 0; k--) {
+            a[deg + 1] = 0.0;
+            for (int i = deg + 1; i >= 1; i--) a[i] = a[i - 1] - z[k] * a[i];
+            a[0] = c[k] - z[k] * a[0];
+            deg++;
+        }
+        double roots[10];
+        const int nr = e5::real_roots10(a, roots);
+        for (int r = 0; r < nr && !nvalid; r++) {
+            const double zz = roots[r];
+            double M[10][10], v[10];
+            e5::matrix(N, zz, M);
+            if (!e5::null10(M, v)) continue;
+            const double x = v[7], y = v[8];
+            double E[9];
+#pragma unroll
+            for (int k = 0; k < 9; k++) E[k] = N[0][k] * x + N[1][k] * y + N[2][k] * zz + N[3][k];
+            double U[3][3], V[3][3];
+            e5::svd3(E, U, V);
+            bool found = false;
+            for (int j = 0; j < 4 && !found; j++) {
+                double P[3][4];
+                e5::projection(U, V, j, P);
+                bool all = true;
+                for (int k = 0; k < 5 && all; k++) {
+                    const float4 p = pts[s[k]];
+                    all = e5::in_front((double)p.x, (double)p.y, (double)p.z, (double)p.w, P);
+                }
+                found = all;
+            }
+            if (found) {
+#pragma unroll
+                for (int k = 0; k < 9; k++) models[(size_t)k * B + h] = (float)E[k];
+                nvalid = 1;
+            }
+        }
+        counts[h] = nvalid ? 0 : -1;
+    }
+    uint32_t incl = (uint32_t)nvalid;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(incl, off, 64);
+        if (lane >= (uint32_t)off) incl += v;
+    }
+    const uint32_t total = __shfl(incl, 63, 64);
+    uint32_t base = 0;
+    if (lane == 63 && total) base = atomicAdd(list_n, total);
+    base = __shfl(base, 63, 64);
+    if (nvalid) list[base + incl - 1] = h;
+}
+
+hipError_t launch_solve_e5(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
+                           int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, float *models,
+                           int32_t *counts, uint32_t *list, uint32_t *list_n) {
+    hipError_t e = hipMemsetAsync(list_n, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_solve_e5, dim3((B + 63) / 64), dim3(64), 0, st, pts, n, samples_in, samples_out, B, seed,
+                       first_hyp, models, counts, list, list_n);
     return hipGetLastError();
 }
 

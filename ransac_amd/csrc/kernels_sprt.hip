@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include "usac_device.hpp"
+#include "usac_device_e5.hpp"
 #include "usac_kernels.h"
 
 namespace usac {
@@ -22,7 +23,7 @@ __global__ __launch_bounds__(256) void k_gather(const P *__restrict__ pts, const
 }
 
 // EST: 1 line (float2 points, models [3][stride]), 2 homography (float4, [18][stride]: H, H^-1),
-// 3 fundamental (float4, [9][stride]).  Lane = one model row; with `list` the rows are
+// 3 fundamental / 4 essential (float4, [9][stride]).  Lane = one model row; with `list` the rows are
 // list[0 .. *list_n) (model slot list[i] -> row i), else rows are slots 0 .. kmax-1.
 // words[w * row_stride + row], bit b = pool position 32 w + b.
 template <int EST>
@@ -54,9 +55,12 @@ __global__ __launch_bounds__(64) void k_pool_mask(const void *__restrict__ pool_
             } else if constexpr (EST == 2) {
                 const float4 p = static_cast<const float4 *>(pool_pts)[p0 + b];
                 e = homography_error(m, m + 9, p.x, p.y, p.z, p.w);
-            } else {
+            } else if constexpr (EST == 3) {
                 const float4 p = static_cast<const float4 *>(pool_pts)[p0 + b];
                 e = fundamental_error(m, p.x, p.y, p.z, p.w);
+            } else {
+                const float4 p = static_cast<const float4 *>(pool_pts)[p0 + b];
+                e = essential_error(m, p.x, p.y, p.z, p.w);
             }
             bits |= (e < thr ? 1u : 0u) << b;
         }
@@ -93,6 +97,10 @@ hipError_t launch_pool_mask(hipStream_t st, int estimator, const void *pool_pts,
             break;
         case USAC_FUNDAMENTAL:
             hipLaunchKernelGGL(k_pool_mask<3>, grid, dim3(64), 0, st, pool_pts, n, models, stride, list, list_n, kmax,
+                               thr, words, row_stride);
+            break;
+        case USAC_ESSENTIAL:
+            hipLaunchKernelGGL(k_pool_mask<4>, grid, dim3(64), 0, st, pool_pts, n, models, stride, list, list_n, kmax,
                                thr, words, row_stride);
             break;
         default:
@@ -133,9 +141,12 @@ __device__ __forceinline__ float sprt_error(const float *m, const void *pts, uin
     } else if constexpr (EST == 2) {
         const float4 q = static_cast<const float4 *>(pts)[p];
         return homography_error(m, m + 9, q.x, q.y, q.z, q.w);
-    } else {
+    } else if constexpr (EST == 3) {
         const float4 q = static_cast<const float4 *>(pts)[p];
         return fundamental_error(m, q.x, q.y, q.z, q.w);
+    } else {
+        const float4 q = static_cast<const float4 *>(pts)[p];
+        return essential_error(m, q.x, q.y, q.z, q.w);
     }
 }
 
@@ -291,6 +302,7 @@ hipError_t launch_score_sprt(hipStream_t st, int estimator, const void *pool_pts
         case USAC_LINE2D: SS(1); break;
         case USAC_HOMOGRAPHY: SS(2); break;
         case USAC_FUNDAMENTAL: SS(3); break;
+        case USAC_ESSENTIAL: SS(4); break;
         default: return hipErrorInvalidValue;
     }
 #undef SS

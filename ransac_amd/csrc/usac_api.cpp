@@ -105,6 +105,9 @@ int fail(usac_ctx *c, int code, const std::string &msg) {
 
 bool is_h(const usac_ctx *c) { return c->estimator == USAC_HOMOGRAPHY; }
 bool is_f(const usac_ctx *c) { return c->estimator == USAC_FUNDAMENTAL; }
+bool is_e(const usac_ctx *c) { return c->estimator == USAC_ESSENTIAL; }
+// solvers that may return no model for a sample: occupied slots are listed (list / list_n)
+bool listed(const usac_ctx *c) { return is_f(c) || is_e(c); }
 bool two_view(const usac_ctx *c) { return c->cols == 4; }
 int ncomp(const usac_ctx *c) { return two_view(c) ? 9 : 3; }
 int ncomp_dev(const usac_ctx *c) { return is_h(c) ? 18 : ncomp(c); }
@@ -119,7 +122,7 @@ int ensure_batch(usac_ctx *c, uint32_t B) {
     HIP_TRY(c, c->best.reserve(sizeof(usac_record)));
     HIP_TRY(c, c->argmax_part.reserve(16 * (S / 2048 + 1)));
     HIP_TRY(c, c->hostmodels.reserve(sizeof(float) * 9 * S));
-    if (is_f(c)) {
+    if (listed(c)) {
         HIP_TRY(c, c->list.reserve(sizeof(uint32_t) * S));
         HIP_TRY(c, c->list_n.reserve(sizeof(uint32_t)));
     }
@@ -142,6 +145,10 @@ int ensure_single(usac_ctx *c) {
 // solve (samples on device, or device RNG when samples_dev == nullptr) into c->models
 hipError_t enqueue_solve(usac_ctx *c, const int32_t *samples_dev, uint32_t B, uint64_t seed, uint64_t first_hyp,
                          int32_t *samples_out) {
+    if (is_e(c))
+        return usac::launch_solve_e5(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, seed,
+                                     first_hyp, c->models.as<float>(), c->counts.as<int32_t>(),
+                                     c->list.as<uint32_t>(), c->list_n.as<uint32_t>());
     if (is_f(c))
         return usac::launch_solve_f7(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, seed,
                                      first_hyp, c->models.as<float>(), c->counts.as<int32_t>(),
@@ -163,15 +170,15 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
         e = c->sprt_surv.reserve(usac::sprt_survivor_bytes() * (size_t)S);
         if (e != hipSuccess) return e;
         return usac::launch_score_sprt(c->stream, c->estimator, c->sprt_pts.p, c->n, c->models.as<float>(),
-                                       is_f(c) ? 3 * (size_t)B : (size_t)B, is_f(c) ? c->list.as<uint32_t>() : nullptr,
-                                       is_f(c) ? c->list_n.as<uint32_t>() : nullptr, S, thr, c->sprt_log_up,
+                                       (size_t)S, listed(c) ? c->list.as<uint32_t>() : nullptr,
+                                       listed(c) ? c->list_n.as<uint32_t>() : nullptr, S, thr, c->sprt_log_up,
                                        c->sprt_log_down, c->sprt_log_A, c->counts.as<int32_t>(), c->sums.as<float>(),
                                        c->sprt_tested.as<uint32_t>(), c->sprt_surv.p, c->sprt_surv_n.as<uint32_t>());
     }
-    if (is_f(c))  // the occupied slots of the last solve
-        return usac::launch_score_f(c->stream, chunks, c->pts.as<float4>(), c->n, c->models.as<float>(), 3 * (size_t)B,
-                                    c->list.as<uint32_t>(), c->list_n.as<uint32_t>(), 3 * B, thr,
-                                    c->counts.as<int32_t>(), c->sums.as<float>());
+    if (listed(c))  // the occupied slots of the last solve
+        return usac::launch_score_f(c->stream, c->estimator, chunks, c->pts.as<float4>(), c->n, c->models.as<float>(),
+                                    (size_t)B * c->spk, c->list.as<uint32_t>(), c->list_n.as<uint32_t>(), B * c->spk,
+                                    thr, c->counts.as<int32_t>(), c->sums.as<float>());
     if (is_h(c)) {
         if (c->score_variant == 1)
             return usac::launch_score_h(c->stream, chunks, c->pts.as<float4>(), c->n, c->models.as<float>(), B, thr,
@@ -192,9 +199,9 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
 
 // exact single-model inliers into c->inl_idx / inl_cnt / inl_sum (device)
 hipError_t enqueue_inliers(usac_ctx *c, const float *model_dev, float thr) {
-    if (is_f(c))
-        return usac::launch_inliers_f(c->stream, c->pts.as<float4>(), c->n, model_dev, thr, c->inl_idx.as<int32_t>(),
-                                      c->inl_cnt.as<int32_t>(), c->inl_sum.as<float>());
+    if (listed(c))
+        return usac::launch_inliers_f(c->stream, c->estimator, c->pts.as<float4>(), c->n, model_dev, thr,
+                                      c->inl_idx.as<int32_t>(), c->inl_cnt.as<int32_t>(), c->inl_sum.as<float>());
     if (is_h(c))
         return usac::launch_inliers_h(c->stream, c->pts.as<float4>(), c->n, model_dev, thr, c->inl_idx.as<int32_t>(),
                                       c->inl_cnt.as<int32_t>(), c->inl_sum.as<float>());
@@ -203,7 +210,7 @@ hipError_t enqueue_inliers(usac_ctx *c, const float *model_dev, float thr) {
 }
 
 hipError_t enqueue_nonminimal(usac_ctx *c, const int32_t *idx_dev, uint32_t n) {
-    if (is_f(c))
+    if (listed(c))  // F and E: EightPointsAlgorithm (essential_estimator.hpp:64-74)
         return usac::launch_nonminimal_f(c->stream, c->pts.as<float4>(), idx_dev, n, c->q.as<float4>(),
                                          c->partial.as<double>(), c->ws.as<float>(), c->nm_model.as<float>(),
                                          c->nm_ok.as<int32_t>());
@@ -232,7 +239,8 @@ int usac_abi_version(void) { return USAC_ABI_VERSION; }
 int usac_create(usac_ctx **out, int device, int estimator, const float *pts, uint32_t n, uint32_t cols) {
     if (!out) return USAC_ERR_ARG;
     *out = nullptr;
-    if (estimator != USAC_LINE2D && estimator != USAC_HOMOGRAPHY && estimator != USAC_FUNDAMENTAL)
+    if (estimator != USAC_LINE2D && estimator != USAC_HOMOGRAPHY && estimator != USAC_FUNDAMENTAL &&
+        estimator != USAC_ESSENTIAL)
         return USAC_ERR_UNSUPPORTED;
     if ((estimator == USAC_LINE2D) != (cols == 2) || (cols != 2 && cols != 4)) return USAC_ERR_ARG;
     if (n == 0 || !pts) return USAC_ERR_ARG;
@@ -241,7 +249,7 @@ int usac_create(usac_ctx **out, int device, int estimator, const float *pts, uin
     c->estimator = estimator;
     c->n = n;
     c->cols = cols;
-    c->m = estimator == USAC_LINE2D ? 2 : estimator == USAC_FUNDAMENTAL ? 7 : 4;
+    c->m = estimator == USAC_LINE2D ? 2 : estimator == USAC_FUNDAMENTAL ? 7 : estimator == USAC_ESSENTIAL ? 5 : 4;
     c->spk = estimator == USAC_FUNDAMENTAL ? 3 : 1;
     int rc = USAC_OK;
     do {
@@ -333,7 +341,7 @@ int usac_estimate_models(usac_ctx *c, const int32_t *samples, uint32_t B, float 
     std::vector<float> soa((size_t)ncomp(c) * S);
     std::vector<int32_t> slot_cnt(S, 0);
     HIP_TRY(c, hipMemcpyAsync(soa.data(), c->models.p, sizeof(float) * soa.size(), hipMemcpyDeviceToHost, c->stream));
-    if (c->spk > 1)
+    if (listed(c))
         HIP_TRY(c, hipMemcpyAsync(slot_cnt.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
     const int nc = ncomp(c);
@@ -356,10 +364,10 @@ int usac_score_models(usac_ctx *c, const float *models, uint32_t nm, float thr, 
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipMemcpyAsync(c->hostmodels.p, models, sizeof(float) * 9 * (size_t)nm, hipMemcpyHostToDevice, c->stream));
-    if (is_f(c)) {
+    if (listed(c)) {
         HIP_TRY(c, usac::launch_prepare_f(c->stream, c->hostmodels.as<float>(), nm, c->models.as<float>()));
-        HIP_TRY(c, usac::launch_score_f(c->stream, 1, c->pts.as<float4>(), c->n, c->models.as<float>(), nm, nullptr,
-                                        nullptr, nm, thr, c->counts.as<int32_t>(), c->sums.as<float>()));
+        HIP_TRY(c, usac::launch_score_f(c->stream, c->estimator, 1, c->pts.as<float4>(), c->n, c->models.as<float>(),
+                                        nm, nullptr, nullptr, nm, thr, c->counts.as<int32_t>(), c->sums.as<float>()));
     } else {
         if (is_h(c))
             HIP_TRY(c, usac::launch_prepare_h(c->stream, c->hostmodels.as<float>(), nm, c->models.as<float>()));
@@ -502,7 +510,6 @@ int usac_set_sprt(usac_ctx *c, int enable, uint32_t seed, double epsilon, double
         c->sprt_on = false;
         return USAC_OK;
     }
-    if (c->estimator == USAC_ESSENTIAL) return fail(c, USAC_ERR_UNSUPPORTED, "SPRT: estimator not supported");
     HIP_TRY(c, hipSetDevice(c->device));
     usac::GlibcRandom g(seed);
     usac::Sprt sp(g, c->estimator, c->n, c->m, 10000);
@@ -671,11 +678,11 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
         HIP_TRY(c, hipMemcpyAsync(c->samples.p, hs.data(), sizeof(int32_t) * (size_t)B * m, hipMemcpyHostToDevice,
                                   c->stream));
         HIP_TRY(c, enqueue_solve(c, c->samples.as<int32_t>(), B, 0, iters, nullptr));
-        const size_t mstride = is_f(c) ? 3 * (size_t)B : (size_t)B;
+        const size_t mstride = (size_t)B * spk;
         if (sprt) {
             HIP_TRY(c, usac::launch_pool_mask(c->stream, c->estimator, c->pool_pts.p, n, c->models.as<float>(), mstride,
-                                              is_f(c) ? c->list.as<uint32_t>() : nullptr,
-                                              is_f(c) ? c->list_n.as<uint32_t>() : nullptr, (uint32_t)S, thr,
+                                              listed(c) ? c->list.as<uint32_t>() : nullptr,
+                                              listed(c) ? c->list_n.as<uint32_t>() : nullptr, (uint32_t)S, thr,
                                               c->masks.as<uint32_t>(), (uint32_t)S));
         } else {
             HIP_TRY(c, enqueue_score(c, B, thr, 1));
@@ -687,7 +694,7 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
                                       sizeof(float) * S, hipMemcpyDeviceToHost, c->stream));
         uint32_t rows = (uint32_t)S;
         if (sprt) {
-            if (is_f(c)) {  // occupied slots -> mask rows
+            if (listed(c)) {  // occupied slots -> mask rows
                 HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
                 HIP_TRY(c, hipMemcpyAsync(&rows, c->list_n.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
                 HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -702,7 +709,7 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
         }
         HIP_TRY(c, hipStreamSynchronize(c->stream));
         if (sprt) {
-            if (is_f(c)) {
+            if (listed(c)) {
                 std::fill(slot_row.begin(), slot_row.begin() + S, -1);
                 for (uint32_t r = 0; r < rows; r++) slot_row[hlist[r]] = (int32_t)r;
             } else {

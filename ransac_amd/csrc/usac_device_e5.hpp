@@ -1,0 +1,527 @@
+// usac_device_e5.hpp -- per-sample device math of the essential 5-point solver
+// (EssentialSolver::FivePoints / Solve5PointEssential, five_points.cpp:13-274) and the
+// essential residual (essential_estimator.hpp:76-107).
+//
+// Written to the spec the oracle restates (oracle/usac_oracle.c "essential (5-pt)"): the
+// same IEEE operation sequence -- fp64 throughout the solver, no FMA contraction, correctly
+// rounded division and square root -- so device and oracle agree bit for bit.  The
+// reference's OpenCV SVD / determinant / inv and rpoly are replaced by: row Jacobi + null
+// complement (basis), LU with partial pivoting (det M(z) at z = -5..5), Newton divided
+// differences (degree-10 coefficients), derivative-recursion root isolation + bisection
+// (real roots), elimination with partial pivoting (null vector of M(z)), and a cheirality
+// test through Jacobi 3x3 SVD + 4x4 linear triangulation.
+#pragma once
+#include "usac_device.hpp"
+
+namespace usac {
+namespace e5 {
+
+// row Jacobi on R rows of C (<= 4) columns with the row_jacobi rules; ACC: also rotate the
+// rows of J (R x R)
+template <int R, int C, bool ACC>
+__device__ __forceinline__ void jacobi_small(double (&W)[R][C], double (&J)[R][R]) {
+    constexpr Tournament<R> T{};
+    for (int sweep = 0; sweep < 30; sweep++) {
+        bool rotated = false;
+        double nrm[R];
+#pragma unroll
+        for (int i = 0; i < R; i++) {
+            double a = 0.0;
+#pragma unroll
+            for (int k = 0; k < C; k++) a += W[i][k] * W[i][k];
+            nrm[i] = a;
+        }
+#pragma unroll
+        for (int pi = 0; pi < Tournament<R>::NP; pi++) {
+            const int p = T.p[pi], q = T.q[pi];
+            const double a = nrm[p], b = nrm[q];
+            double g = 0.0;
+#pragma unroll
+            for (int k = 0; k < C; k++) g += W[p][k] * W[q][k];
+            if (!(g * g <= 1e-28 * (a * b))) {
+                rotated = true;
+                const double d = b - a, g2 = 2.0 * g;
+                double t = g2 / (fabs(d) + sqrt(d * d + g2 * g2));
+                if (d < 0.0) t = -t;
+                const double c = 1.0 / sqrt(1.0 + t * t);
+                const double s = c * t;
+#pragma unroll
+                for (int k = 0; k < C; k++) {
+                    const double wp = W[p][k], wq = W[q][k];
+                    W[p][k] = c * wp - s * wq;
+                    W[q][k] = s * wp + c * wq;
+                }
+                if (ACC) {
+#pragma unroll
+                    for (int k = 0; k < R; k++) {
+                        const double jp = J[p][k], jq = J[q][k];
+                        J[p][k] = c * jp - s * jq;
+                        J[q][k] = s * jp + c * jq;
+                    }
+                }
+                nrm[p] = a - t * g;
+                nrm[q] = b + t * g;
+            }
+        }
+        if (!rotated) break;
+    }
+}
+
+// the four null-space rows of the 5 x 9 system (oracle null_complement(W, 5, 4, N))
+__device__ __forceinline__ void null_basis4(double (&W)[5][9], double (&N)[4][9]) {
+    double n2[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) {
+        double a = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) a += W[i][k] * W[i][k];
+        n2[i] = a;
+        if (a > 0.0) {
+            const double inv = 1.0 / sqrt(a);
+#pragma unroll
+            for (int k = 0; k < 9; k++) W[i][k] = W[i][k] * inv;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        int ks = 0;
+        double bestc = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            double c = 0.0;
+#pragma unroll
+            for (int i = 0; i < 5; i++)
+                if (n2[i] > 0.0) c += W[i][k] * W[i][k];
+#pragma unroll
+            for (int l = 0; l < j; l++) c += N[l][k] * N[l][k];
+            if (k == 0 || c < bestc) {
+                bestc = c;
+                ks = k;
+            }
+        }
+        double x[9];
+#pragma unroll
+        for (int k = 0; k < 9; k++) x[k] = (k == ks) ? 1.0 : 0.0;
+#pragma unroll
+        for (int pass = 0; pass < 2; pass++) {
+#pragma unroll
+            for (int i = 0; i < 5; i++) {
+                if (n2[i] > 0.0) {
+                    double d = 0.0;
+#pragma unroll
+                    for (int k = 0; k < 9; k++) d += W[i][k] * x[k];
+#pragma unroll
+                    for (int k = 0; k < 9; k++) x[k] -= d * W[i][k];
+                }
+            }
+#pragma unroll
+            for (int l = 0; l < j; l++) {
+                double d = 0.0;
+#pragma unroll
+                for (int k = 0; k < 9; k++) d += N[l][k] * x[k];
+#pragma unroll
+                for (int k = 0; k < 9; k++) x[k] -= d * N[l][k];
+            }
+        }
+        double nrm = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) nrm += x[k] * x[k];
+        nrm = sqrt(nrm);
+#pragma unroll
+        for (int k = 0; k < 9; k++) N[j][k] = x[k] / nrm;
+    }
+}
+
+// bivariate cubic algebra over [x^3, y^3, x^2y, xy^2, x^2, y^2, xy, x, y, 1]
+struct Lin {
+    double a, b, c;
+};
+struct Quad {
+    double x2, y2, xy, x, y, k;
+};
+__device__ __forceinline__ Quad qmul(const Lin &u, const Lin &v) {
+    Quad q;
+    q.x2 = u.a * v.a;
+    q.y2 = u.b * v.b;
+    q.xy = u.a * v.b + u.b * v.a;
+    q.x = u.a * v.c + u.c * v.a;
+    q.y = u.b * v.c + u.c * v.b;
+    q.k = u.c * v.c;
+    return q;
+}
+__device__ __forceinline__ Quad qadd(const Quad &p, const Quad &q) {
+    return Quad{p.x2 + q.x2, p.y2 + q.y2, p.xy + q.xy, p.x + q.x, p.y + q.y, p.k + q.k};
+}
+__device__ __forceinline__ Quad qsub(const Quad &p, const Quad &q) {
+    return Quad{p.x2 - q.x2, p.y2 - q.y2, p.xy - q.xy, p.x - q.x, p.y - q.y, p.k - q.k};
+}
+__device__ __forceinline__ void cmul(const Quad &q, const Lin &l, double *c) {
+    c[0] = q.x2 * l.a;
+    c[1] = q.y2 * l.b;
+    c[2] = q.x2 * l.b + q.xy * l.a;
+    c[3] = q.y2 * l.a + q.xy * l.b;
+    c[4] = q.x2 * l.c + q.x * l.a;
+    c[5] = q.y2 * l.c + q.y * l.b;
+    c[6] = q.xy * l.c + q.x * l.b + q.y * l.a;
+    c[7] = q.x * l.c + q.k * l.a;
+    c[8] = q.y * l.c + q.k * l.b;
+    c[9] = q.k * l.c;
+}
+
+// M(z) (oracle e5_matrix)
+__device__ __forceinline__ void matrix(const double (&N)[4][9], double z, double (&M)[10][10]) {
+    Lin E[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) E[k] = Lin{N[0][k], N[1][k], z * N[2][k] + N[3][k]};
+    Quad EEt[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            Quad acc = qmul(E[3 * i], E[3 * j]);
+            acc = qadd(acc, qmul(E[3 * i + 1], E[3 * j + 1]));
+            acc = qadd(acc, qmul(E[3 * i + 2], E[3 * j + 2]));
+            EEt[i][j] = acc;
+        }
+    const Quad tr = qadd(qadd(EEt[0][0], EEt[1][1]), EEt[2][2]);
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            double t0[10], t1[10], t2[10], tt[10];
+            cmul(EEt[i][0], E[j], t0);
+            cmul(EEt[i][1], E[3 + j], t1);
+            cmul(EEt[i][2], E[6 + j], t2);
+            cmul(tr, E[3 * i + j], tt);
+#pragma unroll
+            for (int m = 0; m < 10; m++) M[3 * i + j][m] = 2.0 * (t0[m] + t1[m] + t2[m]) - tt[m];
+        }
+    double d0[10], d1[10], d2[10];
+    cmul(qsub(qmul(E[4], E[8]), qmul(E[5], E[7])), E[0], d0);
+    cmul(qsub(qmul(E[3], E[8]), qmul(E[5], E[6])), E[1], d1);
+    cmul(qsub(qmul(E[3], E[7]), qmul(E[4], E[6])), E[2], d2);
+#pragma unroll
+    for (int m = 0; m < 10; m++) M[9][m] = d0[m] - d1[m] + d2[m];
+}
+
+// in-place elimination with partial pivoting over the first NCOL columns (first maximal
+// |pivot|, rows swapped); returns false on an exactly zero pivot column, sign = (-1)^swaps
+template <int NCOL>
+__device__ __forceinline__ bool eliminate(double (&A)[10][10], double &sign) {
+#pragma unroll
+    for (int k = 0; k < NCOL; k++) {
+        int p = k;
+        double best = fabs(A[k][k]);
+#pragma unroll
+        for (int i = k + 1; i < 10; i++)
+            if (fabs(A[i][k]) > best) {
+                best = fabs(A[i][k]);
+                p = i;
+            }
+        // bring the pivot row up (register-resident: select instead of indexed swap)
+        double pr[10];
+#pragma unroll
+        for (int j = 0; j < 10; j++) {
+            double v = A[k][j];
+#pragma unroll
+            for (int i = k + 1; i < 10; i++) v = (i == p) ? A[i][j] : v;
+            pr[j] = v;
+        }
+        if (pr[k] == 0.0) return false;
+        if (p != k) {
+#pragma unroll
+            for (int i = k + 1; i < 10; i++)
+                if (i == p) {
+#pragma unroll
+                    for (int j = 0; j < 10; j++) A[i][j] = A[k][j];
+                }
+            sign = -sign;
+        }
+#pragma unroll
+        for (int j = 0; j < 10; j++) A[k][j] = pr[j];
+#pragma unroll
+        for (int i = k + 1; i < 10; i++) {
+            const double f = A[i][k] / A[k][k];
+#pragma unroll
+            for (int j = k + 1; j < 10; j++) A[i][j] -= f * A[k][j];
+        }
+    }
+    return true;
+}
+
+__device__ __forceinline__ double det10(double (&A)[10][10]) {
+    double sign = 1.0;
+    if (!eliminate<10>(A, sign)) return 0.0;
+    double det = sign;
+#pragma unroll
+    for (int k = 0; k < 10; k++) det *= A[k][k];
+    return det;
+}
+
+__device__ __forceinline__ bool null10(double (&A)[10][10], double (&v)[10]) {
+    double sign = 1.0;
+    if (!eliminate<9>(A, sign)) return false;
+    v[9] = 1.0;
+#pragma unroll
+    for (int k = 8; k >= 0; k--) {
+        double sum = A[k][9];
+#pragma unroll
+        for (int j = k + 1; j < 9; j++) sum += A[k][j] * v[j];
+        v[k] = -sum / A[k][k];
+    }
+    return true;
+}
+
+__device__ __forceinline__ double poly_eval(const double *c, int deg, double x) {
+    double r = c[deg];
+    for (int i = deg - 1; i >= 0; i--) r = r * x + c[i];
+    return r;
+}
+
+__device__ __noinline__ double poly_bisect(const double *c, int deg, double lo, double hi, double flo) {
+    for (int it = 0; it < 200; it++) {
+        const double mid = 0.5 * (lo + hi);
+        if (!(mid > lo && mid < hi)) break;
+        const double fm = poly_eval(c, deg, mid);
+        if (fm == 0.0) return mid;
+        if ((fm < 0.0) == (flo < 0.0)) {
+            lo = mid;
+            flo = fm;
+        } else {
+            hi = mid;
+        }
+    }
+    return 0.5 * (lo + hi);
+}
+
+// real roots of a[0] + ... + a[10] z^10, ascending (oracle real_roots)
+__device__ __noinline__ int real_roots10(const double *a, double *roots) {
+    int n = 10;
+    while (n > 0 && a[n] == 0.0) n--;
+    if (n == 0) return 0;
+    double R = 0.0;
+    for (int i = 0; i < n; i++) {
+        const double q = fabs(a[i] / a[n]);
+        if (q > R) R = q;
+    }
+    R = R + 1.0;
+    double crit[10], next[10];
+    int ncrit = 0;
+    for (int d = n - 1; d >= 0; d--) {
+        double c[11];
+        const int deg = n - d;
+        for (int j = 0; j <= deg; j++) {
+            double f = 1.0;
+            for (int m = j + d; m > j; m--) f *= (double)m;
+            c[j] = a[j + d] * f;
+        }
+        int nn = 0;
+        double lo = -R, flo = poly_eval(c, deg, lo);
+        for (int k = 0; k <= ncrit; k++) {
+            const double hi = k < ncrit ? crit[k] : R;
+            const double fhi = poly_eval(c, deg, hi);
+            if (hi > lo && ((flo < 0.0) != (fhi < 0.0))) next[nn++] = poly_bisect(c, deg, lo, hi, flo);
+            lo = hi;
+            flo = fhi;
+        }
+        for (int k = 0; k < nn; k++) crit[k] = next[k];
+        ncrit = nn;
+    }
+    for (int k = 0; k < ncrit; k++) roots[k] = crit[k];
+    return ncrit;
+}
+
+// null vector of a 4x4 triangulation system (oracle null4)
+__device__ __forceinline__ void null4(double (&A)[4][4], double (&X)[4]) {
+    double J[4][4];
+    jacobi_small<4, 4, false>(A, J);
+    double n2[4];
+    int m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        double a = 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) a += A[i][k] * A[i][k];
+        n2[i] = a;
+    }
+#pragma unroll
+    for (int i = 1; i < 4; i++)
+        if (n2[i] < n2[m]) m = i;
+    double U[3][4];
+    bool use[3];
+    int nu = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        if (i == m) continue;
+        const bool ok = n2[i] > 0.0;
+        const double inv = ok ? 1.0 / sqrt(n2[i]) : 0.0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) U[nu][k] = A[i][k] * inv;
+        use[nu] = ok;
+        nu++;
+    }
+    int ks = 0;
+    double bestc = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        double cc = 0.0;
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+            if (use[i]) cc += U[i][k] * U[i][k];
+        if (k == 0 || cc < bestc) {
+            bestc = cc;
+            ks = k;
+        }
+    }
+    double x[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) x[k] = k == ks ? 1.0 : 0.0;
+#pragma unroll
+    for (int pass = 0; pass < 2; pass++)
+#pragma unroll
+        for (int i = 0; i < 3; i++) {
+            if (!use[i]) continue;
+            double d = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) d += U[i][k] * x[k];
+#pragma unroll
+            for (int k = 0; k < 4; k++) x[k] -= d * U[i][k];
+        }
+    double nrm = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) nrm += x[k] * x[k];
+    nrm = sqrt(nrm);
+#pragma unroll
+    for (int k = 0; k < 4; k++) X[k] = x[k] / nrm;
+}
+
+__device__ __forceinline__ double det3p(const double (&P)[3][4]) {
+    return P[0][0] * (P[1][1] * P[2][2] - P[1][2] * P[2][1]) - P[0][1] * (P[1][0] * P[2][2] - P[1][2] * P[2][0]) +
+           P[0][2] * (P[1][0] * P[2][1] - P[1][1] * P[2][0]);
+}
+
+// CalcDepth (five_points.cpp:278-302)
+__device__ __forceinline__ double calc_depth(const double (&X)[4], const double (&P)[3][4]) {
+    double w = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) w += P[2][k] * X[k];
+    const double det = det3p(P);
+    const double a = P[0][2], b = P[1][2], c = P[2][2];
+    const double m3 = sqrt(a * a + b * b + c * c);
+    const double sign = det > 0 ? 1.0 : -1.0;
+    return (w / X[3]) * (sign / m3);
+}
+
+// both depths of a correspondence for P_ref = [I|0] and P (TriangulatePoint :304-334)
+__device__ __forceinline__ bool in_front(double x1, double y1, double x2, double y2, const double (&P)[3][4]) {
+    constexpr double Pr[3][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}};
+    double A[4][4];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        A[0][c] = x1 * Pr[2][c] - Pr[0][c];
+        A[1][c] = y1 * Pr[2][c] - Pr[1][c];
+        A[2][c] = x2 * P[2][c] - P[0][c];
+        A[3][c] = y2 * P[2][c] - P[1][c];
+    }
+    double X[4];
+    null4(A, X);
+    return calc_depth(X, Pr) > 0 && calc_depth(X, P) > 0;
+}
+
+// ProjectionsFromEssential (five_points.cpp:336-371), projection j in 0..3
+__device__ __forceinline__ void projection(const double (&U)[3][3], const double (&V)[3][3], int j,
+                                           double (&P)[3][4]) {
+    constexpr double Wm[3][3] = {{0, -1, 0}, {1, 0, 0}, {0, 0, 1}};
+    const int w = j >> 1, sgn = j & 1;
+    double T[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            double sum = 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; k++) sum += U[r][k] * (w == 0 ? Wm[k][c] : Wm[c][k]);
+            T[r][c] = sum;
+        }
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            double sum = 0.0;
+#pragma unroll
+            for (int k = 0; k < 3; k++) sum += T[r][k] * V[c][k];
+            P[r][c] = sum;
+        }
+        P[r][3] = sgn == 0 ? U[r][2] : -U[r][2];
+    }
+}
+
+// 3x3 SVD columns U, V (oracle projections(): rows Jacobi with accumulated rotations,
+// singular values descending, v3 = v1 x v2)
+__device__ __forceinline__ void svd3(const double (&E)[9], double (&U)[3][3], double (&V)[3][3]) {
+    double B[3][3], J[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            B[i][k] = E[3 * i + k];
+            J[i][k] = i == k ? 1.0 : 0.0;
+        }
+    jacobi_small<3, 3, true>(B, J);
+    double sg[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        double a = 0.0;
+#pragma unroll
+        for (int k = 0; k < 3; k++) a += B[i][k] * B[i][k];
+        sg[i] = sqrt(a);
+    }
+    int o[3] = {0, 1, 2};
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = i + 1; j < 3; j++)
+            if (sg[o[j]] > sg[o[i]]) {
+                const int t = o[i];
+                o[i] = o[j];
+                o[j] = t;
+            }
+    // o[] is a permutation: gather rows by value (no dynamic register indexing)
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        double jr[3], br[3], s = 0.0;
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            jr[r] = o[k] == 0 ? J[0][r] : o[k] == 1 ? J[1][r] : J[2][r];
+            br[r] = o[k] == 0 ? B[0][r] : o[k] == 1 ? B[1][r] : B[2][r];
+        }
+        s = o[k] == 0 ? sg[0] : o[k] == 1 ? sg[1] : sg[2];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            U[r][k] = jr[r];
+            if (k < 2) V[r][k] = br[r] / s;
+        }
+    }
+    V[0][2] = V[1][0] * V[2][1] - V[2][0] * V[1][1];
+    V[1][2] = V[2][0] * V[0][1] - V[0][0] * V[2][1];
+    V[2][2] = V[0][0] * V[1][1] - V[1][0] * V[0][1];
+}
+
+}  // namespace e5
+
+// EssentialEstimator::GetError (essential_estimator.hpp:76-107)
+__device__ __forceinline__ float essential_error(const float *E, float x1, float y1, float x2, float y2) {
+    const float l1 = E[0] * x2 + E[3] * y2 + E[6];
+    const float l2 = E[1] * x2 + E[4] * y2 + E[7];
+    const float l3 = E[2] * x2 + E[5] * y2 + E[8];
+    const float t1 = E[0] * x1 + E[1] * y1 + E[2];
+    const float t2 = E[3] * x1 + E[4] * y1 + E[5];
+    const float t3 = E[6] * x1 + E[7] * y1 + E[8];
+    const float a1 = l1 * x1 + l2 * y1 + l3;
+    const float a2 = (float)sqrt((double)(l1 * l1 + l2 * l2));
+    const float b1 = t1 * x2 + t2 * y2 + t3;
+    const float b2 = (float)sqrt((double)(t1 * t1 + t2 * t2));
+    return (fabsf(a1 / a2) + fabsf(b1 / b2)) / 2;
+}
+
+}  // namespace usac
