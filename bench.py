@@ -30,8 +30,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--estimator", choices=["homography", "fundamental"], default="homography",
-                    help="homography = cfg2 (the BASELINE metric's config); fundamental = cfg3 without SPRT")
+    ap.add_argument("--estimator", choices=["homography", "fundamental", "essential"], default="homography",
+                    help="homography = cfg2 (the BASELINE metric's config); fundamental = cfg3; essential = cfg4 "
+                         "(use --points 50000 --threshold 0.002)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=65536)
@@ -52,7 +53,7 @@ def cpu_baseline(kind, pts, thr, dlt_mode, seconds):
     from oracle import oracle as O
 
     O.lib()
-    okind = O.FUNDAMENTAL if kind == "fundamental" else O.HOMOGRAPHY
+    okind = {"fundamental": O.FUNDAMENTAL, "essential": O.ESSENTIAL}.get(kind, O.HOMOGRAPHY)
     t0 = time.perf_counter()
     O.hypothesis_loop(okind, pts, thr, 1, 50, dlt_mode)
     per = max((time.perf_counter() - t0) / 50, 1e-6)
@@ -60,7 +61,8 @@ def cpu_baseline(kind, pts, thr, dlt_mode, seconds):
     t0 = time.perf_counter()
     O.hypothesis_loop(okind, pts, thr, 2, count, dlt_mode)
     dt = time.perf_counter() - t0
-    what = "7-pt solve+oriented filter+Sampson score" if kind == "fundamental" else "DLT4+inverse+score"
+    what = {"fundamental": "7-pt solve+oriented filter+Sampson score",
+            "essential": "5-pt solve+cheirality+epipolar-distance score"}.get(kind, "DLT4+inverse+score")
     return {"value": count / dt, "unit": "hypotheses/s", "cores": 1, "kind": "port",
             "sample": "%d hypotheses of the same workload (N=%d, sample+%s, glibc sampler), "
                       "%.1f s on 1 core of %s" % (count, len(pts), what, dt,
@@ -72,11 +74,17 @@ def parity_check(usac, kind, pts, thr, dlt_mode):
     from oracle import oracle as O
 
     fund = kind == "fundamental"
-    m = 7 if fund else 4
+    ess = kind == "essential"
+    m = 7 if fund else 5 if ess else 4
     samples = O.uniform_samples(77, len(pts), m, 256)
-    est = O.Estimator(O.FUNDAMENTAL if fund else O.HOMOGRAPHY, pts, dlt_mode)
+    est = O.Estimator(O.FUNDAMENTAL if fund else O.ESSENTIAL if ess else O.HOMOGRAPHY, pts, dlt_mode)
     om, onm = est.estimate_batch(samples)
-    if fund:
+    if ess:
+        oc, osum = est.score_models(om, thr)
+        occupied = onm == 1
+        oc = np.where(occupied, oc, -1)
+        osum = np.where(occupied, osum, 0).astype(np.float32)
+    elif fund:
         slots = om.reshape(-1, 9)
         oc, osum = est.score_models(slots, thr)
         occupied = (np.arange(3)[None, :] < onm[:, None]).reshape(-1)
@@ -85,7 +93,7 @@ def parity_check(usac, kind, pts, thr, dlt_mode):
     else:
         oc, osum = est.score_models(om, thr)
         occupied = np.ones(len(oc), bool)
-    est_id = usac.ESTIMATOR.Fundamental if fund else usac.ESTIMATOR.Homography
+    est_id = usac.ESTIMATOR.Fundamental if fund else usac.ESTIMATOR.Essential if ess else usac.ESTIMATOR.Homography
     with usac.Context(est_id, pts, device=usac_device()) as ctx:
         ctx.set_dlt_mode(dlt_mode)
         c, s, _ = ctx.hypothesize_score(samples=samples, thr=thr)
@@ -139,12 +147,14 @@ def main():
     if world > 1:
         dist.init_process_group("gloo")
     fund = args.estimator == "fundamental"
-    if fund:
-        pts, _, _ = synthetic.fundamental_points(n=args.points, inlier_ratio=0.3, seed=args.seed)
+    ess = args.estimator == "essential"
+    if fund or ess:
+        pts, _, _ = synthetic.fundamental_points(n=args.points, inlier_ratio=0.3, seed=args.seed, normalized=ess)
     else:
         pts, _, _ = synthetic.homography_points(n=args.points, inlier_ratio=0.3, seed=args.seed)
     dlt_mode = 0 if args.dlt == "thin" else 1
-    ctx = usac.Context(usac.ESTIMATOR.Fundamental if fund else usac.ESTIMATOR.Homography, pts, device=local_rank)
+    est_id = usac.ESTIMATOR.Fundamental if fund else usac.ESTIMATOR.Essential if ess else usac.ESTIMATOR.Homography
+    ctx = usac.Context(est_id, pts, device=local_rank)
     ctx.set_dlt_mode(dlt_mode)
     ctx.set_score_chunks(args.chunks)
     if world > 1:
@@ -155,7 +165,7 @@ def main():
     if args.sprt:
         ctx.set_sprt(True, seed=args.seed)
     models_per_hyp = 1.0
-    if fund:  # occupied model slots per sample of the device sampler's stream (one batch)
+    if fund or ess:  # occupied model slots per sample of the device sampler's stream (one batch)
         ctx.set_sprt(False)
         c0, _, _ = ctx.hypothesize_score(B=B, seed=args.seed + 1000, first_hyp=0, thr=args.threshold)
         models_per_hyp = float((c0 >= 0).sum()) / B
@@ -205,7 +215,7 @@ def main():
         total = world * args.steps * B
         value = total / elapsed
         n = args.points
-        m = 7 if fund else 4
+        m = 7 if fund else 5 if ess else 4
         # N*S per scored model + m*4 + k*(36+8)
         if args.sprt:  # with SPRT, the bytes actually tested (16 B x tested points)
             bytes_per_hyp = 16.0 * tested_per_batch / B + m * 4 + models_per_hyp * (36 + 8)
@@ -213,10 +223,11 @@ def main():
             bytes_per_hyp = models_per_hyp * 16 * n + m * 4 + models_per_hyp * (36 + 8)
         avg_score_ms = float(np.mean(score_ms))
         achieved = bytes_per_hyp * B / (avg_score_ms * 1e-3) / 1e9
-        kname = ("void usac::k_score_f<%d>" if fund else "void usac::k_score_hf<%d, false>") % args.chunks
-        traffic = measured_traffic(kname, n, B) if not (fund or args.sprt) else None
-        kshort = ("k_score_sprt<%d>" % (3 if fund else 2)) if args.sprt else \
-            (("k_score_f<%d>" if fund else "k_score_hf<%d,false>") % args.chunks)
+        kname = ("void usac::k_score_f<%d>" if (fund or ess) else "void usac::k_score_hf<%d, false>") % args.chunks
+        traffic = measured_traffic(kname, n, B) if not (fund or ess or args.sprt) else None
+        kshort = ("k_sprt_head/tail<%d>" % (3 if fund else 4 if ess else 2)) if args.sprt else \
+            (("k_score_f<%d,%s>" % (args.chunks, "E" if ess else "F")) if (fund or ess) else
+             ("k_score_hf<%d,false>" % args.chunks))
         out = {
             "metric": "model hypotheses/sec (sample+solve+score) and inlier-count match vs ref",
             "value": value,
@@ -230,11 +241,16 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": ("synthetic (SURVEY §8(d) cfg3 generator: two views, 30% inliers, 0.5 px noise)" if fund else
-                     "synthetic (SURVEY §8(d) cfg2 generator: 30% inliers, 1 px noise, 70% uniform outliers)"),
+                     "synthetic (SURVEY §8(d) cfg4 generator: cfg3 geometry in K^-1-normalised coordinates)" if ess
+                     else "synthetic (SURVEY §8(d) cfg2 generator: 30% inliers, 1 px noise, 70% uniform outliers)"),
             "config": {"workload": ("cfg3%s: Fundamental_estimator (7-pt, oriented filter, Sampson) + "
                                     "Uniform sampler (device xorshift), %d correspondences, %d-hypothesis batch per "
                                     "GPU, %.3f models/sample" % (" + batch SPRT" if args.sprt else " without SPRT", n, B,
                                                                  models_per_hyp)) if fund else
+                                   ("cfg4%s: Essential_estimator (5-pt, cheirality, epipolar distance) + Uniform "
+                                    "sampler (device xorshift), %d correspondences, %d-hypothesis batch per GPU, "
+                                    "%.3f models/sample" % (" + batch SPRT" if args.sprt else "", n, B,
+                                                            models_per_hyp)) if ess else
                                    ("cfg2%s: Homography_estimator (4-pt DLT, %s) + Uniform sampler (device "
                                     "xorshift), %d correspondences, %d-hypothesis batch per GPU" %
                                     (" + batch SPRT" if args.sprt else "", args.dlt, n, B)),

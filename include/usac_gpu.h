@@ -47,12 +47,14 @@
 extern "C" {
 #endif
 
-#define USAC_ABI_VERSION 2
+#define USAC_ABI_VERSION 3
 
 /* = enum ESTIMATOR (usac/model.hpp:10) */
 enum { USAC_LINE2D = 1, USAC_HOMOGRAPHY = 2, USAC_FUNDAMENTAL = 3, USAC_ESSENTIAL = 4 };
-/* = enum SAMPLER (usac/model.hpp:11); Uniform and Prosac in ABI v2 */
-enum { USAC_SAMPLER_UNIFORM = 1, USAC_SAMPLER_PROSAC = 4 };
+/* = enum SAMPLER (usac/model.hpp:11): Uniform, Napsac (grid neighbours), Prosac */
+enum { USAC_SAMPLER_UNIFORM = 1, USAC_SAMPLER_NAPSAC = 3, USAC_SAMPLER_PROSAC = 4 };
+/* = enum LocOpt (usac/model.hpp:13): inner + iterative LO-RANSAC (unlimited / limited) */
+enum { USAC_LO_NONE = 0, USAC_LO_INITLORSC = 1, USAC_LO_INITFLORSC = 2 };
 /* 4-pt DLT: THIN = reference semantics (vt.row(7) of the thin 8x9 SVD, dlt.cpp:43-48);
  * NULLSPACE = true null vector. */
 enum { USAC_DLT_THIN = 0, USAC_DLT_NULLSPACE = 1 };
@@ -86,8 +88,14 @@ typedef struct usac_params {
                                    also seeds PROSAC's mt19937 (the reference uses random_device) */
     int32_t dlt_mode;           /* USAC_DLT_* */
     uint32_t batch;             /* hypotheses per device batch (0 = default) */
-    int32_t sampler;            /* USAC_SAMPLER_UNIFORM | USAC_SAMPLER_PROSAC (points sorted by quality) */
+    int32_t sampler;            /* USAC_SAMPLER_UNIFORM | _NAPSAC (grid) | _PROSAC (points sorted by quality) */
     int32_t sprt;               /* Model::setSprt (model.hpp:104): SPRT verification, sprt.hpp */
+    int32_t lo;                 /* USAC_LO_* (model.hpp:26) */
+    uint32_t lo_sample_size;          /* model.hpp:27 (14) */
+    uint32_t lo_iterative_iterations; /* model.hpp:28 (4) */
+    uint32_t lo_inner_iterations;     /* model.hpp:29 (20) */
+    uint32_t lo_threshold_multiplier; /* model.hpp:30 (10) */
+    int32_t cell_size;                /* model.hpp:43 (50): NAPSAC grid cell */
 } usac_params;
 
 /* RansacOutput getters (ransac_output.hpp:57-97) */
@@ -105,6 +113,8 @@ typedef struct usac_run_output {
     int32_t sprt_histories;     /* SPRT tests designed (sprt_histories.size()) */
     uint32_t prosac_term_len;   /* final PROSAC termination_length (n without PROSAC) */
     uint32_t rollbacks;         /* PROSAC speculative batches cut short by a termination_length change */
+    uint32_t lo_inner_iters;    /* getLOIters (ransac_output.hpp): inner LO iterations */
+    uint32_t lo_iterative_iters;
 } usac_run_output;
 
 /* ---- lifetime ----------------------------------------------------------------- */
@@ -168,9 +178,11 @@ int usac_sprt_tested(usac_ctx *ctx, uint64_t *points_tested);
 /* ---- loop --------------------------------------------------------------------- */
 uint32_t usac_std_termination(uint32_t inliers, uint32_t points_size, uint32_t sample_size, float desired_prob,
                               uint32_t max_iterations);
-/* Ransac::run (ransac.cpp:14-238) with the Uniform (glibc random() stream) or PROSAC
- * (prosac_sampler.hpp + prosac_termination_criteria.hpp) sampler, optional SPRT
- * (sprt.hpp; pool shuffle from the same glibc stream), no LO.  inliers_out (capacity n,
+/* Ransac::run (ransac.cpp:14-238) with the Uniform (glibc random() stream), NAPSAC (grid
+ * neighbours, napsac_sampler.hpp) or PROSAC (prosac_sampler.hpp + prosac_termination_criteria.hpp)
+ * sampler, optional SPRT (sprt.hpp; pool shuffle from the same glibc stream), optional
+ * inner + iterative LO-RANSAC (inner_local_optimization.hpp, iterative_local_optimization.hpp;
+ * its mt19937 seeded with seed + 1).  inliers_out (capacity n,
  * nullable): final inliers ascending.  records (nullable, capacity rec_cap): best-score
  * updates in loop order (hyp_index = iteration, SPRT double counting included). */
 int usac_ransac_run(usac_ctx *ctx, const usac_params *params, usac_run_output *out, int32_t *inliers_out,

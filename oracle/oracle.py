@@ -33,15 +33,23 @@ class OrcResult(ctypes.Structure):
         ("sprt_rejected", ctypes.c_int),
         ("sprt_histories", ctypes.c_int),
         ("prosac_term_len", ctypes.c_uint),
+        ("lo_inner_iters", ctypes.c_uint),
+        ("lo_iterative_iters", ctypes.c_uint),
     ]
 
 
 SAMPLER_UNIFORM, SAMPLER_NAPSAC, SAMPLER_PROSAC = 1, 3, 4  # usac/model.hpp:11
 
 
+LO_NONE, LO_INITLORSC, LO_INITFLORSC = 0, 1, 2  # usac/model.hpp:13
+
+
 class OrcConfig(ctypes.Structure):
     _fields_ = [("threshold", ctypes.c_float), ("desired_prob", ctypes.c_float), ("max_iterations", ctypes.c_uint),
-                ("seed", ctypes.c_uint), ("dlt_mode", ctypes.c_int), ("sampler", ctypes.c_int), ("sprt", ctypes.c_int)]
+                ("seed", ctypes.c_uint), ("dlt_mode", ctypes.c_int), ("sampler", ctypes.c_int), ("sprt", ctypes.c_int),
+                ("lo", ctypes.c_int), ("lo_sample_size", ctypes.c_uint), ("lo_iterative_iterations", ctypes.c_uint),
+                ("lo_inner_iterations", ctypes.c_uint), ("lo_threshold_multiplier", ctypes.c_uint),
+                ("cell_size", ctypes.c_int)]
 
 
 class OrcMT(ctypes.Structure):
@@ -263,7 +271,7 @@ def std_termination(inliers, n, m, p, max_iters=10000):
 
 
 def ransac_run(kind, points, thr, p, seed, max_iters=10000, dlt_mode=DLT_THIN, rec_cap=4096,
-               sampler=SAMPLER_UNIFORM, sprt=False):
+               sampler=SAMPLER_UNIFORM, sprt=False, lo=LO_NONE, lo_params=(14, 4, 20, 10), cell_size=50):
     points = np.ascontiguousarray(points, dtype=np.float32)
     n = points.shape[0]
     res = OrcResult()
@@ -271,7 +279,7 @@ def ransac_run(kind, points, thr, p, seed, max_iters=10000, dlt_mode=DLT_THIN, r
     ri = np.zeros(rec_cap, dtype=np.uint32)
     rc = np.zeros(rec_cap, dtype=np.int32)
     rs = np.zeros(rec_cap, dtype=np.float32)
-    cfg = OrcConfig(thr, p, max_iters, seed, dlt_mode, sampler, 1 if sprt else 0)
+    cfg = OrcConfig(thr, p, max_iters, seed, dlt_mode, sampler, 1 if sprt else 0, lo, *lo_params, cell_size)
     ret = lib().orc_ransac_run_cfg(kind, _p(points, _f32p), n, ctypes.byref(cfg), ctypes.byref(res), _p(inl, _i32p),
                                    _p(ri, _u32p), _p(rc, _i32p), _p(rs, _f32p), rec_cap)
     k = min(res.n_records, rec_cap)
@@ -288,7 +296,28 @@ def ransac_run(kind, points, thr, p, seed, max_iters=10000, dlt_mode=DLT_THIN, r
         "sprt_rejected": res.sprt_rejected,
         "sprt_histories": res.sprt_histories,
         "prosac_term_len": res.prosac_term_len,
+        "lo_inner_iters": res.lo_inner_iters,
+        "lo_iterative_iters": res.lo_iterative_iters,
     }
+
+
+def grid_neighbors(points, cell_size):
+    """Grid neighbour lists (nearest_neighbors.cpp:160-202) as a list of int arrays."""
+    L = lib()
+    pts = np.ascontiguousarray(points, dtype=np.float32)
+    L.orc_grid_new.restype = ctypes.c_void_p
+    L.orc_grid_new.argtypes = [_f32p, ctypes.c_uint, ctypes.c_int]
+    L.orc_grid_count.argtypes = [ctypes.c_void_p, ctypes.c_uint]
+    L.orc_grid_list.argtypes = [ctypes.c_void_p, ctypes.c_uint]
+    L.orc_grid_list.restype = _i32p
+    L.orc_grid_free.argtypes = [ctypes.c_void_p]
+    g = L.orc_grid_new(_p(pts, _f32p), len(pts), cell_size)
+    out = []
+    for i in range(len(pts)):
+        k = L.orc_grid_count(g, i)
+        out.append(np.ctypeslib.as_array(L.orc_grid_list(g, i), shape=(k,)).copy() if k else np.zeros(0, np.int32))
+    L.orc_grid_free(g)
+    return out
 
 
 def mt19937_stream(seed, count):

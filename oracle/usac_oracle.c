@@ -1795,13 +1795,252 @@ unsigned int orc_sprt_upper_bound(const orc_sprt *s, int inliers_size) {
     return k < s->max_iters ? k : s->max_iters;
 }
 
-/* ------------------------------------------------------------ Ransac::run */
 static int score_bigger(int c1, float s1, int c2, float s2) {
     /* Score::bigger (quality.hpp:22-26) */
     if (c1 > c2) return 1;
     if (c1 == c2) return s1 > s2;
     return 0;
 }
+
+/* ------------------------------------------------------------ NAPSAC (grid) */
+/* NearestNeighbors::getGridNearestNeighbors (nearest_neighbors.cpp:160-202): cell =
+ * ((int)(x1/cs), (int)(y1/cs), (int)(x2/cs), (int)(y2/cs)) (float division, truncation);
+ * a point's neighbours are the other points of its cell in ascending index order (the
+ * pair loop over each cell's index-ordered list yields exactly that order). CSR output. */
+typedef struct {
+    int c[4];
+    int i;
+} cell_key;
+
+static int cell_cmp(const void *a, const void *b) {
+    const cell_key *x = (const cell_key *)a, *y = (const cell_key *)b;
+    for (int k = 0; k < 4; k++)
+        if (x->c[k] != y->c[k]) return x->c[k] < y->c[k] ? -1 : 1;
+    return x->i < y->i ? -1 : x->i > y->i;
+}
+
+struct orc_grid {
+    unsigned int n;
+    int *off; /* n + 1 */
+    int *nb;
+};
+
+orc_grid *orc_grid_new(const float *pts, unsigned int n, int cell_size) {
+    orc_grid *g = (orc_grid *)calloc(1, sizeof(*g));
+    g->n = n;
+    cell_key *keys = (cell_key *)malloc(sizeof(cell_key) * (n ? n : 1));
+    for (unsigned int i = 0; i < n; i++) {
+        for (int k = 0; k < 4; k++) keys[i].c[k] = (int)(pts[4 * (size_t)i + k] / (float)cell_size);
+        keys[i].i = (int)i;
+    }
+    qsort(keys, n, sizeof(cell_key), cell_cmp);
+    int *cnt = (int *)calloc(n ? n : 1, sizeof(int));
+    int *cell_start = (int *)malloc(sizeof(int) * (n ? n : 1)); /* per sorted position */
+    for (unsigned int a = 0; a < n;) {
+        unsigned int b = a;
+        while (b < n && cell_cmp(&keys[a], &keys[b]) <= 0 && memcmp(keys[a].c, keys[b].c, sizeof(keys[a].c)) == 0) b++;
+        for (unsigned int k = a; k < b; k++) {
+            cnt[keys[k].i] = (int)(b - a) - 1;
+            cell_start[k] = (int)a;
+        }
+        a = b;
+    }
+    g->off = (int *)malloc(sizeof(int) * (n + 1));
+    g->off[0] = 0;
+    for (unsigned int i = 0; i < n; i++) g->off[i + 1] = g->off[i] + cnt[i];
+    g->nb = (int *)malloc(sizeof(int) * (size_t)(g->off[n] ? g->off[n] : 1));
+    for (unsigned int k = 0; k < n;) {
+        const unsigned int a = (unsigned int)cell_start[k];
+        unsigned int b = k;
+        while (b < n && cell_start[b] == (int)a) b++;
+        for (unsigned int u = a; u < b; u++) {
+            int w = g->off[keys[u].i];
+            for (unsigned int v = a; v < b; v++)
+                if (v != u) g->nb[w++] = keys[v].i;
+        }
+        k = b;
+    }
+    free(keys);
+    free(cnt);
+    free(cell_start);
+    return g;
+}
+
+void orc_grid_free(orc_grid *g) {
+    if (!g) return;
+    free(g->off);
+    free(g->nb);
+    free(g);
+}
+
+int orc_grid_count(const orc_grid *g, unsigned int i) { return g->off[i + 1] - g->off[i]; }
+const int *orc_grid_list(const orc_grid *g, unsigned int i) { return g->nb + g->off[i]; }
+
+/* NapsacSampler with Grid neighbours (napsac_sampler.hpp:40-158) over the glibc stream;
+ * ArrayRandomGenerator (array_random_generator.hpp:21-49) with its member `max` defined 0
+ * (SURVEY Q8).  A point needs >= m neighbours (Q18); after n failed draws the sampler turns
+ * uniform and thereafter rewrites only sample[0] (subset size 1, reference behaviour). */
+struct orc_napsac {
+    const orc_grid *g;
+    unsigned int n, m, max;
+    int *array, *next;
+    int do_uniform;
+};
+
+orc_napsac *orc_napsac_new(const orc_grid *g, unsigned int n, unsigned int m) {
+    orc_napsac *s = (orc_napsac *)calloc(1, sizeof(*s));
+    s->g = g;
+    s->n = n;
+    s->m = m;
+    s->array = (int *)malloc(sizeof(int) * (n ? n : 1));
+    for (unsigned int i = 0; i < n; i++) s->array[i] = (int)i;
+    s->next = (int *)calloc(n ? n : 1, sizeof(int));
+    s->max = 0;
+    return s;
+}
+
+void orc_napsac_free(orc_napsac *s) {
+    if (!s) return;
+    free(s->array);
+    free(s->next);
+    free(s);
+}
+
+static int napsac_random(orc_napsac *s) {
+    if (s->max == 0) s->max = s->n;
+    const unsigned int k = (unsigned int)random() % s->max;
+    const int v = s->array[k];
+    s->max--;
+    s->array[k] = s->array[s->max];
+    s->array[s->max] = v;
+    return v;
+}
+
+void orc_napsac_sample(orc_napsac *s, int *sample) {
+    if (s->do_uniform) {
+        sample[0] = napsac_random(s);
+        return;
+    }
+    unsigned int i;
+    int initial = 0;
+    for (i = 0; i < s->n; i++) {
+        initial = napsac_random(s);
+        if ((unsigned int)orc_grid_count(s->g, (unsigned int)initial) < s->m) continue;
+        break;
+    }
+    if (i == s->n) {
+        s->do_uniform = 1;
+        return;
+    }
+    sample[0] = initial;
+    const int *nb = orc_grid_list(s->g, (unsigned int)initial);
+    const int sz = orc_grid_count(s->g, (unsigned int)initial);
+    for (unsigned int k = 1; k < s->m; k++) {
+        sample[k] = nb[s->next[initial]];
+        s->next[initial]++;
+        if (s->next[initial] >= sz) s->next[initial] = 0;
+    }
+}
+
+/* ------------------------------------------------------------ LO-RANSAC */
+/* InnerLocalOptimization (inner_local_optimization.hpp:40-133) + IterativeLocalOptimization
+ * (iterative_local_optimization.hpp:28-136).  Its UniformRandomGenerator is an mt19937 seeded
+ * here with seed + 1 (the reference: std::random_device).  lo_model's threshold persists
+ * across calls and compounds. */
+typedef struct {
+    orc_mt g;
+    int limited;
+    unsigned int inner, iters, limit, mult, m, n;
+    float theta, lo_thr, step;
+    int *max_inl, *lo_inl, *lo_sample;
+    unsigned int inner_count, iterative_count;
+    float lo_model[9];
+} orc_lo;
+
+static void lo_init(orc_lo *L, const orc_config *cfg, unsigned int n, unsigned int m) {
+    memset(L, 0, sizeof(*L));
+    orc_mt_seed(&L->g, cfg->seed + 1u);
+    L->limited = cfg->lo == ORC_LO_INITFLORSC;
+    L->inner = cfg->lo_inner_iterations;
+    L->iters = cfg->lo_iterative_iterations;
+    L->limit = cfg->lo_sample_size;
+    L->mult = cfg->lo_threshold_multiplier;
+    L->m = m;
+    L->n = n;
+    L->theta = cfg->threshold;
+    L->lo_thr = cfg->threshold;
+    L->step = (L->theta * L->mult - L->theta) / L->iters;
+    L->max_inl = (int *)malloc(sizeof(int) * (n ? n : 1));
+    L->lo_inl = (int *)malloc(sizeof(int) * (n ? n : 1));
+    L->lo_sample = (int *)malloc(sizeof(int) * (L->limit ? L->limit : 1));
+}
+
+static void lo_free(orc_lo *L) {
+    free(L->max_inl);
+    free(L->lo_inl);
+    free(L->lo_sample);
+}
+
+/* returns fail */
+static int lo_iterative(orc_lo *L, orc_est *e, int *lo_cnt, float *lo_sum, int best_cnt, float best_sum) {
+    for (unsigned int it = 0; it < L->iters; it++) {
+        L->lo_thr -= L->step;
+        if (*lo_cnt <= (int)L->m) break;
+        if (L->limited) {
+            if (*lo_cnt > (int)L->limit) {
+                mt_unique_set(&L->g, L->lo_sample, L->limit, (unsigned int)(*lo_cnt - 1));
+                for (unsigned int k = 0; k < L->limit; k++) L->lo_sample[k] = L->lo_inl[L->lo_sample[k]];
+                if (!orc_est_nonminimal(e, L->lo_sample, L->limit, L->lo_model)) continue;
+            } else {
+                if (!orc_est_nonminimal(e, L->lo_inl, (unsigned int)*lo_cnt, L->lo_model)) break;
+            }
+            orc_quality(e, L->lo_model, L->lo_thr, lo_cnt, lo_sum, L->lo_inl);
+        } else {
+            if (!orc_est_nonminimal(e, L->lo_inl, (unsigned int)*lo_cnt, L->lo_model)) break;
+            orc_quality(e, L->lo_model, L->lo_thr, lo_cnt, lo_sum, L->lo_inl);
+            if (score_bigger(best_cnt, best_sum, *lo_cnt, *lo_sum)) break;
+        }
+        L->iterative_count++;
+    }
+    int fail = 0;
+    if (fabsf(L->lo_thr - L->theta) > 0.00001) {
+        fail = 1;
+        L->lo_thr = L->theta;
+    }
+    return fail;
+}
+
+/* GetModelScore(model, score): model / (cnt, sum) improved in place */
+static void lo_run(orc_lo *L, orc_est *e, float *model, int *cnt, float *sum) {
+    if (*cnt < 12) return;
+    int c0;
+    float s0;
+    orc_quality(e, model, L->theta, &c0, &s0, L->max_inl);
+    for (unsigned int it = 0; it < L->inner; it++) {
+        if (*cnt > (int)L->limit) {
+            mt_unique_set(&L->g, L->lo_sample, L->limit, (unsigned int)(*cnt - 1));
+            for (unsigned int k = 0; k < L->limit; k++) L->lo_sample[k] = L->max_inl[L->lo_sample[k]];
+            if (!orc_est_nonminimal(e, L->lo_sample, L->limit, L->lo_model)) continue;
+        } else {
+            if (!orc_est_nonminimal(e, L->max_inl, (unsigned int)*cnt, L->lo_model)) return;
+        }
+        L->lo_thr = L->mult * L->lo_thr;
+        int lo_cnt;
+        float lo_sum;
+        orc_quality(e, L->lo_model, L->lo_thr, &lo_cnt, &lo_sum, L->lo_inl);
+        if (lo_cnt <= (int)L->m) continue;
+        const int fail = lo_iterative(L, e, &lo_cnt, &lo_sum, *cnt, *sum);
+        if (!fail && score_bigger(lo_cnt, lo_sum, *cnt, *sum)) {
+            memcpy(model, L->lo_model, sizeof(float) * 9);
+            *cnt = lo_cnt;
+            *sum = lo_sum;
+            memcpy(L->max_inl, L->lo_inl, sizeof(int) * (size_t)lo_cnt);
+        }
+        L->inner_count++;
+    }
+}
+
+/* ------------------------------------------------------------ Ransac::run */
 
 int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_config *cfg, orc_result *out,
                        int *inliers_out, unsigned int *rec_iter, int *rec_count, float *rec_score, int rec_cap) {
@@ -1810,11 +2049,17 @@ int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_
     const int m = orc_est_sample_size(e);
     const float threshold = cfg->threshold;
     const int prosac = cfg->sampler == ORC_SAMPLER_PROSAC;
+    const int napsac = cfg->sampler == ORC_SAMPLER_NAPSAC;
     /* Ransac ctor order (ransac.hpp:41-93): sampler, termination, then SPRT (whose pool
      * shuffle consumes n glibc draws before the Uniform sampler's first). */
     orc_srandom(cfg->seed);
-    orc_uniform *smp = prosac ? NULL : orc_uniform_new(n, (unsigned int)m);
+    orc_uniform *smp = (prosac || napsac) ? NULL : orc_uniform_new(n, (unsigned int)m);
     orc_prosac *ps = prosac ? orc_prosac_new((unsigned int)m, n, cfg->seed) : NULL;
+    orc_lo lo;
+    const int use_lo = cfg->lo == ORC_LO_INITLORSC || cfg->lo == ORC_LO_INITFLORSC;
+    if (use_lo) lo_init(&lo, cfg, n, (unsigned int)m);
+    orc_grid *grid = napsac ? orc_grid_new(points, n, cfg->cell_size) : NULL;
+    orc_napsac *ns = napsac ? orc_napsac_new(grid, n, (unsigned int)m) : NULL;
     orc_prosac_term *pt = prosac ? orc_prosac_term_new(orc_prosac_growth(ps), n, (unsigned int)m, cfg->desired_prob,
                                                        cfg->max_iterations)
                                  : NULL;
@@ -1822,6 +2067,7 @@ int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_
     int *inl = (int *)malloc(sizeof(int) * (n ? n : 1));
     unsigned char *flags = (unsigned char *)malloc(n ? n : 1);
     int sample[16];
+    memset(sample, 0, sizeof(sample));
     float models[27], best_model[9];
     memset(best_model, 0, sizeof(best_model));
     int best_cnt = 0, nrec = 0;
@@ -1834,6 +2080,8 @@ int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_
         if (prosac) {
             orc_prosac_set_term_len(ps, orc_prosac_term_length(pt));
             orc_prosac_sample(ps, sample);
+        } else if (napsac) {
+            orc_napsac_sample(ns, sample);
         } else {
             orc_uniform_sample(smp, sample);
         }
@@ -1855,6 +2103,7 @@ int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_
                 orc_quality(e, models + 9 * i, threshold, &cnt, &sum, NULL);
             }
             if (score_bigger(cnt, sum, best_cnt, best_sum)) {
+                if (use_lo) lo_run(&lo, e, models + 9 * i, &cnt, &sum); /* ransac.cpp:110-112 */
                 best_cnt = cnt;
                 best_sum = sum;
                 memcpy(best_model, models + 9 * i, sizeof(best_model));
@@ -1886,6 +2135,8 @@ int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_
     out->polish_passes = 0;
     out->sprt_histories = sp ? (int)orc_sprt_histories(sp) : 0;
     out->prosac_term_len = pt ? orc_prosac_term_length(pt) : n;
+    out->lo_inner_iters = use_lo ? lo.inner_count : 0;
+    out->lo_iterative_iters = use_lo ? lo.iterative_count : 0;
     memcpy(out->minimal_model, best_model, sizeof(best_model));
     out->minimal_inliers = best_cnt;
     if (best_cnt == 0) {
@@ -1918,6 +2169,9 @@ int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_
     orc_prosac_free(ps);
     orc_prosac_term_free(pt);
     orc_sprt_free(sp);
+    orc_napsac_free(ns);
+    orc_grid_free(grid);
+    if (use_lo) lo_free(&lo);
     orc_est_free(e);
     return rc;
 }
@@ -1934,6 +2188,12 @@ int orc_ransac_run(int kind, const float *points, unsigned int n, float threshol
     cfg.dlt_mode = dlt_mode;
     cfg.sampler = ORC_SAMPLER_UNIFORM;
     cfg.sprt = 0;
+    cfg.lo = 0;
+    cfg.lo_sample_size = 14;
+    cfg.lo_iterative_iterations = 4;
+    cfg.lo_inner_iterations = 20;
+    cfg.lo_threshold_multiplier = 10;
+    cfg.cell_size = 50;
     return orc_ransac_run_cfg(kind, points, n, &cfg, out, inliers_out, rec_iter, rec_count, rec_score, rec_cap);
 }
 

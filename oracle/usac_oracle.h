@@ -93,16 +93,32 @@ typedef struct {
     int sprt_rejected;    /* models SPRT rejected */
     int sprt_histories;   /* SPRT tests designed (history length) */
     unsigned int prosac_term_len; /* final PROSAC termination_length (n without PROSAC) */
+    unsigned int lo_inner_iters, lo_iterative_iters; /* RansacOutput LO counters */
 } orc_result;
 
 enum { ORC_SAMPLER_UNIFORM = 1, ORC_SAMPLER_NAPSAC = 3, ORC_SAMPLER_PROSAC = 4 }; /* = SAMPLER, usac/model.hpp:11 */
+enum { ORC_LO_NONE = 0, ORC_LO_INITLORSC = 1, ORC_LO_INITFLORSC = 2 };              /* = LocOpt, usac/model.hpp:13 */
 typedef struct {
     float threshold, desired_prob;
     unsigned int max_iterations, seed;
     int dlt_mode;
-    int sampler; /* ORC_SAMPLER_* */
+    int sampler; /* ORC_SAMPLER_* (NAPSAC: grid neighbours of cell_size) */
     int sprt;    /* Model::setSprt */
+    int lo;      /* ORC_LO_* */
+    unsigned int lo_sample_size, lo_iterative_iterations, lo_inner_iterations, lo_threshold_multiplier; /* model.hpp:27-30 */
+    int cell_size; /* model.hpp:43 */
 } orc_config;
+
+/* grid neighbours (nearest_neighbors.cpp:160-202) and the NAPSAC grid sampler (napsac_sampler.hpp) */
+typedef struct orc_grid orc_grid;
+orc_grid *orc_grid_new(const float *pts, unsigned int n, int cell_size);
+void orc_grid_free(orc_grid *g);
+int orc_grid_count(const orc_grid *g, unsigned int i);
+const int *orc_grid_list(const orc_grid *g, unsigned int i);
+typedef struct orc_napsac orc_napsac;
+orc_napsac *orc_napsac_new(const orc_grid *g, unsigned int n, unsigned int m);
+void orc_napsac_free(orc_napsac *s);
+void orc_napsac_sample(orc_napsac *s, int *sample);
 
 /* Ransac::run with the sampler / SPRT of cfg (PROSAC: points sorted by quality; its
  * mt19937 is seeded with cfg->seed instead of std::random_device). */

@@ -15,7 +15,7 @@ import subprocess
 
 import numpy as np
 
-__all__ = ["ESTIMATOR", "SAMPLER", "DLT", "Model", "Ransac", "RansacOutput", "Score", "Context", "Record",
+__all__ = ["ESTIMATOR", "SAMPLER", "LocOpt", "NeighborsSearch", "DLT", "Model", "Ransac", "RansacOutput", "Score", "Context", "Record",
            "build", "lib", "std_termination", "uniform_samples", "prosac_samples", "sprt_pool", "UsacError"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -38,6 +38,18 @@ class SAMPLER(enum.IntEnum):  # usac/model.hpp:11
     Prosac = 4
     Evsac = 5
     ProsacNapsac = 6
+
+
+class LocOpt(enum.IntEnum):  # usac/model.hpp:13 (GC and IRLS are out of scope)
+    NullLO = 0
+    InItLORsc = 1
+    InItFLORsc = 2
+
+
+class NeighborsSearch(enum.IntEnum):  # usac/model.hpp:12 (Nanoflann KNN is out of scope)
+    NullN = 0
+    Nanoflann = 1
+    Grid = 2
 
 
 class DLT(enum.IntEnum):
@@ -63,7 +75,10 @@ class Record(ctypes.Structure):
 class _Params(ctypes.Structure):
     _fields_ = [("threshold", ctypes.c_float), ("desired_prob", ctypes.c_float), ("max_iterations", ctypes.c_uint32),
                 ("seed", ctypes.c_uint32), ("dlt_mode", ctypes.c_int32), ("batch", ctypes.c_uint32),
-                ("sampler", ctypes.c_int32), ("sprt", ctypes.c_int32)]
+                ("sampler", ctypes.c_int32), ("sprt", ctypes.c_int32), ("lo", ctypes.c_int32),
+                ("lo_sample_size", ctypes.c_uint32), ("lo_iterative_iterations", ctypes.c_uint32),
+                ("lo_inner_iterations", ctypes.c_uint32), ("lo_threshold_multiplier", ctypes.c_uint32),
+                ("cell_size", ctypes.c_int32)]
 
 
 class _RunOutput(ctypes.Structure):
@@ -71,7 +86,8 @@ class _RunOutput(ctypes.Structure):
                 ("time_us", ctypes.c_int64), ("n_records", ctypes.c_int32), ("polish_passes", ctypes.c_int32),
                 ("minimal_model", ctypes.c_float * 9), ("minimal_inliers", ctypes.c_int32),
                 ("batches", ctypes.c_uint32), ("sprt_rejected", ctypes.c_int32), ("sprt_histories", ctypes.c_int32),
-                ("prosac_term_len", ctypes.c_uint32), ("rollbacks", ctypes.c_uint32)]
+                ("prosac_term_len", ctypes.c_uint32), ("rollbacks", ctypes.c_uint32),
+                ("lo_inner_iters", ctypes.c_uint32), ("lo_iterative_iters", ctypes.c_uint32)]
 
 
 # every symbol include/usac_gpu.h declares (checked by tests/test_abi.py)
@@ -397,6 +413,13 @@ class Model:
         self.dlt_mode = DLT.THIN
         self.batch = 0
         self.device = 0
+        self.lo = LocOpt.NullLO
+        self.lo_sample_size = 14
+        self.lo_iterative_iterations = 4
+        self.lo_inner_iterations = 20
+        self.lo_threshold_multiplier = 10
+        self.cell_size = 50
+        self.neighborsType = NeighborsSearch.NullN
 
     def ResetRandomGenerator(self, reset):
         self.reset_random_generator = bool(reset)
@@ -414,6 +437,17 @@ class Model:
     def setSprt(self, sprt):
         self.sprt = bool(sprt)
 
+    def setLOParametres(self, lo_iterative_iters, lo_inner_iters, lo_thresh_mult):
+        self.lo_iterative_iterations = int(lo_iterative_iters)
+        self.lo_inner_iterations = int(lo_inner_iters)
+        self.lo_threshold_multiplier = int(lo_thresh_mult)
+
+    def setCellSize(self, cell_size):
+        self.cell_size = int(cell_size)
+
+    def setNeighborsType(self, t):
+        self.neighborsType = NeighborsSearch(t)
+
     def setDLTMode(self, mode):
         self.dlt_mode = DLT(mode)
 
@@ -421,13 +455,14 @@ class Model:
 class RansacOutput:
     """usac/ransac/ransac_output.hpp:11-99 getters."""
 
-    def __init__(self, model, inliers, time_us, n_inliers, iters, raw):
+    def __init__(self, model, inliers, time_us, n_inliers, iters, raw, lo_iters=0):
         self._model = model
         self._inliers = inliers
         self._time = time_us
         self._n = n_inliers
         self._iters = iters
         self.raw = raw
+        self._lo = lo_iters
 
     def getModel(self):
         return self._model
@@ -445,15 +480,19 @@ class RansacOutput:
         return self._iters
 
     def getLOIters(self):
-        return 0
+        return self._lo
 
 
 class Ransac:
     """usac/ransac/ransac.hpp:41-115 -- Ransac(model, points); run(); getRansacOutput()."""
 
     def __init__(self, model, points):
-        if model.sampler not in (SAMPLER.Uniform, SAMPLER.Prosac):
-            raise NotImplementedError("sampler %s is not in ABI v2 (Uniform, Prosac)" % model.sampler.name)
+        if model.sampler not in (SAMPLER.Uniform, SAMPLER.Prosac, SAMPLER.Napsac):
+            raise NotImplementedError("sampler %s is not in ABI v3 (Uniform, Napsac, Prosac)" % model.sampler.name)
+        if model.sampler == SAMPLER.Napsac and model.neighborsType == NeighborsSearch.Nanoflann:
+            raise NotImplementedError("NAPSAC KNN neighbours (nanoflann) are not in ABI v3; use the Grid")
+        if int(model.lo) not in (0, 1, 2):
+            raise NotImplementedError("LO %r is not in ABI v3 (InItLORsc, InItFLORsc)" % model.lo)
         self.model = model
         self.ctx = Context(model.estimator, points, device=model.device)
         self._out = None
@@ -466,7 +505,8 @@ class Ransac:
         if m.reset_random_generator and seed == 0:
             seed = int.from_bytes(os.urandom(4), "little") or 1
         p = _Params(m.threshold, m.desired_prob, m.max_iterations, seed, int(m.dlt_mode), m.batch, int(m.sampler),
-                    1 if m.sprt else 0)
+                    1 if m.sprt else 0, int(m.lo), m.lo_sample_size, m.lo_iterative_iterations,
+                    m.lo_inner_iterations, m.lo_threshold_multiplier, m.cell_size)
         out = _RunOutput()
         inl = np.zeros(self.ctx.n, dtype=np.int32)
         recs = (Record * rec_cap)()
@@ -481,9 +521,9 @@ class Ransac:
                "minimal_inliers": out.minimal_inliers, "polish_passes": out.polish_passes,
                "n_records": out.n_records, "batches": out.batches, "sprt_rejected": out.sprt_rejected,
                "sprt_histories": out.sprt_histories, "prosac_term_len": out.prosac_term_len,
-               "rollbacks": out.rollbacks}
+               "rollbacks": out.rollbacks, "lo_iterative_iters": out.lo_iterative_iters}
         self._out = RansacOutput(np.array(out.model[:], dtype=np.float32), inl[: out.inliers].copy(), out.time_us,
-                                 out.inliers, out.iters, raw)
+                                 out.inliers, out.iters, raw, out.lo_inner_iters)
 
     def getRansacOutput(self):
         return self._out

@@ -478,86 +478,6 @@ __global__ __launch_bounds__(256) void k_argmax_final(const BestEntry *__restric
     }
 }
 
-// ------------------------------------------------------------------------ inliers (exact)
-// Quality::getNumberInliers(get_inliers=true) for one model: 256 lanes evaluate a tile of
-// points, then lane 0 walks the tile in point order -- ascending inlier list and the
-// sequential fp32 sum of quality.hpp:80-87.
-__global__ __launch_bounds__(256) void k_inliers_h(const float4 *__restrict__ pts, uint32_t n, const float *model,
-                                                   float thr, int32_t *idx, int32_t *count, float *sum) {
-    __shared__ float s_err[256];
-    __shared__ float m[18];
-    if (threadIdx.x == 0) {
-        for (int k = 0; k < 9; k++) m[k] = model[k];
-        inv3x3(m, m + 9);
-    }
-    __syncthreads();
-    float H[9], Hi[9];
-    for (int k = 0; k < 9; k++) {
-        H[k] = m[k];
-        Hi[k] = m[9 + k];
-    }
-    int cnt = 0;
-    float s = 0.f;
-    for (uint32_t base = 0; base < n; base += 256) {
-        const uint32_t i = base + threadIdx.x;
-        float e = 0.f;
-        if (i < n) {
-            float4 p = pts[i];
-            e = homography_error(H, Hi, p.x, p.y, p.z, p.w);
-        }
-        s_err[threadIdx.x] = e;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t lim = n - base < 256 ? n - base : 256;
-            for (uint32_t j = 0; j < lim; j++) {
-                const float e2 = s_err[j];
-                if (e2 < thr) {
-                    idx[cnt++] = (int32_t)(base + j);
-                    s += e2;
-                }
-            }
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        *count = cnt;
-        *sum = s;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_inliers_line(const float2 *__restrict__ pts, uint32_t n, const float *model,
-                                                      float thr, int32_t *idx, int32_t *count, float *sum) {
-    __shared__ float s_err[256];
-    const float a = model[0], b = model[1], c = model[2];
-    int cnt = 0;
-    float s = 0.f;
-    for (uint32_t base = 0; base < n; base += 256) {
-        const uint32_t i = base + threadIdx.x;
-        float e = 0.f;
-        if (i < n) {
-            float2 p = pts[i];
-            e = line2d_error(a, b, c, p.x, p.y);
-        }
-        s_err[threadIdx.x] = e;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t lim = n - base < 256 ? n - base : 256;
-            for (uint32_t j = 0; j < lim; j++) {
-                const float e2 = s_err[j];
-                if (e2 < thr) {
-                    idx[cnt++] = (int32_t)(base + j);
-                    s += e2;
-                }
-            }
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        *count = cnt;
-        *sum = s;
-    }
-}
-
 // ------------------------------------------------------------------------ launchers
 #define LAUNCH_CHECK() hipGetLastError()
 
@@ -651,18 +571,6 @@ hipError_t launch_argmax(hipStream_t st, const int32_t *counts, const float *sum
     hipLaunchKernelGGL(k_argmax_part, dim3(nparts), dim3(256), 0, st, counts, sums, B, part);
     hipLaunchKernelGGL(k_argmax_final, dim3(1), dim3(256), 0, st, part, nparts, B, models, ncomp, first_hyp, spk,
                        out);
-    return LAUNCH_CHECK();
-}
-
-hipError_t launch_inliers_h(hipStream_t st, const float4 *pts, uint32_t n, const float *model, float thr,
-                            int32_t *idx, int32_t *count, float *sum) {
-    hipLaunchKernelGGL(k_inliers_h, dim3(1), dim3(256), 0, st, pts, n, model, thr, idx, count, sum);
-    return LAUNCH_CHECK();
-}
-
-hipError_t launch_inliers_line(hipStream_t st, const float2 *pts, uint32_t n, const float *model, float thr,
-                               int32_t *idx, int32_t *count, float *sum) {
-    hipLaunchKernelGGL(k_inliers_line, dim3(1), dim3(256), 0, st, pts, n, model, thr, idx, count, sum);
     return LAUNCH_CHECK();
 }
 

@@ -171,43 +171,6 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_f(const float4 *__restric
     }
 }
 
-// Quality::getNumberInliers(get_inliers=true) for one F / E (exact, ascending, sequential Σ)
-template <int EST>
-__global__ __launch_bounds__(256) void k_inliers_f(const float4 *__restrict__ pts, uint32_t n, const float *model,
-                                                   float thr, int32_t *idx, int32_t *count, float *sum) {
-    __shared__ float s_err[256];
-    float f[9];
-#pragma unroll
-    for (int k = 0; k < 9; k++) f[k] = model[k];
-    int cnt = 0;
-    float s = 0.f;
-    for (uint32_t base = 0; base < n; base += 256) {
-        const uint32_t i = base + threadIdx.x;
-        float e = 0.f;
-        if (i < n) {
-            const float4 p = pts[i];
-            e = two_view_error<EST>(f, p.x, p.y, p.z, p.w);
-        }
-        s_err[threadIdx.x] = e;
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            const uint32_t lim = n - base < 256 ? n - base : 256;
-            for (uint32_t j = 0; j < lim; j++) {
-                const float e2 = s_err[j];
-                if (e2 < thr) {
-                    idx[cnt++] = (int32_t)(base + j);
-                    s += e2;
-                }
-            }
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        *count = cnt;
-        *sum = s;
-    }
-}
-
 hipError_t launch_solve_f7(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
                            int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, float *models,
                            int32_t *counts, uint32_t *list, uint32_t *list_n) {
@@ -239,16 +202,6 @@ hipError_t launch_score_f(hipStream_t st, int estimator, int chunks, const float
         default: return hipErrorInvalidValue;
     }
 #undef SF
-    return hipGetLastError();
-}
-
-hipError_t launch_inliers_f(hipStream_t st, int estimator, const float4 *pts, uint32_t n, const float *model,
-                            float thr, int32_t *idx, int32_t *count, float *sum) {
-    if (estimator == USAC_ESSENTIAL)
-        hipLaunchKernelGGL(k_inliers_f<USAC_ESSENTIAL>, dim3(1), dim3(256), 0, st, pts, n, model, thr, idx, count, sum);
-    else
-        hipLaunchKernelGGL(k_inliers_f<USAC_FUNDAMENTAL>, dim3(1), dim3(256), 0, st, pts, n, model, thr, idx, count,
-                           sum);
     return hipGetLastError();
 }
 

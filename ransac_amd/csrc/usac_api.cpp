@@ -63,6 +63,7 @@ struct usac_ctx {
     DevBuf samples, models, counts, sums, best, hostmodels, argmax_part;
     DevBuf list, list_n;    // fundamental: occupied model slots (compacted) and their number
     DevBuf pool_idx, pool_pts, masks;  // SPRT parity path: pool order, permuted points, flag words
+    DevBuf lo_idx;                     // LO-RANSAC: host-drawn index lists for the device LSQ
     // throughput SPRT (usac_set_sprt): batch-fixed test on the pool-ordered points
     bool sprt_on = false;
     float sprt_log_up = 0.f, sprt_log_down = 0.f, sprt_log_A = 0.f;
@@ -70,7 +71,7 @@ struct usac_ctx {
     DevBuf sprt_pts, sprt_tested, sprt_surv, sprt_surv_n;
     uint32_t spk = 1;       // model slots per hypothesis (3 for the 7-point solver)
     // single-model / polish buffers
-    DevBuf one_model, inl_idx, inl_cnt, inl_sum, q, partial, ws, nm_model, nm_ok;
+    DevBuf one_model, inl_idx, inl_cnt, inl_sum, inl_scratch, q, partial, ws, nm_model, nm_ok;
     // comm
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -199,14 +200,10 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
 
 // exact single-model inliers into c->inl_idx / inl_cnt / inl_sum (device)
 hipError_t enqueue_inliers(usac_ctx *c, const float *model_dev, float thr) {
-    if (listed(c))
-        return usac::launch_inliers_f(c->stream, c->estimator, c->pts.as<float4>(), c->n, model_dev, thr,
-                                      c->inl_idx.as<int32_t>(), c->inl_cnt.as<int32_t>(), c->inl_sum.as<float>());
-    if (is_h(c))
-        return usac::launch_inliers_h(c->stream, c->pts.as<float4>(), c->n, model_dev, thr, c->inl_idx.as<int32_t>(),
-                                      c->inl_cnt.as<int32_t>(), c->inl_sum.as<float>());
-    return usac::launch_inliers_line(c->stream, c->pts.as<float2>(), c->n, model_dev, thr, c->inl_idx.as<int32_t>(),
-                                     c->inl_cnt.as<int32_t>(), c->inl_sum.as<float>());
+    hipError_t e = c->inl_scratch.reserve(usac::inliers_scratch_bytes(c->n));
+    if (e != hipSuccess) return e;
+    return usac::launch_inliers(c->stream, c->estimator, c->pts.p, c->n, model_dev, thr, c->inl_idx.as<int32_t>(),
+                                c->inl_cnt.as<int32_t>(), c->inl_sum.as<float>(), c->inl_scratch.p);
 }
 
 hipError_t enqueue_nonminimal(usac_ctx *c, const int32_t *idx_dev, uint32_t n) {
@@ -221,6 +218,125 @@ hipError_t enqueue_nonminimal(usac_ctx *c, const int32_t *idx_dev, uint32_t n) {
     return usac::launch_nonminimal_line(c->stream, c->pts.as<float2>(), idx_dev, n, c->q.as<float2>(),
                                         c->nm_model.as<float>(), c->nm_ok.as<int32_t>());
 }
+
+// LO-RANSAC: InnerLocalOptimization::GetModelScore (inner_local_optimization.hpp:74-133) with
+// IterativeLocalOptimization (iterative_local_optimization.hpp:61-136).  The control flow runs
+// here; every least-squares fit (EstimateModelNonMinimalSample) and every scored inlier list
+// (Quality::getNumberInliers(..., get_inliers = true)) runs on the device.  lo_model's
+// threshold persists across calls and compounds like the reference's; the LO
+// mt19937 is seeded with seed + 1 (the reference: std::random_device).
+struct LoRansac {
+    usac_ctx *c;
+    usac::Mt19937 g;
+    bool limited;
+    uint32_t inner, iters, limit, mult, m, n;
+    float theta, lo_thr, step;
+    std::vector<int32_t> max_inl, lo_inl, lo_sample;
+    uint32_t inner_count = 0, iterative_count = 0;
+    float lo_model[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    int rc = USAC_OK;
+
+    LoRansac(usac_ctx *ctx, const usac_params *p)
+        : c(ctx),
+          g(p->seed + 1u),
+          limited(p->lo == USAC_LO_INITFLORSC),
+          inner(p->lo_inner_iterations),
+          iters(p->lo_iterative_iterations),
+          limit(p->lo_sample_size),
+          mult(p->lo_threshold_multiplier),
+          m(ctx->m),
+          n(ctx->n),
+          theta(p->threshold),
+          lo_thr(p->threshold),
+          step((p->threshold * p->lo_threshold_multiplier - p->threshold) / p->lo_iterative_iterations),
+          max_inl(ctx->n),
+          lo_inl(ctx->n),
+          lo_sample(p->lo_sample_size ? p->lo_sample_size : 1) {}
+
+    bool lsq(const int32_t *idx, uint32_t k, float *model) {
+        if (rc) return false;
+        int32_t ok = 0;
+        hipError_t e = hipMemcpyAsync(c->lo_idx.p, idx, sizeof(int32_t) * k, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess) e = enqueue_nonminimal(c, c->lo_idx.as<int32_t>(), k);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(model, c->nm_model.p, sizeof(float) * 9, hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(&ok, c->nm_ok.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) rc = fail(c, USAC_ERR_HIP, std::string("LO least squares: ") + hipGetErrorString(e));
+        return rc == USAC_OK && ok;
+    }
+    void quality(const float *model, float thr, int &cnt, float &sum, int32_t *inl) {
+        if (rc) return;
+        hipError_t e = hipMemcpyAsync(c->one_model.p, model, sizeof(float) * 9, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess) e = enqueue_inliers(c, c->one_model.as<float>(), thr);
+        if (e == hipSuccess) e = hipMemcpyAsync(&cnt, c->inl_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(&sum, c->inl_sum.p, sizeof(float), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e == hipSuccess && cnt > 0)
+            e = hipMemcpy(inl, c->inl_idx.p, sizeof(int32_t) * (size_t)cnt, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = fail(c, USAC_ERR_HIP, std::string("LO scoring: ") + hipGetErrorString(e));
+    }
+    static bool bigger(int c1, float s1, int c2, float s2) { return c1 > c2 || (c1 == c2 && s1 > s2); }
+
+    // IterativeLocalOptimization::GetScoreUnlimited / GetScoreLimited; returns fail
+    bool iterative(int &lo_cnt, float &lo_sum, int best_cnt, float best_sum) {
+        for (uint32_t it = 0; it < iters && !rc; it++) {
+            lo_thr -= step;
+            if (lo_cnt <= (int)m) break;
+            if (limited) {
+                if (lo_cnt > (int)limit) {
+                    usac::unique_set(g, lo_sample.data(), limit, (uint32_t)(lo_cnt - 1));
+                    for (uint32_t k = 0; k < limit; k++) lo_sample[k] = lo_inl[lo_sample[k]];
+                    if (!lsq(lo_sample.data(), limit, lo_model)) continue;
+                } else {
+                    if (!lsq(lo_inl.data(), (uint32_t)lo_cnt, lo_model)) break;
+                }
+                quality(lo_model, lo_thr, lo_cnt, lo_sum, lo_inl.data());
+            } else {
+                if (!lsq(lo_inl.data(), (uint32_t)lo_cnt, lo_model)) break;
+                quality(lo_model, lo_thr, lo_cnt, lo_sum, lo_inl.data());
+                if (bigger(best_cnt, best_sum, lo_cnt, lo_sum)) break;
+            }
+            iterative_count++;
+        }
+        bool failed = false;
+        if (fabsf(lo_thr - theta) > 0.00001) {
+            failed = true;
+            lo_thr = theta;
+        }
+        return failed;
+    }
+
+    // GetModelScore(best_model, best_score): model / (cnt, sum) improved in place
+    void run(float *model, int &cnt, float &sum) {
+        if (cnt < 12) return;
+        int c0 = 0;
+        float s0 = 0.f;
+        quality(model, theta, c0, s0, max_inl.data());
+        for (uint32_t it = 0; it < inner && !rc; it++) {
+            if (cnt > (int)limit) {
+                usac::unique_set(g, lo_sample.data(), limit, (uint32_t)(cnt - 1));
+                for (uint32_t k = 0; k < limit; k++) lo_sample[k] = max_inl[lo_sample[k]];
+                if (!lsq(lo_sample.data(), limit, lo_model)) continue;
+            } else {
+                if (!lsq(max_inl.data(), (uint32_t)cnt, lo_model)) return;
+            }
+            lo_thr = mult * lo_thr;
+            int lo_cnt = 0;
+            float lo_sum = 0.f;
+            quality(lo_model, lo_thr, lo_cnt, lo_sum, lo_inl.data());
+            if (lo_cnt <= (int)m) continue;
+            const bool failed = iterative(lo_cnt, lo_sum, cnt, sum);
+            if (!failed && bigger(lo_cnt, lo_sum, cnt, sum)) {
+                memcpy(model, lo_model, sizeof(lo_model));
+                cnt = lo_cnt;
+                sum = lo_sum;
+                std::copy(lo_inl.begin(), lo_inl.begin() + lo_cnt, max_inl.begin());
+            }
+            inner_count++;
+        }
+    }
+};
 
 bool rec_better(const usac_record &a, const usac_record &b) {
     if (!a.valid) return false;
@@ -294,7 +410,7 @@ void usac_destroy(usac_ctx *c) {
     if (c->comm) ncclCommDestroy(c->comm);
     for (DevBuf *b : {&c->pts, &c->rec, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
-                      &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->one_model,
+                      &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->inl_scratch, &c->lo_idx, &c->one_model,
                       &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok,
                       &c->rec_send, &c->rec_all})
         b->release();
@@ -579,8 +695,16 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
     if (!c || !prm || !out) return USAC_ERR_ARG;
     memset(out, 0, sizeof(*out));
     const bool prosac = prm->sampler == USAC_SAMPLER_PROSAC;
-    if (!prosac && prm->sampler != USAC_SAMPLER_UNIFORM && prm->sampler != 0)
-        return fail(c, USAC_ERR_UNSUPPORTED, "sampler not supported (Uniform, Prosac)");
+    const bool napsac = prm->sampler == USAC_SAMPLER_NAPSAC;
+    if (!prosac && !napsac && prm->sampler != USAC_SAMPLER_UNIFORM && prm->sampler != 0)
+        return fail(c, USAC_ERR_UNSUPPORTED, "sampler not supported (Uniform, Napsac, Prosac)");
+    if (napsac && c->cols != 4)
+        return fail(c, USAC_ERR_ARG, "NAPSAC grid neighbours need 4-column points (SURVEY Q17)");
+    if (napsac && prm->cell_size <= 0) return fail(c, USAC_ERR_ARG, "NAPSAC cell_size must be > 0");
+    const bool use_lo = prm->lo == USAC_LO_INITLORSC || prm->lo == USAC_LO_INITFLORSC;
+    if (prm->lo != USAC_LO_NONE && !use_lo) return fail(c, USAC_ERR_UNSUPPORTED, "LO: InItLORsc / InItFLORsc only");
+    if (use_lo && (prm->lo_sample_size == 0 || prm->lo_iterative_iterations == 0))
+        return fail(c, USAC_ERR_ARG, "LO parameters must be > 0");
     if (prosac && c->n <= 20) return fail(c, USAC_ERR_ARG, "PROSAC needs > 20 points (prosac_termination_criteria.hpp:158-163)");
     if (prosac && prm->max_iterations > usac::ProsacSampler::kGrowthMax)
         return fail(c, USAC_ERR_ARG, "PROSAC max_iterations > 200000 (reference draws outside the point range)");
@@ -613,11 +737,23 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
     std::unique_ptr<usac::UniformSampler> uni;
     std::unique_ptr<usac::ProsacSampler> pro;
     std::unique_ptr<usac::ProsacTerminationCriteria> pterm;
+    std::unique_ptr<usac::GridNeighbors> grid;
+    std::unique_ptr<usac::NapsacSampler> nap;
     if (prosac) {
         pro.reset(new usac::ProsacSampler(prm->seed, n, m));
         pterm.reset(new usac::ProsacTerminationCriteria(pro->growth(), prm->desired_prob, m, n, prm->max_iterations));
+    } else if (napsac) {
+        std::vector<float> hp((size_t)n * 4);
+        HIP_TRY(c, hipMemcpy(hp.data(), c->pts.p, sizeof(float) * hp.size(), hipMemcpyDeviceToHost));
+        grid.reset(new usac::GridNeighbors(hp.data(), n, prm->cell_size));
+        nap.reset(new usac::NapsacSampler(grng, *grid, n, m));
     } else {
         uni.reset(new usac::UniformSampler(grng, n, m));
+    }
+    std::unique_ptr<LoRansac> lo;
+    if (use_lo) {
+        HIP_TRY(c, c->lo_idx.reserve(sizeof(int32_t) * (size_t)n));
+        lo.reset(new LoRansac(c, prm));
     }
     usac::StandardTerminationCriteria term(prm->desired_prob, m, n, prm->max_iterations);
     std::unique_ptr<usac::Sprt> sprt;
@@ -634,10 +770,11 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
     }
 
     const size_t SB = (size_t)batch * spk;  // slot stride of the host copies
-    std::vector<int32_t> hs((size_t)batch * m), hc(SB), slot_row(SB);
+    std::vector<int32_t> hs((size_t)batch * m, 0), hc(SB), slot_row(SB);
     std::vector<float> hsum(SB), hmod((size_t)ncomp(c) * SB);
     std::vector<uint32_t> hlist(SB), hmask(sprt ? (size_t)nw * SB : 0);
     std::vector<uint32_t> subset_at(batch), largest_at(batch);
+    std::vector<int32_t> last_sample(m, 0);
     std::vector<uint8_t> flags(prosac ? n : 0);
     std::vector<int32_t> inl_list(prosac ? n : 0);
     usac::Score best;
@@ -669,6 +806,13 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
                 subset_at[j] = pro->subset();
                 pro->generateSample(smp, gen_term);
                 largest_at[j] = pro->largest();
+            } else if (napsac) {
+                // the reference reuses one sample array: a sample the sampler leaves
+                // (partly) unwritten keeps the previous sample's entries
+                if (j > 0) memcpy(smp, smp - m, sizeof(int32_t) * m);
+                else memcpy(smp, last_sample.data(), sizeof(int32_t) * m);
+                nap->generateSample(smp);
+                if (j + 1 == B) memcpy(last_sample.data(), smp, sizeof(int32_t) * m);
             } else {
                 uni->generateSample(smp);
             }
@@ -743,8 +887,14 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
                     cur.score = hsum[sl];
                 }
                 if (!cur.bigger(best)) continue;
+                float model[9];
+                for (int k = 0; k < 9; k++) model[k] = k < ncomp(c) ? hmod[(size_t)k * SB + sl] : 0.f;
+                if (lo) {  // ransac.cpp:110-112, before the best is replaced
+                    lo->run(model, cur.inlier_number, cur.score);
+                    if (lo->rc) return lo->rc;
+                }
                 best = cur;
-                for (int k = 0; k < 9; k++) best_model[k] = k < ncomp(c) ? hmod[(size_t)k * SB + sl] : 0.f;
+                memcpy(best_model, model, sizeof(best_model));
                 if (prosac) {
                     if ((rc = score_inliers(best_model))) return rc;
                     if (cnt > 0)
@@ -788,6 +938,8 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
     out->n_records = nrec;
     out->sprt_histories = sprt ? (int32_t)sprt->histories() : 0;
     out->prosac_term_len = prosac ? pterm->terminationLength() : n;
+    out->lo_inner_iters = lo ? lo->inner_count : 0;
+    out->lo_iterative_iters = lo ? lo->iterative_count : 0;
     memcpy(out->minimal_model, best_model, sizeof(best_model));
     out->minimal_inliers = best.inlier_number;
     if (best.inlier_number == 0) {

@@ -509,7 +509,11 @@ __device__ __forceinline__ void svd3(const double (&E)[9], double (&U)[3][3], do
 
 }  // namespace e5
 
-// EssentialEstimator::GetError (essential_estimator.hpp:76-107)
+// EssentialEstimator::GetError (essential_estimator.hpp:76-107).  The reference's
+// `float a2 = sqrt(float)` is C's double sqrt rounded to float; for a float argument that
+// equals the correctly rounded fp32 square root (53 >= 2*24 + 2 bits: no double rounding),
+// so the correctly rounded fp32 sqrtf is used -- bit-identical, a fraction of the cost.
+// (Not __fsqrt_rn: on gfx950 it lowers to the 1-ulp v_sqrt_f32.)
 __device__ __forceinline__ float essential_error(const float *E, float x1, float y1, float x2, float y2) {
     const float l1 = E[0] * x2 + E[3] * y2 + E[6];
     const float l2 = E[1] * x2 + E[4] * y2 + E[7];
@@ -518,9 +522,9 @@ __device__ __forceinline__ float essential_error(const float *E, float x1, float
     const float t2 = E[3] * x1 + E[4] * y1 + E[5];
     const float t3 = E[6] * x1 + E[7] * y1 + E[8];
     const float a1 = l1 * x1 + l2 * y1 + l3;
-    const float a2 = (float)sqrt((double)(l1 * l1 + l2 * l2));
+    const float a2 = sqrtf(l1 * l1 + l2 * l2);
     const float b1 = t1 * x2 + t2 * y2 + t3;
-    const float b2 = (float)sqrt((double)(t1 * t1 + t2 * t2));
+    const float b2 = sqrtf(t1 * t1 + t2 * t2);
     return (fabsf(a1 / a2) + fabsf(b1 / b2)) / 2;
 }
 

@@ -11,6 +11,8 @@
 //   usac::ProsacSampler              prosac_sampler.hpp:62-172
 //   usac::ProsacTerminationCriteria  prosac_termination_criteria.hpp:44-201
 //   usac::Sprt                       sprt.hpp:89-491 (decisions on device inlier masks)
+//   usac::GridNeighbors              nearest_neighbors.cpp:160-202
+//   usac::NapsacSampler              napsac_sampler.hpp:40-158 (grid), array_random_generator.hpp
 #pragma once
 #include <stdint.h>
 #include <stdlib.h>
@@ -440,6 +442,104 @@ class Sprt {
     uint32_t n_, m_, max_iters_, idx_ = 0, cur_ = 0;
     int max_before_, last_update_ = 0;
     double t_M_ = 0, m_S_ = 0;
+};
+
+// ---------------------------------------------------------------- NAPSAC (grid)
+// Grid neighbours: cell = ((int)(x1/cs), (int)(y1/cs), (int)(x2/cs), (int)(y2/cs)) with fp32
+// division and truncation; a point's neighbours are the other points of its cell in
+// ascending index order (what the reference's pair loop over each cell produces).  CSR.
+class GridNeighbors {
+   public:
+    GridNeighbors(const float *pts, uint32_t n, int cell_size) : off_(n + 1, 0) {
+        struct Key {
+            int c[4];
+            uint32_t i;
+        };
+        std::vector<Key> keys(n);
+        for (uint32_t i = 0; i < n; i++) {
+            for (int k = 0; k < 4; k++) keys[i].c[k] = (int)(pts[4 * (size_t)i + k] / (float)cell_size);
+            keys[i].i = i;
+        }
+        std::sort(keys.begin(), keys.end(), [](const Key &a, const Key &b) {
+            for (int k = 0; k < 4; k++)
+                if (a.c[k] != b.c[k]) return a.c[k] < b.c[k];
+            return a.i < b.i;
+        });
+        std::vector<std::pair<uint32_t, uint32_t>> cell(n);  // (first, end) sorted position range
+        for (uint32_t a = 0; a < n;) {
+            uint32_t b = a + 1;
+            while (b < n && std::equal(keys[a].c, keys[a].c + 4, keys[b].c)) b++;
+            for (uint32_t k = a; k < b; k++) off_[keys[k].i + 1] = b - a - 1;
+            for (uint32_t k = a; k < b; k++) cell[k] = {a, b};
+            a = b;
+        }
+        for (uint32_t i = 0; i < n; i++) off_[i + 1] += off_[i];
+        nb_.resize(off_[n]);
+        for (uint32_t u = 0; u < n; u++) {
+            uint32_t w = off_[keys[u].i];
+            for (uint32_t v = cell[u].first; v < cell[u].second; v++)
+                if (v != u) nb_[w++] = (int32_t)keys[v].i;
+        }
+    }
+    uint32_t count(uint32_t i) const { return off_[i + 1] - off_[i]; }
+    const int32_t *list(uint32_t i) const { return nb_.data() + off_[i]; }
+
+   private:
+    std::vector<uint32_t> off_;
+    std::vector<int32_t> nb_;
+};
+
+// NapsacSampler (grid): ArrayRandomGenerator pool over [0, n) on the shared glibc stream
+// (its member `max` starts at 0); an initial point needs >= m neighbours (Q18);
+// after n failed draws the sampler turns uniform and, as the reference, then rewrites only
+// sample[0] (generateUniqueRandomSet with subset size 1).
+class NapsacSampler {
+   public:
+    NapsacSampler(GlibcRandom &rng, const GridNeighbors &g, uint32_t n, uint32_t m)
+        : rng_(rng), g_(g), array_(n), next_(n, 0), n_(n), m_(m) {
+        for (uint32_t i = 0; i < n; i++) array_[i] = (int32_t)i;
+    }
+    void generateSample(int32_t *sample) {
+        if (uniform_) {
+            sample[0] = draw();
+            return;
+        }
+        uint32_t i;
+        int32_t init = 0;
+        for (i = 0; i < n_; i++) {
+            init = draw();
+            if (g_.count((uint32_t)init) < m_) continue;
+            break;
+        }
+        if (i == n_) {
+            uniform_ = true;
+            return;
+        }
+        sample[0] = init;
+        const int32_t *nb = g_.list((uint32_t)init);
+        const uint32_t sz = g_.count((uint32_t)init);
+        for (uint32_t k = 1; k < m_; k++) {
+            sample[k] = nb[next_[init]];
+            if (++next_[init] >= sz) next_[init] = 0;
+        }
+    }
+
+   private:
+    int32_t draw() {
+        if (max_ == 0) max_ = n_;
+        const uint32_t k = rng_.next() % max_;
+        const int32_t v = array_[k];
+        max_--;
+        array_[k] = array_[max_];
+        array_[max_] = v;
+        return v;
+    }
+    GlibcRandom &rng_;
+    const GridNeighbors &g_;
+    std::vector<int32_t> array_;
+    std::vector<uint32_t> next_;
+    uint32_t n_, m_, max_ = 0;
+    bool uniform_ = false;
 };
 
 }  // namespace usac

@@ -43,8 +43,6 @@ hipError_t launch_prepare_f(hipStream_t st, const float *in, uint32_t K, float *
 hipError_t launch_score_f(hipStream_t st, int estimator, int chunks, const float4 *pts, uint32_t n,
                           const float *models, size_t stride, const uint32_t *list, const uint32_t *list_n,
                           uint32_t kmax, float thr, int32_t *counts, float *sums);
-hipError_t launch_inliers_f(hipStream_t st, int estimator, const float4 *pts, uint32_t n, const float *model,
-                            float thr, int32_t *idx, int32_t *count, float *sum);
 // essential 5-point: one slot per sample (models [9][B], counts 0 / -1, list / list_n)
 hipError_t launch_solve_e5(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
                            int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, float *models,
@@ -69,10 +67,12 @@ hipError_t launch_score_sprt(hipStream_t st, int estimator, const void *pool_pts
                              uint32_t *tested_total, void *surv, uint32_t *surv_n);
 size_t sprt_survivor_bytes();
 
-hipError_t launch_inliers_h(hipStream_t st, const float4 *pts, uint32_t n, const float *model, float thr,
-                            int32_t *idx, int32_t *count, float *sum);
-hipError_t launch_inliers_line(hipStream_t st, const float2 *pts, uint32_t n, const float *model, float thr,
-                               int32_t *idx, int32_t *count, float *sum);
+// exact inliers of one model (kernels_inliers.hip): ascending idx, count, sequential Σ;
+// scratch = inliers_scratch_bytes(n)
+hipError_t launch_inliers(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *model, float thr,
+                          int32_t *idx, int32_t *count, float *sum, void *scratch);
+size_t inliers_scratch_bytes(uint32_t n);
+
 
 hipError_t launch_nonminimal_h(hipStream_t st, const float4 *pts, const int32_t *idx, uint32_t n, float4 *q,
                                double *partial, float *ws, float *model_out, int32_t *ok);

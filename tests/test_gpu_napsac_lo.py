@@ -1,0 +1,62 @@
+"""GPU parity of the loop with NAPSAC (grid) and LO-RANSAC (inner + iterative, unlimited and
+limited) against the oracle: iterations, best-score updates, LO counters, models and inlier
+lists identical."""
+import numpy as np
+import pytest
+
+from ransac_amd import synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.int32)
+
+
+CASES = [("H", "napsac", 0, False), ("H", "napsac", 1, False), ("H", "napsac", 2, True), ("H", "uniform", 1, True),
+         ("F", "uniform", 1, False), ("L", "uniform", 1, False), ("E", "uniform", 2, False),
+         ("H", "prosac", 1, False)]
+
+
+@pytest.mark.parametrize("kind,sampler,lo,sprt", CASES)
+def test_loop_napsac_lo_identical(usac, oracle, kind, sampler, lo, sprt):
+    if kind == "H":
+        pts, _, inl = synthetic.homography_points(n=4000, inlier_ratio=0.2, seed=7, cluster=(500, 500, 150))
+        if sampler == "prosac":
+            q = np.random.default_rng(7).uniform(0, 1, len(pts)) + 0.5 * inl
+            pts = np.ascontiguousarray(pts[np.argsort(-q, kind="stable")])
+        thr, okind, est, m = 2.0, oracle.HOMOGRAPHY, usac.ESTIMATOR.Homography, 4
+    elif kind == "F":
+        pts, _, _ = synthetic.fundamental_points(n=3000, inlier_ratio=0.4, seed=7, prosac_order=False)
+        thr, okind, est, m = 2.0, oracle.FUNDAMENTAL, usac.ESTIMATOR.Fundamental, 7
+    elif kind == "E":
+        pts, _, _ = synthetic.fundamental_points(n=2000, inlier_ratio=0.5, seed=7, normalized=True,
+                                                 prosac_order=False)
+        thr, okind, est, m = 0.002, oracle.ESSENTIAL, usac.ESTIMATOR.Essential, 5
+    else:
+        pts, _ = synthetic.line_points(n=1000, inlier_ratio=0.3, seed=7)
+        thr, okind, est, m = 8.0, oracle.LINE2D, usac.ESTIMATOR.Line2d, 2
+    osmp = {"uniform": oracle.SAMPLER_UNIFORM, "napsac": oracle.SAMPLER_NAPSAC,
+            "prosac": oracle.SAMPLER_PROSAC}[sampler]
+    ref = oracle.ransac_run(okind, pts, thr, 0.95, 5, sampler=osmp, sprt=sprt, lo=lo, max_iters=4000)
+    smp = {"uniform": usac.SAMPLER.Uniform, "napsac": usac.SAMPLER.Napsac, "prosac": usac.SAMPLER.Prosac}[sampler]
+    mdl = usac.Model(thr, m, 0.95, 7, est, smp)
+    mdl.ResetRandomGenerator(False)
+    mdl.setSeed(5)
+    mdl.setSprt(sprt)
+    mdl.lo = usac.LocOpt(lo)
+    mdl.max_iterations = 4000
+    mdl.batch = 512
+    if sampler == "napsac":
+        mdl.setNeighborsType(usac.NeighborsSearch.Grid)
+    r = usac.Ransac(mdl, pts)
+    r.run()
+    out = r.getRansacOutput()
+    assert out.getNumberOfMainIterations() == ref["iters"]
+    assert [(i, c) for i, c, _ in r.records] == [(i, c) for i, c, _ in ref["records"]]
+    assert [np.float32(s) for _, _, s in r.records] == [np.float32(s) for _, _, s in ref["records"]]
+    assert out.getLOIters() == ref["lo_inner_iters"]
+    assert out.raw["lo_iterative_iters"] == ref["lo_iterative_iters"]
+    assert (_bits(out.raw["minimal_model"]) == _bits(ref["minimal_model"])).all()
+    assert (_bits(out.getModel()) == _bits(ref["model"])).all()
+    assert (out.getInliers() == ref["inlier_idx"]).all()
