@@ -44,6 +44,9 @@ def parse():
                     help="batch SPRT verification (reference initial epsilon/delta for the estimator)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--pipeline", type=int, default=3,
+                    help="batches in flight: one context (stream + buffers) per in-flight batch, so batch i+1's "
+                         "solve overlaps batch i's scoring")
     return ap.parse_args()
 
 
@@ -154,16 +157,20 @@ def main():
         pts, _, _ = synthetic.homography_points(n=args.points, inlier_ratio=0.3, seed=args.seed)
     dlt_mode = 0 if args.dlt == "thin" else 1
     est_id = usac.ESTIMATOR.Fundamental if fund else usac.ESTIMATOR.Essential if ess else usac.ESTIMATOR.Homography
-    ctx = usac.Context(est_id, pts, device=local_rank)
-    ctx.set_dlt_mode(dlt_mode)
-    ctx.set_score_chunks(args.chunks)
+    P = max(1, args.pipeline)
+    ctxs = [usac.Context(est_id, pts, device=local_rank) for _ in range(P)]
+    for c in ctxs:
+        c.set_dlt_mode(dlt_mode)
+        c.set_score_chunks(args.chunks)
+    ctx = ctxs[0]
     if world > 1:
         uid = [usac.Context.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(world, rank, uid[0])
     B = args.batch
     if args.sprt:
-        ctx.set_sprt(True, seed=args.seed)
+        for c in ctxs:
+            c.set_sprt(True, seed=args.seed)
     models_per_hyp = 1.0
     if fund or ess:  # occupied model slots per sample of the device sampler's stream (one batch)
         ctx.set_sprt(False)
@@ -173,39 +180,64 @@ def main():
             ctx.set_sprt(True, seed=args.seed)
 
     def sync():
-        ctx.sync()
+        for c in ctxs:
+            c.sync()
         if torch.cuda.is_available():
             torch.cuda.synchronize(local_rank)
 
-    def step(i):
+    def launch(i):
         first = (i * world + rank) * B
-        ctx.hypothesize_async(B, args.seed, first, args.threshold)
-        best = ctx.fetch_best()
+        ctxs[i % P].hypothesize_async(B, args.seed, first, args.threshold)
+
+    def finish(i):
+        c = ctxs[i % P]
+        best = c.fetch_best()
+        t = c.last_timings()
         if world > 1:
             best = usac.merge_records(ctx.allgather_record(best))
-        return best
+        return best, t
 
-    for i in range(args.warmup):
-        step(i)
+    def run(first_step, count, sink):
+        # keep P batches in flight: batch i is launched before batch i - P + 1 is fetched
+        for j in range(count):
+            launch(first_step + j)
+            if j >= P - 1:
+                sink(*finish(first_step + j - P + 1))
+        for j in range(max(0, count - P + 1), count):
+            sink(*finish(first_step + j))
+
+    run(0, args.warmup, lambda rec, t: None)
     if world > 1:
         dist.barrier()
     sync()
     score_ms, solve_ms, batch_ms = [], [], []
-    t0 = time.perf_counter()
-    best = None
-    for i in range(args.steps):
-        rec = step(args.warmup + i)
-        t = ctx.last_timings()
+    best_box = [None]
+
+    def keep(rec, t):
         score_ms.append(t["score_ms"])
         solve_ms.append(t["solve_ms"])
         batch_ms.append(t["batch_ms"])
-        if best is None or usac.merge_records([rec, best]).hyp_index == rec.hyp_index:
-            best = rec
+        b = best_box[0]
+        if b is None or usac.merge_records([rec, b]).hyp_index == rec.hyp_index:
+            best_box[0] = rec
+
+    t0 = time.perf_counter()
+    run(args.warmup, args.steps, keep)
+    best = best_box[0]
     sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    tested_per_batch = ctx.sprt_tested() if args.sprt else None
+    tested_per_batch = ctxs[(args.warmup + args.steps - 1) % P].sprt_tested() if args.sprt else None
+    # roofline pass: the same batches one at a time (no overlap), so the per-kernel durations
+    # are the kernels' own (what rocprofv3 reports for `bench.py --pipeline 1`)
+    solo_score, solo_solve = [], []
+    for i in range(max(5, min(args.steps, 20))):
+        ctx.hypothesize_async(B, args.seed, ((args.warmup + args.steps + i) * world + rank) * B, args.threshold)
+        ctx.fetch_best()
+        t = ctx.last_timings()
+        solo_score.append(t["score_ms"])
+        solo_solve.append(t["solve_ms"])
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -221,7 +253,7 @@ def main():
             bytes_per_hyp = 16.0 * tested_per_batch / B + m * 4 + models_per_hyp * (36 + 8)
         else:
             bytes_per_hyp = models_per_hyp * 16 * n + m * 4 + models_per_hyp * (36 + 8)
-        avg_score_ms = float(np.mean(score_ms))
+        avg_score_ms = float(np.mean(solo_score))
         achieved = bytes_per_hyp * B / (avg_score_ms * 1e-3) / 1e9
         kname = ("void usac::k_score_f<%d>" if (fund or ess) else "void usac::k_score_hf<%d, false>") % args.chunks
         traffic = measured_traffic(kname, n, B) if not (fund or ess or args.sprt) else None
@@ -255,7 +287,8 @@ def main():
                                     "xorshift), %d correspondences, %d-hypothesis batch per GPU" %
                                     (" + batch SPRT" if args.sprt else "", args.dlt, n, B)),
                        "n_points": n, "batch_per_gpu": B, "threshold": args.threshold,
-                       "score_chunks": args.chunks, "parallelism": "hypothesis-sharded x%d" % world},
+                       "score_chunks": args.chunks, "batches_in_flight": P,
+                       "parallelism": "hypothesis-sharded x%d" % world},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
                          "traffic_unit": "bytes/launch", "traffic_source": traffic[1] if traffic else None,
@@ -268,7 +301,10 @@ def main():
                                  "reference scan reads) / measured kernel time; the point set is L2-resident, so "
                                  "true HBM traffic (`traffic`) is ~0.1%% of it and the kernel is VALU-issue bound "
                                  "(DESIGN.md 'Roofline')",
-                         "solve_kernel_ms": float(np.mean(solve_ms)), "batch_device_ms": float(np.mean(batch_ms))},
+                         "solve_kernel_ms": float(np.mean(solo_solve)),
+                         "kernel_ms_in_pipeline": float(np.mean(score_ms)),
+                         "solve_kernel_ms_in_pipeline": float(np.mean(solve_ms)),
+                         "batch_device_ms_in_pipeline": float(np.mean(batch_ms))},
             "best": {"inliers": int(best.inliers), "hyp_index": int(best.hyp_index)},
         }
         if world == 1:
@@ -277,7 +313,8 @@ def main():
                 out["cpu_baseline"] = cpu_baseline(args.estimator, pts, args.threshold, dlt_mode, args.cpu_seconds)
                 out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
         print(json.dumps(out), flush=True)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -160,8 +160,9 @@ int usac_sync(usac_ctx *ctx);
 int usac_last_timings(usac_ctx *ctx, float *ms3);
 /* Score-kernel split factor (point chunks per hypothesis tile, 1 = exact sequential sums). */
 int usac_set_score_chunks(usac_ctx *ctx, int chunks);
-/* Homography score kernel: 0 = guard-band fast path (default), 1 = exact reference
- * expression for every pair (A/B and debugging; same results). */
+/* Homography score kernel: 0 = guard-band fast path with the hypothesis pre-sort (default),
+ * 1 = exact reference expression for every pair, 2 = fast path without the pre-sort (A/B and
+ * debugging; all three give the same results). */
 int usac_set_score_variant(usac_ctx *ctx, int variant);
 
 /* Throughput SPRT (sprt.hpp:191-317 as a batch test): with enable != 0 every later

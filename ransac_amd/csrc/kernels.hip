@@ -130,8 +130,10 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_h(const float4 *__restric
 }
 
 // ------------------------------------------------------------------------ score (H), fast path
-// Point records for the fast kernel, in groups of 4 points (128 B per group):
-//   float4 [0..3] = {x1, x2, y1, y2} of points 4g..4g+3,
+// Point records for the fast kernel, in groups of 4 points (128 B per group), one
+// coordinate of the four points per float4 so that consecutive points' values are adjacent
+// SGPRs (the packed stage-A FMAs take them as 64-bit scalar operands without s_mov):
+//   float4 [0..3] = x1[4], y1[4], x2[4], y2[4] of points 4g..4g+3,
 //   float4 [4]    = guard bands for the current threshold          band_i
 //   float4 [5]    = forward-rejection radii (T + band_i)(1 + 2^-18), T = 2 thr
 //   float4 [6..7] = padding.
@@ -144,30 +146,37 @@ __global__ __launch_bounds__(256) void k_prepare_rec(const float4 *__restrict__ 
     const uint32_t ngroups = (n + 3) / 4;
     if (i >= 4 * ngroups) return;
     const uint32_t g = i >> 2, j = i & 3;
-    float4 out;
+    float4 p;
     float band, tr;
     if (i < n) {
-        const float4 p = pts[i];
+        p = pts[i];
         const float mp = fabsf(p.x) + fabsf(p.y) + fabsf(p.z) + fabsf(p.w);
-        out = make_float4(p.x, p.z, p.y, p.w);
         band = kBandMp * mp + kBandT * T;
         tr = (T + band) * 1.000003814697265625f;  // (1 + 2^-18)
     } else {
-        out = make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
+        p = make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
         band = 0.f;
         tr = __builtin_nanf("");
     }
-    rec[8 * g + j] = out;
+    float *r = reinterpret_cast<float *>(rec + 8 * g);
+    r[0 + j] = p.x;
+    r[4 + j] = p.y;
+    r[8 + j] = p.z;
+    r[12 + j] = p.w;
     reinterpret_cast<float *>(rec + 8 * g + 4)[j] = band;
     reinterpret_cast<float *>(rec + 8 * g + 5)[j] = tr;
     if (j < 2) rec[8 * g + 6 + j] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 
 // Model registers of a lane: h[9] = H, hi[9] = H^-1; plus the lane's stage-A error
-// bounds dZ, E (below).
+// bounds dZ, E (below), and H / dZ / E duplicated into both halves of 2-wide vectors for the
+// packed stage A (two points per v_pk_fma_f32).
+typedef float v2f __attribute__((ext_vector_type(2)));
+
 struct HModel {
     float h[9], hi[9];
     float dZ, E;
+    v2f h2[9], dZ2, E2;
 };
 
 // Stage-A bounds of one hypothesis over the dataset box |x1| <= c.x, |y1| <= c.y,
@@ -183,6 +192,26 @@ __device__ __forceinline__ void stage_a_bounds(HModel &M, float4 c) {
     const float dx = s * kx, dy = s * ky, dz = s * kz;
     M.dZ = dz;
     M.E = ((c.z * dz + dx) + (c.w * dz + dy)) * 1.000003814697265625f;
+#pragma unroll
+    for (int k = 0; k < 9; k++) M.h2[k] = v2f{M.h[k], M.h[k]};
+    M.dZ2 = v2f{M.dZ, M.dZ};
+    M.E2 = v2f{M.E, M.E};
+}
+
+// Stage A for two points at once: the same FMA chain element-wise (v_pk_fma_f32), so each
+// half is bit-identical to stage_a_reject.
+__device__ __forceinline__ void stage_a_reject2(const HModel &M, v2f x1, v2f y1, v2f x2, v2f y2, v2f tr, bool &k0,
+                                                bool &k1) {
+    const v2f X = __builtin_elementwise_fma(M.h2[1], y1, __builtin_elementwise_fma(M.h2[0], x1, M.h2[2]));
+    const v2f Y = __builtin_elementwise_fma(M.h2[4], y1, __builtin_elementwise_fma(M.h2[3], x1, M.h2[5]));
+    const v2f Z = __builtin_elementwise_fma(M.h2[7], y1, __builtin_elementwise_fma(M.h2[6], x1, M.h2[8]));
+    const v2f ex = __builtin_elementwise_fma(x2, Z, -X);
+    const v2f ey = __builtin_elementwise_fma(y2, Z, -Y);
+    const v2f lhs = __builtin_elementwise_fma(ex, ex, ey * ey);
+    const v2f r = __builtin_elementwise_fma(tr, __builtin_elementwise_abs(Z) + M.dZ2, M.E2);
+    const v2f rr = r * r;
+    k0 = lhs.x > rr.x;
+    k1 = lhs.y > rr.y;
 }
 
 // Stage A -- forward-only rejection, 14 VALU ops, no rcp / sqrt.  X, Y, Z by FMA chains,
@@ -239,32 +268,40 @@ __device__ __forceinline__ void stage_b(const HModel &M, float x1, float y1, flo
     }
 }
 
-// Four points of a group: stage A for all four first (independent chains), then stage B
-// per point behind a branch that the wave skips unless one of its 64 hypotheses survived.
+// Four points of a group: stage A for all four first (independent chains); the wave takes
+// the stage-B path at all only if one of its 64 hypotheses kept one of the four points
+// (one scalar branch per group in the common case), then per point behind its own branch.
 template <bool EXACT_SUM>
-__device__ __forceinline__ void score_group(const HModel &M, float4 a0, float4 a1, float4 a2, float4 a3, float4 bd,
+__device__ __forceinline__ void score_group(const HModel &M, float4 X1, float4 Y1, float4 X2, float4 Y2, float4 bd,
                                             float4 tr, float T, float thr, int &cnt, float &sum) {
-    const bool k0 = stage_a_reject(M, a0.x, a0.z, a0.y, a0.w, tr.x);
-    const bool k1 = stage_a_reject(M, a1.x, a1.z, a1.y, a1.w, tr.y);
-    const bool k2 = stage_a_reject(M, a2.x, a2.z, a2.y, a2.w, tr.z);
-    const bool k3 = stage_a_reject(M, a3.x, a3.z, a3.y, a3.w, tr.w);
-    if (!k0) stage_b<EXACT_SUM>(M, a0.x, a0.z, a0.y, a0.w, bd.x, T, thr, cnt, sum);
-    if (!k1) stage_b<EXACT_SUM>(M, a1.x, a1.z, a1.y, a1.w, bd.y, T, thr, cnt, sum);
-    if (!k2) stage_b<EXACT_SUM>(M, a2.x, a2.z, a2.y, a2.w, bd.z, T, thr, cnt, sum);
-    if (!k3) stage_b<EXACT_SUM>(M, a3.x, a3.z, a3.y, a3.w, bd.w, T, thr, cnt, sum);
+    bool k0, k1, k2, k3;
+    stage_a_reject2(M, v2f{X1.x, X1.y}, v2f{Y1.x, Y1.y}, v2f{X2.x, X2.y}, v2f{Y2.x, Y2.y}, v2f{tr.x, tr.y}, k0, k1);
+    stage_a_reject2(M, v2f{X1.z, X1.w}, v2f{Y1.z, Y1.w}, v2f{X2.z, X2.w}, v2f{Y2.z, Y2.w}, v2f{tr.z, tr.w}, k2, k3);
+    if (__builtin_amdgcn_ballot_w64(!(k0 && k1 && k2 && k3)) == 0) return;
+    if (!k0) stage_b<EXACT_SUM>(M, X1.x, Y1.x, X2.x, Y2.x, bd.x, T, thr, cnt, sum);
+    if (!k1) stage_b<EXACT_SUM>(M, X1.y, Y1.y, X2.y, Y2.y, bd.y, T, thr, cnt, sum);
+    if (!k2) stage_b<EXACT_SUM>(M, X1.z, Y1.z, X2.z, Y2.z, bd.z, T, thr, cnt, sum);
+    if (!k3) stage_b<EXACT_SUM>(M, X1.w, Y1.w, X2.w, Y2.w, bd.w, T, thr, cnt, sum);
 }
 
-// Lanes = hypotheses (64 per wave), point groups wave-uniform (scalar loads, double-
-// buffered one group ahead).  CHUNKS waves of a workgroup split the groups of the same 64
+// Lanes = hypotheses (64 per wave), point groups wave-uniform (scalar loads, two groups per
+// iteration).  CHUNKS waves of a workgroup split the groups of the same 64
 // hypotheses and combine (count, Σ) in chunk order.  ext = dataset box (see above).
+//
+// perm (nullable): lane i of the grid scores hypothesis perm[i] (k_presort_h groups the
+// hypotheses that survive stage A often into the same waves, so the other waves rarely
+// take the stage-B branch); results land at the hypothesis' own index.
 template <int CHUNKS, bool EXACT_SUM>
 __global__ __launch_bounds__(64 * CHUNKS) void k_score_hf(const float4 *__restrict__ rec, uint32_t n, float4 ext,
                                                           const float *__restrict__ models, uint32_t B, float thr,
+                                                          const uint32_t *__restrict__ perm,
                                                           int32_t *__restrict__ counts, float *__restrict__ sums) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t h = blockIdx.x * 64 + lane;
-    const uint32_t hc = h < B ? h : B - 1;
+    const uint32_t i = blockIdx.x * 64 + lane;
+    const uint32_t ic = i < B ? i : B - 1;
+    const uint32_t h = perm ? perm[ic] : i;
+    const uint32_t hc = perm ? h : ic;
     HModel M;
 #pragma unroll
     for (int k = 0; k < 9; k++) {
@@ -279,29 +316,26 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_hf(const float4 *__restri
     const uint32_t gend = gbeg + per < ngroups ? gbeg + per : ngroups;
     int cnt = 0;
     float sum = 0.f;
-    if (gbeg < gend) {
-        const float4 *p = rec + 8 * (size_t)gbeg;
-        float4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], ab = p[4], at = p[5];
-        float4 b0, b1, b2, b3, bb, bt;
-        uint32_t g = gbeg;
-        for (;;) {
-            // buffer B <- group g+1 (clamped), evaluate buffer A = group g
-            p = rec + 8 * (size_t)(g + 1 < gend ? g + 1 : g);
-            b0 = p[0]; b1 = p[1]; b2 = p[2]; b3 = p[3]; bb = p[4]; bt = p[5];
-            score_group<EXACT_SUM>(M, a0, a1, a2, a3, ab, at, T, thr, cnt, sum);
-            if (++g >= gend) break;
-            // buffer A <- group g+1 (clamped), evaluate buffer B = group g
-            p = rec + 8 * (size_t)(g + 1 < gend ? g + 1 : g);
-            a0 = p[0]; a1 = p[1]; a2 = p[2]; a3 = p[3]; ab = p[4]; at = p[5];
-            score_group<EXACT_SUM>(M, b0, b1, b2, b3, bb, bt, T, thr, cnt, sum);
-            if (++g >= gend) break;
-        }
+    // the two groups of an iteration load into fixed SGPR tuples, so the packed stage A reads
+    // its point pairs straight from the loaded registers (no copies); 8 waves per SIMD hide
+    // the scalar-load latency
+    uint32_t g = gbeg;
+    for (; g + 2 <= gend; g += 2) {
+        const float4 *p = rec + 8 * (size_t)g;
+        const float4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], ab = p[4], at = p[5];
+        const float4 b0 = p[8], b1 = p[9], b2 = p[10], b3 = p[11], bb = p[12], bt = p[13];
+        score_group<EXACT_SUM>(M, a0, a1, a2, a3, ab, at, T, thr, cnt, sum);
+        score_group<EXACT_SUM>(M, b0, b1, b2, b3, bb, bt, T, thr, cnt, sum);
+    }
+    if (g < gend) {
+        const float4 *p = rec + 8 * (size_t)g;
+        score_group<EXACT_SUM>(M, p[0], p[1], p[2], p[3], p[4], p[5], T, thr, cnt, sum);
     }
     if (!EXACT_SUM) sum *= 0.5f;
     if constexpr (CHUNKS == 1) {
-        if (h < B) {
-            counts[h] = cnt;
-            sums[h] = sum;
+        if (i < B) {
+            counts[hc] = cnt;
+            sums[hc] = sum;
         }
     } else {
         __shared__ int s_cnt[CHUNKS][64];
@@ -309,7 +343,7 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_hf(const float4 *__restri
         s_cnt[wave][lane] = cnt;
         s_sum[wave][lane] = sum;
         __syncthreads();
-        if (wave == 0 && h < B) {
+        if (wave == 0 && i < B) {
             int c = s_cnt[0][lane];
             float s = s_sum[0][lane];
 #pragma unroll
@@ -317,10 +351,57 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_hf(const float4 *__restri
                 c += s_cnt[w][lane];
                 s += s_sum[w][lane];
             }
-            counts[h] = c;
-            sums[h] = s;
+            counts[hc] = c;
+            sums[hc] = s;
         }
     }
+}
+
+// Hypothesis pre-sort for the fast score kernel: forward-distance hits of every hypothesis
+// on the first kPresortGroups point groups (fp32 with v_rcp -- a heuristic, it only
+// decides WHERE a hypothesis is scored, never its result).  Hypotheses with >= kPresortHits
+// hits go to the front of perm, the rest to the back (wave-aggregated atomics).
+constexpr uint32_t kPresortGroups = 32;  // 128 points
+constexpr int kPresortHits = 3;
+
+__global__ __launch_bounds__(64) void k_presort_h(const float4 *__restrict__ rec, uint32_t n,
+                                                  const float *__restrict__ models, uint32_t B, float thr,
+                                                  uint32_t *__restrict__ perm, uint32_t *__restrict__ ends) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t h = blockIdx.x * 64 + lane;
+    const uint32_t hc = h < B ? h : B - 1;
+    float m[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) m[k] = models[(size_t)k * B + hc];
+    const float T2 = 4.0f * thr * thr;  // forward distance < 2 thr
+    const uint32_t ngroups = (n + 3) / 4;
+    const uint32_t g1 = ngroups < kPresortGroups ? ngroups : kPresortGroups;
+    int hits = 0;
+    for (uint32_t g = 0; g < g1; g++) {
+        const float *p = reinterpret_cast<const float *>(rec + 8 * (size_t)g);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const float x1 = p[u], y1 = p[4 + u], x2 = p[8 + u], y2 = p[12 + u];
+            const float X = __builtin_fmaf(m[1], y1, __builtin_fmaf(m[0], x1, m[2]));
+            const float Y = __builtin_fmaf(m[4], y1, __builtin_fmaf(m[3], x1, m[5]));
+            const float Z = __builtin_fmaf(m[7], y1, __builtin_fmaf(m[6], x1, m[8]));
+            const float r = __builtin_amdgcn_rcpf(Z);
+            const float dx = __builtin_fmaf(-X, r, x2), dy = __builtin_fmaf(-Y, r, y2);
+            hits += __builtin_fmaf(dx, dx, dy * dy) < T2 ? 1 : 0;
+        }
+    }
+    const bool valid = h < B;
+    const bool good = valid && hits >= kPresortHits;
+    const uint64_t bg = __ballot(good), bb = __ballot(valid && !good);
+    const uint32_t below = (uint32_t)__popcll(good ? bg & ((1ull << lane) - 1) : bb & ((1ull << lane) - 1));
+    uint32_t fbase = 0, bbase = 0;
+    if (lane == 0) {
+        if (bg) fbase = atomicAdd(&ends[0], (uint32_t)__popcll(bg));
+        if (bb) bbase = atomicAdd(&ends[1], (uint32_t)__popcll(bb));
+    }
+    fbase = __shfl(fbase, 0, 64);
+    bbase = __shfl(bbase, 0, 64);
+    if (valid) perm[good ? fbase + below : B - 1 - (bbase + below)] = h;
 }
 
 // ------------------------------------------------------------------------ line2d
@@ -514,10 +595,16 @@ hipError_t launch_prepare_rec(hipStream_t st, const float4 *pts, uint32_t n, flo
 }
 
 hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const float4 *rec, uint32_t n, float4 ext,
-                           const float *models, uint32_t B, float thr, int32_t *counts, float *sums) {
+                           const float *models, uint32_t B, float thr, uint32_t *perm, int32_t *counts, float *sums) {
     dim3 grid((B + 63) / 64);
+    if (perm) {  // perm: B entries followed by 2 counters
+        uint32_t *ends = perm + B;
+        hipError_t e = hipMemsetAsync(ends, 0, 2 * sizeof(uint32_t), st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_presort_h, grid, dim3(64), 0, st, rec, n, models, B, thr, perm, ends);
+    }
 #define SHF(C, E) \
-    hipLaunchKernelGGL((k_score_hf<C, E>), grid, dim3(64 * C), 0, st, rec, n, ext, models, B, thr, counts, sums)
+    hipLaunchKernelGGL((k_score_hf<C, E>), grid, dim3(64 * C), 0, st, rec, n, ext, models, B, thr, perm, counts, sums)
     if (exact_sum) {
         switch (chunks) {
             case 1: SHF(1, true); break;

@@ -53,10 +53,11 @@ struct usac_ctx {
     uint32_t n = 0, cols = 0, m = 0;
     int dlt_mode = USAC_DLT_THIN;
     int chunks = 4;
-    int score_variant = 0;  // 0 = guard-band fast path, 1 = exact reference expression only
+    int score_variant = 0;  // 0 = guard-band fast path (+ pre-sort), 1 = exact expression only, 2 = fast, no pre-sort
     hipStream_t stream = nullptr;
     DevBuf pts;
     DevBuf rec;             // fast-kernel point records (32 B / point)
+    DevBuf perm;            // hypothesis pre-sort order of the fast kernel (B + 2 uint32)
     float rec_thr = -1.f;   // threshold the record bands were built for
     float4 ext = {0, 0, 0, 0};  // dataset box: max |x1|, |y1|, |x2|, |y2| (fast-kernel bounds)
     // batch buffers
@@ -191,8 +192,14 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
             if (e != hipSuccess) return e;
             c->rec_thr = thr;
         }
+        uint32_t *perm = nullptr;
+        if (c->score_variant == 0) {  // 2: fast kernel without the hypothesis pre-sort (A/B)
+            hipError_t e = c->perm.reserve(sizeof(uint32_t) * ((size_t)B + 2));
+            if (e != hipSuccess) return e;
+            perm = c->perm.as<uint32_t>();
+        }
         return usac::launch_score_hf(c->stream, chunks, chunks == 1, c->rec.as<float4>(), c->n, c->ext,
-                                     c->models.as<float>(), B, thr, c->counts.as<int32_t>(), c->sums.as<float>());
+                                     c->models.as<float>(), B, thr, perm, c->counts.as<int32_t>(), c->sums.as<float>());
     }
     return usac::launch_score_line(c->stream, chunks, c->pts.as<float2>(), c->n, c->models.as<float>(), B, thr,
                                    c->counts.as<int32_t>(), c->sums.as<float>());
@@ -408,7 +415,7 @@ void usac_destroy(usac_ctx *c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
-    for (DevBuf *b : {&c->pts, &c->rec, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
+    for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
                       &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->inl_scratch, &c->lo_idx, &c->one_model,
                       &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok,
@@ -435,7 +442,7 @@ int usac_set_score_chunks(usac_ctx *c, int chunks) {
 }
 
 int usac_set_score_variant(usac_ctx *c, int variant) {
-    if (!c || (variant != 0 && variant != 1)) return USAC_ERR_ARG;
+    if (!c || variant < 0 || variant > 2) return USAC_ERR_ARG;
     c->score_variant = variant;
     return USAC_OK;
 }
