@@ -176,7 +176,8 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 struct HModel {
     float h[9], hi[9];
     float dZ, E;
-    v2f h2[9], dZ2, E2;
+    v2f h2[9];
+    float trm, F;  // packed stage A: r = |Z| trm + F (see stage_a_bounds)
 };
 
 // Stage-A bounds of one hypothesis over the dataset box |x1| <= c.x, |y1| <= c.y,
@@ -184,7 +185,11 @@ struct HModel {
 // reference's X = (h0 x1 + h1 y1) + h2 and in the FMA chain below, so the two differ by at
 // most 2^-21 K_X; dX = 2^-20 K_X (2x slack), likewise dY, dZ;
 // E = ((c.z dZ + dX) + (c.w dZ + dY)) (1 + 2^-18).
-__device__ __forceinline__ void stage_a_bounds(HModel &M, float4 c) {
+// For the packed stage A the per-point radius factor tr_i = (T + band_i)(1 + 2^-18) is
+// replaced by its dataset maximum trm (band_max from the box: Mp <= c.x + c.y + c.z + c.w)
+// and tr (|Z| + dZ) + E by |Z| trm + F with F = (trm dZ + E)(1 + 2^-20) -- never a smaller
+// radius, so never a wrong rejection, and one v_fma_f32 (|Z| as an abs modifier) per point.
+__device__ __forceinline__ void stage_a_bounds(HModel &M, float4 c, float T) {
     const float kx = fabsf(M.h[0]) * c.x + fabsf(M.h[1]) * c.y + fabsf(M.h[2]);
     const float ky = fabsf(M.h[3]) * c.x + fabsf(M.h[4]) * c.y + fabsf(M.h[5]);
     const float kz = fabsf(M.h[6]) * c.x + fabsf(M.h[7]) * c.y + fabsf(M.h[8]);
@@ -194,13 +199,14 @@ __device__ __forceinline__ void stage_a_bounds(HModel &M, float4 c) {
     M.E = ((c.z * dz + dx) + (c.w * dz + dy)) * 1.000003814697265625f;
 #pragma unroll
     for (int k = 0; k < 9; k++) M.h2[k] = v2f{M.h[k], M.h[k]};
-    M.dZ2 = v2f{M.dZ, M.dZ};
-    M.E2 = v2f{M.E, M.E};
+    const float band_max = kBandMp * (((c.x + c.y) + (c.z + c.w)) * 1.00000095367431640625f) + kBandT * T;
+    M.trm = (T + band_max) * 1.000003814697265625f;                  // (1 + 2^-18)
+    M.F = (M.trm * M.dZ + M.E) * 1.00000095367431640625f;             // (1 + 2^-20)
 }
 
 // Stage A for two points at once: the same FMA chain element-wise (v_pk_fma_f32), so each
 // half is bit-identical to stage_a_reject.
-__device__ __forceinline__ void stage_a_reject2(const HModel &M, v2f x1, v2f y1, v2f x2, v2f y2, v2f tr, bool &k0,
+__device__ __forceinline__ void stage_a_reject2(const HModel &M, v2f x1, v2f y1, v2f x2, v2f y2, bool &k0,
                                                 bool &k1) {
     const v2f X = __builtin_elementwise_fma(M.h2[1], y1, __builtin_elementwise_fma(M.h2[0], x1, M.h2[2]));
     const v2f Y = __builtin_elementwise_fma(M.h2[4], y1, __builtin_elementwise_fma(M.h2[3], x1, M.h2[5]));
@@ -208,7 +214,7 @@ __device__ __forceinline__ void stage_a_reject2(const HModel &M, v2f x1, v2f y1,
     const v2f ex = __builtin_elementwise_fma(x2, Z, -X);
     const v2f ey = __builtin_elementwise_fma(y2, Z, -Y);
     const v2f lhs = __builtin_elementwise_fma(ex, ex, ey * ey);
-    const v2f r = __builtin_elementwise_fma(tr, __builtin_elementwise_abs(Z) + M.dZ2, M.E2);
+    const v2f r = v2f{__builtin_fmaf(fabsf(Z.x), M.trm, M.F), __builtin_fmaf(fabsf(Z.y), M.trm, M.F)};
     const v2f rr = r * r;
     k0 = lhs.x > rr.x;
     k1 = lhs.y > rr.y;
@@ -275,8 +281,8 @@ template <bool EXACT_SUM>
 __device__ __forceinline__ void score_group(const HModel &M, float4 X1, float4 Y1, float4 X2, float4 Y2, float4 bd,
                                             float4 tr, float T, float thr, int &cnt, float &sum) {
     bool k0, k1, k2, k3;
-    stage_a_reject2(M, v2f{X1.x, X1.y}, v2f{Y1.x, Y1.y}, v2f{X2.x, X2.y}, v2f{Y2.x, Y2.y}, v2f{tr.x, tr.y}, k0, k1);
-    stage_a_reject2(M, v2f{X1.z, X1.w}, v2f{Y1.z, Y1.w}, v2f{X2.z, X2.w}, v2f{Y2.z, Y2.w}, v2f{tr.z, tr.w}, k2, k3);
+    stage_a_reject2(M, v2f{X1.x, X1.y}, v2f{Y1.x, Y1.y}, v2f{X2.x, X2.y}, v2f{Y2.x, Y2.y}, k0, k1);
+    stage_a_reject2(M, v2f{X1.z, X1.w}, v2f{Y1.z, Y1.w}, v2f{X2.z, X2.w}, v2f{Y2.z, Y2.w}, k2, k3);
     if (__builtin_amdgcn_ballot_w64(!(k0 && k1 && k2 && k3)) == 0) return;
     if (!k0) stage_b<EXACT_SUM>(M, X1.x, Y1.x, X2.x, Y2.x, bd.x, T, thr, cnt, sum);
     if (!k1) stage_b<EXACT_SUM>(M, X1.y, Y1.y, X2.y, Y2.y, bd.y, T, thr, cnt, sum);
@@ -308,8 +314,8 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_hf(const float4 *__restri
         M.h[k] = models[(size_t)k * B + hc];
         M.hi[k] = models[(size_t)(9 + k) * B + hc];
     }
-    stage_a_bounds(M, ext);
     const float T = 2.0f * thr;
+    stage_a_bounds(M, ext, T);
     const uint32_t ngroups = (n + 3) / 4;
     const uint32_t per = (ngroups + CHUNKS - 1) / CHUNKS;
     const uint32_t gbeg = wave * per < ngroups ? wave * per : ngroups;
