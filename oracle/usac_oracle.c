@@ -774,7 +774,7 @@ static inline float fundamental_error(const orc_est *e, unsigned int pidx) {
  *   3. det M(z) at z = -5..5 (LU, partial pivoting), Newton divided differences ->
  *      degree-10 coefficients (:113-136 interpolates at the same nodes);
  *   4. real roots, ascending: derivative-recursion isolation (Gauss-Lucas: every
- *      derivative's roots lie inside the Cauchy bound) + bisection (:139-158);
+ *      derivative's roots lie inside the root bound) + safeguarded Newton (:139-158);
  *   5. per root: null vector of M(z) by elimination with partial pivoting (v9 = 1):
  *      x = v7, y = v8 (:180-187); E assembled as :190-200;
  *   6. cheirality (:202-262): 3x3 SVD (row Jacobi with accumulated rotations), the four
@@ -962,57 +962,108 @@ static double poly_eval(const double *c, int deg, double x) {
     return r;
 }
 
-static double poly_bisect(const double *c, int deg, double lo, double hi, double flo) {
-    for (int it = 0; it < 200; it++) {
-        const double mid = 0.5 * (lo + hi);
-        if (!(mid > lo && mid < hi)) break;
-        const double fm = poly_eval(c, deg, mid);
-        if (fm == 0.0) return mid;
-        if ((fm < 0.0) == (flo < 0.0)) {
-            lo = mid;
-            flo = fm;
-        } else {
-            hi = mid;
-        }
+/* Root refinement inside a sign-changing bracket (monotone there): safeguarded Newton in the
+ * manner of rtsafe, started at the secant (regula falsi) point of the bracket -- a Newton
+ * step when it stays strictly inside the bracket and at least halves the previous step
+ * (|2f| <= |dxold f'|), else bisection; the bracket is tightened at every evaluation.  Stops
+ * on an exact zero, a Newton step below 2^-50 |x| (the root to a few ulp; its end point is
+ * taken when inside the bracket), an unsplittable bracket, or 200 evaluations.  p and p' by one Horner pass. */
+static void poly_eval2(const double *c, int deg, double x, double *f, double *df) {
+    double v = c[deg], d = 0.0;
+    for (int j = deg - 1; j >= 0; j--) {
+        d = d * x + v;
+        v = v * x + c[j];
     }
-    return 0.5 * (lo + hi);
+    *f = v;
+    *df = d;
+}
+
+static double poly_refine(const double *c, int deg, double lo, double hi, double flo, double fhi) {
+    double x = lo - flo * ((hi - lo) / (fhi - flo));
+    if (!(x > lo && x < hi)) x = 0.5 * (lo + hi);
+    double dxold = hi - lo, dx = dxold, f, df;
+    poly_eval2(c, deg, x, &f, &df);
+    for (int it = 0; it < 200; it++) {
+        if (f == 0.0) return x;
+        if ((f < 0.0) == (flo < 0.0)) {
+            lo = x;
+            flo = f;
+        } else {
+            hi = x;
+        }
+        const double step = f / df;
+        const double xn = x - step;
+        const int inside = xn > lo && xn < hi;
+        if (xn == x || fabs(step) <= 0x1p-50 * fabs(x)) return inside ? xn : x;
+        const int newton = inside && !(fabs(2.0 * f) > fabs(dxold * df));
+        dxold = dx;
+        if (newton) {
+            dx = step;
+            x = xn;
+        } else {
+            const double mid = 0.5 * (lo + hi);
+            if (!(mid > lo && mid < hi)) return mid;
+            dx = mid - x;
+            x = mid;
+        }
+        poly_eval2(c, deg, x, &f, &df);
+    }
+    return x;
+}
+
+/* root bound with IEEE operations only: the smallest r = 2^k (k >= 0) with
+ * |a_n| r > sum_i |a_i| r^(i-n+1) (then no root has |z| >= r) */
+static double root_bound(const double *a, int n) {
+    double r = 1.0;
+    const double an = fabs(a[n]);
+    for (int it = 0; it < 2100; it++) {
+        double t = fabs(a[0]);
+        for (int i = 1; i < n; i++) t = t / r + fabs(a[i]);
+        if (an * r > t) break;
+        r = r * 2.0;
+    }
+    return r;
 }
 
 /* real roots of a[0] + a[1] z + ... + a[n] z^n, ascending (<= n) */
 static int real_roots(const double *a_in, int n, double *roots) {
     while (n > 0 && a_in[n] == 0.0) n--;
     if (n == 0) return 0;
-    double R = 0.0;
-    for (int i = 0; i < n; i++) {
-        double q = fabs(a_in[i] / a_in[n]);
-        if (q > R) R = q;
-    }
-    R = R + 1.0;
+    const double R = root_bound(a_in, n);
+    /* level g works on the derivative of order n-g (degree g) and leaves exactly g points,
+     * ascending: the root of each sign-changing interval, or the interval's left end as a
+     * filler where it has none (fillers only split monotone intervals further, and keep the
+     * per-level counts fixed) */
     double crit[10], next[10];
-    int ncrit = 0;
-    for (int d = n - 1; d >= 0; d--) {
-        /* coefficients of the d-th derivative: a[j+d] (j+d)!/j! */
+    int found[10] = {0};
+    for (int g = 1; g <= n; g++) {
+        const int d = n - g;
         double c[11];
-        const int deg = n - d;
-        for (int j = 0; j <= deg; j++) {
+        for (int j = 0; j <= g; j++) {
             double f = 1.0;
             for (int m = j + d; m > j; m--) f *= (double)m;
             c[j] = a_in[j + d] * f;
         }
-        int nn = 0;
-        double lo = -R, flo = poly_eval(c, deg, lo);
-        for (int k = 0; k <= ncrit; k++) {
-            const double hi = k < ncrit ? crit[k] : R;
-            const double fhi = poly_eval(c, deg, hi);
-            if (hi > lo && ((flo < 0.0) != (fhi < 0.0))) next[nn++] = poly_bisect(c, deg, lo, hi, flo);
+        double lo = -R, flo = poly_eval(c, g, lo);
+        for (int k = 0; k < g; k++) {
+            const double hi = k < g - 1 ? crit[k] : R;
+            const double fhi = poly_eval(c, g, hi);
+            if (hi > lo && ((flo < 0.0) != (fhi < 0.0))) {
+                next[k] = poly_refine(c, g, lo, hi, flo, fhi);
+                found[k] = 1;
+            } else {
+                next[k] = lo;
+                found[k] = 0;
+            }
             lo = hi;
             flo = fhi;
         }
-        for (int k = 0; k < nn; k++) crit[k] = next[k];
-        ncrit = nn;
+        for (int k = 0; k < g; k++) crit[k] = next[k];
     }
-    for (int k = 0; k < ncrit; k++) roots[k] = crit[k];
-    return ncrit;
+    int nr = 0;
+    for (int k = 0; k < n; k++)
+        if (found[k]) roots[nr++] = crit[k];
+    return nr;
 }
 
 /* null vector of a 4x4 system: rows Jacobi-orthogonalised, the smallest row dropped, unit

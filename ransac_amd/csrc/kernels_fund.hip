@@ -205,119 +205,4 @@ hipError_t launch_score_f(hipStream_t st, int estimator, int chunks, const float
     return hipGetLastError();
 }
 
-// ------------------------------------------------------------------------ essential (5-pt)
-// One lane per sample: 5 x 9 fp64 rows -> Jacobi -> four null-space rows -> det M(z) at
-// z = -5..5 -> degree-10 coefficients -> real roots -> per root: null vector of M(z), E,
-// cheirality over the sample; the first root that puts all five points in front of both
-// cameras gives the sample's (single) model (five_points.cpp:30-34, 239-273).  Slot layout
-// as the fundamental path with one slot per sample: models [9][B], counts 0 / -1, list.
-__global__ __launch_bounds__(64) void k_solve_e5(const float4 *__restrict__ pts, uint32_t n,
-                                                 const int32_t *__restrict__ samples_in, int32_t *samples_out,
-                                                 uint32_t B, uint64_t seed, uint64_t first_hyp,
-                                                 float *__restrict__ models, int32_t *__restrict__ counts,
-                                                 uint32_t *__restrict__ list, uint32_t *__restrict__ list_n) {
-    const uint32_t lane = threadIdx.x;
-    const uint32_t h = blockIdx.x * 64 + lane;
-    const bool active = h < B;
-    int nvalid = 0;
-    if (active) {
-        int32_t s[5];
-        if (samples_in) {
-#pragma unroll
-            for (int i = 0; i < 5; i++) s[i] = samples_in[5 * (size_t)h + i];
-        } else {
-            draw_sample<5>(seed, first_hyp + h, n, s);
-            if (samples_out) {
-#pragma unroll
-                for (int i = 0; i < 5; i++) samples_out[5 * (size_t)h + i] = s[i];
-            }
-        }
-        double N[4][9];
-        {
-            double W[5][9];
-#pragma unroll
-            for (int i = 0; i < 5; i++) {
-                const float4 p = pts[s[i]];
-                const double x1 = p.x, y1 = p.y, x2 = p.z, y2 = p.w;
-                W[i][0] = x1 * x2; W[i][1] = x2 * y1; W[i][2] = x2;
-                W[i][3] = x1 * y2; W[i][4] = y1 * y2; W[i][5] = y2;
-                W[i][6] = x1; W[i][7] = y1; W[i][8] = 1.0;
-            }
-            row_jacobi<5>(W);
-            e5::null_basis4(W, N);
-        }
-        double c[11], z[11];
-        for (int k = 0; k < 11; k++) {
-            z[k] = (double)(k - 5);
-            double M[10][10];
-            e5::matrix(N, z[k], M);
-            c[k] = e5::det10(M);
-        }
-        for (int j = 1; j < 11; j++)
-            for (int i = 10; i >= j; i--) c[i] = (c[i] - c[i - 1]) / (z[i] - z[i - j]);
-        double a[11];
-        for (int i = 0; i < 11; i++) a[i] = 0.0;
-        a[0] = c[10];
-        int deg = 0;
-        for (int k = 9; k >= 0; k--) {
-            a[deg + 1] = 0.0;
-            for (int i = deg + 1; i >= 1; i--) a[i] = a[i - 1] - z[k] * a[i];
-            a[0] = c[k] - z[k] * a[0];
-            deg++;
-        }
-        double roots[10];
-        const int nr = e5::real_roots10(a, roots);
-        for (int r = 0; r < nr && !nvalid; r++) {
-            const double zz = roots[r];
-            double M[10][10], v[10];
-            e5::matrix(N, zz, M);
-            if (!e5::null10(M, v)) continue;
-            const double x = v[7], y = v[8];
-            double E[9];
-#pragma unroll
-            for (int k = 0; k < 9; k++) E[k] = N[0][k] * x + N[1][k] * y + N[2][k] * zz + N[3][k];
-            double U[3][3], V[3][3];
-            e5::svd3(E, U, V);
-            bool found = false;
-            for (int j = 0; j < 4 && !found; j++) {
-                double P[3][4];
-                e5::projection(U, V, j, P);
-                bool all = true;
-                for (int k = 0; k < 5 && all; k++) {
-                    const float4 p = pts[s[k]];
-                    all = e5::in_front((double)p.x, (double)p.y, (double)p.z, (double)p.w, P);
-                }
-                found = all;
-            }
-            if (found) {
-#pragma unroll
-                for (int k = 0; k < 9; k++) models[(size_t)k * B + h] = (float)E[k];
-                nvalid = 1;
-            }
-        }
-        counts[h] = nvalid ? 0 : -1;
-    }
-    uint32_t incl = (uint32_t)nvalid;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t v = __shfl_up(incl, off, 64);
-        if (lane >= (uint32_t)off) incl += v;
-    }
-    const uint32_t total = __shfl(incl, 63, 64);
-    uint32_t base = 0;
-    if (lane == 63 && total) base = atomicAdd(list_n, total);
-    base = __shfl(base, 63, 64);
-    if (nvalid) list[base + incl - 1] = h;
-}
-
-hipError_t launch_solve_e5(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
-                           int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, float *models,
-                           int32_t *counts, uint32_t *list, uint32_t *list_n) {
-    hipError_t e = hipMemsetAsync(list_n, 0, sizeof(uint32_t), st);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_solve_e5, dim3((B + 63) / 64), dim3(64), 0, st, pts, n, samples_in, samples_out, B, seed,
-                       first_hyp, models, counts, list, list_n);
-    return hipGetLastError();
-}
-
 }  // namespace usac

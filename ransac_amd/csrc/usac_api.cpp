@@ -65,6 +65,7 @@ struct usac_ctx {
     DevBuf list, list_n;    // fundamental: occupied model slots (compacted) and their number
     DevBuf pool_idx, pool_pts, masks;  // SPRT parity path: pool order, permuted points, flag words
     DevBuf lo_idx;                     // LO-RANSAC: host-drawn index lists for the device LSQ
+    DevBuf e5_ws;                      // staged 5-point solver workspace
     // throughput SPRT (usac_set_sprt): batch-fixed test on the pool-ordered points
     bool sprt_on = false;
     float sprt_log_up = 0.f, sprt_log_down = 0.f, sprt_log_A = 0.f;
@@ -147,10 +148,13 @@ int ensure_single(usac_ctx *c) {
 // solve (samples on device, or device RNG when samples_dev == nullptr) into c->models
 hipError_t enqueue_solve(usac_ctx *c, const int32_t *samples_dev, uint32_t B, uint64_t seed, uint64_t first_hyp,
                          int32_t *samples_out) {
-    if (is_e(c))
+    if (is_e(c)) {
+        hipError_t e = c->e5_ws.reserve(usac::e5_workspace_bytes(B));
+        if (e != hipSuccess) return e;
         return usac::launch_solve_e5(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, seed,
                                      first_hyp, c->models.as<float>(), c->counts.as<int32_t>(),
-                                     c->list.as<uint32_t>(), c->list_n.as<uint32_t>());
+                                     c->list.as<uint32_t>(), c->list_n.as<uint32_t>(), c->e5_ws.p);
+    }
     if (is_f(c))
         return usac::launch_solve_f7(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, seed,
                                      first_hyp, c->models.as<float>(), c->counts.as<int32_t>(),
@@ -417,7 +421,7 @@ void usac_destroy(usac_ctx *c) {
     if (c->comm) ncclCommDestroy(c->comm);
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
-                      &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->inl_scratch, &c->lo_idx, &c->one_model,
+                      &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->inl_scratch, &c->lo_idx, &c->e5_ws, &c->one_model,
                       &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok,
                       &c->rec_send, &c->rec_all})
         b->release();

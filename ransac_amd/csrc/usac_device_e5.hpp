@@ -11,6 +11,8 @@
 // (real roots), elimination with partial pivoting (null vector of M(z)), and a cheirality
 // test through Jacobi 3x3 SVD + 4x4 linear triangulation.
 #pragma once
+#include <type_traits>
+
 #include "usac_device.hpp"
 
 namespace usac {
@@ -204,49 +206,77 @@ __device__ __forceinline__ void matrix(const double (&N)[4][9], double z, double
     for (int m = 0; m < 10; m++) M[9][m] = d0[m] - d1[m] + d2[m];
 }
 
+// compile-time loop: f(std::integral_constant<int, I>) for I = B .. E-1.  Used where a
+// "#pragma unroll" loop is not enough: the indices must be constants when the IR is first
+// built, or instcombine folds select chains of array loads into one indexed load
+// (A[p][j]) before unrolling, and the matrix can never leave scratch memory.
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+// A value the optimiser must treat as freshly computed: select chains over opaque values
+// cannot be folded into one dynamically indexed load, which would force the whole matrix
+// into scratch memory.  Emits no instruction.
+__device__ __forceinline__ double opaque(double x) {
+    asm("" : "+v"(x));
+    return x;
+}
+
 // in-place elimination with partial pivoting over the first NCOL columns (first maximal
-// |pivot|, rows swapped); returns false on an exactly zero pivot column, sign = (-1)^swaps
+// |pivot|, rows swapped); returns false on an exactly zero pivot column, sign = (-1)^swaps.
+// Columns < k are dead after step k and never touched again.
 template <int NCOL>
 __device__ __forceinline__ bool eliminate(double (&A)[10][10], double &sign) {
-#pragma unroll
-    for (int k = 0; k < NCOL; k++) {
+    bool ok = true;
+    static_for<0, NCOL>([&](auto K) {
+        constexpr int k = decltype(K)::value;
+        if (!ok) return;
         int p = k;
         double best = fabs(A[k][k]);
-#pragma unroll
-        for (int i = k + 1; i < 10; i++)
+        static_for<k + 1, 10>([&](auto I) {
+            constexpr int i = decltype(I)::value;
             if (fabs(A[i][k]) > best) {
                 best = fabs(A[i][k]);
                 p = i;
             }
-        // bring the pivot row up (register-resident: select instead of indexed swap)
+        });
         double pr[10];
-#pragma unroll
-        for (int j = 0; j < 10; j++) {
+        static_for<k, 10>([&](auto J) {
+            constexpr int j = decltype(J)::value;
             double v = A[k][j];
-#pragma unroll
-            for (int i = k + 1; i < 10; i++) v = (i == p) ? A[i][j] : v;
+            static_for<k + 1, 10>([&](auto I) {
+                constexpr int i = decltype(I)::value;
+                v = (i == p) ? opaque(A[i][j]) : v;
+            });
             pr[j] = v;
+        });
+        if (pr[k] == 0.0) {
+            ok = false;
+            return;
         }
-        if (pr[k] == 0.0) return false;
-        if (p != k) {
-#pragma unroll
-            for (int i = k + 1; i < 10; i++)
-                if (i == p) {
-#pragma unroll
-                    for (int j = 0; j < 10; j++) A[i][j] = A[k][j];
-                }
-            sign = -sign;
-        }
-#pragma unroll
-        for (int j = 0; j < 10; j++) A[k][j] = pr[j];
-#pragma unroll
-        for (int i = k + 1; i < 10; i++) {
+        sign = (p != k) ? -sign : sign;
+        static_for<k + 1, 10>([&](auto I) {
+            constexpr int i = decltype(I)::value;
+            static_for<k, 10>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                A[i][j] = (i == p) ? opaque(A[k][j]) : opaque(A[i][j]);
+            });
+        });
+        static_for<k, 10>([&](auto J) { A[k][decltype(J)::value] = pr[decltype(J)::value]; });
+        static_for<k + 1, 10>([&](auto I) {
+            constexpr int i = decltype(I)::value;
             const double f = A[i][k] / A[k][k];
-#pragma unroll
-            for (int j = k + 1; j < 10; j++) A[i][j] -= f * A[k][j];
-        }
-    }
-    return true;
+            static_for<k + 1, 10>([&](auto J) {
+                constexpr int j = decltype(J)::value;
+                A[i][j] -= f * A[k][j];
+            });
+        });
+    });
+    return ok;
 }
 
 __device__ __forceinline__ double det10(double (&A)[10][10]) {
@@ -278,57 +308,207 @@ __device__ __forceinline__ double poly_eval(const double *c, int deg, double x) 
     return r;
 }
 
-__device__ __noinline__ double poly_bisect(const double *c, int deg, double lo, double hi, double flo) {
-    for (int it = 0; it < 200; it++) {
-        const double mid = 0.5 * (lo + hi);
-        if (!(mid > lo && mid < hi)) break;
-        const double fm = poly_eval(c, deg, mid);
-        if (fm == 0.0) return mid;
-        if ((fm < 0.0) == (flo < 0.0)) {
-            lo = mid;
-            flo = fm;
-        } else {
-            hi = mid;
-        }
+__device__ __forceinline__ void poly_eval2(const double *c, int deg, double x, double &f, double &df) {
+    double v = c[deg], d = 0.0;
+    for (int j = deg - 1; j >= 0; j--) {
+        d = d * x + v;
+        v = v * x + c[j];
     }
-    return 0.5 * (lo + hi);
+    f = v;
+    df = d;
 }
 
-// real roots of a[0] + ... + a[10] z^10, ascending (oracle real_roots)
-__device__ __noinline__ int real_roots10(const double *a, double *roots) {
+// safeguarded Newton from the secant point of a sign-changing bracket (oracle poly_refine,
+// same op sequence)
+__device__ __noinline__ double poly_refine(const double *c, int deg, double lo, double hi, double flo, double fhi) {
+    double x = lo - flo * ((hi - lo) / (fhi - flo));
+    if (!(x > lo && x < hi)) x = 0.5 * (lo + hi);
+    double dxold = hi - lo, dx = dxold, f, df;
+    poly_eval2(c, deg, x, f, df);
+    for (int it = 0; it < 200; it++) {
+        if (f == 0.0) return x;
+        if ((f < 0.0) == (flo < 0.0)) {
+            lo = x;
+            flo = f;
+        } else {
+            hi = x;
+        }
+        const double step = f / df;
+        const double xn = x - step;
+        const bool inside = xn > lo && xn < hi;
+        if (xn == x || fabs(step) <= 0x1p-50 * fabs(x)) return inside ? xn : x;
+        const bool newton = inside && !(fabs(2.0 * f) > fabs(dxold * df));
+        dxold = dx;
+        if (newton) {
+            dx = step;
+            x = xn;
+        } else {
+            const double mid = 0.5 * (lo + hi);
+            if (!(mid > lo && mid < hi)) return mid;
+            dx = mid - x;
+            x = mid;
+        }
+        poly_eval2(c, deg, x, f, df);
+    }
+    return x;
+}
+
+// IEEE-only root bound (oracle root_bound): smallest r = 2^k with |a_n| r > sum |a_i| r^(i-n+1)
+__device__ __forceinline__ double root_bound(const double *a, int n) {
+    double r = 1.0;
+    const double an = fabs(a[n]);
+    for (int it = 0; it < 2100; it++) {
+        double t = fabs(a[0]);
+        for (int i = 1; i < n; i++) t = t / r + fabs(a[i]);
+        if (an * r > t) break;
+        r = r * 2.0;
+    }
+    return r;
+}
+
+// real roots of a[0] + ... + a[n] z^n (oracle real_roots, any n <= 10), ascending; the
+// general-degree path with indexed arrays, taken only when a[10] == 0
+__device__ __noinline__ int real_roots_dyn(const double *a, double *roots) {
     int n = 10;
     while (n > 0 && a[n] == 0.0) n--;
     if (n == 0) return 0;
-    double R = 0.0;
-    for (int i = 0; i < n; i++) {
-        const double q = fabs(a[i] / a[n]);
-        if (q > R) R = q;
-    }
-    R = R + 1.0;
+    const double R = root_bound(a, n);
     double crit[10], next[10];
-    int ncrit = 0;
-    for (int d = n - 1; d >= 0; d--) {
+    int found[10] = {0};
+    for (int g = 1; g <= n; g++) {
+        const int d = n - g;
         double c[11];
-        const int deg = n - d;
-        for (int j = 0; j <= deg; j++) {
+        for (int j = 0; j <= g; j++) {
             double f = 1.0;
             for (int m = j + d; m > j; m--) f *= (double)m;
             c[j] = a[j + d] * f;
         }
-        int nn = 0;
-        double lo = -R, flo = poly_eval(c, deg, lo);
-        for (int k = 0; k <= ncrit; k++) {
-            const double hi = k < ncrit ? crit[k] : R;
-            const double fhi = poly_eval(c, deg, hi);
-            if (hi > lo && ((flo < 0.0) != (fhi < 0.0))) next[nn++] = poly_bisect(c, deg, lo, hi, flo);
+        double lo = -R, flo = poly_eval(c, g, lo);
+        for (int k = 0; k < g; k++) {
+            const double hi = k < g - 1 ? crit[k] : R;
+            const double fhi = poly_eval(c, g, hi);
+            if (hi > lo && ((flo < 0.0) != (fhi < 0.0))) {
+                next[k] = poly_refine(c, g, lo, hi, flo, fhi);
+                found[k] = 1;
+            } else {
+                next[k] = lo;
+                found[k] = 0;
+            }
             lo = hi;
             flo = fhi;
         }
-        for (int k = 0; k < nn; k++) crit[k] = next[k];
-        ncrit = nn;
+        for (int k = 0; k < g; k++) crit[k] = next[k];
     }
-    for (int k = 0; k < ncrit; k++) roots[k] = crit[k];
-    return ncrit;
+    int nr = 0;
+    for (int k = 0; k < n; k++)
+        if (found[k]) roots[nr++] = crit[k];
+    return nr;
+}
+
+// The same spec for a true degree-10 polynomial with every degree a compile-time constant:
+// coefficients, partition points and Horner loops all stay in registers.
+template <int G>
+__device__ __forceinline__ double poly_eval_t(const double (&c)[11], double x) {
+    double r = c[G];
+#pragma unroll
+    for (int i = G - 1; i >= 0; i--) r = r * x + c[i];
+    return r;
+}
+
+template <int G>
+__device__ __forceinline__ double poly_refine_t(const double (&c)[11], double lo, double hi, double flo, double fhi) {
+    double x = lo - flo * ((hi - lo) / (fhi - flo));
+    if (!(x > lo && x < hi)) x = 0.5 * (lo + hi);
+    double dxold = hi - lo, dx = dxold, f, df;
+    {
+        double v = c[G], d = 0.0;
+#pragma unroll
+        for (int j = G - 1; j >= 0; j--) {
+            d = d * x + v;
+            v = v * x + c[j];
+        }
+        f = v;
+        df = d;
+    }
+    for (int it = 0; it < 200; it++) {
+        if (f == 0.0) return x;
+        if ((f < 0.0) == (flo < 0.0)) {
+            lo = x;
+            flo = f;
+        } else {
+            hi = x;
+        }
+        const double step = f / df;
+        const double xn = x - step;
+        const bool inside = xn > lo && xn < hi;
+        if (xn == x || fabs(step) <= 0x1p-50 * fabs(x)) return inside ? xn : x;
+        const bool newton = inside && !(fabs(2.0 * f) > fabs(dxold * df));
+        dxold = dx;
+        if (newton) {
+            dx = step;
+            x = xn;
+        } else {
+            const double mid = 0.5 * (lo + hi);
+            if (!(mid > lo && mid < hi)) return mid;
+            dx = mid - x;
+            x = mid;
+        }
+        double v = c[G], d = 0.0;
+#pragma unroll
+        for (int j = G - 1; j >= 0; j--) {
+            d = d * x + v;
+            v = v * x + c[j];
+        }
+        f = v;
+        df = d;
+    }
+    return x;
+}
+
+template <int G>
+__device__ __forceinline__ void roots_level(const double (&a)[11], double R, double (&crit)[10], bool (&found)[10]) {
+    constexpr int d = 10 - G;
+    double c[11];
+#pragma unroll
+    for (int j = 0; j <= G; j++) {
+        double f = 1.0;
+#pragma unroll
+        for (int m = j + d; m > j; m--) f *= (double)m;
+        c[j] = a[j + d] * f;
+    }
+    double next[10];
+    double lo = -R, flo = poly_eval_t<G>(c, lo);
+#pragma unroll
+    for (int k = 0; k < G; k++) {
+        const double hi = k < G - 1 ? crit[k] : R;
+        const double fhi = poly_eval_t<G>(c, hi);
+        if (hi > lo && ((flo < 0.0) != (fhi < 0.0))) {
+            next[k] = poly_refine_t<G>(c, lo, hi, flo, fhi);
+            found[k] = true;
+        } else {
+            next[k] = lo;
+            found[k] = false;
+        }
+        lo = hi;
+        flo = fhi;
+    }
+#pragma unroll
+    for (int k = 0; k < G; k++) crit[k] = next[k];
+    if constexpr (G < 10) roots_level<G + 1>(a, R, crit, found);
+}
+
+// a[10] != 0 required; root k (ascending) is crit[k] where found[k]
+__device__ __forceinline__ void real_roots10(const double (&a)[11], double (&crit)[10], bool (&found)[10]) {
+    double r = 1.0;
+    const double an = fabs(a[10]);
+    for (int it = 0; it < 2100; it++) {
+        double t = fabs(a[0]);
+#pragma unroll
+        for (int i = 1; i < 10; i++) t = t / r + fabs(a[i]);
+        if (an * r > t) break;
+        r = r * 2.0;
+    }
+    roots_level<1>(a, r, crit, found);
 }
 
 // null vector of a 4x4 triangulation system (oracle null4)

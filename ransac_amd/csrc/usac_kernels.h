@@ -44,10 +44,12 @@ hipError_t launch_prepare_f(hipStream_t st, const float *in, uint32_t K, float *
 hipError_t launch_score_f(hipStream_t st, int estimator, int chunks, const float4 *pts, uint32_t n,
                           const float *models, size_t stride, const uint32_t *list, const uint32_t *list_n,
                           uint32_t kmax, float thr, int32_t *counts, float *sums);
-// essential 5-point: one slot per sample (models [9][B], counts 0 / -1, list / list_n)
+// essential 5-point (kernels_ess.hip): one slot per sample (models [9][B], counts 0 / -1,
+// list / list_n); workspace = e5_workspace_bytes(B)
 hipError_t launch_solve_e5(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
                            int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, float *models,
-                           int32_t *counts, uint32_t *list, uint32_t *list_n);
+                           int32_t *counts, uint32_t *list, uint32_t *list_n, void *workspace);
+size_t e5_workspace_bytes(uint32_t B);
 hipError_t launch_nonminimal_f(hipStream_t st, const float4 *pts, const int32_t *idx, uint32_t n, float4 *q,
                                double *partial, float *ws, float *model_out, int32_t *ok);
 
