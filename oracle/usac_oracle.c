@@ -778,7 +778,8 @@ static inline float fundamental_error(const orc_est *e, unsigned int pidx) {
  *   5. per root: null vector of M(z) by elimination with partial pivoting (v9 = 1):
  *      x = v7, y = v8 (:180-187); E assembled as :190-200;
  *   6. cheirality (:202-262): 3x3 SVD (row Jacobi with accumulated rotations), the four
- *      projections, linear triangulation (4x4 row Jacobi, null vector), CalcDepth; the
+ *      projections, linear triangulation (the rank-3 DLT null vector on the first ray,
+ *      see triangulate()), CalcDepth; the
  *      first root whose E puts all five points in front of both cameras is returned. */
 
 /* row Jacobi on r rows of `cols` (<= 4) columns, same rules as row_jacobi; J (nullable,
@@ -1066,50 +1067,6 @@ static int real_roots(const double *a_in, int n, double *roots) {
     return nr;
 }
 
-/* null vector of a 4x4 system: rows Jacobi-orthogonalised, the smallest row dropped, unit
- * complement of the other three (least represented axis, two Gram-Schmidt passes) */
-static void null4(double A[4][4], double *X) {
-    row_jacobi_small(A, 4, 4, NULL);
-    double n2[4];
-    int m = 0;
-    for (int i = 0; i < 4; i++) {
-        double a = 0.0;
-        for (int k = 0; k < 4; k++) a += A[i][k] * A[i][k];
-        n2[i] = a;
-        if (i > 0 && a < n2[m]) m = i;
-    }
-    double U[3][4];
-    int nu = 0;
-    for (int i = 0; i < 4; i++) {
-        if (i == m || !(n2[i] > 0.0)) continue;
-        const double inv = 1.0 / sqrt(n2[i]);
-        for (int k = 0; k < 4; k++) U[nu][k] = A[i][k] * inv;
-        nu++;
-    }
-    int ks = 0;
-    double bestc = 0.0;
-    for (int k = 0; k < 4; k++) {
-        double cc = 0.0;
-        for (int i = 0; i < nu; i++) cc += U[i][k] * U[i][k];
-        if (k == 0 || cc < bestc) {
-            bestc = cc;
-            ks = k;
-        }
-    }
-    double x[4];
-    for (int k = 0; k < 4; k++) x[k] = k == ks ? 1.0 : 0.0;
-    for (int pass = 0; pass < 2; pass++)
-        for (int i = 0; i < nu; i++) {
-            double d = 0.0;
-            for (int k = 0; k < 4; k++) d += U[i][k] * x[k];
-            for (int k = 0; k < 4; k++) x[k] -= d * U[i][k];
-        }
-    double nrm = 0.0;
-    for (int k = 0; k < 4; k++) nrm += x[k] * x[k];
-    nrm = sqrt(nrm);
-    for (int k = 0; k < 4; k++) X[k] = x[k] / nrm;
-}
-
 static double det3d(const double P[3][4]) {
     return P[0][0] * (P[1][1] * P[2][2] - P[1][2] * P[2][1]) - P[0][1] * (P[1][0] * P[2][2] - P[1][2] * P[2][0]) +
            P[0][2] * (P[1][0] * P[2][1] - P[1][1] * P[2][0]);
@@ -1126,17 +1083,31 @@ static double calc_depth(const double *X, const double P[3][4]) {
     return (w / X[3]) * (sign / m3);
 }
 
-/* TriangulatePoint (five_points.cpp:304-334) */
-static void triangulate(double x1, double y1, double x2, double y2, const double P1[3][4], const double P2[3][4],
-                        double *X) {
-    double A[4][4];
-    for (int c = 0; c < 4; c++) {
-        A[0][c] = x1 * P1[2][c] - P1[0][c];
-        A[1][c] = y1 * P1[2][c] - P1[1][c];
-        A[2][c] = x2 * P2[2][c] - P2[0][c];
-        A[3][c] = y2 * P2[2][c] - P2[1][c];
+/* TriangulatePoint (five_points.cpp:304-334) with P1 = P_ref = [I|0].  The reference takes
+ * the smallest right singular vector of the 4x4 DLT system.  A correspondence that satisfies
+ * the epipolar constraint of E -- the five sample points do, up to rounding -- makes that
+ * system rank 3, and its null vector lies on the first camera's ray: rows 0-1 give
+ * X = (x1 s, y1 s, s, w) exactly, and (s, w) is the null vector of the remaining rank-1
+ * 2x2 system, perpendicular to its larger row.  CalcDepth is scale- and sign-invariant in
+ * X, so the depth signs are the reference's wherever they exceed the SVD's own rounding
+ * noise -- at a few dozen operations instead of a 4x4 SVD. */
+static void triangulate(double x1, double y1, double x2, double y2, const double P[3][4], double *X) {
+    double b[2][2];
+    for (int r = 0; r < 2; r++) {
+        const double u = r == 0 ? x2 : y2;
+        double row[4];
+        for (int c = 0; c < 4; c++) row[c] = u * P[2][c] - P[r][c];
+        b[r][0] = row[0] * x1 + row[1] * y1 + row[2];
+        b[r][1] = row[3];
     }
-    null4(A, X);
+    const double n0 = b[0][0] * b[0][0] + b[0][1] * b[0][1];
+    const double n1 = b[1][0] * b[1][0] + b[1][1] * b[1][1];
+    const int i = n0 >= n1 ? 0 : 1;
+    const double sc = b[i][1], w = -b[i][0];
+    X[0] = x1 * sc;
+    X[1] = y1 * sc;
+    X[2] = sc;
+    X[3] = w;
 }
 
 /* ProjectionsFromEssential (five_points.cpp:336-371): P[j] = [R | t], R in {U W V^T, U W^T V^T},
@@ -1253,11 +1224,11 @@ static int essential_5pt_all(const orc_est *e, const int *sample, float *Eout, f
         int found = 0;
         for (int j = 0; j < 4 && !found; j++) {
             double X[4];
-            triangulate(p1[0][0], p1[0][1], p2[0][0], p2[0][1], Pref, P[j], X);
+            triangulate(p1[0][0], p1[0][1], p2[0][0], p2[0][1], P[j], X);
             if (!(calc_depth(X, Pref) > 0 && calc_depth(X, P[j]) > 0)) continue;
             int inl = 1;
             for (int k = 1; k < 5; k++) {
-                triangulate(p1[k][0], p1[k][1], p2[k][0], p2[k][1], Pref, P[j], X);
+                triangulate(p1[k][0], p1[k][1], p2[k][0], p2[k][1], P[j], X);
                 if (calc_depth(X, Pref) > 0 && calc_depth(X, P[j]) > 0) inl++;
             }
             if (inl >= 5) found = 1;

@@ -511,70 +511,6 @@ __device__ __forceinline__ void real_roots10(const double (&a)[11], double (&cri
     roots_level<1>(a, r, crit, found);
 }
 
-// null vector of a 4x4 triangulation system (oracle null4)
-__device__ __forceinline__ void null4(double (&A)[4][4], double (&X)[4]) {
-    double J[4][4];
-    jacobi_small<4, 4, false>(A, J);
-    double n2[4];
-    int m = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        double a = 0.0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) a += A[i][k] * A[i][k];
-        n2[i] = a;
-    }
-#pragma unroll
-    for (int i = 1; i < 4; i++)
-        if (n2[i] < n2[m]) m = i;
-    double U[3][4];
-    bool use[3];
-    int nu = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        if (i == m) continue;
-        const bool ok = n2[i] > 0.0;
-        const double inv = ok ? 1.0 / sqrt(n2[i]) : 0.0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) U[nu][k] = A[i][k] * inv;
-        use[nu] = ok;
-        nu++;
-    }
-    int ks = 0;
-    double bestc = 0.0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        double cc = 0.0;
-#pragma unroll
-        for (int i = 0; i < 3; i++)
-            if (use[i]) cc += U[i][k] * U[i][k];
-        if (k == 0 || cc < bestc) {
-            bestc = cc;
-            ks = k;
-        }
-    }
-    double x[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) x[k] = k == ks ? 1.0 : 0.0;
-#pragma unroll
-    for (int pass = 0; pass < 2; pass++)
-#pragma unroll
-        for (int i = 0; i < 3; i++) {
-            if (!use[i]) continue;
-            double d = 0.0;
-#pragma unroll
-            for (int k = 0; k < 4; k++) d += U[i][k] * x[k];
-#pragma unroll
-            for (int k = 0; k < 4; k++) x[k] -= d * U[i][k];
-        }
-    double nrm = 0.0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) nrm += x[k] * x[k];
-    nrm = sqrt(nrm);
-#pragma unroll
-    for (int k = 0; k < 4; k++) X[k] = x[k] / nrm;
-}
-
 __device__ __forceinline__ double det3p(const double (&P)[3][4]) {
     return P[0][0] * (P[1][1] * P[2][2] - P[1][2] * P[2][1]) - P[0][1] * (P[1][0] * P[2][2] - P[1][2] * P[2][0]) +
            P[0][2] * (P[1][0] * P[2][1] - P[1][1] * P[2][0]);
@@ -592,19 +528,26 @@ __device__ __forceinline__ double calc_depth(const double (&X)[4], const double 
     return (w / X[3]) * (sign / m3);
 }
 
-// both depths of a correspondence for P_ref = [I|0] and P (TriangulatePoint :304-334)
+// both depths of a correspondence for P_ref = [I|0] and P (TriangulatePoint :304-334 as the
+// rank-3 null vector on the first ray, oracle triangulate)
 __device__ __forceinline__ bool in_front(double x1, double y1, double x2, double y2, const double (&P)[3][4]) {
     constexpr double Pr[3][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}};
-    double A[4][4];
+    double b[2][2];
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-        A[0][c] = x1 * Pr[2][c] - Pr[0][c];
-        A[1][c] = y1 * Pr[2][c] - Pr[1][c];
-        A[2][c] = x2 * P[2][c] - P[0][c];
-        A[3][c] = y2 * P[2][c] - P[1][c];
+    for (int r = 0; r < 2; r++) {
+        const double u = r == 0 ? x2 : y2;
+        double row[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++) row[c] = u * P[2][c] - P[r][c];
+        b[r][0] = row[0] * x1 + row[1] * y1 + row[2];
+        b[r][1] = row[3];
     }
-    double X[4];
-    null4(A, X);
+    const double n0 = b[0][0] * b[0][0] + b[0][1] * b[0][1];
+    const double n1 = b[1][0] * b[1][0] + b[1][1] * b[1][1];
+    const bool first = n0 >= n1;
+    const double sc = first ? b[0][1] : b[1][1];
+    const double w = first ? -b[0][0] : -b[1][0];
+    const double X[4] = {x1 * sc, y1 * sc, sc, w};
     return calc_depth(X, Pr) > 0 && calc_depth(X, P) > 0;
 }
 
