@@ -957,9 +957,10 @@ static int null10(double A[10][10], double *v) {
     return 1;
 }
 
+/* Horner with fused multiply-adds (fma: one IEEE rounding, as v_fma_f64 on the device) */
 static double poly_eval(const double *c, int deg, double x) {
     double r = c[deg];
-    for (int i = deg - 1; i >= 0; i--) r = r * x + c[i];
+    for (int i = deg - 1; i >= 0; i--) r = fma(r, x, c[i]);
     return r;
 }
 
@@ -968,12 +969,12 @@ static double poly_eval(const double *c, int deg, double x) {
  * step when it stays strictly inside the bracket and at least halves the previous step
  * (|2f| <= |dxold f'|), else bisection; the bracket is tightened at every evaluation.  Stops
  * on an exact zero, a Newton step below 2^-50 |x| (the root to a few ulp; its end point is
- * taken when inside the bracket), an unsplittable bracket, or 200 evaluations.  p and p' by one Horner pass. */
+ * taken when inside the bracket), an unsplittable bracket, or 200 evaluations.  p and p' by one fused Horner pass. */
 static void poly_eval2(const double *c, int deg, double x, double *f, double *df) {
     double v = c[deg], d = 0.0;
     for (int j = deg - 1; j >= 0; j--) {
-        d = d * x + v;
-        v = v * x + c[j];
+        d = fma(d, x, v);
+        v = fma(v, x, c[j]);
     }
     *f = v;
     *df = d;

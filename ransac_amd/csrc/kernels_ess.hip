@@ -138,11 +138,11 @@ __global__ __launch_bounds__(64) void k_e5_roots(uint32_t B, E5Work w) {
         for (int r = 0; r < 10; r++) w.flags[(size_t)r * B + h] = 0;
         if (a[10] != 0.0) {
             double crit[10];
-            bool found[10];
+            uint32_t found;
             e5::real_roots10(a, crit, found);
 #pragma unroll
             for (int k = 0; k < 10; k++)
-                if (found[k]) {
+                if (found & (1u << k)) {
                     w.roots[(size_t)nr * B + h] = crit[k];
                     nr++;
                 }

@@ -302,17 +302,18 @@ __device__ __forceinline__ bool null10(double (&A)[10][10], double (&v)[10]) {
     return true;
 }
 
+// Horner with fused multiply-adds (oracle poly_eval / poly_eval2)
 __device__ __forceinline__ double poly_eval(const double *c, int deg, double x) {
     double r = c[deg];
-    for (int i = deg - 1; i >= 0; i--) r = r * x + c[i];
+    for (int i = deg - 1; i >= 0; i--) r = fma(r, x, c[i]);
     return r;
 }
 
 __device__ __forceinline__ void poly_eval2(const double *c, int deg, double x, double &f, double &df) {
     double v = c[deg], d = 0.0;
     for (int j = deg - 1; j >= 0; j--) {
-        d = d * x + v;
-        v = v * x + c[j];
+        d = fma(d, x, v);
+        v = fma(v, x, c[j]);
     }
     f = v;
     df = d;
@@ -406,67 +407,32 @@ __device__ __noinline__ int real_roots_dyn(const double *a, double *roots) {
 }
 
 // The same spec for a true degree-10 polynomial with every degree a compile-time constant:
-// coefficients, partition points and Horner loops all stay in registers.
+// coefficients, partition points and Horner loops all stay in registers.  Within a level
+// the sign-changing intervals are refined by ONE flat loop: each trip performs one step of
+// the lane's current interval and, when that interval is done, moves the lane on to its
+// next one -- a wave pays the max over lanes of the per-level sum of steps, not the sum
+// over intervals of the per-interval max.  Every interval's result is poly_refine's (the
+// oracle's), only the schedule differs.
 template <int G>
 __device__ __forceinline__ double poly_eval_t(const double (&c)[11], double x) {
     double r = c[G];
 #pragma unroll
-    for (int i = G - 1; i >= 0; i--) r = r * x + c[i];
+    for (int i = G - 1; i >= 0; i--) r = fma(r, x, c[i]);
+    return r;
+}
+
+// value at compile-time-unrolled index k of v[0..N) (selects on opaque values: stays in
+// registers, see opaque())
+template <int N>
+__device__ __forceinline__ double pick(const double (&v)[N], int k) {
+    double r = opaque(v[0]);
+#pragma unroll
+    for (int i = 1; i < N; i++) r = (k == i) ? opaque(v[i]) : r;
     return r;
 }
 
 template <int G>
-__device__ __forceinline__ double poly_refine_t(const double (&c)[11], double lo, double hi, double flo, double fhi) {
-    double x = lo - flo * ((hi - lo) / (fhi - flo));
-    if (!(x > lo && x < hi)) x = 0.5 * (lo + hi);
-    double dxold = hi - lo, dx = dxold, f, df;
-    {
-        double v = c[G], d = 0.0;
-#pragma unroll
-        for (int j = G - 1; j >= 0; j--) {
-            d = d * x + v;
-            v = v * x + c[j];
-        }
-        f = v;
-        df = d;
-    }
-    for (int it = 0; it < 200; it++) {
-        if (f == 0.0) return x;
-        if ((f < 0.0) == (flo < 0.0)) {
-            lo = x;
-            flo = f;
-        } else {
-            hi = x;
-        }
-        const double step = f / df;
-        const double xn = x - step;
-        const bool inside = xn > lo && xn < hi;
-        if (xn == x || fabs(step) <= 0x1p-50 * fabs(x)) return inside ? xn : x;
-        const bool newton = inside && !(fabs(2.0 * f) > fabs(dxold * df));
-        dxold = dx;
-        if (newton) {
-            dx = step;
-            x = xn;
-        } else {
-            const double mid = 0.5 * (lo + hi);
-            if (!(mid > lo && mid < hi)) return mid;
-            dx = mid - x;
-            x = mid;
-        }
-        double v = c[G], d = 0.0;
-#pragma unroll
-        for (int j = G - 1; j >= 0; j--) {
-            d = d * x + v;
-            v = v * x + c[j];
-        }
-        f = v;
-        df = d;
-    }
-    return x;
-}
-
-template <int G>
-__device__ __forceinline__ void roots_level(const double (&a)[11], double R, double (&crit)[10], bool (&found)[10]) {
+__device__ __forceinline__ void roots_level(const double (&a)[11], double R, double (&crit)[10], uint32_t &found) {
     constexpr int d = 10 - G;
     double c[11];
 #pragma unroll
@@ -476,29 +442,96 @@ __device__ __forceinline__ void roots_level(const double (&a)[11], double R, dou
         for (int m = j + d; m > j; m--) f *= (double)m;
         c[j] = a[j + d] * f;
     }
-    double next[10];
-    double lo = -R, flo = poly_eval_t<G>(c, lo);
+    // interval k = [e[k], e[k+1]]; fillers (left ends) unless refined
+    double e[G + 1], fe[G + 1], next[10];
+    e[0] = -R;
+#pragma unroll
+    for (int k = 1; k < G; k++) e[k] = crit[k - 1];
+    e[G] = R;
+#pragma unroll
+    for (int k = 0; k <= G; k++) fe[k] = poly_eval_t<G>(c, e[k]);
+    uint32_t todo = 0;
 #pragma unroll
     for (int k = 0; k < G; k++) {
-        const double hi = k < G - 1 ? crit[k] : R;
-        const double fhi = poly_eval_t<G>(c, hi);
-        if (hi > lo && ((flo < 0.0) != (fhi < 0.0))) {
-            next[k] = poly_refine_t<G>(c, lo, hi, flo, fhi);
-            found[k] = true;
-        } else {
-            next[k] = lo;
-            found[k] = false;
+        next[k] = e[k];
+        if (e[k + 1] > e[k] && ((fe[k] < 0.0) != (fe[k + 1] < 0.0))) todo |= 1u << k;
+    }
+    found = todo;
+    // per-lane refinement state of the current interval k
+    int k = 0, it = 0;
+    double lo = 0.0, hi = 0.0, flo = 0.0, x = 0.0, dxold = 0.0, dx = 0.0;
+    bool fresh = true;  // set up interval `k = lowest bit of todo` at the top of the trip
+    while (todo) {
+        if (fresh) {
+            k = __builtin_ctz(todo);
+            lo = pick(e, k);
+            hi = pick(e, k + 1);
+            flo = pick(fe, k);
+            const double fhi = pick(fe, k + 1);
+            x = lo - flo * ((hi - lo) / (fhi - flo));
+            if (!(x > lo && x < hi)) x = 0.5 * (lo + hi);
+            dxold = hi - lo;
+            dx = dxold;
+            it = 0;
+            fresh = false;
         }
-        lo = hi;
-        flo = fhi;
+        double v = c[G], dd = 0.0;
+#pragma unroll
+        for (int j = G - 1; j >= 0; j--) {
+            dd = fma(dd, x, v);
+            v = fma(v, x, c[j]);
+        }
+        const double f = v, df = dd;
+        bool done = false;
+        double res = x;
+        if (it == 200 || f == 0.0) {
+            done = true;
+        } else {
+            it++;
+            if ((f < 0.0) == (flo < 0.0)) {
+                lo = x;
+                flo = f;
+            } else {
+                hi = x;
+            }
+            const double step = f / df;
+            const double xn = x - step;
+            const bool inside = xn > lo && xn < hi;
+            if (xn == x || fabs(step) <= 0x1p-50 * fabs(x)) {
+                done = true;
+                res = inside ? xn : x;
+            } else {
+                const bool newton = inside && !(fabs(2.0 * f) > fabs(dxold * df));
+                dxold = dx;
+                if (newton) {
+                    dx = step;
+                    x = xn;
+                } else {
+                    const double mid = 0.5 * (lo + hi);
+                    if (!(mid > lo && mid < hi)) {
+                        done = true;
+                        res = mid;
+                    } else {
+                        dx = mid - x;
+                        x = mid;
+                    }
+                }
+            }
+        }
+        if (done) {
+#pragma unroll
+            for (int q = 0; q < G; q++) next[q] = (q == k) ? res : next[q];
+            todo &= todo - 1;
+            fresh = true;
+        }
     }
 #pragma unroll
-    for (int k = 0; k < G; k++) crit[k] = next[k];
+    for (int q = 0; q < G; q++) crit[q] = next[q];
     if constexpr (G < 10) roots_level<G + 1>(a, R, crit, found);
 }
 
-// a[10] != 0 required; root k (ascending) is crit[k] where found[k]
-__device__ __forceinline__ void real_roots10(const double (&a)[11], double (&crit)[10], bool (&found)[10]) {
+// a[10] != 0 required; root k (ascending) is crit[k] where bit k of found
+__device__ __forceinline__ void real_roots10(const double (&a)[11], double (&crit)[10], uint32_t &found) {
     double r = 1.0;
     const double an = fabs(a[10]);
     for (int it = 0; it < 2100; it++) {
