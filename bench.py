@@ -32,13 +32,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--estimator", choices=["homography", "fundamental", "essential"], default="homography",
                     help="homography = cfg2 (the BASELINE metric's config); fundamental = cfg3; essential = cfg4 "
-                         "(use --points 50000 --threshold 0.002)")
+                         "(50k correspondences in K^-1-normalised coordinates, threshold 0.002)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=65536)
-    ap.add_argument("--points", type=int, default=10000)
-    ap.add_argument("--threshold", type=float, default=2.0)
-    ap.add_argument("--chunks", type=int, default=8)
+    ap.add_argument("--points", type=int, default=None, help="default: 10000 (cfg2/cfg3), 50000 (cfg4)")
+    ap.add_argument("--threshold", type=float, default=None,
+                    help="default: 2.0 px (cfg2/cfg3), 0.002 (cfg4, normalised coordinates)")
+    ap.add_argument("--chunks", type=int, default=None, help="score point chunks (default 8 homography, 64 two-view)")
     ap.add_argument("--dlt", choices=["thin", "nullspace"], default="thin")
     ap.add_argument("--sprt", action="store_true",
                     help="batch SPRT verification (reference initial epsilon/delta for the estimator)")
@@ -47,7 +48,15 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=3,
                     help="batches in flight: one context (stream + buffers) per in-flight batch, so batch i+1's "
                          "solve overlaps batch i's scoring")
-    return ap.parse_args()
+    args = ap.parse_args()
+    ess = args.estimator == "essential"
+    if args.points is None:
+        args.points = 50000 if ess else 10000
+    if args.threshold is None:
+        args.threshold = 0.002 if ess else 2.0
+    if args.chunks is None:
+        args.chunks = 8 if args.estimator == "homography" else 64
+    return args
 
 
 def cpu_baseline(kind, pts, thr, dlt_mode, seconds):
@@ -255,10 +264,10 @@ def main():
             bytes_per_hyp = models_per_hyp * 16 * n + m * 4 + models_per_hyp * (36 + 8)
         avg_score_ms = float(np.mean(solo_score))
         achieved = bytes_per_hyp * B / (avg_score_ms * 1e-3) / 1e9
-        kname = ("void usac::k_score_f<%d>" if (fund or ess) else "void usac::k_score_hf<%d, false>") % args.chunks
+        kname = ("void usac::k_score_f2<%d>" if (fund or ess) else "void usac::k_score_hf<%d, false>") % args.chunks
         traffic = measured_traffic(kname, n, B) if not (fund or ess or args.sprt) else None
         kshort = ("k_sprt_head/tail<%d>" % (3 if fund else 4 if ess else 2)) if args.sprt else \
-            (("k_score_f<%d,%s>" % (args.chunks, "E" if ess else "F")) if (fund or ess) else
+            (("k_score_f2<%d,%s>" % (args.chunks, "E" if ess else "F")) if (fund or ess) else
              ("k_score_hf<%d,false>" % args.chunks))
         out = {
             "metric": "model hypotheses/sec (sample+solve+score) and inlier-count match vs ref",

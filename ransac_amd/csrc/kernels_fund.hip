@@ -171,6 +171,257 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_f(const float4 *__restric
     }
 }
 
+// ---------------------------------------------------------------- fast two-view scoring
+// Same results as k_score_f (counts and Σerr bit for bit), two points per packed VALU op:
+//
+//   stage A  the reference's own operation sequence (v_pk_mul_f32 / v_pk_add_f32 are the
+//            scalar IEEE ops element-wise, so every intermediate equals the exact path's)
+//            up to the quantities below, then a division-free test that can only reject
+//            points whose reference error is >= thr:
+//              Sampson   e = S / D:        reject if S > fl(fl(thr D) (1 + 2^-20))
+//                        (e < thr  =>  S < thr D, and the factor dominates both roundings)
+//              essential e = (|a1/a2| + |b1/b2|) / 2 with a2 = sqrt(Qa):
+//                        reject if a1^2 > fl(fl(4 thr^2 Qa) (1 + 2^-18))
+//                        (e < thr  =>  fl(|a1/a2|) < 2 thr  =>  a1^2 < 4 thr^2 Qa (1 + 2^-21))
+//            a NaN on either side rejects (the exact error is then NaN, never an inlier --
+//            this also drops the NaN-padded tail points); inf only rejects when the exact
+//            error is inf as well;
+//   stage B  the exact expression (two_view_error) on the kept pairs only, sequential
+//            accumulation per model (see the queues below).
+//
+// Points come from the fast-kernel records (k_prepare_rec: SoA groups of four, NaN-padded
+// tail -- NaN points are never inliers).
+typedef float v2f __attribute__((ext_vector_type(2)));
+
+template <int EST>
+struct TwoViewModel {
+    float f[9];
+    v2f f2[9];
+    float k;  // Sampson: thr (1 + 2^-20) applied as fl(fl(thr D) K); essential: 4 thr^2
+};
+
+// stage A for two points: true = sure outlier
+template <int EST>
+__device__ __forceinline__ void two_view_reject2(const TwoViewModel<EST> &M, float thr, v2f x1, v2f y1, v2f x2,
+                                                 v2f y2, bool &r0, bool &r1) {
+    const v2f *f = M.f2;
+    if constexpr (EST == USAC_ESSENTIAL) {
+        const v2f l1 = (f[0] * x2 + f[3] * y2) + f[6];
+        const v2f l2 = (f[1] * x2 + f[4] * y2) + f[7];
+        const v2f l3 = (f[2] * x2 + f[5] * y2) + f[8];
+        const v2f a1 = (l1 * x1 + l2 * y1) + l3;
+        const v2f Qa = l1 * l1 + l2 * l2;
+        const v2f A = a1 * a1;
+        const v2f T = (v2f{M.k, M.k} * Qa) * v2f{1.000003814697265625f, 1.000003814697265625f};  // 1 + 2^-18
+        r0 = !(A.x <= T.x);
+        r1 = !(A.y <= T.y);
+    } else {
+        const v2f Fx = (f[0] * x1 + f[1] * y1) + f[2];
+        const v2f Fy = (f[3] * x1 + f[4] * y1) + f[5];
+        const v2f Gx = (f[0] * x2 + f[3] * y2) + f[6];
+        const v2f Gy = (f[1] * x2 + f[4] * y2) + f[7];
+        const v2f sv = (((x2 * Fx + y2 * Fy) + f[6] * x1) + f[7] * y1) + f[8];
+        const v2f S = sv * sv;
+        const v2f D = ((Fx * Fx + Fy * Fy) + Gx * Gx) + Gy * Gy;
+        const v2f T = (v2f{thr, thr} * D) * v2f{1.00000095367431640625f, 1.00000095367431640625f};  // 1 + 2^-20
+        r0 = !(S.x <= T.x);
+        r1 = !(S.y <= T.y);
+    }
+}
+
+// Stage B is deferred: a lane appends the index of every point its model kept to a private
+// LDS queue (in point order); when some lane's queue is nearly full -- and at the end -- the
+// wave drains all queues together, entry t of every lane per trip, each lane evaluating the
+// exact expression on its own kept points in order (sequential Σ, bit-exact).  Stage A keeps
+// ~1 % of the (model, point) pairs on typical data, so a per-group "any lane kept a point"
+// branch would run the exact path nearly always; the queues run it only for kept pairs, at
+// the cost of idle lanes in the drain (avg / max queue length).
+constexpr int kTvQueue = 16;  // entries per lane (4 KB of LDS per wave)
+
+template <int EST>
+__device__ __forceinline__ void two_view_drain(const TwoViewModel<EST> &M, const float4 *__restrict__ pts,
+                                               const uint32_t *q, int &len, float thr, int &cnt, float &sum) {
+    for (int t = 0; __builtin_amdgcn_ballot_w64(t < len); t++) {
+        if (t < len) {
+            const float4 p = pts[q[t * 64]];
+            const float e = two_view_error<EST>(M.f, p.x, p.y, p.z, p.w);
+            if (e < thr) {
+                cnt++;
+                sum += e;
+            }
+        }
+    }
+    len = 0;
+}
+
+template <int EST>
+__device__ __forceinline__ void two_view_group(const TwoViewModel<EST> &M, float4 X1, float4 Y1, float4 X2,
+                                               float4 Y2, uint32_t base, uint32_t n, float thr, uint32_t *q,
+                                               int &len) {
+    bool r0, r1, r2, r3;
+    two_view_reject2<EST>(M, thr, v2f{X1.x, X1.y}, v2f{Y1.x, Y1.y}, v2f{X2.x, X2.y}, v2f{Y2.x, Y2.y}, r0, r1);
+    two_view_reject2<EST>(M, thr, v2f{X1.z, X1.w}, v2f{Y1.z, Y1.w}, v2f{X2.z, X2.w}, v2f{Y2.z, Y2.w}, r2, r3);
+    // branch-free append: the slot at len is always written, len advances only for a kept
+    // point (the caller keeps len <= kTvQueue - 8 before every 8 appends)
+    q[64 * len] = base + 0;
+    len += r0 ? 0 : 1;
+    q[64 * len] = base + 1;
+    len += r1 ? 0 : 1;
+    q[64 * len] = base + 2;
+    len += r2 ? 0 : 1;
+    q[64 * len] = base + 3;
+    len += r3 ? 0 : 1;
+}
+
+// One wave per workgroup: blockIdx.x = 64 listed models, blockIdx.y = point chunk.  With
+// one chunk the wave writes (count, Σ) at the slots; with C > 1 it writes its partials at
+// [chunk][list position] and k_tv_combine adds them in chunk order (deterministic).  Small
+// workgroups spread the few model tiles of a two-view batch evenly over the 256 CUs.
+template <int EST>
+__global__ __launch_bounds__(64) void k_score_f2(const float4 *__restrict__ rec, const float4 *__restrict__ pts,
+                                                 uint32_t n, const float *__restrict__ models, size_t stride,
+                                                 const uint32_t *__restrict__ list,
+                                                 const uint32_t *__restrict__ list_n, uint32_t kmax, float thr,
+                                                 const uint32_t *__restrict__ perm,
+                                                 int32_t *__restrict__ counts, float *__restrict__ sums,
+                                                 int32_t *__restrict__ part_cnt, float *__restrict__ part_sum) {
+    __shared__ uint32_t s_q[kTvQueue * 64];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t chunk = blockIdx.y, C = gridDim.y;
+    const uint32_t K = list ? __builtin_amdgcn_readfirstlane(*list_n) : kmax;
+    const uint32_t i0 = blockIdx.x * 64;
+    if (i0 >= K) return;  // block-uniform
+    const uint32_t j = i0 + lane < K ? i0 + lane : K - 1;
+    const uint32_t ic = perm ? perm[j] : j;  // list position scored by this lane
+    const bool live = i0 + lane < K;
+    const uint32_t slot = list ? list[ic] : ic;
+    TwoViewModel<EST> M;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        M.f[k] = models[(size_t)k * stride + slot];
+        M.f2[k] = v2f{M.f[k], M.f[k]};
+    }
+    M.k = EST == USAC_ESSENTIAL ? (4.0f * thr) * thr : thr;
+    const uint32_t ngroups = (n + 3) / 4;
+    const uint32_t per = (ngroups + C - 1) / C;
+    const uint32_t gbeg = chunk * per < ngroups ? chunk * per : ngroups;
+    const uint32_t gend = gbeg + per < ngroups ? gbeg + per : ngroups;
+    uint32_t *q = &s_q[lane];
+    int len = 0, cnt = 0;
+    float sum = 0.f;
+    uint32_t g = gbeg;
+    if (g + 2 <= gend) {
+        // software-pipelined scalar loads: the next two groups are in flight while the
+        // current two are evaluated
+        const float4 *p = rec + 8 * (size_t)g;
+        float4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3];
+        float4 b0 = p[8], b1 = p[9], b2 = p[10], b3 = p[11];
+        for (; g + 2 <= gend; g += 2) {
+            const uint32_t gn = g + 4 <= gend ? g + 2 : g;
+            const float4 *pn = rec + 8 * (size_t)gn;
+            const float4 c0 = pn[0], c1 = pn[1], c2 = pn[2], c3 = pn[3];
+            const float4 d0 = pn[8], d1 = pn[9], d2 = pn[10], d3 = pn[11];
+            two_view_group<EST>(M, a0, a1, a2, a3, 4 * g, n, thr, q, len);
+            two_view_group<EST>(M, b0, b1, b2, b3, 4 * g + 4, n, thr, q, len);
+            if (__builtin_amdgcn_ballot_w64(len > kTvQueue - 8)) two_view_drain<EST>(M, pts, q, len, thr, cnt, sum);
+            a0 = c0; a1 = c1; a2 = c2; a3 = c3;
+            b0 = d0; b1 = d1; b2 = d2; b3 = d3;
+        }
+    }
+    if (g < gend) {
+        const float4 *p = rec + 8 * (size_t)g;
+        two_view_group<EST>(M, p[0], p[1], p[2], p[3], 4 * g, n, thr, q, len);
+    }
+    two_view_drain<EST>(M, pts, q, len, thr, cnt, sum);
+    if (!live) return;
+    if (C == 1) {
+        counts[slot] = cnt;
+        sums[slot] = sum;
+    } else {
+        part_cnt[(size_t)chunk * kmax + ic] = cnt;
+        part_sum[(size_t)chunk * kmax + ic] = sum;
+    }
+}
+
+// Model pre-sort for k_score_f2: stage-A keeps of every listed model on the first
+// kTvPresortGroups point groups (the exact stage-A test -- a heuristic only for WHERE a model
+// is scored, never for its result).  Models with >= kTvPresortKeeps keeps (those with many
+// inliers, whose queues fill fast) go to the front of perm, the rest to the back, so the
+// costly drains concentrate in few waves instead of one slow lane per wave.
+constexpr uint32_t kTvPresortGroups = 32;  // 128 points
+constexpr int kTvPresortKeeps = 8;
+
+template <int EST>
+__global__ __launch_bounds__(64) void k_presort_tv(const float4 *__restrict__ rec, uint32_t n,
+                                                   const float *__restrict__ models, size_t stride,
+                                                   const uint32_t *__restrict__ list,
+                                                   const uint32_t *__restrict__ list_n, uint32_t kmax, float thr,
+                                                   uint32_t *__restrict__ perm, uint32_t *__restrict__ ends) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t K = list ? __builtin_amdgcn_readfirstlane(*list_n) : kmax;
+    const uint32_t i0 = blockIdx.x * 64;
+    if (i0 >= K) return;
+    const uint32_t i = i0 + lane;
+    const uint32_t ic = i < K ? i : K - 1;
+    const uint32_t slot = list ? list[ic] : ic;
+    TwoViewModel<EST> M;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        M.f[k] = models[(size_t)k * stride + slot];
+        M.f2[k] = v2f{M.f[k], M.f[k]};
+    }
+    M.k = EST == USAC_ESSENTIAL ? (4.0f * thr) * thr : thr;
+    const uint32_t ngroups = (n + 3) / 4;
+    const uint32_t g1 = ngroups < kTvPresortGroups ? ngroups : kTvPresortGroups;
+    int keeps = 0;
+    for (uint32_t g = 0; g < g1; g++) {
+        const float4 *p = rec + 8 * (size_t)g;
+        const float4 X1 = p[0], Y1 = p[1], X2 = p[2], Y2 = p[3];
+        bool r0, r1, r2, r3;
+        two_view_reject2<EST>(M, thr, v2f{X1.x, X1.y}, v2f{Y1.x, Y1.y}, v2f{X2.x, X2.y}, v2f{Y2.x, Y2.y}, r0, r1);
+        two_view_reject2<EST>(M, thr, v2f{X1.z, X1.w}, v2f{Y1.z, Y1.w}, v2f{X2.z, X2.w}, v2f{Y2.z, Y2.w}, r2, r3);
+        keeps += (r0 ? 0 : 1) + (r1 ? 0 : 1) + (r2 ? 0 : 1) + (r3 ? 0 : 1);
+    }
+    const bool valid = i < K;
+    const bool heavy = valid && keeps >= kTvPresortKeeps;
+    const uint64_t bh = __ballot(heavy), bl = __ballot(valid && !heavy);
+    const uint64_t below_mask = (1ull << lane) - 1;
+    const uint32_t below = (uint32_t)__popcll((heavy ? bh : bl) & below_mask);
+    uint32_t hbase = 0, lbase = 0;
+    if (lane == 0) {
+        if (bh) hbase = atomicAdd(&ends[0], (uint32_t)__popcll(bh));
+        if (bl) lbase = atomicAdd(&ends[1], (uint32_t)__popcll(bl));
+    }
+    hbase = __shfl(hbase, 0, 64);
+    lbase = __shfl(lbase, 0, 64);
+    if (valid) perm[heavy ? hbase + below : K - 1 - (lbase + below)] = i;
+}
+
+// (count, Σ) of listed model i = chunk partials added in chunk order
+__global__ __launch_bounds__(256) void k_tv_combine(const uint32_t *__restrict__ list,
+                                                    const uint32_t *__restrict__ list_n, uint32_t kmax, uint32_t C,
+                                                    const int32_t *__restrict__ part_cnt,
+                                                    const float *__restrict__ part_sum, int32_t *__restrict__ counts,
+                                                    float *__restrict__ sums) {
+    const uint32_t K = list ? *list_n : kmax;
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= K) return;
+    int c = part_cnt[i];
+    float s = part_sum[i];
+    for (uint32_t j = 1; j < C; j++) {
+        c += part_cnt[(size_t)j * kmax + i];
+        s += part_sum[(size_t)j * kmax + i];
+    }
+    const uint32_t slot = list ? list[i] : i;
+    counts[slot] = c;
+    sums[slot] = s;
+}
+
+size_t tv_scratch_bytes(uint32_t kmax, int chunks) {
+    return 256 + sizeof(uint32_t) * (((size_t)kmax + 63) & ~(size_t)63) +
+           (chunks > 1 ? (sizeof(int32_t) + sizeof(float)) * (size_t)chunks * kmax : 0);
+}
+
 hipError_t launch_solve_f7(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
                            int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, float *models,
                            int32_t *counts, uint32_t *list, uint32_t *list_n) {
@@ -205,4 +456,41 @@ hipError_t launch_score_f(hipStream_t st, int estimator, int chunks, const float
     return hipGetLastError();
 }
 
+}  // namespace usac
+
+namespace usac {
+hipError_t launch_score_f2(hipStream_t st, int estimator, int chunks, const float4 *rec, const float4 *pts,
+                           uint32_t n, const float *models, size_t stride, const uint32_t *list, const uint32_t *list_n,
+                           uint32_t kmax, float thr, int32_t *counts, float *sums, void *scratch) {
+    if (chunks < 1 || chunks > 128 || !scratch) return hipErrorInvalidValue;
+    // scratch: ends[2] (padded to 256 B), perm[kmax], then the chunk partials
+    uint32_t *ends = static_cast<uint32_t *>(scratch);
+    uint32_t *perm = ends + 64;
+    int32_t *pc = reinterpret_cast<int32_t *>(perm + (((size_t)kmax + 63) & ~(size_t)63));
+    float *ps = reinterpret_cast<float *>(pc + (size_t)chunks * kmax);
+    hipError_t e = hipMemsetAsync(ends, 0, 2 * sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    const bool ess = estimator == USAC_ESSENTIAL;
+    const dim3 pgrid((kmax + 63) / 64);
+    if (ess)
+        hipLaunchKernelGGL((k_presort_tv<USAC_ESSENTIAL>), pgrid, dim3(64), 0, st, rec, n, models, stride, list,
+                           list_n, kmax, thr, perm, ends);
+    else
+        hipLaunchKernelGGL((k_presort_tv<USAC_FUNDAMENTAL>), pgrid, dim3(64), 0, st, rec, n, models, stride, list,
+                           list_n, kmax, thr, perm, ends);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const dim3 grid((kmax + 63) / 64, chunks);
+    if (ess)
+        hipLaunchKernelGGL((k_score_f2<USAC_ESSENTIAL>), grid, dim3(64), 0, st, rec, pts, n, models, stride, list,
+                           list_n, kmax, thr, perm, counts, sums, pc, ps);
+    else
+        hipLaunchKernelGGL((k_score_f2<USAC_FUNDAMENTAL>), grid, dim3(64), 0, st, rec, pts, n, models, stride, list,
+                           list_n, kmax, thr, perm, counts, sums, pc, ps);
+    e = hipGetLastError();
+    if (e != hipSuccess || chunks == 1) return e;
+    hipLaunchKernelGGL(k_tv_combine, dim3((kmax + 255) / 256), dim3(256), 0, st, list, list_n, kmax,
+                       (uint32_t)chunks, pc, ps, counts, sums);
+    return hipGetLastError();
+}
 }  // namespace usac

@@ -57,6 +57,7 @@ struct usac_ctx {
     hipStream_t stream = nullptr;
     DevBuf pts;
     DevBuf rec;             // fast-kernel point records (32 B / point)
+    DevBuf tv_part;         // two-view scorer scratch: pre-sort permutation, chunk partials
     DevBuf perm;            // hypothesis pre-sort order of the fast kernel (B + 2 uint32)
     float rec_thr = -1.f;   // threshold the record bands were built for
     float4 ext = {0, 0, 0, 0};  // dataset box: max |x1|, |y1|, |x2|, |y2| (fast-kernel bounds)
@@ -181,21 +182,30 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
                                        c->sprt_log_down, c->sprt_log_A, c->counts.as<int32_t>(), c->sums.as<float>(),
                                        c->sprt_tested.as<uint32_t>(), c->sprt_surv.p, c->sprt_surv_n.as<uint32_t>());
     }
-    if (listed(c))  // the occupied slots of the last solve
-        return usac::launch_score_f(c->stream, c->estimator, chunks, c->pts.as<float4>(), c->n, c->models.as<float>(),
-                                    (size_t)B * c->spk, c->list.as<uint32_t>(), c->list_n.as<uint32_t>(), B * c->spk,
-                                    thr, c->counts.as<int32_t>(), c->sums.as<float>());
+    if ((listed(c) || is_h(c)) && c->score_variant != 1 && c->rec_thr != thr) {  // fast-kernel point records
+        hipError_t e = c->rec.reserve(sizeof(float) * 32 * (((size_t)c->n + 3) / 4));
+        if (e != hipSuccess) return e;
+        e = usac::launch_prepare_rec(c->stream, c->pts.as<float4>(), c->n, thr, c->rec.as<float4>());
+        if (e != hipSuccess) return e;
+        c->rec_thr = thr;
+    }
+    if (listed(c)) {  // the occupied slots of the last solve
+        if (c->score_variant == 1)
+            return usac::launch_score_f(c->stream, c->estimator, chunks, c->pts.as<float4>(), c->n,
+                                        c->models.as<float>(), (size_t)B * c->spk, c->list.as<uint32_t>(),
+                                        c->list_n.as<uint32_t>(), B * c->spk, thr, c->counts.as<int32_t>(),
+                                        c->sums.as<float>());
+        hipError_t e = c->tv_part.reserve(usac::tv_scratch_bytes(B * c->spk, chunks));
+        if (e != hipSuccess) return e;
+        return usac::launch_score_f2(c->stream, c->estimator, chunks, c->rec.as<float4>(), c->pts.as<float4>(), c->n,
+                                     c->models.as<float>(),
+                                     (size_t)B * c->spk, c->list.as<uint32_t>(), c->list_n.as<uint32_t>(), B * c->spk,
+                                     thr, c->counts.as<int32_t>(), c->sums.as<float>(), c->tv_part.p);
+    }
     if (is_h(c)) {
         if (c->score_variant == 1)
             return usac::launch_score_h(c->stream, chunks, c->pts.as<float4>(), c->n, c->models.as<float>(), B, thr,
                                         c->counts.as<int32_t>(), c->sums.as<float>());
-        if (c->rec_thr != thr) {
-            hipError_t e = c->rec.reserve(sizeof(float) * 32 * (((size_t)c->n + 3) / 4));
-            if (e != hipSuccess) return e;
-            e = usac::launch_prepare_rec(c->stream, c->pts.as<float4>(), c->n, thr, c->rec.as<float4>());
-            if (e != hipSuccess) return e;
-            c->rec_thr = thr;
-        }
         uint32_t *perm = nullptr;
         if (c->score_variant == 0) {  // 2: fast kernel without the hypothesis pre-sort (A/B)
             hipError_t e = c->perm.reserve(sizeof(uint32_t) * ((size_t)B + 2));
@@ -378,6 +388,9 @@ int usac_create(usac_ctx **out, int device, int estimator, const float *pts, uin
     c->cols = cols;
     c->m = estimator == USAC_LINE2D ? 2 : estimator == USAC_FUNDAMENTAL ? 7 : estimator == USAC_ESSENTIAL ? 5 : 4;
     c->spk = estimator == USAC_FUNDAMENTAL ? 3 : 1;
+    // two-view scoring: a batch yields few models (about 0.4-1.3 per sample) and the few with
+    // many inliers are much slower to score, so their point ranges are cut finer
+    if (estimator == USAC_FUNDAMENTAL || estimator == USAC_ESSENTIAL) c->chunks = 64;
     int rc = USAC_OK;
     do {
         hipError_t e = hipSetDevice(device);
@@ -423,7 +436,7 @@ void usac_destroy(usac_ctx *c) {
                       &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
                       &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->inl_scratch, &c->lo_idx, &c->e5_ws, &c->one_model,
                       &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok,
-                      &c->rec_send, &c->rec_all})
+                      &c->rec_send, &c->rec_all, &c->tv_part})
         b->release();
     for (auto &ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -440,7 +453,9 @@ int usac_set_dlt_mode(usac_ctx *c, int mode) {
 }
 
 int usac_set_score_chunks(usac_ctx *c, int chunks) {
-    if (!c || (chunks != 1 && chunks != 2 && chunks != 4 && chunks != 8)) return USAC_ERR_ARG;
+    if (!c) return USAC_ERR_ARG;
+    const bool ok = listed(c) ? (chunks >= 1 && chunks <= 128) : (chunks == 1 || chunks == 2 || chunks == 4 || chunks == 8);
+    if (!ok) return USAC_ERR_ARG;
     c->chunks = chunks;
     return USAC_OK;
 }
