@@ -229,48 +229,50 @@ __device__ __forceinline__ void two_view_reject2(const TwoViewModel<EST> &M, flo
     }
 }
 
-// Stage B is deferred: a lane appends the index of every point its model kept to a private
-// LDS queue (in point order); when some lane's queue is nearly full -- and at the end -- the
-// wave drains all queues together, entry t of every lane per trip, each lane evaluating the
-// exact expression on its own kept points in order (sequential Σ, bit-exact).  Stage A keeps
+// Stage B is deferred: per eight points (two groups) a lane appends one entry -- the group
+// index and an 8-bit mask of the points its model kept -- to a private LDS queue, only when
+// the mask is not empty.  When some lane's queue is full, and at the end, the wave drains
+// all queues together, entry t of every lane per trip, each lane evaluating the exact
+// expression on its own kept points in point order (sequential Σ, bit-exact).  Stage A keeps
 // ~1 % of the (model, point) pairs on typical data, so a per-group "any lane kept a point"
-// branch would run the exact path nearly always; the queues run it only for kept pairs, at
-// the cost of idle lanes in the drain (avg / max queue length).
+// branch would run the exact path nearly always; the queues run it only for kept pairs.
 constexpr int kTvQueue = 16;  // entries per lane (4 KB of LDS per wave)
 
 template <int EST>
 __device__ __forceinline__ void two_view_drain(const TwoViewModel<EST> &M, const float4 *__restrict__ pts,
                                                const uint32_t *q, int &len, float thr, int &cnt, float &sum) {
     for (int t = 0; __builtin_amdgcn_ballot_w64(t < len); t++) {
-        if (t < len) {
-            const float4 p = pts[q[t * 64]];
-            const float e = two_view_error<EST>(M.f, p.x, p.y, p.z, p.w);
-            if (e < thr) {
+        const uint32_t e = t < len ? q[t * 64] : 0u;
+        const uint32_t base = (e >> 8) * 4;
+        uint32_t m = e & 255u;
+        while (m) {
+            const uint32_t b = __builtin_ctz(m);
+            m &= m - 1;
+            const float4 p = pts[base + b];
+            const float err = two_view_error<EST>(M.f, p.x, p.y, p.z, p.w);
+            if (err < thr) {
                 cnt++;
-                sum += e;
+                sum += err;
             }
         }
     }
     len = 0;
 }
 
+// stage A of four points -> 4-bit mask of the kept ones
 template <int EST>
-__device__ __forceinline__ void two_view_group(const TwoViewModel<EST> &M, float4 X1, float4 Y1, float4 X2,
-                                               float4 Y2, uint32_t base, uint32_t n, float thr, uint32_t *q,
-                                               int &len) {
+__device__ __forceinline__ uint32_t two_view_group(const TwoViewModel<EST> &M, float4 X1, float4 Y1, float4 X2,
+                                                   float4 Y2, float thr) {
     bool r0, r1, r2, r3;
     two_view_reject2<EST>(M, thr, v2f{X1.x, X1.y}, v2f{Y1.x, Y1.y}, v2f{X2.x, X2.y}, v2f{Y2.x, Y2.y}, r0, r1);
     two_view_reject2<EST>(M, thr, v2f{X1.z, X1.w}, v2f{Y1.z, Y1.w}, v2f{X2.z, X2.w}, v2f{Y2.z, Y2.w}, r2, r3);
-    // branch-free append: the slot at len is always written, len advances only for a kept
-    // point (the caller keeps len <= kTvQueue - 8 before every 8 appends)
-    q[64 * len] = base + 0;
-    len += r0 ? 0 : 1;
-    q[64 * len] = base + 1;
-    len += r1 ? 0 : 1;
-    q[64 * len] = base + 2;
-    len += r2 ? 0 : 1;
-    q[64 * len] = base + 3;
-    len += r3 ? 0 : 1;
+    return (r0 ? 0u : 1u) | (r1 ? 0u : 2u) | (r2 ? 0u : 4u) | (r3 ? 0u : 8u);
+}
+
+// append (g, mask) when the mask is not empty (the slot is written either way)
+__device__ __forceinline__ void two_view_append(uint32_t *q, int &len, uint32_t g, uint32_t mask) {
+    q[64 * len] = (g << 8) | mask;
+    len += mask ? 1 : 0;
 }
 
 // One wave per workgroup: blockIdx.x = 64 listed models, blockIdx.y = point chunk.  With
@@ -321,16 +323,17 @@ __global__ __launch_bounds__(64) void k_score_f2(const float4 *__restrict__ rec,
             const float4 *pn = rec + 8 * (size_t)gn;
             const float4 c0 = pn[0], c1 = pn[1], c2 = pn[2], c3 = pn[3];
             const float4 d0 = pn[8], d1 = pn[9], d2 = pn[10], d3 = pn[11];
-            two_view_group<EST>(M, a0, a1, a2, a3, 4 * g, n, thr, q, len);
-            two_view_group<EST>(M, b0, b1, b2, b3, 4 * g + 4, n, thr, q, len);
-            if (__builtin_amdgcn_ballot_w64(len > kTvQueue - 8)) two_view_drain<EST>(M, pts, q, len, thr, cnt, sum);
+            const uint32_t ma = two_view_group<EST>(M, a0, a1, a2, a3, thr);
+            const uint32_t mb = two_view_group<EST>(M, b0, b1, b2, b3, thr);
+            two_view_append(q, len, g, ma | (mb << 4));
+            if (__builtin_amdgcn_ballot_w64(len == kTvQueue)) two_view_drain<EST>(M, pts, q, len, thr, cnt, sum);
             a0 = c0; a1 = c1; a2 = c2; a3 = c3;
             b0 = d0; b1 = d1; b2 = d2; b3 = d3;
         }
     }
     if (g < gend) {
         const float4 *p = rec + 8 * (size_t)g;
-        two_view_group<EST>(M, p[0], p[1], p[2], p[3], 4 * g, n, thr, q, len);
+        two_view_append(q, len, g, two_view_group<EST>(M, p[0], p[1], p[2], p[3], thr));
     }
     two_view_drain<EST>(M, pts, q, len, thr, cnt, sum);
     if (!live) return;
@@ -376,11 +379,7 @@ __global__ __launch_bounds__(64) void k_presort_tv(const float4 *__restrict__ re
     int keeps = 0;
     for (uint32_t g = 0; g < g1; g++) {
         const float4 *p = rec + 8 * (size_t)g;
-        const float4 X1 = p[0], Y1 = p[1], X2 = p[2], Y2 = p[3];
-        bool r0, r1, r2, r3;
-        two_view_reject2<EST>(M, thr, v2f{X1.x, X1.y}, v2f{Y1.x, Y1.y}, v2f{X2.x, X2.y}, v2f{Y2.x, Y2.y}, r0, r1);
-        two_view_reject2<EST>(M, thr, v2f{X1.z, X1.w}, v2f{Y1.z, Y1.w}, v2f{X2.z, X2.w}, v2f{Y2.z, Y2.w}, r2, r3);
-        keeps += (r0 ? 0 : 1) + (r1 ? 0 : 1) + (r2 ? 0 : 1) + (r3 ? 0 : 1);
+        keeps += __builtin_popcount(two_view_group<EST>(M, p[0], p[1], p[2], p[3], thr));
     }
     const bool valid = i < K;
     const bool heavy = valid && keeps >= kTvPresortKeeps;
