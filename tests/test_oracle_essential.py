@@ -34,6 +34,23 @@ def test_real_roots_match_numpy(oracle):
     np.testing.assert_allclose(got, [-2.0, 1.0], atol=1e-9)
 
 
+def test_real_roots_wide_range(oracle):
+    """Roots spread over six decades, both signs: none lost, full precision (the root
+    bound, filler partition points and safeguarded Newton of the spec)."""
+    rng = np.random.default_rng(1)
+    worst, tested = 0.0, 0
+    for _ in range(800):
+        k = int(rng.integers(2, 11))
+        roots = np.sort(rng.choice([-1.0, 1.0], k) * 10 ** rng.uniform(-3, 3, k))
+        if np.min(np.diff(roots) / np.maximum(1.0, np.abs(roots[1:]))) < 1e-3:
+            continue
+        got = oracle.real_roots(np.poly(roots)[::-1])
+        assert len(got) == len(roots)
+        worst = max(worst, float(np.max(np.abs(got - roots) / np.maximum(np.abs(roots), 1e-3))))
+        tested += 1
+    assert tested > 600 and worst < 1e-10
+
+
 def test_essential_error_closed_form(oracle):
     pts, E, inl = synthetic.fundamental_points(n=500, inlier_ratio=0.5, seed=2, normalized=True)
     est = oracle.Estimator(oracle.ESSENTIAL, pts)
