@@ -45,13 +45,17 @@ def parse():
                     help="batch SPRT verification (reference initial epsilon/delta for the estimator)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--cfg5", action="store_true",
+                    help="BASELINE configs[4]: full USAC runs (homography + NAPSAC grid sampler + LO-RANSAC) "
+                         "over 100k correspondences; one step = one run, value = main-loop hypotheses/s")
+    ap.add_argument("--lo", type=int, default=1, help="cfg5 LO variant: 1 InItLORsc (unlimited), 2 InItFLORsc")
     ap.add_argument("--pipeline", type=int, default=3,
                     help="batches in flight: one context (stream + buffers) per in-flight batch, so batch i+1's "
                          "solve overlaps batch i's scoring")
     args = ap.parse_args()
     ess = args.estimator == "essential"
     if args.points is None:
-        args.points = 50000 if ess else 10000
+        args.points = 100000 if args.cfg5 else 50000 if ess else 10000
     if args.threshold is None:
         args.threshold = 0.002 if ess else 2.0
     if args.chunks is None:
@@ -143,6 +147,107 @@ def usac_device():
     return _DEV
 
 
+def cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank):
+    """Full-run mode (BASELINE configs[4]): each rank runs whole USAC loops -- batched device
+    solve + score of the NAPSAC samples, exact host replay of the sequential loop, LO-RANSAC
+    (every LSQ fit and inlier scan on the device) -- on its own seeds (replicas, weak scaling).
+    value = main-loop hypotheses of all ranks / max wall time."""
+    from oracle import oracle as O
+
+    pts, _, _ = synthetic.homography_points(n=args.points, inlier_ratio=0.2, seed=args.seed, cluster=(500, 500, 150))
+    max_iters = 5000
+
+    def model(seed):
+        mdl = usac.Model(args.threshold, 4, 0.95, 7, usac.ESTIMATOR.Homography, usac.SAMPLER.Napsac)
+        mdl.ResetRandomGenerator(False)
+        mdl.setSeed(seed)
+        mdl.lo = usac.LocOpt(args.lo)
+        mdl.max_iterations = max_iters
+        mdl.setNeighborsType(usac.NeighborsSearch.Grid)
+        return mdl
+
+    def one_run(seed):
+        r = usac.Ransac(model(seed), pts)
+        r.run()
+        return r.getRansacOutput()
+
+    for i in range(args.warmup):
+        one_run(10_000 + i)
+    if world > 1:
+        dist.barrier()
+    iters = 0
+    t0 = time.perf_counter()
+    for step in range(args.steps):
+        iters += one_run(args.seed + step * world + rank).getNumberOfMainIterations()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed, float(iters)], dtype=torch.float64)
+        dist.all_reduce(tt[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
+        elapsed, iters = float(tt[0]), int(tt[1])
+    if rank != 0:
+        return
+    # roofline of the dominant loop kernel: the score of one batch of B hypotheses at N = 100k
+    B = args.batch
+    with usac.Context(usac.ESTIMATOR.Homography, pts, device=local_rank) as ctx:
+        ctx.set_score_chunks(8)
+        for i in range(3):
+            ctx.hypothesize_async(B, args.seed, i * B, args.threshold)
+            ctx.fetch_best()
+        sc = []
+        for i in range(10):
+            ctx.hypothesize_async(B, args.seed, (3 + i) * B, args.threshold)
+            ctx.fetch_best()
+            sc.append(ctx.last_timings()["score_ms"])
+    n = args.points
+    bytes_per_hyp = 16.0 * n + 16 + 44
+    score_ms = float(np.mean(sc))
+    achieved = bytes_per_hyp * B / (score_ms * 1e-3) / 1e9
+    # parity: one run against the oracle (same seed): iterations, LO counters, model, inliers
+    out = one_run(args.seed)
+    ref = O.ransac_run(O.HOMOGRAPHY, pts, args.threshold, 0.95, args.seed, sampler=O.SAMPLER_NAPSAC, sprt=False,
+                       lo=args.lo, max_iters=max_iters)
+    parity = {"runs": 1, "iterations_equal": out.getNumberOfMainIterations() == ref["iters"],
+              "lo_iters_equal": out.getLOIters() == ref["lo_inner_iters"],
+              "model_bit_equal": bool((np.asarray(out.getModel(), np.float32).view(np.int32) ==
+                                       np.asarray(ref["model"], np.float32).view(np.int32)).all()),
+              "inliers_equal": bool(np.array_equal(out.getInliers(), ref["inlier_idx"]))}
+    line = {
+        "metric": "model hypotheses/sec (sample+solve+score) and inlier-count match vs ref",
+        "value": iters / elapsed, "unit": "hypotheses/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (clustered homography inliers 20%%, uniform outliers), %d correspondences" % n,
+        "config": {"workload": "cfg5: Homography_estimator + Napsac_sampler (grid) + LO-RANSAC (%s), full runs, "
+                               "%d correspondences; one step = one run per rank" %
+                               ("InItLORsc" if args.lo == 1 else "InItFLORsc", n),
+                   "n_points": n, "threshold": args.threshold, "max_iterations": max_iters,
+                   "hypotheses_per_gpu": iters / world, "parallelism": "replicas x%d" % world},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_score_hf<8,false>",
+                     "kernel_ms": score_ms, "hypotheses_per_launch": B,
+                     "algorithmic_bytes_per_hypothesis": bytes_per_hyp,
+                     "note": "score kernel of one %d-hypothesis batch at N = %d (the loop's batched verify); a run "
+                             "is dominated by LO and the host replay, see DESIGN.md" % (B, n)},
+        "parity": parity,
+    }
+    if args.cpu_seconds > 0:
+        t1 = time.perf_counter()
+        runs, it = 0, 0
+        while runs == 0 or time.perf_counter() - t1 < args.cpu_seconds:
+            r = O.ransac_run(O.HOMOGRAPHY, pts, args.threshold, 0.95, args.seed + 1000 + runs, sampler=O.SAMPLER_NAPSAC,
+                             sprt=False, lo=args.lo, max_iters=max_iters)
+            it += r["iters"]
+            runs += 1
+        dt = time.perf_counter() - t1
+        line["cpu_baseline"] = {"value": it / dt, "unit": "hypotheses/s", "cores": 1, "kind": "port",
+                                "sample": "%d full runs (%d hypotheses, NAPSAC + LO, N=%d), %.1f s on 1 core of %s" %
+                                          (runs, it, n, dt, platform.processor() or platform.machine())}
+    print(json.dumps(line))
+
+
 def main():
     global _DEV
     args = parse()
@@ -158,6 +263,8 @@ def main():
 
     if world > 1:
         dist.init_process_group("gloo")
+    if args.cfg5:
+        return cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank)
     fund = args.estimator == "fundamental"
     ess = args.estimator == "essential"
     if fund or ess:

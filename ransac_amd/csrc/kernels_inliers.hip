@@ -7,7 +7,7 @@
 //   k_inl_flags   grid over points: exact residual, per-block inlier count      (parallel)
 //   k_inl_scan    one workgroup: exclusive scan of the block counts -> offsets  (tiny)
 //   k_inl_compact grid over points: ordered compaction of indices and residuals (parallel)
-//   k_inl_sum     one wave: the sequential fp32 sum over the compacted residuals
+//   k_inl_sum     one workgroup: the sequential fp32 sum over the compacted residuals
 //                 (the only inherently serial part: one dependent add per inlier)
 #include <hip/hip_runtime.h>
 
@@ -123,22 +123,46 @@ __global__ __launch_bounds__(kInlBlock) void k_inl_compact(const void *__restric
 
 // sequential fp32 sum in point order (quality.hpp:85), one wave: 64 residuals per step are
 // loaded in parallel and added one after the other through v_readlane (no LDS round trip)
-__global__ __launch_bounds__(64) void k_inl_sum(const float *__restrict__ errs, const int32_t *__restrict__ total,
-                                                float *__restrict__ sum) {
-    const int32_t n = *total;
+// 256 threads stage 4096-residual chunks in LDS with coalesced loads; lane 0 adds them in
+// order (the reference's sequential fp32 sum, one dependent add per inlier)
+constexpr uint32_t kSumChunk = 4096;
+
+__global__ __launch_bounds__(256) void k_inl_sum(const float *__restrict__ errs, const int32_t *__restrict__ total,
+                                                 float *__restrict__ sum) {
+    __shared__ __attribute__((aligned(16))) float s_e[kSumChunk];
+    const uint32_t n = (uint32_t)*total;
+    const uint32_t t = threadIdx.x;
     float s = 0.f;
-    int32_t b = 0;
-    for (; b + 64 <= n; b += 64) {
-        const int v = __float_as_int(errs[b + (int32_t)threadIdx.x]);
-#pragma unroll
-        for (int k = 0; k < 64; k++) s += __int_as_float(__builtin_amdgcn_readlane(v, k));
+    for (uint32_t c0 = 0; c0 < n; c0 += kSumChunk) {
+        const uint32_t m = n - c0 < kSumChunk ? n - c0 : kSumChunk;
+        for (uint32_t i = t; i < m; i += 256) s_e[i] = errs[c0 + i];
+        __syncthreads();
+        if (t == 0) {
+            // 16 residuals in registers, the next 16 in flight from LDS
+            const float4 *v = reinterpret_cast<const float4 *>(s_e);
+            uint32_t k = 0;
+            if (m >= 16) {
+                float4 c0 = v[0], c1 = v[1], c2 = v[2], c3 = v[3];
+                for (; k + 32 <= m; k += 16) {
+                    const uint32_t j = (k + 16) / 4;
+                    const float4 n0 = v[j], n1 = v[j + 1], n2 = v[j + 2], n3 = v[j + 3];
+                    s += c0.x; s += c0.y; s += c0.z; s += c0.w;
+                    s += c1.x; s += c1.y; s += c1.z; s += c1.w;
+                    s += c2.x; s += c2.y; s += c2.z; s += c2.w;
+                    s += c3.x; s += c3.y; s += c3.z; s += c3.w;
+                    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+                }
+                s += c0.x; s += c0.y; s += c0.z; s += c0.w;
+                s += c1.x; s += c1.y; s += c1.z; s += c1.w;
+                s += c2.x; s += c2.y; s += c2.z; s += c2.w;
+                s += c3.x; s += c3.y; s += c3.z; s += c3.w;
+                k += 16;
+            }
+            for (; k < m; k++) s += s_e[k];
+        }
+        __syncthreads();
     }
-    if (b < n) {
-        const int32_t i = b + (int32_t)threadIdx.x;
-        const int v = __float_as_int(i < n ? errs[i] : 0.f);
-        for (int k = 0; k < n - b; k++) s += __int_as_float(__builtin_amdgcn_readlane(v, k));
-    }
-    if (threadIdx.x == 0) *sum = s;
+    if (t == 0) *sum = s;
 }
 
 hipError_t launch_inliers(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *model, float thr,
@@ -152,7 +176,7 @@ hipError_t launch_inliers(hipStream_t st, int estimator, const void *pts, uint32
         hipLaunchKernelGGL(k_inl_flags<E>, dim3(nb), dim3(kInlBlock), 0, st, pts, n, model, thr, bc);               \
         hipLaunchKernelGGL(k_inl_scan, dim3(1), dim3(1024), 0, st, bc, nb, count);                                 \
         hipLaunchKernelGGL(k_inl_compact<E>, dim3(nb), dim3(kInlBlock), 0, st, pts, n, model, thr, bc, idx, errs); \
-        hipLaunchKernelGGL(k_inl_sum, dim3(1), dim3(64), 0, st, errs, count, sum);                                 \
+        hipLaunchKernelGGL(k_inl_sum, dim3(1), dim3(256), 0, st, errs, count, sum);                                \
     } while (0)
     switch (estimator) {
         case USAC_LINE2D: INL(USAC_LINE2D); break;

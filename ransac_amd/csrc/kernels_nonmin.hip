@@ -29,32 +29,88 @@ __global__ __launch_bounds__(256) void k_gather2(const float2 *__restrict__ pts,
 }
 
 // normalizing transformation: lanes 0..3 = the four coordinate means, lanes 0..1 = the
-// two distance sums; then every lane normalises a strided share of the points.
+// two distance sums (each a sequential fp32 chain in point order, as the reference sums);
+// then every lane normalises a strided share of the points.  The chains are latency-bound,
+// so the whole workgroup stages 2048-point chunks in LDS with coalesced loads (and computes
+// the distance terms in parallel) and the chain lanes add from LDS.
 // ws layout (floats): [0..8] T1, [9..17] T2.
+constexpr uint32_t kNormChunk = 2048;
+
 __global__ __launch_bounds__(256) void k_normalize(float4 *__restrict__ q, uint32_t n, float *ws) {
+    __shared__ float4 s_pts[kNormChunk];
+    __shared__ double s_sq[2][kNormChunk];
     __shared__ float s_mean[4];
     __shared__ float s_scale[2];
     const uint32_t t = threadIdx.x;
-    if (t < 4) {
-        float acc = 0.f;
-        for (uint32_t i = 0; i < n; i++) {
-            const float4 p = q[i];
-            acc += (t == 0 ? p.x : t == 1 ? p.y : t == 2 ? p.z : p.w);
+    float acc = 0.f;
+    for (uint32_t c0 = 0; c0 < n; c0 += kNormChunk) {
+        const uint32_t m = n - c0 < kNormChunk ? n - c0 : kNormChunk;
+        for (uint32_t i = t; i < m; i += 256) s_pts[i] = q[c0 + i];
+        __syncthreads();
+        if (t < 4) {
+            // 16 points in registers, the next 16 in flight from LDS
+            const float *f = reinterpret_cast<const float *>(s_pts) + t;
+            uint32_t k = 0;
+            if (m >= 16) {
+                float c[16];
+#pragma unroll
+                for (int u = 0; u < 16; u++) c[u] = f[4 * u];
+                for (; k + 32 <= m; k += 16) {
+                    float nx[16];
+#pragma unroll
+                    for (int u = 0; u < 16; u++) nx[u] = f[4 * (k + 16 + u)];
+#pragma unroll
+                    for (int u = 0; u < 16; u++) acc += c[u];
+#pragma unroll
+                    for (int u = 0; u < 16; u++) c[u] = nx[u];
+                }
+#pragma unroll
+                for (int u = 0; u < 16; u++) acc += c[u];
+                k += 16;
+            }
+            for (; k < m; k++) acc += f[4 * k];
         }
-        s_mean[t] = acc / (float)n;
+        __syncthreads();
     }
+    if (t < 4) s_mean[t] = acc / (float)n;
     __syncthreads();
-    if (t < 2) {
-        const float mx = s_mean[2 * t], my = s_mean[2 * t + 1];
-        float d = 0.f;
-        for (uint32_t i = 0; i < n; i++) {
-            const float4 p = q[i];
-            const float xm = (t == 0 ? p.x : p.z) - mx;
-            const float ym = (t == 0 ? p.y : p.w) - my;
-            d = (float)((double)d + sqrt((double)(xm * xm + ym * ym)));
+    const float mx1 = s_mean[0], my1 = s_mean[1], mx2 = s_mean[2], my2 = s_mean[3];
+    float d = 0.f;
+    for (uint32_t c0 = 0; c0 < n; c0 += kNormChunk) {
+        const uint32_t m = n - c0 < kNormChunk ? n - c0 : kNormChunk;
+        for (uint32_t i = t; i < m; i += 256) {
+            const float4 p = q[c0 + i];
+            const float xm1 = p.x - mx1, ym1 = p.y - my1;
+            const float xm2 = p.z - mx2, ym2 = p.w - my2;
+            s_sq[0][i] = sqrt((double)(xm1 * xm1 + ym1 * ym1));
+            s_sq[1][i] = sqrt((double)(xm2 * xm2 + ym2 * ym2));
         }
-        s_scale[t] = (float)(M_SQRT2 / (double)(d / (float)n));
+        __syncthreads();
+        if (t < 2) {
+            const double *sq = s_sq[t];
+            uint32_t k = 0;
+            if (m >= 16) {
+                double c[16];
+#pragma unroll
+                for (int u = 0; u < 16; u++) c[u] = sq[u];
+                for (; k + 32 <= m; k += 16) {
+                    double nx[16];
+#pragma unroll
+                    for (int u = 0; u < 16; u++) nx[u] = sq[k + 16 + u];
+#pragma unroll
+                    for (int u = 0; u < 16; u++) d = (float)((double)d + c[u]);
+#pragma unroll
+                    for (int u = 0; u < 16; u++) c[u] = nx[u];
+                }
+#pragma unroll
+                for (int u = 0; u < 16; u++) d = (float)((double)d + c[u]);
+                k += 16;
+            }
+            for (; k < m; k++) d = (float)((double)d + sq[k]);
+        }
+        __syncthreads();
     }
+    if (t < 2) s_scale[t] = (float)(M_SQRT2 / (double)(d / (float)n));
     __syncthreads();
     const float s1 = s_scale[0], s2 = s_scale[1];
     const float t1[9] = {s1, 0.f, -s_mean[0] * s1, 0.f, s1, -s_mean[1] * s1, 0.f, 0.f, 1.f};

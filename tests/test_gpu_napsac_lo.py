@@ -60,3 +60,28 @@ def test_loop_napsac_lo_identical(usac, oracle, kind, sampler, lo, sprt):
     assert (_bits(out.raw["minimal_model"]) == _bits(ref["minimal_model"])).all()
     assert (_bits(out.getModel()) == _bits(ref["model"])).all()
     assert (out.getInliers() == ref["inlier_idx"]).all()
+
+
+@pytest.mark.parametrize("lo", [1, 2])
+def test_cfg5_full_size(usac, oracle, lo):
+    """BASELINE configs[4] at full size: homography + NAPSAC (grid) + LO-RANSAC over 100k
+    correspondences -- the device loop's iterations, records, LO counters, final model and
+    inlier list identical to the oracle's."""
+    pts, _, _ = synthetic.homography_points(n=100000, inlier_ratio=0.2, seed=11, cluster=(500, 500, 150))
+    ref = oracle.ransac_run(oracle.HOMOGRAPHY, pts, 2.0, 0.95, 5, sampler=oracle.SAMPLER_NAPSAC, sprt=False, lo=lo,
+                            max_iters=5000)
+    mdl = usac.Model(2.0, 4, 0.95, 7, usac.ESTIMATOR.Homography, usac.SAMPLER.Napsac)
+    mdl.ResetRandomGenerator(False)
+    mdl.setSeed(5)
+    mdl.lo = usac.LocOpt(lo)
+    mdl.max_iterations = 5000
+    mdl.setNeighborsType(usac.NeighborsSearch.Grid)
+    r = usac.Ransac(mdl, pts)
+    r.run()
+    out = r.getRansacOutput()
+    assert out.getNumberOfMainIterations() == ref["iters"]
+    assert [(i, c) for i, c, _ in r.records] == [(i, c) for i, c, _ in ref["records"]]
+    assert out.getLOIters() == ref["lo_inner_iters"]
+    assert out.raw["lo_iterative_iters"] == ref["lo_iterative_iters"]
+    assert (_bits(out.getModel()) == _bits(ref["model"])).all()
+    assert (out.getInliers() == ref["inlier_idx"]).all()
