@@ -19,7 +19,7 @@ __all__ = ["ESTIMATOR", "SAMPLER", "LocOpt", "NeighborsSearch", "DLT", "Model", 
            "build", "lib", "std_termination", "uniform_samples", "prosac_samples", "sprt_pool", "UsacError"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libransac_amd.so")
+LIB_PATH = os.environ.get("RANSAC_AMD_LIB") or os.path.join(_HERE, "libransac_amd.so")  # override: A/B builds
 
 
 class ESTIMATOR(enum.IntEnum):  # usac/model.hpp:10
