@@ -508,8 +508,21 @@ int usac_score_models(usac_ctx *c, const float *models, uint32_t nm, float thr, 
     HIP_TRY(c, hipMemcpyAsync(c->hostmodels.p, models, sizeof(float) * 9 * (size_t)nm, hipMemcpyHostToDevice, c->stream));
     if (listed(c)) {
         HIP_TRY(c, usac::launch_prepare_f(c->stream, c->hostmodels.as<float>(), nm, c->models.as<float>()));
-        HIP_TRY(c, usac::launch_score_f(c->stream, c->estimator, 1, c->pts.as<float4>(), c->n, c->models.as<float>(),
-                                        nm, nullptr, nullptr, nm, thr, c->counts.as<int32_t>(), c->sums.as<float>()));
+        if (c->score_variant == 1) {
+            HIP_TRY(c, usac::launch_score_f(c->stream, c->estimator, 1, c->pts.as<float4>(), c->n,
+                                            c->models.as<float>(), nm, nullptr, nullptr, nm, thr,
+                                            c->counts.as<int32_t>(), c->sums.as<float>()));
+        } else {  // the fast two-view kernel, one chunk: exact sequential sums
+            if (c->rec_thr != thr) {
+                HIP_TRY(c, c->rec.reserve(sizeof(float) * 32 * (((size_t)c->n + 3) / 4)));
+                HIP_TRY(c, usac::launch_prepare_rec(c->stream, c->pts.as<float4>(), c->n, thr, c->rec.as<float4>()));
+                c->rec_thr = thr;
+            }
+            HIP_TRY(c, c->tv_part.reserve(usac::tv_scratch_bytes(nm, 1)));
+            HIP_TRY(c, usac::launch_score_f2(c->stream, c->estimator, 1, c->rec.as<float4>(), c->pts.as<float4>(),
+                                             c->n, c->models.as<float>(), nm, nullptr, nullptr, nm, thr,
+                                             c->counts.as<int32_t>(), c->sums.as<float>(), c->tv_part.p));
+        }
     } else {
         if (is_h(c))
             HIP_TRY(c, usac::launch_prepare_h(c->stream, c->hostmodels.as<float>(), nm, c->models.as<float>()));
