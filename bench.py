@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--points", type=int, default=None, help="default: 10000 (cfg2/cfg3), 50000 (cfg4)")
     ap.add_argument("--threshold", type=float, default=None,
                     help="default: 2.0 px (cfg2/cfg3), 0.002 (cfg4, normalised coordinates)")
-    ap.add_argument("--chunks", type=int, default=None, help="score point chunks (default 8 homography, 64 two-view)")
+    ap.add_argument("--chunks", type=int, default=None, help="score point chunks (default 8 homography, 96 two-view)")
     ap.add_argument("--dlt", choices=["thin", "nullspace"], default="thin")
     ap.add_argument("--sprt", action="store_true",
                     help="batch SPRT verification (reference initial epsilon/delta for the estimator)")
@@ -59,7 +59,7 @@ def parse():
     if args.threshold is None:
         args.threshold = 0.002 if ess else 2.0
     if args.chunks is None:
-        args.chunks = 8 if args.estimator == "homography" else 64
+        args.chunks = 8 if args.estimator == "homography" else 96
     return args
 
 

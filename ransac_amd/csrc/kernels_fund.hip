@@ -172,61 +172,111 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_f(const float4 *__restric
 }
 
 // ---------------------------------------------------------------- fast two-view scoring
-// Same results as k_score_f (counts and Σerr bit for bit), two points per packed VALU op:
+// Same results as k_score_f (counts and Σerr bit for bit):
 //
-//   stage A  the reference's own operation sequence (v_pk_mul_f32 / v_pk_add_f32 are the
-//            scalar IEEE ops element-wise, so every intermediate equals the exact path's)
-//            up to the quantities below, then a division-free test that can only reject
-//            points whose reference error is >= thr:
-//              Sampson   e = S / D:        reject if S > fl(fl(thr D) (1 + 2^-20))
-//                        (e < thr  =>  S < thr D, and the factor dominates both roundings)
-//              essential e = (|a1/a2| + |b1/b2|) / 2 with a2 = sqrt(Qa):
-//                        reject if a1^2 > fl(fl(4 thr^2 Qa) (1 + 2^-18))
-//                        (e < thr  =>  fl(|a1/a2|) < 2 thr  =>  a1^2 < 4 thr^2 Qa (1 + 2^-21))
-//            a NaN on either side rejects (the exact error is then NaN, never an inlier --
-//            this also drops the NaN-padded tail points); inf only rejects when the exact
-//            error is inf as well;
+//   stage A  FMA chains (two points per v_pk_fma_f32) for the quantities of the reference's
+//            residual, then a division- and sqrt-free test that only rejects pairs whose
+//            REFERENCE error is provably >= thr.  The fused values differ from the reference's
+//            (rounded, differently associated) ones by at most per-model bounds derived from
+//            the dataset box |x1| <= c.x, |y1| <= c.y, |x2| <= c.z, |y2| <= c.w (DESIGN.md
+//            "Two-view stage A" has the derivation); the test absorbs them:
+//              Sampson   e = S/D, s the numerator root:  reject iff ¬(s² <= D K + C)
+//              essential e = (|a1/a2| + |b1/b2|)/2:      reject iff ¬(a1² <= Qa K + C)
+//            with K = thr (1 + 2^-9) resp. 4 thr² (1 + 2^-9) and C = (δD K + 1026 δs²)(1 + 2^-20)
+//            (δ = the per-model bounds), C >= 2^-126.  Models whose bounds are not finite and
+//            <= 2^60 (overflow could otherwise hide in the fused chain) skip stage A: every
+//            point of theirs goes to stage B.  A NaN point rejects (its exact error is NaN);
 //   stage B  the exact expression (two_view_error) on the kept pairs only, sequential
 //            accumulation per model (see the queues below).
 //
 // Points come from the fast-kernel records (k_prepare_rec: SoA groups of four, NaN-padded
-// tail -- NaN points are never inliers).
+// tail, never queued).
 typedef float v2f __attribute__((ext_vector_type(2)));
 
 template <int EST>
 struct TwoViewModel {
     float f[9];
     v2f f2[9];
-    float k;  // Sampson: thr (1 + 2^-20) applied as fl(fl(thr D) K); essential: 4 thr^2
+    v2f K, C;          // stage-A test constants, duplicated for the packed halves
+    uint32_t all;      // 0xFF: stage A disabled for this model (every point kept)
 };
+
+__device__ __forceinline__ float ceil_fudge(float x) { return x * 1.00000095367431640625f; }  // (1 + 2^-20)
+
+template <int EST>
+__device__ __forceinline__ void two_view_setup(TwoViewModel<EST> &M, float4 c, float thr) {
+    const float *f = M.f;
+#pragma unroll
+    for (int k = 0; k < 9; k++) M.f2[k] = v2f{f[k], f[k]};
+    float dv2, ds2, lim1, lim2;  // bound of the squared quantity's error, of the root's error^2
+    float K;
+    if constexpr (EST == USAC_ESSENTIAL) {
+        const float L1 = ceil_fudge(fabsf(f[0]) * c.z + fabsf(f[3]) * c.w + fabsf(f[6]));
+        const float L2 = ceil_fudge(fabsf(f[1]) * c.z + fabsf(f[4]) * c.w + fabsf(f[7]));
+        const float L3 = ceil_fudge(fabsf(f[2]) * c.z + fabsf(f[5]) * c.w + fabsf(f[8]));
+        const float Aa = ceil_fudge(L1 * c.x + L2 * c.y + L3);
+        const float LQ = ceil_fudge(L1 * L1 + L2 * L2);
+        const float da = ceil_fudge(Aa * 9.5367431640625e-07f);  // 2^-20 Aa
+        dv2 = ceil_fudge(LQ * 1.9073486328125e-06f);             // δQ = 2^-19 LQ
+        ds2 = ceil_fudge(da * da);
+        lim1 = Aa;
+        lim2 = LQ;
+        K = ((4.0f * thr) * thr) * 1.001953125f;                  // 4 thr² (1 + 2^-9)
+    } else {
+        const float LFx = ceil_fudge(fabsf(f[0]) * c.x + fabsf(f[1]) * c.y + fabsf(f[2]));
+        const float LFy = ceil_fudge(fabsf(f[3]) * c.x + fabsf(f[4]) * c.y + fabsf(f[5]));
+        const float LGx = ceil_fudge(fabsf(f[0]) * c.z + fabsf(f[3]) * c.w + fabsf(f[6]));
+        const float LGy = ceil_fudge(fabsf(f[1]) * c.z + fabsf(f[4]) * c.w + fabsf(f[7]));
+        const float Ls =
+            ceil_fudge(c.z * LFx + c.w * LFy + fabsf(f[6]) * c.x + fabsf(f[7]) * c.y + fabsf(f[8]));
+        const float LD = ceil_fudge(LFx * LFx + LFy * LFy + LGx * LGx + LGy * LGy);
+        const float ds = ceil_fudge(Ls * 1.9073486328125e-06f);  // δs = 2^-19 Ls
+        dv2 = ceil_fudge(LD * 1.9073486328125e-06f);             // δD = 2^-19 LD
+        ds2 = ceil_fudge(ds * ds);
+        lim1 = Ls;
+        lim2 = LD;
+        K = thr * 1.001953125f;                                   // thr (1 + 2^-9)
+    }
+    float C = ceil_fudge(ceil_fudge(dv2 * K) + ceil_fudge(1026.0f * ds2));
+    C = C > 1.17549435e-38f ? C : 1.17549435e-38f;                // >= 2^-126
+    M.all = (lim1 <= 1.152921504606846976e18f && lim2 <= 1.329227995784915873e36f) ? 0u : 0xFFu;  // 2^60, 2^120
+    M.K = v2f{K, K};
+    M.C = v2f{C, C};
+}
 
 // stage A for two points: true = sure outlier
 template <int EST>
-__device__ __forceinline__ void two_view_reject2(const TwoViewModel<EST> &M, float thr, v2f x1, v2f y1, v2f x2,
-                                                 v2f y2, bool &r0, bool &r1) {
+__device__ __forceinline__ void two_view_reject2(const TwoViewModel<EST> &M, v2f x1, v2f y1, v2f x2, v2f y2,
+                                                 bool &r0, bool &r1) {
     const v2f *f = M.f2;
+    v2f A, T;
     if constexpr (EST == USAC_ESSENTIAL) {
-        const v2f l1 = (f[0] * x2 + f[3] * y2) + f[6];
-        const v2f l2 = (f[1] * x2 + f[4] * y2) + f[7];
-        const v2f l3 = (f[2] * x2 + f[5] * y2) + f[8];
-        const v2f a1 = (l1 * x1 + l2 * y1) + l3;
-        const v2f Qa = l1 * l1 + l2 * l2;
-        const v2f A = a1 * a1;
-        const v2f T = (v2f{M.k, M.k} * Qa) * v2f{1.000003814697265625f, 1.000003814697265625f};  // 1 + 2^-18
-        r0 = !(A.x <= T.x);
-        r1 = !(A.y <= T.y);
+        const v2f l1 = __builtin_elementwise_fma(f[0], x2, __builtin_elementwise_fma(f[3], y2, f[6]));
+        const v2f l2 = __builtin_elementwise_fma(f[1], x2, __builtin_elementwise_fma(f[4], y2, f[7]));
+        const v2f l3 = __builtin_elementwise_fma(f[2], x2, __builtin_elementwise_fma(f[5], y2, f[8]));
+        const v2f a1 = __builtin_elementwise_fma(l1, x1, __builtin_elementwise_fma(l2, y1, l3));
+        const v2f Qa = __builtin_elementwise_fma(l1, l1, l2 * l2);
+        A = a1 * a1;
+        T = __builtin_elementwise_fma(Qa, M.K, M.C);
     } else {
-        const v2f Fx = (f[0] * x1 + f[1] * y1) + f[2];
-        const v2f Fy = (f[3] * x1 + f[4] * y1) + f[5];
-        const v2f Gx = (f[0] * x2 + f[3] * y2) + f[6];
-        const v2f Gy = (f[1] * x2 + f[4] * y2) + f[7];
-        const v2f sv = (((x2 * Fx + y2 * Fy) + f[6] * x1) + f[7] * y1) + f[8];
-        const v2f S = sv * sv;
-        const v2f D = ((Fx * Fx + Fy * Fy) + Gx * Gx) + Gy * Gy;
-        const v2f T = (v2f{thr, thr} * D) * v2f{1.00000095367431640625f, 1.00000095367431640625f};  // 1 + 2^-20
-        r0 = !(S.x <= T.x);
-        r1 = !(S.y <= T.y);
+        const v2f Fx = __builtin_elementwise_fma(f[0], x1, __builtin_elementwise_fma(f[1], y1, f[2]));
+        const v2f Fy = __builtin_elementwise_fma(f[3], x1, __builtin_elementwise_fma(f[4], y1, f[5]));
+        const v2f Gx = __builtin_elementwise_fma(f[0], x2, __builtin_elementwise_fma(f[3], y2, f[6]));
+        const v2f Gy = __builtin_elementwise_fma(f[1], x2, __builtin_elementwise_fma(f[4], y2, f[7]));
+        const v2f sv = __builtin_elementwise_fma(
+            x2, Fx, __builtin_elementwise_fma(y2, Fy, __builtin_elementwise_fma(f[6], x1, __builtin_elementwise_fma(f[7], y1, f[8]))));
+        const v2f D = __builtin_elementwise_fma(
+            Fx, Fx, __builtin_elementwise_fma(Fy, Fy, __builtin_elementwise_fma(Gx, Gx, Gy * Gy)));
+        A = sv * sv;
+        T = __builtin_elementwise_fma(D, M.K, M.C);
     }
+#ifdef TV_EXP_NOKEEP
+    r0 = !(A.x <= T.x) || true;
+    r1 = !(A.y <= T.y) || true;
+#else
+    r0 = !(A.x <= T.x);
+    r1 = !(A.y <= T.y);
+#endif
 }
 
 // Stage B is deferred: per eight points (two groups) a lane appends one entry -- the group
@@ -262,15 +312,17 @@ __device__ __forceinline__ void two_view_drain(const TwoViewModel<EST> &M, const
 // stage A of four points -> 4-bit mask of the kept ones
 template <int EST>
 __device__ __forceinline__ uint32_t two_view_group(const TwoViewModel<EST> &M, float4 X1, float4 Y1, float4 X2,
-                                                   float4 Y2, float thr) {
+                                                   float4 Y2) {
     bool r0, r1, r2, r3;
-    two_view_reject2<EST>(M, thr, v2f{X1.x, X1.y}, v2f{Y1.x, Y1.y}, v2f{X2.x, X2.y}, v2f{Y2.x, Y2.y}, r0, r1);
-    two_view_reject2<EST>(M, thr, v2f{X1.z, X1.w}, v2f{Y1.z, Y1.w}, v2f{X2.z, X2.w}, v2f{Y2.z, Y2.w}, r2, r3);
+    two_view_reject2<EST>(M, v2f{X1.x, X1.y}, v2f{Y1.x, Y1.y}, v2f{X2.x, X2.y}, v2f{Y2.x, Y2.y}, r0, r1);
+    two_view_reject2<EST>(M, v2f{X1.z, X1.w}, v2f{Y1.z, Y1.w}, v2f{X2.z, X2.w}, v2f{Y2.z, Y2.w}, r2, r3);
     return (r0 ? 0u : 1u) | (r1 ? 0u : 2u) | (r2 ? 0u : 4u) | (r3 ? 0u : 8u);
 }
 
-// append (g, mask) when the mask is not empty (the slot is written either way)
-__device__ __forceinline__ void two_view_append(uint32_t *q, int &len, uint32_t g, uint32_t mask) {
+// append (g, mask) when the mask is not empty (the slot is written either way).  Points
+// 4g .. 4g+7 past n (the NaN padding) are masked off: a model without stage A keeps all.
+__device__ __forceinline__ void two_view_append(uint32_t *q, int &len, uint32_t g, uint32_t n, uint32_t mask) {
+    if (4 * g + 8 > n) mask &= (1u << (n - 4 * g)) - 1u;  // wave-uniform: the last group(s) only
     q[64 * len] = (g << 8) | mask;
     len += mask ? 1 : 0;
 }
@@ -281,7 +333,7 @@ __device__ __forceinline__ void two_view_append(uint32_t *q, int &len, uint32_t 
 // workgroups spread the few model tiles of a two-view batch evenly over the 256 CUs.
 template <int EST>
 __global__ __launch_bounds__(64) void k_score_f2(const float4 *__restrict__ rec, const float4 *__restrict__ pts,
-                                                 uint32_t n, const float *__restrict__ models, size_t stride,
+                                                 uint32_t n, float4 ext, const float *__restrict__ models, size_t stride,
                                                  const uint32_t *__restrict__ list,
                                                  const uint32_t *__restrict__ list_n, uint32_t kmax, float thr,
                                                  const uint32_t *__restrict__ perm,
@@ -299,11 +351,8 @@ __global__ __launch_bounds__(64) void k_score_f2(const float4 *__restrict__ rec,
     const uint32_t slot = list ? list[ic] : ic;
     TwoViewModel<EST> M;
 #pragma unroll
-    for (int k = 0; k < 9; k++) {
-        M.f[k] = models[(size_t)k * stride + slot];
-        M.f2[k] = v2f{M.f[k], M.f[k]};
-    }
-    M.k = EST == USAC_ESSENTIAL ? (4.0f * thr) * thr : thr;
+    for (int k = 0; k < 9; k++) M.f[k] = models[(size_t)k * stride + slot];
+    two_view_setup<EST>(M, ext, thr);
     const uint32_t ngroups = (n + 3) / 4;
     const uint32_t per = (ngroups + C - 1) / C;
     const uint32_t gbeg = chunk * per < ngroups ? chunk * per : ngroups;
@@ -323,9 +372,9 @@ __global__ __launch_bounds__(64) void k_score_f2(const float4 *__restrict__ rec,
             const float4 *pn = rec + 8 * (size_t)gn;
             const float4 c0 = pn[0], c1 = pn[1], c2 = pn[2], c3 = pn[3];
             const float4 d0 = pn[8], d1 = pn[9], d2 = pn[10], d3 = pn[11];
-            const uint32_t ma = two_view_group<EST>(M, a0, a1, a2, a3, thr);
-            const uint32_t mb = two_view_group<EST>(M, b0, b1, b2, b3, thr);
-            two_view_append(q, len, g, ma | (mb << 4));
+            const uint32_t ma = two_view_group<EST>(M, a0, a1, a2, a3);
+            const uint32_t mb = two_view_group<EST>(M, b0, b1, b2, b3);
+            two_view_append(q, len, g, n, ma | (mb << 4) | M.all);
             if (__builtin_amdgcn_ballot_w64(len == kTvQueue)) two_view_drain<EST>(M, pts, q, len, thr, cnt, sum);
             a0 = c0; a1 = c1; a2 = c2; a3 = c3;
             b0 = d0; b1 = d1; b2 = d2; b3 = d3;
@@ -333,7 +382,7 @@ __global__ __launch_bounds__(64) void k_score_f2(const float4 *__restrict__ rec,
     }
     if (g < gend) {
         const float4 *p = rec + 8 * (size_t)g;
-        two_view_append(q, len, g, two_view_group<EST>(M, p[0], p[1], p[2], p[3], thr));
+        two_view_append(q, len, g, n, (two_view_group<EST>(M, p[0], p[1], p[2], p[3]) | M.all) & 0xFu);
     }
     two_view_drain<EST>(M, pts, q, len, thr, cnt, sum);
     if (!live) return;
@@ -355,7 +404,7 @@ constexpr uint32_t kTvPresortGroups = 32;  // 128 points
 constexpr int kTvPresortKeeps = 8;
 
 template <int EST>
-__global__ __launch_bounds__(64) void k_presort_tv(const float4 *__restrict__ rec, uint32_t n,
+__global__ __launch_bounds__(64) void k_presort_tv(const float4 *__restrict__ rec, uint32_t n, float4 ext,
                                                    const float *__restrict__ models, size_t stride,
                                                    const uint32_t *__restrict__ list,
                                                    const uint32_t *__restrict__ list_n, uint32_t kmax, float thr,
@@ -369,17 +418,14 @@ __global__ __launch_bounds__(64) void k_presort_tv(const float4 *__restrict__ re
     const uint32_t slot = list ? list[ic] : ic;
     TwoViewModel<EST> M;
 #pragma unroll
-    for (int k = 0; k < 9; k++) {
-        M.f[k] = models[(size_t)k * stride + slot];
-        M.f2[k] = v2f{M.f[k], M.f[k]};
-    }
-    M.k = EST == USAC_ESSENTIAL ? (4.0f * thr) * thr : thr;
+    for (int k = 0; k < 9; k++) M.f[k] = models[(size_t)k * stride + slot];
+    two_view_setup<EST>(M, ext, thr);
     const uint32_t ngroups = (n + 3) / 4;
     const uint32_t g1 = ngroups < kTvPresortGroups ? ngroups : kTvPresortGroups;
     int keeps = 0;
     for (uint32_t g = 0; g < g1; g++) {
         const float4 *p = rec + 8 * (size_t)g;
-        keeps += __builtin_popcount(two_view_group<EST>(M, p[0], p[1], p[2], p[3], thr));
+        keeps += __builtin_popcount(two_view_group<EST>(M, p[0], p[1], p[2], p[3]) | (M.all & 0xFu));
     }
     const bool valid = i < K;
     const bool heavy = valid && keeps >= kTvPresortKeeps;
@@ -459,8 +505,9 @@ hipError_t launch_score_f(hipStream_t st, int estimator, int chunks, const float
 
 namespace usac {
 hipError_t launch_score_f2(hipStream_t st, int estimator, int chunks, const float4 *rec, const float4 *pts,
-                           uint32_t n, const float *models, size_t stride, const uint32_t *list, const uint32_t *list_n,
-                           uint32_t kmax, float thr, int32_t *counts, float *sums, void *scratch) {
+                           uint32_t n, float4 ext, const float *models, size_t stride, const uint32_t *list,
+                           const uint32_t *list_n, uint32_t kmax, float thr, int32_t *counts, float *sums,
+                           void *scratch) {
     if (chunks < 1 || chunks > 128 || !scratch) return hipErrorInvalidValue;
     // scratch: ends[2] (padded to 256 B), perm[kmax], then the chunk partials
     uint32_t *ends = static_cast<uint32_t *>(scratch);
@@ -472,19 +519,19 @@ hipError_t launch_score_f2(hipStream_t st, int estimator, int chunks, const floa
     const bool ess = estimator == USAC_ESSENTIAL;
     const dim3 pgrid((kmax + 63) / 64);
     if (ess)
-        hipLaunchKernelGGL((k_presort_tv<USAC_ESSENTIAL>), pgrid, dim3(64), 0, st, rec, n, models, stride, list,
+        hipLaunchKernelGGL((k_presort_tv<USAC_ESSENTIAL>), pgrid, dim3(64), 0, st, rec, n, ext, models, stride, list,
                            list_n, kmax, thr, perm, ends);
     else
-        hipLaunchKernelGGL((k_presort_tv<USAC_FUNDAMENTAL>), pgrid, dim3(64), 0, st, rec, n, models, stride, list,
+        hipLaunchKernelGGL((k_presort_tv<USAC_FUNDAMENTAL>), pgrid, dim3(64), 0, st, rec, n, ext, models, stride, list,
                            list_n, kmax, thr, perm, ends);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     const dim3 grid((kmax + 63) / 64, chunks);
     if (ess)
-        hipLaunchKernelGGL((k_score_f2<USAC_ESSENTIAL>), grid, dim3(64), 0, st, rec, pts, n, models, stride, list,
+        hipLaunchKernelGGL((k_score_f2<USAC_ESSENTIAL>), grid, dim3(64), 0, st, rec, pts, n, ext, models, stride, list,
                            list_n, kmax, thr, perm, counts, sums, pc, ps);
     else
-        hipLaunchKernelGGL((k_score_f2<USAC_FUNDAMENTAL>), grid, dim3(64), 0, st, rec, pts, n, models, stride, list,
+        hipLaunchKernelGGL((k_score_f2<USAC_FUNDAMENTAL>), grid, dim3(64), 0, st, rec, pts, n, ext, models, stride, list,
                            list_n, kmax, thr, perm, counts, sums, pc, ps);
     e = hipGetLastError();
     if (e != hipSuccess || chunks == 1) return e;

@@ -198,7 +198,7 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
         hipError_t e = c->tv_part.reserve(usac::tv_scratch_bytes(B * c->spk, chunks));
         if (e != hipSuccess) return e;
         return usac::launch_score_f2(c->stream, c->estimator, chunks, c->rec.as<float4>(), c->pts.as<float4>(), c->n,
-                                     c->models.as<float>(),
+                                     c->ext, c->models.as<float>(),
                                      (size_t)B * c->spk, c->list.as<uint32_t>(), c->list_n.as<uint32_t>(), B * c->spk,
                                      thr, c->counts.as<int32_t>(), c->sums.as<float>(), c->tv_part.p);
     }
@@ -390,7 +390,7 @@ int usac_create(usac_ctx **out, int device, int estimator, const float *pts, uin
     c->spk = estimator == USAC_FUNDAMENTAL ? 3 : 1;
     // two-view scoring: a batch yields few models (about 0.4-1.3 per sample) and the few with
     // many inliers are much slower to score, so their point ranges are cut finer
-    if (estimator == USAC_FUNDAMENTAL || estimator == USAC_ESSENTIAL) c->chunks = 64;
+    if (estimator == USAC_FUNDAMENTAL || estimator == USAC_ESSENTIAL) c->chunks = 96;
     int rc = USAC_OK;
     do {
         hipError_t e = hipSetDevice(device);
@@ -520,7 +520,7 @@ int usac_score_models(usac_ctx *c, const float *models, uint32_t nm, float thr, 
             }
             HIP_TRY(c, c->tv_part.reserve(usac::tv_scratch_bytes(nm, 1)));
             HIP_TRY(c, usac::launch_score_f2(c->stream, c->estimator, 1, c->rec.as<float4>(), c->pts.as<float4>(),
-                                             c->n, c->models.as<float>(), nm, nullptr, nullptr, nm, thr,
+                                             c->n, c->ext, c->models.as<float>(), nm, nullptr, nullptr, nm, thr,
                                              c->counts.as<int32_t>(), c->sums.as<float>(), c->tv_part.p));
         }
     } else {

@@ -48,8 +48,9 @@ hipError_t launch_score_f(hipStream_t st, int estimator, int chunks, const float
 // (chunks 1..128; scratch = tv_scratch_bytes(kmax, chunks): pre-sort permutation + chunk
 // partials)
 hipError_t launch_score_f2(hipStream_t st, int estimator, int chunks, const float4 *rec, const float4 *pts,
-                           uint32_t n, const float *models, size_t stride, const uint32_t *list, const uint32_t *list_n,
-                           uint32_t kmax, float thr, int32_t *counts, float *sums, void *scratch);
+                           uint32_t n, float4 ext, const float *models, size_t stride, const uint32_t *list,
+                           const uint32_t *list_n, uint32_t kmax, float thr, int32_t *counts, float *sums,
+                           void *scratch);
 size_t tv_scratch_bytes(uint32_t kmax, int chunks);
 // essential 5-point (kernels_ess.hip): one slot per sample (models [9][B], counts 0 / -1,
 // list / list_n); workspace = e5_workspace_bytes(B)
