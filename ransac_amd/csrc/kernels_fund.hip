@@ -291,19 +291,41 @@ constexpr int kTvQueue = 16;  // entries per lane (4 KB of LDS per wave)
 template <int EST>
 __device__ __forceinline__ void two_view_drain(const TwoViewModel<EST> &M, const float4 *__restrict__ pts,
                                                const uint32_t *q, int &len, float thr, int &cnt, float &sum) {
-    for (int t = 0; __builtin_amdgcn_ballot_w64(t < len); t++) {
-        const uint32_t e = t < len ? q[t * 64] : 0u;
-        const uint32_t base = (e >> 8) * 4;
-        uint32_t m = e & 255u;
-        while (m) {
-            const uint32_t b = __builtin_ctz(m);
-            m &= m - 1;
-            const float4 p = pts[base + b];
-            const float err = two_view_error<EST>(M.f, p.x, p.y, p.z, p.w);
-            if (err < thr) {
-                cnt++;
-                sum += err;
-            }
+    // each lane walks its kept points in order, two per trip: the two loads and exact
+    // evaluations of a trip are independent (latency overlap), the adds stay in order
+    int t = 0;
+    uint32_t m = 0, base = 0;
+    for (;;) {
+        if (m == 0 && t < len) {  // queue entries never have an empty mask
+            const uint32_t e = q[t * 64];
+            t++;
+            m = e & 255u;
+            base = (e >> 8) * 4;
+        }
+        const bool h0 = m != 0;
+        const uint32_t i0 = h0 ? base + __builtin_ctz(m) : 0u;
+        m &= m - 1;
+        if (m == 0 && t < len) {
+            const uint32_t e = q[t * 64];
+            t++;
+            m = e & 255u;
+            base = (e >> 8) * 4;
+        }
+        const bool h1 = m != 0;
+        const uint32_t i1 = h1 ? base + __builtin_ctz(m) : 0u;
+        m &= m - 1;
+        if (!__builtin_amdgcn_ballot_w64(h0)) break;
+        const float4 p0 = pts[i0];
+        const float4 p1 = pts[i1];
+        const float e0 = two_view_error<EST>(M.f, p0.x, p0.y, p0.z, p0.w);
+        const float e1 = two_view_error<EST>(M.f, p1.x, p1.y, p1.z, p1.w);
+        if (h0 && e0 < thr) {
+            cnt++;
+            sum += e0;
+        }
+        if (h1 && e1 < thr) {
+            cnt++;
+            sum += e1;
         }
     }
     len = 0;
