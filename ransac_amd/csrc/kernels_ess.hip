@@ -109,6 +109,7 @@ __global__ __launch_bounds__(64) void k_e5_dets(uint32_t B, E5Work w) {
 }
 
 __global__ __launch_bounds__(64) void k_e5_roots(uint32_t B, E5Work w) {
+    __shared__ double s_lvl[32 * 64];  // root-isolation level arrays (e5::RootsLds), 16 KB
     const uint32_t lane = threadIdx.x;
     const uint32_t h = blockIdx.x * 64 + lane;
     int nr = 0;
@@ -137,13 +138,13 @@ __global__ __launch_bounds__(64) void k_e5_roots(uint32_t B, E5Work w) {
 #pragma unroll
         for (int r = 0; r < 10; r++) w.flags[(size_t)r * B + h] = 0;
         if (a[10] != 0.0) {
-            double crit[10];
+            const e5::RootsLds L{s_lvl + lane, s_lvl + 11 * 64 + lane, s_lvl + 22 * 64 + lane};
             uint32_t found;
-            e5::real_roots10(a, crit, found);
+            e5::real_roots10(a, L, found);
 #pragma unroll
             for (int k = 0; k < 10; k++)
                 if (found & (1u << k)) {
-                    w.roots[(size_t)nr * B + h] = crit[k];
+                    w.roots[(size_t)nr * B + h] = L.NX[64 * k];
                     nr++;
                 }
         } else {

@@ -421,18 +421,17 @@ __device__ __forceinline__ double poly_eval_t(const double (&c)[11], double x) {
     return r;
 }
 
-// value at compile-time-unrolled index k of v[0..N) (selects on opaque values: stays in
-// registers, see opaque())
-template <int N>
-__device__ __forceinline__ double pick(const double (&v)[N], int k) {
-    double r = opaque(v[0]);
-#pragma unroll
-    for (int i = 1; i < N; i++) r = (k == i) ? opaque(v[i]) : r;
-    return r;
-}
+// Per-lane level arrays live in LDS (the caller's 64-lane block, stride 64 doubles):
+// E[0..G] the interval ends, FE[0..G] p at the ends, NX[0..G) the level's output points.
+// The flat loop picks a new interval's ends with dynamically indexed LDS reads -- one
+// ds_read each, where register arrays would cost G selects per value on every trip on
+// which some lane starts an interval (nearly every trip).
+struct RootsLds {
+    double *E, *FE, *NX;  // already offset by the lane; element k at [64 k]
+};
 
 template <int G>
-__device__ __forceinline__ void roots_level(const double (&a)[11], double R, double (&crit)[10], uint32_t &found) {
+__device__ __forceinline__ void roots_level(const double (&a)[11], double R, const RootsLds &L, uint32_t &found) {
     constexpr int d = 10 - G;
     double c[11];
 #pragma unroll
@@ -442,19 +441,25 @@ __device__ __forceinline__ void roots_level(const double (&a)[11], double R, dou
         for (int m = j + d; m > j; m--) f *= (double)m;
         c[j] = a[j + d] * f;
     }
-    // interval k = [e[k], e[k+1]]; fillers (left ends) unless refined
-    double e[G + 1], fe[G + 1], next[10];
+    // interval k = [E[k], E[k+1]]: the previous level's points between -R and R; left ends
+    // are the fillers unless the interval is refined
+    double e[G + 1];
     e[0] = -R;
 #pragma unroll
-    for (int k = 1; k < G; k++) e[k] = crit[k - 1];
+    for (int k = 1; k < G; k++) e[k] = L.NX[64 * (k - 1)];
     e[G] = R;
-#pragma unroll
-    for (int k = 0; k <= G; k++) fe[k] = poly_eval_t<G>(c, e[k]);
     uint32_t todo = 0;
+    double fprev = poly_eval_t<G>(c, e[0]);
+    L.E[0] = e[0];
+    L.FE[0] = fprev;
 #pragma unroll
     for (int k = 0; k < G; k++) {
-        next[k] = e[k];
-        if (e[k + 1] > e[k] && ((fe[k] < 0.0) != (fe[k + 1] < 0.0))) todo |= 1u << k;
+        const double fk = poly_eval_t<G>(c, e[k + 1]);
+        L.E[64 * (k + 1)] = e[k + 1];
+        L.FE[64 * (k + 1)] = fk;
+        L.NX[64 * k] = e[k];
+        if (e[k + 1] > e[k] && ((fprev < 0.0) != (fk < 0.0))) todo |= 1u << k;
+        fprev = fk;
     }
     found = todo;
     // per-lane refinement state of the current interval k
@@ -464,10 +469,10 @@ __device__ __forceinline__ void roots_level(const double (&a)[11], double R, dou
     while (todo) {
         if (fresh) {
             k = __builtin_ctz(todo);
-            lo = pick(e, k);
-            hi = pick(e, k + 1);
-            flo = pick(fe, k);
-            const double fhi = pick(fe, k + 1);
+            lo = L.E[64 * k];
+            hi = L.E[64 * (k + 1)];
+            flo = L.FE[64 * k];
+            const double fhi = L.FE[64 * (k + 1)];
             x = lo - flo * ((hi - lo) / (fhi - flo));
             if (!(x > lo && x < hi)) x = 0.5 * (lo + hi);
             dxold = hi - lo;
@@ -519,19 +524,16 @@ __device__ __forceinline__ void roots_level(const double (&a)[11], double R, dou
             }
         }
         if (done) {
-#pragma unroll
-            for (int q = 0; q < G; q++) next[q] = (q == k) ? res : next[q];
+            L.NX[64 * k] = res;
             todo &= todo - 1;
             fresh = true;
         }
     }
-#pragma unroll
-    for (int q = 0; q < G; q++) crit[q] = next[q];
-    if constexpr (G < 10) roots_level<G + 1>(a, R, crit, found);
+    if constexpr (G < 10) roots_level<G + 1>(a, R, L, found);
 }
 
-// a[10] != 0 required; root k (ascending) is crit[k] where bit k of found
-__device__ __forceinline__ void real_roots10(const double (&a)[11], double (&crit)[10], uint32_t &found) {
+// a[10] != 0 required; root k (ascending) is L.NX[64 k] where bit k of found
+__device__ __forceinline__ void real_roots10(const double (&a)[11], const RootsLds &L, uint32_t &found) {
     double r = 1.0;
     const double an = fabs(a[10]);
     for (int it = 0; it < 2100; it++) {
@@ -541,7 +543,7 @@ __device__ __forceinline__ void real_roots10(const double (&a)[11], double (&cri
         if (an * r > t) break;
         r = r * 2.0;
     }
-    roots_level<1>(a, r, crit, found);
+    roots_level<1>(a, r, L, found);
 }
 
 __device__ __forceinline__ double det3p(const double (&P)[3][4]) {
