@@ -41,8 +41,12 @@ def parse():
                     help="default: 2.0 px (cfg2/cfg3), 0.002 (cfg4, normalised coordinates)")
     ap.add_argument("--chunks", type=int, default=None, help="score point chunks (default 8 homography, 96 two-view)")
     ap.add_argument("--dlt", choices=["thin", "nullspace"], default="thin")
-    ap.add_argument("--sprt", action="store_true",
-                    help="batch SPRT verification (reference initial epsilon/delta for the estimator)")
+    ap.add_argument("--sprt", action="store_true", default=None,
+                    help="batch SPRT verification (reference initial epsilon/delta for the estimator); "
+                         "default on for fundamental (cfg3), off otherwise")
+    ap.add_argument("--no-sprt", dest="sprt", action="store_false")
+    ap.add_argument("--sampler", choices=["uniform", "prosac"], default=None,
+                    help="device sampler of the batches (default prosac for fundamental = cfg3, else uniform)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cfg5", action="store_true",
@@ -60,6 +64,11 @@ def parse():
         args.threshold = 0.002 if ess else 2.0
     if args.chunks is None:
         args.chunks = 8 if args.estimator == "homography" else 96
+    fund = args.estimator == "fundamental"
+    if args.sprt is None:
+        args.sprt = fund
+    if args.sampler is None:
+        args.sampler = "prosac" if fund else "uniform"
     return args
 
 
@@ -278,6 +287,8 @@ def main():
     for c in ctxs:
         c.set_dlt_mode(dlt_mode)
         c.set_score_chunks(args.chunks)
+        if args.sampler == "prosac":  # points are quality-sorted (synthetic generator)
+            c.set_device_sampler(usac.SAMPLER.Prosac)
     ctx = ctxs[0]
     if world > 1:
         uid = [usac.Context.comm_unique_id() if rank == 0 else None]
@@ -376,6 +387,7 @@ def main():
         kshort = ("k_sprt_head/tail<%d>" % (3 if fund else 4 if ess else 2)) if args.sprt else \
             (("k_score_f2<%d,%s>" % (args.chunks, "E" if ess else "F")) if (fund or ess) else
              ("k_score_hf<%d,false>" % args.chunks))
+        smp_name = "Prosac (reference subset schedule, T_N = 200000)" if args.sampler == "prosac" else "Uniform"
         out = {
             "metric": "model hypotheses/sec (sample+solve+score) and inlier-count match vs ref",
             "value": value,
@@ -392,16 +404,17 @@ def main():
                      "synthetic (SURVEY §8(d) cfg4 generator: cfg3 geometry in K^-1-normalised coordinates)" if ess
                      else "synthetic (SURVEY §8(d) cfg2 generator: 30% inliers, 1 px noise, 70% uniform outliers)"),
             "config": {"workload": ("cfg3%s: Fundamental_estimator (7-pt, oriented filter, Sampson) + "
-                                    "Uniform sampler (device xorshift), %d correspondences, %d-hypothesis batch per "
-                                    "GPU, %.3f models/sample" % (" + batch SPRT" if args.sprt else " without SPRT", n, B,
-                                                                 models_per_hyp)) if fund else
-                                   ("cfg4%s: Essential_estimator (5-pt, cheirality, epipolar distance) + Uniform "
-                                    "sampler (device xorshift), %d correspondences, %d-hypothesis batch per GPU, "
-                                    "%.3f models/sample" % (" + batch SPRT" if args.sprt else "", n, B,
+                                    "%s sampler (device stream), %d correspondences, %d-hypothesis batch per "
+                                    "GPU, %.3f models/sample" % (" + batch SPRT" if args.sprt else " without SPRT",
+                                                                 smp_name, n, B, models_per_hyp)) if fund else
+                                   ("cfg4%s: Essential_estimator (5-pt, cheirality, epipolar distance) + %s "
+                                    "sampler (device stream), %d correspondences, %d-hypothesis batch per GPU, "
+                                    "%.3f models/sample" % (" + batch SPRT" if args.sprt else "", smp_name, n, B,
                                                             models_per_hyp)) if ess else
-                                   ("cfg2%s: Homography_estimator (4-pt DLT, %s) + Uniform sampler (device "
-                                    "xorshift), %d correspondences, %d-hypothesis batch per GPU" %
-                                    (" + batch SPRT" if args.sprt else "", args.dlt, n, B)),
+                                   ("cfg2%s: Homography_estimator (4-pt DLT, %s) + %s sampler (device "
+                                    "stream), %d correspondences, %d-hypothesis batch per GPU" %
+                                    (" + batch SPRT" if args.sprt else "", args.dlt, smp_name, n, B)),
+                       "sampler": args.sampler,
                        "n_points": n, "batch_per_gpu": B, "threshold": args.threshold,
                        "score_chunks": args.chunks, "batches_in_flight": P,
                        "parallelism": "hypothesis-sharded x%d" % world},

@@ -29,6 +29,8 @@
  *   usac_set_sprt / usac_sprt_tested  SPRT::verifyModelAndGetModelScore as a batch test
  *                                  (sprt.hpp:191-317, 332-355)
  *   usac_prosac_samples            ProsacSampler::generateSample (prosac_sampler.hpp:117-172)
+ *   usac_set_device_sampler        Sampler choice of the throughput batches (Uniform / PROSAC
+ *   usac_draw_samples              schedule, prosac_sampler.hpp:62-172) and its samples
  *   usac_sprt_pool                 SPRT ctor pool + A0 (sprt.hpp:89-175)
  *   usac_ransac_run                Ransac::run + RansacOutput (ransac.cpp:14-238,
  *                                  ransac_output.hpp:29-97), Uniform sampler
@@ -47,7 +49,7 @@
 extern "C" {
 #endif
 
-#define USAC_ABI_VERSION 3
+#define USAC_ABI_VERSION 4
 
 /* = enum ESTIMATOR (usac/model.hpp:10) */
 enum { USAC_LINE2D = 1, USAC_HOMOGRAPHY = 2, USAC_FUNDAMENTAL = 3, USAC_ESSENTIAL = 4 };
@@ -177,6 +179,17 @@ int usac_set_score_variant(usac_ctx *ctx, int variant);
 int usac_set_sprt(usac_ctx *ctx, int enable, uint32_t seed, double epsilon, double delta);
 /* pool points the SPRT tested in the last batch (the scoring work actually done) */
 int usac_sprt_tested(usac_ctx *ctx, uint64_t *points_tested);
+/* Sampler of the throughput batches' device stream (usac_hypothesize_score with samples ==
+ * NULL, usac_hypothesize_async): USAC_SAMPLER_UNIFORM (default) or USAC_SAMPLER_PROSAC --
+ * hypothesis h (the global index first_hyp + b) uses the reference's PROSAC subset schedule
+ * (growth function prosac_sampler.hpp:62-114, termination_length = n; points must be sorted
+ * by quality): the subset's last point plus m - 1 distinct points before it, for
+ * h < T_N = 200000, uniform afterwards (prosac_sampler.hpp:117-172).  The random draws are
+ * the device SplitMix64 stream, not the host mt19937 (usac_ransac_run keeps that one). */
+int usac_set_device_sampler(usac_ctx *ctx, int sampler);
+/* The device stream's samples for hypotheses first_hyp .. first_hyp + B - 1 (B x m int32,
+ * host memory): what the solve kernels draw.  For tests. */
+int usac_draw_samples(usac_ctx *ctx, uint32_t B, uint64_t seed, uint64_t first_hyp, int32_t *out);
 
 /* ---- loop --------------------------------------------------------------------- */
 uint32_t usac_std_termination(uint32_t inliers, uint32_t points_size, uint32_t sample_size, float desired_prob,

@@ -96,7 +96,8 @@ ABI_SYMBOLS = [
     "usac_num_points", "usac_estimate_models", "usac_score_models", "usac_get_inliers", "usac_nonminimal",
     "usac_hypothesize_score", "usac_hypothesize_async", "usac_fetch_best", "usac_sync", "usac_last_timings",
     "usac_set_score_chunks", "usac_set_score_variant", "usac_std_termination", "usac_ransac_run", "usac_uniform_samples",
-    "usac_prosac_samples", "usac_sprt_pool", "usac_set_sprt", "usac_sprt_tested",
+    "usac_prosac_samples", "usac_sprt_pool", "usac_set_sprt", "usac_sprt_tested", "usac_set_device_sampler",
+    "usac_draw_samples",
     "usac_comm_unique_id", "usac_comm_init", "usac_allgather_records", "usac_merge_records",
 ]
 
@@ -151,6 +152,8 @@ def lib():
         "usac_sprt_pool": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, u32p,
                                           _P(ctypes.c_double)]),
         "usac_set_sprt": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_double, ctypes.c_double]),
+        "usac_set_device_sampler": (ctypes.c_int, [_vp, ctypes.c_int]),
+        "usac_draw_samples": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, _vp]),
         "usac_sprt_tested": (ctypes.c_int, [_vp, _P(ctypes.c_uint64)]),
         "usac_comm_unique_id": (ctypes.c_int, [u8p]),
         "usac_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, u8p]),
@@ -325,6 +328,18 @@ class Context:
         """Batch SPRT verification for the throughput entry points (reference defaults when
         epsilon / delta are 0)."""
         self._check(lib().usac_set_sprt(self._h, 1 if enable else 0, seed, epsilon, delta), "set_sprt")
+
+    def set_device_sampler(self, sampler):
+        """Sampler of the throughput batches' device stream: SAMPLER.Uniform or SAMPLER.Prosac
+        (the reference's PROSAC subset schedule; points sorted by quality)."""
+        self._check(lib().usac_set_device_sampler(self._h, int(sampler)), "set_device_sampler")
+
+    def draw_samples(self, B, seed, first_hyp=0):
+        """The device stream's samples for hypotheses first_hyp .. first_hyp + B - 1 (B x m)."""
+        out = np.zeros((B, self.m), dtype=np.int32)
+        self._check(lib().usac_draw_samples(self._h, B, seed, first_hyp, out.ctypes.data_as(ctypes.c_void_p)),
+                    "draw_samples")
+        return out
 
     def sprt_tested(self):
         t = ctypes.c_uint64(0)

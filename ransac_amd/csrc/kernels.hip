@@ -25,7 +25,7 @@ namespace usac {
 // ------------------------------------------------------------------------ solve (H, 4-pt)
 __global__ __launch_bounds__(64) void k_solve_h4(const float4 *__restrict__ pts, uint32_t n,
                                                  const int32_t *__restrict__ samples_in, int32_t *samples_out,
-                                                 uint32_t B, uint64_t seed, uint64_t first_hyp, int nullspace,
+                                                 uint32_t B, DevSampler ds, uint64_t first_hyp, int nullspace,
                                                  float *__restrict__ models) {
     const uint32_t h = blockIdx.x * 64 + threadIdx.x;
     if (h >= B) return;
@@ -34,7 +34,7 @@ __global__ __launch_bounds__(64) void k_solve_h4(const float4 *__restrict__ pts,
 #pragma unroll
         for (int i = 0; i < 4; i++) s[i] = samples_in[4 * (size_t)h + i];
     } else {
-        draw_sample<4>(seed, first_hyp + h, n, s);
+        draw_sample<4>(ds, first_hyp + h, n, s);
         if (samples_out) {
 #pragma unroll
             for (int i = 0; i < 4; i++) samples_out[4 * (size_t)h + i] = s[i];
@@ -413,7 +413,7 @@ __global__ __launch_bounds__(64) void k_presort_h(const float4 *__restrict__ rec
 // ------------------------------------------------------------------------ line2d
 __global__ __launch_bounds__(256) void k_solve_line(const float2 *__restrict__ pts, uint32_t n,
                                                     const int32_t *__restrict__ samples_in, int32_t *samples_out,
-                                                    uint32_t B, uint64_t seed, uint64_t first_hyp,
+                                                    uint32_t B, DevSampler ds, uint64_t first_hyp,
                                                     float *__restrict__ models) {
     const uint32_t h = blockIdx.x * 256 + threadIdx.x;
     if (h >= B) return;
@@ -422,7 +422,7 @@ __global__ __launch_bounds__(256) void k_solve_line(const float2 *__restrict__ p
         s[0] = samples_in[2 * (size_t)h];
         s[1] = samples_in[2 * (size_t)h + 1];
     } else {
-        draw_sample<2>(seed, first_hyp + h, n, s);
+        draw_sample<2>(ds, first_hyp + h, n, s);
         if (samples_out) {
             samples_out[2 * (size_t)h] = s[0];
             samples_out[2 * (size_t)h + 1] = s[1];
@@ -569,9 +569,9 @@ __global__ __launch_bounds__(256) void k_argmax_final(const BestEntry *__restric
 #define LAUNCH_CHECK() hipGetLastError()
 
 hipError_t launch_solve_h4(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
-                           int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, int nullspace,
+                           int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, int nullspace,
                            float *models) {
-    hipLaunchKernelGGL(k_solve_h4, dim3((B + 63) / 64), dim3(64), 0, st, pts, n, samples_in, samples_out, B, seed,
+    hipLaunchKernelGGL(k_solve_h4, dim3((B + 63) / 64), dim3(64), 0, st, pts, n, samples_in, samples_out, B, ds,
                        first_hyp, nullspace, models);
     return LAUNCH_CHECK();
 }
@@ -632,9 +632,33 @@ hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const flo
     return LAUNCH_CHECK();
 }
 
+template <int M>
+__global__ __launch_bounds__(256) void k_draw_samples(uint32_t n, uint32_t B, DevSampler ds, uint64_t first_hyp,
+                                                      int32_t *__restrict__ out) {
+    const uint32_t h = blockIdx.x * 256 + threadIdx.x;
+    if (h >= B) return;
+    int32_t s[M];
+    draw_sample<M>(ds, first_hyp + h, n, s);
+#pragma unroll
+    for (int i = 0; i < M; i++) out[(size_t)M * h + i] = s[i];
+}
+
+hipError_t launch_draw_samples(hipStream_t st, int m, uint32_t n, uint32_t B, DevSampler ds, uint64_t first_hyp,
+                               int32_t *out) {
+    const dim3 g((B + 255) / 256), b(256);
+    switch (m) {
+        case 2: hipLaunchKernelGGL(k_draw_samples<2>, g, b, 0, st, n, B, ds, first_hyp, out); break;
+        case 4: hipLaunchKernelGGL(k_draw_samples<4>, g, b, 0, st, n, B, ds, first_hyp, out); break;
+        case 5: hipLaunchKernelGGL(k_draw_samples<5>, g, b, 0, st, n, B, ds, first_hyp, out); break;
+        case 7: hipLaunchKernelGGL(k_draw_samples<7>, g, b, 0, st, n, B, ds, first_hyp, out); break;
+        default: return hipErrorInvalidValue;
+    }
+    return LAUNCH_CHECK();
+}
+
 hipError_t launch_solve_line(hipStream_t st, const float2 *pts, uint32_t n, const int32_t *samples_in,
-                             int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, float *models) {
-    hipLaunchKernelGGL(k_solve_line, dim3((B + 255) / 256), dim3(256), 0, st, pts, n, samples_in, samples_out, B, seed,
+                             int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, float *models) {
+    hipLaunchKernelGGL(k_solve_line, dim3((B + 255) / 256), dim3(256), 0, st, pts, n, samples_in, samples_out, B, ds,
                        first_hyp, models);
     return LAUNCH_CHECK();
 }

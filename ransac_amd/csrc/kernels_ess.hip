@@ -58,7 +58,7 @@ size_t e5_workspace_bytes(uint32_t B) {
 
 __global__ __launch_bounds__(64) void k_e5_basis(const float4 *__restrict__ pts, uint32_t n,
                                                  const int32_t *__restrict__ samples_in, int32_t *samples_out,
-                                                 uint32_t B, uint64_t seed, uint64_t first_hyp, E5Work w) {
+                                                 uint32_t B, DevSampler ds, uint64_t first_hyp, E5Work w) {
     const uint32_t h = blockIdx.x * 64 + threadIdx.x;
     if (h >= B) return;
     int32_t s[5];
@@ -66,7 +66,7 @@ __global__ __launch_bounds__(64) void k_e5_basis(const float4 *__restrict__ pts,
 #pragma unroll
         for (int i = 0; i < 5; i++) s[i] = samples_in[5 * (size_t)h + i];
     } else {
-        draw_sample<5>(seed, first_hyp + h, n, s);
+        draw_sample<5>(ds, first_hyp + h, n, s);
         if (samples_out) {
 #pragma unroll
             for (int i = 0; i < 5; i++) samples_out[5 * (size_t)h + i] = s[i];
@@ -238,14 +238,14 @@ __global__ __launch_bounds__(64) void k_e5_select(uint32_t B, E5Work w, float *_
 }
 
 hipError_t launch_solve_e5(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
-                           int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, float *models,
+                           int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, float *models,
                            int32_t *counts, uint32_t *list, uint32_t *list_n, void *workspace) {
     const E5Work w = e5_carve(workspace, B);
     hipError_t e = hipMemsetAsync(list_n, 0, sizeof(uint32_t), st);
     if (e == hipSuccess) e = hipMemsetAsync(w.npairs, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     const dim3 g1((B + 63) / 64), g11((11 * B + 63) / 64), g10((10 * B + 63) / 64);
-    hipLaunchKernelGGL(k_e5_basis, g1, dim3(64), 0, st, pts, n, samples_in, samples_out, B, seed, first_hyp, w);
+    hipLaunchKernelGGL(k_e5_basis, g1, dim3(64), 0, st, pts, n, samples_in, samples_out, B, ds, first_hyp, w);
     hipLaunchKernelGGL(k_e5_dets, g11, dim3(64), 0, st, B, w);
     hipLaunchKernelGGL(k_e5_roots, g1, dim3(64), 0, st, B, w);
     hipLaunchKernelGGL(k_e5_check, g10, dim3(64), 0, st, pts, B, 10 * B, w);

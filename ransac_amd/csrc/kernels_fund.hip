@@ -21,7 +21,7 @@ namespace usac {
 // IEEE cubic roots -> F per root -> oriented filter -> slot write + compaction.
 __global__ __launch_bounds__(64) void k_solve_f7(const float4 *__restrict__ pts, uint32_t n,
                                                  const int32_t *__restrict__ samples_in, int32_t *samples_out,
-                                                 uint32_t B, uint64_t seed, uint64_t first_hyp,
+                                                 uint32_t B, DevSampler ds, uint64_t first_hyp,
                                                  float *__restrict__ models, int32_t *__restrict__ counts,
                                                  uint32_t *__restrict__ list, uint32_t *__restrict__ list_n) {
     const uint32_t lane = threadIdx.x;
@@ -35,7 +35,7 @@ __global__ __launch_bounds__(64) void k_solve_f7(const float4 *__restrict__ pts,
 #pragma unroll
             for (int i = 0; i < 7; i++) s[i] = samples_in[7 * (size_t)h + i];
         } else {
-            draw_sample<7>(seed, first_hyp + h, n, s);
+            draw_sample<7>(ds, first_hyp + h, n, s);
             if (samples_out) {
 #pragma unroll
                 for (int i = 0; i < 7; i++) samples_out[7 * (size_t)h + i] = s[i];
@@ -490,11 +490,11 @@ size_t tv_scratch_bytes(uint32_t kmax, int chunks) {
 }
 
 hipError_t launch_solve_f7(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
-                           int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, float *models,
+                           int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, float *models,
                            int32_t *counts, uint32_t *list, uint32_t *list_n) {
     hipError_t e = hipMemsetAsync(list_n, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_solve_f7, dim3((B + 63) / 64), dim3(64), 0, st, pts, n, samples_in, samples_out, B, seed,
+    hipLaunchKernelGGL(k_solve_f7, dim3((B + 63) / 64), dim3(64), 0, st, pts, n, samples_in, samples_out, B, ds,
                        first_hyp, models, counts, list, list_n);
     return hipGetLastError();
 }

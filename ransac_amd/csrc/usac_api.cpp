@@ -57,6 +57,8 @@ struct usac_ctx {
     hipStream_t stream = nullptr;
     DevBuf pts;
     DevBuf rec;             // fast-kernel point records (32 B / point)
+    DevBuf prosac_tab;      // device PROSAC schedule: subset size per hypothesis (< T_N)
+    int dev_sampler = USAC_SAMPLER_UNIFORM;
     DevBuf tv_part;         // two-view scorer scratch: pre-sort permutation, chunk partials
     DevBuf perm;            // hypothesis pre-sort order of the fast kernel (B + 2 uint32)
     float rec_thr = -1.f;   // threshold the record bands were built for
@@ -146,24 +148,31 @@ int ensure_single(usac_ctx *c) {
     return USAC_OK;
 }
 
+usac::DevSampler dev_sampler(const usac_ctx *c, uint64_t seed) {
+    const bool prosac = c->dev_sampler == USAC_SAMPLER_PROSAC;
+    return usac::DevSampler{seed, prosac ? c->prosac_tab.as<uint32_t>() : nullptr,
+                            prosac ? (uint32_t)(c->prosac_tab.bytes / sizeof(uint32_t)) : 0u};
+}
+
 // solve (samples on device, or device RNG when samples_dev == nullptr) into c->models
 hipError_t enqueue_solve(usac_ctx *c, const int32_t *samples_dev, uint32_t B, uint64_t seed, uint64_t first_hyp,
                          int32_t *samples_out) {
+    const usac::DevSampler ds = dev_sampler(c, seed);
     if (is_e(c)) {
         hipError_t e = c->e5_ws.reserve(usac::e5_workspace_bytes(B));
         if (e != hipSuccess) return e;
-        return usac::launch_solve_e5(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, seed,
+        return usac::launch_solve_e5(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, ds,
                                      first_hyp, c->models.as<float>(), c->counts.as<int32_t>(),
                                      c->list.as<uint32_t>(), c->list_n.as<uint32_t>(), c->e5_ws.p);
     }
     if (is_f(c))
-        return usac::launch_solve_f7(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, seed,
+        return usac::launch_solve_f7(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, ds,
                                      first_hyp, c->models.as<float>(), c->counts.as<int32_t>(),
                                      c->list.as<uint32_t>(), c->list_n.as<uint32_t>());
     if (is_h(c))
-        return usac::launch_solve_h4(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, seed,
+        return usac::launch_solve_h4(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, ds,
                                      first_hyp, c->dlt_mode == USAC_DLT_NULLSPACE, c->models.as<float>());
-    return usac::launch_solve_line(c->stream, c->pts.as<float2>(), c->n, samples_dev, samples_out, B, seed, first_hyp,
+    return usac::launch_solve_line(c->stream, c->pts.as<float2>(), c->n, samples_dev, samples_out, B, ds, first_hyp,
                                    c->models.as<float>());
 }
 
@@ -436,7 +445,7 @@ void usac_destroy(usac_ctx *c) {
                       &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
                       &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->inl_scratch, &c->lo_idx, &c->e5_ws, &c->one_model,
                       &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok,
-                      &c->rec_send, &c->rec_all, &c->tv_part})
+                      &c->rec_send, &c->rec_all, &c->tv_part, &c->prosac_tab})
         b->release();
     for (auto &ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -656,6 +665,40 @@ int usac_uniform_samples(uint32_t seed, uint32_t n_points, uint32_t m, uint32_t 
     if (!out || n_points == 0 || m == 0) return USAC_ERR_ARG;
     usac::UniformSampler s(seed, n_points, m);
     for (uint32_t i = 0; i < count; i++) s.generateSample(out + (size_t)i * m);
+    return USAC_OK;
+}
+
+int usac_set_device_sampler(usac_ctx *c, int sampler) {
+    if (!c || (sampler != USAC_SAMPLER_UNIFORM && sampler != USAC_SAMPLER_PROSAC)) return USAC_ERR_ARG;
+    if (sampler == USAC_SAMPLER_PROSAC) {
+        if (c->n < c->m) return fail(c, USAC_ERR_ARG, "PROSAC needs n >= sample size");
+        // the subset sequence of ProsacSampler::generateSample with termination_length = n
+        usac::ProsacSampler ps(1, c->n, c->m);
+        const uint32_t T = usac::ProsacSampler::kGrowthMax;
+        std::vector<int32_t> smp(c->m);
+        std::vector<uint32_t> tab(T);
+        for (uint32_t h = 0; h < T; h++) {
+            ps.generateSample(smp.data(), c->n);
+            tab[h] = ps.subset();
+        }
+        HIP_TRY(c, hipSetDevice(c->device));
+        HIP_TRY(c, c->prosac_tab.reserve(sizeof(uint32_t) * T));
+        HIP_TRY(c, hipMemcpy(c->prosac_tab.p, tab.data(), sizeof(uint32_t) * T, hipMemcpyHostToDevice));
+        c->prosac_tab.bytes = sizeof(uint32_t) * T;
+    }
+    c->dev_sampler = sampler;
+    return USAC_OK;
+}
+
+int usac_draw_samples(usac_ctx *c, uint32_t B, uint64_t seed, uint64_t first_hyp, int32_t *out) {
+    if (!c || !out || B == 0) return USAC_ERR_ARG;
+    int rc = ensure_batch(c, B);
+    if (rc) return rc;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, usac::launch_draw_samples(c->stream, (int)c->m, c->n, B, dev_sampler(c, seed), first_hyp,
+                                         c->samples.as<int32_t>()));
+    HIP_TRY(c, hipMemcpyAsync(out, c->samples.p, sizeof(int32_t) * (size_t)B * c->m, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     return USAC_OK;
 }
 

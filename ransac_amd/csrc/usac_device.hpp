@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "usac_kernels.h"
+
 namespace usac {
 
 // ---------------------------------------------------------------- counter-based sampler
@@ -22,9 +24,9 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t &s) {
     return z ^ (z >> 31);
 }
 
+// m distinct indices in [0, n) from the (seed, hyp) stream
 template <int M>
-__device__ __forceinline__ void draw_sample(uint64_t seed, uint64_t hyp, uint32_t n, int32_t (&s)[M]) {
-    uint64_t st = seed ^ (hyp * 0xD1B54A32D192ED03ull);
+__device__ __forceinline__ void draw_unique(uint64_t &st, uint32_t n, int32_t *s) {
 #pragma unroll
     for (int i = 0; i < M; i++) {
         int32_t v;
@@ -37,6 +39,20 @@ __device__ __forceinline__ void draw_sample(uint64_t seed, uint64_t hyp, uint32_
             for (int j = 0; j < i; j++) dup |= (s[j] == v);
         } while (dup);
         s[i] = v;
+    }
+}
+
+// UniformSampler (device stream) or PROSAC: the last point of the current subset plus
+// m - 1 distinct points of the ones before it (prosac_sampler.hpp:160-168)
+template <int M>
+__device__ __forceinline__ void draw_sample(const DevSampler &ds, uint64_t hyp, uint32_t n, int32_t (&s)[M]) {
+    uint64_t st = ds.seed ^ (hyp * 0xD1B54A32D192ED03ull);
+    if (ds.prosac && hyp < ds.prosac_len) {
+        const uint32_t sub = ds.prosac[hyp];  // >= M
+        draw_unique<M - 1>(st, sub - 1, s);
+        s[M - 1] = (int32_t)sub - 1;
+    } else {
+        draw_unique<M>(st, n, s);
     }
 }
 

@@ -9,8 +9,23 @@
 
 namespace usac {
 
+// Throughput-path sampler state (one per batch): the SplitMix64 stream keyed by (seed,
+// hypothesis index), and optionally the PROSAC schedule -- prosac[h] = the subset size the
+// reference's ProsacSampler uses for hypothesis h (prosac_sampler.hpp:117-172, growth
+// function of :62-114, termination_length = N) for h < prosac_len; later hypotheses are
+// uniform, as the reference's are after T_N = 200000.
+struct DevSampler {
+    uint64_t seed;
+    const uint32_t *prosac;  // nullptr: uniform sampler
+    uint32_t prosac_len;
+};
+
+// device-drawn samples only (B x m int32), the stream the solve kernels use
+hipError_t launch_draw_samples(hipStream_t st, int m, uint32_t n, uint32_t B, DevSampler ds, uint64_t first_hyp,
+                               int32_t *out);
+
 hipError_t launch_solve_h4(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
-                           int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, int nullspace,
+                           int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, int nullspace,
                            float *models);
 hipError_t launch_prepare_h(hipStream_t st, const float *in, uint32_t B, float *models);
 hipError_t launch_score_h(hipStream_t st, int chunks, const float4 *pts, uint32_t n, const float *models, uint32_t B,
@@ -23,7 +38,7 @@ hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const flo
                            const float *models, uint32_t B, float thr, uint32_t *perm, int32_t *counts, float *sums);
 
 hipError_t launch_solve_line(hipStream_t st, const float2 *pts, uint32_t n, const int32_t *samples_in,
-                             int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, float *models);
+                             int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, float *models);
 hipError_t launch_prepare_line(hipStream_t st, const float *in, uint32_t B, float *models);
 hipError_t launch_score_line(hipStream_t st, int chunks, const float2 *pts, uint32_t n, const float *models,
                              uint32_t B, float thr, int32_t *counts, float *sums);
@@ -36,7 +51,7 @@ hipError_t launch_argmax(hipStream_t st, const int32_t *counts, const float *sum
 // fundamental (kernels_fund.hip): slots 3*b + j, counts -1 on empty slots, list/list_n =
 // occupied slots (list_n zeroed by the launcher)
 hipError_t launch_solve_f7(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
-                           int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, float *models,
+                           int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, float *models,
                            int32_t *counts, uint32_t *list, uint32_t *list_n);
 hipError_t launch_prepare_f(hipStream_t st, const float *in, uint32_t K, float *models);
 // list == nullptr: lanes = slots 0..kmax-1; else lanes walk list[0 .. *list_n) (<= kmax);
@@ -55,7 +70,7 @@ size_t tv_scratch_bytes(uint32_t kmax, int chunks);
 // essential 5-point (kernels_ess.hip): one slot per sample (models [9][B], counts 0 / -1,
 // list / list_n); workspace = e5_workspace_bytes(B)
 hipError_t launch_solve_e5(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
-                           int32_t *samples_out, uint32_t B, uint64_t seed, uint64_t first_hyp, float *models,
+                           int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, float *models,
                            int32_t *counts, uint32_t *list, uint32_t *list_n, void *workspace);
 size_t e5_workspace_bytes(uint32_t B);
 hipError_t launch_nonminimal_f(hipStream_t st, const float4 *pts, const int32_t *idx, uint32_t n, float4 *q,
