@@ -12,8 +12,9 @@ run() {  # name, args...
 run h_cfg2
 run h_sprt_b262k --sprt --batch 262144 --cpu-seconds 0
 run f_cfg3 --estimator fundamental
-run f_b262k --estimator fundamental --batch 262144 --cpu-seconds 0
-run f_sprt_b262k --estimator fundamental --sprt --batch 262144 --cpu-seconds 0
+run f_full_uniform --estimator fundamental --no-sprt --sampler uniform --cpu-seconds 0
+run f_full_b262k --estimator fundamental --no-sprt --sampler uniform --batch 262144 --cpu-seconds 0
+run f_cfg3_b262k --estimator fundamental --batch 262144 --cpu-seconds 0
 run e_cfg4 --estimator essential
 run e_b262k --estimator essential --batch 262144 --cpu-seconds 0
 run e_sprt --estimator essential --sprt --cpu-seconds 0
