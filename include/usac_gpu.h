@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define USAC_ABI_VERSION 4
+#define USAC_ABI_VERSION 5
 
 /* = enum ESTIMATOR (usac/model.hpp:10) */
 enum { USAC_LINE2D = 1, USAC_HOMOGRAPHY = 2, USAC_FUNDAMENTAL = 3, USAC_ESSENTIAL = 4 };
@@ -117,6 +117,9 @@ typedef struct usac_run_output {
     uint32_t rollbacks;         /* PROSAC speculative batches cut short by a termination_length change */
     uint32_t lo_inner_iters;    /* getLOIters (ransac_output.hpp): inner LO iterations */
     uint32_t lo_iterative_iters;
+    uint32_t lo_rounds;         /* LO speculation rounds (batches of inner iterations run at once) */
+    uint32_t lo_stages;         /* LO device stages (one batched fit or one batched scoring each) */
+    uint32_t sum_models;        /* models whose exact sequential Σerr the replay needed */
 } usac_run_output;
 
 /* ---- lifetime ----------------------------------------------------------------- */

@@ -46,32 +46,50 @@ __device__ __forceinline__ void inl_model(const float *model, float *sm) {
     __syncthreads();
 }
 
+// Batched over W models: blockIdx.y = model w (model w at models + 9 w, threshold thrs[w]
+// or the scalar thr).  Per model the scratch holds its block counts (nb padded to 64)
+// followed by its compacted residuals (n floats): inl_stride(n) words.  Every model's
+// result is exactly the single-model one (the kernels never mix models).
+__host__ __device__ __forceinline__ size_t inl_stride(uint32_t n) {
+    const uint32_t nb = (n + kInlBlock - 1) / kInlBlock;
+    return (size_t)((nb + 63) & ~63u) + n;
+}
+
+// model slot of workgroup row b: slots[b] when a slot list is given (a subset of the W models)
+__device__ __forceinline__ uint32_t inl_slot(const uint32_t *slots, uint32_t b) { return slots ? slots[b] : b; }
+
 template <int EST>
 __global__ __launch_bounds__(kInlBlock) void k_inl_flags(const void *__restrict__ pts, uint32_t n,
-                                                         const float *__restrict__ model, float thr,
-                                                         uint32_t *__restrict__ block_counts) {
+                                                         const float *__restrict__ models, float thr,
+                                                         const float *__restrict__ thrs,
+                                                         const uint32_t *__restrict__ slots,
+                                                         uint32_t *__restrict__ scratch) {
     __shared__ float sm[18];
     __shared__ uint32_t wsum[kInlBlock / 64];
-    inl_model<EST>(model, sm);
+    const uint32_t w = inl_slot(slots, blockIdx.y);
+    inl_model<EST>(models + 9 * (size_t)w, sm);
+    const float t = thrs ? thrs[w] : thr;
     float m[18];
 #pragma unroll
     for (int k = 0; k < 18; k++) m[k] = sm[k];
     const uint32_t i = blockIdx.x * kInlBlock + threadIdx.x;
-    const bool in = i < n && inl_error<EST>(m, pts, i) < thr;
+    const bool in = i < n && inl_error<EST>(m, pts, i) < t;
     const uint64_t bal = __ballot(in);
     if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = (uint32_t)__popcll(bal);
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t t = 0;
-        for (uint32_t w = 0; w < kInlBlock / 64; w++) t += wsum[w];
-        block_counts[blockIdx.x] = t;
+        uint32_t tot = 0;
+        for (uint32_t w = 0; w < kInlBlock / 64; w++) tot += wsum[w];
+        scratch[w * inl_stride(n) + blockIdx.x] = tot;
     }
 }
 
-__global__ __launch_bounds__(1024) void k_inl_scan(uint32_t *__restrict__ block_counts, uint32_t nblocks,
-                                                   int32_t *__restrict__ total) {
+__global__ __launch_bounds__(1024) void k_inl_scan(uint32_t *__restrict__ scratch, uint32_t n, uint32_t nblocks,
+                                                   const uint32_t *__restrict__ slots, int32_t *__restrict__ totals) {
     // exclusive scan in place, 1024 threads, sequential chunks per thread
     __shared__ uint32_t part[1024];
+    const uint32_t w = inl_slot(slots, blockIdx.x);
+    uint32_t *block_counts = scratch + w * inl_stride(n);
     const uint32_t t = threadIdx.x;
     const uint32_t per = (nblocks + 1023) / 1024;
     const uint32_t b0 = t * per, b1 = b0 + per < nblocks ? b0 + per : nblocks;
@@ -91,23 +109,31 @@ __global__ __launch_bounds__(1024) void k_inl_scan(uint32_t *__restrict__ block_
         block_counts[b] = run;
         run += c;
     }
-    if (t == 1023) *total = (int32_t)part[1023];
+    if (t == 1023) totals[w] = (int32_t)part[1023];
 }
 
 template <int EST>
 __global__ __launch_bounds__(kInlBlock) void k_inl_compact(const void *__restrict__ pts, uint32_t n,
-                                                           const float *__restrict__ model, float thr,
-                                                           const uint32_t *__restrict__ block_offsets,
-                                                           int32_t *__restrict__ idx, float *__restrict__ errs) {
+                                                           const float *__restrict__ models, float thr,
+                                                           const float *__restrict__ thrs,
+                                                           const uint32_t *__restrict__ slots,
+                                                           uint32_t *__restrict__ scratch, int32_t *__restrict__ idx,
+                                                           size_t idx_stride) {
     __shared__ float sm[18];
     __shared__ uint32_t wsum[kInlBlock / 64];
-    inl_model<EST>(model, sm);
+    const uint32_t ws = inl_slot(slots, blockIdx.y);
+    inl_model<EST>(models + 9 * (size_t)ws, sm);
+    const float t = thrs ? thrs[ws] : thr;
     float m[18];
 #pragma unroll
     for (int k = 0; k < 18; k++) m[k] = sm[k];
+    const size_t stride = inl_stride(n);
+    const uint32_t nb = (n + kInlBlock - 1) / kInlBlock;
+    const uint32_t *block_offsets = scratch + ws * stride;
+    float *errs = reinterpret_cast<float *>(scratch + ws * stride + ((nb + 63) & ~63u));
     const uint32_t i = blockIdx.x * kInlBlock + threadIdx.x;
     const float e = i < n ? inl_error<EST>(m, pts, i) : 0.f;
-    const bool in = i < n && e < thr;
+    const bool in = i < n && e < t;
     const uint64_t bal = __ballot(in);
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) wsum[wave] = (uint32_t)__popcll(bal);
@@ -116,21 +142,24 @@ __global__ __launch_bounds__(kInlBlock) void k_inl_compact(const void *__restric
     for (uint32_t w = 0; w < wave; w++) base += wsum[w];
     if (in) {
         const uint32_t r = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
-        idx[r] = (int32_t)i;
+        if (idx) idx[ws * idx_stride + r] = (int32_t)i;
         errs[r] = e;
     }
 }
 
-// sequential fp32 sum in point order (quality.hpp:85), one wave: 64 residuals per step are
-// loaded in parallel and added one after the other through v_readlane (no LDS round trip)
-// 256 threads stage 4096-residual chunks in LDS with coalesced loads; lane 0 adds them in
-// order (the reference's sequential fp32 sum, one dependent add per inlier)
+// the reference's sequential fp32 sum in point order (quality.hpp:85): 256 threads stage
+// 4096-residual chunks in LDS with coalesced loads; lane 0 adds them in order (one
+// dependent add per inlier -- the only inherently serial part).  One workgroup per model.
 constexpr uint32_t kSumChunk = 4096;
 
-__global__ __launch_bounds__(256) void k_inl_sum(const float *__restrict__ errs, const int32_t *__restrict__ total,
-                                                 float *__restrict__ sum) {
+__global__ __launch_bounds__(256) void k_inl_sum(const uint32_t *__restrict__ scratch, uint32_t n_pts,
+                                                 const uint32_t *__restrict__ slots,
+                                                 const int32_t *__restrict__ totals, float *__restrict__ sums) {
     __shared__ __attribute__((aligned(16))) float s_e[kSumChunk];
-    const uint32_t n = (uint32_t)*total;
+    const uint32_t nb = (n_pts + kInlBlock - 1) / kInlBlock;
+    const uint32_t w = inl_slot(slots, blockIdx.x);
+    const float *errs = reinterpret_cast<const float *>(scratch + w * inl_stride(n_pts) + ((nb + 63) & ~63u));
+    const uint32_t n = (uint32_t)totals[w];
     const uint32_t t = threadIdx.x;
     float s = 0.f;
     for (uint32_t c0 = 0; c0 < n; c0 += kSumChunk) {
@@ -162,21 +191,23 @@ __global__ __launch_bounds__(256) void k_inl_sum(const float *__restrict__ errs,
         }
         __syncthreads();
     }
-    if (t == 0) *sum = s;
+    if (t == 0) sums[w] = s;
 }
 
-hipError_t launch_inliers(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *model, float thr,
-                          int32_t *idx, int32_t *count, float *sum, void *scratch) {
-    // scratch: block counts (nblocks u32) followed by the compacted residuals (n floats)
+hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *models,
+                                uint32_t W, float thr, const float *thrs, const uint32_t *slots, int32_t *idx,
+                                size_t idx_stride, int32_t *counts, float *sums, void *scratch) {
+    if (W == 0) return hipSuccess;
     const uint32_t nb = (n + kInlBlock - 1) / kInlBlock;
-    uint32_t *bc = static_cast<uint32_t *>(scratch);
-    float *errs = reinterpret_cast<float *>(bc + ((nb + 63) & ~63u));
-#define INL(E)                                                                                                      \
-    do {                                                                                                            \
-        hipLaunchKernelGGL(k_inl_flags<E>, dim3(nb), dim3(kInlBlock), 0, st, pts, n, model, thr, bc);               \
-        hipLaunchKernelGGL(k_inl_scan, dim3(1), dim3(1024), 0, st, bc, nb, count);                                 \
-        hipLaunchKernelGGL(k_inl_compact<E>, dim3(nb), dim3(kInlBlock), 0, st, pts, n, model, thr, bc, idx, errs); \
-        hipLaunchKernelGGL(k_inl_sum, dim3(1), dim3(256), 0, st, errs, count, sum);                                \
+    uint32_t *scr = static_cast<uint32_t *>(scratch);
+    const dim3 grid(nb, W);
+#define INL(E)                                                                                                   \
+    do {                                                                                                         \
+        hipLaunchKernelGGL(k_inl_flags<E>, grid, dim3(kInlBlock), 0, st, pts, n, models, thr, thrs, slots, scr);        \
+        hipLaunchKernelGGL(k_inl_scan, dim3(W), dim3(1024), 0, st, scr, n, nb, slots, counts);                         \
+        hipLaunchKernelGGL(k_inl_compact<E>, grid, dim3(kInlBlock), 0, st, pts, n, models, thr, thrs, slots, scr, \
+                           idx, idx_stride);                                                                     \
+        hipLaunchKernelGGL(k_inl_sum, dim3(W), dim3(256), 0, st, scr, n, slots, counts, sums);                         \
     } while (0)
     switch (estimator) {
         case USAC_LINE2D: INL(USAC_LINE2D); break;
@@ -189,9 +220,11 @@ hipError_t launch_inliers(hipStream_t st, int estimator, const void *pts, uint32
     return hipGetLastError();
 }
 
-size_t inliers_scratch_bytes(uint32_t n) {
-    const uint32_t nb = (n + kInlBlock - 1) / kInlBlock;
-    return sizeof(uint32_t) * ((nb + 63) & ~63u) + sizeof(float) * (size_t)n;
+hipError_t launch_inliers(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *model, float thr,
+                          int32_t *idx, int32_t *count, float *sum, void *scratch) {
+    return launch_inliers_batch(st, estimator, pts, n, model, 1, thr, nullptr, nullptr, idx, 0, count, sum, scratch);
 }
+
+size_t inliers_scratch_bytes(uint32_t n, uint32_t W) { return sizeof(uint32_t) * inl_stride(n) * W; }
 
 }  // namespace usac

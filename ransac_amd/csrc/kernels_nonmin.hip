@@ -16,16 +16,24 @@ namespace usac {
 
 constexpr uint32_t kAtaBlock = 64;
 
+// Every kernel below is batched over W independent fits (blockIdx.y, or blockIdx.x for the
+// one-workgroup stages): fit w uses the index list base + w * base_stride (through the
+// positions pos + w * pos_stride when pos is given: idx_i = list[pos_i]), ns[w] points, and
+// its own slices of q / partial / ws / model_out / ok.  A fit never reads another fit's
+// data, so each result is exactly the single-fit one.
+
 // gather q[i] = pts[idx[i]] so the sequential passes read contiguous memory
-__global__ __launch_bounds__(256) void k_gather4(const float4 *__restrict__ pts, const int32_t *__restrict__ idx,
-                                                 uint32_t n, float4 *__restrict__ q) {
+template <class P>
+__global__ __launch_bounds__(256) void k_gather(const P *__restrict__ pts, const int32_t *__restrict__ base,
+                                                size_t base_stride, const int32_t *__restrict__ pos,
+                                                size_t pos_stride, const uint32_t *__restrict__ ns, uint32_t n1,
+                                                P *__restrict__ q, size_t q_stride) {
+    const uint32_t w = blockIdx.y;
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i < n) q[i] = pts[idx[i]];
-}
-__global__ __launch_bounds__(256) void k_gather2(const float2 *__restrict__ pts, const int32_t *__restrict__ idx,
-                                                 uint32_t n, float2 *__restrict__ q) {
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    if (i < n) q[i] = pts[idx[i]];
+    if (i >= (ns ? ns[w] : n1)) return;
+    const int32_t *list = base + w * base_stride;
+    const int32_t j = pos ? pos[w * pos_stride + i] : (int32_t)i;
+    q[w * q_stride + i] = pts[list[j]];
 }
 
 // normalizing transformation: lanes 0..3 = the four coordinate means, lanes 0..1 = the
@@ -36,8 +44,12 @@ __global__ __launch_bounds__(256) void k_gather2(const float2 *__restrict__ pts,
 // ws layout (floats): [0..8] T1, [9..17] T2.
 constexpr uint32_t kNormChunk = 2048;
 
-__global__ __launch_bounds__(256) void k_normalize(float4 *__restrict__ q, uint32_t n, float *ws) {
+__global__ __launch_bounds__(256) void k_normalize(float4 *__restrict__ q_all, size_t q_stride,
+                                                   const uint32_t *__restrict__ ns, uint32_t n1, float *ws_all) {
     __shared__ float4 s_pts[kNormChunk];
+    float4 *q = q_all + blockIdx.x * q_stride;
+    const uint32_t n = ns ? ns[blockIdx.x] : n1;
+    float *ws = ws_all + 18 * blockIdx.x;
     __shared__ double s_sq[2][kNormChunk];
     __shared__ float s_mean[4];
     __shared__ float s_scale[2];
@@ -141,10 +153,16 @@ __device__ __forceinline__ double sel9(const double *r, int j) {
 // block partials of A^T A: block c, lane e < 45 -> upper-triangle entry e (row-major j<=k).
 // FUND: one 8-point row per correspondence (eight_points.cpp:26-45), else two DLT rows.
 template <bool FUND>
-__global__ __launch_bounds__(64) void k_ata_partial(const float4 *__restrict__ q, uint32_t n,
-                                                    double *__restrict__ partial) {
+__global__ __launch_bounds__(64) void k_ata_partial(const float4 *__restrict__ q_all, size_t q_stride,
+                                                    const uint32_t *__restrict__ ns, uint32_t n1,
+                                                    double *__restrict__ partial_all,
+                                                    size_t p_stride) {
     const uint32_t e = threadIdx.x;
-    if (e >= 45) return;
+    const uint32_t w = blockIdx.y;
+    const uint32_t n = ns ? ns[w] : n1;
+    if (e >= 45 || (FUND ? n <= 8 : 2 * n <= 9) || blockIdx.x * kAtaBlock >= n) return;
+    const float4 *q = q_all + w * q_stride;
+    double *partial = partial_all + w * p_stride;
     int j = 0, k = e, rem = (int)e;
     for (int r = 0; r < 9; r++) {
         if (rem < 9 - r) {
@@ -200,13 +218,26 @@ __device__ void thin_solve(const float4 *q, double *v) {
 }
 
 template <bool FUND>
-__global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q, uint32_t n,
-                                                   const double *__restrict__ partial, uint32_t nblocks,
-                                                   const float *ws, float *model_out, int32_t *ok) {
+__global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_all, size_t q_stride,
+                                                   const uint32_t *__restrict__ ns, uint32_t n1,
+                                                   const double *__restrict__ partial_all, size_t p_stride,
+                                                   const float *ws_all, float *model_all, int32_t *ok_all) {
     __shared__ double A[9][9];
     __shared__ double V[9][9];
     __shared__ double s_v[9];
     const uint32_t t = threadIdx.x;
+    const uint32_t w = blockIdx.x;
+    const uint32_t n = ns ? ns[w] : n1;
+    const float4 *q = q_all + w * q_stride;
+    const double *partial = partial_all + w * p_stride;
+    const uint32_t nblocks = (n + kAtaBlock - 1) / kAtaBlock;
+    const float *ws = ws_all + 18 * w;
+    float *model_out = model_all + 9 * w;
+    int32_t *ok = ok_all + w;
+    if (n == 0) {  // EstimateModelNonMinimalSample of no points fails
+        if (t == 0) *ok = 0;
+        return;
+    }
     if (FUND ? n <= 8 : 2 * n <= 9) {
         if (t == 0) {
             double v[9];
@@ -339,9 +370,18 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q,
 
 // Line PCA: one lane, sequential fp32 moments (sum_xy = 0 initialised),
 // closed-form eigenvector of the smaller eigenvalue of the 2x2 covariance (fp64).
-__global__ __launch_bounds__(64) void k_line_pca(const float2 *__restrict__ q, uint32_t n, float *model_out,
-                                                 int32_t *ok) {
+__global__ __launch_bounds__(64) void k_line_pca(const float2 *__restrict__ q_all, size_t q_stride,
+                                                 const uint32_t *__restrict__ ns, uint32_t n1, float *model_all,
+                                                 int32_t *ok_all) {
     if (threadIdx.x != 0) return;
+    const float2 *q = q_all + blockIdx.x * q_stride;
+    const uint32_t n = ns ? ns[blockIdx.x] : n1;
+    float *model_out = model_all + 9 * blockIdx.x;
+    int32_t *ok = ok_all + blockIdx.x;
+    if (n == 0) {
+        *ok = 0;
+        return;
+    }
     float sx = 0, sy = 0, sxy = 0, sx2 = 0, sy2 = 0;
     for (uint32_t i = 0; i < n; i++) {
         const float2 p = q[i];
@@ -377,33 +417,36 @@ __global__ __launch_bounds__(64) void k_line_pca(const float2 *__restrict__ q, u
     *ok = 1;
 }
 
-hipError_t launch_nonminimal_h(hipStream_t st, const float4 *pts, const int32_t *idx, uint32_t n, float4 *q,
-                               double *partial, float *ws, float *model_out, int32_t *ok) {
-    hipLaunchKernelGGL(k_gather4, dim3((n + 255) / 256), dim3(256), 0, st, pts, idx, n, q);
-    hipLaunchKernelGGL(k_normalize, dim3(1), dim3(256), 0, st, q, n, ws);
-    const uint32_t nb = (n + kAtaBlock - 1) / kAtaBlock;
-    if (2 * n > 9) hipLaunchKernelGGL(k_ata_partial<false>, dim3(nb), dim3(64), 0, st, q, n, partial);
-    hipLaunchKernelGGL(k_dlt_finish<false>, dim3(1), dim3(64), 0, st, q, n, partial, nb, ws, model_out, ok);
+// EstimateModelNonMinimalSample for W fits: homography (normalized_dlt.cpp:7-23), F and E
+// (EightPointsAlgorithm, fundamental_estimator.hpp:65-76, essential_estimator.hpp:64-74,
+// eight_points.cpp:4-100), line (line2d_estimator.hpp:59-107).  nmax >= every ns[w].
+hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pts, const NmBatch &b) {
+    if (b.W == 0) return hipSuccess;
+    const dim3 gg((b.nmax + 255) / 256 ? (b.nmax + 255) / 256 : 1, b.W);
+    if (estimator == USAC_LINE2D) {
+        float2 *q = static_cast<float2 *>(b.q);
+        hipLaunchKernelGGL(k_gather<float2>, gg, dim3(256), 0, st, static_cast<const float2 *>(pts), b.base,
+                           b.base_stride, b.pos, b.pos_stride, b.ns, b.n1, q, b.q_stride);
+        hipLaunchKernelGGL(k_line_pca, dim3(b.W), dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.model_out, b.ok);
+        return hipGetLastError();
+    }
+    float4 *q = static_cast<float4 *>(b.q);
+    hipLaunchKernelGGL(k_gather<float4>, gg, dim3(256), 0, st, static_cast<const float4 *>(pts), b.base,
+                       b.base_stride, b.pos, b.pos_stride, b.ns, b.n1, q, b.q_stride);
+    hipLaunchKernelGGL(k_normalize, dim3(b.W), dim3(256), 0, st, q, b.q_stride, b.ns, b.n1, b.ws);
+    const dim3 ga((b.nmax + kAtaBlock - 1) / kAtaBlock ? (b.nmax + kAtaBlock - 1) / kAtaBlock : 1, b.W);
+    if (estimator == USAC_HOMOGRAPHY) {
+        hipLaunchKernelGGL(k_ata_partial<false>, ga, dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial, b.p_stride);
+        hipLaunchKernelGGL(k_dlt_finish<false>, dim3(b.W), dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial,
+                           b.p_stride, b.ws, b.model_out, b.ok);
+    } else {
+        hipLaunchKernelGGL(k_ata_partial<true>, ga, dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial, b.p_stride);
+        hipLaunchKernelGGL(k_dlt_finish<true>, dim3(b.W), dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial,
+                           b.p_stride, b.ws, b.model_out, b.ok);
+    }
     return hipGetLastError();
 }
 
-// FundamentalEstimator::EstimateModelNonMinimalSample -> EightPointsAlgorithm
-// (fundamental_estimator.hpp:65-76, eight_points.cpp:4-100)
-hipError_t launch_nonminimal_f(hipStream_t st, const float4 *pts, const int32_t *idx, uint32_t n, float4 *q,
-                               double *partial, float *ws, float *model_out, int32_t *ok) {
-    hipLaunchKernelGGL(k_gather4, dim3((n + 255) / 256), dim3(256), 0, st, pts, idx, n, q);
-    hipLaunchKernelGGL(k_normalize, dim3(1), dim3(256), 0, st, q, n, ws);
-    const uint32_t nb = (n + kAtaBlock - 1) / kAtaBlock;
-    if (n > 8) hipLaunchKernelGGL(k_ata_partial<true>, dim3(nb), dim3(64), 0, st, q, n, partial);
-    hipLaunchKernelGGL(k_dlt_finish<true>, dim3(1), dim3(64), 0, st, q, n, partial, nb, ws, model_out, ok);
-    return hipGetLastError();
-}
-
-hipError_t launch_nonminimal_line(hipStream_t st, const float2 *pts, const int32_t *idx, uint32_t n, float2 *q,
-                                  float *model_out, int32_t *ok) {
-    hipLaunchKernelGGL(k_gather2, dim3((n + 255) / 256), dim3(256), 0, st, pts, idx, n, q);
-    hipLaunchKernelGGL(k_line_pca, dim3(1), dim3(64), 0, st, q, n, model_out, ok);
-    return hipGetLastError();
-}
+size_t nonminimal_partial_stride(uint32_t nmax) { return 45 * ((size_t)nmax / kAtaBlock + 2); }
 
 }  // namespace usac

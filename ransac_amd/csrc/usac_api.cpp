@@ -67,7 +67,11 @@ struct usac_ctx {
     DevBuf samples, models, counts, sums, best, hostmodels, argmax_part;
     DevBuf list, list_n;    // fundamental: occupied model slots (compacted) and their number
     DevBuf pool_idx, pool_pts, masks;  // SPRT parity path: pool order, permuted points, flag words
-    DevBuf lo_idx;                     // LO-RANSAC: host-drawn index lists for the device LSQ
+    // LO-RANSAC (LoRansac): W speculative inner iterations in flight -- their inlier lists
+    // (W x N), LSQ sample positions (W x lo_sample_size), point counts, thresholds, models,
+    // fit flags, scores, fit and scoring scratch; lo_max = the current best's inlier list
+    DevBuf lo_max, lo_lists, lo_pos, lo_ns, lo_thrs, lo_slots, lo_models, lo_ok, lo_cnts, lo_sums, lo_q, lo_part,
+        lo_ws, lo_scr;
     DevBuf e5_ws;                      // staged 5-point solver workspace
     // throughput SPRT (usac_set_sprt): batch-fixed test on the pool-ordered points
     bool sprt_on = false;
@@ -230,41 +234,76 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
 
 // exact single-model inliers into c->inl_idx / inl_cnt / inl_sum (device)
 hipError_t enqueue_inliers(usac_ctx *c, const float *model_dev, float thr) {
-    hipError_t e = c->inl_scratch.reserve(usac::inliers_scratch_bytes(c->n));
+    hipError_t e = c->inl_scratch.reserve(usac::inliers_scratch_bytes(c->n, 1));
     if (e != hipSuccess) return e;
     return usac::launch_inliers(c->stream, c->estimator, c->pts.p, c->n, model_dev, thr, c->inl_idx.as<int32_t>(),
                                 c->inl_cnt.as<int32_t>(), c->inl_sum.as<float>(), c->inl_scratch.p);
 }
 
 hipError_t enqueue_nonminimal(usac_ctx *c, const int32_t *idx_dev, uint32_t n) {
-    if (listed(c))  // F and E: EightPointsAlgorithm (essential_estimator.hpp:64-74)
-        return usac::launch_nonminimal_f(c->stream, c->pts.as<float4>(), idx_dev, n, c->q.as<float4>(),
-                                         c->partial.as<double>(), c->ws.as<float>(), c->nm_model.as<float>(),
-                                         c->nm_ok.as<int32_t>());
-    if (is_h(c))
-        return usac::launch_nonminimal_h(c->stream, c->pts.as<float4>(), idx_dev, n, c->q.as<float4>(),
-                                         c->partial.as<double>(), c->ws.as<float>(), c->nm_model.as<float>(),
-                                         c->nm_ok.as<int32_t>());
-    return usac::launch_nonminimal_line(c->stream, c->pts.as<float2>(), idx_dev, n, c->q.as<float2>(),
-                                        c->nm_model.as<float>(), c->nm_ok.as<int32_t>());
+    usac::NmBatch b{};
+    b.base = idx_dev;
+    b.n1 = n;
+    b.W = 1;
+    b.nmax = n;
+    b.q = c->q.p;
+    b.partial = c->partial.as<double>();
+    b.ws = c->ws.as<float>();
+    b.model_out = c->nm_model.as<float>();
+    b.ok = c->nm_ok.as<int32_t>();
+    return usac::launch_nonminimal_batch(c->stream, c->estimator, c->pts.p, b);
 }
 
 // LO-RANSAC: InnerLocalOptimization::GetModelScore (inner_local_optimization.hpp:74-133) with
-// IterativeLocalOptimization (iterative_local_optimization.hpp:61-136).  The control flow runs
-// here; every least-squares fit (EstimateModelNonMinimalSample) and every scored inlier list
-// (Quality::getNumberInliers(..., get_inliers = true)) runs on the device.  lo_model's
-// threshold persists across calls and compounds like the reference's; the LO
-// mt19937 is seeded with seed + 1 (the reference: std::random_device).
+// IterativeLocalOptimization (iterative_local_optimization.hpp:61-136).  lo_model's threshold
+// persists across calls and compounds like the reference's; the LO mt19937 is
+// seeded with seed + 1 (the reference: std::random_device).
+//
+// The reference runs its <= 20 inner iterations one after the other, each a chain of up to
+// five dependent (least-squares fit -> scored inlier list) steps whose sequential fp32 sums
+// make every step latency-bound.  Inner iteration j depends on the earlier ones only through
+// (a) the best model / inlier list, which changes only when an iteration improves it,
+// (b) the generator, which (unlimited variant) only the inner sample draws advance, and
+// (c) the LO threshold each iteration starts from.  So all remaining iterations run at once
+// as speculative chains: their samples are drawn up front under "no improvement", each starts
+// from the threshold the previous one would leave after a completed iterative stage, and the
+// chains advance in lockstep -- one batched fit launch, then one batched scoring launch, per
+// stage (kernels_nonmin.hip / kernels_inliers.hip, W fits at once).  The host then replays
+// the iterations in order with the reference's exact control flow: a chain whose start
+// threshold was mis-predicted, or every chain after one that improved the best, is discarded
+// and the speculation restarts there with the generator rewound to just after the last kept
+// draw.  Every kept result is bit-identical to the sequential order.  The limited variant
+// (InItFLORsc) draws inside the iterative stage, so it runs one chain at a time.
 struct LoRansac {
+    enum Phase { INNER_FIT, INNER_SCORE, ITER_FIT, ITER_SCORE, DONE };
+    enum Outcome { RETURN, SKIP, FEW, ITERATED };
+    struct Chain {
+        float thr_start = 0.f, thr = 0.f;
+        Phase phase = DONE;
+        Outcome outcome = SKIP;
+        int lo_cnt = 0;
+        float lo_sum = 0.f;
+        uint32_t it = 0, iter_count = 0;
+        bool failed = false, fit_pos = false;
+        float model[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    };
+
     usac_ctx *c;
     usac::Mt19937 g;
     bool limited;
-    uint32_t inner, iters, limit, mult, m, n;
+    uint32_t inner, iters, limit, mult, m, n, wmax;
     float theta, lo_thr, step;
-    std::vector<int32_t> max_inl, lo_inl, lo_sample;
     uint32_t inner_count = 0, iterative_count = 0;
-    float lo_model[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t rounds = 0, stages = 0;  // speculation rounds and device stages (statistics)
     int rc = USAC_OK;
+    // entry best of the current call
+    int best_cnt = 0;
+    float best_sum = 0.f;
+    std::vector<Chain> ch;
+    std::vector<usac::Mt19937> g_after;  // generator after chain w's inner draw
+    std::vector<int32_t> hpos, hcnt, hok;
+    std::vector<uint32_t> hns, hslots;
+    std::vector<float> hthr, hsum, hmod;
 
     LoRansac(usac_ctx *ctx, const usac_params *p)
         : c(ctx),
@@ -276,97 +315,322 @@ struct LoRansac {
           mult(p->lo_threshold_multiplier),
           m(ctx->m),
           n(ctx->n),
+          wmax(std::max<uint32_t>(1u, p->lo == USAC_LO_INITFLORSC ? 1u : p->lo_inner_iterations)),
           theta(p->threshold),
           lo_thr(p->threshold),
           step((p->threshold * p->lo_threshold_multiplier - p->threshold) / p->lo_iterative_iterations),
-          max_inl(ctx->n),
-          lo_inl(ctx->n),
-          lo_sample(p->lo_sample_size ? p->lo_sample_size : 1) {}
+          ch(wmax),
+          g_after(wmax, usac::Mt19937(0)),
+          hpos((size_t)wmax * std::max<uint32_t>(1u, p->lo_sample_size)),
+          hcnt(wmax),
+          hok(wmax),
+          hns(wmax),
+          hslots(wmax),
+          hthr(wmax),
+          hsum(wmax),
+          hmod((size_t)9 * wmax) {}
 
-    bool lsq(const int32_t *idx, uint32_t k, float *model) {
-        if (rc) return false;
-        int32_t ok = 0;
-        hipError_t e = hipMemcpyAsync(c->lo_idx.p, idx, sizeof(int32_t) * k, hipMemcpyHostToDevice, c->stream);
-        if (e == hipSuccess) e = enqueue_nonminimal(c, c->lo_idx.as<int32_t>(), k);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(model, c->nm_model.p, sizeof(float) * 9, hipMemcpyDeviceToHost, c->stream);
-        if (e == hipSuccess) e = hipMemcpyAsync(&ok, c->nm_ok.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-        if (e != hipSuccess) rc = fail(c, USAC_ERR_HIP, std::string("LO least squares: ") + hipGetErrorString(e));
-        return rc == USAC_OK && ok;
+    int reserve() {
+        const size_t W = wmax, N = n;
+        HIP_TRY(c, c->lo_max.reserve(sizeof(int32_t) * N));
+        HIP_TRY(c, c->lo_lists.reserve(sizeof(int32_t) * N * W));
+        HIP_TRY(c, c->lo_pos.reserve(sizeof(int32_t) * hpos.size()));
+        HIP_TRY(c, c->lo_ns.reserve(sizeof(uint32_t) * W));
+        HIP_TRY(c, c->lo_thrs.reserve(sizeof(float) * W));
+        HIP_TRY(c, c->lo_slots.reserve(sizeof(uint32_t) * W));
+        HIP_TRY(c, c->lo_models.reserve(sizeof(float) * 9 * W));
+        HIP_TRY(c, c->lo_ok.reserve(sizeof(int32_t) * W));
+        HIP_TRY(c, c->lo_cnts.reserve(sizeof(int32_t) * W));
+        HIP_TRY(c, c->lo_sums.reserve(sizeof(float) * W));
+        HIP_TRY(c, c->lo_q.reserve(sizeof(float) * c->cols * N * W));
+        HIP_TRY(c, c->lo_part.reserve(sizeof(double) * usac::nonminimal_partial_stride(n) * W));
+        HIP_TRY(c, c->lo_ws.reserve(sizeof(float) * 18 * W));
+        HIP_TRY(c, c->lo_scr.reserve(usac::inliers_scratch_bytes(n, wmax)));
+        return USAC_OK;
     }
-    void quality(const float *model, float thr, int &cnt, float &sum, int32_t *inl) {
-        if (rc) return;
-        hipError_t e = hipMemcpyAsync(c->one_model.p, model, sizeof(float) * 9, hipMemcpyHostToDevice, c->stream);
-        if (e == hipSuccess) e = enqueue_inliers(c, c->one_model.as<float>(), thr);
-        if (e == hipSuccess) e = hipMemcpyAsync(&cnt, c->inl_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
-        if (e == hipSuccess) e = hipMemcpyAsync(&sum, c->inl_sum.p, sizeof(float), hipMemcpyDeviceToHost, c->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-        if (e == hipSuccess && cnt > 0)
-            e = hipMemcpy(inl, c->inl_idx.p, sizeof(int32_t) * (size_t)cnt, hipMemcpyDeviceToHost);
-        if (e != hipSuccess) rc = fail(c, USAC_ERR_HIP, std::string("LO scoring: ") + hipGetErrorString(e));
-    }
+
     static bool bigger(int c1, float s1, int c2, float s2) { return c1 > c2 || (c1 == c2 && s1 > s2); }
 
-    // IterativeLocalOptimization::GetScoreUnlimited / GetScoreLimited; returns fail
-    bool iterative(int &lo_cnt, float &lo_sum, int best_cnt, float best_sum) {
-        for (uint32_t it = 0; it < iters && !rc; it++) {
-            lo_thr -= step;
-            if (lo_cnt <= (int)m) break;
-            if (limited) {
-                if (lo_cnt > (int)limit) {
-                    usac::unique_set(g, lo_sample.data(), limit, (uint32_t)(lo_cnt - 1));
-                    for (uint32_t k = 0; k < limit; k++) lo_sample[k] = lo_inl[lo_sample[k]];
-                    if (!lsq(lo_sample.data(), limit, lo_model)) continue;
-                } else {
-                    if (!lsq(lo_inl.data(), (uint32_t)lo_cnt, lo_model)) break;
-                }
-                quality(lo_model, lo_thr, lo_cnt, lo_sum, lo_inl.data());
-            } else {
-                if (!lsq(lo_inl.data(), (uint32_t)lo_cnt, lo_model)) break;
-                quality(lo_model, lo_thr, lo_cnt, lo_sum, lo_inl.data());
-                if (bigger(best_cnt, best_sum, lo_cnt, lo_sum)) break;
+    // the threshold an inner iteration leaves when its iterative stage runs all its steps
+    float predict(float t) const {
+        t = (float)mult * t;
+        for (uint32_t k = 0; k < iters; k++) t -= step;
+        return fabsf(t - theta) > 0.00001f ? theta : t;
+    }
+
+    // IterativeLocalOptimization loop head: decrement, the break tests, then the next fit
+    void iter_head(Chain &h, uint32_t w) {
+        for (;;) {
+            if (h.it >= iters) return finish(h);
+            h.thr -= step;
+            if (h.lo_cnt <= (int)m) return finish(h);
+            h.fit_pos = false;
+            if (limited && h.lo_cnt > (int)limit) {  // GetScoreLimited: a random subset of lo_inliers
+                usac::unique_set(g, hpos.data() + (size_t)w * limit, limit, (uint32_t)(h.lo_cnt - 1));
+                h.fit_pos = true;
             }
-            iterative_count++;
+            h.phase = ITER_FIT;
+            return;
         }
-        bool failed = false;
-        if (fabsf(lo_thr - theta) > 0.00001) {
-            failed = true;
-            lo_thr = theta;
+    }
+    void finish(Chain &h) {
+        h.failed = fabsf(h.thr - theta) > 0.00001f;
+        if (h.failed) h.thr = theta;
+        h.outcome = ITERATED;
+        h.phase = DONE;
+    }
+
+    // one lockstep stage: a batched fit (INNER_FIT / ITER_FIT chains) or a batched scoring
+    // (INNER_SCORE / ITER_SCORE chains) on the device, then every chain's state machine steps
+    int stage(uint32_t W, int inner_cnt) {
+        bool fit = false, score = false, inner_fit = false, pos = false;
+        uint32_t nmax = 0, ns = 0;
+        for (uint32_t w = 0; w < W; w++) {
+            const Chain &h = ch[w];
+            hns[w] = 0;
+            if (h.phase == INNER_FIT || h.phase == ITER_FIT) {
+                fit = true;
+                inner_fit = h.phase == INNER_FIT;
+                if (inner_fit) {
+                    pos = inner_cnt > (int)limit;
+                    hns[w] = pos ? limit : (uint32_t)inner_cnt;
+                } else {
+                    pos = h.fit_pos;
+                    hns[w] = pos ? limit : (uint32_t)h.lo_cnt;
+                }
+                nmax = std::max(nmax, hns[w]);
+            } else if (h.phase == INNER_SCORE || h.phase == ITER_SCORE) {
+                score = true;
+                hslots[ns++] = w;
+                hthr[w] = h.thr;
+            }
         }
-        return failed;
+        if (fit && score) return fail(c, USAC_ERR_HIP, "LO chains out of lockstep");  // never: fit, score alternate
+        hipStream_t st = c->stream;
+        if (fit) {
+            HIP_TRY(c, hipMemcpyAsync(c->lo_ns.p, hns.data(), sizeof(uint32_t) * W, hipMemcpyHostToDevice, st));
+            if (pos)
+                HIP_TRY(c, hipMemcpyAsync(c->lo_pos.p, hpos.data(), sizeof(int32_t) * (size_t)W * limit,
+                                          hipMemcpyHostToDevice, st));
+            usac::NmBatch b{};
+            b.base = inner_fit ? c->lo_max.as<int32_t>() : c->lo_lists.as<int32_t>();
+            b.base_stride = inner_fit ? 0 : n;
+            b.pos = pos ? c->lo_pos.as<int32_t>() : nullptr;
+            b.pos_stride = limit;
+            b.ns = c->lo_ns.as<uint32_t>();
+            b.W = W;
+            b.nmax = nmax;
+            b.q = c->lo_q.p;
+            b.q_stride = n;
+            b.partial = c->lo_part.as<double>();
+            b.p_stride = usac::nonminimal_partial_stride(n);
+            b.ws = c->lo_ws.as<float>();
+            b.model_out = c->lo_models.as<float>();
+            b.ok = c->lo_ok.as<int32_t>();
+            HIP_TRY(c, usac::launch_nonminimal_batch(st, c->estimator, c->pts.p, b));
+            HIP_TRY(c, hipMemcpyAsync(hmod.data(), c->lo_models.p, sizeof(float) * 9 * W, hipMemcpyDeviceToHost, st));
+            HIP_TRY(c, hipMemcpyAsync(hok.data(), c->lo_ok.p, sizeof(int32_t) * W, hipMemcpyDeviceToHost, st));
+        } else {
+            HIP_TRY(c, hipMemcpyAsync(c->lo_thrs.p, hthr.data(), sizeof(float) * W, hipMemcpyHostToDevice, st));
+            HIP_TRY(c, hipMemcpyAsync(c->lo_slots.p, hslots.data(), sizeof(uint32_t) * ns, hipMemcpyHostToDevice, st));
+            HIP_TRY(c, usac::launch_inliers_batch(st, c->estimator, c->pts.p, n, c->lo_models.as<float>(), ns, 0.f,
+                                                  c->lo_thrs.as<float>(), c->lo_slots.as<uint32_t>(),
+                                                  c->lo_lists.as<int32_t>(), n, c->lo_cnts.as<int32_t>(),
+                                                  c->lo_sums.as<float>(), c->lo_scr.p));
+            HIP_TRY(c, hipMemcpyAsync(hcnt.data(), c->lo_cnts.p, sizeof(int32_t) * W, hipMemcpyDeviceToHost, st));
+            HIP_TRY(c, hipMemcpyAsync(hsum.data(), c->lo_sums.p, sizeof(float) * W, hipMemcpyDeviceToHost, st));
+        }
+        HIP_TRY(c, hipStreamSynchronize(st));
+        stages++;
+        for (uint32_t w = 0; w < W; w++) {
+            Chain &h = ch[w];
+            switch (h.phase) {
+                case INNER_FIT:  // LeastSquaresFitting(lo_sample | max_inliers) -> lo_model
+                    memcpy(h.model, hmod.data() + 9 * (size_t)w, sizeof(h.model));
+                    if (!hok[w]) {
+                        h.outcome = inner_cnt > (int)limit ? SKIP : RETURN;
+                        h.phase = DONE;
+                    } else {
+                        h.thr = (float)mult * h.thr;  // K * theta
+                        h.phase = INNER_SCORE;
+                    }
+                    break;
+                case INNER_SCORE:
+                    h.lo_cnt = hcnt[w];
+                    h.lo_sum = hsum[w];
+                    if (h.lo_cnt <= (int)m) {
+                        h.outcome = FEW;
+                        h.phase = DONE;
+                    } else {
+                        h.it = 0;
+                        h.iter_count = 0;
+                        iter_head(h, w);
+                    }
+                    break;
+                case ITER_FIT:
+                    memcpy(h.model, hmod.data() + 9 * (size_t)w, sizeof(h.model));
+                    if (hok[w]) {
+                        h.phase = ITER_SCORE;
+                    } else if (h.fit_pos) {  // GetScoreLimited: continue
+                        h.it++;
+                        iter_head(h, w);
+                    } else {
+                        finish(h);  // break
+                    }
+                    break;
+                case ITER_SCORE:
+                    h.lo_cnt = hcnt[w];
+                    h.lo_sum = hsum[w];
+                    if (!limited && bigger(best_cnt, best_sum, h.lo_cnt, h.lo_sum)) {
+                        finish(h);  // GetScoreUnlimited: the best is bigger -> break
+                    } else {
+                        h.iter_count++;
+                        h.it++;
+                        iter_head(h, w);
+                    }
+                    break;
+                default:
+                    break;
+            }
+        }
+        return USAC_OK;
     }
 
     // GetModelScore(best_model, best_score): model / (cnt, sum) improved in place
     void run(float *model, int &cnt, float &sum) {
-        if (cnt < 12) return;
-        int c0 = 0;
-        float s0 = 0.f;
-        quality(model, theta, c0, s0, max_inl.data());
-        for (uint32_t it = 0; it < inner && !rc; it++) {
-            if (cnt > (int)limit) {
-                usac::unique_set(g, lo_sample.data(), limit, (uint32_t)(cnt - 1));
-                for (uint32_t k = 0; k < limit; k++) lo_sample[k] = max_inl[lo_sample[k]];
-                if (!lsq(lo_sample.data(), limit, lo_model)) continue;
-            } else {
-                if (!lsq(max_inl.data(), (uint32_t)cnt, lo_model)) return;
+        if (cnt < 12 || rc) return;
+        // quality->getInliers(best_model) -> max_inliers (device)
+        hipError_t e = hipMemcpyAsync(c->one_model.p, model, sizeof(float) * 9, hipMemcpyHostToDevice, c->stream);
+        if (e == hipSuccess) e = c->inl_scratch.reserve(usac::inliers_scratch_bytes(n, 1));
+        if (e == hipSuccess)
+            e = usac::launch_inliers(c->stream, c->estimator, c->pts.p, n, c->one_model.as<float>(), theta,
+                                     c->lo_max.as<int32_t>(), c->inl_cnt.as<int32_t>(), c->inl_sum.as<float>(),
+                                     c->inl_scratch.p);
+        if (e != hipSuccess) {
+            rc = fail(c, USAC_ERR_HIP, std::string("LO inliers: ") + hipGetErrorString(e));
+            return;
+        }
+        uint32_t j0 = 0;
+        while (j0 < inner && !rc) {
+            // speculate iterations j0 .. j0 + W - 1 under "no improvement"
+            const uint32_t W = std::min(wmax, inner - j0);
+            const usac::Mt19937 g_before = g;
+            best_cnt = cnt;
+            best_sum = sum;
+            float t = lo_thr;
+            for (uint32_t w = 0; w < W; w++) {
+                Chain &h = ch[w];
+                h = Chain();
+                h.thr_start = h.thr = t;
+                h.phase = INNER_FIT;
+                if (cnt > (int)limit) {
+                    usac::unique_set(g, hpos.data() + (size_t)w * limit, limit, (uint32_t)(cnt - 1));
+                }
+                g_after[w] = g;
+                t = predict(t);
             }
-            lo_thr = mult * lo_thr;
-            int lo_cnt = 0;
-            float lo_sum = 0.f;
-            quality(lo_model, lo_thr, lo_cnt, lo_sum, lo_inl.data());
-            if (lo_cnt <= (int)m) continue;
-            const bool failed = iterative(lo_cnt, lo_sum, cnt, sum);
-            if (!failed && bigger(lo_cnt, lo_sum, cnt, sum)) {
-                memcpy(model, lo_model, sizeof(lo_model));
-                cnt = lo_cnt;
-                sum = lo_sum;
-                std::copy(lo_inl.begin(), lo_inl.begin() + lo_cnt, max_inl.begin());
+            rounds++;
+            for (;;) {
+                bool active = false;
+                for (uint32_t w = 0; w < W; w++) active |= ch[w].phase != DONE;
+                if (!active) break;
+                if ((rc = stage(W, cnt))) return;
             }
-            inner_count++;
+            if (limited) g_after[0] = g;  // the iterative stage's draws
+            // replay in order
+            bool restart = false;
+            uint32_t w = 0;
+            for (; w < W; w++) {
+                const Chain &h = ch[w];
+                if (memcmp(&h.thr_start, &lo_thr, sizeof(float)) != 0) {  // mis-predicted start
+                    g = w ? g_after[w - 1] : g_before;
+                    j0 += w;
+                    restart = true;
+                    break;
+                }
+                if (h.outcome == RETURN) {
+                    g = g_after[w];
+                    return;
+                }
+                if (h.outcome == SKIP) continue;
+                lo_thr = h.thr;
+                if (h.outcome == FEW) continue;
+                iterative_count += h.iter_count;
+                inner_count++;
+                if (!h.failed && bigger(h.lo_cnt, h.lo_sum, cnt, sum)) {
+                    memcpy(model, h.model, sizeof(h.model));
+                    cnt = h.lo_cnt;
+                    sum = h.lo_sum;
+                    e = hipMemcpyAsync(c->lo_max.p, c->lo_lists.as<int32_t>() + (size_t)w * n,
+                                       sizeof(int32_t) * (size_t)cnt, hipMemcpyDeviceToDevice, c->stream);
+                    if (e != hipSuccess) {
+                        rc = fail(c, USAC_ERR_HIP, std::string("LO inliers copy: ") + hipGetErrorString(e));
+                        return;
+                    }
+                    g = g_after[w];
+                    j0 += w + 1;
+                    restart = true;
+                    break;
+                }
+            }
+            if (!restart) {
+                g = g_after[W - 1];
+                j0 += W;
+            }
         }
     }
 };
+
+// Σerr where the replay can read it.  The loop compares a model's Σ only against the running
+// best with an equal count, and stores it only when the model becomes the best (Score::bigger,
+// quality.hpp:22-31); both need count >= the running best count, which is at least
+// max(best count at batch start, every earlier count of the batch).  So only the slots whose
+// count reaches that running maximum get the reference's sequential fp32 sum -- computed
+// exactly on the device, 64 models per launch (launch_inliers_batch) -- and the batch itself
+// is scored by the fast multi-chunk kernel, whose counts are exact.  Other slots' sums are
+// never read.  The recount doubles as a check of the fast kernel's counts.
+int exact_sums(usac_ctx *c, float thr, int best_count, const int32_t *hc, const float *hmod, size_t SB, size_t S,
+               float *hsum, uint32_t *n_models) {
+    constexpr uint32_t kMax = 64;
+    std::vector<uint32_t> cand;
+    int run_max = best_count;
+    for (size_t sl = 0; sl < S; sl++) {
+        if (hc[sl] < 0) continue;
+        if (hc[sl] >= run_max) {
+            cand.push_back((uint32_t)sl);
+            run_max = hc[sl];
+        }
+    }
+    if (cand.empty()) return USAC_OK;
+    const int nc = ncomp(c);
+    std::vector<float> am(9 * (size_t)kMax);
+    std::vector<int32_t> cc(kMax);
+    std::vector<float> cs(kMax);
+    HIP_TRY(c, c->lo_models.reserve(sizeof(float) * 9 * kMax));
+    HIP_TRY(c, c->lo_cnts.reserve(sizeof(int32_t) * kMax));
+    HIP_TRY(c, c->lo_sums.reserve(sizeof(float) * kMax));
+    HIP_TRY(c, c->lo_scr.reserve(usac::inliers_scratch_bytes(c->n, kMax)));
+    for (size_t k0 = 0; k0 < cand.size(); k0 += kMax) {
+        const uint32_t K = (uint32_t)std::min<size_t>(kMax, cand.size() - k0);
+        for (uint32_t k = 0; k < K; k++)
+            for (int e = 0; e < 9; e++) am[9 * k + e] = e < nc ? hmod[(size_t)e * SB + cand[k0 + k]] : 0.f;
+        HIP_TRY(c, hipMemcpyAsync(c->lo_models.p, am.data(), sizeof(float) * 9 * K, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, usac::launch_inliers_batch(c->stream, c->estimator, c->pts.p, c->n, c->lo_models.as<float>(), K, thr,
+                                              nullptr, nullptr, nullptr, 0, c->lo_cnts.as<int32_t>(),
+                                              c->lo_sums.as<float>(), c->lo_scr.p));
+        HIP_TRY(c, hipMemcpyAsync(cc.data(), c->lo_cnts.p, sizeof(int32_t) * K, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(cs.data(), c->lo_sums.p, sizeof(float) * K, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        for (uint32_t k = 0; k < K; k++) {
+            if (cc[k] != hc[cand[k0 + k]])
+                return fail(c, USAC_ERR_HIP, "score kernel count differs from the exact recount (slot " +
+                                                 std::to_string(cand[k0 + k]) + ")");
+            hsum[cand[k0 + k]] = cs[k];
+        }
+    }
+    *n_models += (uint32_t)cand.size();
+    return USAC_OK;
+}
 
 bool rec_better(const usac_record &a, const usac_record &b) {
     if (!a.valid) return false;
@@ -443,9 +707,11 @@ void usac_destroy(usac_ctx *c) {
     if (c->comm) ncclCommDestroy(c->comm);
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
-                      &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->inl_scratch, &c->lo_idx, &c->e5_ws, &c->one_model,
+                      &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->inl_scratch, &c->e5_ws, &c->one_model,
                       &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok,
-                      &c->rec_send, &c->rec_all, &c->tv_part, &c->prosac_tab})
+                      &c->rec_send, &c->rec_all, &c->tv_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
+                      &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
+                      &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr})
         b->release();
     for (auto &ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -834,8 +1100,8 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
     }
     std::unique_ptr<LoRansac> lo;
     if (use_lo) {
-        HIP_TRY(c, c->lo_idx.reserve(sizeof(int32_t) * (size_t)n));
         lo.reset(new LoRansac(c, prm));
+        if ((rc = lo->reserve())) return rc;
     }
     usac::StandardTerminationCriteria term(prm->desired_prob, m, n, prm->max_iterations);
     std::unique_ptr<usac::Sprt> sprt;
@@ -910,10 +1176,9 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
                                               listed(c) ? c->list.as<uint32_t>() : nullptr,
                                               listed(c) ? c->list_n.as<uint32_t>() : nullptr, (uint32_t)S, thr,
                                               c->masks.as<uint32_t>(), (uint32_t)S));
-        } else {
-            HIP_TRY(c, enqueue_score(c, B, thr, 1));
+        } else {  // exact counts from the fast multi-chunk scorer; exact sums below, where needed
+            HIP_TRY(c, enqueue_score(c, B, thr, c->chunks));
             HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(c, hipMemcpyAsync(hsum.data(), c->sums.p, sizeof(float) * S, hipMemcpyDeviceToHost, c->stream));
         }
         for (int k = 0; k < ncomp(c); k++)
             HIP_TRY(c, hipMemcpyAsync(hmod.data() + (size_t)k * SB, c->models.as<float>() + (size_t)k * S,
@@ -942,6 +1207,9 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
                 for (size_t sl = 0; sl < S; sl++) slot_row[sl] = (int32_t)sl;
             }
         }
+        if (!sprt && (rc = exact_sums(c, thr, best.inlier_number, hc.data(), hmod.data(), SB, S, hsum.data(),
+                                      &out->sum_models)))
+            return rc;
         out->batches++;
         // ---- sequential replay
         std::vector<uint32_t> wbuf(sprt ? nw : 0);
@@ -1022,6 +1290,8 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
     out->prosac_term_len = prosac ? pterm->terminationLength() : n;
     out->lo_inner_iters = lo ? lo->inner_count : 0;
     out->lo_iterative_iters = lo ? lo->iterative_count : 0;
+    out->lo_rounds = lo ? lo->rounds : 0;
+    out->lo_stages = lo ? lo->stages : 0;
     memcpy(out->minimal_model, best_model, sizeof(best_model));
     out->minimal_inliers = best.inlier_number;
     if (best.inlier_number == 0) {

@@ -73,8 +73,6 @@ hipError_t launch_solve_e5(hipStream_t st, const float4 *pts, uint32_t n, const 
                            int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, float *models,
                            int32_t *counts, uint32_t *list, uint32_t *list_n, void *workspace);
 size_t e5_workspace_bytes(uint32_t B);
-hipError_t launch_nonminimal_f(hipStream_t st, const float4 *pts, const int32_t *idx, uint32_t n, float4 *q,
-                               double *partial, float *ws, float *model_out, int32_t *ok);
 
 // SPRT parity support (kernels_sprt.hip): points permuted into pool order, and per-model
 // pool-order inlier words (words[w * row_stride + row], bit b = position 32 w + b)
@@ -94,15 +92,38 @@ hipError_t launch_score_sprt(hipStream_t st, int estimator, const void *pool_pts
 size_t sprt_survivor_bytes();
 
 // exact inliers of one model (kernels_inliers.hip): ascending idx, count, sequential Σ;
-// scratch = inliers_scratch_bytes(n)
+// scratch = inliers_scratch_bytes(n, 1)
 hipError_t launch_inliers(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *model, float thr,
                           int32_t *idx, int32_t *count, float *sum, void *scratch);
-size_t inliers_scratch_bytes(uint32_t n);
+// the same for W models at once (models slot w at models + 9 w, row-major; thrs[w], or thr
+// when thrs is null; list at idx + w * idx_stride, idx nullable = counts and sums only;
+// counts[w], sums[w]).  slots (nullable): the W launched rows are slots[0..W) of a larger
+// set, every other slot is left untouched.  scratch = inliers_scratch_bytes(n, max slot + 1)
+hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *models,
+                                uint32_t W, float thr, const float *thrs, const uint32_t *slots, int32_t *idx,
+                                size_t idx_stride, int32_t *counts, float *sums, void *scratch);
+size_t inliers_scratch_bytes(uint32_t n, uint32_t W);
 
-
-hipError_t launch_nonminimal_h(hipStream_t st, const float4 *pts, const int32_t *idx, uint32_t n, float4 *q,
-                               double *partial, float *ws, float *model_out, int32_t *ok);
-hipError_t launch_nonminimal_line(hipStream_t st, const float2 *pts, const int32_t *idx, uint32_t n, float2 *q,
-                                  float *model_out, int32_t *ok);
+// W independent non-minimal fits (kernels_nonmin.hip).  Fit w: index list base + w *
+// base_stride, read through pos + w * pos_stride when pos != nullptr; ns[w] points (device;
+// ns == nullptr: every fit has n1 points);
+// q: W x q_stride points (float4, float2 for line); partial: W x p_stride doubles
+// (p_stride >= nonminimal_partial_stride(ns[w])); ws: W x 18; model_out: W x 9; ok: W.
+struct NmBatch {
+    const int32_t *base;
+    size_t base_stride;
+    const int32_t *pos;
+    size_t pos_stride;
+    const uint32_t *ns;
+    uint32_t n1, W, nmax;
+    void *q;
+    size_t q_stride;
+    double *partial;
+    size_t p_stride;
+    float *ws, *model_out;
+    int32_t *ok;
+};
+hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pts, const NmBatch &b);
+size_t nonminimal_partial_stride(uint32_t nmax);
 
 }  // namespace usac
