@@ -241,7 +241,11 @@ def cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank):
                      "note": "score kernel of one %d-hypothesis batch at N = %d (the loop's batched verify); a run "
                              "is dominated by LO and the host replay, see DESIGN.md" % (B, n)},
         "parity": parity,
+        "run_stats": {k: int(out.raw[k]) for k in ("batches", "n_records", "lo_rounds", "lo_stages", "sum_models",
+                                                     "lo_iterative_iters", "polish_passes")},
     }
+    line["run_stats"]["lo_inner_iters"] = int(out.getLOIters())
+    line["run_stats"]["time_us"] = int(out.getTimeMicroSeconds())
     if args.cpu_seconds > 0:
         t1 = time.perf_counter()
         runs, it = 0, 0

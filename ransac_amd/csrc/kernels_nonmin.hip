@@ -143,51 +143,47 @@ __global__ __launch_bounds__(256) void k_normalize(float4 *__restrict__ q_all, s
     }
 }
 
-__device__ __forceinline__ double sel9(const double *r, int j) {
-    double v = r[0];
-#pragma unroll
-    for (int k = 1; k < 9; k++) v = (j == k) ? r[k] : v;
-    return v;
-}
-
-// block partials of A^T A: block c, lane e < 45 -> upper-triangle entry e (row-major j<=k).
+// block partials of A^T A: one lane per 64-point block (the spec's unit), its 45
+// upper-triangle entries (row-major j <= k) accumulated in registers over the block's points
+// in order -- each point's rows are built once per lane, not once per entry.
 // FUND: one 8-point row per correspondence (eight_points.cpp:26-45), else two DLT rows.
 template <bool FUND>
 __global__ __launch_bounds__(64) void k_ata_partial(const float4 *__restrict__ q_all, size_t q_stride,
                                                     const uint32_t *__restrict__ ns, uint32_t n1,
-                                                    double *__restrict__ partial_all,
-                                                    size_t p_stride) {
-    const uint32_t e = threadIdx.x;
+                                                    double *__restrict__ partial_all, size_t p_stride) {
     const uint32_t w = blockIdx.y;
     const uint32_t n = ns ? ns[w] : n1;
-    if (e >= 45 || (FUND ? n <= 8 : 2 * n <= 9) || blockIdx.x * kAtaBlock >= n) return;
+    const uint32_t blk = blockIdx.x * 64 + threadIdx.x;
+    if ((FUND ? n <= 8 : 2 * n <= 9) || blk * kAtaBlock >= n) return;
     const float4 *q = q_all + w * q_stride;
-    double *partial = partial_all + w * p_stride;
-    int j = 0, k = e, rem = (int)e;
-    for (int r = 0; r < 9; r++) {
-        if (rem < 9 - r) {
-            j = r;
-            k = r + rem;
-            break;
-        }
-        rem -= 9 - r;
-    }
-    const uint32_t b0 = blockIdx.x * kAtaBlock;
+    const uint32_t b0 = blk * kAtaBlock;
     const uint32_t b1 = b0 + kAtaBlock < n ? b0 + kAtaBlock : n;
-    double acc = 0.0;
+    double acc[45];
+#pragma unroll
+    for (int e = 0; e < 45; e++) acc[e] = 0.0;
     for (uint32_t i = b0; i < b1; i++) {
         const float4 p = q[i];
         if (FUND) {
             double r[9];
             fund_row(p.x, p.y, p.z, p.w, r);
-            acc += sel9(r, j) * sel9(r, k);
+            int e = 0;
+#pragma unroll
+            for (int j = 0; j < 9; j++)
+#pragma unroll
+                for (int k = j; k < 9; k++) acc[e++] += r[j] * r[k];
         } else {
             double r0[9], r1[9];
             dlt_rows(p.x, p.y, p.z, p.w, r0, r1);
-            acc += sel9(r0, j) * sel9(r0, k) + sel9(r1, j) * sel9(r1, k);
+            int e = 0;
+#pragma unroll
+            for (int j = 0; j < 9; j++)
+#pragma unroll
+                for (int k = j; k < 9; k++) acc[e++] += r0[j] * r0[k] + r1[j] * r1[k];
         }
     }
-    partial[(size_t)blockIdx.x * 45 + e] = acc;
+    double *out = partial_all + w * p_stride + (size_t)blk * 45;
+#pragma unroll
+    for (int e = 0; e < 45; e++) out[e] = acc[e];
 }
 
 // Final solve, one wave: A^T A from the partials (lane e), cyclic Jacobi eigen on 9
@@ -434,7 +430,8 @@ hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pt
     hipLaunchKernelGGL(k_gather<float4>, gg, dim3(256), 0, st, static_cast<const float4 *>(pts), b.base,
                        b.base_stride, b.pos, b.pos_stride, b.ns, b.n1, q, b.q_stride);
     hipLaunchKernelGGL(k_normalize, dim3(b.W), dim3(256), 0, st, q, b.q_stride, b.ns, b.n1, b.ws);
-    const dim3 ga((b.nmax + kAtaBlock - 1) / kAtaBlock ? (b.nmax + kAtaBlock - 1) / kAtaBlock : 1, b.W);
+    const uint32_t nblk = (b.nmax + kAtaBlock - 1) / kAtaBlock;
+    const dim3 ga(nblk ? (nblk + 63) / 64 : 1, b.W);
     if (estimator == USAC_HOMOGRAPHY) {
         hipLaunchKernelGGL(k_ata_partial<false>, ga, dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial, b.p_stride);
         hipLaunchKernelGGL(k_dlt_finish<false>, dim3(b.W), dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial,

@@ -1057,6 +1057,15 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
     if (prosac && prm->max_iterations > usac::ProsacSampler::kGrowthMax)
         return fail(c, USAC_ERR_ARG, "PROSAC max_iterations > 200000 (reference draws outside the point range)");
     const auto t0 = std::chrono::steady_clock::now();
+    // wall-time split of the run, printed to stderr when USAC_PROFILE is set
+    enum { T_SETUP, T_DRAW, T_DEVICE, T_SUMS, T_REPLAY, T_LO, T_POLISH, T_N };
+    double tsplit[T_N] = {0, 0, 0, 0, 0, 0, 0};
+    auto tmark = std::chrono::steady_clock::now();
+    auto lap = [&](int k) {
+        const auto t = std::chrono::steady_clock::now();
+        tsplit[k] += std::chrono::duration<double, std::milli>(t - tmark).count();
+        tmark = t;
+    };
     HIP_TRY(c, hipSetDevice(c->device));
     const uint32_t batch = prm->batch ? prm->batch : (prm->sprt ? 1024u : kDefaultBatch);
     int rc = ensure_batch(c, batch);
@@ -1142,6 +1151,7 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
         return USAC_OK;
     };
 
+    lap(T_SETUP);
     while (iters < max_iters) {
         const uint32_t B = std::min(batch, max_iters - iters);
         // ---- draw the batch (speculatively for PROSAC)
@@ -1165,6 +1175,7 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
                 uni->generateSample(smp);
             }
         }
+        lap(T_DRAW);
         // ---- device: solve, then exact scores or pool-order flags
         const size_t S = (size_t)B * spk;
         HIP_TRY(c, hipMemcpyAsync(c->samples.p, hs.data(), sizeof(int32_t) * (size_t)B * m, hipMemcpyHostToDevice,
@@ -1207,9 +1218,11 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
                 for (size_t sl = 0; sl < S; sl++) slot_row[sl] = (int32_t)sl;
             }
         }
+        lap(T_DEVICE);
         if (!sprt && (rc = exact_sums(c, thr, best.inlier_number, hc.data(), hmod.data(), SB, S, hsum.data(),
                                       &out->sum_models)))
             return rc;
+        lap(T_SUMS);
         out->batches++;
         // ---- sequential replay
         std::vector<uint32_t> wbuf(sprt ? nw : 0);
@@ -1240,8 +1253,10 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
                 float model[9];
                 for (int k = 0; k < 9; k++) model[k] = k < ncomp(c) ? hmod[(size_t)k * SB + sl] : 0.f;
                 if (lo) {  // ransac.cpp:110-112, before the best is replaced
+                    lap(T_REPLAY);
                     lo->run(model, cur.inlier_number, cur.score);
                     if (lo->rc) return lo->rc;
+                    lap(T_LO);
                 }
                 best = cur;
                 memcpy(best_model, model, sizeof(best_model));
@@ -1299,6 +1314,7 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
         return fail(c, USAC_ERR_NO_MODEL, "best score is 0 (ransac.cpp:143-147)");
     }
 
+    lap(T_REPLAY);
     // ---- polish (ransac.cpp:157-207) on the device
     if ((rc = score_inliers(best_model))) return rc;  // quality->getInliers(best_model)
     int prev = 0;
@@ -1319,6 +1335,13 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
         out->polish_passes++;
     }
     const auto t1 = std::chrono::steady_clock::now();
+    lap(T_POLISH);
+    if (getenv("USAC_PROFILE"))
+        fprintf(stderr,
+                "usac_ransac_run ms: setup %.3f draw %.3f device %.3f sums %.3f replay %.3f lo %.3f polish %.3f "
+                "(lo rounds %u stages %u)\n",
+                tsplit[T_SETUP], tsplit[T_DRAW], tsplit[T_DEVICE], tsplit[T_SUMS], tsplit[T_REPLAY], tsplit[T_LO],
+                tsplit[T_POLISH], lo ? lo->rounds : 0u, lo ? lo->stages : 0u);
     if ((rc = score_inliers(best_model))) return rc;  // ransac.cpp:214
     if (inliers_out && cnt > 0)
         HIP_TRY(c, hipMemcpy(inliers_out, c->inl_idx.p, sizeof(int32_t) * (size_t)cnt, hipMemcpyDeviceToHost));

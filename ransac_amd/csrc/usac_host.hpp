@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <unordered_map>
 #include <vector>
 
 namespace usac {
@@ -450,43 +451,74 @@ class Sprt {
 // ascending index order (what the reference's pair loop over each cell produces).  CSR.
 class GridNeighbors {
    public:
-    GridNeighbors(const float *pts, uint32_t n, int cell_size) : off_(n + 1, 0) {
+    // neighbours of point i = the other points of its 4-D cell, ascending index.  Stored as
+    // the cells' member lists (O(n), not the O(sum cell^2) pair lists): point i knows its
+    // cell and its rank in it, and neighbour k skips that rank.
+    GridNeighbors(const float *pts, uint32_t n, int cell_size) : cell_(n), rank_(n), members_(n) {
         struct Key {
             int c[4];
-            uint32_t i;
+            bool operator==(const Key &o) const {
+                return c[0] == o.c[0] && c[1] == o.c[1] && c[2] == o.c[2] && c[3] == o.c[3];
+            }
         };
+        struct Hash {
+            size_t operator()(const Key &k) const {
+                uint64_t h = 0x9e3779b97f4a7c15ull;
+                for (int j = 0; j < 4; j++) {
+                    h ^= (uint32_t)k.c[j];
+                    h *= 0xff51afd7ed558ccdull;
+                    h ^= h >> 32;
+                }
+                return (size_t)h;
+            }
+        };
+        std::vector<uint32_t> size;
         std::vector<Key> keys(n);
-        for (uint32_t i = 0; i < n; i++) {
-            for (int k = 0; k < 4; k++) keys[i].c[k] = (int)(pts[4 * (size_t)i + k] / (float)cell_size);
-            keys[i].i = i;
+        bool packable = true;
+        for (uint32_t i = 0; i < n; i++)
+            for (int j = 0; j < 4; j++) {
+                const int v = (int)(pts[4 * (size_t)i + j] / (float)cell_size);
+                keys[i].c[j] = v;
+                packable &= v >= -32768 && v <= 32767;
+            }
+        if (packable) {  // open addressing on the 64-bit packed cell
+            size_t cap = 16;
+            while (cap < 2 * (size_t)n) cap <<= 1;
+            std::vector<uint64_t> slot_key(cap);
+            std::vector<uint32_t> slot_id(cap, UINT32_MAX);
+            for (uint32_t i = 0; i < n; i++) {
+                uint64_t k = 0;
+                for (int j = 0; j < 4; j++) k = (k << 16) | (uint16_t)(int16_t)keys[i].c[j];
+                size_t h = (size_t)((k * 0x9e3779b97f4a7c15ull) >> 20) & (cap - 1);
+                while (slot_id[h] != UINT32_MAX && slot_key[h] != k) h = (h + 1) & (cap - 1);
+                if (slot_id[h] == UINT32_MAX) {
+                    slot_key[h] = k;
+                    slot_id[h] = (uint32_t)size.size();
+                    size.push_back(0);
+                }
+                cell_[i] = slot_id[h];
+                rank_[i] = size[cell_[i]]++;
+            }
+        } else {
+            std::unordered_map<Key, uint32_t, Hash> ids;
+            ids.reserve(n);
+            for (uint32_t i = 0; i < n; i++) {
+                auto it = ids.emplace(keys[i], (uint32_t)size.size());
+                if (it.second) size.push_back(0);
+                cell_[i] = it.first->second;
+                rank_[i] = size[cell_[i]]++;
+            }
         }
-        std::sort(keys.begin(), keys.end(), [](const Key &a, const Key &b) {
-            for (int k = 0; k < 4; k++)
-                if (a.c[k] != b.c[k]) return a.c[k] < b.c[k];
-            return a.i < b.i;
-        });
-        std::vector<std::pair<uint32_t, uint32_t>> cell(n);  // (first, end) sorted position range
-        for (uint32_t a = 0; a < n;) {
-            uint32_t b = a + 1;
-            while (b < n && std::equal(keys[a].c, keys[a].c + 4, keys[b].c)) b++;
-            for (uint32_t k = a; k < b; k++) off_[keys[k].i + 1] = b - a - 1;
-            for (uint32_t k = a; k < b; k++) cell[k] = {a, b};
-            a = b;
-        }
-        for (uint32_t i = 0; i < n; i++) off_[i + 1] += off_[i];
-        nb_.resize(off_[n]);
-        for (uint32_t u = 0; u < n; u++) {
-            uint32_t w = off_[keys[u].i];
-            for (uint32_t v = cell[u].first; v < cell[u].second; v++)
-                if (v != u) nb_[w++] = (int32_t)keys[v].i;
-        }
+        start_.assign(size.size() + 1, 0);
+        for (size_t c = 0; c < size.size(); c++) start_[c + 1] = start_[c] + size[c];
+        for (uint32_t i = 0; i < n; i++) members_[start_[cell_[i]] + rank_[i]] = (int32_t)i;
     }
-    uint32_t count(uint32_t i) const { return off_[i + 1] - off_[i]; }
-    const int32_t *list(uint32_t i) const { return nb_.data() + off_[i]; }
+    uint32_t count(uint32_t i) const { return start_[cell_[i] + 1] - start_[cell_[i]] - 1; }
+    int32_t at(uint32_t i, uint32_t k) const { return members_[start_[cell_[i]] + (k < rank_[i] ? k : k + 1)]; }
 
    private:
-    std::vector<uint32_t> off_;
-    std::vector<int32_t> nb_;
+    std::vector<uint32_t> cell_, rank_, start_;
+    std::vector<int32_t> members_;
 };
 
 // NapsacSampler (grid): ArrayRandomGenerator pool over [0, n) on the shared glibc stream
@@ -516,10 +548,9 @@ class NapsacSampler {
             return;
         }
         sample[0] = init;
-        const int32_t *nb = g_.list((uint32_t)init);
         const uint32_t sz = g_.count((uint32_t)init);
         for (uint32_t k = 1; k < m_; k++) {
-            sample[k] = nb[next_[init]];
+            sample[k] = g_.at((uint32_t)init, next_[init]);
             if (++next_[init] >= sz) next_[init] = 0;
         }
     }
