@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define USAC_ABI_VERSION 5
+#define USAC_ABI_VERSION 6
 
 /* = enum ESTIMATOR (usac/model.hpp:10) */
 enum { USAC_LINE2D = 1, USAC_HOMOGRAPHY = 2, USAC_FUNDAMENTAL = 3, USAC_ESSENTIAL = 4 };
@@ -57,6 +57,9 @@ enum { USAC_LINE2D = 1, USAC_HOMOGRAPHY = 2, USAC_FUNDAMENTAL = 3, USAC_ESSENTIA
 enum { USAC_SAMPLER_UNIFORM = 1, USAC_SAMPLER_NAPSAC = 3, USAC_SAMPLER_PROSAC = 4 };
 /* = enum LocOpt (usac/model.hpp:13): inner + iterative LO-RANSAC (unlimited / limited) */
 enum { USAC_LO_NONE = 0, USAC_LO_INITLORSC = 1, USAC_LO_INITFLORSC = 2 };
+/* = enum NeighborsSearch (usac/model.hpp:12): the Ransac ctor (ransac.hpp:60-78) builds Grid
+ * neighbours for Grid and nanoflann KNN for any other value (NullN included) */
+enum { USAC_NEIGHBORS_NULL = 0, USAC_NEIGHBORS_NANOFLANN = 1, USAC_NEIGHBORS_GRID = 2 };
 /* 4-pt DLT: THIN = reference semantics (vt.row(7) of the thin 8x9 SVD, dlt.cpp:43-48);
  * NULLSPACE = true null vector. */
 enum { USAC_DLT_THIN = 0, USAC_DLT_NULLSPACE = 1 };
@@ -98,6 +101,8 @@ typedef struct usac_params {
     uint32_t lo_inner_iterations;     /* model.hpp:29 (20) */
     uint32_t lo_threshold_multiplier; /* model.hpp:30 (10) */
     int32_t cell_size;                /* model.hpp:43 (50): NAPSAC grid cell */
+    int32_t neighbors;                /* USAC_NEIGHBORS_* (model.hpp:42): NAPSAC Grid or KNN */
+    uint32_t knn;                     /* model.hpp:23 k_nearest_neighbors (NAPSAC KNN, 1..32) */
 } usac_params;
 
 /* RansacOutput getters (ransac_output.hpp:57-97) */
@@ -145,6 +150,11 @@ int usac_score_models(usac_ctx *ctx, const float *models, uint32_t n_models, flo
                       float *sums);
 /* One model: ascending inlier indices (idx capacity >= n points), count and sum. */
 int usac_get_inliers(usac_ctx *ctx, const float *model, float thr, int32_t *idx, uint32_t *n, float *sum);
+/* NearestNeighbors::getNearestNeighbors_nanoflann (nearest_neighbors.cpp:69-128) on the
+ * device: the k nearest neighbours of every point (1 <= k <= 32; idx n x k, d2 n x k
+ * squared distances, nullable) by nanoflann's float L2 distance, the point itself excluded,
+ * ascending distance, equal distances by ascending index; -1 / +inf where n - 1 < k. */
+int usac_knn(usac_ctx *ctx, uint32_t k, int32_t *idx, float *d2);
 /* Non-minimal least squares on the listed points; returns USAC_OK and writes model. */
 int usac_nonminimal(usac_ctx *ctx, const int32_t *idx, uint32_t n, float *model);
 
@@ -197,8 +207,8 @@ int usac_draw_samples(usac_ctx *ctx, uint32_t B, uint64_t seed, uint64_t first_h
 /* ---- loop --------------------------------------------------------------------- */
 uint32_t usac_std_termination(uint32_t inliers, uint32_t points_size, uint32_t sample_size, float desired_prob,
                               uint32_t max_iterations);
-/* Ransac::run (ransac.cpp:14-238) with the Uniform (glibc random() stream), NAPSAC (grid
- * neighbours, napsac_sampler.hpp) or PROSAC (prosac_sampler.hpp + prosac_termination_criteria.hpp)
+/* Ransac::run (ransac.cpp:14-238) with the Uniform (glibc random() stream), NAPSAC (grid or
+ * KNN neighbours, napsac_sampler.hpp) or PROSAC (prosac_sampler.hpp + prosac_termination_criteria.hpp)
  * sampler, optional SPRT (sprt.hpp; pool shuffle from the same glibc stream), optional
  * inner + iterative LO-RANSAC (inner_local_optimization.hpp, iterative_local_optimization.hpp;
  * its mt19937 seeded with seed + 1).  inliers_out (capacity n,

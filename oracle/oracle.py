@@ -42,6 +42,7 @@ SAMPLER_UNIFORM, SAMPLER_NAPSAC, SAMPLER_PROSAC = 1, 3, 4  # usac/model.hpp:11
 
 
 LO_NONE, LO_INITLORSC, LO_INITFLORSC = 0, 1, 2  # usac/model.hpp:13
+NEIGHBORS_NULL, NEIGHBORS_NANOFLANN, NEIGHBORS_GRID = 0, 1, 2  # usac/model.hpp:12 (NeighborsSearch)
 
 
 class OrcConfig(ctypes.Structure):
@@ -49,7 +50,7 @@ class OrcConfig(ctypes.Structure):
                 ("seed", ctypes.c_uint), ("dlt_mode", ctypes.c_int), ("sampler", ctypes.c_int), ("sprt", ctypes.c_int),
                 ("lo", ctypes.c_int), ("lo_sample_size", ctypes.c_uint), ("lo_iterative_iterations", ctypes.c_uint),
                 ("lo_inner_iterations", ctypes.c_uint), ("lo_threshold_multiplier", ctypes.c_uint),
-                ("cell_size", ctypes.c_int)]
+                ("cell_size", ctypes.c_int), ("neighbors", ctypes.c_int), ("knn", ctypes.c_uint)]
 
 
 class OrcMT(ctypes.Structure):
@@ -271,7 +272,8 @@ def std_termination(inliers, n, m, p, max_iters=10000):
 
 
 def ransac_run(kind, points, thr, p, seed, max_iters=10000, dlt_mode=DLT_THIN, rec_cap=4096,
-               sampler=SAMPLER_UNIFORM, sprt=False, lo=LO_NONE, lo_params=(14, 4, 20, 10), cell_size=50):
+               sampler=SAMPLER_UNIFORM, sprt=False, lo=LO_NONE, lo_params=(14, 4, 20, 10), cell_size=50,
+               neighbors=NEIGHBORS_GRID, knn=7):
     points = np.ascontiguousarray(points, dtype=np.float32)
     n = points.shape[0]
     res = OrcResult()
@@ -279,7 +281,8 @@ def ransac_run(kind, points, thr, p, seed, max_iters=10000, dlt_mode=DLT_THIN, r
     ri = np.zeros(rec_cap, dtype=np.uint32)
     rc = np.zeros(rec_cap, dtype=np.int32)
     rs = np.zeros(rec_cap, dtype=np.float32)
-    cfg = OrcConfig(thr, p, max_iters, seed, dlt_mode, sampler, 1 if sprt else 0, lo, *lo_params, cell_size)
+    cfg = OrcConfig(thr, p, max_iters, seed, dlt_mode, sampler, 1 if sprt else 0, lo, *lo_params, cell_size,
+                    neighbors, knn)
     ret = lib().orc_ransac_run_cfg(kind, _p(points, _f32p), n, ctypes.byref(cfg), ctypes.byref(res), _p(inl, _i32p),
                                    _p(ri, _u32p), _p(rc, _i32p), _p(rs, _f32p), rec_cap)
     k = min(res.n_records, rec_cap)
@@ -299,6 +302,20 @@ def ransac_run(kind, points, thr, p, seed, max_iters=10000, dlt_mode=DLT_THIN, r
         "lo_inner_iters": res.lo_inner_iters,
         "lo_iterative_iters": res.lo_iterative_iters,
     }
+
+
+def knn(points, k):
+    """KNN neighbours (nearest_neighbors.cpp:69-128): (idx n x k int32, d2 n x k float32),
+    self excluded, equal distances by ascending index."""
+    L = lib()
+    pts = np.ascontiguousarray(points, dtype=np.float32)
+    n, cols = pts.shape
+    idx = np.zeros((n, k), dtype=np.int32)
+    d2 = np.zeros((n, k), dtype=np.float32)
+    L.orc_knn.argtypes = [_f32p, ctypes.c_uint, ctypes.c_uint, ctypes.c_uint, _i32p, _f32p]
+    L.orc_knn.restype = None
+    L.orc_knn(_p(pts, _f32p), n, cols, k, _p(idx, _i32p), _p(d2, _f32p))
+    return idx, d2
 
 
 def grid_neighbors(points, cell_size):

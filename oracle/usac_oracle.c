@@ -291,6 +291,7 @@ void orc_est_free(orc_est *e) { free(e); }
 int orc_est_sample_size(const orc_est *e) {
     return e->kind == ORC_LINE2D ? 2 : e->kind == ORC_FUNDAMENTAL ? 7 : e->kind == ORC_ESSENTIAL ? 5 : 4;
 }
+static int orc_est_cols(const orc_est *e) { return e->kind == ORC_LINE2D ? 2 : 4; }
 int orc_est_max_models(const orc_est *e) { return e->kind == ORC_FUNDAMENTAL ? 3 : 1; }
 
 /* DLt::DLT4p (usac/estimator/dlt/dlt.cpp:7-52): rows of A built in fp32 exactly as
@@ -1965,6 +1966,98 @@ void orc_napsac_sample(orc_napsac *s, int *sample) {
     }
 }
 
+/* ------------------------------------------------------------ KNN neighbours */
+/* NearestNeighbors::getNearestNeighbors_nanoflann (nearest_neighbors.cpp:69-128): the k
+ * nearest points of every point by nanoflann's L2_Adaptor squared distance in float --
+ * components in groups of four, result += d0*d0 + d1*d1 + d2*d2 + d3*d3, then the rest one
+ * by one (nanoflann.hpp L2_Adaptor::evalMetric; the version is unpinned, this form is the
+ * same in all releases) -- the query itself excluded (the reference drops the first result,
+ * which is the point itself).  Equal distances: ascending index (nanoflann keeps the order
+ * its KD-tree visits them in -- unpinned).  Fewer than k other points: index -1, distance
+ * +inf. */
+float orc_l2_dist(const float *a, const float *b, unsigned int cols) {
+    float r = 0.f;
+    unsigned int d = 0;
+    for (; d + 4 <= cols; d += 4) {
+        const float d0 = a[d] - b[d], d1 = a[d + 1] - b[d + 1], d2 = a[d + 2] - b[d + 2], d3 = a[d + 3] - b[d + 3];
+        r += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+    }
+    for (; d < cols; d++) {
+        const float d0 = a[d] - b[d];
+        r += d0 * d0;
+    }
+    return r;
+}
+
+void orc_knn(const float *pts, unsigned int n, unsigned int cols, unsigned int k, int *idx, float *d2) {
+    for (unsigned int p = 0; p < n; p++) {
+        int *li = idx + (size_t)p * k;
+        float *ld = d2 + (size_t)p * k;
+        for (unsigned int t = 0; t < k; t++) {
+            li[t] = -1;
+            ld[t] = INFINITY;
+        }
+        for (unsigned int j = 0; j < n; j++) {
+            if (j == p) continue;
+            const float d = orc_l2_dist(pts + (size_t)p * cols, pts + (size_t)j * cols, cols);
+            if (!(d < ld[k - 1])) continue; /* ties keep the earlier (smaller) index; NaN never enters */
+            unsigned int t = k - 1;
+            while (t > 0 && ld[t - 1] > d) {
+                ld[t] = ld[t - 1];
+                li[t] = li[t - 1];
+                t--;
+            }
+            ld[t] = d;
+            li[t] = (int)j;
+        }
+    }
+}
+
+/* NapsacSampler::generateSampleKNN (napsac_sampler.hpp:76-98): the initial point from the
+ * ArrayRandomGenerator pool, then m - 1 points walking its neighbour row from the farthest
+ * (column knn - 1) backwards, cyclically, the per-point cursor persisting across samples. */
+struct orc_napsac_knn {
+    const int *nb;
+    unsigned int n, m, knn, max;
+    int *array, *next;
+};
+
+orc_napsac_knn *orc_napsac_knn_new(const int *nb, unsigned int n, unsigned int m, unsigned int knn) {
+    orc_napsac_knn *s = (orc_napsac_knn *)calloc(1, sizeof(*s));
+    s->nb = nb;
+    s->n = n;
+    s->m = m;
+    s->knn = knn;
+    s->array = (int *)malloc(sizeof(int) * (n ? n : 1));
+    for (unsigned int i = 0; i < n; i++) s->array[i] = (int)i;
+    s->next = (int *)calloc(n ? n : 1, sizeof(int));
+    s->max = 0;
+    return s;
+}
+
+void orc_napsac_knn_free(orc_napsac_knn *s) {
+    if (!s) return;
+    free(s->array);
+    free(s->next);
+    free(s);
+}
+
+void orc_napsac_knn_sample(orc_napsac_knn *s, int *sample) {
+    if (s->max == 0) s->max = s->n; /* ArrayRandomGenerator::getRandomNumber */
+    const unsigned int r = (unsigned int)random() % s->max;
+    const int init = s->array[r];
+    s->max--;
+    s->array[r] = s->array[s->max];
+    s->array[s->max] = init;
+    sample[0] = init;
+    const int knn = (int)s->knn;
+    for (unsigned int i = 1; i < s->m; i++) {
+        sample[i] = s->nb[(size_t)knn * (size_t)init + (size_t)(s->next[init] + knn - 1)];
+        s->next[init]--;
+        if (s->next[init] == -knn) s->next[init] = 0;
+    }
+}
+
 /* ------------------------------------------------------------ LO-RANSAC */
 /* InnerLocalOptimization (inner_local_optimization.hpp:40-133) + IterativeLocalOptimization
  * (iterative_local_optimization.hpp:28-136).  Its UniformRandomGenerator is an mt19937 seeded
@@ -2081,8 +2174,20 @@ int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_
     orc_lo lo;
     const int use_lo = cfg->lo == ORC_LO_INITLORSC || cfg->lo == ORC_LO_INITFLORSC;
     if (use_lo) lo_init(&lo, cfg, n, (unsigned int)m);
-    orc_grid *grid = napsac ? orc_grid_new(points, n, cfg->cell_size) : NULL;
-    orc_napsac *ns = napsac ? orc_napsac_new(grid, n, (unsigned int)m) : NULL;
+    /* Ransac ctor (ransac.hpp:60-78): Grid neighbours, or nanoflann KNN for any other type */
+    const int knn_mode = napsac && cfg->neighbors != ORC_NEIGHBORS_GRID;
+    orc_grid *grid = napsac && !knn_mode ? orc_grid_new(points, n, cfg->cell_size) : NULL;
+    orc_napsac *ns = grid ? orc_napsac_new(grid, n, (unsigned int)m) : NULL;
+    int *knn_tab = NULL;
+    orc_napsac_knn *nk = NULL;
+    if (knn_mode) {
+        const unsigned int k = cfg->knn;
+        knn_tab = (int *)malloc(sizeof(int) * (size_t)n * (k ? k : 1));
+        float *kd = (float *)malloc(sizeof(float) * (size_t)n * (k ? k : 1));
+        orc_knn(points, n, (unsigned int)orc_est_cols(e), k, knn_tab, kd);
+        free(kd);
+        nk = orc_napsac_knn_new(knn_tab, n, (unsigned int)m, k);
+    }
     orc_prosac_term *pt = prosac ? orc_prosac_term_new(orc_prosac_growth(ps), n, (unsigned int)m, cfg->desired_prob,
                                                        cfg->max_iterations)
                                  : NULL;
@@ -2103,6 +2208,8 @@ int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_
         if (prosac) {
             orc_prosac_set_term_len(ps, orc_prosac_term_length(pt));
             orc_prosac_sample(ps, sample);
+        } else if (nk) {
+            orc_napsac_knn_sample(nk, sample);
         } else if (napsac) {
             orc_napsac_sample(ns, sample);
         } else {
@@ -2193,6 +2300,8 @@ int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_
     orc_prosac_term_free(pt);
     orc_sprt_free(sp);
     orc_napsac_free(ns);
+    orc_napsac_knn_free(nk);
+    free(knn_tab);
     orc_grid_free(grid);
     if (use_lo) lo_free(&lo);
     orc_est_free(e);

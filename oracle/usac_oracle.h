@@ -107,7 +107,18 @@ typedef struct {
     int lo;      /* ORC_LO_* */
     unsigned int lo_sample_size, lo_iterative_iterations, lo_inner_iterations, lo_threshold_multiplier; /* model.hpp:27-30 */
     int cell_size; /* model.hpp:43 */
+    int neighbors;        /* ORC_NEIGHBORS_* (model.hpp:12,42): Grid, else nanoflann KNN */
+    unsigned int knn;     /* model.hpp:23 k_nearest_neighbors (NAPSAC KNN) */
 } orc_config;
+enum { ORC_NEIGHBORS_NULL = 0, ORC_NEIGHBORS_NANOFLANN = 1, ORC_NEIGHBORS_GRID = 2 }; /* = NeighborsSearch */
+
+/* KNN neighbours (nearest_neighbors.cpp:69-128): idx/d2 n x k, self excluded, ties by index */
+float orc_l2_dist(const float *a, const float *b, unsigned int cols);
+void orc_knn(const float *pts, unsigned int n, unsigned int cols, unsigned int k, int *idx, float *d2);
+typedef struct orc_napsac_knn orc_napsac_knn;
+orc_napsac_knn *orc_napsac_knn_new(const int *nb, unsigned int n, unsigned int m, unsigned int knn);
+void orc_napsac_knn_free(orc_napsac_knn *s);
+void orc_napsac_knn_sample(orc_napsac_knn *s, int *sample);
 
 /* grid neighbours (nearest_neighbors.cpp:160-202) and the NAPSAC grid sampler (napsac_sampler.hpp) */
 typedef struct orc_grid orc_grid;

@@ -46,7 +46,7 @@ class LocOpt(enum.IntEnum):  # usac/model.hpp:13 (GC and IRLS are out of scope)
     InItFLORsc = 2
 
 
-class NeighborsSearch(enum.IntEnum):  # usac/model.hpp:12 (Nanoflann KNN is out of scope)
+class NeighborsSearch(enum.IntEnum):  # usac/model.hpp:12 (NullN / Nanoflann = KNN on the device)
     NullN = 0
     Nanoflann = 1
     Grid = 2
@@ -78,7 +78,7 @@ class _Params(ctypes.Structure):
                 ("sampler", ctypes.c_int32), ("sprt", ctypes.c_int32), ("lo", ctypes.c_int32),
                 ("lo_sample_size", ctypes.c_uint32), ("lo_iterative_iterations", ctypes.c_uint32),
                 ("lo_inner_iterations", ctypes.c_uint32), ("lo_threshold_multiplier", ctypes.c_uint32),
-                ("cell_size", ctypes.c_int32)]
+                ("cell_size", ctypes.c_int32), ("neighbors", ctypes.c_int32), ("knn", ctypes.c_uint32)]
 
 
 class _RunOutput(ctypes.Structure):
@@ -94,7 +94,8 @@ class _RunOutput(ctypes.Structure):
 # every symbol include/usac_gpu.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = [
     "usac_create", "usac_destroy", "usac_last_error", "usac_abi_version", "usac_set_dlt_mode", "usac_sample_size",
-    "usac_num_points", "usac_estimate_models", "usac_score_models", "usac_get_inliers", "usac_nonminimal",
+    "usac_num_points", "usac_estimate_models", "usac_score_models", "usac_get_inliers", "usac_knn",
+    "usac_nonminimal",
     "usac_hypothesize_score", "usac_hypothesize_async", "usac_fetch_best", "usac_sync", "usac_last_timings",
     "usac_set_score_chunks", "usac_set_score_variant", "usac_std_termination", "usac_ransac_run", "usac_uniform_samples",
     "usac_prosac_samples", "usac_sprt_pool", "usac_set_sprt", "usac_sprt_tested", "usac_set_device_sampler",
@@ -135,6 +136,7 @@ def lib():
         "usac_estimate_models": (ctypes.c_int, [_vp, i32p, ctypes.c_uint32, f32p, i32p]),
         "usac_score_models": (ctypes.c_int, [_vp, f32p, ctypes.c_uint32, ctypes.c_float, i32p, f32p]),
         "usac_get_inliers": (ctypes.c_int, [_vp, f32p, ctypes.c_float, i32p, u32p, f32p]),
+        "usac_knn": (ctypes.c_int, [_vp, ctypes.c_uint32, i32p, f32p]),
         "usac_nonminimal": (ctypes.c_int, [_vp, i32p, ctypes.c_uint32, f32p]),
         "usac_hypothesize_score": (ctypes.c_int, [_vp, i32p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
                                                   ctypes.c_float, i32p, f32p, _P(Record)]),
@@ -285,6 +287,16 @@ class Context:
         self._check(lib().usac_score_models(self._h, _ptr(full, ctypes.c_float), full.shape[0], ctypes.c_float(thr),
                                             _ptr(c, ctypes.c_int32), _ptr(s, ctypes.c_float)), "score_models")
         return c, s
+
+    def knn(self, k, distances=True):
+        """NearestNeighbors::getNearestNeighbors_nanoflann (nearest_neighbors.cpp:69-128) on the
+        device -> (idx n x k int32, d2 n x k float32 or None): self excluded, ascending squared
+        distance, equal distances by ascending index, -1 / inf where n - 1 < k."""
+        idx = np.zeros((self.n, int(k)), dtype=np.int32)
+        d2 = np.zeros((self.n, int(k)), dtype=np.float32) if distances else None
+        self._check(lib().usac_knn(self._h, int(k), _ptr(idx, ctypes.c_int32),
+                                   _ptr(d2, ctypes.c_float) if distances else None), "knn")
+        return idx, d2
 
     def get_inliers(self, model, thr):
         """Quality::getNumberInliers(get_inliers=true) -> (count, sum, ascending indices)."""
@@ -504,11 +516,9 @@ class Ransac:
 
     def __init__(self, model, points):
         if model.sampler not in (SAMPLER.Uniform, SAMPLER.Prosac, SAMPLER.Napsac):
-            raise NotImplementedError("sampler %s is not in ABI v3 (Uniform, Napsac, Prosac)" % model.sampler.name)
-        if model.sampler == SAMPLER.Napsac and model.neighborsType == NeighborsSearch.Nanoflann:
-            raise NotImplementedError("NAPSAC KNN neighbours (nanoflann) are not in ABI v3; use the Grid")
+            raise NotImplementedError("sampler %s is not supported (Uniform, Napsac, Prosac)" % model.sampler.name)
         if int(model.lo) not in (0, 1, 2):
-            raise NotImplementedError("LO %r is not in ABI v3 (InItLORsc, InItFLORsc)" % model.lo)
+            raise NotImplementedError("LO %r is not supported (InItLORsc, InItFLORsc)" % model.lo)
         self.model = model
         self.ctx = Context(model.estimator, points, device=model.device)
         self._out = None
@@ -522,7 +532,8 @@ class Ransac:
             seed = int.from_bytes(os.urandom(4), "little") or 1
         p = _Params(m.threshold, m.desired_prob, m.max_iterations, seed, int(m.dlt_mode), m.batch, int(m.sampler),
                     1 if m.sprt else 0, int(m.lo), m.lo_sample_size, m.lo_iterative_iterations,
-                    m.lo_inner_iterations, m.lo_threshold_multiplier, m.cell_size)
+                    m.lo_inner_iterations, m.lo_threshold_multiplier, m.cell_size, int(m.neighborsType),
+                    m.k_nearest_neighbors)
         out = _RunOutput()
         inl = np.zeros(self.ctx.n, dtype=np.int32)
         recs = (Record * rec_cap)()

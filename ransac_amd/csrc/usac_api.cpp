@@ -72,6 +72,7 @@ struct usac_ctx {
     // fit flags, scores, fit and scoring scratch; lo_max = the current best's inlier list
     DevBuf lo_max, lo_lists, lo_pos, lo_ns, lo_thrs, lo_slots, lo_models, lo_ok, lo_cnts, lo_sums, lo_q, lo_part,
         lo_ws, lo_scr;
+    DevBuf knn_idx, knn_d2;  // KNN neighbour table (usac_knn, NAPSAC KNN)
     DevBuf e5_ws;                      // staged 5-point solver workspace
     // throughput SPRT (usac_set_sprt): batch-fixed test on the pool-ordered points
     bool sprt_on = false;
@@ -711,7 +712,7 @@ void usac_destroy(usac_ctx *c) {
                       &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok,
                       &c->rec_send, &c->rec_all, &c->tv_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
-                      &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr})
+                      &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2})
         b->release();
     for (auto &ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -827,6 +828,20 @@ int usac_get_inliers(usac_ctx *c, const float *model, float thr, int32_t *idx, u
         HIP_TRY(c, hipMemcpy(idx, c->inl_idx.p, sizeof(int32_t) * (size_t)cnt, hipMemcpyDeviceToHost));
     if (n) *n = (uint32_t)cnt;
     if (sum) *sum = s;
+    return USAC_OK;
+}
+
+int usac_knn(usac_ctx *c, uint32_t k, int32_t *idx, float *d2) {
+    if (!c || !idx || k == 0 || k > usac::kKnnMax) return USAC_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    const size_t nk = (size_t)c->n * k;
+    HIP_TRY(c, c->knn_idx.reserve(sizeof(int32_t) * nk));
+    if (d2) HIP_TRY(c, c->knn_d2.reserve(sizeof(float) * nk));
+    HIP_TRY(c, usac::launch_knn(c->stream, c->pts.as<float>(), c->n, c->cols, k, c->knn_idx.as<int32_t>(),
+                                d2 ? c->knn_d2.as<float>() : nullptr));
+    HIP_TRY(c, hipMemcpyAsync(idx, c->knn_idx.p, sizeof(int32_t) * nk, hipMemcpyDeviceToHost, c->stream));
+    if (d2) HIP_TRY(c, hipMemcpyAsync(d2, c->knn_d2.p, sizeof(float) * nk, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     return USAC_OK;
 }
 
@@ -1046,9 +1061,13 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
     const bool napsac = prm->sampler == USAC_SAMPLER_NAPSAC;
     if (!prosac && !napsac && prm->sampler != USAC_SAMPLER_UNIFORM && prm->sampler != 0)
         return fail(c, USAC_ERR_UNSUPPORTED, "sampler not supported (Uniform, Napsac, Prosac)");
-    if (napsac && c->cols != 4)
+    const bool knn_mode = napsac && prm->neighbors != USAC_NEIGHBORS_GRID;  // ransac.hpp:62-78
+    if (napsac && !knn_mode && c->cols != 4)
         return fail(c, USAC_ERR_ARG, "NAPSAC grid neighbours need 4-column points (SURVEY Q17)");
-    if (napsac && prm->cell_size <= 0) return fail(c, USAC_ERR_ARG, "NAPSAC cell_size must be > 0");
+    if (napsac && !knn_mode && prm->cell_size <= 0) return fail(c, USAC_ERR_ARG, "NAPSAC cell_size must be > 0");
+    if (knn_mode && (prm->knn == 0 || prm->knn > usac::kKnnMax || prm->knn + 1 < c->m))
+        return fail(c, USAC_ERR_ARG, "NAPSAC KNN: k_nearest_neighbors must be in [sample_size - 1, 32] "
+                                     "(napsac_sampler.hpp:48)");
     const bool use_lo = prm->lo == USAC_LO_INITLORSC || prm->lo == USAC_LO_INITFLORSC;
     if (prm->lo != USAC_LO_NONE && !use_lo) return fail(c, USAC_ERR_UNSUPPORTED, "LO: InItLORsc / InItFLORsc only");
     if (use_lo && (prm->lo_sample_size == 0 || prm->lo_iterative_iterations == 0))
@@ -1096,9 +1115,15 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
     std::unique_ptr<usac::ProsacTerminationCriteria> pterm;
     std::unique_ptr<usac::GridNeighbors> grid;
     std::unique_ptr<usac::NapsacSampler> nap;
+    std::unique_ptr<usac::NapsacKnnSampler> napk;
+    std::vector<int32_t> knn_tab;
     if (prosac) {
         pro.reset(new usac::ProsacSampler(prm->seed, n, m));
         pterm.reset(new usac::ProsacTerminationCriteria(pro->growth(), prm->desired_prob, m, n, prm->max_iterations));
+    } else if (knn_mode) {  // NearestNeighbors::getNearestNeighbors_nanoflann on the device
+        knn_tab.resize((size_t)n * prm->knn);
+        if ((rc = usac_knn(c, prm->knn, knn_tab.data(), nullptr))) return rc;
+        napk.reset(new usac::NapsacKnnSampler(grng, knn_tab.data(), n, m, prm->knn));
     } else if (napsac) {
         std::vector<float> hp((size_t)n * 4);
         HIP_TRY(c, hipMemcpy(hp.data(), c->pts.p, sizeof(float) * hp.size(), hipMemcpyDeviceToHost));
@@ -1164,6 +1189,8 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
                 subset_at[j] = pro->subset();
                 pro->generateSample(smp, gen_term);
                 largest_at[j] = pro->largest();
+            } else if (napk) {
+                napk->generateSample(smp);
             } else if (napsac) {
                 // the reference reuses one sample array: a sample the sampler leaves
                 // (partly) unwritten keeps the previous sample's entries

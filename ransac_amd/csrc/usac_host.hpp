@@ -13,6 +13,7 @@
 //   usac::Sprt                       sprt.hpp:89-491 (decisions on device inlier masks)
 //   usac::GridNeighbors              nearest_neighbors.cpp:160-202
 //   usac::NapsacSampler              napsac_sampler.hpp:40-158 (grid), array_random_generator.hpp
+//   usac::NapsacKnnSampler           napsac_sampler.hpp:76-98 (KNN rows from usac_knn)
 #pragma once
 #include <stdint.h>
 #include <stdlib.h>
@@ -571,6 +572,39 @@ class NapsacSampler {
     std::vector<uint32_t> next_;
     uint32_t n_, m_, max_ = 0;
     bool uniform_ = false;
+};
+
+// NapsacSampler::generateSampleKNN (napsac_sampler.hpp:76-98): the initial point from the
+// ArrayRandomGenerator pool on the shared glibc stream (member max = 0), then m - 1
+// neighbours walking the point's KNN row (ascending distance) from the farthest, backwards
+// and cyclically; the per-point cursor persists across samples.
+class NapsacKnnSampler {
+   public:
+    NapsacKnnSampler(GlibcRandom &rng, const int32_t *nb, uint32_t n, uint32_t m, uint32_t knn)
+        : rng_(rng), nb_(nb), array_(n), next_(n, 0), n_(n), m_(m), knn_((int)knn) {
+        for (uint32_t i = 0; i < n; i++) array_[i] = (int32_t)i;
+    }
+    void generateSample(int32_t *sample) {
+        if (max_ == 0) max_ = n_;
+        const uint32_t k = rng_.next() % max_;
+        const int32_t init = array_[k];
+        max_--;
+        array_[k] = array_[max_];
+        array_[max_] = init;
+        sample[0] = init;
+        for (uint32_t i = 1; i < m_; i++) {
+            sample[i] = nb_[(size_t)knn_ * (size_t)init + (size_t)(next_[init] + knn_ - 1)];
+            if (--next_[init] == -knn_) next_[init] = 0;
+        }
+    }
+
+   private:
+    GlibcRandom &rng_;
+    const int32_t *nb_;
+    std::vector<int32_t> array_;
+    std::vector<int> next_;
+    uint32_t n_, m_, max_ = 0;
+    int knn_;
 };
 
 }  // namespace usac

@@ -126,4 +126,10 @@ struct NmBatch {
 hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pts, const NmBatch &b);
 size_t nonminimal_partial_stride(uint32_t nmax);
 
+// k nearest neighbours of every point (kernels_knn.hip, nearest_neighbors.cpp:69-128):
+// idx / d2 (nullable) n x k, self excluded, ascending distance, ties by index; 1 <= k <= 32
+constexpr uint32_t kKnnMax = 32;
+hipError_t launch_knn(hipStream_t st, const float *pts, uint32_t n, uint32_t cols, uint32_t k, int32_t *idx,
+                      float *d2);
+
 }  // namespace usac
