@@ -55,8 +55,9 @@ extern "C" {
 enum { USAC_LINE2D = 1, USAC_HOMOGRAPHY = 2, USAC_FUNDAMENTAL = 3, USAC_ESSENTIAL = 4 };
 /* = enum SAMPLER (usac/model.hpp:11): Uniform, Napsac (grid neighbours), Prosac */
 enum { USAC_SAMPLER_UNIFORM = 1, USAC_SAMPLER_NAPSAC = 3, USAC_SAMPLER_PROSAC = 4 };
-/* = enum LocOpt (usac/model.hpp:13): inner + iterative LO-RANSAC (unlimited / limited) */
-enum { USAC_LO_NONE = 0, USAC_LO_INITLORSC = 1, USAC_LO_INITFLORSC = 2 };
+/* = enum LocOpt (usac/model.hpp:13): inner + iterative LO-RANSAC (unlimited / limited), graph-cut
+ * LO (graphcut.hpp) */
+enum { USAC_LO_NONE = 0, USAC_LO_INITLORSC = 1, USAC_LO_INITFLORSC = 2, USAC_LO_GC = 3 };
 /* = enum NeighborsSearch (usac/model.hpp:12): the Ransac ctor (ransac.hpp:60-78) builds Grid
  * neighbours for Grid and nanoflann KNN for any other value (NullN included) */
 enum { USAC_NEIGHBORS_NULL = 0, USAC_NEIGHBORS_NANOFLANN = 1, USAC_NEIGHBORS_GRID = 2 };
@@ -102,7 +103,8 @@ typedef struct usac_params {
     uint32_t lo_threshold_multiplier; /* model.hpp:30 (10) */
     int32_t cell_size;                /* model.hpp:43 (50): NAPSAC grid cell */
     int32_t neighbors;                /* USAC_NEIGHBORS_* (model.hpp:42): NAPSAC Grid or KNN */
-    uint32_t knn;                     /* model.hpp:23 k_nearest_neighbors (NAPSAC KNN, 1..32) */
+    uint32_t knn;                     /* model.hpp:23 k_nearest_neighbors (NAPSAC KNN / GC, 1..32) */
+    float spatial_coherence_gc;       /* model.hpp:33 (0.1): GC pairwise weight; <= 0 selects 0.1 */
 } usac_params;
 
 /* RansacOutput getters (ransac_output.hpp:57-97) */
@@ -120,8 +122,8 @@ typedef struct usac_run_output {
     int32_t sprt_histories;     /* SPRT tests designed (sprt_histories.size()) */
     uint32_t prosac_term_len;   /* final PROSAC termination_length (n without PROSAC) */
     uint32_t rollbacks;         /* PROSAC speculative batches cut short by a termination_length change */
-    uint32_t lo_inner_iters;    /* getLOIters (ransac_output.hpp): inner LO iterations */
-    uint32_t lo_iterative_iters;
+    uint32_t lo_inner_iters;    /* getLOIters (ransac_output.hpp): inner LO iterations (GC: gc_iterations) */
+    uint32_t lo_iterative_iters; /* iterative LO iterations (GC: labellings) */
     uint32_t lo_rounds;         /* LO speculation rounds (batches of inner iterations run at once) */
     uint32_t lo_stages;         /* LO device stages (one batched fit or one batched scoring each) */
     uint32_t sum_models;        /* models whose exact sequential Σerr the replay needed */
@@ -150,6 +152,12 @@ int usac_score_models(usac_ctx *ctx, const float *models, uint32_t n_models, flo
                       float *sums);
 /* One model: ascending inlier indices (idx capacity >= n points), count and sum. */
 int usac_get_inliers(usac_ctx *ctx, const float *model, float thr, int32_t *idx, uint32_t *n, float *sum);
+/* The graph-cut LO's min cut, host side (usac_maxflow.hpp; gco-v3.0 energy.h + maxflow.inl
+ * semantics): n nodes with add_term1(i, unary[i], 0), add_term2(ei[k], ej[k], e00[k], e01[k],
+ * e10[k], e11[k]) in order, BK max-flow; sink_out[i] = 1 iff what_segment(i) == SINK.
+ * Returns the flow.  No device work (exposed for parity tests against the gco sources). */
+float usac_bk_label(int n, const float *unary, int m, const int32_t *ei, const int32_t *ej, const float *e00,
+                    const float *e01, const float *e10, const float *e11, int32_t *sink_out);
 /* NearestNeighbors::getNearestNeighbors_nanoflann (nearest_neighbors.cpp:69-128) on the
  * device: the k nearest neighbours of every point (1 <= k <= 32; idx n x k, d2 n x k
  * squared distances, nullable) by nanoflann's float L2 distance, the point itself excluded,
@@ -208,7 +216,8 @@ int usac_draw_samples(usac_ctx *ctx, uint32_t B, uint64_t seed, uint64_t first_h
 uint32_t usac_std_termination(uint32_t inliers, uint32_t points_size, uint32_t sample_size, float desired_prob,
                               uint32_t max_iterations);
 /* Ransac::run (ransac.cpp:14-238) with the Uniform (glibc random() stream), NAPSAC (grid or
- * KNN neighbours, napsac_sampler.hpp) or PROSAC (prosac_sampler.hpp + prosac_termination_criteria.hpp)
+ * KNN neighbours, napsac_sampler.hpp), graph-cut LO (graphcut.hpp; KNN or grid neighbours;
+ * not with NAPSAC, whose combination the reference leaves undefined) or PROSAC (prosac_sampler.hpp + prosac_termination_criteria.hpp)
  * sampler, optional SPRT (sprt.hpp; pool shuffle from the same glibc stream), optional
  * inner + iterative LO-RANSAC (inner_local_optimization.hpp, iterative_local_optimization.hpp;
  * its mt19937 seeded with seed + 1).  inliers_out (capacity n,

@@ -41,7 +41,7 @@ class OrcResult(ctypes.Structure):
 SAMPLER_UNIFORM, SAMPLER_NAPSAC, SAMPLER_PROSAC = 1, 3, 4  # usac/model.hpp:11
 
 
-LO_NONE, LO_INITLORSC, LO_INITFLORSC = 0, 1, 2  # usac/model.hpp:13
+LO_NONE, LO_INITLORSC, LO_INITFLORSC, LO_GC = 0, 1, 2, 3  # usac/model.hpp:13
 NEIGHBORS_NULL, NEIGHBORS_NANOFLANN, NEIGHBORS_GRID = 0, 1, 2  # usac/model.hpp:12 (NeighborsSearch)
 
 
@@ -50,7 +50,8 @@ class OrcConfig(ctypes.Structure):
                 ("seed", ctypes.c_uint), ("dlt_mode", ctypes.c_int), ("sampler", ctypes.c_int), ("sprt", ctypes.c_int),
                 ("lo", ctypes.c_int), ("lo_sample_size", ctypes.c_uint), ("lo_iterative_iterations", ctypes.c_uint),
                 ("lo_inner_iterations", ctypes.c_uint), ("lo_threshold_multiplier", ctypes.c_uint),
-                ("cell_size", ctypes.c_int), ("neighbors", ctypes.c_int), ("knn", ctypes.c_uint)]
+                ("cell_size", ctypes.c_int), ("neighbors", ctypes.c_int), ("knn", ctypes.c_uint),
+                ("spatial_coherence_gc", ctypes.c_float)]
 
 
 class OrcMT(ctypes.Structure):
@@ -273,7 +274,7 @@ def std_termination(inliers, n, m, p, max_iters=10000):
 
 def ransac_run(kind, points, thr, p, seed, max_iters=10000, dlt_mode=DLT_THIN, rec_cap=4096,
                sampler=SAMPLER_UNIFORM, sprt=False, lo=LO_NONE, lo_params=(14, 4, 20, 10), cell_size=50,
-               neighbors=NEIGHBORS_GRID, knn=7):
+               neighbors=NEIGHBORS_GRID, knn=7, spatial_coherence_gc=0.1):
     points = np.ascontiguousarray(points, dtype=np.float32)
     n = points.shape[0]
     res = OrcResult()
@@ -282,7 +283,7 @@ def ransac_run(kind, points, thr, p, seed, max_iters=10000, dlt_mode=DLT_THIN, r
     rc = np.zeros(rec_cap, dtype=np.int32)
     rs = np.zeros(rec_cap, dtype=np.float32)
     cfg = OrcConfig(thr, p, max_iters, seed, dlt_mode, sampler, 1 if sprt else 0, lo, *lo_params, cell_size,
-                    neighbors, knn)
+                    neighbors, knn, spatial_coherence_gc)
     ret = lib().orc_ransac_run_cfg(kind, _p(points, _f32p), n, ctypes.byref(cfg), ctypes.byref(res), _p(inl, _i32p),
                                    _p(ri, _u32p), _p(rc, _i32p), _p(rs, _f32p), rec_cap)
     k = min(res.n_records, rec_cap)
@@ -316,6 +317,45 @@ def knn(points, k):
     L.orc_knn.restype = None
     L.orc_knn(_p(pts, _f32p), n, cols, k, _p(idx, _i32p), _p(d2, _f32p))
     return idx, d2
+
+
+def _bk_args(unary, ei, ej, e00, e01, e10, e11):
+    a = [np.ascontiguousarray(unary, np.float32), np.ascontiguousarray(ei, np.int32), np.ascontiguousarray(ej, np.int32)]
+    a += [np.ascontiguousarray(x, np.float32) for x in (e00, e01, e10, e11)]
+    return a
+
+
+def _bk_call(fn, unary, ei, ej, e00, e01, e10, e11):
+    a = _bk_args(unary, ei, ej, e00, e01, e10, e11)
+    n, m = len(a[0]), len(a[1])
+    out = np.zeros(n, np.int32)
+    fn.restype = ctypes.c_float
+    fn.argtypes = [ctypes.c_int, _f32p, ctypes.c_int, _i32p, _i32p, _f32p, _f32p, _f32p, _f32p, _i32p]
+    f = fn(n, _p(a[0], _f32p), m, _p(a[1], _i32p), _p(a[2], _i32p), _p(a[3], _f32p), _p(a[4], _f32p),
+           _p(a[5], _f32p), _p(a[6], _f32p), _p(out, _i32p))
+    return out.astype(bool), f
+
+
+def bk_label(unary, ei, ej, e00, e01, e10, e11):
+    """The oracle's BK restatement: add_term1(i, unary[i], 0), add_term2 per pair, maxflow ->
+    (sink mask, flow)."""
+    return _bk_call(lib().orc_bk_label, unary, ei, ej, e00, e01, e10, e11)
+
+
+GCO_REF_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_ref", "libgco_ref.so")
+_gco = None
+
+
+def gco_ref_available():
+    return os.path.exists(GCO_REF_PATH)
+
+
+def gco_ref_label(unary, ei, ej, e00, e01, e10, e11):
+    """The reference's own gco-v3.0 max-flow (oracle/_ref, built from /root/reference)."""
+    global _gco
+    if _gco is None:
+        _gco = ctypes.CDLL(GCO_REF_PATH)
+    return _bk_call(_gco.gco_ref_label, unary, ei, ej, e00, e01, e10, e11)
 
 
 def grid_neighbors(points, cell_size):

@@ -2156,6 +2156,489 @@ static void lo_run(orc_lo *L, orc_est *e, float *model, int *cnt, float *sum) {
     }
 }
 
+/* ------------------------------------------------------------ Graph-cut LO */
+/* Boykov-Kolmogorov max-flow as the reference's vendored gco-v3.0 implements it
+ * (include/gco-v3.0/graph.h, graph.inl, maxflow.inl; energy.h for the term encoding),
+ * restated over index arrays: arcs in pairs (sister = a ^ 1) prepended to their node's arc
+ * list, two-queue FIFO of active nodes, augmentation orphans pushed to the front of the
+ * orphan list and adoption orphans to the rear, TIME/DIST distance heuristic.  Capacities,
+ * flows and every comparison in float, in gco's operation order, so the final search trees
+ * -- and so what_segment -- are the reference's.  Pinned against the gco sources themselves
+ * (oracle/_ref/libgco_ref.so, built from /root/reference by oracle/Makefile). */
+enum { BK_NONE = -1, BK_TERMINAL = -2, BK_ORPHAN = -3 };
+#define BK_INF_D 0x7fffffff
+
+struct orc_bk {
+    int n, n_cap, m, m_cap;
+    int *first, *parent, *next, *ts, *dist;
+    unsigned char *is_sink;
+    float *tr_cap;
+    int *head, *anext;
+    float *r_cap;
+    int *op_node, *op_next, op_cap, op_used, op_free;
+    int orphan_first, orphan_last, q_first[2], q_last[2], time;
+    float flow;
+};
+
+orc_bk *orc_bk_new(int n_nodes, int n_edges) {
+    orc_bk *g = (orc_bk *)calloc(1, sizeof(*g));
+    g->n_cap = n_nodes > 16 ? n_nodes : 16;
+    g->m_cap = 2 * (n_edges > 16 ? n_edges : 16);
+    g->first = (int *)malloc(sizeof(int) * g->n_cap);
+    g->parent = (int *)malloc(sizeof(int) * g->n_cap);
+    g->next = (int *)malloc(sizeof(int) * g->n_cap);
+    g->ts = (int *)malloc(sizeof(int) * g->n_cap);
+    g->dist = (int *)malloc(sizeof(int) * g->n_cap);
+    g->is_sink = (unsigned char *)malloc(g->n_cap);
+    g->tr_cap = (float *)malloc(sizeof(float) * g->n_cap);
+    g->head = (int *)malloc(sizeof(int) * g->m_cap);
+    g->anext = (int *)malloc(sizeof(int) * g->m_cap);
+    g->r_cap = (float *)malloc(sizeof(float) * g->m_cap);
+    g->op_free = -1;
+    return g;
+}
+
+void orc_bk_free(orc_bk *g) {
+    if (!g) return;
+    free(g->first); free(g->parent); free(g->next); free(g->ts); free(g->dist); free(g->is_sink);
+    free(g->tr_cap); free(g->head); free(g->anext); free(g->r_cap); free(g->op_node); free(g->op_next);
+    free(g);
+}
+
+int orc_bk_add_node(orc_bk *g) {
+    if (g->n == g->n_cap) {
+        g->n_cap += g->n_cap / 2;
+        g->first = (int *)realloc(g->first, sizeof(int) * g->n_cap);
+        g->parent = (int *)realloc(g->parent, sizeof(int) * g->n_cap);
+        g->next = (int *)realloc(g->next, sizeof(int) * g->n_cap);
+        g->ts = (int *)realloc(g->ts, sizeof(int) * g->n_cap);
+        g->dist = (int *)realloc(g->dist, sizeof(int) * g->n_cap);
+        g->is_sink = (unsigned char *)realloc(g->is_sink, g->n_cap);
+        g->tr_cap = (float *)realloc(g->tr_cap, sizeof(float) * g->n_cap);
+    }
+    g->first[g->n] = -1;
+    g->tr_cap[g->n] = 0.f;
+    return g->n++;
+}
+
+/* graph.h add_tweights */
+void orc_bk_add_tweights(orc_bk *g, int i, float cap_source, float cap_sink) {
+    const float delta = g->tr_cap[i];
+    if (delta > 0) cap_source += delta;
+    else cap_sink -= delta;
+    g->flow += (cap_source < cap_sink) ? cap_source : cap_sink;
+    g->tr_cap[i] = cap_source - cap_sink;
+}
+
+/* graph.h add_edge: arc pair (i -> j, j -> i), each prepended to its tail's list */
+void orc_bk_add_edge(orc_bk *g, int i, int j, float cap, float rev_cap) {
+    if (g->m + 2 > g->m_cap) {
+        g->m_cap += g->m_cap / 2;
+        if (g->m_cap & 1) g->m_cap++;
+        g->head = (int *)realloc(g->head, sizeof(int) * g->m_cap);
+        g->anext = (int *)realloc(g->anext, sizeof(int) * g->m_cap);
+        g->r_cap = (float *)realloc(g->r_cap, sizeof(float) * g->m_cap);
+    }
+    const int a = g->m, ar = g->m + 1;
+    g->m += 2;
+    g->anext[a] = g->first[i];
+    g->first[i] = a;
+    g->anext[ar] = g->first[j];
+    g->first[j] = ar;
+    g->head[a] = j;
+    g->head[ar] = i;
+    g->r_cap[a] = cap;
+    g->r_cap[ar] = rev_cap;
+}
+
+/* energy.h add_term1 / add_term2 */
+void orc_bk_add_term1(orc_bk *g, int x, float e0, float e1) { orc_bk_add_tweights(g, x, e1, e0); }
+void orc_bk_add_term2(orc_bk *g, int x, int y, float A, float B, float C, float D) {
+    orc_bk_add_tweights(g, x, D, A);
+    B -= A;
+    C -= D;
+    if (B < 0) {
+        orc_bk_add_tweights(g, x, 0, B);
+        orc_bk_add_tweights(g, y, 0, -B);
+        orc_bk_add_edge(g, x, y, 0, B + C);
+    } else if (C < 0) {
+        orc_bk_add_tweights(g, x, 0, -C);
+        orc_bk_add_tweights(g, y, 0, C);
+        orc_bk_add_edge(g, x, y, B + C, 0);
+    } else {
+        orc_bk_add_edge(g, x, y, B, C);
+    }
+}
+
+static void bk_set_active(orc_bk *g, int i) {
+    if (g->next[i] != -1) return;
+    if (g->q_last[1] >= 0) g->next[g->q_last[1]] = i;
+    else g->q_first[1] = i;
+    g->q_last[1] = i;
+    g->next[i] = i;
+}
+
+static int bk_next_active(orc_bk *g) {
+    for (;;) {
+        int i = g->q_first[0];
+        if (i < 0) {
+            g->q_first[0] = i = g->q_first[1];
+            g->q_last[0] = g->q_last[1];
+            g->q_first[1] = g->q_last[1] = -1;
+            if (i < 0) return -1;
+        }
+        if (g->next[i] == i) g->q_first[0] = g->q_last[0] = -1;
+        else g->q_first[0] = g->next[i];
+        g->next[i] = -1;
+        if (g->parent[i] != BK_NONE) return i;
+    }
+}
+
+static int bk_np_new(orc_bk *g, int node) {
+    int np;
+    if (g->op_free >= 0) {
+        np = g->op_free;
+        g->op_free = g->op_next[np];
+    } else {
+        if (g->op_used == g->op_cap) {
+            g->op_cap = g->op_cap ? 2 * g->op_cap : 128;
+            g->op_node = (int *)realloc(g->op_node, sizeof(int) * g->op_cap);
+            g->op_next = (int *)realloc(g->op_next, sizeof(int) * g->op_cap);
+        }
+        np = g->op_used++;
+    }
+    g->op_node[np] = node;
+    return np;
+}
+static void bk_np_delete(orc_bk *g, int np) {
+    g->op_next[np] = g->op_free;
+    g->op_free = np;
+}
+static void bk_orphan_front(orc_bk *g, int i) {
+    g->parent[i] = BK_ORPHAN;
+    const int np = bk_np_new(g, i);
+    g->op_next[np] = g->orphan_first;
+    g->orphan_first = np;
+}
+static void bk_orphan_rear(orc_bk *g, int i) {
+    g->parent[i] = BK_ORPHAN;
+    const int np = bk_np_new(g, i);
+    if (g->orphan_last >= 0) g->op_next[g->orphan_last] = np;
+    else g->orphan_first = np;
+    g->orphan_last = np;
+    g->op_next[np] = -1;
+}
+
+static void bk_augment(orc_bk *g, int mid) {
+    int i, a;
+    float b = g->r_cap[mid];
+    for (i = g->head[mid ^ 1];; i = g->head[a]) { /* source tree */
+        a = g->parent[i];
+        if (a == BK_TERMINAL) break;
+        if (b > g->r_cap[a ^ 1]) b = g->r_cap[a ^ 1];
+    }
+    if (b > g->tr_cap[i]) b = g->tr_cap[i];
+    for (i = g->head[mid];; i = g->head[a]) { /* sink tree */
+        a = g->parent[i];
+        if (a == BK_TERMINAL) break;
+        if (b > g->r_cap[a]) b = g->r_cap[a];
+    }
+    if (b > -g->tr_cap[i]) b = -g->tr_cap[i];
+    g->r_cap[mid ^ 1] += b;
+    g->r_cap[mid] -= b;
+    for (i = g->head[mid ^ 1];; i = g->head[a]) {
+        a = g->parent[i];
+        if (a == BK_TERMINAL) break;
+        g->r_cap[a] += b;
+        g->r_cap[a ^ 1] -= b;
+        if (!g->r_cap[a ^ 1]) bk_orphan_front(g, i);
+    }
+    g->tr_cap[i] -= b;
+    if (!g->tr_cap[i]) bk_orphan_front(g, i);
+    for (i = g->head[mid];; i = g->head[a]) {
+        a = g->parent[i];
+        if (a == BK_TERMINAL) break;
+        g->r_cap[a ^ 1] += b;
+        g->r_cap[a] -= b;
+        if (!g->r_cap[a]) bk_orphan_front(g, i);
+    }
+    g->tr_cap[i] += b;
+    if (!g->tr_cap[i]) bk_orphan_front(g, i);
+    g->flow += b;
+}
+
+/* process_source_orphan (sink = 0) / process_sink_orphan (sink = 1) */
+static void bk_process_orphan(orc_bk *g, int i, int sink) {
+    int a0, a0_min = BK_NONE, a, j, d, d_min = BK_INF_D;
+    for (a0 = g->first[i]; a0 >= 0; a0 = g->anext[a0]) {
+        if (!(sink ? g->r_cap[a0] : g->r_cap[a0 ^ 1])) continue;
+        j = g->head[a0];
+        if ((int)g->is_sink[j] != sink || (a = g->parent[j]) == BK_NONE) continue;
+        d = 0; /* the origin of j */
+        for (;;) {
+            if (g->ts[j] == g->time) {
+                d += g->dist[j];
+                break;
+            }
+            a = g->parent[j];
+            d++;
+            if (a == BK_TERMINAL) {
+                g->ts[j] = g->time;
+                g->dist[j] = 1;
+                break;
+            }
+            if (a == BK_ORPHAN) {
+                d = BK_INF_D;
+                break;
+            }
+            j = g->head[a];
+        }
+        if (d < BK_INF_D) {
+            if (d < d_min) {
+                a0_min = a0;
+                d_min = d;
+            }
+            for (j = g->head[a0]; g->ts[j] != g->time; j = g->head[g->parent[j]]) {
+                g->ts[j] = g->time;
+                g->dist[j] = d--;
+            }
+        }
+    }
+    if ((g->parent[i] = a0_min) != BK_NONE) {
+        g->ts[i] = g->time;
+        g->dist[i] = d_min + 1;
+        return;
+    }
+    for (a0 = g->first[i]; a0 >= 0; a0 = g->anext[a0]) {
+        j = g->head[a0];
+        if ((int)g->is_sink[j] != sink || (a = g->parent[j]) == BK_NONE) continue;
+        if (sink ? g->r_cap[a0] : g->r_cap[a0 ^ 1]) bk_set_active(g, j);
+        if (a != BK_TERMINAL && a != BK_ORPHAN && g->head[a] == i) bk_orphan_rear(g, j);
+    }
+}
+
+/* Graph::maxflow() (reuse_trees = false) */
+float orc_bk_maxflow(orc_bk *g) {
+    int i, j, a, np, np_next, current = -1;
+    g->q_first[0] = g->q_last[0] = g->q_first[1] = g->q_last[1] = -1;
+    g->orphan_first = g->orphan_last = -1;
+    g->time = 0;
+    for (i = 0; i < g->n; i++) { /* maxflow_init */
+        g->next[i] = -1;
+        g->ts[i] = g->time;
+        if (g->tr_cap[i] > 0) {
+            g->is_sink[i] = 0;
+            g->parent[i] = BK_TERMINAL;
+            bk_set_active(g, i);
+            g->dist[i] = 1;
+        } else if (g->tr_cap[i] < 0) {
+            g->is_sink[i] = 1;
+            g->parent[i] = BK_TERMINAL;
+            bk_set_active(g, i);
+            g->dist[i] = 1;
+        } else {
+            g->parent[i] = BK_NONE;
+        }
+    }
+    for (;;) {
+        i = current;
+        if (i >= 0) {
+            g->next[i] = -1;
+            if (g->parent[i] == BK_NONE) i = -1;
+        }
+        if (i < 0 && (i = bk_next_active(g)) < 0) break;
+        if (!g->is_sink[i]) { /* grow the source tree */
+            for (a = g->first[i]; a >= 0; a = g->anext[a]) {
+                if (!g->r_cap[a]) continue;
+                j = g->head[a];
+                if (g->parent[j] == BK_NONE) {
+                    g->is_sink[j] = 0;
+                    g->parent[j] = a ^ 1;
+                    g->ts[j] = g->ts[i];
+                    g->dist[j] = g->dist[i] + 1;
+                    bk_set_active(g, j);
+                } else if (g->is_sink[j]) {
+                    break;
+                } else if (g->ts[j] <= g->ts[i] && g->dist[j] > g->dist[i]) {
+                    g->parent[j] = a ^ 1;
+                    g->ts[j] = g->ts[i];
+                    g->dist[j] = g->dist[i] + 1;
+                }
+            }
+        } else { /* grow the sink tree */
+            for (a = g->first[i]; a >= 0; a = g->anext[a]) {
+                if (!g->r_cap[a ^ 1]) continue;
+                j = g->head[a];
+                if (g->parent[j] == BK_NONE) {
+                    g->is_sink[j] = 1;
+                    g->parent[j] = a ^ 1;
+                    g->ts[j] = g->ts[i];
+                    g->dist[j] = g->dist[i] + 1;
+                    bk_set_active(g, j);
+                } else if (!g->is_sink[j]) {
+                    a = a ^ 1;
+                    break;
+                } else if (g->ts[j] <= g->ts[i] && g->dist[j] > g->dist[i]) {
+                    g->parent[j] = a ^ 1;
+                    g->ts[j] = g->ts[i];
+                    g->dist[j] = g->dist[i] + 1;
+                }
+            }
+        }
+        g->time++;
+        if (a >= 0) {
+            g->next[i] = i; /* stays active */
+            current = i;
+            bk_augment(g, a);
+            while ((np = g->orphan_first) >= 0) { /* adoption */
+                np_next = g->op_next[np];
+                g->op_next[np] = -1;
+                while ((np = g->orphan_first) >= 0) {
+                    g->orphan_first = g->op_next[np];
+                    i = g->op_node[np];
+                    bk_np_delete(g, np);
+                    if (g->orphan_first < 0) g->orphan_last = -1;
+                    bk_process_orphan(g, i, g->is_sink[i]);
+                }
+                g->orphan_first = np_next;
+            }
+        } else {
+            current = -1;
+        }
+    }
+    return g->flow;
+}
+
+/* what_segment(i) == SINK (default segment SOURCE for free nodes) */
+int orc_bk_is_sink(const orc_bk *g, int i) { return g->parent[i] != BK_NONE && g->is_sink[i]; }
+
+/* gco_ref-compatible driver: n nodes, add_term1(i, unary[i], 0), then add_term2 for the m
+ * listed pairs in order; sink_out[i] = what_segment(i) == SINK.  Returns the flow. */
+float orc_bk_label(int n, const float *unary, int m, const int *ei, const int *ej, const float *e00,
+                   const float *e01, const float *e10, const float *e11, int *sink_out) {
+    orc_bk *g = orc_bk_new(n, m);
+    for (int i = 0; i < n; i++) orc_bk_add_node(g);
+    for (int i = 0; i < n; i++) orc_bk_add_term1(g, i, unary[i], 0.f);
+    for (int k = 0; k < m; k++) orc_bk_add_term2(g, ei[k], ej[k], e00[k], e01[k], e10[k], e11[k]);
+    const float f = orc_bk_maxflow(g);
+    for (int i = 0; i < n; i++) sink_out[i] = orc_bk_is_sink(g, i);
+    orc_bk_free(g);
+    return f;
+}
+
+/* GraphCut::labeling (graphcut.cpp:7-101): residuals of `model`, unary energies
+ * exp(-(e*e) / (2 thr^2)) (float argument, the C library's double exp -- the reference's
+ * unqualified exp on a float, see DESIGN), pairwise terms over the neighbour lists
+ * (skipping non-submodular / NaN terms), BK min cut; inliers = SINK nodes, ascending. */
+typedef struct {
+    const int *knn_tab; /* n x knn (NULL: grid) */
+    unsigned int knn;
+    const orc_grid *grid;
+    float lambda, sqr_thr;
+} orc_gc_graph;
+
+static int gc_labeling(orc_est *e, const orc_gc_graph *G, const float *model, int *inliers, float *errors) {
+    const unsigned int n = e->n;
+    orc_est_set_model(e, model);
+    orc_bk *g = orc_bk_new((int)n, (int)(G->knn_tab ? G->knn * n : n));
+    for (unsigned int i = 0; i < n; i++) orc_bk_add_node(g);
+    for (unsigned int i = 0; i < n; i++) {
+        const float d = orc_est_error(e, i);
+        errors[i] = d;
+        const float energy = (float)exp(-(d * d) / G->sqr_thr);
+        orc_bk_add_term1(g, (int)i, energy, 0.f);
+    }
+    const float e01 = 1.f, e10 = 1.f, lam = G->lambda;
+    for (unsigned int i = 0; i < n; i++) {
+        const float d1 = errors[i];
+        const float energy1 = (float)exp(-(d1 * d1) / G->sqr_thr);
+        const unsigned int cnt = G->knn_tab ? G->knn : (unsigned int)orc_grid_count(G->grid, i);
+        const int *row = G->knn_tab ? G->knn_tab + (size_t)G->knn * i : orc_grid_list(G->grid, i);
+        for (unsigned int k = 0; k < cnt; k++) {
+            const int j = row[k];
+            if (j == (int)i || j < 0) continue;
+            const float d2 = errors[j];
+            const float energy2 = (float)exp(-(d2 * d2) / G->sqr_thr);
+            const float e00 = (energy1 + energy2) / 2;
+            const float e11 = 1 - e00;
+            if (e00 + e11 > e01 + e10 || isnan(e00)) continue;
+            orc_bk_add_term2(g, (int)i, j, e00 * lam, e01 * lam, e10 * lam, e11 * lam);
+        }
+    }
+    orc_bk_maxflow(g);
+    int cnt = 0;
+    for (unsigned int i = 0; i < n; i++)
+        if (orc_bk_is_sink(g, (int)i)) inliers[cnt++] = (int)i;
+    orc_bk_free(g);
+    return cnt;
+}
+
+/* GraphCut::GetModelScore (graphcut.hpp:99-153): while the best improves: label, then up to
+ * lo_inner_iterations least-squares fits on 7m-point random subsets of the labelling's
+ * inliers (all of them, once, when there are <= 7m), each scored at the model threshold and
+ * kept when Score::bigger.  Its mt19937 is seeded with seed + 1 (reference: random_device). */
+typedef struct {
+    orc_mt g;
+    orc_gc_graph G;
+    unsigned int inner, m, n, limit;
+    float thr;
+    int *inl, *sample;
+    float *errors;
+    unsigned int gc_iters, labelings;
+} orc_gc;
+
+static void gc_init(orc_gc *C, const orc_config *cfg, unsigned int n, unsigned int m) {
+    memset(C, 0, sizeof(*C));
+    orc_mt_seed(&C->g, cfg->seed + 1u);
+    C->inner = cfg->lo_inner_iterations;
+    C->m = m;
+    C->n = n;
+    C->limit = 7 * m;
+    C->thr = cfg->threshold;
+    C->G.lambda = cfg->spatial_coherence_gc > 0.f ? cfg->spatial_coherence_gc : 0.1f; /* model.hpp:33 */
+    C->G.sqr_thr = 2 * cfg->threshold * cfg->threshold;
+    C->inl = (int *)malloc(sizeof(int) * (n ? n : 1));
+    C->errors = (float *)malloc(sizeof(float) * (n ? n : 1));
+    C->sample = (int *)malloc(sizeof(int) * C->limit);
+}
+
+static void gc_free(orc_gc *C) {
+    free(C->inl);
+    free(C->errors);
+    free(C->sample);
+}
+
+static void gc_run(orc_gc *C, orc_est *e, float *model, int *cnt, float *sum) {
+    int updated = 1;
+    float gc_model[9];
+    while (updated) {
+        updated = 0;
+        const int L = gc_labeling(e, &C->G, model, C->inl, C->errors);
+        C->labelings++;
+        if (L <= (int)C->m) break;
+        for (unsigned int it = 0; it < C->inner; it++) {
+            if ((unsigned int)L > C->limit) {
+                mt_unique_set(&C->g, C->sample, C->limit, (unsigned int)(L - 1));
+                for (unsigned int k = 0; k < C->limit; k++) C->sample[k] = C->inl[C->sample[k]];
+                if (!orc_est_nonminimal(e, C->sample, C->limit, gc_model)) break;
+            } else {
+                if (it > 0) break;
+                if (!orc_est_nonminimal(e, C->inl, (unsigned int)L, gc_model)) break;
+            }
+            int c;
+            float s;
+            orc_quality(e, gc_model, C->thr, &c, &s, NULL);
+            if (score_bigger(c, s, *cnt, *sum)) {
+                updated = 1;
+                *cnt = c;
+                *sum = s;
+                memcpy(model, gc_model, sizeof(gc_model));
+            }
+            C->gc_iters++;
+        }
+    }
+}
+
 /* ------------------------------------------------------------ Ransac::run */
 
 int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_config *cfg, orc_result *out,
@@ -2174,19 +2657,36 @@ int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_
     orc_lo lo;
     const int use_lo = cfg->lo == ORC_LO_INITLORSC || cfg->lo == ORC_LO_INITFLORSC;
     if (use_lo) lo_init(&lo, cfg, n, (unsigned int)m);
+    const int use_gc = cfg->lo == ORC_LO_GC;
+    /* NAPSAC + GC: the reference hands the neighbours to the sampler only and leaves the
+     * graph cut's neighbour type uninitialised (ransac.hpp:62-78) -- not reproducible */
+    if (use_gc && napsac) {
+        orc_est_free(e);
+        if (smp) orc_uniform_free(smp);
+        return -2;
+    }
+    orc_gc gc;
+    if (use_gc) gc_init(&gc, cfg, n, (unsigned int)m);
     /* Ransac ctor (ransac.hpp:60-78): Grid neighbours, or nanoflann KNN for any other type */
     const int knn_mode = napsac && cfg->neighbors != ORC_NEIGHBORS_GRID;
     orc_grid *grid = napsac && !knn_mode ? orc_grid_new(points, n, cfg->cell_size) : NULL;
     orc_napsac *ns = grid ? orc_napsac_new(grid, n, (unsigned int)m) : NULL;
     int *knn_tab = NULL;
     orc_napsac_knn *nk = NULL;
-    if (knn_mode) {
+    const int gc_knn = use_gc && cfg->neighbors != ORC_NEIGHBORS_GRID;
+    orc_grid *gc_grid = use_gc && !gc_knn ? orc_grid_new(points, n, cfg->cell_size) : NULL;
+    if (knn_mode || gc_knn) {
         const unsigned int k = cfg->knn;
         knn_tab = (int *)malloc(sizeof(int) * (size_t)n * (k ? k : 1));
         float *kd = (float *)malloc(sizeof(float) * (size_t)n * (k ? k : 1));
         orc_knn(points, n, (unsigned int)orc_est_cols(e), k, knn_tab, kd);
         free(kd);
-        nk = orc_napsac_knn_new(knn_tab, n, (unsigned int)m, k);
+        if (knn_mode) nk = orc_napsac_knn_new(knn_tab, n, (unsigned int)m, k);
+    }
+    if (use_gc) {
+        gc.G.knn_tab = gc_knn ? knn_tab : NULL;
+        gc.G.knn = cfg->knn;
+        gc.G.grid = gc_grid;
     }
     orc_prosac_term *pt = prosac ? orc_prosac_term_new(orc_prosac_growth(ps), n, (unsigned int)m, cfg->desired_prob,
                                                        cfg->max_iterations)
@@ -2234,6 +2734,7 @@ int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_
             }
             if (score_bigger(cnt, sum, best_cnt, best_sum)) {
                 if (use_lo) lo_run(&lo, e, models + 9 * i, &cnt, &sum); /* ransac.cpp:110-112 */
+                if (use_gc) gc_run(&gc, e, models + 9 * i, &cnt, &sum);
                 best_cnt = cnt;
                 best_sum = sum;
                 memcpy(best_model, models + 9 * i, sizeof(best_model));
@@ -2265,8 +2766,8 @@ int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_
     out->polish_passes = 0;
     out->sprt_histories = sp ? (int)orc_sprt_histories(sp) : 0;
     out->prosac_term_len = pt ? orc_prosac_term_length(pt) : n;
-    out->lo_inner_iters = use_lo ? lo.inner_count : 0;
-    out->lo_iterative_iters = use_lo ? lo.iterative_count : 0;
+    out->lo_inner_iters = use_lo ? lo.inner_count : use_gc ? gc.gc_iters : 0;
+    out->lo_iterative_iters = use_lo ? lo.iterative_count : use_gc ? gc.labelings : 0;
     memcpy(out->minimal_model, best_model, sizeof(best_model));
     out->minimal_inliers = best_cnt;
     if (best_cnt == 0) {
@@ -2304,6 +2805,8 @@ int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_
     free(knn_tab);
     orc_grid_free(grid);
     if (use_lo) lo_free(&lo);
+    if (use_gc) gc_free(&gc);
+    orc_grid_free(gc_grid);
     orc_est_free(e);
     return rc;
 }

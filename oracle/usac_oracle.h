@@ -97,7 +97,7 @@ typedef struct {
 } orc_result;
 
 enum { ORC_SAMPLER_UNIFORM = 1, ORC_SAMPLER_NAPSAC = 3, ORC_SAMPLER_PROSAC = 4 }; /* = SAMPLER, usac/model.hpp:11 */
-enum { ORC_LO_NONE = 0, ORC_LO_INITLORSC = 1, ORC_LO_INITFLORSC = 2 };              /* = LocOpt, usac/model.hpp:13 */
+enum { ORC_LO_NONE = 0, ORC_LO_INITLORSC = 1, ORC_LO_INITFLORSC = 2, ORC_LO_GC = 3 }; /* = LocOpt, usac/model.hpp:13 */
 typedef struct {
     float threshold, desired_prob;
     unsigned int max_iterations, seed;
@@ -108,7 +108,8 @@ typedef struct {
     unsigned int lo_sample_size, lo_iterative_iterations, lo_inner_iterations, lo_threshold_multiplier; /* model.hpp:27-30 */
     int cell_size; /* model.hpp:43 */
     int neighbors;        /* ORC_NEIGHBORS_* (model.hpp:12,42): Grid, else nanoflann KNN */
-    unsigned int knn;     /* model.hpp:23 k_nearest_neighbors (NAPSAC KNN) */
+    unsigned int knn;     /* model.hpp:23 k_nearest_neighbors (NAPSAC KNN, GC) */
+    float spatial_coherence_gc; /* model.hpp:33 (0.1); <= 0 selects 0.1 */
 } orc_config;
 enum { ORC_NEIGHBORS_NULL = 0, ORC_NEIGHBORS_NANOFLANN = 1, ORC_NEIGHBORS_GRID = 2 }; /* = NeighborsSearch */
 
@@ -119,6 +120,20 @@ typedef struct orc_napsac_knn orc_napsac_knn;
 orc_napsac_knn *orc_napsac_knn_new(const int *nb, unsigned int n, unsigned int m, unsigned int knn);
 void orc_napsac_knn_free(orc_napsac_knn *s);
 void orc_napsac_knn_sample(orc_napsac_knn *s, int *sample);
+
+/* Boykov-Kolmogorov max-flow (gco-v3.0 graph.h / maxflow.inl) and its energy.h terms */
+typedef struct orc_bk orc_bk;
+orc_bk *orc_bk_new(int n_nodes, int n_edges);
+void orc_bk_free(orc_bk *g);
+int orc_bk_add_node(orc_bk *g);
+void orc_bk_add_tweights(orc_bk *g, int i, float cap_source, float cap_sink);
+void orc_bk_add_edge(orc_bk *g, int i, int j, float cap, float rev_cap);
+void orc_bk_add_term1(orc_bk *g, int x, float e0, float e1);
+void orc_bk_add_term2(orc_bk *g, int x, int y, float A, float B, float C, float D);
+float orc_bk_maxflow(orc_bk *g);
+int orc_bk_is_sink(const orc_bk *g, int i);
+float orc_bk_label(int n, const float *unary, int m, const int *ei, const int *ej, const float *e00,
+                   const float *e01, const float *e10, const float *e11, int *sink_out);
 
 /* grid neighbours (nearest_neighbors.cpp:160-202) and the NAPSAC grid sampler (napsac_sampler.hpp) */
 typedef struct orc_grid orc_grid;

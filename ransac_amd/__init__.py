@@ -40,10 +40,11 @@ class SAMPLER(enum.IntEnum):  # usac/model.hpp:11
     ProsacNapsac = 6
 
 
-class LocOpt(enum.IntEnum):  # usac/model.hpp:13 (GC and IRLS are out of scope)
+class LocOpt(enum.IntEnum):  # usac/model.hpp:13 (IRLS is out of scope: debug prints only)
     NullLO = 0
     InItLORsc = 1
     InItFLORsc = 2
+    GC = 3
 
 
 class NeighborsSearch(enum.IntEnum):  # usac/model.hpp:12 (NullN / Nanoflann = KNN on the device)
@@ -78,7 +79,8 @@ class _Params(ctypes.Structure):
                 ("sampler", ctypes.c_int32), ("sprt", ctypes.c_int32), ("lo", ctypes.c_int32),
                 ("lo_sample_size", ctypes.c_uint32), ("lo_iterative_iterations", ctypes.c_uint32),
                 ("lo_inner_iterations", ctypes.c_uint32), ("lo_threshold_multiplier", ctypes.c_uint32),
-                ("cell_size", ctypes.c_int32), ("neighbors", ctypes.c_int32), ("knn", ctypes.c_uint32)]
+                ("cell_size", ctypes.c_int32), ("neighbors", ctypes.c_int32), ("knn", ctypes.c_uint32),
+                ("spatial_coherence_gc", ctypes.c_float)]
 
 
 class _RunOutput(ctypes.Structure):
@@ -94,7 +96,7 @@ class _RunOutput(ctypes.Structure):
 # every symbol include/usac_gpu.h declares (checked by tests/test_abi.py)
 ABI_SYMBOLS = [
     "usac_create", "usac_destroy", "usac_last_error", "usac_abi_version", "usac_set_dlt_mode", "usac_sample_size",
-    "usac_num_points", "usac_estimate_models", "usac_score_models", "usac_get_inliers", "usac_knn",
+    "usac_num_points", "usac_estimate_models", "usac_score_models", "usac_get_inliers", "usac_knn", "usac_bk_label",
     "usac_nonminimal",
     "usac_hypothesize_score", "usac_hypothesize_async", "usac_fetch_best", "usac_sync", "usac_last_timings",
     "usac_set_score_chunks", "usac_set_score_variant", "usac_std_termination", "usac_ransac_run", "usac_uniform_samples",
@@ -137,6 +139,7 @@ def lib():
         "usac_score_models": (ctypes.c_int, [_vp, f32p, ctypes.c_uint32, ctypes.c_float, i32p, f32p]),
         "usac_get_inliers": (ctypes.c_int, [_vp, f32p, ctypes.c_float, i32p, u32p, f32p]),
         "usac_knn": (ctypes.c_int, [_vp, ctypes.c_uint32, i32p, f32p]),
+        "usac_bk_label": (ctypes.c_float, [ctypes.c_int, f32p, ctypes.c_int, i32p, i32p, f32p, f32p, f32p, f32p, i32p]),
         "usac_nonminimal": (ctypes.c_int, [_vp, i32p, ctypes.c_uint32, f32p]),
         "usac_hypothesize_score": (ctypes.c_int, [_vp, i32p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
                                                   ctypes.c_float, i32p, f32p, _P(Record)]),
@@ -173,6 +176,18 @@ def lib():
 
 def _ptr(a, t):
     return a.ctypes.data_as(_P(t)) if a is not None else None
+
+
+def bk_label(unary, ei, ej, e00, e01, e10, e11):
+    """The graph-cut LO's host min cut (usac_bk_label): add_term1(i, unary[i], 0), add_term2 per
+    pair, BK max-flow -> (sink mask, flow).  No device work."""
+    a = [np.ascontiguousarray(unary, np.float32), np.ascontiguousarray(ei, np.int32), np.ascontiguousarray(ej, np.int32)]
+    a += [np.ascontiguousarray(x, np.float32) for x in (e00, e01, e10, e11)]
+    out = np.zeros(len(a[0]), np.int32)
+    f = lib().usac_bk_label(len(a[0]), _ptr(a[0], ctypes.c_float), len(a[1]), _ptr(a[1], ctypes.c_int32),
+                            _ptr(a[2], ctypes.c_int32), _ptr(a[3], ctypes.c_float), _ptr(a[4], ctypes.c_float),
+                            _ptr(a[5], ctypes.c_float), _ptr(a[6], ctypes.c_float), _ptr(out, ctypes.c_int32))
+    return out.astype(bool), f
 
 
 def std_termination(inliers, points_size, sample_size, desired_prob, max_iterations=10000):
@@ -448,6 +463,7 @@ class Model:
         self.lo_threshold_multiplier = 10
         self.cell_size = 50
         self.neighborsType = NeighborsSearch.NullN
+        self.spatial_coherence_gc = 0.1
 
     def ResetRandomGenerator(self, reset):
         self.reset_random_generator = bool(reset)
@@ -517,8 +533,8 @@ class Ransac:
     def __init__(self, model, points):
         if model.sampler not in (SAMPLER.Uniform, SAMPLER.Prosac, SAMPLER.Napsac):
             raise NotImplementedError("sampler %s is not supported (Uniform, Napsac, Prosac)" % model.sampler.name)
-        if int(model.lo) not in (0, 1, 2):
-            raise NotImplementedError("LO %r is not supported (InItLORsc, InItFLORsc)" % model.lo)
+        if int(model.lo) not in (0, 1, 2, 3):
+            raise NotImplementedError("LO %r is not supported (InItLORsc, InItFLORsc, GC)" % model.lo)
         self.model = model
         self.ctx = Context(model.estimator, points, device=model.device)
         self._out = None
@@ -533,7 +549,7 @@ class Ransac:
         p = _Params(m.threshold, m.desired_prob, m.max_iterations, seed, int(m.dlt_mode), m.batch, int(m.sampler),
                     1 if m.sprt else 0, int(m.lo), m.lo_sample_size, m.lo_iterative_iterations,
                     m.lo_inner_iterations, m.lo_threshold_multiplier, m.cell_size, int(m.neighborsType),
-                    m.k_nearest_neighbors)
+                    m.k_nearest_neighbors, m.spatial_coherence_gc)
         out = _RunOutput()
         inl = np.zeros(self.ctx.n, dtype=np.int32)
         recs = (Record * rec_cap)()

@@ -220,6 +220,34 @@ hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, 
     return hipGetLastError();
 }
 
+// every point's exact residual under one model (Estimator::GetError, e.g. for the graph-cut
+// LO's energies, graphcut.cpp:17-28)
+template <int EST>
+__global__ __launch_bounds__(kInlBlock) void k_point_errors(const void *__restrict__ pts, uint32_t n,
+                                                            const float *__restrict__ model,
+                                                            float *__restrict__ errors) {
+    __shared__ float sm[18];
+    inl_model<EST>(model, sm);
+    float m[18];
+#pragma unroll
+    for (int k = 0; k < 18; k++) m[k] = sm[k];
+    const uint32_t i = blockIdx.x * kInlBlock + threadIdx.x;
+    if (i < n) errors[i] = inl_error<EST>(m, pts, i);
+}
+
+hipError_t launch_point_errors(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *model,
+                               float *errors) {
+    const dim3 grid((n + kInlBlock - 1) / kInlBlock);
+    switch (estimator) {
+        case USAC_LINE2D: hipLaunchKernelGGL(k_point_errors<USAC_LINE2D>, grid, dim3(kInlBlock), 0, st, pts, n, model, errors); break;
+        case USAC_HOMOGRAPHY: hipLaunchKernelGGL(k_point_errors<USAC_HOMOGRAPHY>, grid, dim3(kInlBlock), 0, st, pts, n, model, errors); break;
+        case USAC_FUNDAMENTAL: hipLaunchKernelGGL(k_point_errors<USAC_FUNDAMENTAL>, grid, dim3(kInlBlock), 0, st, pts, n, model, errors); break;
+        case USAC_ESSENTIAL: hipLaunchKernelGGL(k_point_errors<USAC_ESSENTIAL>, grid, dim3(kInlBlock), 0, st, pts, n, model, errors); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_inliers(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *model, float thr,
                           int32_t *idx, int32_t *count, float *sum, void *scratch) {
     return launch_inliers_batch(st, estimator, pts, n, model, 1, thr, nullptr, nullptr, idx, 0, count, sum, scratch);

@@ -16,6 +16,7 @@
 
 #include "../../include/usac_gpu.h"
 #include "usac_host.hpp"
+#include "usac_maxflow.hpp"
 #include "usac_kernels.h"
 
 namespace {
@@ -73,6 +74,7 @@ struct usac_ctx {
     DevBuf lo_max, lo_lists, lo_pos, lo_ns, lo_thrs, lo_slots, lo_models, lo_ok, lo_cnts, lo_sums, lo_q, lo_part,
         lo_ws, lo_scr;
     DevBuf knn_idx, knn_d2;  // KNN neighbour table (usac_knn, NAPSAC KNN)
+    DevBuf gc_err;           // graph-cut LO: residuals of the model being labelled
     DevBuf e5_ws;                      // staged 5-point solver workspace
     // throughput SPRT (usac_set_sprt): batch-fixed test on the pool-ordered points
     bool sprt_on = false;
@@ -356,7 +358,7 @@ struct LoRansac {
     float predict(float t) const {
         t = (float)mult * t;
         for (uint32_t k = 0; k < iters; k++) t -= step;
-        return fabsf(t - theta) > 0.00001f ? theta : t;
+        return fabsf(t - theta) > 0.00001 ? theta : t;
     }
 
     // IterativeLocalOptimization loop head: decrement, the break tests, then the next fit
@@ -375,7 +377,7 @@ struct LoRansac {
         }
     }
     void finish(Chain &h) {
-        h.failed = fabsf(h.thr - theta) > 0.00001f;
+        h.failed = fabsf(h.thr - theta) > 0.00001;  // double literal, as the reference
         if (h.failed) h.thr = theta;
         h.outcome = ITERATED;
         h.phase = DONE;
@@ -633,6 +635,180 @@ int exact_sums(usac_ctx *c, float thr, int best_count, const int32_t *hc, const 
     return USAC_OK;
 }
 
+// Graph-cut LO: GraphCut::GetModelScore (graphcut.hpp:99-153) with GraphCut::labeling
+// (graphcut.cpp:7-101).  Per labelling: the device computes every point's exact residual
+// under the best model; the host turns them into the reference's energies -- unary
+// exp(-(e*e) / (2 thr^2)) (float argument, double exp as the reference's unqualified exp of
+// a float), pairwise terms over the KNN (device usac_knn) or grid neighbour lists, skipping
+// non-submodular / NaN terms, lambda = spatial_coherence_gc 0.1 (model.hpp:33) -- and runs
+// the reference's BK min cut (usac_maxflow.hpp); inliers = SINK nodes.  The <=
+// lo_inner_iterations least-squares fits on 7m-point subsets of the labelling's inliers do
+// not depend on each other (only the comparisons with the best do), so all of them run as
+// one batched fit and one batched scoring on the device, then the host replays them in
+// order (a failed fit ends the round; the generator is rewound to just after its draw).
+// Its mt19937 is seeded with seed + 1 (reference: std::random_device).
+struct GcLo {
+    usac_ctx *c;
+    usac::Mt19937 g;
+    uint32_t inner, m, n, limit;
+    float thr, lambda, sqr_thr;
+    const int32_t *knn_tab;
+    uint32_t knn;
+    const usac::GridNeighbors *grid;
+    uint32_t gc_iters = 0, labelings = 0, stages = 0;
+    int rc = USAC_OK;
+    std::vector<float> err, en, hsum, hmod;
+    std::vector<int32_t> inl, hpos, hcnt, hok;
+    std::vector<usac::Mt19937> g_after;
+
+    GcLo(usac_ctx *ctx, const usac_params *p, const int32_t *knn_table, uint32_t k, const usac::GridNeighbors *gr)
+        : c(ctx),
+          g(p->seed + 1u),
+          inner(p->lo_inner_iterations),
+          m(ctx->m),
+          n(ctx->n),
+          limit(7 * ctx->m),
+          thr(p->threshold),
+          lambda(p->spatial_coherence_gc > 0.f ? p->spatial_coherence_gc : 0.1f),
+          sqr_thr(2 * p->threshold * p->threshold),
+          knn_tab(knn_table),
+          knn(k),
+          grid(gr),
+          err(ctx->n),
+          en(ctx->n),
+          hsum(std::max<uint32_t>(1u, p->lo_inner_iterations)),
+          hmod(9 * (size_t)std::max<uint32_t>(1u, p->lo_inner_iterations)),
+          inl(ctx->n),
+          hpos((size_t)7 * ctx->m * std::max<uint32_t>(1u, p->lo_inner_iterations)),
+          hcnt(std::max<uint32_t>(1u, p->lo_inner_iterations)),
+          hok(std::max<uint32_t>(1u, p->lo_inner_iterations)),
+          g_after(std::max<uint32_t>(1u, p->lo_inner_iterations), usac::Mt19937(0)) {}
+
+    int reserve() {
+        const size_t W = std::max<uint32_t>(1u, inner);
+        HIP_TRY(c, c->lo_max.reserve(sizeof(int32_t) * n));
+        HIP_TRY(c, c->lo_pos.reserve(sizeof(int32_t) * hpos.size()));
+        HIP_TRY(c, c->lo_models.reserve(sizeof(float) * 9 * W));
+        HIP_TRY(c, c->lo_ok.reserve(sizeof(int32_t) * W));
+        HIP_TRY(c, c->lo_cnts.reserve(sizeof(int32_t) * W));
+        HIP_TRY(c, c->lo_sums.reserve(sizeof(float) * W));
+        HIP_TRY(c, c->lo_q.reserve(sizeof(float) * c->cols * limit * W));
+        HIP_TRY(c, c->lo_part.reserve(sizeof(double) * usac::nonminimal_partial_stride(limit) * W));
+        HIP_TRY(c, c->lo_ws.reserve(sizeof(float) * 18 * W));
+        HIP_TRY(c, c->lo_scr.reserve(usac::inliers_scratch_bytes(n, (uint32_t)W)));
+        HIP_TRY(c, c->gc_err.reserve(sizeof(float) * n));
+        return USAC_OK;
+    }
+
+    static bool bigger(int c1, float s1, int c2, float s2) { return c1 > c2 || (c1 == c2 && s1 > s2); }
+
+    // GraphCut::labeling -> number of SINK nodes, their ascending list in inl (host) and lo_max
+    int labeling(const float *model) {
+        HIP_TRY(c, hipMemcpyAsync(c->one_model.p, model, sizeof(float) * 9, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, usac::launch_point_errors(c->stream, c->estimator, c->pts.p, n, c->one_model.as<float>(),
+                                             c->gc_err.as<float>()));
+        HIP_TRY(c, hipMemcpyAsync(err.data(), c->gc_err.p, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        for (uint32_t i = 0; i < n; i++) {
+            const float d = err[i];
+            en[i] = (float)std::exp((double)(-(d * d) / sqr_thr));
+        }
+        usac::BkGraph G((int)n, knn_tab ? (size_t)knn * n : (size_t)n);
+        for (uint32_t i = 0; i < n; i++) G.add_node();
+        for (uint32_t i = 0; i < n; i++) G.add_term1((int)i, en[i], 0.f);
+        const float e01 = 1.f, e10 = 1.f;
+        for (uint32_t i = 0; i < n; i++) {
+            const float energy1 = en[i];
+            const uint32_t cnt = knn_tab ? knn : grid->count(i);
+            for (uint32_t k = 0; k < cnt; k++) {
+                const int32_t j = knn_tab ? knn_tab[(size_t)knn * i + k] : grid->at(i, k);
+                if (j == (int32_t)i || j < 0) continue;
+                const float energy2 = en[j];
+                const float e00 = (energy1 + energy2) / 2;
+                const float e11 = 1 - e00;
+                if (e00 + e11 > e01 + e10 || std::isnan(e00)) continue;
+                G.add_term2((int)i, j, e00 * lambda, e01 * lambda, e10 * lambda, e11 * lambda);
+            }
+        }
+        G.maxflow();
+        int L = 0;
+        for (uint32_t i = 0; i < n; i++)
+            if (G.is_sink((int)i)) inl[L++] = (int32_t)i;
+        if (L > 0)
+            HIP_TRY(c, hipMemcpyAsync(c->lo_max.p, inl.data(), sizeof(int32_t) * L, hipMemcpyHostToDevice, c->stream));
+        labelings++;
+        return L;
+    }
+
+    void run(float *model, int &cnt, float &sum) {
+        bool updated = true;
+        while (updated && !rc) {
+            updated = false;
+            const int L = labeling(model);
+            if (L < 0) {
+                rc = L;
+                return;
+            }
+            if (L <= (int)m) break;
+            const bool sampled = (uint32_t)L > limit;
+            const uint32_t W = std::min<uint32_t>(inner, sampled ? inner : 1u);
+            if (W == 0) break;
+            for (uint32_t w = 0; w < W; w++) {
+                if (sampled) usac::unique_set(g, hpos.data() + (size_t)w * limit, limit, (uint32_t)(L - 1));
+                g_after[w] = g;
+            }
+            if ((rc = fit_and_score(W, sampled ? limit : (uint32_t)L, sampled))) return;
+            uint32_t w = 0;
+            for (; w < W; w++) {
+                if (!hok[w]) break;  // EstimateModelNonMinimalSample failed: end of this round
+                if (bigger(hcnt[w], hsum[w], cnt, sum)) {
+                    updated = true;
+                    cnt = hcnt[w];
+                    sum = hsum[w];
+                    memcpy(model, hmod.data() + 9 * (size_t)w, sizeof(float) * 9);
+                }
+                gc_iters++;
+            }
+            g = g_after[w < W ? w : W - 1];
+        }
+    }
+
+    // W least-squares fits (sampled positions into lo_max, or all npts of it) and their
+    // (count, sequential sum) at the model threshold
+    int fit_and_score(uint32_t W, uint32_t npts, bool sampled) {
+        hipStream_t st = c->stream;
+        if (sampled)
+            HIP_TRY(c, hipMemcpyAsync(c->lo_pos.p, hpos.data(), sizeof(int32_t) * (size_t)W * limit,
+                                      hipMemcpyHostToDevice, st));
+        usac::NmBatch b{};
+        b.base = c->lo_max.as<int32_t>();
+        b.base_stride = 0;
+        b.pos = sampled ? c->lo_pos.as<int32_t>() : nullptr;
+        b.pos_stride = limit;
+        b.n1 = npts;
+        b.W = W;
+        b.nmax = npts;
+        b.q = c->lo_q.p;
+        b.q_stride = limit;
+        b.partial = c->lo_part.as<double>();
+        b.p_stride = usac::nonminimal_partial_stride(limit);
+        b.ws = c->lo_ws.as<float>();
+        b.model_out = c->lo_models.as<float>();
+        b.ok = c->lo_ok.as<int32_t>();
+        HIP_TRY(c, usac::launch_nonminimal_batch(st, c->estimator, c->pts.p, b));
+        HIP_TRY(c, usac::launch_inliers_batch(st, c->estimator, c->pts.p, n, c->lo_models.as<float>(), W, thr, nullptr,
+                                              nullptr, nullptr, 0, c->lo_cnts.as<int32_t>(), c->lo_sums.as<float>(),
+                                              c->lo_scr.p));
+        HIP_TRY(c, hipMemcpyAsync(hmod.data(), c->lo_models.p, sizeof(float) * 9 * W, hipMemcpyDeviceToHost, st));
+        HIP_TRY(c, hipMemcpyAsync(hok.data(), c->lo_ok.p, sizeof(int32_t) * W, hipMemcpyDeviceToHost, st));
+        HIP_TRY(c, hipMemcpyAsync(hcnt.data(), c->lo_cnts.p, sizeof(int32_t) * W, hipMemcpyDeviceToHost, st));
+        HIP_TRY(c, hipMemcpyAsync(hsum.data(), c->lo_sums.p, sizeof(float) * W, hipMemcpyDeviceToHost, st));
+        HIP_TRY(c, hipStreamSynchronize(st));
+        stages++;
+        return USAC_OK;
+    }
+};
+
 bool rec_better(const usac_record &a, const usac_record &b) {
     if (!a.valid) return false;
     if (!b.valid) return true;
@@ -712,7 +888,7 @@ void usac_destroy(usac_ctx *c) {
                       &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok,
                       &c->rec_send, &c->rec_all, &c->tv_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
-                      &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2})
+                      &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2, &c->gc_err})
         b->release();
     for (auto &ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -829,6 +1005,17 @@ int usac_get_inliers(usac_ctx *c, const float *model, float thr, int32_t *idx, u
     if (n) *n = (uint32_t)cnt;
     if (sum) *sum = s;
     return USAC_OK;
+}
+
+float usac_bk_label(int n, const float *unary, int m, const int32_t *ei, const int32_t *ej, const float *e00,
+                    const float *e01, const float *e10, const float *e11, int32_t *sink_out) {
+    usac::BkGraph G(n, (size_t)m);
+    for (int i = 0; i < n; i++) G.add_node();
+    for (int i = 0; i < n; i++) G.add_term1(i, unary[i], 0.f);
+    for (int k = 0; k < m; k++) G.add_term2(ei[k], ej[k], e00[k], e01[k], e10[k], e11[k]);
+    const float f = G.maxflow();
+    for (int i = 0; i < n; i++) sink_out[i] = G.is_sink(i) ? 1 : 0;
+    return f;
 }
 
 int usac_knn(usac_ctx *c, uint32_t k, int32_t *idx, float *d2) {
@@ -1069,7 +1256,16 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
         return fail(c, USAC_ERR_ARG, "NAPSAC KNN: k_nearest_neighbors must be in [sample_size - 1, 32] "
                                      "(napsac_sampler.hpp:48)");
     const bool use_lo = prm->lo == USAC_LO_INITLORSC || prm->lo == USAC_LO_INITFLORSC;
-    if (prm->lo != USAC_LO_NONE && !use_lo) return fail(c, USAC_ERR_UNSUPPORTED, "LO: InItLORsc / InItFLORsc only");
+    const bool use_gc = prm->lo == USAC_LO_GC;
+    if (prm->lo != USAC_LO_NONE && !use_lo && !use_gc)
+        return fail(c, USAC_ERR_UNSUPPORTED, "LO: InItLORsc / InItFLORsc / GC only");
+    if (use_gc && napsac)  // ransac.hpp:62-78 gives the neighbours to the sampler only: GC's are unset
+        return fail(c, USAC_ERR_UNSUPPORTED, "NAPSAC + GC: the reference leaves the graph cut without neighbours");
+    const bool gc_knn = use_gc && prm->neighbors != USAC_NEIGHBORS_GRID;
+    if (use_gc && !gc_knn && (c->cols != 4 || prm->cell_size <= 0))
+        return fail(c, USAC_ERR_ARG, "GC grid neighbours need 4-column points and cell_size > 0");
+    if (gc_knn && (prm->knn == 0 || prm->knn > usac::kKnnMax))
+        return fail(c, USAC_ERR_ARG, "GC KNN: k_nearest_neighbors must be in [1, 32]");
     if (use_lo && (prm->lo_sample_size == 0 || prm->lo_iterative_iterations == 0))
         return fail(c, USAC_ERR_ARG, "LO parameters must be > 0");
     if (prosac && c->n <= 20) return fail(c, USAC_ERR_ARG, "PROSAC needs > 20 points (prosac_termination_criteria.hpp:158-163)");
@@ -1136,6 +1332,19 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
     if (use_lo) {
         lo.reset(new LoRansac(c, prm));
         if ((rc = lo->reserve())) return rc;
+    }
+    std::unique_ptr<GcLo> gc;
+    if (use_gc) {  // Ransac ctor neighbours for the graph cut (ransac.hpp:60-78)
+        if (gc_knn) {
+            knn_tab.resize((size_t)n * prm->knn);
+            if ((rc = usac_knn(c, prm->knn, knn_tab.data(), nullptr))) return rc;
+        } else {
+            std::vector<float> hp((size_t)n * 4);
+            HIP_TRY(c, hipMemcpy(hp.data(), c->pts.p, sizeof(float) * hp.size(), hipMemcpyDeviceToHost));
+            grid.reset(new usac::GridNeighbors(hp.data(), n, prm->cell_size));
+        }
+        gc.reset(new GcLo(c, prm, gc_knn ? knn_tab.data() : nullptr, prm->knn, grid.get()));
+        if ((rc = gc->reserve())) return rc;
     }
     usac::StandardTerminationCriteria term(prm->desired_prob, m, n, prm->max_iterations);
     std::unique_ptr<usac::Sprt> sprt;
@@ -1285,6 +1494,12 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
                     if (lo->rc) return lo->rc;
                     lap(T_LO);
                 }
+                if (gc) {
+                    lap(T_REPLAY);
+                    gc->run(model, cur.inlier_number, cur.score);
+                    if (gc->rc) return gc->rc;
+                    lap(T_LO);
+                }
                 best = cur;
                 memcpy(best_model, model, sizeof(best_model));
                 if (prosac) {
@@ -1330,10 +1545,10 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
     out->n_records = nrec;
     out->sprt_histories = sprt ? (int32_t)sprt->histories() : 0;
     out->prosac_term_len = prosac ? pterm->terminationLength() : n;
-    out->lo_inner_iters = lo ? lo->inner_count : 0;
-    out->lo_iterative_iters = lo ? lo->iterative_count : 0;
-    out->lo_rounds = lo ? lo->rounds : 0;
-    out->lo_stages = lo ? lo->stages : 0;
+    out->lo_inner_iters = lo ? lo->inner_count : gc ? gc->gc_iters : 0;
+    out->lo_iterative_iters = lo ? lo->iterative_count : gc ? gc->labelings : 0;
+    out->lo_rounds = lo ? lo->rounds : gc ? gc->labelings : 0;
+    out->lo_stages = lo ? lo->stages : gc ? gc->stages : 0;
     memcpy(out->minimal_model, best_model, sizeof(best_model));
     out->minimal_inliers = best.inlier_number;
     if (best.inlier_number == 0) {

@@ -103,6 +103,9 @@ hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, 
                                 uint32_t W, float thr, const float *thrs, const uint32_t *slots, int32_t *idx,
                                 size_t idx_stride, int32_t *counts, float *sums, void *scratch);
 size_t inliers_scratch_bytes(uint32_t n, uint32_t W);
+// every point's exact residual under one model (n floats)
+hipError_t launch_point_errors(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *model,
+                               float *errors);
 
 // W independent non-minimal fits (kernels_nonmin.hip).  Fit w: index list base + w *
 // base_stride, read through pos + w * pos_stride when pos != nullptr; ns[w] points (device;
