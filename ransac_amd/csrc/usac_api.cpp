@@ -1583,7 +1583,7 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
                 "usac_ransac_run ms: setup %.3f draw %.3f device %.3f sums %.3f replay %.3f lo %.3f polish %.3f "
                 "(lo rounds %u stages %u)\n",
                 tsplit[T_SETUP], tsplit[T_DRAW], tsplit[T_DEVICE], tsplit[T_SUMS], tsplit[T_REPLAY], tsplit[T_LO],
-                tsplit[T_POLISH], lo ? lo->rounds : 0u, lo ? lo->stages : 0u);
+                tsplit[T_POLISH], lo ? lo->rounds : gc ? gc->labelings : 0u, lo ? lo->stages : gc ? gc->stages : 0u);
     if ((rc = score_inliers(best_model))) return rc;  // ransac.cpp:214
     if (inliers_out && cnt > 0)
         HIP_TRY(c, hipMemcpy(inliers_out, c->inl_idx.p, sizeof(int32_t) * (size_t)cnt, hipMemcpyDeviceToHost));

@@ -18,36 +18,28 @@ namespace usac {
 class BkGraph {
    public:
     BkGraph(int n_nodes, size_t n_edges) {
-        first_.reserve(n_nodes);
-        tr_cap_.reserve(n_nodes);
-        head_.reserve(2 * n_edges);
-        anext_.reserve(2 * n_edges);
-        r_cap_.reserve(2 * n_edges);
+        nd_.reserve(n_nodes);
+        arcs_.reserve(2 * n_edges);
     }
     int add_node() {
-        first_.push_back(-1);
-        tr_cap_.push_back(0.f);
-        return (int)first_.size() - 1;
+        nd_.push_back(Node{-1, kNone, -1, 0, 0, 0.f, 0});
+        return (int)nd_.size() - 1;
     }
     // graph.h add_tweights
     void add_tweights(int i, float cap_source, float cap_sink) {
-        const float delta = tr_cap_[i];
+        const float delta = nd_[i].tr_cap;
         if (delta > 0) cap_source += delta;
         else cap_sink -= delta;
         flow_ += (cap_source < cap_sink) ? cap_source : cap_sink;
-        tr_cap_[i] = cap_source - cap_sink;
+        nd_[i].tr_cap = cap_source - cap_sink;
     }
     // graph.h add_edge
     void add_edge(int i, int j, float cap, float rev_cap) {
-        const int a = (int)head_.size();
-        head_.push_back(j);
-        anext_.push_back(first_[i]);
-        r_cap_.push_back(cap);
-        first_[i] = a;
-        head_.push_back(i);
-        anext_.push_back(first_[j]);
-        r_cap_.push_back(rev_cap);
-        first_[j] = a + 1;
+        const int a = (int)arcs_.size();
+        arcs_.push_back(Arc{j, nd_[i].first, cap});
+        nd_[i].first = a;
+        arcs_.push_back(Arc{i, nd_[j].first, rev_cap});
+        nd_[j].first = a + 1;
     }
     // energy.h add_term1(x, E0, E1) / add_term2(x, y, E00, E01, E10, E11)
     void add_term1(int x, float e0, float e1) { add_tweights(x, e1, e0); }
@@ -70,62 +62,64 @@ class BkGraph {
 
     // Graph::maxflow(reuse_trees = false)
     float maxflow() {
-        const int n = (int)first_.size();
-        parent_.assign(n, kNone);
-        next_.assign(n, -1);
-        ts_.assign(n, 0);
-        dist_.assign(n, 0);
-        is_sink_.assign(n, 0);
+        const int n = (int)nd_.size();
+        for (Node &v : nd_) {
+            v.parent = kNone;
+            v.next = -1;
+            v.ts = 0;
+            v.dist = 0;
+            v.is_sink = 0;
+        }
         q_first_[0] = q_last_[0] = q_first_[1] = q_last_[1] = -1;
         orphan_first_ = orphan_last_ = -1;
         time_ = 0;
         for (int i = 0; i < n; i++) {
-            if (tr_cap_[i] > 0) {
-                is_sink_[i] = 0;
-                parent_[i] = kTerminal;
+            if (nd_[i].tr_cap > 0) {
+                nd_[i].is_sink = 0;
+                nd_[i].parent = kTerminal;
                 set_active(i);
-                dist_[i] = 1;
-            } else if (tr_cap_[i] < 0) {
-                is_sink_[i] = 1;
-                parent_[i] = kTerminal;
+                nd_[i].dist = 1;
+            } else if (nd_[i].tr_cap < 0) {
+                nd_[i].is_sink = 1;
+                nd_[i].parent = kTerminal;
                 set_active(i);
-                dist_[i] = 1;
+                nd_[i].dist = 1;
             }
         }
         int current = -1;
         for (;;) {
             int i = current;
             if (i >= 0) {
-                next_[i] = -1;
-                if (parent_[i] == kNone) i = -1;
+                nd_[i].next = -1;
+                if (nd_[i].parent == kNone) i = -1;
             }
             if (i < 0 && (i = next_active()) < 0) break;
             int a;
-            if (!is_sink_[i]) {  // grow the source tree
-                for (a = first_[i]; a >= 0; a = anext_[a]) {
-                    if (!r_cap_[a]) continue;
-                    const int j = head_[a];
-                    if (parent_[j] == kNone) {
+            if (!nd_[i].is_sink) {  // grow the source tree
+                for (a = nd_[i].first; a >= 0; a = arcs_[a].next) {
+                    if (!arcs_[a].r_cap) continue;
+                    const int j = arcs_[a].head;
+                    if (nd_[j].parent == kNone) {
                         adopt(j, a ^ 1, i, 0);
                         set_active(j);
-                    } else if (is_sink_[j]) {
+                    } else if (nd_[j].is_sink) {
                         break;
-                    } else if (ts_[j] <= ts_[i] && dist_[j] > dist_[i]) {
-                        adopt(j, a ^ 1, i, is_sink_[j]);
+                    } else if (nd_[j].ts <= nd_[i].ts && nd_[j].dist > nd_[i].dist) {
+                        adopt(j, a ^ 1, i, nd_[j].is_sink);
                     }
                 }
             } else {  // grow the sink tree
-                for (a = first_[i]; a >= 0; a = anext_[a]) {
-                    if (!r_cap_[a ^ 1]) continue;
-                    const int j = head_[a];
-                    if (parent_[j] == kNone) {
+                for (a = nd_[i].first; a >= 0; a = arcs_[a].next) {
+                    if (!arcs_[a ^ 1].r_cap) continue;
+                    const int j = arcs_[a].head;
+                    if (nd_[j].parent == kNone) {
                         adopt(j, a ^ 1, i, 1);
                         set_active(j);
-                    } else if (!is_sink_[j]) {
+                    } else if (!nd_[j].is_sink) {
                         a ^= 1;
                         break;
-                    } else if (ts_[j] <= ts_[i] && dist_[j] > dist_[i]) {
-                        adopt(j, a ^ 1, i, is_sink_[j]);
+                    } else if (nd_[j].ts <= nd_[i].ts && nd_[j].dist > nd_[i].dist) {
+                        adopt(j, a ^ 1, i, nd_[j].is_sink);
                     }
                 }
             }
@@ -134,7 +128,7 @@ class BkGraph {
                 current = -1;
                 continue;
             }
-            next_[i] = i;  // stays active
+            nd_[i].next = i;  // stays active
             current = i;
             augment(a);
             int np;
@@ -147,7 +141,7 @@ class BkGraph {
                     op_next_[np] = op_free_;  // back to the pool
                     op_free_ = np;
                     if (orphan_first_ < 0) orphan_last_ = -1;
-                    process_orphan(o, is_sink_[o]);
+                    process_orphan(o, nd_[o].is_sink);
                 }
                 orphan_first_ = np_next;
             }
@@ -155,23 +149,23 @@ class BkGraph {
         return flow_;
     }
     // what_segment(i) == SINK (free nodes: SOURCE)
-    bool is_sink(int i) const { return parent_[i] != kNone && is_sink_[i]; }
+    bool is_sink(int i) const { return nd_[i].parent != kNone && nd_[i].is_sink; }
 
    private:
     static constexpr int kNone = -1, kTerminal = -2, kOrphan = -3, kInfD = 0x7fffffff;
 
     void adopt(int j, int parent_arc, int i, uint8_t sink) {
-        is_sink_[j] = sink;
-        parent_[j] = parent_arc;
-        ts_[j] = ts_[i];
-        dist_[j] = dist_[i] + 1;
+        nd_[j].is_sink = sink;
+        nd_[j].parent = parent_arc;
+        nd_[j].ts = nd_[i].ts;
+        nd_[j].dist = nd_[i].dist + 1;
     }
     void set_active(int i) {
-        if (next_[i] != -1) return;
-        if (q_last_[1] >= 0) next_[q_last_[1]] = i;
+        if (nd_[i].next != -1) return;
+        if (q_last_[1] >= 0) nd_[q_last_[1]].next = i;
         else q_first_[1] = i;
         q_last_[1] = i;
-        next_[i] = i;
+        nd_[i].next = i;
     }
     int next_active() {
         for (;;) {
@@ -182,10 +176,10 @@ class BkGraph {
                 q_first_[1] = q_last_[1] = -1;
                 if (i < 0) return -1;
             }
-            if (next_[i] == i) q_first_[0] = q_last_[0] = -1;
-            else q_first_[0] = next_[i];
-            next_[i] = -1;
-            if (parent_[i] != kNone) return i;
+            if (nd_[i].next == i) q_first_[0] = q_last_[0] = -1;
+            else q_first_[0] = nd_[i].next;
+            nd_[i].next = -1;
+            if (nd_[i].parent != kNone) return i;
         }
     }
     int np_new(int node) {
@@ -202,13 +196,13 @@ class BkGraph {
         return np;
     }
     void orphan_front(int i) {
-        parent_[i] = kOrphan;
+        nd_[i].parent = kOrphan;
         const int np = np_new(i);
         op_next_[np] = orphan_first_;
         orphan_first_ = np;
     }
     void orphan_rear(int i) {
-        parent_[i] = kOrphan;
+        nd_[i].parent = kOrphan;
         const int np = np_new(i);
         if (orphan_last_ >= 0) op_next_[orphan_last_] = np;
         else orphan_first_ = np;
@@ -217,95 +211,104 @@ class BkGraph {
     }
     void augment(int mid) {
         int i, a;
-        float b = r_cap_[mid];
-        for (i = head_[mid ^ 1];; i = head_[a]) {
-            a = parent_[i];
+        float b = arcs_[mid].r_cap;
+        for (i = arcs_[mid ^ 1].head;; i = arcs_[a].head) {
+            a = nd_[i].parent;
             if (a == kTerminal) break;
-            if (b > r_cap_[a ^ 1]) b = r_cap_[a ^ 1];
+            if (b > arcs_[a ^ 1].r_cap) b = arcs_[a ^ 1].r_cap;
         }
-        if (b > tr_cap_[i]) b = tr_cap_[i];
-        for (i = head_[mid];; i = head_[a]) {
-            a = parent_[i];
+        if (b > nd_[i].tr_cap) b = nd_[i].tr_cap;
+        for (i = arcs_[mid].head;; i = arcs_[a].head) {
+            a = nd_[i].parent;
             if (a == kTerminal) break;
-            if (b > r_cap_[a]) b = r_cap_[a];
+            if (b > arcs_[a].r_cap) b = arcs_[a].r_cap;
         }
-        if (b > -tr_cap_[i]) b = -tr_cap_[i];
-        r_cap_[mid ^ 1] += b;
-        r_cap_[mid] -= b;
-        for (i = head_[mid ^ 1];; i = head_[a]) {
-            a = parent_[i];
+        if (b > -nd_[i].tr_cap) b = -nd_[i].tr_cap;
+        arcs_[mid ^ 1].r_cap += b;
+        arcs_[mid].r_cap -= b;
+        for (i = arcs_[mid ^ 1].head;; i = arcs_[a].head) {
+            a = nd_[i].parent;
             if (a == kTerminal) break;
-            r_cap_[a] += b;
-            r_cap_[a ^ 1] -= b;
-            if (!r_cap_[a ^ 1]) orphan_front(i);
+            arcs_[a].r_cap += b;
+            arcs_[a ^ 1].r_cap -= b;
+            if (!arcs_[a ^ 1].r_cap) orphan_front(i);
         }
-        tr_cap_[i] -= b;
-        if (!tr_cap_[i]) orphan_front(i);
-        for (i = head_[mid];; i = head_[a]) {
-            a = parent_[i];
+        nd_[i].tr_cap -= b;
+        if (!nd_[i].tr_cap) orphan_front(i);
+        for (i = arcs_[mid].head;; i = arcs_[a].head) {
+            a = nd_[i].parent;
             if (a == kTerminal) break;
-            r_cap_[a ^ 1] += b;
-            r_cap_[a] -= b;
-            if (!r_cap_[a]) orphan_front(i);
+            arcs_[a ^ 1].r_cap += b;
+            arcs_[a].r_cap -= b;
+            if (!arcs_[a].r_cap) orphan_front(i);
         }
-        tr_cap_[i] += b;
-        if (!tr_cap_[i]) orphan_front(i);
+        nd_[i].tr_cap += b;
+        if (!nd_[i].tr_cap) orphan_front(i);
         flow_ += b;
     }
     // process_source_orphan (sink = 0) / process_sink_orphan (sink = 1)
     void process_orphan(int i, uint8_t sink) {
         int a0_min = kNone, d_min = kInfD;
-        for (int a0 = first_[i]; a0 >= 0; a0 = anext_[a0]) {
-            if (!(sink ? r_cap_[a0] : r_cap_[a0 ^ 1])) continue;
-            int j = head_[a0];
-            if (is_sink_[j] != sink || parent_[j] == kNone) continue;
+        for (int a0 = nd_[i].first; a0 >= 0; a0 = arcs_[a0].next) {
+            if (!(sink ? arcs_[a0].r_cap : arcs_[a0 ^ 1].r_cap)) continue;
+            int j = arcs_[a0].head;
+            if (nd_[j].is_sink != sink || nd_[j].parent == kNone) continue;
             int d = 0;  // the origin of j
             for (;;) {
-                if (ts_[j] == time_) {
-                    d += dist_[j];
+                if (nd_[j].ts == time_) {
+                    d += nd_[j].dist;
                     break;
                 }
-                const int a = parent_[j];
+                const int a = nd_[j].parent;
                 d++;
                 if (a == kTerminal) {
-                    ts_[j] = time_;
-                    dist_[j] = 1;
+                    nd_[j].ts = time_;
+                    nd_[j].dist = 1;
                     break;
                 }
                 if (a == kOrphan) {
                     d = kInfD;
                     break;
                 }
-                j = head_[a];
+                j = arcs_[a].head;
             }
             if (d < kInfD) {
                 if (d < d_min) {
                     a0_min = a0;
                     d_min = d;
                 }
-                for (j = head_[a0]; ts_[j] != time_; j = head_[parent_[j]]) {
-                    ts_[j] = time_;
-                    dist_[j] = d--;
+                for (j = arcs_[a0].head; nd_[j].ts != time_; j = arcs_[nd_[j].parent].head) {
+                    nd_[j].ts = time_;
+                    nd_[j].dist = d--;
                 }
             }
         }
-        if ((parent_[i] = a0_min) != kNone) {
-            ts_[i] = time_;
-            dist_[i] = d_min + 1;
+        if ((nd_[i].parent = a0_min) != kNone) {
+            nd_[i].ts = time_;
+            nd_[i].dist = d_min + 1;
             return;
         }
-        for (int a0 = first_[i]; a0 >= 0; a0 = anext_[a0]) {
-            const int j = head_[a0];
-            const int a = parent_[j];
-            if (is_sink_[j] != sink || a == kNone) continue;
-            if (sink ? r_cap_[a0] : r_cap_[a0 ^ 1]) set_active(j);
-            if (a != kTerminal && a != kOrphan && head_[a] == i) orphan_rear(j);
+        for (int a0 = nd_[i].first; a0 >= 0; a0 = arcs_[a0].next) {
+            const int j = arcs_[a0].head;
+            const int a = nd_[j].parent;
+            if (nd_[j].is_sink != sink || a == kNone) continue;
+            if (sink ? arcs_[a0].r_cap : arcs_[a0 ^ 1].r_cap) set_active(j);
+            if (a != kTerminal && a != kOrphan && arcs_[a].head == i) orphan_rear(j);
         }
     }
 
-    std::vector<int> first_, head_, anext_, parent_, next_, ts_, dist_, op_node_, op_next_;
-    std::vector<float> tr_cap_, r_cap_;
-    std::vector<uint8_t> is_sink_;
+    struct Arc {
+        int head, next;  // node the arc points to, next arc out of the same node
+        float r_cap;     // residual capacity
+    };
+    struct Node {
+        int first, parent, next, ts, dist;  // first out-arc, tree parent arc, active-list link, TIME / DIST
+        float tr_cap;                       // > 0: residual SOURCE -> node, < 0: node -> SINK
+        uint8_t is_sink;
+    };
+    std::vector<Arc> arcs_;
+    std::vector<Node> nd_;
+    std::vector<int> op_node_, op_next_;
     int q_first_[2] = {-1, -1}, q_last_[2] = {-1, -1}, orphan_first_ = -1, orphan_last_ = -1, op_free_ = -1,
         time_ = 0;
     float flow_ = 0.f;
