@@ -204,20 +204,25 @@ __device__ __forceinline__ void stage_a_bounds(HModel &M, float4 c, float T) {
     M.F = (M.trm * M.dZ + M.E) * 1.00000095367431640625f;             // (1 + 2^-20)
 }
 
-// Stage A for two points at once: the same FMA chain element-wise (v_pk_fma_f32), so each
-// half is bit-identical to stage_a_reject.
-__device__ __forceinline__ void stage_a_reject2(const HModel &M, v2f x1, v2f y1, v2f x2, v2f y2, bool &k0,
-                                                bool &k1) {
+// Stage A for two points at once: the FMA chains element-wise (v_pk_fma_f32), then the
+// L-infinity test per point: keep iff !(max(|ex|, |ey|) > r) with r = |Z| trm + F.
+// |e| >= max(|ex|, |ey|), so this rejects only where the Euclidean test |e| > r does
+// (stage_a_reject derives that one) -- it lets through the few pairs between the circle and
+// its circumscribed square -- for 11 VALU slots per point instead of 13 (no |e|^2, no r^2).
+// One rounding (r, downwards by at most 2^-24 relative) against the (1 + 2^-18) slack
+// already in trm and F.  Non-finite: if Z or its bound is infinite, r = inf and nothing is
+// rejected; a NaN component can only come with an infinite X / Z, where the reference's
+// error is not finite or not below thr.  Returns the KEEP flags.
+__device__ __forceinline__ void stage_a_keep2(const HModel &M, v2f x1, v2f y1, v2f x2, v2f y2, bool &k0,
+                                              bool &k1) {
     const v2f X = __builtin_elementwise_fma(M.h2[1], y1, __builtin_elementwise_fma(M.h2[0], x1, M.h2[2]));
     const v2f Y = __builtin_elementwise_fma(M.h2[4], y1, __builtin_elementwise_fma(M.h2[3], x1, M.h2[5]));
     const v2f Z = __builtin_elementwise_fma(M.h2[7], y1, __builtin_elementwise_fma(M.h2[6], x1, M.h2[8]));
     const v2f ex = __builtin_elementwise_fma(x2, Z, -X);
     const v2f ey = __builtin_elementwise_fma(y2, Z, -Y);
-    const v2f lhs = __builtin_elementwise_fma(ex, ex, ey * ey);
-    const v2f r = v2f{__builtin_fmaf(fabsf(Z.x), M.trm, M.F), __builtin_fmaf(fabsf(Z.y), M.trm, M.F)};
-    const v2f rr = r * r;
-    k0 = lhs.x > rr.x;
-    k1 = lhs.y > rr.y;
+    const float m0 = __builtin_fmaxf(fabsf(ex.x), fabsf(ey.x)), m1 = __builtin_fmaxf(fabsf(ex.y), fabsf(ey.y));
+    k0 = !(m0 > __builtin_fmaf(fabsf(Z.x), M.trm, M.F));
+    k1 = !(m1 > __builtin_fmaf(fabsf(Z.y), M.trm, M.F));
 }
 
 // Stage A -- forward-only rejection, 14 VALU ops, no rcp / sqrt.  X, Y, Z by FMA chains,
@@ -281,13 +286,13 @@ template <bool EXACT_SUM>
 __device__ __forceinline__ void score_group(const HModel &M, float4 X1, float4 Y1, float4 X2, float4 Y2, float4 bd,
                                             float4 tr, float T, float thr, int &cnt, float &sum) {
     bool k0, k1, k2, k3;
-    stage_a_reject2(M, v2f{X1.x, X1.y}, v2f{Y1.x, Y1.y}, v2f{X2.x, X2.y}, v2f{Y2.x, Y2.y}, k0, k1);
-    stage_a_reject2(M, v2f{X1.z, X1.w}, v2f{Y1.z, Y1.w}, v2f{X2.z, X2.w}, v2f{Y2.z, Y2.w}, k2, k3);
-    if (__builtin_amdgcn_ballot_w64(!(k0 && k1 && k2 && k3)) == 0) return;
-    if (!k0) stage_b<EXACT_SUM>(M, X1.x, Y1.x, X2.x, Y2.x, bd.x, T, thr, cnt, sum);
-    if (!k1) stage_b<EXACT_SUM>(M, X1.y, Y1.y, X2.y, Y2.y, bd.y, T, thr, cnt, sum);
-    if (!k2) stage_b<EXACT_SUM>(M, X1.z, Y1.z, X2.z, Y2.z, bd.z, T, thr, cnt, sum);
-    if (!k3) stage_b<EXACT_SUM>(M, X1.w, Y1.w, X2.w, Y2.w, bd.w, T, thr, cnt, sum);
+    stage_a_keep2(M, v2f{X1.x, X1.y}, v2f{Y1.x, Y1.y}, v2f{X2.x, X2.y}, v2f{Y2.x, Y2.y}, k0, k1);
+    stage_a_keep2(M, v2f{X1.z, X1.w}, v2f{Y1.z, Y1.w}, v2f{X2.z, X2.w}, v2f{Y2.z, Y2.w}, k2, k3);
+    if (__builtin_amdgcn_ballot_w64(k0 | k1 | k2 | k3) == 0) return;
+    if (k0) stage_b<EXACT_SUM>(M, X1.x, Y1.x, X2.x, Y2.x, bd.x, T, thr, cnt, sum);
+    if (k1) stage_b<EXACT_SUM>(M, X1.y, Y1.y, X2.y, Y2.y, bd.y, T, thr, cnt, sum);
+    if (k2) stage_b<EXACT_SUM>(M, X1.z, Y1.z, X2.z, Y2.z, bd.z, T, thr, cnt, sum);
+    if (k3) stage_b<EXACT_SUM>(M, X1.w, Y1.w, X2.w, Y2.w, bd.w, T, thr, cnt, sum);
 }
 
 // Lanes = hypotheses (64 per wave), point groups wave-uniform (scalar loads, two groups per
