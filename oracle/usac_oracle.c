@@ -220,10 +220,21 @@ static void pick_vector(double W[][9], int r, int mode, double *h) {
     }
 }
 
-/* Cyclic two-sided Jacobi eigen-decomposition of a symmetric 9x9 (fp64); returns the
- * eigenvector of the smallest eigenvalue in v.  Restates cv::SVD::compute's last vt row
- * for a tall (2n > 9) DLT system via the normal matrix (dlt.cpp:92-98,
- * eight_points.cpp:38-44). */
+/* Two-sided Jacobi eigen-decomposition of a symmetric 9x9 (fp64), round-robin ("parallel")
+ * ordering: a sweep is 9 rounds of 4 disjoint (p, q) planes (the circle schedule over 10
+ * indices, the 10th a dummy).  Per round: every plane's rotation from the matrix at the start
+ * of the round (planes with a zero off-diagonal are skipped), then all column updates, then
+ * all row updates, then V's columns -- the disjoint planes make each element's update
+ * unambiguous, so the device runs the four planes of a round at once (kernels_nonmin.hip).
+ * Stops when the off-diagonal mass is <= 1e-30 of the diagonal's.  Returns the eigenvector
+ * of the smallest eigenvalue in v.  Restates cv::SVD::compute's last vt row for a tall
+ * (2n > 9) DLT system via the normal matrix (dlt.cpp:92-98, eight_points.cpp:38-44); the
+ * rotation order is this build's spec (OpenCV's is unpinned). */
+static const signed char kJacobiRounds[9][4][2] = {
+    {{1, 8}, {2, 7}, {3, 6}, {4, 5}}, {{0, 8}, {1, 6}, {2, 5}, {3, 4}}, {{0, 7}, {1, 4}, {2, 3}, {6, 8}},
+    {{0, 6}, {1, 2}, {4, 8}, {5, 7}}, {{0, 5}, {2, 8}, {3, 7}, {4, 6}}, {{0, 4}, {1, 7}, {2, 6}, {3, 5}},
+    {{0, 3}, {1, 5}, {2, 4}, {7, 8}}, {{0, 2}, {1, 3}, {5, 8}, {6, 7}}, {{0, 1}, {3, 8}, {4, 7}, {5, 6}}};
+
 static void sym_eig_min(double A[9][9], double *v) {
     double V[9][9];
     for (int i = 0; i < 9; i++)
@@ -235,27 +246,48 @@ static void sym_eig_min(double A[9][9], double *v) {
             for (int q = p + 1; q < 9; q++) off += A[p][q] * A[p][q];
         }
         if (off <= 1e-30 * diag || off == 0.0) break;
-        for (int p = 0; p < 8; p++) {
-            for (int q = p + 1; q < 9; q++) {
-                double apq = A[p][q];
-                if (apq == 0.0) continue;
-                double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
-                double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
-                for (int k = 0; k < 9; k++) {
-                    double akp = A[k][p], akq = A[k][q];
-                    A[k][p] = c * akp - s * akq;
-                    A[k][q] = s * akp + c * akq;
+        for (int r = 0; r < 9; r++) {
+            double cs[4][2];
+            int on[4];
+            for (int k = 0; k < 4; k++) {
+                const int p = kJacobiRounds[r][k][0], q = kJacobiRounds[r][k][1];
+                const double apq = A[p][q];
+                on[k] = apq != 0.0;
+                if (!on[k]) continue;
+                const double theta = (A[q][q] - A[p][p]) / (2.0 * apq);
+                const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+                cs[k][0] = c;
+                cs[k][1] = s;
+            }
+            for (int k = 0; k < 4; k++) { /* columns */
+                if (!on[k]) continue;
+                const int p = kJacobiRounds[r][k][0], q = kJacobiRounds[r][k][1];
+                const double c = cs[k][0], s = cs[k][1];
+                for (int i = 0; i < 9; i++) {
+                    const double aip = A[i][p], aiq = A[i][q];
+                    A[i][p] = c * aip - s * aiq;
+                    A[i][q] = s * aip + c * aiq;
                 }
-                for (int k = 0; k < 9; k++) {
-                    double apk = A[p][k], aqk = A[q][k];
-                    A[p][k] = c * apk - s * aqk;
-                    A[q][k] = s * apk + c * aqk;
+            }
+            for (int k = 0; k < 4; k++) { /* rows */
+                if (!on[k]) continue;
+                const int p = kJacobiRounds[r][k][0], q = kJacobiRounds[r][k][1];
+                const double c = cs[k][0], s = cs[k][1];
+                for (int j = 0; j < 9; j++) {
+                    const double apj = A[p][j], aqj = A[q][j];
+                    A[p][j] = c * apj - s * aqj;
+                    A[q][j] = s * apj + c * aqj;
                 }
-                for (int k = 0; k < 9; k++) {
-                    double vkp = V[k][p], vkq = V[k][q];
-                    V[k][p] = c * vkp - s * vkq;
-                    V[k][q] = s * vkp + c * vkq;
+            }
+            for (int k = 0; k < 4; k++) { /* V columns */
+                if (!on[k]) continue;
+                const int p = kJacobiRounds[r][k][0], q = kJacobiRounds[r][k][1];
+                const double c = cs[k][0], s = cs[k][1];
+                for (int i = 0; i < 9; i++) {
+                    const double vip = V[i][p], viq = V[i][q];
+                    V[i][p] = c * vip - s * viq;
+                    V[i][q] = s * vip + c * viq;
                 }
             }
         }

@@ -16,6 +16,12 @@ namespace usac {
 
 constexpr uint32_t kAtaBlock = 64;
 
+// round-robin Jacobi schedule: 9 rounds of 4 disjoint planes (oracle kJacobiRounds)
+__constant__ signed char kJacobiRounds[9][4][2] = {
+    {{1, 8}, {2, 7}, {3, 6}, {4, 5}}, {{0, 8}, {1, 6}, {2, 5}, {3, 4}}, {{0, 7}, {1, 4}, {2, 3}, {6, 8}},
+    {{0, 6}, {1, 2}, {4, 8}, {5, 7}}, {{0, 5}, {2, 8}, {3, 7}, {4, 6}}, {{0, 4}, {1, 7}, {2, 6}, {3, 5}},
+    {{0, 3}, {1, 5}, {2, 4}, {7, 8}}, {{0, 2}, {1, 3}, {5, 8}, {6, 7}}, {{0, 1}, {3, 8}, {4, 7}, {5, 6}}};
+
 // Every kernel below is batched over W independent fits (blockIdx.y, or blockIdx.x for the
 // one-workgroup stages): fit w uses the index list base + w * base_stride (through the
 // positions pos + w * pos_stride when pos is given: idx_i = list[pos_i]), ns[w] points, and
@@ -186,8 +192,8 @@ __global__ __launch_bounds__(64) void k_ata_partial(const float4 *__restrict__ q
     for (int e = 0; e < 45; e++) out[e] = acc[e];
 }
 
-// Final solve, one wave: A^T A from the partials (lane e), cyclic Jacobi eigen on 9
-// lanes (LDS), smallest-eigenvalue vector; or the thin row-Jacobi when the system has
+// Final solve, one wave: A^T A from the partials (lane e), round-robin Jacobi eigen over
+// 36 lanes (LDS), smallest-eigenvalue vector; or the thin row-Jacobi when the system has
 // <= 8 rows (homography 2n <= 8, fundamental n <= 8: SURVEY Q1/Q2); then
 //   homography : H = T2^-1 * Hn * T1 (fp64), H /= H33 (normalized_dlt.cpp:18-22);
 //   fundamental: F = T2^T * Fn * T1 (fp64), F /= F33 when |F33| > FLT_EPSILON
@@ -276,6 +282,12 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
         if (t < 9)
             for (int j = 0; j < 9; j++) V[j][t] = (j == (int)t) ? 1.0 : 0.0;
         __syncthreads();
+        // round-robin Jacobi (the oracle's sym_eig_min spec): per round the rotations of 4
+        // disjoint planes from the matrix at the round's start (lanes 0-3), then all column
+        // updates (lane = (row, plane), V alongside), then all row updates (lane = (plane,
+        // column)) -- every lane owns disjoint element pairs, 3 barriers per round
+        __shared__ double s_cs[4][2];
+        __shared__ int s_on[4];
         for (int sweep = 0; sweep < 50; sweep++) {
             double off = 0.0, diag = 0.0;
             for (int p = 0; p < 9; p++) {
@@ -283,30 +295,45 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
                 for (int qq = p + 1; qq < 9; qq++) off += A[p][qq] * A[p][qq];
             }
             if (off <= 1e-30 * diag || off == 0.0) break;
-            for (int p = 0; p < 8; p++) {
-                for (int qq = p + 1; qq < 9; qq++) {
+            for (int r = 0; r < 9; r++) {
+                if (t < 4) {
+                    const int p = kJacobiRounds[r][t][0], qq = kJacobiRounds[r][t][1];
                     const double apq = A[p][qq];
-                    if (apq == 0.0) continue;
-                    const double theta = (A[qq][qq] - A[p][p]) / (2.0 * apq);
-                    const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                    const double c = 1.0 / sqrt(tt * tt + 1.0), s = tt * c;
-                    __syncthreads();
-                    if (t < 9) {
-                        const double akp = A[t][p], akq = A[t][qq];
-                        A[t][p] = c * akp - s * akq;
-                        A[t][qq] = s * akp + c * akq;
+                    s_on[t] = apq != 0.0;
+                    if (apq != 0.0) {
+                        const double theta = (A[qq][qq] - A[p][p]) / (2.0 * apq);
+                        const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                        const double c = 1.0 / sqrt(tt * tt + 1.0);
+                        s_cs[t][0] = c;
+                        s_cs[t][1] = tt * c;
                     }
-                    __syncthreads();
-                    if (t < 9) {
-                        const double apk = A[p][t], aqk = A[qq][t];
-                        A[p][t] = c * apk - s * aqk;
-                        A[qq][t] = s * apk + c * aqk;
-                        const double vkp = V[t][p], vkq = V[t][qq];
-                        V[t][p] = c * vkp - s * vkq;
-                        V[t][qq] = s * vkp + c * vkq;
-                    }
-                    __syncthreads();
                 }
+                __syncthreads();
+                const int k = (int)t / 9, e = (int)t - 9 * k;  // 36 lanes: plane k, row / column e
+                const bool act = t < 36 && s_on[k < 4 ? k : 0];
+                int p = 0, qq = 0;
+                double c = 0.0, sn = 0.0;
+                if (t < 36) {
+                    p = kJacobiRounds[r][k][0];
+                    qq = kJacobiRounds[r][k][1];
+                    c = s_cs[k][0];
+                    sn = s_cs[k][1];
+                }
+                if (act) {  // columns p, q of row e; V likewise
+                    const double aip = A[e][p], aiq = A[e][qq];
+                    A[e][p] = c * aip - sn * aiq;
+                    A[e][qq] = sn * aip + c * aiq;
+                    const double vip = V[e][p], viq = V[e][qq];
+                    V[e][p] = c * vip - sn * viq;
+                    V[e][qq] = sn * vip + c * viq;
+                }
+                __syncthreads();
+                if (act) {  // rows p, q at column e
+                    const double apj = A[p][e], aqj = A[qq][e];
+                    A[p][e] = c * apj - sn * aqj;
+                    A[qq][e] = sn * apj + c * aqj;
+                }
+                __syncthreads();
             }
         }
         if (t == 0) {
