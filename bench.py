@@ -267,6 +267,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("USAC_BENCH_SAME_DEVICE"):  # rehearsal of the N > 1 path on a 1-GPU box
+        local_rank = 0
     _DEV = local_rank
     import torch  # noqa: F401  (torch.distributed rendezvous; loads the process's HIP runtime first)
     import torch.distributed as dist
@@ -294,10 +296,28 @@ def main():
         if args.sampler == "prosac":  # points are quality-sorted (synthetic generator)
             c.set_device_sampler(usac.SAMPLER.Prosac)
     ctx = ctxs[0]
-    if world > 1:
+    exchange = "none"
+    if world > 1:  # the per-batch best-record exchange: RCCL all-gather on the context stream
         uid = [usac.Context.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        ctx.comm_init(world, rank, uid[0])
+        try:
+            ctx.comm_init(world, rank, uid[0])
+            exchange = "rccl_allgather"
+        except usac.UsacError as e:  # keep the scaling run alive: the 56-byte record over gloo
+            print("bench: RCCL init failed (%s); exchanging records over gloo" % e, file=sys.stderr)
+            exchange = "gloo_allgather"
+        ok = torch.tensor([1 if exchange == "rccl_allgather" else 0])
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok) == 0:
+            exchange = "gloo_allgather"
+
+    def allgather(rec):
+        if exchange == "rccl_allgather":
+            return ctx.allgather_record(rec)
+        buf = torch.frombuffer(bytearray(bytes(rec)), dtype=torch.uint8)
+        out = [torch.zeros_like(buf) for _ in range(world)]
+        dist.all_gather(out, buf)
+        return [usac.Record.from_buffer_copy(bytes(o.numpy().tobytes())) for o in out]
     B = args.batch
     if args.sprt:
         for c in ctxs:
@@ -325,7 +345,7 @@ def main():
         best = c.fetch_best()
         t = c.last_timings()
         if world > 1:
-            best = usac.merge_records(ctx.allgather_record(best))
+            best = usac.merge_records(allgather(best))
         return best, t
 
     def run(first_step, count, sink):
@@ -421,7 +441,7 @@ def main():
                        "sampler": args.sampler,
                        "n_points": n, "batch_per_gpu": B, "threshold": args.threshold,
                        "score_chunks": args.chunks, "batches_in_flight": P,
-                       "parallelism": "hypothesis-sharded x%d" % world},
+                       "parallelism": "hypothesis-sharded x%d" % world, "exchange": exchange},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
                          "traffic_unit": "bytes/launch", "traffic_source": traffic[1] if traffic else None,
