@@ -182,7 +182,7 @@ int usac_sync(usac_ctx *ctx);
  * context stream: [0] whole batch, [1] score kernel, [2] solve kernel (ms). */
 int usac_last_timings(usac_ctx *ctx, float *ms3);
 /* Score-kernel split factor (point chunks per hypothesis tile, 1 = exact sequential sums):
- * 1, 2, 4, 8; any of 1..128 for the fundamental / essential estimators (their chunks are
+ * 1, 2, 4, 8, 16; any of 1..128 for the fundamental / essential estimators (their chunks are
  * separate workgroups, combined in chunk order; default 96). */
 int usac_set_score_chunks(usac_ctx *ctx, int chunks);
 /* Homography score kernel: 0 = guard-band fast path with the hypothesis pre-sort (default),

@@ -594,6 +594,7 @@ hipError_t launch_score_h(hipStream_t st, int chunks, const float4 *pts, uint32_
         case 2: hipLaunchKernelGGL(k_score_h<2>, grid, dim3(128), 0, st, pts, n, models, B, thr, counts, sums); break;
         case 4: hipLaunchKernelGGL(k_score_h<4>, grid, dim3(256), 0, st, pts, n, models, B, thr, counts, sums); break;
         case 8: hipLaunchKernelGGL(k_score_h<8>, grid, dim3(512), 0, st, pts, n, models, B, thr, counts, sums); break;
+        case 16: hipLaunchKernelGGL(k_score_h<16>, grid, dim3(1024), 0, st, pts, n, models, B, thr, counts, sums); break;
         default: return hipErrorInvalidValue;
     }
     return LAUNCH_CHECK();
@@ -622,6 +623,7 @@ hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const flo
             case 2: SHF(2, true); break;
             case 4: SHF(4, true); break;
             case 8: SHF(8, true); break;
+            case 16: SHF(16, true); break;
             default: return hipErrorInvalidValue;
         }
     } else {
@@ -630,6 +632,7 @@ hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const flo
             case 2: SHF(2, false); break;
             case 4: SHF(4, false); break;
             case 8: SHF(8, false); break;
+            case 16: SHF(16, false); break;
             default: return hipErrorInvalidValue;
         }
     }
@@ -681,6 +684,7 @@ hipError_t launch_score_line(hipStream_t st, int chunks, const float2 *pts, uint
         case 2: hipLaunchKernelGGL(k_score_line<2>, grid, dim3(128), 0, st, pts, n, models, B, thr, counts, sums); break;
         case 4: hipLaunchKernelGGL(k_score_line<4>, grid, dim3(256), 0, st, pts, n, models, B, thr, counts, sums); break;
         case 8: hipLaunchKernelGGL(k_score_line<8>, grid, dim3(512), 0, st, pts, n, models, B, thr, counts, sums); break;
+        case 16: hipLaunchKernelGGL(k_score_line<16>, grid, dim3(1024), 0, st, pts, n, models, B, thr, counts, sums); break;
         default: return hipErrorInvalidValue;
     }
     return LAUNCH_CHECK();

@@ -235,6 +235,17 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
                                    c->counts.as<int32_t>(), c->sums.as<float>());
 }
 
+// point chunks for the loop's batches (counts only -- the sums the replay reads are exact,
+// exact_sums): lanes-over-hypotheses kernels need ~4 waves per SIMD, and the loop's batches
+// are small (<= 8192 samples, often max_iterations), so H / line split the points finer
+int loop_chunks(const usac_ctx *c, uint32_t B) {
+    if (listed(c)) return c->chunks;
+    const uint32_t tiles = (B + 63) / 64;
+    int ch = c->chunks;
+    while (ch < 16 && tiles * (uint32_t)ch < 4096u) ch *= 2;
+    return ch;
+}
+
 // exact single-model inliers into c->inl_idx / inl_cnt / inl_sum (device)
 hipError_t enqueue_inliers(usac_ctx *c, const float *model_dev, float thr) {
     hipError_t e = c->inl_scratch.reserve(usac::inliers_scratch_bytes(c->n, 1));
@@ -906,7 +917,8 @@ int usac_set_dlt_mode(usac_ctx *c, int mode) {
 
 int usac_set_score_chunks(usac_ctx *c, int chunks) {
     if (!c) return USAC_ERR_ARG;
-    const bool ok = listed(c) ? (chunks >= 1 && chunks <= 128) : (chunks == 1 || chunks == 2 || chunks == 4 || chunks == 8);
+    const bool ok = listed(c) ? (chunks >= 1 && chunks <= 128)
+                              : (chunks == 1 || chunks == 2 || chunks == 4 || chunks == 8 || chunks == 16);
     if (!ok) return USAC_ERR_ARG;
     c->chunks = chunks;
     return USAC_OK;
@@ -1424,7 +1436,7 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
                                               listed(c) ? c->list_n.as<uint32_t>() : nullptr, (uint32_t)S, thr,
                                               c->masks.as<uint32_t>(), (uint32_t)S));
         } else {  // exact counts from the fast multi-chunk scorer; exact sums below, where needed
-            HIP_TRY(c, enqueue_score(c, B, thr, c->chunks));
+            HIP_TRY(c, enqueue_score(c, B, thr, loop_chunks(c, B)));
             HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
         }
         for (int k = 0; k < ncomp(c); k++)
