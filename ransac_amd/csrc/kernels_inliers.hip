@@ -147,28 +147,39 @@ __global__ __launch_bounds__(kInlBlock) void k_inl_compact(const void *__restric
     }
 }
 
-// the reference's sequential fp32 sum in point order (quality.hpp:85): 256 threads stage
-// 4096-residual chunks in LDS with coalesced loads; lane 0 adds them in order (one
-// dependent add per inlier -- the only inherently serial part).  One workgroup per model.
-constexpr uint32_t kSumChunk = 4096;
+// the reference's sequential fp32 sum in point order (quality.hpp:85), one workgroup per
+// model: lane 0 adds the residuals of one 2048-entry LDS chunk in order (one dependent add
+// per inlier -- the only inherently serial part) while waves 1-3 stage the next chunk into
+// the other buffer with coalesced loads; one barrier per chunk.
+constexpr uint32_t kSumChunk = 2048;
 
 __global__ __launch_bounds__(256) void k_inl_sum(const uint32_t *__restrict__ scratch, uint32_t n_pts,
                                                  const uint32_t *__restrict__ slots,
                                                  const int32_t *__restrict__ totals, float *__restrict__ sums) {
-    __shared__ __attribute__((aligned(16))) float s_e[kSumChunk];
+    __shared__ __attribute__((aligned(16))) float s_e[2][kSumChunk];
     const uint32_t nb = (n_pts + kInlBlock - 1) / kInlBlock;
     const uint32_t w = inl_slot(slots, blockIdx.x);
     const float *errs = reinterpret_cast<const float *>(scratch + w * inl_stride(n_pts) + ((nb + 63) & ~63u));
     const uint32_t n = (uint32_t)totals[w];
     const uint32_t t = threadIdx.x;
+    const bool loader = t >= 64;
+    const uint32_t lt = t - 64;
+    const uint32_t nch = (n + kSumChunk - 1) / kSumChunk;
+    auto len = [&](uint32_t c) { return n - c * kSumChunk < kSumChunk ? n - c * kSumChunk : kSumChunk; };
+    if (loader && nch > 0)
+        for (uint32_t i = lt; i < len(0); i += 192) s_e[0][i] = errs[i];
+    __syncthreads();
     float s = 0.f;
-    for (uint32_t c0 = 0; c0 < n; c0 += kSumChunk) {
-        const uint32_t m = n - c0 < kSumChunk ? n - c0 : kSumChunk;
-        for (uint32_t i = t; i < m; i += 256) s_e[i] = errs[c0 + i];
-        __syncthreads();
+    for (uint32_t c = 0; c < nch; c++) {
+        if (loader && c + 1 < nch) {
+            const uint32_t m1 = len(c + 1), base = (c + 1) * kSumChunk;
+            for (uint32_t i = lt; i < m1; i += 192) s_e[(c + 1) & 1][i] = errs[base + i];
+        }
         if (t == 0) {
             // 16 residuals in registers, the next 16 in flight from LDS
-            const float4 *v = reinterpret_cast<const float4 *>(s_e);
+            const uint32_t m = len(c);
+            const float *e = s_e[c & 1];
+            const float4 *v = reinterpret_cast<const float4 *>(e);
             uint32_t k = 0;
             if (m >= 16) {
                 float4 c0 = v[0], c1 = v[1], c2 = v[2], c3 = v[3];
@@ -187,7 +198,7 @@ __global__ __launch_bounds__(256) void k_inl_sum(const uint32_t *__restrict__ sc
                 s += c3.x; s += c3.y; s += c3.z; s += c3.w;
                 k += 16;
             }
-            for (; k < m; k++) s += s_e[k];
+            for (; k < m; k++) s += e[k];
         }
         __syncthreads();
     }

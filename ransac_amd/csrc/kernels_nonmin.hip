@@ -44,88 +44,108 @@ __global__ __launch_bounds__(256) void k_gather(const P *__restrict__ pts, const
 
 // normalizing transformation: lanes 0..3 = the four coordinate means, lanes 0..1 = the
 // two distance sums (each a sequential fp32 chain in point order, as the reference sums);
-// then every lane normalises a strided share of the points.  The chains are latency-bound,
-// so the whole workgroup stages 2048-point chunks in LDS with coalesced loads (and computes
-// the distance terms in parallel) and the chain lanes add from LDS.
+// then every lane normalises a strided share of the points.  The chains are latency-bound:
+// waves 1-3 stage the NEXT 1024-point chunk into LDS (coalesced loads; for the distance pass
+// they also compute its sqrt terms) while lanes of wave 0 add the current chunk from the
+// other buffer -- one barrier per chunk, the staging hidden behind the chain.
 // ws layout (floats): [0..8] T1, [9..17] T2.
-constexpr uint32_t kNormChunk = 2048;
+constexpr uint32_t kNormChunk = 1024;
+
+__device__ __forceinline__ float chain_add_f32(float acc, const float *f, uint32_t m) {
+    // 16 values in registers, the next 16 in flight from LDS (stride 4 floats)
+    uint32_t k = 0;
+    if (m >= 16) {
+        float c[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) c[u] = f[4 * u];
+        for (; k + 32 <= m; k += 16) {
+            float nx[16];
+#pragma unroll
+            for (int u = 0; u < 16; u++) nx[u] = f[4 * (k + 16 + u)];
+#pragma unroll
+            for (int u = 0; u < 16; u++) acc += c[u];
+#pragma unroll
+            for (int u = 0; u < 16; u++) c[u] = nx[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++) acc += c[u];
+        k += 16;
+    }
+    for (; k < m; k++) acc += f[4 * k];
+    return acc;
+}
+
+// d = (float)((double)d + s_k): the reference's float += double (sqrt of a float in C)
+__device__ __forceinline__ float chain_add_f64(float d, const double *sq, uint32_t m) {
+    uint32_t k = 0;
+    if (m >= 16) {
+        double c[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) c[u] = sq[u];
+        for (; k + 32 <= m; k += 16) {
+            double nx[16];
+#pragma unroll
+            for (int u = 0; u < 16; u++) nx[u] = sq[k + 16 + u];
+#pragma unroll
+            for (int u = 0; u < 16; u++) d = (float)((double)d + c[u]);
+#pragma unroll
+            for (int u = 0; u < 16; u++) c[u] = nx[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++) d = (float)((double)d + c[u]);
+        k += 16;
+    }
+    for (; k < m; k++) d = (float)((double)d + sq[k]);
+    return d;
+}
 
 __global__ __launch_bounds__(256) void k_normalize(float4 *__restrict__ q_all, size_t q_stride,
                                                    const uint32_t *__restrict__ ns, uint32_t n1, float *ws_all) {
-    __shared__ float4 s_pts[kNormChunk];
+    __shared__ float4 s_pts[2][kNormChunk];
+    __shared__ double s_sq[2][2][kNormChunk];
+    __shared__ float s_mean[4];
+    __shared__ float s_scale[2];
     float4 *q = q_all + blockIdx.x * q_stride;
     const uint32_t n = ns ? ns[blockIdx.x] : n1;
     float *ws = ws_all + 18 * blockIdx.x;
-    __shared__ double s_sq[2][kNormChunk];
-    __shared__ float s_mean[4];
-    __shared__ float s_scale[2];
     const uint32_t t = threadIdx.x;
+    const bool loader = t >= 64;
+    const uint32_t lt = t - 64;  // loader index, 192 loaders
+    const uint32_t nch = (n + kNormChunk - 1) / kNormChunk;
+    auto chunk_len = [&](uint32_t c) { return n - c * kNormChunk < kNormChunk ? n - c * kNormChunk : kNormChunk; };
+    // means
+    if (loader && nch > 0)
+        for (uint32_t i = lt; i < chunk_len(0); i += 192) s_pts[0][i] = q[i];
+    __syncthreads();
     float acc = 0.f;
-    for (uint32_t c0 = 0; c0 < n; c0 += kNormChunk) {
-        const uint32_t m = n - c0 < kNormChunk ? n - c0 : kNormChunk;
-        for (uint32_t i = t; i < m; i += 256) s_pts[i] = q[c0 + i];
-        __syncthreads();
-        if (t < 4) {
-            // 16 points in registers, the next 16 in flight from LDS
-            const float *f = reinterpret_cast<const float *>(s_pts) + t;
-            uint32_t k = 0;
-            if (m >= 16) {
-                float c[16];
-#pragma unroll
-                for (int u = 0; u < 16; u++) c[u] = f[4 * u];
-                for (; k + 32 <= m; k += 16) {
-                    float nx[16];
-#pragma unroll
-                    for (int u = 0; u < 16; u++) nx[u] = f[4 * (k + 16 + u)];
-#pragma unroll
-                    for (int u = 0; u < 16; u++) acc += c[u];
-#pragma unroll
-                    for (int u = 0; u < 16; u++) c[u] = nx[u];
-                }
-#pragma unroll
-                for (int u = 0; u < 16; u++) acc += c[u];
-                k += 16;
-            }
-            for (; k < m; k++) acc += f[4 * k];
+    for (uint32_t c = 0; c < nch; c++) {
+        if (loader && c + 1 < nch) {
+            const uint32_t m1 = chunk_len(c + 1), base = (c + 1) * kNormChunk;
+            for (uint32_t i = lt; i < m1; i += 192) s_pts[(c + 1) & 1][i] = q[base + i];
         }
+        if (t < 4) acc = chain_add_f32(acc, reinterpret_cast<const float *>(s_pts[c & 1]) + t, chunk_len(c));
         __syncthreads();
     }
     if (t < 4) s_mean[t] = acc / (float)n;
     __syncthreads();
     const float mx1 = s_mean[0], my1 = s_mean[1], mx2 = s_mean[2], my2 = s_mean[3];
-    float d = 0.f;
-    for (uint32_t c0 = 0; c0 < n; c0 += kNormChunk) {
-        const uint32_t m = n - c0 < kNormChunk ? n - c0 : kNormChunk;
-        for (uint32_t i = t; i < m; i += 256) {
-            const float4 p = q[c0 + i];
+    // average distances
+    auto stage_sq = [&](uint32_t c) {
+        const uint32_t m = chunk_len(c), base = c * kNormChunk;
+        for (uint32_t i = lt; i < m; i += 192) {
+            const float4 p = q[base + i];
             const float xm1 = p.x - mx1, ym1 = p.y - my1;
             const float xm2 = p.z - mx2, ym2 = p.w - my2;
-            s_sq[0][i] = sqrt((double)(xm1 * xm1 + ym1 * ym1));
-            s_sq[1][i] = sqrt((double)(xm2 * xm2 + ym2 * ym2));
+            s_sq[c & 1][0][i] = sqrt((double)(xm1 * xm1 + ym1 * ym1));
+            s_sq[c & 1][1][i] = sqrt((double)(xm2 * xm2 + ym2 * ym2));
         }
-        __syncthreads();
-        if (t < 2) {
-            const double *sq = s_sq[t];
-            uint32_t k = 0;
-            if (m >= 16) {
-                double c[16];
-#pragma unroll
-                for (int u = 0; u < 16; u++) c[u] = sq[u];
-                for (; k + 32 <= m; k += 16) {
-                    double nx[16];
-#pragma unroll
-                    for (int u = 0; u < 16; u++) nx[u] = sq[k + 16 + u];
-#pragma unroll
-                    for (int u = 0; u < 16; u++) d = (float)((double)d + c[u]);
-#pragma unroll
-                    for (int u = 0; u < 16; u++) c[u] = nx[u];
-                }
-#pragma unroll
-                for (int u = 0; u < 16; u++) d = (float)((double)d + c[u]);
-                k += 16;
-            }
-            for (; k < m; k++) d = (float)((double)d + sq[k]);
-        }
+    };
+    if (loader && nch > 0) stage_sq(0);
+    __syncthreads();
+    float d = 0.f;
+    for (uint32_t c = 0; c < nch; c++) {
+        if (loader && c + 1 < nch) stage_sq(c + 1);
+        if (t < 2) d = chain_add_f64(d, s_sq[c & 1][t], chunk_len(c));
         __syncthreads();
     }
     if (t < 2) s_scale[t] = (float)(M_SQRT2 / (double)(d / (float)n));
