@@ -375,10 +375,14 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_hf(const float4 *__restri
 constexpr uint32_t kPresortGroups = 32;  // 128 points
 constexpr int kPresortHits = 3;
 
-__global__ __launch_bounds__(64) void k_presort_h(const float4 *__restrict__ rec, uint32_t n,
-                                                  const float *__restrict__ models, uint32_t B, float thr,
-                                                  uint32_t *__restrict__ perm, uint32_t *__restrict__ ends) {
-    const uint32_t lane = threadIdx.x;
+constexpr int kPresortWaves = 4;  // waves per 64 hypotheses, each on kPresortGroups / 4 groups
+
+__global__ __launch_bounds__(64 * kPresortWaves) void k_presort_h(const float4 *__restrict__ rec, uint32_t n,
+                                                                  const float *__restrict__ models, uint32_t B,
+                                                                  float thr, uint32_t *__restrict__ perm,
+                                                                  uint32_t *__restrict__ ends) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t h = blockIdx.x * 64 + lane;
     const uint32_t hc = h < B ? h : B - 1;
     float m[9];
@@ -387,8 +391,10 @@ __global__ __launch_bounds__(64) void k_presort_h(const float4 *__restrict__ rec
     const float T2 = 4.0f * thr * thr;  // forward distance < 2 thr
     const uint32_t ngroups = (n + 3) / 4;
     const uint32_t g1 = ngroups < kPresortGroups ? ngroups : kPresortGroups;
+    constexpr uint32_t per = kPresortGroups / kPresortWaves;
+    const uint32_t gb = wave * per < g1 ? wave * per : g1, ge = gb + per < g1 ? gb + per : g1;
     int hits = 0;
-    for (uint32_t g = 0; g < g1; g++) {
+    for (uint32_t g = gb; g < ge; g++) {
         const float *p = reinterpret_cast<const float *>(rec + 8 * (size_t)g);
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -401,6 +407,12 @@ __global__ __launch_bounds__(64) void k_presort_h(const float4 *__restrict__ rec
             hits += __builtin_fmaf(dx, dx, dy * dy) < T2 ? 1 : 0;
         }
     }
+    __shared__ int s_hits[kPresortWaves][64];
+    s_hits[wave][lane] = hits;
+    __syncthreads();
+    if (wave != 0) return;
+#pragma unroll
+    for (int w = 1; w < kPresortWaves; w++) hits += s_hits[w][lane];
     const bool valid = h < B;
     const bool good = valid && hits >= kPresortHits;
     const uint64_t bg = __ballot(good), bb = __ballot(valid && !good);
@@ -613,7 +625,7 @@ hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const flo
         uint32_t *ends = perm + B;
         hipError_t e = hipMemsetAsync(ends, 0, 2 * sizeof(uint32_t), st);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_presort_h, grid, dim3(64), 0, st, rec, n, models, B, thr, perm, ends);
+        hipLaunchKernelGGL(k_presort_h, grid, dim3(64 * kPresortWaves), 0, st, rec, n, models, B, thr, perm, ends);
     }
 #define SHF(C, E) \
     hipLaunchKernelGGL((k_score_hf<C, E>), grid, dim3(64 * C), 0, st, rec, n, ext, models, B, thr, perm, counts, sums)

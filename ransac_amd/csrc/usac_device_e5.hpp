@@ -422,12 +422,15 @@ __device__ __forceinline__ double poly_eval_t(const double (&c)[11], double x) {
 }
 
 // Per-lane level arrays live in LDS (the caller's 64-lane block, stride 64 doubles):
-// E[0..G] the interval ends, FE[0..G] p at the ends, NX[0..G) the level's output points.
+// E[0..G] the interval ends, FE[0..G] p at the ends.  The level's output points overwrite
+// E in place: output k starts as the filler E[k] (the interval's left end) and a refined
+// interval k stores its root into E[k] when it completes -- intervals complete in
+// ascending order and interval k+1 only reads E[k+1], E[k+2], so no later read sees it.
 // The flat loop picks a new interval's ends with dynamically indexed LDS reads -- one
 // ds_read each, where register arrays would cost G selects per value on every trip on
 // which some lane starts an interval (nearly every trip).
 struct RootsLds {
-    double *E, *FE, *NX;  // already offset by the lane; element k at [64 k]
+    double *E, *FE;  // already offset by the lane; element k at [64 k]
 };
 
 template <int G>
@@ -446,7 +449,7 @@ __device__ __forceinline__ void roots_level(const double (&a)[11], double R, con
     double e[G + 1];
     e[0] = -R;
 #pragma unroll
-    for (int k = 1; k < G; k++) e[k] = L.NX[64 * (k - 1)];
+    for (int k = 1; k < G; k++) e[k] = L.E[64 * (k - 1)];
     e[G] = R;
     uint32_t todo = 0;
     double fprev = poly_eval_t<G>(c, e[0]);
@@ -457,7 +460,6 @@ __device__ __forceinline__ void roots_level(const double (&a)[11], double R, con
         const double fk = poly_eval_t<G>(c, e[k + 1]);
         L.E[64 * (k + 1)] = e[k + 1];
         L.FE[64 * (k + 1)] = fk;
-        L.NX[64 * k] = e[k];
         if (e[k + 1] > e[k] && ((fprev < 0.0) != (fk < 0.0))) todo |= 1u << k;
         fprev = fk;
     }
@@ -524,7 +526,7 @@ __device__ __forceinline__ void roots_level(const double (&a)[11], double R, con
             }
         }
         if (done) {
-            L.NX[64 * k] = res;
+            L.E[64 * k] = res;
             todo &= todo - 1;
             fresh = true;
         }
@@ -532,7 +534,7 @@ __device__ __forceinline__ void roots_level(const double (&a)[11], double R, con
     if constexpr (G < 10) roots_level<G + 1>(a, R, L, found);
 }
 
-// a[10] != 0 required; root k (ascending) is L.NX[64 k] where bit k of found
+// a[10] != 0 required; root k (ascending) is L.E[64 k] where bit k of found
 __device__ __forceinline__ void real_roots10(const double (&a)[11], const RootsLds &L, uint32_t &found) {
     double r = 1.0;
     const double an = fabs(a[10]);
