@@ -127,11 +127,10 @@ def parity_check(usac, kind, pts, thr, dlt_mode):
             "scores_bit_equal": bool((s.view(np.int32) == osum.view(np.int32)).all())}
 
 
-def measured_traffic(kernel_prefix, n_points, batch):
-    """HBM bytes per launch of `kernel_prefix` from the committed rocprofv3 PMC summary
-    (profiles/<round>_summary.json, made by tools/profile.sh + tools/summarize_profile.py:
-    FETCH_SIZE x 1024 x 2 (gfx950 half-count correction) + WRITE_SIZE x 1024), only when
-    that profile ran the same workload shape; else None."""
+def _profile_entry(kernel_prefix, n_points, batch):
+    """(summary entry, source) of `kernel_prefix` in the newest committed rocprofv3 summary
+    (profiles/<round>_summary.json, made by tools/profile.sh + tools/summarize_profile.py)
+    that ran the same workload shape; else None."""
     import glob
 
     best = None
@@ -144,9 +143,38 @@ def measured_traffic(kernel_prefix, n_points, batch):
         if shape and (shape.get("n_points") != n_points or shape.get("batch") != batch):
             continue
         for k, v in d.get("kernels", {}).items():
-            if k.replace(" ", "").startswith(kernel_prefix.replace(" ", "")) and "hbm_bytes_per_launch" in v:
-                best = (v["hbm_bytes_per_launch"], os.path.relpath(f, ROOT))
+            if k.replace(" ", "").startswith(kernel_prefix.replace(" ", "")):
+                best = (v, os.path.relpath(f, ROOT))
     return best
+
+
+def measured_traffic(kernel_prefix, n_points, batch):
+    """HBM bytes per launch of `kernel_prefix` from the committed PMC summary: FETCH_SIZE x
+    1024 x 2 (gfx950 half-count correction) + WRITE_SIZE x 1024; else None."""
+    e = _profile_entry(kernel_prefix, n_points, batch)
+    if e is None or "hbm_bytes_per_launch" not in e[0]:
+        return None
+    return e[0]["hbm_bytes_per_launch"], e[1]
+
+
+# VALU issue peak: 1024 SIMDs, one wave64 VALU instruction per 2 cycles each at 2.4 GHz
+# (MI355X_MICROARCH.md, wave scheduling); a v_pk_fma_f32 counts as one instruction here
+# although it takes two issue slots (tools/ubench/valu_rate.hip)
+VALU_PEAK_INSTR_S = 1024 * 2.4e9 / 2
+
+
+def measured_valu(kernel_prefix, n_points, batch, kernel_ms):
+    """VALU-issue roofline of the score kernel: SQ_INSTS_VALU per launch (committed PMC
+    summary) / the kernel time measured in this run, against VALU_PEAK_INSTR_S."""
+    e = _profile_entry(kernel_prefix, n_points, batch)
+    if e is None or not kernel_ms:
+        return None
+    n_instr = e[0].get("pmc", {}).get("SQ_INSTS_VALU")
+    if not n_instr:
+        return None
+    rate = n_instr / (kernel_ms * 1e-3)
+    return {"instructions_per_launch": n_instr, "achieved": rate, "peak": VALU_PEAK_INSTR_S,
+            "unit": "wave-instr/s", "frac": rate / VALU_PEAK_INSTR_S, "source": e[1]}
 
 
 _DEV = 0
@@ -408,6 +436,7 @@ def main():
         achieved = bytes_per_hyp * B / (avg_score_ms * 1e-3) / 1e9
         kname = ("void usac::k_score_f2<%d>" if (fund or ess) else "void usac::k_score_hf<%d, false>") % args.chunks
         traffic = measured_traffic(kname, n, B) if not (fund or ess or args.sprt) else None
+        valu = measured_valu(kname, n, B, avg_score_ms) if not (fund or ess or args.sprt) else None
         kshort = ("k_sprt_head/tail<%d>" % (3 if fund else 4 if ess else 2)) if args.sprt else \
             (("k_score_f2<%d,%s>" % (args.chunks, "E" if ess else "F")) if (fund or ess) else
              ("k_score_hf<%d,false>" % args.chunks))
@@ -457,7 +486,8 @@ def main():
                          "solve_kernel_ms": float(np.mean(solo_solve)),
                          "kernel_ms_in_pipeline": float(np.mean(score_ms)),
                          "solve_kernel_ms_in_pipeline": float(np.mean(solve_ms)),
-                         "batch_device_ms_in_pipeline": float(np.mean(batch_ms))},
+                         "batch_device_ms_in_pipeline": float(np.mean(batch_ms)),
+                         "valu_issue": valu},
             "best": {"inliers": int(best.inliers), "hyp_index": int(best.hyp_index)},
         }
         if world == 1:

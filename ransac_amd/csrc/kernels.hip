@@ -288,7 +288,9 @@ __device__ __forceinline__ void score_group(const HModel &M, float4 X1, float4 Y
     bool k0, k1, k2, k3;
     stage_a_keep2(M, v2f{X1.x, X1.y}, v2f{Y1.x, Y1.y}, v2f{X2.x, X2.y}, v2f{Y2.x, Y2.y}, k0, k1);
     stage_a_keep2(M, v2f{X1.z, X1.w}, v2f{Y1.z, Y1.w}, v2f{X2.z, X2.w}, v2f{Y2.z, Y2.w}, k2, k3);
-    if (__builtin_amdgcn_ballot_w64(k0 | k1 | k2 | k3) == 0) return;
+    // marked unlikely: the stage-B blocks are placed out of line, so the common path falls
+    // through from one group's stage A to the next instead of jumping over them
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(k0 | k1 | k2 | k3) == 0, 1)) return;
     if (k0) stage_b<EXACT_SUM>(M, X1.x, Y1.x, X2.x, Y2.x, bd.x, T, thr, cnt, sum);
     if (k1) stage_b<EXACT_SUM>(M, X1.y, Y1.y, X2.y, Y2.y, bd.y, T, thr, cnt, sum);
     if (k2) stage_b<EXACT_SUM>(M, X1.z, Y1.z, X2.z, Y2.z, bd.z, T, thr, cnt, sum);
