@@ -18,6 +18,7 @@ def _bits(a):
 def _run(usac, oracle, kind, pts, thr, seed=5, max_iters=10000, lo=0, sampler="uniform"):
     okind, est, m = {"H": (oracle.HOMOGRAPHY, usac.ESTIMATOR.Homography, 4),
                      "F": (oracle.FUNDAMENTAL, usac.ESTIMATOR.Fundamental, 7),
+                     "E": (oracle.ESSENTIAL, usac.ESTIMATOR.Essential, 5),
                      "L": (oracle.LINE2D, usac.ESTIMATOR.Line2d, 2)}[kind]
     ref = oracle.ransac_run(okind, pts, thr, 0.95, seed, max_iters=max_iters, lo=lo)
     mdl = usac.Model(thr, m, 0.95, 7, est, usac.SAMPLER.Uniform)
@@ -48,16 +49,22 @@ def _same(ref, r, err):
     assert (out.getInliers() == ref["inlier_idx"]).all()
 
 
-@pytest.mark.parametrize("kind", ["H", "F"])
-def test_nan_rows(usac, oracle, kind):
+def _points(kind, n, ratio, seed):
     if kind == "H":
-        pts, _, _ = synthetic.homography_points(n=2001, inlier_ratio=0.4, seed=3)
-    else:
-        pts, _, _ = synthetic.fundamental_points(n=2001, inlier_ratio=0.4, seed=3, prosac_order=False)
+        return synthetic.homography_points(n=n, inlier_ratio=ratio, seed=seed)[0], 2.0
+    if kind == "F":
+        return synthetic.fundamental_points(n=n, inlier_ratio=ratio, seed=seed, prosac_order=False)[0], 2.0
+    return synthetic.fundamental_points(n=n, inlier_ratio=ratio, seed=seed, normalized=True,
+                                        prosac_order=False)[0], 0.002
+
+
+@pytest.mark.parametrize("kind", ["H", "F", "E"])
+def test_nan_rows(usac, oracle, kind):
+    pts, thr = _points(kind, 2001, 0.4, 3)
     pts = pts.copy()
     rng = np.random.default_rng(1)
     pts[rng.choice(len(pts), 100, replace=False), rng.integers(0, 4, 100)] = np.nan
-    _same(*_run(usac, oracle, kind, pts, 2.0, lo=1))
+    _same(*_run(usac, oracle, kind, pts, thr, lo=1, max_iters=3000))
 
 
 def test_duplicated_points_and_odd_count(usac, oracle):
@@ -70,6 +77,12 @@ def test_duplicated_points_and_odd_count(usac, oracle):
 def test_smallest_sets(usac, oracle, n):
     pts, _, _ = synthetic.homography_points(n=n, inlier_ratio=1.0, seed=n)
     _same(*_run(usac, oracle, "H", pts, 2.0, max_iters=50))
+
+
+@pytest.mark.parametrize("kind,n", [("F", 7), ("F", 8), ("E", 5), ("E", 6)])
+def test_smallest_sets_two_view(usac, oracle, kind, n):
+    pts, thr = _points(kind, n, 1.0, n)
+    _same(*_run(usac, oracle, kind, pts, thr, max_iters=50))
 
 
 def test_one_iteration(usac, oracle):
