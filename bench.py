@@ -33,8 +33,8 @@ def parse():
     ap.add_argument("--estimator", choices=["homography", "fundamental", "essential"], default="homography",
                     help="homography = cfg2 (the BASELINE metric's config); fundamental = cfg3; essential = cfg4 "
                          "(50k correspondences in K^-1-normalised coordinates, threshold 0.002)")
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--points", type=int, default=None, help="default: 10000 (cfg2/cfg3), 50000 (cfg4)")
     ap.add_argument("--threshold", type=float, default=None,
