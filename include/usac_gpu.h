@@ -104,7 +104,8 @@ typedef struct usac_params {
     int32_t cell_size;                /* model.hpp:43 (50): NAPSAC grid cell */
     int32_t neighbors;                /* USAC_NEIGHBORS_* (model.hpp:42): NAPSAC Grid or KNN */
     uint32_t knn;                     /* model.hpp:23 k_nearest_neighbors (NAPSAC KNN / GC, 1..32) */
-    float spatial_coherence_gc;       /* model.hpp:33 (0.1): GC pairwise weight; <= 0 selects 0.1 */
+    float spatial_coherence_gc;       /* model.hpp:33 (0.1): GC pairwise weight, used as given
+                                         (graphcut.hpp:43; 0 = no pairwise term) */
 } usac_params;
 
 /* RansacOutput getters (ransac_output.hpp:57-97) */

@@ -433,3 +433,9 @@ def generate_line2d(seed, noise, inliers, outliers, border_x, border_y):
     lib().orc_generate_line2d(seed, ctypes.c_float(noise), inliers, outliers, border_x, border_y,
                               _p(pts, _f32p), _p(gt, _f32p))
     return pts, gt
+
+
+def set_f8_rank2(on):
+    """Rank-2 enforcement in the 8-point polish (eight_points.cpp:58-68, commented out in the
+    current reference): the revision that produced results/kusvod2/*.csv ran it.  Test-only."""
+    lib().orc_set_f8_rank2(1 if on else 0)

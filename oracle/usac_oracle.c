@@ -719,6 +719,46 @@ static int fundamental_7pt(const orc_est *e, const int *sample, float *models) {
  * n x 9 rows in fp32; thin last row for n <= 8, fp64 normal-matrix smallest
  * eigenvector otherwise (blocked order as the DLT); F = T2^T F T1 (fp64), F /= F33 when
  * |F33| > FLT_EPSILON (:76-99). */
+/* Rank-2 variant of the 8-point polish: the block eight_points.cpp:58-68 keeps commented out
+ * (SVD of F, smallest singular value zeroed, F = U S V^T).  The reference's published kusvod2
+ * statistics (results/kusvod2/ CSVs) and its stored GT F models (exactly rank 2)
+ * come from a revision that ran it; tests/test_reference_statistics.py switches it on to pin
+ * the 7-point / Sampson / graph-cut path against those CSVs.  Off by default (current code). */
+static int g_f8_rank2 = 0;
+void orc_set_f8_rank2(int on) { g_f8_rank2 = on; }
+
+static void row_jacobi_small(double W[][4], int r, int cols, double J[][4]);
+
+/* F = J^T B after the row Jacobi (B = J F, orthogonal rows): zero the smallest-norm row of B,
+ * i.e. the smallest singular value, and rebuild (fp64). */
+static void rank2_project(double v[9]) {
+    double B[4][4], J[4][4];
+    memset(B, 0, sizeof(B));
+    memset(J, 0, sizeof(J));
+    for (int i = 0; i < 3; i++) {
+        for (int k = 0; k < 3; k++) B[i][k] = v[3 * i + k];
+        J[i][i] = 1.0;
+    }
+    row_jacobi_small(B, 3, 3, J);
+    int mi = 0;
+    double nmin = 0.0;
+    for (int i = 0; i < 3; i++) {
+        double a = 0.0;
+        for (int k = 0; k < 3; k++) a += B[i][k] * B[i][k];
+        if (i == 0 || a < nmin) {
+            nmin = a;
+            mi = i;
+        }
+    }
+    for (int k = 0; k < 3; k++) B[mi][k] = 0.0;
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) {
+            double a = 0.0;
+            for (int i = 0; i < 3; i++) a += J[i][r] * B[i][c];
+            v[3 * r + c] = a;
+        }
+}
+
 static int fundamental_8pt(const orc_est *e, const int *sample, unsigned int n, float *F) {
     if (n == 0) return 0;
     float T1[9], T2[9];
@@ -757,6 +797,7 @@ static int fundamental_8pt(const orc_est *e, const int *sample, unsigned int n, 
         sym_eig_min(AtA, v);
     }
     free(norm);
+    if (g_f8_rank2) rank2_project(v);
     /* T2^T = [s2 0 0; 0 s2 0; t2_13 t2_23 1] */
     double T2t[9] = {T2[0], 0.0, 0.0, 0.0, T2[4], 0.0, T2[2], T2[5], 1.0};
     double tmp[9], Fd[9];
@@ -2627,7 +2668,7 @@ static void gc_init(orc_gc *C, const orc_config *cfg, unsigned int n, unsigned i
     C->n = n;
     C->limit = 7 * m;
     C->thr = cfg->threshold;
-    C->G.lambda = cfg->spatial_coherence_gc > 0.f ? cfg->spatial_coherence_gc : 0.1f; /* model.hpp:33 */
+    C->G.lambda = cfg->spatial_coherence_gc; /* model.hpp:33 (default 0.1), graphcut.hpp:43 as given */
     C->G.sqr_thr = 2 * cfg->threshold * cfg->threshold;
     C->inl = (int *)malloc(sizeof(int) * (n ? n : 1));
     C->errors = (float *)malloc(sizeof(float) * (n ? n : 1));
@@ -2798,6 +2839,8 @@ int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_
     out->polish_passes = 0;
     out->sprt_histories = sp ? (int)orc_sprt_histories(sp) : 0;
     out->prosac_term_len = pt ? orc_prosac_term_length(pt) : n;
+    if (best_cnt != 0 && use_gc && gc.gc_iters == 0) /* ransac.cpp:149-153: GC set but never ran */
+        gc_run(&gc, e, best_model, &best_cnt, &best_sum);
     out->lo_inner_iters = use_lo ? lo.inner_count : use_gc ? gc.gc_iters : 0;
     out->lo_iterative_iters = use_lo ? lo.iterative_count : use_gc ? gc.labelings : 0;
     memcpy(out->minimal_model, best_model, sizeof(best_model));

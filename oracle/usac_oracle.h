@@ -148,6 +148,8 @@ void orc_napsac_sample(orc_napsac *s, int *sample);
 
 /* Ransac::run with the sampler / SPRT of cfg (PROSAC: points sorted by quality; its
  * mt19937 is seeded with cfg->seed instead of std::random_device). */
+/* test switch: rank-2 enforcement in the 8-point polish (older reference revision) */
+void orc_set_f8_rank2(int on);
 int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_config *cfg, orc_result *out,
                        int *inliers_out, unsigned int *rec_iter, int *rec_count, float *rec_score, int rec_cap);
 

@@ -651,7 +651,8 @@ int exact_sums(usac_ctx *c, float thr, int best_count, const int32_t *hc, const 
 // under the best model; the host turns them into the reference's energies -- unary
 // exp(-(e*e) / (2 thr^2)) (float argument, double exp as the reference's unqualified exp of
 // a float), pairwise terms over the KNN (device usac_knn) or grid neighbour lists, skipping
-// non-submodular / NaN terms, lambda = spatial_coherence_gc 0.1 (model.hpp:33) -- and runs
+// non-submodular / NaN terms, lambda = spatial_coherence_gc as given (model.hpp:33 default 0.1;
+// graphcut.hpp:43 uses it unchanged, 0 = no pairwise term) -- and runs
 // the reference's BK min cut (usac_maxflow.hpp); inliers = SINK nodes.  The <=
 // lo_inner_iterations least-squares fits on 7m-point subsets of the labelling's inliers do
 // not depend on each other (only the comparisons with the best do), so all of them run as
@@ -680,7 +681,7 @@ struct GcLo {
           n(ctx->n),
           limit(7 * ctx->m),
           thr(p->threshold),
-          lambda(p->spatial_coherence_gc > 0.f ? p->spatial_coherence_gc : 0.1f),
+          lambda(p->spatial_coherence_gc),
           sqr_thr(2 * p->threshold * p->threshold),
           knn_tab(knn_table),
           knn(k),
@@ -969,6 +970,14 @@ int usac_score_models(usac_ctx *c, const float *models, uint32_t nm, float thr, 
     int rc = ensure_batch(c, nm);
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
+    // Quality::getNumberInliers never runs the SPRT (quality.hpp:60-101): the throughput SPRT of
+    // usac_set_sprt applies to the hypothesize_* batches only, so it is off for this call.
+    struct SprtOff {
+        usac_ctx *c;
+        bool saved;
+        ~SprtOff() { c->sprt_on = saved; }
+    } sprt_off{c, c->sprt_on};
+    c->sprt_on = false;
     HIP_TRY(c, hipMemcpyAsync(c->hostmodels.p, models, sizeof(float) * 9 * (size_t)nm, hipMemcpyHostToDevice, c->stream));
     if (listed(c)) {
         HIP_TRY(c, usac::launch_prepare_f(c->stream, c->hostmodels.as<float>(), nm, c->models.as<float>()));
@@ -1557,15 +1566,27 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
     out->n_records = nrec;
     out->sprt_histories = sprt ? (int32_t)sprt->histories() : 0;
     out->prosac_term_len = prosac ? pterm->terminationLength() : n;
-    out->lo_inner_iters = lo ? lo->inner_count : gc ? gc->gc_iters : 0;
-    out->lo_iterative_iters = lo ? lo->iterative_count : gc ? gc->labelings : 0;
-    out->lo_rounds = lo ? lo->rounds : gc ? gc->labelings : 0;
-    out->lo_stages = lo ? lo->stages : gc ? gc->stages : 0;
+    auto lo_counters = [&]() {
+        out->lo_inner_iters = lo ? lo->inner_count : gc ? gc->gc_iters : 0;
+        out->lo_iterative_iters = lo ? lo->iterative_count : gc ? gc->labelings : 0;
+        out->lo_rounds = lo ? lo->rounds : gc ? gc->labelings : 0;
+        out->lo_stages = lo ? lo->stages : gc ? gc->stages : 0;
+    };
+    lo_counters();
     memcpy(out->minimal_model, best_model, sizeof(best_model));
     out->minimal_inliers = best.inlier_number;
     if (best.inlier_number == 0) {
         memcpy(out->model, best_model, sizeof(best_model));
         return fail(c, USAC_ERR_NO_MODEL, "best score is 0 (ransac.cpp:143-147)");
+    }
+    if (gc && gc->gc_iters == 0) {  // "Graph Cut lo was set, but did not run, run it" (ransac.cpp:149-153)
+        lap(T_REPLAY);
+        gc->run(best_model, best.inlier_number, best.score);
+        if (gc->rc) return gc->rc;
+        lap(T_LO);
+        lo_counters();
+        memcpy(out->minimal_model, best_model, sizeof(best_model));
+        out->minimal_inliers = best.inlier_number;
     }
 
     lap(T_REPLAY);

@@ -20,7 +20,11 @@ Fixtures are DATA only -- inputs and expected outputs the reference already hold
     DATASET::Kusvod2_SIFT branch of dataset/GetImage.h:56-66) and their GT F
     (<scene>_vpts_model.txt).  The "GT Inl" column of results/kusvod2/*.csv is NOT
     reproducible from these files with the Sampson error at thr 2 (e.g. booksh: published
-    149, F/F^T give 61/4), so it is not a fixture; the scenes serve as real-data inputs.
+    149, F/F^T give 61/4), so it is not a fixture; the scenes serve as real-data inputs;
+  * reference_stats.json  : every per-scene row (averages, standard deviations, medians) and
+    the run settings of the reference's published statistical CSVs the pin tests use
+    (results/line2d/{uniform,napsac,prosac}_*.csv, results/homography/uniform_gc*_Grid_c_sz_50.csv,
+    results/kusvod2/uniform_gc*_Grid_c_sz_50.csv) -- numbers copied from the CSVs, nothing else.
 """
 import csv
 import ctypes
@@ -129,7 +133,50 @@ def kusvod2():
     np.savez_compressed(os.path.join(OUT, "kusvod2_scenes.npz"), **arrays)
 
 
+STAT_FILES = [
+    "line2d/uniform_000.csv", "line2d/uniform_001.csv", "line2d/uniform_010.csv", "line2d/uniform_100.csv",
+    "line2d/napsac_000.csv", "line2d/prosac_000.csv",
+    "homography/uniform_gc_Grid_c_sz_50.csv", "homography/uniform_gc_sprt_Grid_c_sz_50.csv",
+    "kusvod2/uniform_gc_Grid_c_sz_50.csv", "kusvod2/uniform_gc_sprt_Grid_c_sz_50.csv",
+]
+
+
+def _num(v):
+    v = v.strip()
+    try:
+        return float(v.split("/")[0]) if "/" in v else float(v)
+    except ValueError:
+        return v
+
+
+def reference_stats():
+    """tests/golden/reference_stats.json: the rows of the reference's statistical CSVs
+    (written by test/tests.h getStatisticalResults + store_results_*)."""
+    out = {}
+    for rel in STAT_FILES:
+        with open(os.path.join(REF, "results", rel)) as f:
+            rows = list(csv.reader(f))
+        settings, header, scenes = {}, None, {}
+        for row in rows:
+            if not row or not row[0].strip():
+                continue
+            if row[0] == "Filename":
+                header = row
+                continue
+            if header is None:
+                if " = " in row[0]:
+                    k, v = row[0].split(" = ", 1)
+                    settings[k.strip()] = _num(v)
+                continue
+            scenes[row[0]] = {h: _num(v) for h, v in zip(header[1:], row[1:])}
+        out[rel] = {"settings": settings, "scenes": scenes}
+    with open(os.path.join(OUT, "reference_stats.json"), "w") as f:
+        json.dump({"source": "/root/reference/results (reference's published statistics)", "files": out}, f,
+                  indent=1, sort_keys=True)
+
+
 if __name__ == "__main__":
+    reference_stats()
     homography()
     line2d()
     kusvod2()

@@ -1,0 +1,71 @@
+"""The reference's published statistics through the device library (usac_ransac_run): the
+homography graph-cut runs of results/homography/uniform_gc*_Grid_c_sz_50.csv and the line2d
+LO-RANSAC runs of results/line2d/uniform_100.csv, each run identical to the oracle's (the
+CPU pins of tests/test_reference_statistics.py therefore carry over) and the averages within
+the same statistical tolerance of the published ones."""
+import numpy as np
+import pytest
+
+from test_reference_statistics import ERR, INL, SD_ERR, SD_INL, check, gt_error, gt_inliers, inl_floor
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.int32)
+
+
+def _run(usac, pts, est, m, thr, p, seed, **kw):
+    mdl = usac.Model(thr, m, p, kw.pop("knn", 7), est, kw.pop("sampler", usac.SAMPLER.Uniform))
+    mdl.ResetRandomGenerator(False)
+    mdl.setSeed(seed)
+    mdl.setSprt(kw.pop("sprt", False))
+    mdl.lo = kw.pop("lo", usac.LocOpt.NullLO)
+    if "cell_size" in kw:
+        mdl.setCellSize(kw.pop("cell_size"))
+    if "neighbors" in kw:
+        mdl.setNeighborsType(kw.pop("neighbors"))
+    r = usac.Ransac(mdl, pts)
+    r.run()
+    return r.getRansacOutput()
+
+
+@pytest.mark.parametrize("rel", ["homography/uniform_gc_Grid_c_sz_50.csv",
+                                 "homography/uniform_gc_sprt_Grid_c_sz_50.csv"])
+def test_homography_gc_statistics_device(usac, oracle, homography_scenes, rel):
+    runs = 20
+    sprt = "sprt" in rel
+    results = {}
+    for scene, (pts, model, _) in homography_scenes.items():
+        est = oracle.Estimator(oracle.HOMOGRAPHY, pts)
+        gt = gt_inliers(oracle, est, pts, model, 2.0)
+        inl, err = [], []
+        for seed in range(1, runs + 1):
+            out = _run(usac, pts, usac.ESTIMATOR.Homography, 4, 2.0, 0.95, seed, lo=usac.LocOpt.GC,
+                       neighbors=usac.NeighborsSearch.Grid, cell_size=50, sprt=sprt)
+            ref = oracle.ransac_run(oracle.HOMOGRAPHY, pts, 2.0, 0.95, seed, lo=oracle.LO_GC,
+                                    neighbors=oracle.NEIGHBORS_GRID, cell_size=50, sprt=sprt)
+            assert out.getNumberOfMainIterations() == ref["iters"], (scene, seed)
+            assert (_bits(out.getModel()) == _bits(ref["model"])).all(), (scene, seed)
+            assert (out.getInliers() == ref["inlier_idx"]).all(), (scene, seed)
+            inl.append(out.getNumberOfInliers())
+            err.append(gt_error(est, out.getModel(), gt))
+        results[scene] = {INL: inl, ERR: err}
+    pinned = check(rel, results, [(INL, SD_INL), (ERR, SD_ERR)],
+                   {INL: inl_floor, ERR: lambda m: max(0.002, 0.005 * m)})
+    assert len(pinned) >= 21
+
+
+def test_line2d_lo_statistics_device(usac, oracle, line2d_scenes):
+    rel = "line2d/uniform_100.csv"
+    results = {}
+    for name, (pts, _, _) in sorted(line2d_scenes.items()):
+        inl = []
+        for seed in range(1, 11):
+            out = _run(usac, pts, usac.ESTIMATOR.Line2d, 2, 10.0, 0.99, seed, lo=usac.LocOpt.InItLORsc)
+            ref = oracle.ransac_run(oracle.LINE2D, pts, 10.0, 0.99, seed, lo=oracle.LO_INITLORSC)
+            assert out.getNumberOfMainIterations() == ref["iters"], (name, seed)
+            assert (_bits(out.getModel()) == _bits(ref["model"])).all(), (name, seed)
+            inl.append(out.getNumberOfInliers())
+        results[name] = {INL: inl}
+    assert len(check(rel, results, [(INL, SD_INL)], {INL: inl_floor})) == 8
