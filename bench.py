@@ -72,9 +72,29 @@ def parse():
     return args
 
 
+def cpu_info():
+    model = platform.processor() or platform.machine()
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    # the box's CPU share (OMP_NUM_THREADS is set to it there), not the whole machine
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or avail
+    return model, avail, min(avail, share)
+
+
 def cpu_baseline(kind, pts, thr, dlt_mode, seconds):
     """The CPU oracle's reference-style loop (glibc pool sampler, per-hypothesis minimal
-    solve, full sequential score of every model) on one host core, bounded sample."""
+    solve, full sequential score of every model), bounded samples: on one host core (the
+    reference is single-threaded: the ≥10x denominator) and on all the cores the box grants
+    (pthreads over disjoint hypothesis ranges, one estimator each)."""
     from oracle import oracle as O
 
     O.lib()
@@ -86,12 +106,17 @@ def cpu_baseline(kind, pts, thr, dlt_mode, seconds):
     t0 = time.perf_counter()
     O.hypothesis_loop(okind, pts, thr, 2, count, dlt_mode)
     dt = time.perf_counter() - t0
+    model, avail, threads = cpu_info()
+    count_mt = max(100, int(seconds / per * threads / 2))
+    dt_mt, _ = O.hypothesis_loop_mt(okind, pts, thr, 3, count_mt, threads, dlt_mode)
     what = {"fundamental": "7-pt solve+oriented filter+Sampson score",
             "essential": "5-pt solve+cheirality+epipolar-distance score"}.get(kind, "DLT4+inverse+score")
     return {"value": count / dt, "unit": "hypotheses/s", "cores": 1, "kind": "port",
-            "sample": "%d hypotheses of the same workload (N=%d, sample+%s, glibc sampler), "
-                      "%.1f s on 1 core of %s" % (count, len(pts), what, dt,
-                                                  platform.processor() or platform.machine())}
+            "sample": "%d hypotheses of the same workload (N=%d, sample+%s, glibc sampler), %.1f s on 1 core of "
+                      "%s" % (count, len(pts), what, dt, model),
+            "all_cores": {"value": count_mt / dt_mt, "unit": "hypotheses/s", "cores": threads,
+                          "sample": "%d hypotheses, %.1f s on %d threads" % (count_mt, dt_mt, threads)},
+            "cpu_model": model, "nproc": os.cpu_count(), "cpus_available": avail}
 
 
 def parity_check(usac, kind, pts, thr, dlt_mode):
@@ -148,33 +173,47 @@ def _profile_entry(kernel_prefix, n_points, batch):
     return best
 
 
-def measured_traffic(kernel_prefix, n_points, batch):
-    """HBM bytes per launch of `kernel_prefix` from the committed PMC summary: FETCH_SIZE x
-    1024 x 2 (gfx950 half-count correction) + WRITE_SIZE x 1024; else None."""
-    e = _profile_entry(kernel_prefix, n_points, batch)
-    if e is None or "hbm_bytes_per_launch" not in e[0]:
-        return None
-    return e[0]["hbm_bytes_per_launch"], e[1]
+# VALU issue peak: 1024 SIMDs (256 CUs x 4), each issuing one wave64 VALU instruction per 2
+# cycles at 2.4 GHz (MI355X_MICROARCH.md, wave scheduling); a v_pk_fma_f32 occupies two such
+# slots (tools/ubench/valu_rate.hip), which SQ_ACTIVE_INST_VALU (VALU-busy quad-cycles per
+# wave, summed over waves) accounts for and SQ_INSTS_VALU (instructions) does not.
+SIMD_CYCLES_S = 1024 * 2.4e9
+VALU_PEAK_INSTR_S = SIMD_CYCLES_S / 2
 
 
-# VALU issue peak: 1024 SIMDs, one wave64 VALU instruction per 2 cycles each at 2.4 GHz
-# (MI355X_MICROARCH.md, wave scheduling); a v_pk_fma_f32 counts as one instruction here
-# although it takes two issue slots (tools/ubench/valu_rate.hip)
-VALU_PEAK_INSTR_S = 1024 * 2.4e9 / 2
-
-
-def measured_valu(kernel_prefix, n_points, batch, kernel_ms):
-    """VALU-issue roofline of the score kernel: SQ_INSTS_VALU per launch (committed PMC
-    summary) / the kernel time measured in this run, against VALU_PEAK_INSTR_S."""
+def valu_roofline(kernel_prefix, n_points, batch, kernel_ms):
+    """Primary roofline of the score kernel (it is fp32-VALU-issue bound, its point
+    set L2-resident): VALU-busy SIMD-cycles per launch (SQ_ACTIVE_INST_VALU x 4, committed PMC
+    summary of the same workload) / this run's measured kernel time, against 1024 SIMDs x
+    2.4 GHz.  Beside it: the instruction-count form (SQ_INSTS_VALU vs one wave64 instruction per
+    2 cycles, packed FMAs counted once), VALUBusy straight from the PMC pass (clock-free), the
+    wave-cycle split and the counter-measured HBM traffic."""
     e = _profile_entry(kernel_prefix, n_points, batch)
     if e is None or not kernel_ms:
         return None
-    n_instr = e[0].get("pmc", {}).get("SQ_INSTS_VALU")
-    if not n_instr:
-        return None
-    rate = n_instr / (kernel_ms * 1e-3)
-    return {"instructions_per_launch": n_instr, "achieved": rate, "peak": VALU_PEAK_INSTR_S,
-            "unit": "wave-instr/s", "frac": rate / VALU_PEAK_INSTR_S, "source": e[1]}
+    pmc, src = e[0].get("pmc", {}), e[1]
+    t = kernel_ms * 1e-3
+    out = {"bound": "valu", "unit": "SIMD-cycles/s", "peak": SIMD_CYCLES_S, "source": src}
+    act = pmc.get("SQ_ACTIVE_INST_VALU")
+    if act:
+        out["achieved"] = act * 4 / t
+        out["frac"] = out["achieved"] / SIMD_CYCLES_S
+        out["valu_busy_cycles_per_launch"] = act * 4
+        if pmc.get("GRBM_GUI_ACTIVE"):
+            out["valu_busy_pmc"] = act * 4 / 1024 / pmc["GRBM_GUI_ACTIVE"]
+    n_instr = pmc.get("SQ_INSTS_VALU")
+    if n_instr:
+        out["instructions_per_launch"] = n_instr
+        out["instr_issue_frac"] = n_instr / t / VALU_PEAK_INSTR_S
+    if pmc.get("SQ_WAVE_CYCLES"):
+        wc = pmc["SQ_WAVE_CYCLES"]
+        out["wave_cycle_split"] = {k.lower(): pmc[k] / wc for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+                                                                    "SQ_ACTIVE_INST_ANY") if k in pmc}
+    if "hbm_bytes_per_launch" in e[0]:
+        hb = e[0]["hbm_bytes_per_launch"]
+        out["hbm"] = {"traffic_bytes_per_launch": hb, "achieved_gbs": hb / t / 1e9, "peak_gbs": HBM_PEAK_GBS,
+                      "frac": hb / t / 1e9 / HBM_PEAK_GBS}
+    return out
 
 
 _DEV = 0
@@ -246,6 +285,14 @@ def cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank):
     out = one_run(args.seed)
     ref = O.ransac_run(O.HOMOGRAPHY, pts, args.threshold, 0.95, args.seed, sampler=O.SAMPLER_NAPSAC, sprt=False,
                        lo=args.lo, max_iters=max_iters)
+    roof = valu_roofline("void usac::k_score_hf<8, false>", n, B, score_ms) or {
+        "bound": "valu", "achieved": None, "peak": SIMD_CYCLES_S, "unit": "SIMD-cycles/s", "frac": None}
+    roof.update({"traffic": roof.get("hbm", {}).get("traffic_bytes_per_launch"), "kernel": "k_score_hf<8,false>",
+                 "kernel_ms": score_ms, "hypotheses_per_launch": B,
+                 "algorithmic_bytes_per_hypothesis": bytes_per_hyp, "algorithmic_equiv_gbs": achieved,
+                 "note": "score kernel of one %d-hypothesis batch at N = %d (the loop's batched verify), VALU-issue "
+                         "roofline as the cfg2 line; a run is dominated by LO and the host replay, see DESIGN.md"
+                         % (B, n)})
     parity = {"runs": 1, "iterations_equal": out.getNumberOfMainIterations() == ref["iters"],
               "lo_iters_equal": out.getLOIters() == ref["lo_inner_iters"],
               "model_bit_equal": bool((np.asarray(out.getModel(), np.float32).view(np.int32) ==
@@ -262,12 +309,7 @@ def cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank):
                                ("InItLORsc" if args.lo == 1 else "InItFLORsc", n),
                    "n_points": n, "threshold": args.threshold, "max_iterations": max_iters,
                    "hypotheses_per_gpu": iters / world, "parallelism": "replicas x%d" % world},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_score_hf<8,false>",
-                     "kernel_ms": score_ms, "hypotheses_per_launch": B,
-                     "algorithmic_bytes_per_hypothesis": bytes_per_hyp,
-                     "note": "score kernel of one %d-hypothesis batch at N = %d (the loop's batched verify); a run "
-                             "is dominated by LO and the host replay, see DESIGN.md" % (B, n)},
+        "roofline": roof,
         "parity": parity,
         "run_stats": {k: int(out.raw[k]) for k in ("batches", "n_records", "lo_rounds", "lo_stages", "sum_models",
                                                      "lo_iterative_iters", "polish_passes")},
@@ -287,6 +329,27 @@ def cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank):
                                 "sample": "%d full runs (%d hypotheses, NAPSAC + LO, N=%d), %.1f s on 1 core of %s" %
                                           (runs, it, n, dt, platform.processor() or platform.machine())}
     print(json.dumps(line))
+
+
+def init_exchange(ctx, usac, dist, torch, world, rank, uid):
+    """RCCL communicator for the per-batch record exchange.  Ranks on distinct GPUs must get
+    one: a failure ends the run (exit 3) instead of reporting a scaling line without RCCL.
+    Only the USAC_BENCH_SAME_DEVICE rehearsal (several ranks on one GPU, which RCCL refuses)
+    falls back to exchanging the 56-byte records over gloo."""
+    try:
+        ctx.comm_init(world, rank, uid)
+        ok = 1
+    except usac.UsacError as e:
+        print("bench: RCCL init failed on rank %d (%s)" % (rank, e), file=sys.stderr)
+        ok = 0
+    t = torch.tensor([ok])
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    if int(t) == 1:
+        return "rccl_allgather"
+    if os.environ.get("USAC_BENCH_SAME_DEVICE"):
+        return "gloo_allgather"
+    print("bench: no RCCL communicator on distinct devices; refusing to report a scaling line", file=sys.stderr)
+    sys.exit(3)
 
 
 def main():
@@ -328,16 +391,7 @@ def main():
     if world > 1:  # the per-batch best-record exchange: RCCL all-gather on the context stream
         uid = [usac.Context.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        try:
-            ctx.comm_init(world, rank, uid[0])
-            exchange = "rccl_allgather"
-        except usac.UsacError as e:  # keep the scaling run alive: the 56-byte record over gloo
-            print("bench: RCCL init failed (%s); exchanging records over gloo" % e, file=sys.stderr)
-            exchange = "gloo_allgather"
-        ok = torch.tensor([1 if exchange == "rccl_allgather" else 0])
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok) == 0:
-            exchange = "gloo_allgather"
+        exchange = init_exchange(ctx, usac, dist, torch, world, rank, uid[0])
 
     def allgather(rec):
         if exchange == "rccl_allgather":
@@ -435,11 +489,27 @@ def main():
         avg_score_ms = float(np.mean(solo_score))
         achieved = bytes_per_hyp * B / (avg_score_ms * 1e-3) / 1e9
         kname = ("void usac::k_score_f2<%d>" if (fund or ess) else "void usac::k_score_hf<%d, false>") % args.chunks
-        traffic = measured_traffic(kname, n, B) if not (fund or ess or args.sprt) else None
-        valu = measured_valu(kname, n, B, avg_score_ms) if not (fund or ess or args.sprt) else None
         kshort = ("k_sprt_head/tail<%d>" % (3 if fund else 4 if ess else 2)) if args.sprt else \
             (("k_score_f2<%d,%s>" % (args.chunks, "E" if ess else "F")) if (fund or ess) else
              ("k_score_hf<%d,false>" % args.chunks))
+        roof = valu_roofline(kname, n, B, avg_score_ms) if not args.sprt else None
+        if roof is None:
+            roof = {"bound": "valu", "achieved": None, "peak": SIMD_CYCLES_S, "unit": "SIMD-cycles/s", "frac": None,
+                    "note": "no committed PMC summary (profiles/r*_summary.json) for this kernel and workload"}
+        roof.update({
+            "traffic": roof.get("hbm", {}).get("traffic_bytes_per_launch"), "traffic_unit": "bytes/launch",
+            "kernel": kshort, "kernel_ms": avg_score_ms, "hypotheses_per_launch": B, "sprt": bool(args.sprt),
+            "sprt_points_tested_per_batch": tested_per_batch, "models_per_hypothesis": models_per_hyp,
+            "algorithmic_bytes_per_hypothesis": bytes_per_hyp,
+            "algorithmic_equiv_gbs": achieved,
+            "note": "frac = VALU-busy SIMD-cycles per launch (PMC SQ_ACTIVE_INST_VALU x 4, packed FMAs at their two "
+                    "issue slots) / measured kernel time / (1024 SIMDs x 2.4 GHz): the score kernel is "
+                    "fp32-VALU-issue bound with its point records L2/scalar-cache resident, so `hbm` (counter-"
+                    "measured bytes) is a small fraction of HBM peak; algorithmic_equiv_gbs = SURVEY §8(d) bytes "
+                    "(16 B x N per hypothesis) / kernel time, a re-read-equivalent rate, not a roofline fraction",
+            "solve_kernel_ms": float(np.mean(solo_solve)), "kernel_ms_in_pipeline": float(np.mean(score_ms)),
+            "solve_kernel_ms_in_pipeline": float(np.mean(solve_ms)),
+            "batch_device_ms_in_pipeline": float(np.mean(batch_ms))})
         smp_name = "Prosac (reference subset schedule, T_N = 200000)" if args.sampler == "prosac" else "Uniform"
         out = {
             "metric": "model hypotheses/sec (sample+solve+score) and inlier-count match vs ref",
@@ -471,23 +541,7 @@ def main():
                        "n_points": n, "batch_per_gpu": B, "threshold": args.threshold,
                        "score_chunks": args.chunks, "batches_in_flight": P,
                        "parallelism": "hypothesis-sharded x%d" % world, "exchange": exchange},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
-                         "traffic_unit": "bytes/launch", "traffic_source": traffic[1] if traffic else None,
-                         "kernel": kshort, "sprt": bool(args.sprt),
-                         "sprt_points_tested_per_batch": tested_per_batch,
-                         "kernel_ms": avg_score_ms, "models_per_hypothesis": models_per_hyp,
-                         "algorithmic_bytes_per_hypothesis": bytes_per_hyp,
-                         "hypotheses_per_launch": B,
-                         "note": "achieved = algorithmic bytes (16 B x N points per hypothesis, the bytes the "
-                                 "reference scan reads) / measured kernel time; the point set is L2-resident, so "
-                                 "true HBM traffic (`traffic`) is ~0.1%% of it and the kernel is VALU-issue bound "
-                                 "(DESIGN.md 'Roofline')",
-                         "solve_kernel_ms": float(np.mean(solo_solve)),
-                         "kernel_ms_in_pipeline": float(np.mean(score_ms)),
-                         "solve_kernel_ms_in_pipeline": float(np.mean(solve_ms)),
-                         "batch_device_ms_in_pipeline": float(np.mean(batch_ms)),
-                         "valu_issue": valu},
+            "roofline": roof,
             "best": {"inliers": int(best.inliers), "hyp_index": int(best.hyp_index)},
         }
         if world == 1:

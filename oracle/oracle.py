@@ -439,3 +439,17 @@ def set_f8_rank2(on):
     """Rank-2 enforcement in the 8-point polish (eight_points.cpp:58-68, commented out in the
     current reference): the revision that produced results/kusvod2/*.csv ran it.  Test-only."""
     lib().orc_set_f8_rank2(1 if on else 0)
+
+
+def hypothesis_loop_mt(kind, points, thr, seed, count, threads, dlt_mode=DLT_THIN):
+    """All-cores CPU baseline: `count` hypotheses of the reference-style loop on `threads`
+    pthreads (disjoint ranges, one estimator each) -> (wall seconds, best inlier count)."""
+    pts = np.ascontiguousarray(points, dtype=np.float32)
+    L = lib()
+    L.orc_hypothesis_loop_mt.restype = ctypes.c_double
+    L.orc_hypothesis_loop_mt.argtypes = [ctypes.c_int, _f32p, ctypes.c_uint, ctypes.c_int, ctypes.c_float,
+                                         ctypes.c_uint, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    best = ctypes.c_int(0)
+    dt = L.orc_hypothesis_loop_mt(kind, _p(pts, _f32p), pts.shape[0], dlt_mode, thr, seed, count, threads,
+                                  ctypes.byref(best))
+    return dt, best.value

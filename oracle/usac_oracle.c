@@ -2931,6 +2931,86 @@ int orc_hypothesis_loop(orc_est *e, orc_uniform *s, int count, float thr, float 
     return best_cnt;
 }
 
+/* All-cores CPU baseline: the same reference-style loop on `threads`
+ * std-thread-like workers (pthreads) over disjoint ranges of one pre-drawn glibc sample stream,
+ * each worker with its own estimator state (the reference's estimator caches the model, so
+ * one instance per thread).  Returns the wall seconds of the parallel region; best via out. */
+#include <pthread.h>
+#include <time.h>
+
+typedef struct {
+    int kind, dlt_mode, m, count;
+    const float *pts;
+    unsigned int n;
+    const int *samples;
+    float thr;
+    int best_cnt;
+    float best_sum;
+} orc_mt_job;
+
+static void *orc_mt_worker(void *arg) {
+    orc_mt_job *j = (orc_mt_job *)arg;
+    orc_est *e = orc_est_new(j->kind, j->pts, j->n, j->dlt_mode);
+    float models[90];
+    int best_cnt = 0;
+    float best_sum = 0.f;
+    for (int it = 0; it < j->count; it++) {
+        int nm = orc_est_estimate(e, j->samples + (size_t)it * j->m, models);
+        for (int i = 0; i < nm; i++) {
+            int cnt;
+            float sum;
+            orc_quality(e, models + 9 * i, j->thr, &cnt, &sum, NULL);
+            if (score_bigger(cnt, sum, best_cnt, best_sum)) {
+                best_cnt = cnt;
+                best_sum = sum;
+            }
+        }
+    }
+    orc_est_free(e);
+    j->best_cnt = best_cnt;
+    j->best_sum = best_sum;
+    return NULL;
+}
+
+double orc_hypothesis_loop_mt(int kind, const float *points, unsigned int n, int dlt_mode, float thr,
+                              unsigned int seed, int count, int threads, int *best_cnt) {
+    if (threads < 1) threads = 1;
+    orc_est *e0 = orc_est_new(kind, points, n, dlt_mode);
+    if (!e0) return -1.0;
+    const int m = orc_est_sample_size(e0);
+    orc_est_free(e0);
+    int *samples = (int *)malloc(sizeof(int) * (size_t)m * (size_t)count);
+    orc_srandom(seed);
+    orc_uniform *u = orc_uniform_new(n, (unsigned int)m);
+    orc_uniform_samples(u, samples, count);
+    orc_uniform_free(u);
+    orc_mt_job *jobs = (orc_mt_job *)calloc((size_t)threads, sizeof(orc_mt_job));
+    pthread_t *tid = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+    int start = 0;
+    for (int t = 0; t < threads; t++) {
+        int c = count / threads + (t < count % threads ? 1 : 0);
+        jobs[t] = (orc_mt_job){kind, dlt_mode, m, c, points, n, samples + (size_t)start * m, thr, 0, 0.f};
+        start += c;
+    }
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int t = 0; t < threads; t++) pthread_create(&tid[t], NULL, orc_mt_worker, &jobs[t]);
+    for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    int bc = 0;
+    float bs = 0.f;
+    for (int t = 0; t < threads; t++)
+        if (score_bigger(jobs[t].best_cnt, jobs[t].best_sum, bc, bs)) {
+            bc = jobs[t].best_cnt;
+            bs = jobs[t].best_sum;
+        }
+    if (best_cnt) *best_cnt = bc;
+    free(samples);
+    free(jobs);
+    free(tid);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
 /* ------------------------------------------------------------ generator */
 /* Generate2DLinePoints (generator/generator.cpp:98-148), SURVEY Q25: fp32 arithmetic on
  * glibc rand(); sin/cos/sqrt are the C double functions. */

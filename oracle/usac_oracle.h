@@ -150,6 +150,9 @@ void orc_napsac_sample(orc_napsac *s, int *sample);
  * mt19937 is seeded with cfg->seed instead of std::random_device). */
 /* test switch: rank-2 enforcement in the 8-point polish (older reference revision) */
 void orc_set_f8_rank2(int on);
+/* all-cores CPU baseline: wall seconds of `count` hypotheses on `threads` workers */
+double orc_hypothesis_loop_mt(int kind, const float *points, unsigned int n, int dlt_mode, float thr,
+                              unsigned int seed, int count, int threads, int *best_cnt);
 int orc_ransac_run_cfg(int kind, const float *points, unsigned int n, const orc_config *cfg, orc_result *out,
                        int *inliers_out, unsigned int *rec_iter, int *rec_count, float *rec_score, int rec_cap);
 

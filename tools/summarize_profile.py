@@ -8,6 +8,8 @@ import csv, collections, json, os, sys
 
 src, tag = sys.argv[1], sys.argv[2]
 out = {"source": src, "kernels": {}}
+if len(sys.argv) > 4:  # workload shape the bench matches on (bench.py _profile_entry)
+    out["workload"] = {"n_points": int(sys.argv[3]), "batch": int(sys.argv[4])}
 stats = os.path.join(src, "trace", "run_kernel_stats.csv")
 for r in csv.DictReader(open(stats)):
     out["kernels"].setdefault(r["Name"], {})["trace"] = {
