@@ -178,6 +178,9 @@ int usac_hypothesize_score(usac_ctx *ctx, const int32_t *samples, uint32_t B, ui
  * argmax on the context stream; usac_fetch_best waits and returns the batch best. */
 int usac_hypothesize_async(usac_ctx *ctx, uint32_t B, uint64_t seed, uint64_t first_hyp, float thr);
 int usac_fetch_best(usac_ctx *ctx, usac_record *best);
+/* Per-slot counts / sums (sums nullable) of the last batch as the score kernel left them (the
+ * throughput kernels' chunked sums included): n <= B x slots.  Waits for the stream.  For tests. */
+int usac_last_counts(usac_ctx *ctx, int32_t *counts, float *sums, uint32_t n);
 int usac_sync(usac_ctx *ctx);
 /* Device time of the last async batch's kernels, measured with HIP events on the
  * context stream: [0] whole batch, [1] score kernel, [2] solve kernel (ms). */

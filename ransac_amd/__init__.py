@@ -99,7 +99,7 @@ ABI_SYMBOLS = [
     "usac_num_points", "usac_estimate_models", "usac_score_models", "usac_get_inliers", "usac_knn", "usac_bk_label",
     "usac_nonminimal",
     "usac_hypothesize_score", "usac_hypothesize_async", "usac_fetch_best", "usac_sync", "usac_last_timings",
-    "usac_set_score_chunks", "usac_set_score_variant", "usac_std_termination", "usac_ransac_run", "usac_uniform_samples",
+    "usac_set_score_chunks", "usac_set_score_variant", "usac_last_counts", "usac_std_termination", "usac_ransac_run", "usac_uniform_samples",
     "usac_prosac_samples", "usac_sprt_pool", "usac_set_sprt", "usac_sprt_tested", "usac_set_device_sampler",
     "usac_draw_samples",
     "usac_comm_unique_id", "usac_comm_init", "usac_allgather_records", "usac_merge_records",
@@ -133,6 +133,8 @@ def lib():
         "usac_set_dlt_mode": (ctypes.c_int, [_vp, ctypes.c_int]),
         "usac_set_score_chunks": (ctypes.c_int, [_vp, ctypes.c_int]),
         "usac_set_score_variant": (ctypes.c_int, [_vp, ctypes.c_int]),
+        "usac_last_counts": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_float),
+                                            ctypes.c_uint32]),
         "usac_sample_size": (ctypes.c_uint32, [_vp]),
         "usac_num_points": (ctypes.c_uint32, [_vp]),
         "usac_estimate_models": (ctypes.c_int, [_vp, i32p, ctypes.c_uint32, f32p, i32p]),
@@ -273,6 +275,14 @@ class Context:
 
     def set_score_chunks(self, chunks):
         self._check(lib().usac_set_score_chunks(self._h, int(chunks)), "set_score_chunks")
+
+    def last_counts(self, n):
+        """Per-slot (counts, sums) of the last batch as the score kernel left them."""
+        c = np.zeros(n, dtype=np.int32)
+        sm = np.zeros(n, dtype=np.float32)
+        self._check(lib().usac_last_counts(self._h, _ptr(c, ctypes.c_int32), _ptr(sm, ctypes.c_float), n),
+                    "last_counts")
+        return c, sm
 
     def set_score_variant(self, variant):
         """0 = guard-band fast path (default), 1 = exact reference expression for every pair."""

@@ -1118,6 +1118,16 @@ int usac_hypothesize_async(usac_ctx *c, uint32_t B, uint64_t seed, uint64_t firs
     return USAC_OK;
 }
 
+int usac_last_counts(usac_ctx *c, int32_t *counts, float *sums, uint32_t n) {
+    if (!c || !counts || n == 0) return USAC_ERR_ARG;
+    if ((size_t)n * sizeof(int32_t) > c->counts.bytes) return fail(c, USAC_ERR_ARG, "more slots than the last batch");
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, hipMemcpyAsync(counts, c->counts.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+    if (sums) HIP_TRY(c, hipMemcpyAsync(sums, c->sums.p, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    return USAC_OK;
+}
+
 int usac_fetch_best(usac_ctx *c, usac_record *best) {
     if (!c || !best) return USAC_ERR_ARG;
     HIP_TRY(c, hipMemcpyAsync(best, c->best.p, sizeof(usac_record), hipMemcpyDeviceToHost, c->stream));
