@@ -53,6 +53,8 @@ def parse():
                     help="BASELINE configs[4]: full USAC runs (homography + NAPSAC grid sampler + LO-RANSAC) "
                          "over 100k correspondences; one step = one run, value = main-loop hypotheses/s")
     ap.add_argument("--lo", type=int, default=1, help="cfg5 LO variant: 1 InItLORsc (unlimited), 2 InItFLORsc")
+    ap.add_argument("--cfg5-replicas", action="store_true",
+                    help="cfg5 with N > 1: independent runs per rank instead of hypothesis-sharded runs")
     ap.add_argument("--pipeline", type=int, default=3,
                     help="batches in flight: one context (stream + buffers) per in-flight batch, so batch i+1's "
                          "solve overlaps batch i's scoring")
@@ -164,8 +166,8 @@ def _profile_entry(kernel_prefix, n_points, batch):
             d = json.load(open(f))
         except Exception:
             continue
-        shape = d.get("workload", {})
-        if shape and (shape.get("n_points") != n_points or shape.get("batch") != batch):
+        shape = d.get("workload", {})  # only summaries of the same workload shape count
+        if shape.get("n_points") != n_points or shape.get("batch") != batch:
             continue
         for k, v in d.get("kernels", {}).items():
             if k.replace(" ", "").startswith(kernel_prefix.replace(" ", "")):
@@ -224,10 +226,13 @@ def usac_device():
 
 
 def cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank):
-    """Full-run mode (BASELINE configs[4]): each rank runs whole USAC loops -- batched device
-    solve + score of the NAPSAC samples, exact host replay of the sequential loop, LO-RANSAC
-    (every LSQ fit and inlier scan on the device) -- on its own seeds (replicas, weak scaling).
-    value = main-loop hypotheses of all ranks / max wall time."""
+    """Full-run mode (BASELINE configs[4]): whole USAC loops -- batched device solve + score of
+    the NAPSAC samples, exact host replay of the sequential loop, LO-RANSAC (every LSQ fit and
+    inlier scan on the device).  With N > 1 ranks each run is hypothesis-sharded (SURVEY §8(e),
+    usac_ransac_run_sharded: every batch split over the ranks, counts and models all-gathered
+    over RCCL, the replay identical on every rank) -- strong scaling, value = main-loop
+    hypotheses of the runs / max wall time; --cfg5-replicas runs independent seeds per rank
+    instead (weak scaling, value summed over ranks)."""
     from oracle import oracle as O
 
     pts, _, _ = synthetic.homography_points(n=args.points, inlier_ratio=0.2, seed=args.seed, cluster=(500, 500, 150))
@@ -242,9 +247,27 @@ def cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank):
         mdl.setNeighborsType(usac.NeighborsSearch.Grid)
         return mdl
 
+    sharded = world > 1 and not args.cfg5_replicas
+    comm_ctx = None
+    if sharded:  # the RCCL communicator lives on one context; each run's context borrows it via the bench
+        comm_ctx = usac.Context(usac.ESTIMATOR.Homography, pts, device=local_rank)
+        uid = [usac.Context.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        exchange = init_exchange(comm_ctx, usac, dist, torch, world, rank, uid[0])
+
+    def gloo_gather(b):
+        t = torch.frombuffer(bytearray(b), dtype=torch.uint8)
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        return [p.numpy().tobytes() for p in parts]
+
     def one_run(seed):
-        r = usac.Ransac(model(seed), pts)
-        r.run()
+        if not sharded:
+            r = usac.Ransac(model(seed), pts)
+            r.run()
+            return r.getRansacOutput()
+        r = usac.Ransac(model(seed), pts, ctx=comm_ctx)
+        r.run(shard=(world, rank, "rccl" if exchange == "rccl_allgather" else gloo_gather))
         return r.getRansacOutput()
 
     for i in range(args.warmup):
@@ -254,15 +277,19 @@ def cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank):
     iters = 0
     t0 = time.perf_counter()
     for step in range(args.steps):
-        iters += one_run(args.seed + step * world + rank).getNumberOfMainIterations()
+        seed = args.seed + step if sharded else args.seed + step * world + rank
+        iters += one_run(seed).getNumberOfMainIterations()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
         tt = torch.tensor([elapsed, float(iters)], dtype=torch.float64)
         dist.all_reduce(tt[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
+        if not sharded:  # replicas: every rank's runs are distinct work
+            dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
         elapsed, iters = float(tt[0]), int(tt[1])
+    # parity: one run against the oracle (same seed) -- every rank takes part in a sharded run
+    out = one_run(args.seed)
     if rank != 0:
         return
     # roofline of the dominant loop kernel: the score of one batch of B hypotheses at N = 100k
@@ -281,8 +308,7 @@ def cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank):
     bytes_per_hyp = 16.0 * n + 16 + 44
     score_ms = float(np.mean(sc))
     achieved = bytes_per_hyp * B / (score_ms * 1e-3) / 1e9
-    # parity: one run against the oracle (same seed): iterations, LO counters, model, inliers
-    out = one_run(args.seed)
+    # parity of that run: iterations, LO counters, model, inliers
     ref = O.ransac_run(O.HOMOGRAPHY, pts, args.threshold, 0.95, args.seed, sampler=O.SAMPLER_NAPSAC, sprt=False,
                        lo=args.lo, max_iters=max_iters)
     roof = valu_roofline("void usac::k_score_hf<8, false>", n, B, score_ms) or {
@@ -302,13 +328,15 @@ def cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank):
         "metric": "model hypotheses/sec (sample+solve+score) and inlier-count match vs ref",
         "value": iters / elapsed, "unit": "hypotheses/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "scaling": "strong" if sharded else "weak", "vs_baseline": None, "dtype": "f32",
         "data": "synthetic (clustered homography inliers 20%%, uniform outliers), %d correspondences" % n,
         "config": {"workload": "cfg5: Homography_estimator + Napsac_sampler (grid) + LO-RANSAC (%s), full runs, "
                                "%d correspondences; one step = one run per rank" %
                                ("InItLORsc" if args.lo == 1 else "InItFLORsc", n),
                    "n_points": n, "threshold": args.threshold, "max_iterations": max_iters,
-                   "hypotheses_per_gpu": iters / world, "parallelism": "replicas x%d" % world},
+                   "hypotheses_per_gpu": iters / world,
+                   "parallelism": ("hypothesis-sharded runs x%d (%s)" % (world, exchange)) if sharded else
+                                  "replicas x%d" % world},
         "roofline": roof,
         "parity": parity,
         "run_stats": {k: int(out.raw[k]) for k in ("batches", "n_records", "lo_rounds", "lo_stages", "sum_models",

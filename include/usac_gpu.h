@@ -34,6 +34,7 @@
  *   usac_sprt_pool                 SPRT ctor pool + A0 (sprt.hpp:89-175)
  *   usac_ransac_run                Ransac::run + RansacOutput (ransac.cpp:14-238,
  *                                  ransac_output.hpp:29-97), Uniform sampler
+ *   usac_ransac_run_sharded        Ransac::run with hypothesis-sharded batches
  *   usac_comm_*                    new: one RCCL all-gather of best records per batch
  *
  * Threading: a context is bound to one device and one HIP stream and is not
@@ -49,7 +50,7 @@
 extern "C" {
 #endif
 
-#define USAC_ABI_VERSION 6
+#define USAC_ABI_VERSION 7
 
 /* = enum ESTIMATOR (usac/model.hpp:10) */
 enum { USAC_LINE2D = 1, USAC_HOMOGRAPHY = 2, USAC_FUNDAMENTAL = 3, USAC_ESSENTIAL = 4 };
@@ -229,6 +230,19 @@ uint32_t usac_std_termination(uint32_t inliers, uint32_t points_size, uint32_t s
  * updates in loop order (hyp_index = iteration, SPRT double counting included). */
 int usac_ransac_run(usac_ctx *ctx, const usac_params *params, usac_run_output *out, int32_t *inliers_out,
                     usac_record *records, uint32_t rec_cap);
+/* All-gather of host bytes across the ranks of a sharded run: every rank passes `bytes` bytes at
+ * `send`; `recv` (nranks x bytes) receives them in rank order.  Returns 0 on success. */
+typedef int (*usac_allgather_fn)(void *user, const void *send, size_t bytes, void *recv);
+/* Ransac::run with every batch's hypotheses sharded over nranks processes / GPUs:
+ * each rank draws the same host sample stream (same params, same seed), solves and scores its
+ * contiguous slice of the batch, and the slices' counts and models are all-gathered -- through
+ * `gather` when non-null (e.g. a torch.distributed gloo group), else RCCL on the communicator of
+ * usac_comm_init(ctx, nranks, rank, id).  Termination, LO, graph cut and polish are then replayed
+ * on the merged batch identically on every rank, so every rank's output equals usac_ransac_run's.
+ * Not with SPRT (its sequential replay reads pool-order flag words of every model). */
+int usac_ransac_run_sharded(usac_ctx *ctx, const usac_params *params, int nranks, int rank, usac_allgather_fn gather,
+                            void *gather_user, usac_run_output *out, int32_t *inliers_out, usac_record *records,
+                            uint32_t rec_cap);
 /* Host glibc-compatible UniformSampler stream (uniform_sampler.hpp:42-54): count x m
  * samples after srandom(seed).  Exposed for parity tests. */
 int usac_uniform_samples(uint32_t seed, uint32_t n_points, uint32_t m, uint32_t count, int32_t *out);

@@ -99,7 +99,7 @@ ABI_SYMBOLS = [
     "usac_num_points", "usac_estimate_models", "usac_score_models", "usac_get_inliers", "usac_knn", "usac_bk_label",
     "usac_nonminimal",
     "usac_hypothesize_score", "usac_hypothesize_async", "usac_fetch_best", "usac_sync", "usac_last_timings",
-    "usac_set_score_chunks", "usac_set_score_variant", "usac_last_counts", "usac_std_termination", "usac_ransac_run", "usac_uniform_samples",
+    "usac_set_score_chunks", "usac_set_score_variant", "usac_last_counts", "usac_std_termination", "usac_ransac_run", "usac_ransac_run_sharded", "usac_uniform_samples",
     "usac_prosac_samples", "usac_sprt_pool", "usac_set_sprt", "usac_sprt_tested", "usac_set_device_sampler",
     "usac_draw_samples",
     "usac_comm_unique_id", "usac_comm_init", "usac_allgather_records", "usac_merge_records",
@@ -153,6 +153,8 @@ def lib():
         "usac_std_termination": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                    ctypes.c_float, ctypes.c_uint32]),
         "usac_ransac_run": (ctypes.c_int, [_vp, _P(_Params), _P(_RunOutput), i32p, _P(Record), ctypes.c_uint32]),
+        "usac_ransac_run_sharded": (ctypes.c_int, [_vp, _P(_Params), ctypes.c_int, ctypes.c_int, _vp, _vp,
+                                                   _P(_RunOutput), i32p, _P(Record), ctypes.c_uint32]),
         "usac_uniform_samples": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                 i32p]),
         "usac_prosac_samples": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
@@ -537,20 +539,29 @@ class RansacOutput:
         return self._lo
 
 
+# usac_allgather_fn (include/usac_gpu.h)
+_ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
+
+
 class Ransac:
     """usac/ransac/ransac.hpp:41-115 -- Ransac(model, points); run(); getRansacOutput()."""
 
-    def __init__(self, model, points):
+    def __init__(self, model, points, ctx=None):
+        """ctx: an existing Context over the same points to run on (e.g. the one holding the RCCL
+        communicator of a sharded run); by default a new one."""
         if model.sampler not in (SAMPLER.Uniform, SAMPLER.Prosac, SAMPLER.Napsac):
             raise NotImplementedError("sampler %s is not supported (Uniform, Napsac, Prosac)" % model.sampler.name)
         if int(model.lo) not in (0, 1, 2, 3):
             raise NotImplementedError("LO %r is not supported (InItLORsc, InItFLORsc, GC)" % model.lo)
         self.model = model
-        self.ctx = Context(model.estimator, points, device=model.device)
+        self.ctx = ctx if ctx is not None else Context(model.estimator, points, device=model.device)
         self._out = None
         self.records = []
 
-    def run(self, rec_cap=4096):
+    def run(self, rec_cap=4096, shard=None):
+        """shard = (nranks, rank, gather): hypothesis-sharded batches (usac_ransac_run_sharded);
+        gather(bytes) -> list of nranks bytes objects in rank order (e.g. a gloo all_gather), or
+        gather = "rccl" for the communicator set up with Context.comm_init."""
         L = lib()
         m = self.model
         seed = m.seed
@@ -563,8 +574,27 @@ class Ransac:
         out = _RunOutput()
         inl = np.zeros(self.ctx.n, dtype=np.int32)
         recs = (Record * rec_cap)()
-        rc = L.usac_ransac_run(self.ctx._h, ctypes.byref(p), ctypes.byref(out), _ptr(inl, ctypes.c_int32), recs,
-                               rec_cap)
+        if shard is None:
+            rc = L.usac_ransac_run(self.ctx._h, ctypes.byref(p), ctypes.byref(out), _ptr(inl, ctypes.c_int32), recs,
+                                   rec_cap)
+        else:
+            nranks, rank, gather = shard
+            cb = None
+            if gather != "rccl":
+                def _cb(user, send, nbytes, recv):
+                    try:
+                        parts = gather(ctypes.string_at(send, nbytes))
+                        buf = b"".join(parts)
+                        if len(parts) != nranks or len(buf) != nranks * nbytes:
+                            return -1
+                        ctypes.memmove(recv, buf, len(buf))
+                        return 0
+                    except Exception:  # reported as a failed all-gather (usac_last_error)
+                        return -1
+                cb = _ALLGATHER_FN(_cb)
+            rc = L.usac_ransac_run_sharded(self.ctx._h, ctypes.byref(p), int(nranks), int(rank),
+                                           ctypes.cast(cb, _vp) if cb is not None else None, None,
+                                           ctypes.byref(out), _ptr(inl, ctypes.c_int32), recs, rec_cap)
         if rc == -111:
             raise UsacError(rc, "best score is 0 (ransac.cpp:143-147)")
         self.ctx._check(rc, "ransac_run")

@@ -88,6 +88,7 @@ struct usac_ctx {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     DevBuf rec_send, rec_all;
+    DevBuf x_send, x_recv;  // sharded-run all-gather staging (RCCL path)
     // timing
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float last_ms[3] = {0, 0, 0};
@@ -900,7 +901,8 @@ void usac_destroy(usac_ctx *c) {
                       &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok,
                       &c->rec_send, &c->rec_all, &c->tv_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
-                      &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2, &c->gc_err})
+                      &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2, &c->gc_err, &c->x_send,
+                      &c->x_recv})
         b->release();
     for (auto &ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -1271,10 +1273,71 @@ int usac_sprt_pool(uint32_t seed, int estimator, uint32_t n_points, uint32_t m, 
 // change would alter a later sample of the batch the rest of the batch is dropped and the
 // sampler is rewound to just after the current sample.  Then the <= 4-pass non-minimal
 // polish on the device.
-int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, int32_t *inliers_out,
-                    usac_record *records, uint32_t rec_cap) {
-    if (!c || !prm || !out) return USAC_ERR_ARG;
+// One batch of a sharded run: rank r solves and scores slots of samples [r P, r P + P) (P =
+// ceil(B / nranks); the last slices may be short or empty), packs its counts and model words
+// (int32 / fp32, padded to P x spk slots, counts -1 on padding) and all-gathers them; every rank
+// unpacks all slices into hc / hmod exactly as the unsharded batch leaves them.
+static int sharded_batch(usac_ctx *c, const int32_t *hs, uint32_t B, uint32_t iters, float thr, int nranks, int rank,
+                         usac_allgather_fn gather, void *user, std::vector<uint8_t> &xbuf, int32_t *hc, float *hmod,
+                         size_t SB) {
+    const uint32_t m = c->m, spk = c->spk;
+    const int nc = ncomp(c);
+    const uint32_t P = (B + (uint32_t)nranks - 1) / (uint32_t)nranks;
+    const uint32_t lo = std::min<uint32_t>(B, (uint32_t)rank * P);
+    const uint32_t Bs = std::min<uint32_t>(B, lo + P) - lo;
+    const size_t Ps = (size_t)P * spk, Ss = (size_t)Bs * spk;
+    const size_t words = (1 + (size_t)nc) * Ps, bytes = 4 * words;
+    xbuf.resize(bytes * (1 + (size_t)nranks));
+    int32_t *send = reinterpret_cast<int32_t *>(xbuf.data());
+    uint8_t *recv = xbuf.data() + bytes;
+    std::fill(send, send + Ps, -1);
+    std::fill(send + Ps, send + words, 0);
+    if (Bs) {
+        HIP_TRY(c, hipMemcpyAsync(c->samples.p, hs + (size_t)lo * m, sizeof(int32_t) * (size_t)Bs * m,
+                                  hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, enqueue_solve(c, c->samples.as<int32_t>(), Bs, 0, (uint64_t)iters + lo, nullptr));
+        HIP_TRY(c, enqueue_score(c, Bs, thr, loop_chunks(c, Bs)));
+        HIP_TRY(c, hipMemcpyAsync(send, c->counts.p, sizeof(int32_t) * Ss, hipMemcpyDeviceToHost, c->stream));
+        for (int k = 0; k < nc; k++)
+            HIP_TRY(c, hipMemcpyAsync(send + (1 + (size_t)k) * Ps, c->models.as<float>() + (size_t)k * Ss,
+                                      sizeof(float) * Ss, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (gather) {
+        if (gather(user, send, bytes, recv) != 0) return fail(c, USAC_ERR_ARG, "all-gather callback failed");
+    } else {
+        HIP_TRY(c, c->x_send.reserve(bytes));
+        HIP_TRY(c, c->x_recv.reserve(bytes * (size_t)nranks));
+        HIP_TRY(c, hipMemcpyAsync(c->x_send.p, send, bytes, hipMemcpyHostToDevice, c->stream));
+        NCCL_TRY(c, ncclAllGather(c->x_send.p, c->x_recv.p, bytes, ncclUint8, c->comm, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(recv, c->x_recv.p, bytes * (size_t)nranks, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipStreamSynchronize(c->stream));
+    }
+    for (int r = 0; r < nranks; r++) {
+        const uint32_t lr = std::min<uint32_t>(B, (uint32_t)r * P);
+        const size_t Sr = (size_t)(std::min<uint32_t>(B, lr + P) - lr) * spk;
+        const int32_t *rc_ = reinterpret_cast<const int32_t *>(recv + (size_t)r * bytes);
+        memcpy(hc + (size_t)lr * spk, rc_, sizeof(int32_t) * Sr);
+        for (int k = 0; k < nc; k++)
+            memcpy(hmod + (size_t)k * SB + (size_t)lr * spk, rc_ + (1 + (size_t)k) * Ps, sizeof(float) * Sr);
+    }
+    return USAC_OK;
+}
+
+// Ransac::run with each batch's hypotheses sharded over nranks: every rank
+// draws the same host sample stream, solves and scores only its contiguous slice of the
+// batch, and the slices' per-slot counts and models are all-gathered (gather(), or RCCL on
+// the context's communicator when gather is null); the replay -- records, termination, LO,
+// polish -- then runs on the merged batch identically on every rank (ransac.cpp:58-139 order).
+static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int rank, usac_allgather_fn gather,
+                           void *gather_user, usac_run_output *out, int32_t *inliers_out, usac_record *records,
+                           uint32_t rec_cap) {
+    if (!c || !prm || !out || nranks < 1 || rank < 0 || rank >= nranks) return USAC_ERR_ARG;
     memset(out, 0, sizeof(*out));
+    if (nranks > 1 && prm->sprt)
+        return fail(c, USAC_ERR_UNSUPPORTED, "sharded run with SPRT: the sequential SPRT replay is not sharded");
+    if (nranks > 1 && !gather && (!c->comm || c->nranks != nranks || c->rank != rank))
+        return fail(c, USAC_ERR_ARG, "sharded run without a gather callback needs usac_comm_init(nranks, rank)");
     const bool prosac = prm->sampler == USAC_SAMPLER_PROSAC;
     const bool napsac = prm->sampler == USAC_SAMPLER_NAPSAC;
     if (!prosac && !napsac && prm->sampler != USAC_SAMPLER_UNIFORM && prm->sampler != 0)
@@ -1392,6 +1455,7 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
     }
 
     const size_t SB = (size_t)batch * spk;  // slot stride of the host copies
+    std::vector<uint8_t> xbuf;               // sharded runs: all-gather send + receive buffers
     std::vector<int32_t> hs((size_t)batch * m, 0), hc(SB), slot_row(SB);
     std::vector<float> hsum(SB), hmod((size_t)ncomp(c) * SB);
     std::vector<uint32_t> hlist(SB), hmask(sprt ? (size_t)nw * SB : 0);
@@ -1445,6 +1509,12 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
         lap(T_DRAW);
         // ---- device: solve, then exact scores or pool-order flags
         const size_t S = (size_t)B * spk;
+        uint32_t rows = (uint32_t)S;
+        if (nranks > 1) {  // this rank's slice, then the all-gather of every slice's counts and models
+            if ((rc = sharded_batch(c, hs.data(), B, iters, thr, nranks, rank, gather, gather_user, xbuf, hc.data(),
+                                    hmod.data(), SB)))
+                return rc;
+        } else {
         HIP_TRY(c, hipMemcpyAsync(c->samples.p, hs.data(), sizeof(int32_t) * (size_t)B * m, hipMemcpyHostToDevice,
                                   c->stream));
         HIP_TRY(c, enqueue_solve(c, c->samples.as<int32_t>(), B, 0, iters, nullptr));
@@ -1461,7 +1531,6 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
         for (int k = 0; k < ncomp(c); k++)
             HIP_TRY(c, hipMemcpyAsync(hmod.data() + (size_t)k * SB, c->models.as<float>() + (size_t)k * S,
                                       sizeof(float) * S, hipMemcpyDeviceToHost, c->stream));
-        uint32_t rows = (uint32_t)S;
         if (sprt) {
             if (listed(c)) {  // occupied slots -> mask rows
                 HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
@@ -1477,6 +1546,7 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
                                           sizeof(uint32_t) * rows, hipMemcpyDeviceToHost, c->stream));
         }
         HIP_TRY(c, hipStreamSynchronize(c->stream));
+        }
         if (sprt) {
             if (listed(c)) {
                 std::fill(slot_row.begin(), slot_row.begin() + S, -1);
@@ -1634,6 +1704,17 @@ int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, i
     out->inliers = best.inlier_number;
     out->time_us = std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
     return USAC_OK;
+}
+
+int usac_ransac_run(usac_ctx *c, const usac_params *prm, usac_run_output *out, int32_t *inliers_out,
+                    usac_record *records, uint32_t rec_cap) {
+    return ransac_run_impl(c, prm, 1, 0, nullptr, nullptr, out, inliers_out, records, rec_cap);
+}
+
+int usac_ransac_run_sharded(usac_ctx *c, const usac_params *prm, int nranks, int rank, usac_allgather_fn gather,
+                            void *gather_user, usac_run_output *out, int32_t *inliers_out, usac_record *records,
+                            uint32_t rec_cap) {
+    return ransac_run_impl(c, prm, nranks, rank, gather, gather_user, out, inliers_out, records, rec_cap);
 }
 
 // ---------------------------------------------------------------- multi-GPU
