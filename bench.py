@@ -201,8 +201,8 @@ def valu_roofline(kernel_prefix, n_points, batch, kernel_ms):
         out["achieved"] = act * 4 / t
         out["frac"] = out["achieved"] / SIMD_CYCLES_S
         out["valu_busy_cycles_per_launch"] = act * 4
-        if pmc.get("GRBM_GUI_ACTIVE"):
-            out["valu_busy_pmc"] = act * 4 / 1024 / pmc["GRBM_GUI_ACTIVE"]
+        if pmc.get("GRBM_GUI_ACTIVE"):  # GRBM_GUI_ACTIVE is summed over the 8 XCDs (18.9 "GHz" per ns)
+            out["valu_busy_pmc"] = act * 4 / 1024 / (pmc["GRBM_GUI_ACTIVE"] / 8)
     n_instr = pmc.get("SQ_INSTS_VALU")
     if n_instr:
         out["instructions_per_launch"] = n_instr

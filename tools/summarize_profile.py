@@ -30,6 +30,8 @@ for k, v in out["kernels"].items():
     p = v.get("pmc", {})
     if "FETCH_SIZE" in p or "WRITE_SIZE" in p:
         v["hbm_bytes_per_launch"] = p.get("FETCH_SIZE", 0.0) * 1024 * 2 + p.get("WRITE_SIZE", 0.0) * 1024
-with open(os.path.join("profiles", "%s_summary.json" % tag), "w") as f:
+outdir = sys.argv[5] if len(sys.argv) > 5 else "profiles"
+os.makedirs(outdir, exist_ok=True)
+with open(os.path.join(outdir, "%s_summary.json" % tag), "w") as f:
     json.dump(out, f, indent=1, sort_keys=True)
 print(json.dumps({k[:60]: (v.get("trace", {}).get("avg_ns"), v.get("hbm_bytes_per_launch")) for k, v in out["kernels"].items()}, indent=1))
