@@ -134,6 +134,8 @@ def lib():
         L.orc_hypothesis_loop.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_float, _f32p]
         L.orc_generate_line2d.argtypes = [ctypes.c_uint, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, _f32p, _f32p]
+        L.orc_generate_line2d_next.argtypes = [ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int, _f32p, _f32p]
         _lib = L
     return _lib
 
@@ -428,11 +430,33 @@ def hypothesis_loop(kind, points, thr, seed, count, dlt_mode=DLT_THIN):
 
 
 def generate_line2d(seed, noise, inliers, outliers, border_x, border_y):
+    """Generate2DLinePoints after srand(seed); seed=None continues the rand() stream."""
     pts = np.zeros((inliers + outliers, 2), dtype=np.float32)
     gt = np.zeros(3, dtype=np.float32)
-    lib().orc_generate_line2d(seed, ctypes.c_float(noise), inliers, outliers, border_x, border_y,
-                              _p(pts, _f32p), _p(gt, _f32p))
+    if seed is None:
+        lib().orc_generate_line2d_next(ctypes.c_float(noise), inliers, outliers, border_x, border_y,
+                                       _p(pts, _f32p), _p(gt, _f32p))
+    else:
+        lib().orc_generate_line2d(seed, ctypes.c_float(noise), inliers, outliers, border_x, border_y,
+                                  _p(pts, _f32p), _p(gt, _f32p))
     return pts, gt
+
+
+def generate_line2d_dataset():
+    """generate_syntectic_dataset (generator/generator.cpp:6-67): the eight scenes of
+    dataset/line2d/ in dataset.txt order on one rand() stream from the default seed 1 ->
+    [(name, points, gt_model)]."""
+    out = []
+    first = True
+    for w in (1000, 1200):
+        for h in (1000, 1200):
+            for pct in (0.02, 0.05):
+                outliers = 10000
+                inliers = int(outliers * np.float32(pct))
+                pts, gt = generate_line2d(1 if first else None, 3.0, inliers, outliers, w, h)
+                first = False
+                out.append(("w=%d_h=%d_n=3.000000_I=%d_N=%d" % (w, h, inliers, inliers + outliers), pts, gt))
+    return out
 
 
 def set_f8_rank2(on):

@@ -3017,6 +3017,14 @@ double orc_hypothesis_loop_mt(int kind, const float *points, unsigned int n, int
 void orc_generate_line2d(unsigned int seed, float noise, int inliers, int outliers, int border_x, int border_y,
                          float *pts, float *gt) {
     srand(seed);
+    orc_generate_line2d_next(noise, inliers, outliers, border_x, border_y, pts, gt);
+}
+
+/* The same, continuing the process's rand() stream: generate_syntectic_dataset
+ * (generator/generator.cpp:6-67) calls Generate2DLinePoints for its eight scenes in a row
+ * without reseeding (default seed 1), which is how dataset/line2d/ was written. */
+void orc_generate_line2d_next(float noise, int inliers, int outliers, int border_x, int border_y, float *pts,
+                              float *gt) {
     const float RM = (float)RAND_MAX;
     float alpha = (float)(M_PI * (double)(float)rand() / (double)RAND_MAX);
     float nx = (float)sin((double)alpha);

@@ -206,6 +206,9 @@ int orc_hypothesis_loop(orc_est *e, orc_uniform *s, int count, float thr, float 
 /* generator/generator.cpp:98-148 Generate2DLinePoints (glibc rand(), srand(seed) first) */
 void orc_generate_line2d(unsigned int seed, float noise, int inliers, int outliers, int border_x, int border_y,
                          float *points_out, float *gt_model);
+/* the same without reseeding (continues rand(); generate_syntectic_dataset, generator.cpp:6-67) */
+void orc_generate_line2d_next(float noise, int inliers, int outliers, int border_x, int border_y,
+                              float *points_out, float *gt_model);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,135 @@
+"""GPU parity at BASELINE.json's full sizes for the configurations the smaller tests do not
+reach (VERDICT r1 "untested BASELINE sizes"):
+
+* cfg4 -- Essential 5-pt + Uniform device stream, 50 000 correspondences, B = 65 536 (the
+  bench workload, `bench.py --estimator essential`): the fast two-view kernel equals the
+  exact-expression kernel on every (model, point) pair of the batch (counts and chunk sums
+  bit-equal), the batch best recounted by the oracle, and 256 host-drawn samples bit-exact
+  against the oracle (models, counts, sequential sums).
+* cfg3 -- Fundamental 7-pt + PROSAC + SPRT, 10 000 correspondences: the batch SPRT of a
+  65 536-sample device batch accepts models with their exact full count (oracle recount of
+  every accepted model), and a whole Ransac::run with PROSAC + SPRT at 10 k equals the
+  oracle's run (iterations, records, SPRT counters, PROSAC termination length, model bits,
+  inlier list).
+"""
+import numpy as np
+import pytest
+
+from ransac_amd import synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, dtype=np.float32).view(np.int32)
+
+
+@pytest.fixture(scope="module")
+def cfg4_points():
+    pts, _, _ = synthetic.fundamental_points(n=50000, inlier_ratio=0.3, seed=1, normalized=True)
+    return pts
+
+
+@pytest.fixture(scope="module")
+def cfg3_points():
+    pts, _, _ = synthetic.fundamental_points(n=10000, inlier_ratio=0.3, seed=1)  # quality-sorted (PROSAC)
+    return pts
+
+
+def test_cfg4_full_batch_fast_equals_exact(usac, oracle, cfg4_points):
+    pts, thr, B = cfg4_points, 0.002, 65536
+    with usac.Context(usac.ESTIMATOR.Essential, pts) as ctx:
+        ctx.set_score_chunks(96)  # the bench's cfg4 chunking
+        ctx.set_score_variant(1)
+        ce, se, be = ctx.hypothesize_score(B=B, seed=1, first_hyp=0, thr=thr)
+        ctx.set_score_variant(0)
+        cf, sf, bf = ctx.hypothesize_score(B=B, seed=1, first_hyp=0, thr=thr)
+    occupied = ce >= 0
+    assert 0.2 * B < occupied.sum() < B  # ~0.4 essential matrices per sample pass cheirality
+    np.testing.assert_array_equal(cf, ce)
+    np.testing.assert_array_equal(sf.view(np.int32), se.view(np.int32))
+    assert bf["hyp_index"] == be["hyp_index"] and bf["inliers"] == be["inliers"] == ce.max()
+    est = oracle.Estimator(oracle.ESSENTIAL, pts)
+    oc, _ = est.quality(bf["model"], thr)
+    assert oc == bf["inliers"]
+    assert bf["inliers"] > 0.25 * len(pts)
+
+
+def test_cfg4_host_samples_bit_exact(usac, oracle, cfg4_points):
+    pts, thr = cfg4_points, 0.002
+    samples = oracle.uniform_samples(77, len(pts), 5, 256)
+    est = oracle.Estimator(oracle.ESSENTIAL, pts)
+    om, onm = est.estimate_batch(samples)
+    oc, osum = est.score_models(om, thr)
+    with usac.Context(usac.ESTIMATOR.Essential, pts) as ctx:
+        gm, gnm = ctx.estimate_models(samples)
+        c, s, _ = ctx.hypothesize_score(samples=samples, thr=thr)
+    np.testing.assert_array_equal(gnm, onm)
+    occ = onm == 1
+    assert occ.sum() > 50
+    np.testing.assert_array_equal(_bits(gm[occ]), _bits(om[occ]))
+    np.testing.assert_array_equal(c, np.where(occ, oc, -1))
+    np.testing.assert_array_equal(_bits(s[occ]), _bits(osum[occ]))
+
+
+def test_cfg3_batch_sprt_full_size(usac, oracle, cfg3_points):
+    """65 536 PROSAC-scheduled device samples at 10 k points with the batch SPRT: accepted
+    slots carry the oracle's exact count of their model (recounted from the device stream's
+    samples), rejected slots -1, every accepted count equal to the unfiltered batch's."""
+    pts, thr, B = cfg3_points, 2.0, 65536
+    with usac.Context(usac.ESTIMATOR.Fundamental, pts) as ctx:
+        ctx.set_device_sampler(usac.SAMPLER.Prosac)
+        ctx.set_score_chunks(96)
+        samples = ctx.draw_samples(B, seed=1, first_hyp=0)
+        ctx.set_sprt(False)
+        cf, _, bf = ctx.hypothesize_score(B=B, seed=1, first_hyp=0, thr=thr)
+        ctx.set_sprt(True, seed=1)
+        c, s, best = ctx.hypothesize_score(B=B, seed=1, first_hyp=0, thr=thr)
+        tested = ctx.sprt_tested()
+    occupied = cf >= 0
+    acc = c >= 0
+    assert (acc <= occupied).all()
+    assert 1 <= acc.sum() <= 0.2 * occupied.sum()
+    np.testing.assert_array_equal(c[acc], cf[acc])
+    assert (s[acc] == c[acc].astype(np.float32)).all()
+    assert tested < 0.05 * occupied.sum() * len(pts)  # SPRT stops early on nearly every model
+    # oracle: the same samples through the reference's 7-point solver + Sampson count
+    est = oracle.Estimator(oracle.FUNDAMENTAL, pts)
+    slots = np.where(acc)[0]
+    om, onm = est.estimate_batch(samples[np.unique(slots // 3)])
+    row = {b: k for k, b in enumerate(np.unique(slots // 3))}
+    models = np.stack([om[row[sl // 3], sl % 3] for sl in slots])
+    assert all(sl % 3 < onm[row[sl // 3]] for sl in slots)
+    oc, _ = est.score_models(models, thr)
+    np.testing.assert_array_equal(c[acc], oc)
+    assert best["inliers"] == c.max() <= bf["inliers"]
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+@pytest.mark.parametrize("sampler", ["prosac", "uniform"])
+def test_cfg3_loop_sprt_identical(usac, oracle, cfg3_points, sampler, seed):
+    """PROSAC finds the model within ~10 iterations on quality-sorted data; the uniform run on
+    the same points in random order runs to max_iters (10 000) with ~1 000 SPRT rejections."""
+    thr = 2.0
+    if sampler == "prosac":
+        pts, osmp, smp = cfg3_points, oracle.SAMPLER_PROSAC, usac.SAMPLER.Prosac
+    else:
+        pts = np.ascontiguousarray(cfg3_points[np.random.default_rng(seed).permutation(len(cfg3_points))])
+        osmp, smp = oracle.SAMPLER_UNIFORM, usac.SAMPLER.Uniform
+    ref = oracle.ransac_run(oracle.FUNDAMENTAL, pts, thr, 0.95, seed, sampler=osmp, sprt=True)
+    m = usac.Model(thr, 7, 0.95, 7, usac.ESTIMATOR.Fundamental, smp)
+    m.ResetRandomGenerator(False)
+    m.setSeed(seed)
+    m.setSprt(True)
+    r = usac.Ransac(m, pts)
+    r.run()
+    out = r.getRansacOutput()
+    assert out.getNumberOfMainIterations() == ref["iters"]
+    assert [(i, c) for i, c, _ in r.records] == [(i, c) for i, c, _ in ref["records"]]
+    assert [np.float32(s) for _, _, s in r.records] == [np.float32(s) for _, _, s in ref["records"]]
+    assert out.raw["sprt_rejected"] == ref["sprt_rejected"]
+    assert out.raw["sprt_histories"] == ref["sprt_histories"]
+    assert out.raw["prosac_term_len"] == ref["prosac_term_len"]
+    assert (_bits(out.getModel()) == _bits(ref["model"])).all()
+    assert out.getNumberOfInliers() == ref["inliers"]
+    assert (out.getInliers() == ref["inlier_idx"]).all()

@@ -78,3 +78,26 @@ def test_prosac_speculative_batches_roll_back(usac, oracle):
     assert outs[0][:3] == outs[1][:3] == outs[2][:3]
     ref = oracle.ransac_run(oracle.FUNDAMENTAL, pts, 2.0, 0.99, 3, sampler=oracle.SAMPLER_PROSAC)
     assert outs[0][0] == ref["iters"]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_cfg1_generator_loop_identical(usac, oracle, seed):
+    """cfg1 (BASELINE configs[0]): Line2d + Uniform on 1 000 points from the reference's own
+    generator (Generate2DLinePoints restated; it rewrites dataset/line2d bit for bit at the
+    printed digits, test_oracle.py) -- the device loop equals the oracle's run."""
+    pts, gt = oracle.generate_line2d(seed, 3.0, 100, 900, 1000, 1000)
+    ref = oracle.ransac_run(oracle.LINE2D, pts, 10.0, 0.99, seed)
+    m = usac.Model(10.0, 2, 0.99, 7, usac.ESTIMATOR.Line2d, usac.SAMPLER.Uniform)
+    m.ResetRandomGenerator(False)
+    m.setSeed(seed)
+    r = usac.Ransac(m, pts)
+    r.run()
+    out = r.getRansacOutput()
+    assert out.getNumberOfMainIterations() == ref["iters"]
+    assert [(i, c) for i, c, _ in r.records] == [(i, c) for i, c, _ in ref["records"]]
+    assert (_bits(out.getModel()) == _bits(ref["model"])).all()
+    assert out.getNumberOfInliers() == ref["inliers"]
+    assert (out.getInliers() == ref["inlier_idx"]).all()
+    # the generator's line is found: |cos| between normals ~1
+    mdl = out.getModel()[:2]
+    assert abs(float(np.dot(mdl, gt[:2]))) / float(np.linalg.norm(mdl)) > 0.99

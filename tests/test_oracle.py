@@ -95,3 +95,18 @@ def test_line2d_generator(oracle):
     assert abs(float(np.hypot(gt[0], gt[1])) - 1.0) < 1e-6
     d = np.abs(pts[900:] @ gt[:2] + gt[2])
     assert d.max() < 3.0 * 1.5
+
+
+def test_line2d_generator_reproduces_reference_dataset(oracle, line2d_scenes):
+    """The restated Generate2DLinePoints, run as generate_syntectic_dataset runs it
+    (eight scenes on one rand() stream from the default seed), rewrites the reference's own
+    dataset/line2d/*.txt: every coordinate and GT line equal at the digits the reference
+    printed (ostream default precision 6)."""
+    fmt = np.vectorize(lambda v: "%.6g" % v)
+    gen = oracle.generate_line2d_dataset()
+    assert sorted(n for n, _, _ in gen) == sorted(line2d_scenes)
+    for name, pts, gt in gen:
+        ref_pts, ref_model, _ = line2d_scenes[name]
+        assert pts.shape == ref_pts.shape, name
+        assert (fmt(pts.astype(np.float64)) == fmt(ref_pts.astype(np.float64))).all(), name
+        assert (fmt(gt.astype(np.float64)) == fmt(ref_model.astype(np.float64))).all(), name
