@@ -58,3 +58,17 @@ def test_merge_records_total_order(usac):
     assert best.hyp_index == 2 and best.inliers == 10
     recs.append(R(9, 10, 3.5, (ctypes.c_float * 9)(), 1))
     assert usac.merge_records(recs).hyp_index == 9
+
+
+def test_cpp_consumer_compiles_and_links(usac):
+    """include/usac_gpu.hpp (the usac_gpu:: plugin layer) compiles with g++ -std=c++11 -Werror in
+    a reference-style consumer that links libransac_amd.so; its ABI check needs no GPU."""
+    import json
+    import subprocess
+
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "cpp")], check=True)
+    r = subprocess.run([os.path.join(ROOT, "tests", "cpp", "build", "consumer"), "abi"], capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout)
+    assert d["abi"] == d["header"] == usac.lib().usac_abi_version()
