@@ -30,7 +30,10 @@
  *                                  (sprt.hpp:191-317, 332-355)
  *   usac_prosac_samples            ProsacSampler::generateSample (prosac_sampler.hpp:117-172)
  *   usac_set_device_sampler        Sampler choice of the throughput batches (Uniform / PROSAC
- *   usac_draw_samples              schedule, prosac_sampler.hpp:62-172) and its samples
+ *   usac_draw_samples              schedule, prosac_sampler.hpp:62-172 / NAPSAC grid,
+ *   usac_set_cell_size             napsac_sampler.hpp:100-138) and its samples
+ *   usac_grid_neighbors            NearestNeighbors::getGridNearestNeighbors
+ *                                  (nearest_neighbors.cpp:160-202) built on the device
  *   usac_sprt_pool                 SPRT ctor pool + A0 (sprt.hpp:89-175)
  *   usac_ransac_run                Ransac::run + RansacOutput (ransac.cpp:14-238,
  *                                  ransac_output.hpp:29-97), Uniform sampler
@@ -50,7 +53,7 @@
 extern "C" {
 #endif
 
-#define USAC_ABI_VERSION 7
+#define USAC_ABI_VERSION 8
 
 /* = enum ESTIMATOR (usac/model.hpp:10) */
 enum { USAC_LINE2D = 1, USAC_HOMOGRAPHY = 2, USAC_FUNDAMENTAL = 3, USAC_ESSENTIAL = 4 };
@@ -206,13 +209,29 @@ int usac_set_sprt(usac_ctx *ctx, int enable, uint32_t seed, double epsilon, doub
 /* pool points the SPRT tested in the last batch (the scoring work actually done) */
 int usac_sprt_tested(usac_ctx *ctx, uint64_t *points_tested);
 /* Sampler of the throughput batches' device stream (usac_hypothesize_score with samples ==
- * NULL, usac_hypothesize_async): USAC_SAMPLER_UNIFORM (default) or USAC_SAMPLER_PROSAC --
+ * NULL, usac_hypothesize_async): USAC_SAMPLER_UNIFORM (default), USAC_SAMPLER_NAPSAC (grid
+ * neighbours of usac_set_cell_size's cell, default 50, built on the device: the initial point
+ * uniform over the points with >= m neighbours, then m - 1 consecutive entries of its
+ * neighbour list from a random phase -- napsac_sampler.hpp:100-138, whose cursor persists
+ * across samples; uniform samples when no point qualifies; 4-column points) or
+ * USAC_SAMPLER_PROSAC --
  * hypothesis h (the global index first_hyp + b) uses the reference's PROSAC subset schedule
  * (growth function prosac_sampler.hpp:62-114, termination_length = n; points must be sorted
  * by quality): the subset's last point plus m - 1 distinct points before it, for
  * h < T_N = 200000, uniform afterwards (prosac_sampler.hpp:117-172).  The random draws are
  * the device SplitMix64 stream, not the host mt19937 (usac_ransac_run keeps that one). */
 int usac_set_device_sampler(usac_ctx *ctx, int sampler);
+/* Grid cell size of the device NAPSAC sampler (model.hpp:43, default 50). */
+int usac_set_cell_size(usac_ctx *ctx, int cell_size);
+/* NearestNeighbors::getGridNearestNeighbors (nearest_neighbors.cpp:160-202) on the device:
+ * cell ((int)(x1/cs), (int)(y1/cs), (int)(x2/cs), (int)(y2/cs)), fp32 division.  CSR (every
+ * output nullable, host memory): cell[n] (cells numbered in order of first appearance),
+ * rank[n] (position in the cell), start[n_cells + 1], members[n] (cells in order, ascending
+ * index) -- point i's neighbours are its cell's members except itself, ascending -- and
+ * eligible[n_eligible] = the points with >= sample-size neighbours (NAPSAC, Q18), ascending.
+ * usac_ransac_run's NAPSAC / graph-cut grids are this one. */
+int usac_grid_neighbors(usac_ctx *ctx, int cell_size, uint32_t *n_cells, uint32_t *cell, uint32_t *rank,
+                        uint32_t *start, int32_t *members, int32_t *eligible, uint32_t *n_eligible);
 /* The device stream's samples for hypotheses first_hyp .. first_hyp + B - 1 (B x m int32,
  * host memory): what the solve kernels draw.  For tests. */
 int usac_draw_samples(usac_ctx *ctx, uint32_t B, uint64_t seed, uint64_t first_hyp, int32_t *out);

@@ -101,7 +101,7 @@ ABI_SYMBOLS = [
     "usac_hypothesize_score", "usac_hypothesize_async", "usac_fetch_best", "usac_sync", "usac_last_timings",
     "usac_set_score_chunks", "usac_set_score_variant", "usac_last_counts", "usac_std_termination", "usac_ransac_run", "usac_ransac_run_sharded", "usac_uniform_samples",
     "usac_prosac_samples", "usac_sprt_pool", "usac_set_sprt", "usac_sprt_tested", "usac_set_device_sampler",
-    "usac_draw_samples",
+    "usac_draw_samples", "usac_set_cell_size", "usac_grid_neighbors",
     "usac_comm_unique_id", "usac_comm_init", "usac_allgather_records", "usac_merge_records",
 ]
 
@@ -164,6 +164,8 @@ def lib():
         "usac_set_sprt": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_uint32, ctypes.c_double, ctypes.c_double]),
         "usac_set_device_sampler": (ctypes.c_int, [_vp, ctypes.c_int]),
         "usac_draw_samples": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, _vp]),
+        "usac_set_cell_size": (ctypes.c_int, [_vp, ctypes.c_int]),
+        "usac_grid_neighbors": (ctypes.c_int, [_vp, ctypes.c_int, u32p, u32p, u32p, u32p, i32p, i32p, u32p]),
         "usac_sprt_tested": (ctypes.c_int, [_vp, _P(ctypes.c_uint64)]),
         "usac_comm_unique_id": (ctypes.c_int, [u8p]),
         "usac_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, u8p]),
@@ -370,9 +372,31 @@ class Context:
         self._check(lib().usac_set_sprt(self._h, 1 if enable else 0, seed, epsilon, delta), "set_sprt")
 
     def set_device_sampler(self, sampler):
-        """Sampler of the throughput batches' device stream: SAMPLER.Uniform or SAMPLER.Prosac
-        (the reference's PROSAC subset schedule; points sorted by quality)."""
+        """Sampler of the throughput batches' device stream: SAMPLER.Uniform, SAMPLER.Prosac
+        (the reference's PROSAC subset schedule; points sorted by quality) or SAMPLER.Napsac
+        (grid neighbours built on the device, cell size of set_cell_size)."""
         self._check(lib().usac_set_device_sampler(self._h, int(sampler)), "set_device_sampler")
+
+    def set_cell_size(self, cell_size):
+        """Grid cell of the device NAPSAC sampler (model.hpp:43, default 50)."""
+        self._check(lib().usac_set_cell_size(self._h, int(cell_size)), "set_cell_size")
+
+    def grid_neighbors(self, cell_size):
+        """NearestNeighbors::getGridNearestNeighbors on the device -> dict of the CSR: cell, rank,
+        start (n_cells + 1), members, and eligible (points with >= m neighbours)."""
+        n = self.n
+        nc, ne = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        cell = np.zeros(n, dtype=np.uint32)
+        rank = np.zeros(n, dtype=np.uint32)
+        start = np.zeros(n + 1, dtype=np.uint32)
+        members = np.zeros(n, dtype=np.int32)
+        elig = np.zeros(n, dtype=np.int32)
+        u32 = ctypes.c_uint32
+        self._check(lib().usac_grid_neighbors(self._h, int(cell_size), ctypes.byref(nc), _ptr(cell, u32),
+                                              _ptr(rank, u32), _ptr(start, u32), _ptr(members, ctypes.c_int32),
+                                              _ptr(elig, ctypes.c_int32), ctypes.byref(ne)), "grid_neighbors")
+        return {"cell": cell, "rank": rank, "start": start[: nc.value + 1].copy(), "members": members,
+                "eligible": elig[: ne.value].copy()}
 
     def draw_samples(self, B, seed, first_hyp=0):
         """The device stream's samples for hypotheses first_hyp .. first_hyp + B - 1 (B x m)."""

@@ -74,6 +74,11 @@ struct usac_ctx {
     DevBuf lo_max, lo_lists, lo_pos, lo_ns, lo_thrs, lo_slots, lo_models, lo_ok, lo_cnts, lo_sums, lo_q, lo_part,
         lo_ws, lo_scr;
     DevBuf knn_idx, knn_d2;  // KNN neighbour table (usac_knn, NAPSAC KNN)
+    // grid neighbours (build_grid): CSR of the cells of size grid_cs, NAPSAC-eligible points
+    DevBuf grid_cell, grid_rank, grid_start, grid_members, grid_elig, grid_ws;
+    int grid_cs = 0;        // cell size the grid was built for (0 = none)
+    int cell_size = 50;     // model.hpp:43, the device NAPSAC sampler's grid
+    uint32_t grid_n_cells = 0, grid_n_elig = 0;
     DevBuf gc_err;           // graph-cut LO: residuals of the model being labelled
     DevBuf e5_ws;                      // staged 5-point solver workspace
     // throughput SPRT (usac_set_sprt): batch-fixed test on the pool-ordered points
@@ -158,8 +163,67 @@ int ensure_single(usac_ctx *c) {
 
 usac::DevSampler dev_sampler(const usac_ctx *c, uint64_t seed) {
     const bool prosac = c->dev_sampler == USAC_SAMPLER_PROSAC;
-    return usac::DevSampler{seed, prosac ? c->prosac_tab.as<uint32_t>() : nullptr,
-                            prosac ? (uint32_t)(c->prosac_tab.bytes / sizeof(uint32_t)) : 0u};
+    usac::DevSampler ds{};
+    ds.seed = seed;
+    ds.prosac = prosac ? c->prosac_tab.as<uint32_t>() : nullptr;
+    ds.prosac_len = prosac ? (uint32_t)(c->prosac_tab.bytes / sizeof(uint32_t)) : 0u;
+    if (c->dev_sampler == USAC_SAMPLER_NAPSAC) {
+        ds.nap_n_eligible = c->grid_n_elig;
+        ds.nap_cell = c->grid_cell.as<uint32_t>();
+        ds.nap_rank = c->grid_rank.as<uint32_t>();
+        ds.nap_start = c->grid_start.as<uint32_t>();
+        ds.nap_members = c->grid_members.as<int32_t>();
+        ds.nap_eligible = c->grid_elig.as<int32_t>();
+    }
+    return ds;
+}
+
+// NearestNeighbors::getGridNearestNeighbors (nearest_neighbors.cpp:160-202) on the device for
+// cell size cs (kept until another size is asked for).  Cells are packed 16 bits per
+// dimension relative to the dataset box's lowest cell.
+int ensure_grid(usac_ctx *c, int cs) {
+    if (c->grid_cs == cs) return USAC_OK;
+    if (c->cols != 4) return fail(c, USAC_ERR_ARG, "grid neighbours need 4-column points (SURVEY Q17)");
+    if (cs <= 0) return fail(c, USAC_ERR_ARG, "grid cell_size must be > 0");
+    const float e[4] = {c->ext.x, c->ext.y, c->ext.z, c->ext.w};
+    int lo[4];
+    for (int j = 0; j < 4; j++) {
+        lo[j] = (int)(-e[j] / (float)cs);
+        if ((long long)(int)(e[j] / (float)cs) - lo[j] > 65535)
+            return fail(c, USAC_ERR_UNSUPPORTED, "grid: more than 65536 cells along one dimension");
+    }
+    const size_t n = c->n;
+    HIP_TRY(c, hipSetDevice(c->device));
+    HIP_TRY(c, c->grid_cell.reserve(sizeof(uint32_t) * n));
+    HIP_TRY(c, c->grid_rank.reserve(sizeof(uint32_t) * n));
+    HIP_TRY(c, c->grid_start.reserve(sizeof(uint32_t) * (n + 1)));
+    HIP_TRY(c, c->grid_members.reserve(sizeof(int32_t) * n));
+    HIP_TRY(c, c->grid_elig.reserve(sizeof(int32_t) * n));
+    HIP_TRY(c, c->grid_ws.reserve(usac::grid_workspace_bytes(c->n)));
+    c->grid_cs = 0;
+    HIP_TRY(c, usac::build_grid(c->stream, c->pts.as<float4>(), c->n, cs, make_int4(lo[0], lo[1], lo[2], lo[3]), c->m,
+                                c->grid_ws.p, c->grid_cell.as<uint32_t>(), c->grid_rank.as<uint32_t>(),
+                                c->grid_start.as<uint32_t>(), c->grid_members.as<int32_t>(),
+                                c->grid_elig.as<int32_t>(), &c->grid_n_cells, &c->grid_n_elig));
+    c->grid_cs = cs;
+    return USAC_OK;
+}
+
+// the device grid as the host loop's GridNeighbors (bit-identical to building it on the host)
+int download_grid(usac_ctx *c, int cs, std::unique_ptr<usac::GridNeighbors> &out) {
+    int rc = ensure_grid(c, cs);
+    if (rc) return rc;
+    std::vector<uint32_t> cell(c->n), rank(c->n), start((size_t)c->grid_n_cells + 1);
+    std::vector<int32_t> members(c->n);
+    HIP_TRY(c, hipMemcpyAsync(cell.data(), c->grid_cell.p, sizeof(uint32_t) * c->n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(rank.data(), c->grid_rank.p, sizeof(uint32_t) * c->n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(start.data(), c->grid_start.p, sizeof(uint32_t) * start.size(), hipMemcpyDeviceToHost,
+                              c->stream));
+    HIP_TRY(c, hipMemcpyAsync(members.data(), c->grid_members.p, sizeof(int32_t) * c->n, hipMemcpyDeviceToHost,
+                              c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    out.reset(new usac::GridNeighbors(std::move(cell), std::move(rank), std::move(start), std::move(members)));
+    return USAC_OK;
 }
 
 // solve (samples on device, or device RNG when samples_dev == nullptr) into c->models
@@ -901,7 +965,8 @@ void usac_destroy(usac_ctx *c) {
                       &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok,
                       &c->rec_send, &c->rec_all, &c->tv_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
-                      &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2, &c->gc_err, &c->x_send,
+                      &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2, &c->gc_err, &c->grid_cell, &c->grid_rank, &c->grid_start,
+                      &c->grid_members, &c->grid_elig, &c->grid_ws, &c->x_send,
                       &c->x_recv})
         b->release();
     for (auto &ev : c->ev)
@@ -1170,7 +1235,12 @@ int usac_uniform_samples(uint32_t seed, uint32_t n_points, uint32_t m, uint32_t 
 }
 
 int usac_set_device_sampler(usac_ctx *c, int sampler) {
-    if (!c || (sampler != USAC_SAMPLER_UNIFORM && sampler != USAC_SAMPLER_PROSAC)) return USAC_ERR_ARG;
+    if (!c || (sampler != USAC_SAMPLER_UNIFORM && sampler != USAC_SAMPLER_PROSAC && sampler != USAC_SAMPLER_NAPSAC))
+        return USAC_ERR_ARG;
+    if (sampler == USAC_SAMPLER_NAPSAC) {
+        const int rc = ensure_grid(c, c->cell_size);
+        if (rc) return rc;
+    }
     if (sampler == USAC_SAMPLER_PROSAC) {
         if (c->n < c->m) return fail(c, USAC_ERR_ARG, "PROSAC needs n >= sample size");
         // the subset sequence of ProsacSampler::generateSample with termination_length = n
@@ -1188,6 +1258,33 @@ int usac_set_device_sampler(usac_ctx *c, int sampler) {
         c->prosac_tab.bytes = sizeof(uint32_t) * T;
     }
     c->dev_sampler = sampler;
+    return USAC_OK;
+}
+
+int usac_set_cell_size(usac_ctx *c, int cell_size) {
+    if (!c || cell_size <= 0) return USAC_ERR_ARG;
+    c->cell_size = cell_size;
+    return c->dev_sampler == USAC_SAMPLER_NAPSAC ? ensure_grid(c, cell_size) : USAC_OK;
+}
+
+int usac_grid_neighbors(usac_ctx *c, int cell_size, uint32_t *n_cells, uint32_t *cell, uint32_t *rank, uint32_t *start,
+                        int32_t *members, int32_t *eligible, uint32_t *n_eligible) {
+    if (!c) return USAC_ERR_ARG;
+    int rc = ensure_grid(c, cell_size);
+    if (rc) return rc;
+    const size_t n = c->n;
+    if (n_cells) *n_cells = c->grid_n_cells;
+    if (n_eligible) *n_eligible = c->grid_n_elig;
+    if (cell) HIP_TRY(c, hipMemcpyAsync(cell, c->grid_cell.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    if (rank) HIP_TRY(c, hipMemcpyAsync(rank, c->grid_rank.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    if (start)
+        HIP_TRY(c, hipMemcpyAsync(start, c->grid_start.p, 4 * ((size_t)c->grid_n_cells + 1), hipMemcpyDeviceToHost,
+                                  c->stream));
+    if (members) HIP_TRY(c, hipMemcpyAsync(members, c->grid_members.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    if (eligible && c->grid_n_elig)
+        HIP_TRY(c, hipMemcpyAsync(eligible, c->grid_elig.p, 4 * (size_t)c->grid_n_elig, hipMemcpyDeviceToHost,
+                                  c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
     return USAC_OK;
 }
 
@@ -1414,10 +1511,8 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         knn_tab.resize((size_t)n * prm->knn);
         if ((rc = usac_knn(c, prm->knn, knn_tab.data(), nullptr))) return rc;
         napk.reset(new usac::NapsacKnnSampler(grng, knn_tab.data(), n, m, prm->knn));
-    } else if (napsac) {
-        std::vector<float> hp((size_t)n * 4);
-        HIP_TRY(c, hipMemcpy(hp.data(), c->pts.p, sizeof(float) * hp.size(), hipMemcpyDeviceToHost));
-        grid.reset(new usac::GridNeighbors(hp.data(), n, prm->cell_size));
+    } else if (napsac) {  // getGridNearestNeighbors on the device (kernels_grid.hip)
+        if ((rc = download_grid(c, prm->cell_size, grid))) return rc;
         nap.reset(new usac::NapsacSampler(grng, *grid, n, m));
     } else {
         uni.reset(new usac::UniformSampler(grng, n, m));
@@ -1432,10 +1527,8 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         if (gc_knn) {
             knn_tab.resize((size_t)n * prm->knn);
             if ((rc = usac_knn(c, prm->knn, knn_tab.data(), nullptr))) return rc;
-        } else {
-            std::vector<float> hp((size_t)n * 4);
-            HIP_TRY(c, hipMemcpy(hp.data(), c->pts.p, sizeof(float) * hp.size(), hipMemcpyDeviceToHost));
-            grid.reset(new usac::GridNeighbors(hp.data(), n, prm->cell_size));
+        } else if ((rc = download_grid(c, prm->cell_size, grid))) {
+            return rc;
         }
         gc.reset(new GcLo(c, prm, gc_knn ? knn_tab.data() : nullptr, prm->knn, grid.get()));
         if ((rc = gc->reserve())) return rc;

@@ -47,7 +47,18 @@ __device__ __forceinline__ void draw_unique(uint64_t &st, uint32_t n, int32_t *s
 template <int M>
 __device__ __forceinline__ void draw_sample(const DevSampler &ds, uint64_t hyp, uint32_t n, int32_t (&s)[M]) {
     uint64_t st = ds.seed ^ (hyp * 0xD1B54A32D192ED03ull);
-    if (ds.prosac && hyp < ds.prosac_len) {
+    if (ds.nap_start && ds.nap_n_eligible) {  // NAPSAC (grid), see DevSampler
+        const int32_t init = ds.nap_eligible[((splitmix64(st) >> 32) * ds.nap_n_eligible) >> 32];
+        const uint32_t c = ds.nap_cell[init], rk = ds.nap_rank[init], b = ds.nap_start[c];
+        const uint32_t cnt = ds.nap_start[c + 1] - b - 1;  // neighbours, >= M
+        uint32_t j = (uint32_t)(((splitmix64(st) >> 32) * cnt) >> 32);
+        s[0] = init;
+#pragma unroll
+        for (int k = 1; k < M; k++) {
+            s[k] = ds.nap_members[b + (j < rk ? j : j + 1)];
+            j = j + 1 == cnt ? 0 : j + 1;
+        }
+    } else if (ds.prosac && hyp < ds.prosac_len) {
         const uint32_t sub = ds.prosac[hyp];  // >= M
         draw_unique<M - 1>(st, sub - 1, s);
         s[M - 1] = (int32_t)sub - 1;

@@ -514,6 +514,10 @@ class GridNeighbors {
         for (size_t c = 0; c < size.size(); c++) start_[c + 1] = start_[c] + size[c];
         for (uint32_t i = 0; i < n; i++) members_[start_[cell_[i]] + rank_[i]] = (int32_t)i;
     }
+    // the same CSR built on the device (build_grid, kernels_grid.hip)
+    GridNeighbors(std::vector<uint32_t> cell, std::vector<uint32_t> rank, std::vector<uint32_t> start,
+                  std::vector<int32_t> members)
+        : cell_(std::move(cell)), rank_(std::move(rank)), start_(std::move(start)), members_(std::move(members)) {}
     uint32_t count(uint32_t i) const { return start_[cell_[i] + 1] - start_[cell_[i]] - 1; }
     int32_t at(uint32_t i, uint32_t k) const { return members_[start_[cell_[i]] + (k < rank_[i] ? k : k + 1)]; }
 

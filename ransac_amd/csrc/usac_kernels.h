@@ -14,11 +14,31 @@ namespace usac {
 // reference's ProsacSampler uses for hypothesis h (prosac_sampler.hpp:117-172, growth
 // function of :62-114, termination_length = N) for h < prosac_len; later hypotheses are
 // uniform, as the reference's are after T_N = 200000.
+//
+// NAPSAC (grid, napsac_sampler.hpp:100-138) when nap_start != nullptr: the initial point is
+// drawn uniformly from the points with >= m grid neighbours (the reference draws from its
+// pool and skips the others, Q18 -- the same distribution), then m - 1 consecutive entries of
+// its neighbour list from a random phase (the reference walks them from a cursor that
+// persists across samples); no eligible point -> uniform samples (the reference turns
+// uniform after n failed draws).  Grid CSR as built by build_grid.
 struct DevSampler {
     uint64_t seed;
     const uint32_t *prosac;  // nullptr: uniform sampler
     uint32_t prosac_len;
+    uint32_t nap_n_eligible;
+    const uint32_t *nap_cell, *nap_rank, *nap_start;  // nap_start == nullptr: no NAPSAC
+    const int32_t *nap_members, *nap_eligible;
 };
+
+// Grid neighbours on the device (kernels_grid.hip): CSR bit-identical to usac_host.hpp's
+// GridNeighbors -- cell[n] (first-appearance numbering), rank[n], start[n_cells + 1],
+// members[n] -- plus eligible[] = points with >= m neighbours, ascending.  cmin = the lowest
+// cell of the dataset box per dimension (every cell - cmin must fit 16 bits).  Synchronises
+// `st` twice (cell and eligible counts).
+size_t grid_workspace_bytes(uint32_t n);
+hipError_t build_grid(hipStream_t st, const float4 *pts, uint32_t n, int cell_size, int4 cmin, uint32_t m, void *ws,
+                      uint32_t *cell, uint32_t *rank, uint32_t *start, int32_t *members, int32_t *eligible,
+                      uint32_t *n_cells, uint32_t *n_eligible);
 
 // device-drawn samples only (B x m int32), the stream the solve kernels use
 hipError_t launch_draw_samples(hipStream_t st, int m, uint32_t n, uint32_t B, DevSampler ds, uint64_t first_hyp,

@@ -59,3 +59,22 @@ def test_lo_improves_and_counts(oracle, lo):
     # LO runs inside the loop: the best minimal score it hands to the polish is never lower
     assert b["minimal_inliers"] >= a["records"][0][1]
     assert b["inliers"] >= 0.95 * a["inliers"]
+
+
+def test_grid_csr_restatement_matches_oracle(oracle):
+    """The numpy CSR the device grid is checked against (tests/helpers/grid_ref.py) gives every
+    point the oracle's neighbour list (orc_grid), negative coordinates included."""
+    from ransac_amd import synthetic
+    from tests.helpers.grid_ref import grid_csr
+
+    pts, _, _ = synthetic.homography_points(n=6000, inlier_ratio=0.2, seed=3, cluster=(500, 500, 150))
+    pts[::4, 1] -= 800.0
+    for cs in (50, 9):
+        g = grid_csr(pts, cs, 4)
+        lists = oracle.grid_neighbors(pts, cs)
+        for i in range(len(pts)):
+            c = g["cell"][i]
+            mem = g["members"][g["start"][c]:g["start"][c + 1]]
+            assert g["members"][g["start"][c] + g["rank"][i]] == i
+            np.testing.assert_array_equal(mem[mem != i], lists[i])
+        assert (np.array([len(x) for x in lists])[g["eligible"]] >= 4).all()
