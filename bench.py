@@ -45,8 +45,10 @@ def parse():
                     help="batch SPRT verification (reference initial epsilon/delta for the estimator); "
                          "default on for fundamental (cfg3), off otherwise")
     ap.add_argument("--no-sprt", dest="sprt", action="store_false")
-    ap.add_argument("--sampler", choices=["uniform", "prosac"], default=None,
-                    help="device sampler of the batches (default prosac for fundamental = cfg3, else uniform)")
+    ap.add_argument("--sampler", choices=["uniform", "prosac", "napsac"], default=None,
+                    help="device sampler of the batches (default prosac for fundamental = cfg3, else uniform); "
+                         "napsac = grid neighbours built on the device (cell 50), homography on the cfg5 "
+                         "generator's clustered points (100k by default)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--cfg5", action="store_true",
@@ -61,7 +63,7 @@ def parse():
     args = ap.parse_args()
     ess = args.estimator == "essential"
     if args.points is None:
-        args.points = 100000 if args.cfg5 else 50000 if ess else 10000
+        args.points = 100000 if args.cfg5 or args.sampler == "napsac" else 50000 if ess else 10000
     if args.threshold is None:
         args.threshold = 0.002 if ess else 2.0
     if args.chunks is None:
@@ -121,14 +123,16 @@ def cpu_baseline(kind, pts, thr, dlt_mode, seconds):
             "cpu_model": model, "nproc": os.cpu_count(), "cpus_available": avail}
 
 
-def parity_check(usac, kind, pts, thr, dlt_mode):
-    """Inlier-count match vs the reference path (CPU oracle) on 256 host-drawn samples."""
+def parity_check(usac, kind, pts, thr, dlt_mode, samples=None):
+    """Inlier-count match vs the reference path (CPU oracle) on 256 host-drawn samples (or the
+    given ones, e.g. the device NAPSAC stream's)."""
     from oracle import oracle as O
 
     fund = kind == "fundamental"
     ess = kind == "essential"
     m = 7 if fund else 5 if ess else 4
-    samples = O.uniform_samples(77, len(pts), m, 256)
+    if samples is None:
+        samples = O.uniform_samples(77, len(pts), m, 256)
     est = O.Estimator(O.FUNDAMENTAL if fund else O.ESSENTIAL if ess else O.HOMOGRAPHY, pts, dlt_mode)
     om, onm = est.estimate_batch(samples)
     if ess:
@@ -401,8 +405,12 @@ def main():
         return cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank)
     fund = args.estimator == "fundamental"
     ess = args.estimator == "essential"
+    napsac = args.sampler == "napsac"
     if fund or ess:
         pts, _, _ = synthetic.fundamental_points(n=args.points, inlier_ratio=0.3, seed=args.seed, normalized=ess)
+    elif napsac:  # the cfg5 generator: inliers clustered (NAPSAC's premise), 20 %
+        pts, _, _ = synthetic.homography_points(n=args.points, inlier_ratio=0.2, seed=args.seed,
+                                                cluster=(500, 500, 150))
     else:
         pts, _, _ = synthetic.homography_points(n=args.points, inlier_ratio=0.3, seed=args.seed)
     dlt_mode = 0 if args.dlt == "thin" else 1
@@ -414,6 +422,8 @@ def main():
         c.set_score_chunks(args.chunks)
         if args.sampler == "prosac":  # points are quality-sorted (synthetic generator)
             c.set_device_sampler(usac.SAMPLER.Prosac)
+        elif napsac:  # grid neighbours built on the device at context setup (not timed)
+            c.set_device_sampler(usac.SAMPLER.Napsac)
     ctx = ctxs[0]
     exchange = "none"
     if world > 1:  # the per-batch best-record exchange: RCCL all-gather on the context stream
@@ -538,7 +548,8 @@ def main():
             "solve_kernel_ms": float(np.mean(solo_solve)), "kernel_ms_in_pipeline": float(np.mean(score_ms)),
             "solve_kernel_ms_in_pipeline": float(np.mean(solve_ms)),
             "batch_device_ms_in_pipeline": float(np.mean(batch_ms))})
-        smp_name = "Prosac (reference subset schedule, T_N = 200000)" if args.sampler == "prosac" else "Uniform"
+        smp_name = {"prosac": "Prosac (reference subset schedule, T_N = 200000)",
+                    "napsac": "Napsac (grid neighbours, cell 50, built on the device)"}.get(args.sampler, "Uniform")
         out = {
             "metric": "model hypotheses/sec (sample+solve+score) and inlier-count match vs ref",
             "value": value,
@@ -553,6 +564,8 @@ def main():
             "dtype": "f32",
             "data": ("synthetic (SURVEY §8(d) cfg3 generator: two views, 30% inliers, 0.5 px noise)" if fund else
                      "synthetic (SURVEY §8(d) cfg4 generator: cfg3 geometry in K^-1-normalised coordinates)" if ess
+                     else "synthetic (cfg5 generator: 20% inliers clustered around (500, 500), r = 150 px, uniform "
+                          "outliers)" if napsac
                      else "synthetic (SURVEY §8(d) cfg2 generator: 30% inliers, 1 px noise, 70% uniform outliers)"),
             "config": {"workload": ("cfg3%s: Fundamental_estimator (7-pt, oriented filter, Sampson) + "
                                     "%s sampler (device stream), %d correspondences, %d-hypothesis batch per "
@@ -562,9 +575,10 @@ def main():
                                     "sampler (device stream), %d correspondences, %d-hypothesis batch per GPU, "
                                     "%.3f models/sample" % (" + batch SPRT" if args.sprt else "", smp_name, n, B,
                                                             models_per_hyp)) if ess else
-                                   ("cfg2%s: Homography_estimator (4-pt DLT, %s) + %s sampler (device "
+                                   ("%s%s: Homography_estimator (4-pt DLT, %s) + %s sampler (device "
                                     "stream), %d correspondences, %d-hypothesis batch per GPU" %
-                                    (" + batch SPRT" if args.sprt else "", args.dlt, smp_name, n, B)),
+                                    ("cfg5 batches (throughput, no LO)" if napsac else "cfg2",
+                                     " + batch SPRT" if args.sprt else "", args.dlt, smp_name, n, B)),
                        "sampler": args.sampler,
                        "n_points": n, "batch_per_gpu": B, "threshold": args.threshold,
                        "score_chunks": args.chunks, "batches_in_flight": P,
@@ -573,7 +587,8 @@ def main():
             "best": {"inliers": int(best.inliers), "hyp_index": int(best.hyp_index)},
         }
         if world == 1:
-            out["parity"] = parity_check(usac, args.estimator, pts, args.threshold, dlt_mode)
+            out["parity"] = parity_check(usac, args.estimator, pts, args.threshold, dlt_mode,
+                                         samples=ctx.draw_samples(256, args.seed) if napsac else None)
             if args.cpu_seconds > 0:
                 out["cpu_baseline"] = cpu_baseline(args.estimator, pts, args.threshold, dlt_mode, args.cpu_seconds)
                 out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
