@@ -7,13 +7,14 @@
 //   k_inl_flags   grid over points: exact residual, per-block inlier count      (parallel)
 //   k_inl_scan    one workgroup: exclusive scan of the block counts -> offsets  (tiny)
 //   k_inl_compact grid over points: ordered compaction of indices and residuals (parallel)
-//   k_inl_sum     one workgroup: the sequential fp32 sum over the compacted residuals
-//                 (the only inherently serial part: one dependent add per inlier)
+//   seqsum        the sequential fp32 sum over the compacted residuals
+//                 (the reference's order; evaluated in parallel, bit-exactly, by launch_seqsum)
 #include <hip/hip_runtime.h>
 
 #include "usac_device.hpp"
 #include "usac_device_e5.hpp"
 #include "usac_kernels.h"
+#include "usac_seqsum.hpp"
 
 namespace usac {
 
@@ -50,10 +51,15 @@ __device__ __forceinline__ void inl_model(const float *model, float *sm) {
 // or the scalar thr).  Per model the scratch holds its block counts (nb padded to 64)
 // followed by its compacted residuals (n floats): inl_stride(n) words.  Every model's
 // result is exactly the single-model one (the kernels never mix models).
-__host__ __device__ __forceinline__ size_t inl_stride(uint32_t n) {
+// The residuals are followed by the model's seqsum scratch (one chain, 8-byte aligned: every
+// part of the stride is even).
+constexpr size_t kInlSeqWords = seq::scratch_bytes(1) / sizeof(uint32_t);
+
+__host__ __device__ __forceinline__ size_t inl_res_words(uint32_t n) {
     const uint32_t nb = (n + kInlBlock - 1) / kInlBlock;
-    return (size_t)((nb + 63) & ~63u) + n;
+    return (size_t)((nb + 63) & ~63u) + ((n + 1) & ~1u);
 }
+__host__ __device__ __forceinline__ size_t inl_stride(uint32_t n) { return inl_res_words(n) + kInlSeqWords; }
 
 // model slot of workgroup row b: slots[b] when a slot list is given (a subset of the W models)
 __device__ __forceinline__ uint32_t inl_slot(const uint32_t *slots, uint32_t b) { return slots ? slots[b] : b; }
@@ -147,64 +153,6 @@ __global__ __launch_bounds__(kInlBlock) void k_inl_compact(const void *__restric
     }
 }
 
-// the reference's sequential fp32 sum in point order (quality.hpp:85), one workgroup per
-// model: lane 0 adds the residuals of one 2048-entry LDS chunk in order (one dependent add
-// per inlier -- the only inherently serial part) while waves 1-3 stage the next chunk into
-// the other buffer with coalesced loads; one barrier per chunk.
-constexpr uint32_t kSumChunk = 2048;
-
-__global__ __launch_bounds__(256) void k_inl_sum(const uint32_t *__restrict__ scratch, uint32_t n_pts,
-                                                 const uint32_t *__restrict__ slots,
-                                                 const int32_t *__restrict__ totals, float *__restrict__ sums) {
-    __shared__ __attribute__((aligned(16))) float s_e[2][kSumChunk];
-    const uint32_t nb = (n_pts + kInlBlock - 1) / kInlBlock;
-    const uint32_t w = inl_slot(slots, blockIdx.x);
-    const float *errs = reinterpret_cast<const float *>(scratch + w * inl_stride(n_pts) + ((nb + 63) & ~63u));
-    const uint32_t n = (uint32_t)totals[w];
-    const uint32_t t = threadIdx.x;
-    const bool loader = t >= 64;
-    const uint32_t lt = t - 64;
-    const uint32_t nch = (n + kSumChunk - 1) / kSumChunk;
-    auto len = [&](uint32_t c) { return n - c * kSumChunk < kSumChunk ? n - c * kSumChunk : kSumChunk; };
-    if (loader && nch > 0)
-        for (uint32_t i = lt; i < len(0); i += 192) s_e[0][i] = errs[i];
-    __syncthreads();
-    float s = 0.f;
-    for (uint32_t c = 0; c < nch; c++) {
-        if (loader && c + 1 < nch) {
-            const uint32_t m1 = len(c + 1), base = (c + 1) * kSumChunk;
-            for (uint32_t i = lt; i < m1; i += 192) s_e[(c + 1) & 1][i] = errs[base + i];
-        }
-        if (t == 0) {
-            // 16 residuals in registers, the next 16 in flight from LDS
-            const uint32_t m = len(c);
-            const float *e = s_e[c & 1];
-            const float4 *v = reinterpret_cast<const float4 *>(e);
-            uint32_t k = 0;
-            if (m >= 16) {
-                float4 c0 = v[0], c1 = v[1], c2 = v[2], c3 = v[3];
-                for (; k + 32 <= m; k += 16) {
-                    const uint32_t j = (k + 16) / 4;
-                    const float4 n0 = v[j], n1 = v[j + 1], n2 = v[j + 2], n3 = v[j + 3];
-                    s += c0.x; s += c0.y; s += c0.z; s += c0.w;
-                    s += c1.x; s += c1.y; s += c1.z; s += c1.w;
-                    s += c2.x; s += c2.y; s += c2.z; s += c2.w;
-                    s += c3.x; s += c3.y; s += c3.z; s += c3.w;
-                    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
-                }
-                s += c0.x; s += c0.y; s += c0.z; s += c0.w;
-                s += c1.x; s += c1.y; s += c1.z; s += c1.w;
-                s += c2.x; s += c2.y; s += c2.z; s += c2.w;
-                s += c3.x; s += c3.y; s += c3.z; s += c3.w;
-                k += 16;
-            }
-            for (; k < m; k++) s += e[k];
-        }
-        __syncthreads();
-    }
-    if (t == 0) sums[w] = s;
-}
-
 hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *models,
                                 uint32_t W, float thr, const float *thrs, const uint32_t *slots, int32_t *idx,
                                 size_t idx_stride, int32_t *counts, float *sums, void *scratch) {
@@ -218,7 +166,6 @@ hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, 
         hipLaunchKernelGGL(k_inl_scan, dim3(W), dim3(1024), 0, st, scr, n, nb, slots, counts);                         \
         hipLaunchKernelGGL(k_inl_compact<E>, grid, dim3(kInlBlock), 0, st, pts, n, models, thr, thrs, slots, scr, \
                            idx, idx_stride);                                                                     \
-        hipLaunchKernelGGL(k_inl_sum, dim3(W), dim3(256), 0, st, scr, n, slots, counts, sums);                         \
     } while (0)
     switch (estimator) {
         case USAC_LINE2D: INL(USAC_LINE2D); break;
@@ -228,7 +175,13 @@ hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, 
         default: return hipErrorInvalidValue;
     }
 #undef INL
-    return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // the reference's sequential fp32 Σ in point order (quality.hpp:85) over the compacted residuals
+    const size_t stride = inl_stride(n), res0 = (nb + 63) & ~63u;
+    return launch_seqsum(st, 1, false, reinterpret_cast<const float *>(scr + res0), stride,
+                         reinterpret_cast<const uint32_t *>(counts), 0, W, slots, scr + inl_res_words(n),
+                         sizeof(uint32_t) * stride, false, sums);
 }
 
 // every point's exact residual under one model (Estimator::GetError, e.g. for the graph-cut

@@ -11,6 +11,7 @@
 
 #include "usac_device.hpp"
 #include "usac_kernels.h"
+#include "usac_seqsum.hpp"
 
 namespace usac {
 
@@ -42,174 +43,139 @@ __global__ __launch_bounds__(256) void k_gather(const P *__restrict__ pts, const
     q[w * q_stride + i] = pts[list[j]];
 }
 
-// normalizing transformation: lanes 0..3 = the four coordinate means, lanes 0..1 = the
-// two distance sums (each a sequential fp32 chain in point order, as the reference sums);
-// then every lane normalises a strided share of the points.  The chains are latency-bound:
-// waves 1-3 stage the NEXT 1024-point chunk into LDS (coalesced loads; for the distance pass
-// they also compute its sqrt terms) while lanes of wave 0 add the current chunk from the
-// other buffer -- one barrier per chunk, the staging hidden behind the chain.
+// normalizing transformation (GetNormalizingTransformation, normalizing_transformation.cpp:
+// 7-113): the four coordinate means and the two average distances are the reference's
+// sequential fp32 sums in point order, evaluated bit-exactly in parallel by launch_seqsum
+// (kernels_seqsum.hip); the kernels here produce the distance terms and apply the transforms.
+// Per-fit seq scratch (nonminimal_seq_stride): [0, kSeqA) the seqsum scratch of the 4 mean
+// chains (reused by the 2 distance chains), then the distance terms, double2 per point; after
+// the W slices, sums4[W][4] (coordinate sums) and dsum2[W][2] (distance sums).
+constexpr size_t kSeqA = seq::scratch_bytes(4);
+
+__host__ __device__ __forceinline__ size_t seq_stride(uint32_t nmax) {
+    return (kSeqA + 16 * (size_t)nmax + 255) & ~(size_t)255;
+}
+
+// distance terms sqrt((double)(xm * xm + ym * ym)) of both images (the reference's unqualified
+// sqrt of a float is C's double sqrt) and their fp64 segment sums (seqsum psum layout, 2 chains)
+__global__ __launch_bounds__(256) void k_norm_dist(const float4 *__restrict__ q_all, size_t q_stride,
+                                                   const uint32_t *__restrict__ ns, uint32_t n1, char *seq_all,
+                                                   size_t sstride, const float *__restrict__ sums4) {
+    __shared__ double red[2][256];
+    const uint32_t j = blockIdx.x, w = blockIdx.y;
+    const uint32_t n = ns ? ns[w] : n1, L = seq::seg_len(n);
+    if (j * L >= n) return;
+    const uint32_t e = (j + 1) * L < n ? (j + 1) * L : n;
+    const float4 *q = q_all + w * q_stride;
+    char *seq = seq_all + w * sstride;
+    double2 *sq = reinterpret_cast<double2 *>(seq + kSeqA);
+    const float mx1 = sums4[4 * w + 0] / (float)n, my1 = sums4[4 * w + 1] / (float)n;
+    const float mx2 = sums4[4 * w + 2] / (float)n, my2 = sums4[4 * w + 3] / (float)n;
+    double a0 = 0.0, a1 = 0.0;
+    for (uint32_t i = j * L + threadIdx.x; i < e; i += 256) {
+        const float4 p = q[i];
+        const float xm1 = p.x - mx1, ym1 = p.y - my1;
+        const float xm2 = p.z - mx2, ym2 = p.w - my2;
+        const double d1 = sqrt((double)(xm1 * xm1 + ym1 * ym1)), d2 = sqrt((double)(xm2 * xm2 + ym2 * ym2));
+        sq[i] = make_double2(d1, d2);
+        a0 += d1;
+        a1 += d2;
+    }
+    red[0][threadIdx.x] = a0;
+    red[1][threadIdx.x] = a1;
+    __syncthreads();
+    for (uint32_t h = 128; h > 0; h >>= 1) {
+        if (threadIdx.x < h) {
+            red[0][threadIdx.x] += red[0][threadIdx.x + h];
+            red[1][threadIdx.x] += red[1][threadIdx.x + h];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 2) reinterpret_cast<double *>(seq)[j * 2 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// T1, T2 from the sums (the reference's expressions) into ws, and q <- normalised points
 // ws layout (floats): [0..8] T1, [9..17] T2.
-constexpr uint32_t kNormChunk = 1024;
-
-__device__ __forceinline__ float chain_add_f32(float acc, const float *f, uint32_t m) {
-    // 16 values in registers, the next 16 in flight from LDS (stride 4 floats)
-    uint32_t k = 0;
-    if (m >= 16) {
-        float c[16];
+__global__ __launch_bounds__(256) void k_norm_apply(float4 *__restrict__ q_all, size_t q_stride,
+                                                    const uint32_t *__restrict__ ns, uint32_t n1,
+                                                    const float *__restrict__ sums4, const float *__restrict__ dsum2,
+                                                    float *ws_all) {
+    const uint32_t w = blockIdx.y;
+    const uint32_t n = ns ? ns[w] : n1;
+    float mean[4];
 #pragma unroll
-        for (int u = 0; u < 16; u++) c[u] = f[4 * u];
-        for (; k + 32 <= m; k += 16) {
-            float nx[16];
-#pragma unroll
-            for (int u = 0; u < 16; u++) nx[u] = f[4 * (k + 16 + u)];
-#pragma unroll
-            for (int u = 0; u < 16; u++) acc += c[u];
-#pragma unroll
-            for (int u = 0; u < 16; u++) c[u] = nx[u];
-        }
-#pragma unroll
-        for (int u = 0; u < 16; u++) acc += c[u];
-        k += 16;
-    }
-    for (; k < m; k++) acc += f[4 * k];
-    return acc;
-}
-
-// d = (float)((double)d + s_k): the reference's float += double (sqrt of a float in C)
-__device__ __forceinline__ float chain_add_f64(float d, const double *sq, uint32_t m) {
-    uint32_t k = 0;
-    if (m >= 16) {
-        double c[16];
-#pragma unroll
-        for (int u = 0; u < 16; u++) c[u] = sq[u];
-        for (; k + 32 <= m; k += 16) {
-            double nx[16];
-#pragma unroll
-            for (int u = 0; u < 16; u++) nx[u] = sq[k + 16 + u];
-#pragma unroll
-            for (int u = 0; u < 16; u++) d = (float)((double)d + c[u]);
-#pragma unroll
-            for (int u = 0; u < 16; u++) c[u] = nx[u];
-        }
-#pragma unroll
-        for (int u = 0; u < 16; u++) d = (float)((double)d + c[u]);
-        k += 16;
-    }
-    for (; k < m; k++) d = (float)((double)d + sq[k]);
-    return d;
-}
-
-__global__ __launch_bounds__(256) void k_normalize(float4 *__restrict__ q_all, size_t q_stride,
-                                                   const uint32_t *__restrict__ ns, uint32_t n1, float *ws_all) {
-    __shared__ float4 s_pts[2][kNormChunk];
-    __shared__ double s_sq[2][2][kNormChunk];
-    __shared__ float s_mean[4];
-    __shared__ float s_scale[2];
-    float4 *q = q_all + blockIdx.x * q_stride;
-    const uint32_t n = ns ? ns[blockIdx.x] : n1;
-    float *ws = ws_all + 18 * blockIdx.x;
+    for (int k = 0; k < 4; k++) mean[k] = sums4[4 * w + k] / (float)n;
+    const float s1 = (float)(M_SQRT2 / (double)(dsum2[2 * w + 0] / (float)n));
+    const float s2 = (float)(M_SQRT2 / (double)(dsum2[2 * w + 1] / (float)n));
+    const float t1[9] = {s1, 0.f, -mean[0] * s1, 0.f, s1, -mean[1] * s1, 0.f, 0.f, 1.f};
+    const float t2[9] = {s2, 0.f, -mean[2] * s2, 0.f, s2, -mean[3] * s2, 0.f, 0.f, 1.f};
     const uint32_t t = threadIdx.x;
-    const bool loader = t >= 64;
-    const uint32_t lt = t - 64;  // loader index, 192 loaders
-    const uint32_t nch = (n + kNormChunk - 1) / kNormChunk;
-    auto chunk_len = [&](uint32_t c) { return n - c * kNormChunk < kNormChunk ? n - c * kNormChunk : kNormChunk; };
-    // means
-    if (loader && nch > 0)
-        for (uint32_t i = lt; i < chunk_len(0); i += 192) s_pts[0][i] = q[i];
-    __syncthreads();
-    float acc = 0.f;
-    for (uint32_t c = 0; c < nch; c++) {
-        if (loader && c + 1 < nch) {
-            const uint32_t m1 = chunk_len(c + 1), base = (c + 1) * kNormChunk;
-            for (uint32_t i = lt; i < m1; i += 192) s_pts[(c + 1) & 1][i] = q[base + i];
-        }
-        if (t < 4) acc = chain_add_f32(acc, reinterpret_cast<const float *>(s_pts[c & 1]) + t, chunk_len(c));
-        __syncthreads();
+    if (blockIdx.x == 0 && t < 9) {
+        ws_all[18 * w + t] = t1[t];
+        ws_all[18 * w + 9 + t] = t2[t];
     }
-    if (t < 4) s_mean[t] = acc / (float)n;
-    __syncthreads();
-    const float mx1 = s_mean[0], my1 = s_mean[1], mx2 = s_mean[2], my2 = s_mean[3];
-    // average distances
-    auto stage_sq = [&](uint32_t c) {
-        const uint32_t m = chunk_len(c), base = c * kNormChunk;
-        for (uint32_t i = lt; i < m; i += 192) {
-            const float4 p = q[base + i];
-            const float xm1 = p.x - mx1, ym1 = p.y - my1;
-            const float xm2 = p.z - mx2, ym2 = p.w - my2;
-            s_sq[c & 1][0][i] = sqrt((double)(xm1 * xm1 + ym1 * ym1));
-            s_sq[c & 1][1][i] = sqrt((double)(xm2 * xm2 + ym2 * ym2));
-        }
-    };
-    if (loader && nch > 0) stage_sq(0);
-    __syncthreads();
-    float d = 0.f;
-    for (uint32_t c = 0; c < nch; c++) {
-        if (loader && c + 1 < nch) stage_sq(c + 1);
-        if (t < 2) d = chain_add_f64(d, s_sq[c & 1][t], chunk_len(c));
-        __syncthreads();
-    }
-    if (t < 2) s_scale[t] = (float)(M_SQRT2 / (double)(d / (float)n));
-    __syncthreads();
-    const float s1 = s_scale[0], s2 = s_scale[1];
-    const float t1[9] = {s1, 0.f, -s_mean[0] * s1, 0.f, s1, -s_mean[1] * s1, 0.f, 0.f, 1.f};
-    const float t2[9] = {s2, 0.f, -s_mean[2] * s2, 0.f, s2, -s_mean[3] * s2, 0.f, 0.f, 1.f};
-    if (t < 9) {
-        ws[t] = t1[t];
-        ws[9 + t] = t2[t];
-    }
-    __syncthreads();
-    for (uint32_t i = t; i < n; i += 256) {
-        float4 p = q[i];
-        float4 o;
-        o.x = t1[0] * p.x + t1[2];
-        o.y = t1[4] * p.y + t1[5];
-        o.z = t2[0] * p.z + t2[2];
-        o.w = t2[4] * p.w + t2[5];
-        q[i] = o;
-    }
+    const uint32_t i = blockIdx.x * 256 + t;
+    if (i >= n) return;
+    float4 *q = q_all + w * q_stride;
+    const float4 p = q[i];
+    float4 o;
+    o.x = t1[0] * p.x + t1[2];
+    o.y = t1[4] * p.y + t1[5];
+    o.z = t2[0] * p.z + t2[2];
+    o.w = t2[4] * p.w + t2[5];
+    q[i] = o;
 }
 
-// block partials of A^T A: one lane per 64-point block (the spec's unit), its 45
-// upper-triangle entries (row-major j <= k) accumulated in registers over the block's points
-// in order -- each point's rows are built once per lane, not once per entry.
-// FUND: one 8-point row per correspondence (eight_points.cpp:26-45), else two DLT rows.
+// block partials of A^T A: one lane per (64-point block, group of 9 of the 45 upper-triangle
+// entries, row-major j <= k) -- five lanes per block, the group wave-uniform (blockIdx.y) and
+// a compile-time constant in the body; each entry accumulated in registers over the block's
+// points in order (the spec's unit and order; the grouping only spreads the entries over
+// lanes).  FUND: one 8-point row per correspondence (eight_points.cpp:26-45), else two DLT rows.
+constexpr int kAtaGroups = 5;  // 45 = 5 x 9 entries
+
+template <bool FUND, int G>
+__device__ __forceinline__ void ata_group(const float4 *q, uint32_t b0, uint32_t b1, double *out) {
+    double acc[9];
+#pragma unroll
+    for (int e = 0; e < 9; e++) acc[e] = 0.0;
+    for (uint32_t i = b0; i < b1; i++) {
+        const float4 p = q[i];
+        double r0[9], r1[9];
+        if (FUND) fund_row(p.x, p.y, p.z, p.w, r0);
+        else dlt_rows(p.x, p.y, p.z, p.w, r0, r1);
+        int e = 0;
+#pragma unroll
+        for (int j = 0; j < 9; j++)
+#pragma unroll
+            for (int k = j; k < 9; k++, e++) {
+                if (e < 9 * G || e >= 9 * G + 9) continue;
+                if (FUND) acc[e - 9 * G] += r0[j] * r0[k];
+                else acc[e - 9 * G] += r0[j] * r0[k] + r1[j] * r1[k];
+            }
+    }
+#pragma unroll
+    for (int e = 0; e < 9; e++) out[9 * G + e] = acc[e];
+}
+
 template <bool FUND>
 __global__ __launch_bounds__(64) void k_ata_partial(const float4 *__restrict__ q_all, size_t q_stride,
                                                     const uint32_t *__restrict__ ns, uint32_t n1,
                                                     double *__restrict__ partial_all, size_t p_stride) {
-    const uint32_t w = blockIdx.y;
+    const uint32_t w = blockIdx.z;
     const uint32_t n = ns ? ns[w] : n1;
     const uint32_t blk = blockIdx.x * 64 + threadIdx.x;
     if ((FUND ? n <= 8 : 2 * n <= 9) || blk * kAtaBlock >= n) return;
     const float4 *q = q_all + w * q_stride;
     const uint32_t b0 = blk * kAtaBlock;
     const uint32_t b1 = b0 + kAtaBlock < n ? b0 + kAtaBlock : n;
-    double acc[45];
-#pragma unroll
-    for (int e = 0; e < 45; e++) acc[e] = 0.0;
-    for (uint32_t i = b0; i < b1; i++) {
-        const float4 p = q[i];
-        if (FUND) {
-            double r[9];
-            fund_row(p.x, p.y, p.z, p.w, r);
-            int e = 0;
-#pragma unroll
-            for (int j = 0; j < 9; j++)
-#pragma unroll
-                for (int k = j; k < 9; k++) acc[e++] += r[j] * r[k];
-        } else {
-            double r0[9], r1[9];
-            dlt_rows(p.x, p.y, p.z, p.w, r0, r1);
-            int e = 0;
-#pragma unroll
-            for (int j = 0; j < 9; j++)
-#pragma unroll
-                for (int k = j; k < 9; k++) acc[e++] += r0[j] * r0[k] + r1[j] * r1[k];
-        }
-    }
     double *out = partial_all + w * p_stride + (size_t)blk * 45;
-#pragma unroll
-    for (int e = 0; e < 45; e++) out[e] = acc[e];
+    switch (blockIdx.y) {
+        case 0: ata_group<FUND, 0>(q, b0, b1, out); break;
+        case 1: ata_group<FUND, 1>(q, b0, b1, out); break;
+        case 2: ata_group<FUND, 2>(q, b0, b1, out); break;
+        case 3: ata_group<FUND, 3>(q, b0, b1, out); break;
+        default: ata_group<FUND, 4>(q, b0, b1, out); break;
+    }
 }
 
 // Final solve, one wave: A^T A from the partials (lane e), round-robin Jacobi eigen over
@@ -294,8 +260,17 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
                 }
                 rem -= 9 - r;
             }
+            // the block partials in block order (spec), sixteen loads in flight per sixteen adds
             double acc = 0.0;
-            for (uint32_t c = 0; c < nblocks; c++) acc += partial[(size_t)c * 45 + t];
+            uint32_t c = 0;
+            for (; c + 16 <= nblocks; c += 16) {
+                double x[16];
+#pragma unroll
+                for (int u = 0; u < 16; u++) x[u] = partial[(size_t)(c + u) * 45 + t];
+#pragma unroll
+                for (int u = 0; u < 16; u++) acc += x[u];
+            }
+            for (; c < nblocks; c++) acc += partial[(size_t)c * 45 + t];
             A[j][k] = acc;
             A[k][j] = acc;
         }
@@ -308,6 +283,9 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
         // column)) -- every lane owns disjoint element pairs, 3 barriers per round
         __shared__ double s_cs[4][2];
         __shared__ int s_on[4];
+        __shared__ signed char s_rounds[9][4][2];  // the schedule in LDS (not a global load per use)
+        for (uint32_t i = t; i < 72; i += 64) (&s_rounds[0][0][0])[i] = (&kJacobiRounds[0][0][0])[i];
+        __syncthreads();
         for (int sweep = 0; sweep < 50; sweep++) {
             double off = 0.0, diag = 0.0;
             for (int p = 0; p < 9; p++) {
@@ -317,7 +295,7 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
             if (off <= 1e-30 * diag || off == 0.0) break;
             for (int r = 0; r < 9; r++) {
                 if (t < 4) {
-                    const int p = kJacobiRounds[r][t][0], qq = kJacobiRounds[r][t][1];
+                    const int p = s_rounds[r][t][0], qq = s_rounds[r][t][1];
                     const double apq = A[p][qq];
                     s_on[t] = apq != 0.0;
                     if (apq != 0.0) {
@@ -334,8 +312,8 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
                 int p = 0, qq = 0;
                 double c = 0.0, sn = 0.0;
                 if (t < 36) {
-                    p = kJacobiRounds[r][k][0];
-                    qq = kJacobiRounds[r][k][1];
+                    p = s_rounds[r][k][0];
+                    qq = s_rounds[r][k][1];
                     c = s_cs[k][0];
                     sn = s_cs[k][1];
                 }
@@ -476,9 +454,22 @@ hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pt
     float4 *q = static_cast<float4 *>(b.q);
     hipLaunchKernelGGL(k_gather<float4>, gg, dim3(256), 0, st, static_cast<const float4 *>(pts), b.base,
                        b.base_stride, b.pos, b.pos_stride, b.ns, b.n1, q, b.q_stride);
-    hipLaunchKernelGGL(k_normalize, dim3(b.W), dim3(256), 0, st, q, b.q_stride, b.ns, b.n1, b.ws);
+    {  // normalising transforms: sequential sums (seqsum), distance terms, apply
+        char *seq = static_cast<char *>(b.seq);
+        const size_t ss = seq_stride(b.nmax);
+        float *sums4 = reinterpret_cast<float *>(seq + b.W * ss), *dsum2 = sums4 + 4 * b.W;
+        hipError_t e = launch_seqsum(st, 4, false, q, 4 * b.q_stride, b.ns, b.n1, b.W, nullptr, seq, ss, false, sums4);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_norm_dist, dim3(seq::kSegMax, b.W), dim3(256), 0, st, q, b.q_stride, b.ns, b.n1, seq, ss,
+                           sums4);
+        e = launch_seqsum(st, 2, true, reinterpret_cast<const double *>(seq + kSeqA), ss / sizeof(double), b.ns, b.n1,
+                          b.W, nullptr, seq, ss, true, dsum2);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_norm_apply, dim3((b.nmax + 255) / 256 ? (b.nmax + 255) / 256 : 1, b.W), dim3(256), 0, st,
+                           q, b.q_stride, b.ns, b.n1, sums4, dsum2, b.ws);
+    }
     const uint32_t nblk = (b.nmax + kAtaBlock - 1) / kAtaBlock;
-    const dim3 ga(nblk ? (nblk + 63) / 64 : 1, b.W);
+    const dim3 ga(nblk ? (nblk + 63) / 64 : 1, kAtaGroups, b.W);
     if (estimator == USAC_HOMOGRAPHY) {
         hipLaunchKernelGGL(k_ata_partial<false>, ga, dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial, b.p_stride);
         hipLaunchKernelGGL(k_dlt_finish<false>, dim3(b.W), dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial,
@@ -492,5 +483,9 @@ hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pt
 }
 
 size_t nonminimal_partial_stride(uint32_t nmax) { return 45 * ((size_t)nmax / kAtaBlock + 2); }
+
+size_t nonminimal_seq_bytes(uint32_t nmax, uint32_t W) {
+    return seq_stride(nmax) * W + sizeof(float) * 6 * W;
+}
 
 }  // namespace usac

@@ -89,6 +89,7 @@ struct usac_ctx {
     uint32_t spk = 1;       // model slots per hypothesis (3 for the 7-point solver)
     // single-model / polish buffers
     DevBuf one_model, inl_idx, inl_cnt, inl_sum, inl_scratch, q, partial, ws, nm_model, nm_ok;
+    DevBuf nm_seq;          // normalisation scratch of the non-minimal fits (polish and LO)
     // comm
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -320,7 +321,10 @@ hipError_t enqueue_inliers(usac_ctx *c, const float *model_dev, float thr) {
 }
 
 hipError_t enqueue_nonminimal(usac_ctx *c, const int32_t *idx_dev, uint32_t n) {
+    hipError_t e = c->nm_seq.reserve(usac::nonminimal_seq_bytes(n, 1));
+    if (e != hipSuccess) return e;
     usac::NmBatch b{};
+    b.seq = c->nm_seq.p;
     b.base = idx_dev;
     b.n1 = n;
     b.W = 1;
@@ -423,6 +427,7 @@ struct LoRansac {
         HIP_TRY(c, c->lo_sums.reserve(sizeof(float) * W));
         HIP_TRY(c, c->lo_q.reserve(sizeof(float) * c->cols * N * W));
         HIP_TRY(c, c->lo_part.reserve(sizeof(double) * usac::nonminimal_partial_stride(n) * W));
+        HIP_TRY(c, c->nm_seq.reserve(usac::nonminimal_seq_bytes(n, (uint32_t)W)));
         HIP_TRY(c, c->lo_ws.reserve(sizeof(float) * 18 * W));
         HIP_TRY(c, c->lo_scr.reserve(usac::inliers_scratch_bytes(n, wmax)));
         return USAC_OK;
@@ -506,6 +511,7 @@ struct LoRansac {
             b.ws = c->lo_ws.as<float>();
             b.model_out = c->lo_models.as<float>();
             b.ok = c->lo_ok.as<int32_t>();
+            b.seq = c->nm_seq.p;
             HIP_TRY(c, usac::launch_nonminimal_batch(st, c->estimator, c->pts.p, b));
             HIP_TRY(c, hipMemcpyAsync(hmod.data(), c->lo_models.p, sizeof(float) * 9 * W, hipMemcpyDeviceToHost, st));
             HIP_TRY(c, hipMemcpyAsync(hok.data(), c->lo_ok.p, sizeof(int32_t) * W, hipMemcpyDeviceToHost, st));
@@ -771,6 +777,7 @@ struct GcLo {
         HIP_TRY(c, c->lo_sums.reserve(sizeof(float) * W));
         HIP_TRY(c, c->lo_q.reserve(sizeof(float) * c->cols * limit * W));
         HIP_TRY(c, c->lo_part.reserve(sizeof(double) * usac::nonminimal_partial_stride(limit) * W));
+        HIP_TRY(c, c->nm_seq.reserve(usac::nonminimal_seq_bytes(limit, (uint32_t)W)));
         HIP_TRY(c, c->lo_ws.reserve(sizeof(float) * 18 * W));
         HIP_TRY(c, c->lo_scr.reserve(usac::inliers_scratch_bytes(n, (uint32_t)W)));
         HIP_TRY(c, c->gc_err.reserve(sizeof(float) * n));
@@ -872,6 +879,7 @@ struct GcLo {
         b.ws = c->lo_ws.as<float>();
         b.model_out = c->lo_models.as<float>();
         b.ok = c->lo_ok.as<int32_t>();
+        b.seq = c->nm_seq.p;
         HIP_TRY(c, usac::launch_nonminimal_batch(st, c->estimator, c->pts.p, b));
         HIP_TRY(c, usac::launch_inliers_batch(st, c->estimator, c->pts.p, n, c->lo_models.as<float>(), W, thr, nullptr,
                                               nullptr, nullptr, 0, c->lo_cnts.as<int32_t>(), c->lo_sums.as<float>(),
@@ -962,7 +970,7 @@ void usac_destroy(usac_ctx *c) {
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
                       &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->inl_scratch, &c->e5_ws, &c->one_model,
-                      &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok,
+                      &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq,
                       &c->rec_send, &c->rec_all, &c->tv_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
                       &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2, &c->gc_err, &c->grid_cell, &c->grid_rank, &c->grid_start,

@@ -127,6 +127,18 @@ size_t inliers_scratch_bytes(uint32_t n, uint32_t W);
 hipError_t launch_point_errors(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *model,
                                float *errors);
 
+// the reference's sequential fp32 sums, in parallel and bit-exact (kernels_seqsum.hip): for
+// rows b < W (fit w = slots ? slots[b] : b), chains q < nch over the elements k < n_w
+// (ns ? ns[w] : n1) at vals[w * vstride + k * nch + q]; out[w * nch + q] = the left-to-right
+// sum from +0 -- op(s, x) = s + x (float vals) or (float)((double)s + y) (f64: double vals).
+// (nch, f64) in {(1, false), (4, false), (2, true)}.  scratch: fit w at scratch + w * sstride
+// (>= seqsum_scratch_bytes(nch), 8-byte aligned); have_psum: its fp64 segment sums are already
+// there (a producer kernel wrote them, layout in kernels_seqsum.hip).
+size_t seqsum_scratch_bytes(int nch);
+hipError_t launch_seqsum(hipStream_t st, int nch, bool f64, const void *vals, size_t vstride, const uint32_t *ns,
+                         uint32_t n1, uint32_t W, const uint32_t *slots, void *scratch, size_t sstride,
+                         bool have_psum, float *out);
+
 // W independent non-minimal fits (kernels_nonmin.hip).  Fit w: index list base + w *
 // base_stride, read through pos + w * pos_stride when pos != nullptr; ns[w] points (device;
 // ns == nullptr: every fit has n1 points);
@@ -145,9 +157,11 @@ struct NmBatch {
     size_t p_stride;
     float *ws, *model_out;
     int32_t *ok;
+    void *seq;  // normalisation scratch, nonminimal_seq_bytes(nmax, W) (not used by line fits)
 };
 hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pts, const NmBatch &b);
 size_t nonminimal_partial_stride(uint32_t nmax);
+size_t nonminimal_seq_bytes(uint32_t nmax, uint32_t W);
 
 // k nearest neighbours of every point (kernels_knn.hip, nearest_neighbors.cpp:69-128):
 // idx / d2 (nullable) n x k, self excluded, ascending distance, ties by index; 1 <= k <= 32
