@@ -10,7 +10,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -23,26 +25,134 @@ namespace {
 
 constexpr uint32_t kDefaultBatch = 8192;
 
+// Device memory of the contexts comes from a process-wide cache per device: a context is
+// typically created per Ransac::run (as the reference constructs its Ransac per run), and
+// hipMalloc / hipFree -- the latter synchronising the whole device -- cost milliseconds per
+// context.  Blocks are kept in power-of-two size classes (>= 4 KB); a released block goes back
+// to its class after its context's stream has drained (usac_destroy synchronises first), a
+// block replaced by a larger one only after the device has (reserve() below), so no block is
+// handed out while a kernel may still use it.  At most kPoolCap bytes per device are cached.
+constexpr size_t kPoolCap = size_t(16) << 30;
+
+struct DevPool {
+    std::mutex mu;
+    std::multimap<std::pair<int, size_t>, void *> free;  // (device, class bytes) -> block
+    std::map<int, size_t> cached;                         // bytes held per device
+    static DevPool &get() {
+        static DevPool *pool = new DevPool();  // never destroyed: no hipFree after runtime teardown
+        return *pool;
+    }
+    static size_t size_class(size_t b) {
+        size_t c = 4096;
+        while (c < b) c <<= 1;
+        return c;
+    }
+    hipError_t alloc(size_t b, void **p, size_t *got) {
+        const size_t c = size_class(b);
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        {
+            std::lock_guard<std::mutex> g(mu);
+            auto it = free.find({dev, c});
+            if (it != free.end()) {
+                *p = it->second;
+                free.erase(it);
+                cached[dev] -= c;
+                *got = c;
+                return hipSuccess;
+            }
+        }
+        hipError_t e = hipMalloc(p, c);
+        if (e == hipSuccess) *got = c;
+        return e;
+    }
+    void give_back(void *p, size_t c) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (cached[dev] + c <= kPoolCap) {
+                free.emplace(std::make_pair(dev, c), p);
+                cached[dev] += c;
+                return;
+            }
+        }
+        (void)hipFree(p);
+    }
+};
+
 struct DevBuf {
     void *p = nullptr;
     size_t bytes = 0;
     hipError_t reserve(size_t b) {
         if (b <= bytes) return hipSuccess;
-        if (p) (void)hipFree(p);
+        if (p) {  // kernels of this context may still read the old block
+            (void)hipDeviceSynchronize();
+            DevPool::get().give_back(p, bytes);
+        }
         p = nullptr;
         bytes = 0;
-        hipError_t e = hipMalloc(&p, b);
-        if (e == hipSuccess) bytes = b;
-        return e;
+        return DevPool::get().alloc(b, &p, &bytes);
     }
-    void release() {
-        if (p) (void)hipFree(p);
+    void release() {  // the owner's stream has drained (usac_destroy)
+        if (p) DevPool::get().give_back(p, bytes);
         p = nullptr;
         bytes = 0;
     }
     template <class T>
     T *as() const {
         return static_cast<T *>(p);
+    }
+};
+
+// streams and events likewise: creating / destroying them per context costs more than a run
+struct StreamPool {
+    std::mutex mu;
+    std::multimap<int, hipStream_t> streams;
+    std::multimap<int, hipEvent_t> events;
+    static StreamPool &get() {
+        static StreamPool *pool = new StreamPool();
+        return *pool;
+    }
+    hipError_t stream(hipStream_t *s) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        {
+            std::lock_guard<std::mutex> g(mu);
+            auto it = streams.find(dev);
+            if (it != streams.end()) {
+                *s = it->second;
+                streams.erase(it);
+                return hipSuccess;
+            }
+        }
+        return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+    }
+    hipError_t event(hipEvent_t *ev) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        {
+            std::lock_guard<std::mutex> g(mu);
+            auto it = events.find(dev);
+            if (it != events.end()) {
+                *ev = it->second;
+                events.erase(it);
+                return hipSuccess;
+            }
+        }
+        return hipEventCreate(ev);
+    }
+    void give_back(hipStream_t s) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        std::lock_guard<std::mutex> g(mu);
+        streams.emplace(dev, s);
+    }
+    void give_back(hipEvent_t ev) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        std::lock_guard<std::mutex> g(mu);
+        events.emplace(dev, ev);
     }
 };
 
@@ -59,6 +169,7 @@ struct usac_ctx {
     DevBuf pts;
     DevBuf rec;             // fast-kernel point records (32 B / point)
     DevBuf prosac_tab;      // device PROSAC schedule: subset size per hypothesis (< T_N)
+    uint32_t prosac_len = 0;  // its entries
     int dev_sampler = USAC_SAMPLER_UNIFORM;
     DevBuf tv_part;         // two-view scorer scratch: pre-sort permutation, chunk partials
     DevBuf perm;            // hypothesis pre-sort order of the fast kernel (B + 2 uint32)
@@ -167,7 +278,7 @@ usac::DevSampler dev_sampler(const usac_ctx *c, uint64_t seed) {
     usac::DevSampler ds{};
     ds.seed = seed;
     ds.prosac = prosac ? c->prosac_tab.as<uint32_t>() : nullptr;
-    ds.prosac_len = prosac ? (uint32_t)(c->prosac_tab.bytes / sizeof(uint32_t)) : 0u;
+    ds.prosac_len = prosac ? c->prosac_len : 0u;
     if (c->dev_sampler == USAC_SAMPLER_NAPSAC) {
         ds.nap_n_eligible = c->grid_n_elig;
         ds.nap_cell = c->grid_cell.as<uint32_t>();
@@ -930,10 +1041,10 @@ int usac_create(usac_ctx **out, int device, int estimator, const float *pts, uin
     do {
         hipError_t e = hipSetDevice(device);
         if (e != hipSuccess) { rc = fail(c, USAC_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e)); break; }
-        e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+        e = StreamPool::get().stream(&c->stream);
         if (e != hipSuccess) { rc = fail(c, USAC_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e)); break; }
         for (auto &ev : c->ev) {
-            e = hipEventCreate(&ev);
+            e = StreamPool::get().event(&ev);
             if (e != hipSuccess) break;
         }
         if (e != hipSuccess) { rc = fail(c, USAC_ERR_HIP, "hipEventCreate failed"); break; }
@@ -965,6 +1076,7 @@ int usac_create(usac_ctx **out, int device, int estimator, const float *pts, uin
 
 void usac_destroy(usac_ctx *c) {
     if (!c) return;
+    (void)hipSetDevice(c->device);  // the pools are per device
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
@@ -978,8 +1090,8 @@ void usac_destroy(usac_ctx *c) {
                       &c->x_recv})
         b->release();
     for (auto &ev : c->ev)
-        if (ev) (void)hipEventDestroy(ev);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+        if (ev) StreamPool::get().give_back(ev);
+    if (c->stream) StreamPool::get().give_back(c->stream);
     delete c;
 }
 
@@ -1263,7 +1375,7 @@ int usac_set_device_sampler(usac_ctx *c, int sampler) {
         HIP_TRY(c, hipSetDevice(c->device));
         HIP_TRY(c, c->prosac_tab.reserve(sizeof(uint32_t) * T));
         HIP_TRY(c, hipMemcpy(c->prosac_tab.p, tab.data(), sizeof(uint32_t) * T, hipMemcpyHostToDevice));
-        c->prosac_tab.bytes = sizeof(uint32_t) * T;
+        c->prosac_len = T;
     }
     c->dev_sampler = sampler;
     return USAC_OK;
