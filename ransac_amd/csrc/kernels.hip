@@ -308,7 +308,8 @@ template <int CHUNKS, bool EXACT_SUM>
 __global__ __launch_bounds__(64 * CHUNKS) void k_score_hf(const float4 *__restrict__ rec, uint32_t n, float4 ext,
                                                           const float *__restrict__ models, uint32_t B, float thr,
                                                           const uint32_t *__restrict__ perm,
-                                                          int32_t *__restrict__ counts, float *__restrict__ sums) {
+                                                          int32_t *__restrict__ counts, float *__restrict__ sums,
+                                                          int32_t *__restrict__ pc, float *__restrict__ ps) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t i = blockIdx.x * 64 + lane;
@@ -323,9 +324,11 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_hf(const float4 *__restri
     }
     const float T = 2.0f * thr;
     stage_a_bounds(M, ext, T);
+    // point chunks: CHUNKS waves per workgroup x gridDim.y workgroups per hypothesis tile
     const uint32_t ngroups = (n + 3) / 4;
-    const uint32_t per = (ngroups + CHUNKS - 1) / CHUNKS;
-    const uint32_t gbeg = wave * per < ngroups ? wave * per : ngroups;
+    const uint32_t nchunks = CHUNKS * gridDim.y, chunk = blockIdx.y * CHUNKS + wave;
+    const uint32_t per = (ngroups + nchunks - 1) / nchunks;
+    const uint32_t gbeg = chunk * per < ngroups ? chunk * per : ngroups;
     const uint32_t gend = gbeg + per < ngroups ? gbeg + per : ngroups;
     int cnt = 0;
     float sum = 0.f;
@@ -345,6 +348,10 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_hf(const float4 *__restri
         score_group<EXACT_SUM>(M, p[0], p[1], p[2], p[3], p[4], p[5], T, thr, cnt, sum);
     }
     if (!EXACT_SUM) sum *= 0.5f;
+    if (pc) {  // gridDim.y > 1: this workgroup's partial at [blockIdx.y][h] (k_score_ycombine adds them)
+        counts = pc + (size_t)blockIdx.y * B;
+        sums = ps + (size_t)blockIdx.y * B;
+    }
     if constexpr (CHUNKS == 1) {
         if (i < B) {
             counts[hc] = cnt;
@@ -368,6 +375,22 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_hf(const float4 *__restri
             sums[hc] = s;
         }
     }
+}
+
+// the gridDim.y partials of k_score_hf, added in workgroup order (deterministic)
+__global__ __launch_bounds__(256) void k_score_ycombine(const int32_t *__restrict__ pc, const float *__restrict__ ps,
+                                                        uint32_t B, uint32_t ny, int32_t *__restrict__ counts,
+                                                        float *__restrict__ sums) {
+    const uint32_t h = blockIdx.x * 256 + threadIdx.x;
+    if (h >= B) return;
+    int c = pc[h];
+    float s = ps[h];
+    for (uint32_t y = 1; y < ny; y++) {
+        c += pc[(size_t)y * B + h];
+        s += ps[(size_t)y * B + h];
+    }
+    counts[h] = c;
+    sums[h] = s;
 }
 
 // Hypothesis pre-sort for the fast score kernel: forward-distance hits of every hypothesis
@@ -426,7 +449,8 @@ __global__ __launch_bounds__(64 * kPresortWaves) void k_presort_h(const float4 *
     }
     fbase = __shfl(fbase, 0, 64);
     bbase = __shfl(bbase, 0, 64);
-    if (valid) perm[good ? fbase + below : B - 1 - (bbase + below)] = h;
+    const uint32_t at = good ? fbase + below : B - 1 - (bbase + below);
+    if (valid && at < B) perm[at] = h;  // (the counters reach B exactly: one grid row of workgroups)
 }
 
 // ------------------------------------------------------------------------ line2d
@@ -621,16 +645,21 @@ hipError_t launch_prepare_rec(hipStream_t st, const float4 *pts, uint32_t n, flo
 }
 
 hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const float4 *rec, uint32_t n, float4 ext,
-                           const float *models, uint32_t B, float thr, uint32_t *perm, int32_t *counts, float *sums) {
-    dim3 grid((B + 63) / 64);
+                           const float *models, uint32_t B, float thr, uint32_t *perm, int32_t *counts, float *sums,
+                           uint32_t ysplit, void *yscratch) {
+    if (exact_sum || !yscratch) ysplit = 1;
+    dim3 grid((B + 63) / 64, ysplit);
+    int32_t *pc = ysplit > 1 ? static_cast<int32_t *>(yscratch) : nullptr;
+    float *ps = ysplit > 1 ? reinterpret_cast<float *>(pc + (size_t)ysplit * B) : nullptr;
     if (perm) {  // perm: B entries followed by 2 counters
         uint32_t *ends = perm + B;
         hipError_t e = hipMemsetAsync(ends, 0, 2 * sizeof(uint32_t), st);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_presort_h, grid, dim3(64 * kPresortWaves), 0, st, rec, n, models, B, thr, perm, ends);
+        hipLaunchKernelGGL(k_presort_h, dim3((B + 63) / 64), dim3(64 * kPresortWaves), 0, st, rec, n, models, B, thr, perm, ends);
     }
 #define SHF(C, E) \
-    hipLaunchKernelGGL((k_score_hf<C, E>), grid, dim3(64 * C), 0, st, rec, n, ext, models, B, thr, perm, counts, sums)
+    hipLaunchKernelGGL((k_score_hf<C, E>), grid, dim3(64 * C), 0, st, rec, n, ext, models, B, thr, perm, counts, sums, \
+                       pc, ps)
     if (exact_sum) {
         switch (chunks) {
             case 1: SHF(1, true); break;
@@ -651,6 +680,8 @@ hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const flo
         }
     }
 #undef SHF
+    if (ysplit > 1)
+        hipLaunchKernelGGL(k_score_ycombine, dim3((B + 255) / 256), dim3(256), 0, st, pc, ps, B, ysplit, counts, sums);
     return LAUNCH_CHECK();
 }
 

@@ -173,6 +173,7 @@ struct usac_ctx {
     int dev_sampler = USAC_SAMPLER_UNIFORM;
     DevBuf tv_part;         // two-view scorer scratch: pre-sort permutation, chunk partials
     DevBuf perm;            // hypothesis pre-sort order of the fast kernel (B + 2 uint32)
+    DevBuf hf_part;         // fast-kernel partials of a point range split over workgroups
     float rec_thr = -1.f;   // threshold the record bands were built for
     float4 ext = {0, 0, 0, 0};  // dataset box: max |x1|, |y1|, |x2|, |y2| (fast-kernel bounds)
     // batch buffers
@@ -405,8 +406,20 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
             if (e != hipSuccess) return e;
             perm = c->perm.as<uint32_t>();
         }
+        // small batches over many points (the loop's batches): split each tile's points over
+        // several workgroups too, so the chip holds ~8 waves per SIMD
+        uint32_t ys = 1;
+        if (chunks > 1) {
+            const uint32_t waves = (B + 63) / 64 * (uint32_t)chunks, groups = (c->n + 3) / 4;
+            while (ys < 16 && waves * ys * 2 <= 8192u && groups / ((uint32_t)chunks * ys * 2) >= 64u) ys *= 2;
+        }
+        if (ys > 1) {
+            hipError_t e = c->hf_part.reserve(sizeof(int32_t) * 2 * (size_t)ys * B);
+            if (e != hipSuccess) return e;
+        }
         return usac::launch_score_hf(c->stream, chunks, chunks == 1, c->rec.as<float4>(), c->n, c->ext,
-                                     c->models.as<float>(), B, thr, perm, c->counts.as<int32_t>(), c->sums.as<float>());
+                                     c->models.as<float>(), B, thr, perm, c->counts.as<int32_t>(), c->sums.as<float>(),
+                                     ys, ys > 1 ? c->hf_part.p : nullptr);
     }
     return usac::launch_score_line(c->stream, chunks, c->pts.as<float2>(), c->n, c->models.as<float>(), B, thr,
                                    c->counts.as<int32_t>(), c->sums.as<float>());
@@ -1083,7 +1096,7 @@ void usac_destroy(usac_ctx *c) {
                       &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
                       &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->inl_scratch, &c->e5_ws, &c->one_model,
                       &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq,
-                      &c->rec_send, &c->rec_all, &c->tv_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
+                      &c->rec_send, &c->rec_all, &c->tv_part, &c->hf_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
                       &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2, &c->gc_err, &c->grid_cell, &c->grid_rank, &c->grid_start,
                       &c->grid_members, &c->grid_elig, &c->grid_ws, &c->x_send,

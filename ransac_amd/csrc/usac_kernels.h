@@ -54,8 +54,11 @@ hipError_t launch_score_h(hipStream_t st, int chunks, const float4 *pts, uint32_
 hipError_t launch_prepare_rec(hipStream_t st, const float4 *pts, uint32_t n, float thr, float4 *rec);
 // ext = dataset box {max|x1|, max|y1|, max|x2|, max|y2|} (stage-A error bounds)
 // perm (nullable, B + 2 uint32): hypothesis pre-sort scratch (k_presort_h)
+// ysplit > 1 (throughput mode): every 64-hypothesis tile's points over chunks x ysplit waves in
+// ysplit workgroups, partials in yscratch (8 B x ysplit x B) added in order by a second launch
 hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const float4 *rec, uint32_t n, float4 ext,
-                           const float *models, uint32_t B, float thr, uint32_t *perm, int32_t *counts, float *sums);
+                           const float *models, uint32_t B, float thr, uint32_t *perm, int32_t *counts, float *sums,
+                           uint32_t ysplit = 1, void *yscratch = nullptr);
 
 hipError_t launch_solve_line(hipStream_t st, const float2 *pts, uint32_t n, const int32_t *samples_in,
                              int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, float *models);
