@@ -124,10 +124,11 @@ __global__ __launch_bounds__(kInlBlock) void k_inl_compact(const void *__restric
                                                            const float *__restrict__ thrs,
                                                            const uint32_t *__restrict__ slots,
                                                            uint32_t *__restrict__ scratch, int32_t *__restrict__ idx,
-                                                           size_t idx_stride) {
+                                                           size_t idx_stride, const int32_t *__restrict__ ok) {
     __shared__ float sm[18];
     __shared__ uint32_t wsum[kInlBlock / 64];
     const uint32_t ws = inl_slot(slots, blockIdx.y);
+    if (ok && !ok[ws]) return;  // a failed fit: its list is left as it was (workgroup-uniform)
     inl_model<EST>(models + 9 * (size_t)ws, sm);
     const float t = thrs ? thrs[ws] : thr;
     float m[18];
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(kInlBlock) void k_inl_compact(const void *__restric
 
 hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *models,
                                 uint32_t W, float thr, const float *thrs, const uint32_t *slots, int32_t *idx,
-                                size_t idx_stride, int32_t *counts, float *sums, void *scratch) {
+                                size_t idx_stride, int32_t *counts, float *sums, void *scratch, const int32_t *ok) {
     if (W == 0) return hipSuccess;
     const uint32_t nb = (n + kInlBlock - 1) / kInlBlock;
     uint32_t *scr = static_cast<uint32_t *>(scratch);
@@ -165,7 +166,7 @@ hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, 
         hipLaunchKernelGGL(k_inl_flags<E>, grid, dim3(kInlBlock), 0, st, pts, n, models, thr, thrs, slots, scr);        \
         hipLaunchKernelGGL(k_inl_scan, dim3(W), dim3(1024), 0, st, scr, n, nb, slots, counts);                         \
         hipLaunchKernelGGL(k_inl_compact<E>, grid, dim3(kInlBlock), 0, st, pts, n, models, thr, thrs, slots, scr, \
-                           idx, idx_stride);                                                                     \
+                           idx, idx_stride, ok);                                                                 \
     } while (0)
     switch (estimator) {
         case USAC_LINE2D: INL(USAC_LINE2D); break;

@@ -588,8 +588,13 @@ struct LoRansac {
         h.phase = DONE;
     }
 
-    // one lockstep stage: a batched fit (INNER_FIT / ITER_FIT chains) or a batched scoring
-    // (INNER_SCORE / ITER_SCORE chains) on the device, then every chain's state machine steps
+    // one lockstep stage: the batched fit of every chain in INNER_FIT / ITER_FIT and, in the
+    // same submission, the batched scoring of the fitted models at the threshold each chain
+    // scores with after its fit (inner: K * thr, iterative: the already decremented thr); the
+    // scoring leaves the index list of a failed fit alone (the limited variant refits from it).
+    // One host synchronisation per stage; then every chain's state machine takes the fit
+    // outcome and, if the fit succeeded, the score.  (A chain in a SCORE phase only arises
+    // without a fused fit -- never here -- so it is scored on its own.)
     int stage(uint32_t W, int inner_cnt) {
         bool fit = false, score = false, inner_fit = false, pos = false;
         uint32_t nmax = 0, ns = 0;
@@ -602,10 +607,13 @@ struct LoRansac {
                 if (inner_fit) {
                     pos = inner_cnt > (int)limit;
                     hns[w] = pos ? limit : (uint32_t)inner_cnt;
+                    hthr[w] = (float)mult * h.thr;
                 } else {
                     pos = h.fit_pos;
                     hns[w] = pos ? limit : (uint32_t)h.lo_cnt;
+                    hthr[w] = h.thr;
                 }
+                hslots[ns++] = w;
                 nmax = std::max(nmax, hns[w]);
             } else if (h.phase == INNER_SCORE || h.phase == ITER_SCORE) {
                 score = true;
@@ -637,18 +645,20 @@ struct LoRansac {
             b.ok = c->lo_ok.as<int32_t>();
             b.seq = c->nm_seq.p;
             HIP_TRY(c, usac::launch_nonminimal_batch(st, c->estimator, c->pts.p, b));
+        }
+        HIP_TRY(c, hipMemcpyAsync(c->lo_thrs.p, hthr.data(), sizeof(float) * W, hipMemcpyHostToDevice, st));
+        HIP_TRY(c, hipMemcpyAsync(c->lo_slots.p, hslots.data(), sizeof(uint32_t) * ns, hipMemcpyHostToDevice, st));
+        HIP_TRY(c, usac::launch_inliers_batch(st, c->estimator, c->pts.p, n, c->lo_models.as<float>(), ns, 0.f,
+                                              c->lo_thrs.as<float>(), c->lo_slots.as<uint32_t>(),
+                                              c->lo_lists.as<int32_t>(), n, c->lo_cnts.as<int32_t>(),
+                                              c->lo_sums.as<float>(), c->lo_scr.p,
+                                              fit ? c->lo_ok.as<int32_t>() : nullptr));
+        if (fit) {
             HIP_TRY(c, hipMemcpyAsync(hmod.data(), c->lo_models.p, sizeof(float) * 9 * W, hipMemcpyDeviceToHost, st));
             HIP_TRY(c, hipMemcpyAsync(hok.data(), c->lo_ok.p, sizeof(int32_t) * W, hipMemcpyDeviceToHost, st));
-        } else {
-            HIP_TRY(c, hipMemcpyAsync(c->lo_thrs.p, hthr.data(), sizeof(float) * W, hipMemcpyHostToDevice, st));
-            HIP_TRY(c, hipMemcpyAsync(c->lo_slots.p, hslots.data(), sizeof(uint32_t) * ns, hipMemcpyHostToDevice, st));
-            HIP_TRY(c, usac::launch_inliers_batch(st, c->estimator, c->pts.p, n, c->lo_models.as<float>(), ns, 0.f,
-                                                  c->lo_thrs.as<float>(), c->lo_slots.as<uint32_t>(),
-                                                  c->lo_lists.as<int32_t>(), n, c->lo_cnts.as<int32_t>(),
-                                                  c->lo_sums.as<float>(), c->lo_scr.p));
-            HIP_TRY(c, hipMemcpyAsync(hcnt.data(), c->lo_cnts.p, sizeof(int32_t) * W, hipMemcpyDeviceToHost, st));
-            HIP_TRY(c, hipMemcpyAsync(hsum.data(), c->lo_sums.p, sizeof(float) * W, hipMemcpyDeviceToHost, st));
         }
+        HIP_TRY(c, hipMemcpyAsync(hcnt.data(), c->lo_cnts.p, sizeof(int32_t) * W, hipMemcpyDeviceToHost, st));
+        HIP_TRY(c, hipMemcpyAsync(hsum.data(), c->lo_sums.p, sizeof(float) * W, hipMemcpyDeviceToHost, st));
         HIP_TRY(c, hipStreamSynchronize(st));
         stages++;
         for (uint32_t w = 0; w < W; w++) {
@@ -661,25 +671,16 @@ struct LoRansac {
                         h.phase = DONE;
                     } else {
                         h.thr = (float)mult * h.thr;  // K * theta
-                        h.phase = INNER_SCORE;
+                        inner_scored(h, w);
                     }
                     break;
                 case INNER_SCORE:
-                    h.lo_cnt = hcnt[w];
-                    h.lo_sum = hsum[w];
-                    if (h.lo_cnt <= (int)m) {
-                        h.outcome = FEW;
-                        h.phase = DONE;
-                    } else {
-                        h.it = 0;
-                        h.iter_count = 0;
-                        iter_head(h, w);
-                    }
+                    inner_scored(h, w);
                     break;
                 case ITER_FIT:
                     memcpy(h.model, hmod.data() + 9 * (size_t)w, sizeof(h.model));
                     if (hok[w]) {
-                        h.phase = ITER_SCORE;
+                        iter_scored(h, w);
                     } else if (h.fit_pos) {  // GetScoreLimited: continue
                         h.it++;
                         iter_head(h, w);
@@ -688,21 +689,38 @@ struct LoRansac {
                     }
                     break;
                 case ITER_SCORE:
-                    h.lo_cnt = hcnt[w];
-                    h.lo_sum = hsum[w];
-                    if (!limited && bigger(best_cnt, best_sum, h.lo_cnt, h.lo_sum)) {
-                        finish(h);  // GetScoreUnlimited: the best is bigger -> break
-                    } else {
-                        h.iter_count++;
-                        h.it++;
-                        iter_head(h, w);
-                    }
+                    iter_scored(h, w);
                     break;
                 default:
                     break;
             }
         }
         return USAC_OK;
+    }
+    // the inner iteration's scoring of lo_model at K * theta
+    void inner_scored(Chain &h, uint32_t w) {
+        h.lo_cnt = hcnt[w];
+        h.lo_sum = hsum[w];
+        if (h.lo_cnt <= (int)m) {
+            h.outcome = FEW;
+            h.phase = DONE;
+        } else {
+            h.it = 0;
+            h.iter_count = 0;
+            iter_head(h, w);
+        }
+    }
+    // an iterative step's scoring of its fit
+    void iter_scored(Chain &h, uint32_t w) {
+        h.lo_cnt = hcnt[w];
+        h.lo_sum = hsum[w];
+        if (!limited && bigger(best_cnt, best_sum, h.lo_cnt, h.lo_sum)) {
+            finish(h);  // GetScoreUnlimited: the best is bigger -> break
+        } else {
+            h.iter_count++;
+            h.it++;
+            iter_head(h, w);
+        }
     }
 
     // GetModelScore(best_model, best_score): model / (cnt, sum) improved in place
