@@ -18,3 +18,4 @@ run f_cfg3_b262k --estimator fundamental --batch 262144 --cpu-seconds 0
 run e_cfg4 --estimator essential
 run e_b262k --estimator essential --batch 262144 --cpu-seconds 0
 run e_sprt --estimator essential --sprt --cpu-seconds 0
+run n_napsac --sampler napsac --cpu-seconds 0

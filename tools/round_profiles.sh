@@ -11,7 +11,7 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 cat $OUT/smoke.log
 timeout -k 10 900 bash tools/bench_all.sh > $OUT/bench_all.txt 2>&1 || { cat $OUT/bench_all.txt; exit 1; }
 cat $OUT/bench_all.txt
-timeout -k 10 300 python bench.py --cfg5 --steps 5 --warmup 1 > $OUT/cfg5.json 2>$OUT/cfg5.err || { tail -5 $OUT/cfg5.err; exit 1; }
+timeout -k 10 300 python bench.py --cfg5 > $OUT/cfg5.json 2>$OUT/cfg5.err || { tail -5 $OUT/cfg5.err; exit 1; }
 cat $OUT/cfg5.json
 USAC_PROFILE=1 timeout -k 10 300 python tools/feature_bench.py > $OUT/features.json 2> $OUT/features.err || { tail -5 $OUT/features.err; exit 1; }
 cat $OUT/features.json
