@@ -156,6 +156,37 @@ struct StreamPool {
     }
 };
 
+// pinned host staging blocks (hipHostMalloc costs far more than a run's copies), by size class
+struct PinnedPool {
+    std::mutex mu;
+    std::multimap<size_t, void *> free;
+    static PinnedPool &get() {
+        static PinnedPool *pool = new PinnedPool();
+        return *pool;
+    }
+    void *take(size_t b, size_t *got) {
+        const size_t c = DevPool::size_class(b);
+        {
+            std::lock_guard<std::mutex> g(mu);
+            auto it = free.find(c);
+            if (it != free.end()) {
+                void *p = it->second;
+                free.erase(it);
+                *got = c;
+                return p;
+            }
+        }
+        void *p = nullptr;
+        if (hipHostMalloc(&p, c, hipHostMallocDefault) != hipSuccess) return nullptr;
+        *got = c;
+        return p;
+    }
+    void give_back(void *p, size_t c) {
+        std::lock_guard<std::mutex> g(mu);
+        free.emplace(c, p);
+    }
+};
+
 }  // namespace
 
 struct usac_ctx {
@@ -202,6 +233,7 @@ struct usac_ctx {
     // single-model / polish buffers
     DevBuf one_model, inl_idx, inl_cnt, inl_sum, inl_scratch, q, partial, ws, nm_model, nm_ok;
     DevBuf nm_seq;          // normalisation scratch of the non-minimal fits (polish and LO)
+    DevBuf lo_io;           // one LO stage's inputs and outputs, contiguous (one copy each way)
     // comm
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -508,9 +540,16 @@ struct LoRansac {
     float best_sum = 0.f;
     std::vector<Chain> ch;
     std::vector<usac::Mt19937> g_after;  // generator after chain w's inner draw
-    std::vector<int32_t> hpos, hcnt, hok;
-    std::vector<uint32_t> hns, hslots;
-    std::vector<float> hthr, hsum, hmod;
+    // a stage's inputs (ns, thresholds, slots, LSQ positions) and outputs (models, fit flags,
+    // counts, sums) as one pinned host block mirrored by one device block: one copy each way
+    void *pin = nullptr;
+    size_t pin_bytes = 0, in_bytes = 0, out_bytes = 0;
+    uint32_t *hns = nullptr, *hslots = nullptr;
+    int32_t *hpos = nullptr, *hcnt = nullptr, *hok = nullptr;
+    float *hthr = nullptr, *hsum = nullptr, *hmod = nullptr;
+    uint32_t *dns = nullptr, *dslots = nullptr;
+    int32_t *dpos = nullptr, *dcnt = nullptr, *dok = nullptr;
+    float *dthr = nullptr, *dsum = nullptr, *dmod = nullptr;
 
     LoRansac(usac_ctx *ctx, const usac_params *p)
         : c(ctx),
@@ -527,28 +566,37 @@ struct LoRansac {
           lo_thr(p->threshold),
           step((p->threshold * p->lo_threshold_multiplier - p->threshold) / p->lo_iterative_iterations),
           ch(wmax),
-          g_after(wmax, usac::Mt19937(0)),
-          hpos((size_t)wmax * std::max<uint32_t>(1u, p->lo_sample_size)),
-          hcnt(wmax),
-          hok(wmax),
-          hns(wmax),
-          hslots(wmax),
-          hthr(wmax),
-          hsum(wmax),
-          hmod((size_t)9 * wmax) {}
+          g_after(wmax, usac::Mt19937(0)) {}
+    ~LoRansac() {
+        if (pin) PinnedPool::get().give_back(pin, pin_bytes);
+    }
 
     int reserve() {
-        const size_t W = wmax, N = n;
+        const size_t W = wmax, N = n, L = std::max<uint32_t>(1u, limit);
         HIP_TRY(c, c->lo_max.reserve(sizeof(int32_t) * N));
         HIP_TRY(c, c->lo_lists.reserve(sizeof(int32_t) * N * W));
-        HIP_TRY(c, c->lo_pos.reserve(sizeof(int32_t) * hpos.size()));
-        HIP_TRY(c, c->lo_ns.reserve(sizeof(uint32_t) * W));
-        HIP_TRY(c, c->lo_thrs.reserve(sizeof(float) * W));
-        HIP_TRY(c, c->lo_slots.reserve(sizeof(uint32_t) * W));
-        HIP_TRY(c, c->lo_models.reserve(sizeof(float) * 9 * W));
-        HIP_TRY(c, c->lo_ok.reserve(sizeof(int32_t) * W));
-        HIP_TRY(c, c->lo_cnts.reserve(sizeof(int32_t) * W));
-        HIP_TRY(c, c->lo_sums.reserve(sizeof(float) * W));
+        in_bytes = sizeof(uint32_t) * (3 * W + W * L);
+        out_bytes = sizeof(float) * 12 * W;
+        HIP_TRY(c, c->lo_io.reserve(in_bytes + out_bytes));
+        pin = PinnedPool::get().take(in_bytes + out_bytes, &pin_bytes);
+        if (!pin) return fail(c, USAC_ERR_HIP, "hipHostMalloc (LO staging) failed");
+        uint32_t *hw = static_cast<uint32_t *>(pin), *dw = c->lo_io.as<uint32_t>();
+        hns = hw;
+        hthr = reinterpret_cast<float *>(hw + W);
+        hslots = hw + 2 * W;
+        hpos = reinterpret_cast<int32_t *>(hw + 3 * W);
+        hmod = reinterpret_cast<float *>(hw + 3 * W + W * L);
+        hok = reinterpret_cast<int32_t *>(hmod + 9 * W);
+        hcnt = hok + W;
+        hsum = reinterpret_cast<float *>(hcnt + W);
+        dns = dw;
+        dthr = reinterpret_cast<float *>(dw + W);
+        dslots = dw + 2 * W;
+        dpos = reinterpret_cast<int32_t *>(dw + 3 * W);
+        dmod = reinterpret_cast<float *>(dw + 3 * W + W * L);
+        dok = reinterpret_cast<int32_t *>(dmod + 9 * W);
+        dcnt = dok + W;
+        dsum = reinterpret_cast<float *>(dcnt + W);
         HIP_TRY(c, c->lo_q.reserve(sizeof(float) * c->cols * N * W));
         HIP_TRY(c, c->lo_part.reserve(sizeof(double) * usac::nonminimal_partial_stride(n) * W));
         HIP_TRY(c, c->nm_seq.reserve(usac::nonminimal_seq_bytes(n, (uint32_t)W)));
@@ -574,7 +622,7 @@ struct LoRansac {
             if (h.lo_cnt <= (int)m) return finish(h);
             h.fit_pos = false;
             if (limited && h.lo_cnt > (int)limit) {  // GetScoreLimited: a random subset of lo_inliers
-                usac::unique_set(g, hpos.data() + (size_t)w * limit, limit, (uint32_t)(h.lo_cnt - 1));
+                usac::unique_set(g, hpos + (size_t)w * limit, limit, (uint32_t)(h.lo_cnt - 1));
                 h.fit_pos = true;
             }
             h.phase = ITER_FIT;
@@ -623,17 +671,14 @@ struct LoRansac {
         }
         if (fit && score) return fail(c, USAC_ERR_HIP, "LO chains out of lockstep");  // never: fit, score alternate
         hipStream_t st = c->stream;
+        HIP_TRY(c, hipMemcpyAsync(c->lo_io.p, pin, in_bytes, hipMemcpyHostToDevice, st));
         if (fit) {
-            HIP_TRY(c, hipMemcpyAsync(c->lo_ns.p, hns.data(), sizeof(uint32_t) * W, hipMemcpyHostToDevice, st));
-            if (pos)
-                HIP_TRY(c, hipMemcpyAsync(c->lo_pos.p, hpos.data(), sizeof(int32_t) * (size_t)W * limit,
-                                          hipMemcpyHostToDevice, st));
             usac::NmBatch b{};
             b.base = inner_fit ? c->lo_max.as<int32_t>() : c->lo_lists.as<int32_t>();
             b.base_stride = inner_fit ? 0 : n;
-            b.pos = pos ? c->lo_pos.as<int32_t>() : nullptr;
+            b.pos = pos ? dpos : nullptr;
             b.pos_stride = limit;
-            b.ns = c->lo_ns.as<uint32_t>();
+            b.ns = dns;
             b.W = W;
             b.nmax = nmax;
             b.q = c->lo_q.p;
@@ -641,31 +686,22 @@ struct LoRansac {
             b.partial = c->lo_part.as<double>();
             b.p_stride = usac::nonminimal_partial_stride(n);
             b.ws = c->lo_ws.as<float>();
-            b.model_out = c->lo_models.as<float>();
-            b.ok = c->lo_ok.as<int32_t>();
+            b.model_out = dmod;
+            b.ok = dok;
             b.seq = c->nm_seq.p;
             HIP_TRY(c, usac::launch_nonminimal_batch(st, c->estimator, c->pts.p, b));
         }
-        HIP_TRY(c, hipMemcpyAsync(c->lo_thrs.p, hthr.data(), sizeof(float) * W, hipMemcpyHostToDevice, st));
-        HIP_TRY(c, hipMemcpyAsync(c->lo_slots.p, hslots.data(), sizeof(uint32_t) * ns, hipMemcpyHostToDevice, st));
-        HIP_TRY(c, usac::launch_inliers_batch(st, c->estimator, c->pts.p, n, c->lo_models.as<float>(), ns, 0.f,
-                                              c->lo_thrs.as<float>(), c->lo_slots.as<uint32_t>(),
-                                              c->lo_lists.as<int32_t>(), n, c->lo_cnts.as<int32_t>(),
-                                              c->lo_sums.as<float>(), c->lo_scr.p,
-                                              fit ? c->lo_ok.as<int32_t>() : nullptr));
-        if (fit) {
-            HIP_TRY(c, hipMemcpyAsync(hmod.data(), c->lo_models.p, sizeof(float) * 9 * W, hipMemcpyDeviceToHost, st));
-            HIP_TRY(c, hipMemcpyAsync(hok.data(), c->lo_ok.p, sizeof(int32_t) * W, hipMemcpyDeviceToHost, st));
-        }
-        HIP_TRY(c, hipMemcpyAsync(hcnt.data(), c->lo_cnts.p, sizeof(int32_t) * W, hipMemcpyDeviceToHost, st));
-        HIP_TRY(c, hipMemcpyAsync(hsum.data(), c->lo_sums.p, sizeof(float) * W, hipMemcpyDeviceToHost, st));
+        HIP_TRY(c, usac::launch_inliers_batch(st, c->estimator, c->pts.p, n, dmod, ns, 0.f, dthr, dslots,
+                                              c->lo_lists.as<int32_t>(), n, dcnt, dsum, c->lo_scr.p,
+                                              fit ? dok : nullptr));
+        HIP_TRY(c, hipMemcpyAsync(hmod, dmod, out_bytes, hipMemcpyDeviceToHost, st));
         HIP_TRY(c, hipStreamSynchronize(st));
         stages++;
         for (uint32_t w = 0; w < W; w++) {
             Chain &h = ch[w];
             switch (h.phase) {
                 case INNER_FIT:  // LeastSquaresFitting(lo_sample | max_inliers) -> lo_model
-                    memcpy(h.model, hmod.data() + 9 * (size_t)w, sizeof(h.model));
+                    memcpy(h.model, hmod + 9 * (size_t)w, sizeof(h.model));
                     if (!hok[w]) {
                         h.outcome = inner_cnt > (int)limit ? SKIP : RETURN;
                         h.phase = DONE;
@@ -678,7 +714,7 @@ struct LoRansac {
                     inner_scored(h, w);
                     break;
                 case ITER_FIT:
-                    memcpy(h.model, hmod.data() + 9 * (size_t)w, sizeof(h.model));
+                    memcpy(h.model, hmod + 9 * (size_t)w, sizeof(h.model));
                     if (hok[w]) {
                         iter_scored(h, w);
                     } else if (h.fit_pos) {  // GetScoreLimited: continue
@@ -751,7 +787,7 @@ struct LoRansac {
                 h.thr_start = h.thr = t;
                 h.phase = INNER_FIT;
                 if (cnt > (int)limit) {
-                    usac::unique_set(g, hpos.data() + (size_t)w * limit, limit, (uint32_t)(cnt - 1));
+                    usac::unique_set(g, hpos + (size_t)w * limit, limit, (uint32_t)(cnt - 1));
                 }
                 g_after[w] = g;
                 t = predict(t);
@@ -1113,7 +1149,7 @@ void usac_destroy(usac_ctx *c) {
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
                       &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->inl_scratch, &c->e5_ws, &c->one_model,
-                      &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq,
+                      &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq, &c->lo_io,
                       &c->rec_send, &c->rec_all, &c->tv_part, &c->hf_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
                       &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2, &c->gc_err, &c->grid_cell, &c->grid_rank, &c->grid_start,
