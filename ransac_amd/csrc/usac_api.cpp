@@ -1808,9 +1808,13 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
             HIP_TRY(c, enqueue_score(c, B, thr, loop_chunks(c, B)));
             HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
         }
-        for (int k = 0; k < ncomp(c); k++)
-            HIP_TRY(c, hipMemcpyAsync(hmod.data() + (size_t)k * SB, c->models.as<float>() + (size_t)k * S,
-                                      sizeof(float) * S, hipMemcpyDeviceToHost, c->stream));
+        if (SB == S)  // the device's component-major [ncomp][S] block in one copy
+            HIP_TRY(c, hipMemcpyAsync(hmod.data(), c->models.p, sizeof(float) * S * ncomp(c), hipMemcpyDeviceToHost,
+                                      c->stream));
+        else
+            for (int k = 0; k < ncomp(c); k++)
+                HIP_TRY(c, hipMemcpyAsync(hmod.data() + (size_t)k * SB, c->models.as<float>() + (size_t)k * S,
+                                          sizeof(float) * S, hipMemcpyDeviceToHost, c->stream));
         if (sprt) {
             if (listed(c)) {  // occupied slots -> mask rows
                 HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
