@@ -21,10 +21,13 @@ Fixtures are DATA only -- inputs and expected outputs the reference already hold
     (<scene>_vpts_model.txt).  The "GT Inl" column of results/kusvod2/*.csv is NOT
     reproducible from these files with the Sampson error at thr 2 (e.g. booksh: published
     149, F/F^T give 61/4), so it is not a fixture; the scenes serve as real-data inputs;
+  * evd_scenes.npz        : the 15 EVD tentative correspondence sets (homography; the
+    reference's EVD statistics are graph-cut runs with KNN or grid neighbours);
   * reference_stats.json  : every per-scene row (averages, standard deviations, medians) and
     the run settings of the reference's published statistical CSVs the pin tests use
     (results/line2d/{uniform,napsac,prosac}_*.csv, results/homography/uniform_gc*_Grid_c_sz_50.csv,
-    results/kusvod2/uniform_gc*_Grid_c_sz_50.csv) -- numbers copied from the CSVs, nothing else.
+    results/kusvod2/uniform_gc*_Grid_c_sz_50.csv, results/EVD/*_gc*_c_sz_50.csv) -- numbers copied
+    from the CSVs, nothing else.
 """
 import csv
 import ctypes
@@ -133,11 +136,30 @@ def kusvod2():
     np.savez_compressed(os.path.join(OUT, "kusvod2_scenes.npz"), **arrays)
 
 
+def evd():
+    """evd_scenes.npz: the EVD tentative correspondences (dataset/EVD/EVD_tentatives/<scene>.png_m.txt,
+    Reader::readEVDPointsInliers, detector/Reader.cpp:215-260: csv after a header line, strtof)
+    of the 15 scenes of results/EVD/*.csv, in file order (the reference's sorted_points for
+    PROSAC are the same points: dataset/GetImage.h:122-136)."""
+    d = os.path.join(REF, "dataset/EVD/EVD_tentatives")
+    scenes = sorted(fn[:-len(".png_m.txt")] for fn in os.listdir(d) if fn.endswith(".png_m.txt"))
+    arrays = {}
+    for scene in scenes:
+        with open(os.path.join(d, scene + ".png_m.txt")) as f:
+            lines = [ln for ln in f.read().splitlines()[1:] if ln.strip()]
+        arrays[scene + "_pts"] = np.array([[strtof(t) for t in ln.split(",")[:4]] for ln in lines], dtype=np.float32)
+    np.savez_compressed(os.path.join(OUT, "evd_scenes.npz"), **arrays)
+
+
 STAT_FILES = [
     "line2d/uniform_000.csv", "line2d/uniform_001.csv", "line2d/uniform_010.csv", "line2d/uniform_100.csv",
     "line2d/napsac_000.csv", "line2d/prosac_000.csv",
     "homography/uniform_gc_Grid_c_sz_50.csv", "homography/uniform_gc_sprt_Grid_c_sz_50.csv",
     "kusvod2/uniform_gc_Grid_c_sz_50.csv", "kusvod2/uniform_gc_sprt_Grid_c_sz_50.csv",
+    # EVD: only the graph-cut runs hold rows (uniform_lo / uniform_sprt / prosac_lo ... are headers only)
+    "EVD/uniform_gc_Nanoflann_c_sz_50.csv", "EVD/uniform_gc_sprt_Nanoflann_c_sz_50.csv",
+    "EVD/prosac_gc_Nanoflann_c_sz_50.csv", "EVD/prosac_gc_sprt_Nanoflann_c_sz_50.csv",
+    "EVD/prosac_gc_sprt_Grid_c_sz_50.csv",
 ]
 
 
@@ -180,4 +202,5 @@ if __name__ == "__main__":
     homography()
     line2d()
     kusvod2()
+    evd()
     print("golden fixtures written to", OUT)

@@ -25,6 +25,8 @@ def _run(usac, pts, est, m, thr, p, seed, **kw):
         mdl.setCellSize(kw.pop("cell_size"))
     if "neighbors" in kw:
         mdl.setNeighborsType(kw.pop("neighbors"))
+    if "max_iterations" in kw:
+        mdl.max_iterations = kw.pop("max_iterations")
     r = usac.Ransac(mdl, pts)
     r.run()
     return r.getRansacOutput()
@@ -69,3 +71,34 @@ def test_line2d_lo_statistics_device(usac, oracle, line2d_scenes):
             inl.append(out.getNumberOfInliers())
         results[name] = {INL: inl}
     assert len(check(rel, results, [(INL, SD_INL)], {INL: inl_floor})) == 8
+
+
+@pytest.mark.parametrize("rel,sprt", [("EVD/uniform_gc_Nanoflann_c_sz_50.csv", False),
+                                      ("EVD/uniform_gc_sprt_Nanoflann_c_sz_50.csv", True)])
+def test_evd_gc_knn_statistics_device(usac, oracle, rel, sprt):
+    """results/EVD uniform graph-cut runs with KNN neighbours (device usac_knn, k = 7) through
+    usac_ransac_run: every run identical to the oracle's, the averages within the pin tolerance."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "evd_scenes.npz"))
+    results = {}
+    for key in sorted(z.files):
+        scene, pts = key[:-4], z[key]
+        inl = []
+        for seed in range(1, 11):
+            ref = oracle.ransac_run(oracle.HOMOGRAPHY, pts, 2.0, 0.95, seed, max_iters=15000, sprt=sprt,
+                                    lo=oracle.LO_GC, neighbors=oracle.NEIGHBORS_NANOFLANN, knn=7)
+            if ref["ret"] != 0:  # no model (the reference's exit(111)): the device says so too
+                with pytest.raises(usac.UsacError) as e:
+                    _run(usac, pts, usac.ESTIMATOR.Homography, 4, 2.0, 0.95, seed, lo=usac.LocOpt.GC,
+                         neighbors=usac.NeighborsSearch.Nanoflann, sprt=sprt, max_iterations=15000)
+                assert e.value.code == -111
+                inl.append(0)
+                continue
+            out = _run(usac, pts, usac.ESTIMATOR.Homography, 4, 2.0, 0.95, seed, lo=usac.LocOpt.GC,
+                       neighbors=usac.NeighborsSearch.Nanoflann, sprt=sprt, max_iterations=15000)
+            assert out.getNumberOfMainIterations() == ref["iters"], (scene, seed)
+            assert (_bits(out.getModel()) == _bits(ref["model"])).all(), (scene, seed)
+            assert (out.getInliers() == ref["inlier_idx"]).all(), (scene, seed)
+            inl.append(out.getNumberOfInliers())
+        results[scene] = {INL: inl}
+    assert len(check(rel, results, [(INL, SD_INL)], {INL: inl_floor})) >= 14

@@ -23,6 +23,9 @@ What is pinned, and what is not (DESIGN.md §3 lists the same):
   * fundamental, Uniform + graph-cut LO (+ SPRT), kusvod2 scenes: final inliers -- the 7-point
     solver, Sampson error, GC-LO -- with the rank-2 8-point polish of the revision that wrote
     the CSVs (oracle.set_f8_rank2; the current eight_points.cpp:58-68 comments it out).
+  * homography, EVD (results/EVD, 15 wide-baseline scenes): graph-cut LO with KNN or grid
+    neighbours, Uniform and PROSAC, with and without SPRT -- final inliers (PROSAC: 14 of 15
+    scenes, EVD_SKIP).
   * line2d (results/line2d): Uniform (inliers + iterations), LO-RANSAC and NAPSAC (inliers).
     Not pinned: SPRT, PROSAC and the iteration counts with LO -- see the EXCEPTIONS notes.
 """
@@ -152,6 +155,56 @@ KUSVOD2_SKIP = {
     "shout": "74.6 +- 5.7 vs 78.0 +- 0.0",
 }
 KUSVOD2_SPRT_SKIP = {"kampa": "with SPRT 103.7 +- 2.5 vs 99.2 +- 2.0 (pinned without SPRT)"}
+
+
+@pytest.fixture(scope="module")
+def evd_scenes():
+    z = np.load(os.path.join(HERE, "golden", "evd_scenes.npz"))
+    return {k[:-4]: z[k] for k in z.files}
+
+
+# EVD (wide-baseline homographies, 83 - 1164 tentatives, 15 - 80 true correspondences): the
+# reference's EVD statistics are graph-cut runs with KNN (nanoflann, k = 7) or grid
+# neighbours, Uniform or PROSAC (the tentatives file is already in quality order, so the
+# sorted points are the points: dataset/GetImage.h:122-136), with and without SPRT; the CSVs
+# cap the iterations at 15 000 (the runs that never meet the termination bound report 15000).
+# Final inliers are pinned; iterations are not (the CSVs predate the current loop, as the
+# homography ones: adam 1467 published vs ~1250 here).
+EVD_CASES = [("EVD/uniform_gc_Nanoflann_c_sz_50.csv", "uniform", False, "knn"),
+             ("EVD/uniform_gc_sprt_Nanoflann_c_sz_50.csv", "uniform", True, "knn"),
+             ("EVD/prosac_gc_Nanoflann_c_sz_50.csv", "prosac", False, "knn"),
+             ("EVD/prosac_gc_sprt_Nanoflann_c_sz_50.csv", "prosac", True, "knn"),
+             ("EVD/prosac_gc_sprt_Grid_c_sz_50.csv", "prosac", True, "grid")]
+# PROSAC scenes the oracle does not reproduce (12 runs, oracle vs published average inliers):
+# here PROSAC finds the 40-inlier plane of `grand` / `pkk` in most runs, the published runs
+# far less often (large published spread: the reference's PROSAC fails on them in many runs).
+# Uniform sampling on the same scenes agrees, so the gap is in the PROSAC schedule (the
+# reference seeds it from std::random_device, and which libstdc++ uniform_int_distribution it
+# ran is unknown -- DESIGN.md §3).  Reported, not pinned.
+EVD_SKIP = {
+    ("EVD/prosac_gc_Nanoflann_c_sz_50.csv", "grand"): "41.0 vs 29.6 +- 9.3",
+    ("EVD/prosac_gc_sprt_Nanoflann_c_sz_50.csv", "grand"): "36.4 vs 12.9 +- 11.9",
+    ("EVD/prosac_gc_sprt_Grid_c_sz_50.csv", "pkk"): "28.5 vs 13.3 +- 13.4",
+}
+
+
+@pytest.mark.parametrize("rel,sampler,sprt,nb", EVD_CASES)
+def test_evd_gc_statistics(oracle, evd_scenes, rel, sampler, sprt, nb):
+    runs = 12
+    results = {}
+    for scene, pts in sorted(evd_scenes.items()):
+        if scene not in STATS[rel]["scenes"] or (rel, scene) in EVD_SKIP:
+            continue
+        inl = []
+        for seed in range(1, runs + 1):
+            r = oracle.ransac_run(oracle.HOMOGRAPHY, pts, 2.0, 0.95, seed, max_iters=15000,
+                                  sampler=oracle.SAMPLER_PROSAC if sampler == "prosac" else oracle.SAMPLER_UNIFORM,
+                                  sprt=sprt, lo=oracle.LO_GC, cell_size=50, knn=7,
+                                  neighbors=oracle.NEIGHBORS_NANOFLANN if nb == "knn" else oracle.NEIGHBORS_GRID)
+            inl.append(r["inliers"] if r["ret"] == 0 else 0)
+        results[scene] = {INL: inl}
+    pinned = check(rel, results, [(INL, SD_INL)], {INL: inl_floor})
+    assert len(pinned) >= 12, pinned
 
 
 def _line2d_runs(oracle, pts, runs, **kw):
