@@ -13,6 +13,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -186,6 +187,17 @@ struct PinnedPool {
         free.emplace(c, p);
     }
 };
+
+// Wait for a stream by polling it: the loop's host replay waits on the device dozens of
+// times per run (LO stages, batches, polish), and a blocking hipStreamSynchronize adds a wake-up
+// latency of ~20 us each time; polling returns within about a microsecond of completion.
+hipError_t stream_wait(hipStream_t st) {
+    for (uint32_t spins = 0;; spins++) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e != hipErrorNotReady) return e;
+        if ((spins & 1023u) == 1023u) std::this_thread::yield();
+    }
+}
 
 }  // namespace
 
@@ -366,7 +378,7 @@ int download_grid(usac_ctx *c, int cs, std::unique_ptr<usac::GridNeighbors> &out
                               c->stream));
     HIP_TRY(c, hipMemcpyAsync(members.data(), c->grid_members.p, sizeof(int32_t) * c->n, hipMemcpyDeviceToHost,
                               c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
     out.reset(new usac::GridNeighbors(std::move(cell), std::move(rank), std::move(start), std::move(members)));
     return USAC_OK;
 }
@@ -695,7 +707,7 @@ struct LoRansac {
                                               c->lo_lists.as<int32_t>(), n, dcnt, dsum, c->lo_scr.p,
                                               fit ? dok : nullptr));
         HIP_TRY(c, hipMemcpyAsync(hmod, dmod, out_bytes, hipMemcpyDeviceToHost, st));
-        HIP_TRY(c, hipStreamSynchronize(st));
+        HIP_TRY(c, stream_wait(st));
         stages++;
         for (uint32_t w = 0; w < W; w++) {
             Chain &h = ch[w];
@@ -883,7 +895,7 @@ int exact_sums(usac_ctx *c, float thr, int best_count, const int32_t *hc, const 
                                               c->lo_sums.as<float>(), c->lo_scr.p));
         HIP_TRY(c, hipMemcpyAsync(cc.data(), c->lo_cnts.p, sizeof(int32_t) * K, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, hipMemcpyAsync(cs.data(), c->lo_sums.p, sizeof(float) * K, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        HIP_TRY(c, stream_wait(c->stream));
         for (uint32_t k = 0; k < K; k++) {
             if (cc[k] != hc[cand[k0 + k]])
                 return fail(c, USAC_ERR_HIP, "score kernel count differs from the exact recount (slot " +
@@ -970,7 +982,7 @@ struct GcLo {
         HIP_TRY(c, usac::launch_point_errors(c->stream, c->estimator, c->pts.p, n, c->one_model.as<float>(),
                                              c->gc_err.as<float>()));
         HIP_TRY(c, hipMemcpyAsync(err.data(), c->gc_err.p, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        HIP_TRY(c, stream_wait(c->stream));
         for (uint32_t i = 0; i < n; i++) {
             const float d = err[i];
             en[i] = (float)std::exp((double)(-(d * d) / sqr_thr));
@@ -1066,7 +1078,7 @@ struct GcLo {
         HIP_TRY(c, hipMemcpyAsync(hok.data(), c->lo_ok.p, sizeof(int32_t) * W, hipMemcpyDeviceToHost, st));
         HIP_TRY(c, hipMemcpyAsync(hcnt.data(), c->lo_cnts.p, sizeof(int32_t) * W, hipMemcpyDeviceToHost, st));
         HIP_TRY(c, hipMemcpyAsync(hsum.data(), c->lo_sums.p, sizeof(float) * W, hipMemcpyDeviceToHost, st));
-        HIP_TRY(c, hipStreamSynchronize(st));
+        HIP_TRY(c, stream_wait(st));
         stages++;
         return USAC_OK;
     }
@@ -1204,7 +1216,7 @@ int usac_estimate_models(usac_ctx *c, const int32_t *samples, uint32_t B, float 
     HIP_TRY(c, hipMemcpyAsync(soa.data(), c->models.p, sizeof(float) * soa.size(), hipMemcpyDeviceToHost, c->stream));
     if (listed(c))
         HIP_TRY(c, hipMemcpyAsync(slot_cnt.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
     const int nc = ncomp(c);
     for (size_t sl = 0; sl < S; sl++) {
         const bool ok = slot_cnt[sl] >= 0;
@@ -1259,7 +1271,7 @@ int usac_score_models(usac_ctx *c, const float *models, uint32_t nm, float thr, 
     }
     HIP_TRY(c, hipMemcpyAsync(counts, c->counts.p, sizeof(int32_t) * nm, hipMemcpyDeviceToHost, c->stream));
     if (sums) HIP_TRY(c, hipMemcpyAsync(sums, c->sums.p, sizeof(float) * nm, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
     return USAC_OK;
 }
 
@@ -1274,7 +1286,7 @@ int usac_get_inliers(usac_ctx *c, const float *model, float thr, int32_t *idx, u
     float s = 0.f;
     HIP_TRY(c, hipMemcpyAsync(&cnt, c->inl_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipMemcpyAsync(&s, c->inl_sum.p, sizeof(float), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
     if (idx && cnt > 0)
         HIP_TRY(c, hipMemcpy(idx, c->inl_idx.p, sizeof(int32_t) * (size_t)cnt, hipMemcpyDeviceToHost));
     if (n) *n = (uint32_t)cnt;
@@ -1303,7 +1315,7 @@ int usac_knn(usac_ctx *c, uint32_t k, int32_t *idx, float *d2) {
                                 d2 ? c->knn_d2.as<float>() : nullptr));
     HIP_TRY(c, hipMemcpyAsync(idx, c->knn_idx.p, sizeof(int32_t) * nk, hipMemcpyDeviceToHost, c->stream));
     if (d2) HIP_TRY(c, hipMemcpyAsync(d2, c->knn_d2.p, sizeof(float) * nk, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
     return USAC_OK;
 }
 
@@ -1323,7 +1335,7 @@ int usac_nonminimal(usac_ctx *c, const int32_t *idx, uint32_t n, float *model) {
     int32_t ok = 0;
     HIP_TRY(c, hipMemcpyAsync(model, c->nm_model.p, sizeof(float) * 9, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipMemcpyAsync(&ok, c->nm_ok.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
     return ok ? USAC_OK : fail(c, USAC_ERR_NO_MODEL, "non-minimal estimation failed");
 }
 
@@ -1350,7 +1362,7 @@ int usac_hypothesize_score(usac_ctx *c, const int32_t *samples, uint32_t B, uint
     if (counts) HIP_TRY(c, hipMemcpyAsync(counts, c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
     if (sums) HIP_TRY(c, hipMemcpyAsync(sums, c->sums.p, sizeof(float) * S, hipMemcpyDeviceToHost, c->stream));
     if (best) HIP_TRY(c, hipMemcpyAsync(best, c->best.p, sizeof(usac_record), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
     return USAC_OK;
 }
 
@@ -1378,20 +1390,20 @@ int usac_last_counts(usac_ctx *c, int32_t *counts, float *sums, uint32_t n) {
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipMemcpyAsync(counts, c->counts.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
     if (sums) HIP_TRY(c, hipMemcpyAsync(sums, c->sums.p, sizeof(float) * n, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
     return USAC_OK;
 }
 
 int usac_fetch_best(usac_ctx *c, usac_record *best) {
     if (!c || !best) return USAC_ERR_ARG;
     HIP_TRY(c, hipMemcpyAsync(best, c->best.p, sizeof(usac_record), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
     return USAC_OK;
 }
 
 int usac_sync(usac_ctx *c) {
     if (!c) return USAC_ERR_ARG;
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
     return USAC_OK;
 }
 
@@ -1471,7 +1483,7 @@ int usac_grid_neighbors(usac_ctx *c, int cell_size, uint32_t *n_cells, uint32_t 
     if (eligible && c->grid_n_elig)
         HIP_TRY(c, hipMemcpyAsync(eligible, c->grid_elig.p, 4 * (size_t)c->grid_n_elig, hipMemcpyDeviceToHost,
                                   c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
     return USAC_OK;
 }
 
@@ -1483,7 +1495,7 @@ int usac_draw_samples(usac_ctx *c, uint32_t B, uint64_t seed, uint64_t first_hyp
     HIP_TRY(c, usac::launch_draw_samples(c->stream, (int)c->m, c->n, B, dev_sampler(c, seed), first_hyp,
                                          c->samples.as<int32_t>()));
     HIP_TRY(c, hipMemcpyAsync(out, c->samples.p, sizeof(int32_t) * (size_t)B * c->m, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
     return USAC_OK;
 }
 
@@ -1511,7 +1523,7 @@ int usac_set_sprt(usac_ctx *c, int enable, uint32_t seed, double epsilon, double
     HIP_TRY(c, usac::launch_gather_points(c->stream, c->pts.p, c->cols, c->pool_idx.as<uint32_t>(), c->n,
                                           c->sprt_pts.p));
     HIP_TRY(c, hipMemsetAsync(c->sprt_tested.p, 0, sizeof(uint32_t), c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
     c->sprt_on = true;
     return USAC_OK;
 }
@@ -1521,7 +1533,7 @@ int usac_sprt_tested(usac_ctx *c, uint64_t *points_tested) {
     if (!c->sprt_on) return fail(c, USAC_ERR_ARG, "SPRT not enabled");
     uint32_t t = 0;
     HIP_TRY(c, hipMemcpyAsync(&t, c->sprt_tested.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
     *points_tested = t;
     return USAC_OK;
 }
@@ -1586,7 +1598,7 @@ static int sharded_batch(usac_ctx *c, const int32_t *hs, uint32_t B, uint32_t it
             HIP_TRY(c, hipMemcpyAsync(send + (1 + (size_t)k) * Ps, c->models.as<float>() + (size_t)k * Ss,
                                       sizeof(float) * Ss, hipMemcpyDeviceToHost, c->stream));
     }
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
     if (gather) {
         if (gather(user, send, bytes, recv) != 0) return fail(c, USAC_ERR_ARG, "all-gather callback failed");
     } else {
@@ -1595,7 +1607,7 @@ static int sharded_batch(usac_ctx *c, const int32_t *hs, uint32_t B, uint32_t it
         HIP_TRY(c, hipMemcpyAsync(c->x_send.p, send, bytes, hipMemcpyHostToDevice, c->stream));
         NCCL_TRY(c, ncclAllGather(c->x_send.p, c->x_recv.p, bytes, ncclUint8, c->comm, c->stream));
         HIP_TRY(c, hipMemcpyAsync(recv, c->x_recv.p, bytes * (size_t)nranks, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        HIP_TRY(c, stream_wait(c->stream));
     }
     for (int r = 0; r < nranks; r++) {
         const uint32_t lr = std::min<uint32_t>(B, (uint32_t)r * P);
@@ -1756,7 +1768,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         HIP_TRY(c, enqueue_inliers(c, c->one_model.as<float>(), thr));
         HIP_TRY(c, hipMemcpyAsync(&cnt, c->inl_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, hipMemcpyAsync(&s, c->inl_sum.p, sizeof(float), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        HIP_TRY(c, stream_wait(c->stream));
         return USAC_OK;
     };
 
@@ -1819,7 +1831,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
             if (listed(c)) {  // occupied slots -> mask rows
                 HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
                 HIP_TRY(c, hipMemcpyAsync(&rows, c->list_n.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
-                HIP_TRY(c, hipStreamSynchronize(c->stream));
+                HIP_TRY(c, stream_wait(c->stream));
                 if (rows) HIP_TRY(c, hipMemcpyAsync(hlist.data(), c->list.p, sizeof(uint32_t) * rows,
                                                     hipMemcpyDeviceToHost, c->stream));
             } else {
@@ -1829,7 +1841,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                 HIP_TRY(c, hipMemcpyAsync(hmask.data() + (size_t)w * rows, c->masks.as<uint32_t>() + (size_t)w * S,
                                           sizeof(uint32_t) * rows, hipMemcpyDeviceToHost, c->stream));
         }
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        HIP_TRY(c, stream_wait(c->stream));
         }
         if (sprt) {
             if (listed(c)) {
@@ -1962,7 +1974,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         HIP_TRY(c, enqueue_nonminimal(c, c->inl_idx.as<int32_t>(), (uint32_t)best.inlier_number));
         HIP_TRY(c, hipMemcpyAsync(nm_model, c->nm_model.p, sizeof(float) * 9, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, hipMemcpyAsync(&ok, c->nm_ok.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipStreamSynchronize(c->stream));
+        HIP_TRY(c, stream_wait(c->stream));
         if (!ok) break;
         if ((rc = score_inliers(nm_model))) return rc;
         if ((double)((float)cnt / (float)best.inlier_number) < 0.8) break;
@@ -2031,7 +2043,7 @@ int usac_allgather_records(usac_ctx *c, const usac_record *local, usac_record *a
     NCCL_TRY(c, ncclAllGather(c->rec_send.p, c->rec_all.p, sizeof(usac_record), ncclUint8, c->comm, c->stream));
     HIP_TRY(c, hipMemcpyAsync(all, c->rec_all.p, sizeof(usac_record) * (size_t)c->nranks, hipMemcpyDeviceToHost,
                               c->stream));
-    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
     return USAC_OK;
 }
 
