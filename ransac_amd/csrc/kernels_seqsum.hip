@@ -92,7 +92,7 @@ __global__ __launch_bounds__(kCand) void k_seq_seg(const typename Op<F64>::V *__
     };
     fetch(0);
     // the earlier segments' sums through LDS (one parallel load, not a dependent load per add)
-    if (t < j * NCH) sp[t] = psum[t];
+    for (uint32_t i = t; i < j * NCH; i += kCand) sp[i] = psum[i];
     __syncthreads();
     float s[NCH];
 #pragma unroll
