@@ -43,6 +43,53 @@ __global__ __launch_bounds__(256) void k_gather(const P *__restrict__ pts, const
     q[w * q_stride + i] = pts[list[j]];
 }
 
+// the gather fused with the coordinate chains' fp64 segment sums (seqsum psum layout, 4 chains):
+// workgroup (segment j, fit w) gathers its segment, four points per thread in flight
+__global__ __launch_bounds__(256) void k_gather_psum4(const float4 *__restrict__ pts, const int32_t *__restrict__ base,
+                                                      size_t base_stride, const int32_t *__restrict__ pos,
+                                                      size_t pos_stride, const uint32_t *__restrict__ ns, uint32_t n1,
+                                                      float4 *__restrict__ q_all, size_t q_stride, char *seq_all,
+                                                      size_t sstride) {
+    __shared__ double red[4][256];
+    const uint32_t j = blockIdx.x, w = blockIdx.y;
+    const uint32_t n = ns ? ns[w] : n1, L = seq::seg_len(n);
+    if (j * L >= n) return;
+    const uint32_t e = (j + 1) * L < n ? (j + 1) * L : n;
+    const int32_t *list = base + w * base_stride;
+    float4 *q = q_all + w * q_stride;
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    for (uint32_t i0 = j * L + threadIdx.x; i0 < e; i0 += 4 * 256) {
+        float4 p[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + 256 * u;
+            if (i < e) p[u] = pts[list[pos ? pos[w * pos_stride + i] : (int32_t)i]];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + 256 * u;
+            if (i < e) {
+                q[i] = p[u];
+                a[0] += (double)p[u].x;
+                a[1] += (double)p[u].y;
+                a[2] += (double)p[u].z;
+                a[3] += (double)p[u].w;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) red[k][threadIdx.x] = a[k];
+    __syncthreads();
+    for (uint32_t h = 128; h > 0; h >>= 1) {
+        if (threadIdx.x < h)
+#pragma unroll
+            for (int k = 0; k < 4; k++) red[k][threadIdx.x] += red[k][threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x < 4) reinterpret_cast<double *>(seq_all + w * sstride)[j * 4 + threadIdx.x] = red[threadIdx.x][0];
+}
+constexpr uint32_t kFusedGatherMax = 64 * 1024;  // up to 8 points per thread and segment
+
 // normalizing transformation (GetNormalizingTransformation, normalizing_transformation.cpp:
 // 7-113): the four coordinate means and the two average distances are the reference's
 // sequential fp32 sums in point order, evaluated bit-exactly in parallel by launch_seqsum
@@ -94,36 +141,38 @@ __global__ __launch_bounds__(256) void k_norm_dist(const float4 *__restrict__ q_
     if (threadIdx.x < 2) reinterpret_cast<double *>(seq)[j * 2 + threadIdx.x] = red[threadIdx.x][0];
 }
 
-// T1, T2 from the sums (the reference's expressions) into ws, and q <- normalised points
-// ws layout (floats): [0..8] T1, [9..17] T2.
-__global__ __launch_bounds__(256) void k_norm_apply(float4 *__restrict__ q_all, size_t q_stride,
-                                                    const uint32_t *__restrict__ ns, uint32_t n1,
-                                                    const float *__restrict__ sums4, const float *__restrict__ dsum2,
-                                                    float *ws_all) {
-    const uint32_t w = blockIdx.y;
-    const uint32_t n = ns ? ns[w] : n1;
+// T1, T2 from the sums (the reference's expressions; ws layout (floats): [0..8] T1, [9..17]
+// T2).  The normalised points are never stored: the A^T A pass (and the thin solve) apply
+// x' = T[0] x + T[2], y' = T[4] y + T[5] on the fly -- the same float operations.
+__device__ __forceinline__ void norm_transforms(const float *__restrict__ sums4, const float *__restrict__ dsum2,
+                                                uint32_t w, uint32_t n, float *t1, float *t2) {
     float mean[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) mean[k] = sums4[4 * w + k] / (float)n;
     const float s1 = (float)(M_SQRT2 / (double)(dsum2[2 * w + 0] / (float)n));
     const float s2 = (float)(M_SQRT2 / (double)(dsum2[2 * w + 1] / (float)n));
-    const float t1[9] = {s1, 0.f, -mean[0] * s1, 0.f, s1, -mean[1] * s1, 0.f, 0.f, 1.f};
-    const float t2[9] = {s2, 0.f, -mean[2] * s2, 0.f, s2, -mean[3] * s2, 0.f, 0.f, 1.f};
-    const uint32_t t = threadIdx.x;
-    if (blockIdx.x == 0 && t < 9) {
-        ws_all[18 * w + t] = t1[t];
-        ws_all[18 * w + 9 + t] = t2[t];
+    const float a[9] = {s1, 0.f, -mean[0] * s1, 0.f, s1, -mean[1] * s1, 0.f, 0.f, 1.f};
+    const float c[9] = {s2, 0.f, -mean[2] * s2, 0.f, s2, -mean[3] * s2, 0.f, 0.f, 1.f};
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        t1[k] = a[k];
+        t2[k] = c[k];
     }
-    const uint32_t i = blockIdx.x * 256 + t;
-    if (i >= n) return;
-    float4 *q = q_all + w * q_stride;
-    const float4 p = q[i];
-    float4 o;
-    o.x = t1[0] * p.x + t1[2];
-    o.y = t1[4] * p.y + t1[5];
-    o.z = t2[0] * p.z + t2[2];
-    o.w = t2[4] * p.w + t2[5];
-    q[i] = o;
+}
+
+struct NormXf {
+    float ax, bx, ay, by, az, bz, aw, bw;
+    __device__ __forceinline__ float4 operator()(const float4 p) const {
+        float4 o;
+        o.x = ax * p.x + bx;
+        o.y = ay * p.y + by;
+        o.z = az * p.z + bz;
+        o.w = aw * p.w + bw;
+        return o;
+    }
+};
+__device__ __forceinline__ NormXf norm_xf(const float *t1, const float *t2) {
+    return NormXf{t1[0], t1[2], t1[4], t1[5], t2[0], t2[2], t2[4], t2[5]};
 }
 
 // block partials of A^T A: one lane per (64-point block, group of 9 of the 45 upper-triangle
@@ -134,12 +183,12 @@ __global__ __launch_bounds__(256) void k_norm_apply(float4 *__restrict__ q_all, 
 constexpr int kAtaGroups = 5;  // 45 = 5 x 9 entries
 
 template <bool FUND, int G>
-__device__ __forceinline__ void ata_group(const float4 *q, uint32_t b0, uint32_t b1, double *out) {
+__device__ __forceinline__ void ata_group(const float4 *q, const NormXf xf, uint32_t b0, uint32_t b1, double *out) {
     double acc[9];
 #pragma unroll
     for (int e = 0; e < 9; e++) acc[e] = 0.0;
     for (uint32_t i = b0; i < b1; i++) {
-        const float4 p = q[i];
+        const float4 p = xf(q[i]);
         double r0[9], r1[9];
         if (FUND) fund_row(p.x, p.y, p.z, p.w, r0);
         else dlt_rows(p.x, p.y, p.z, p.w, r0, r1);
@@ -160,21 +209,30 @@ __device__ __forceinline__ void ata_group(const float4 *q, uint32_t b0, uint32_t
 template <bool FUND>
 __global__ __launch_bounds__(64) void k_ata_partial(const float4 *__restrict__ q_all, size_t q_stride,
                                                     const uint32_t *__restrict__ ns, uint32_t n1,
-                                                    double *__restrict__ partial_all, size_t p_stride) {
+                                                    double *__restrict__ partial_all, size_t p_stride,
+                                                    const float *__restrict__ sums4, const float *__restrict__ dsum2,
+                                                    float *__restrict__ ws_all) {
     const uint32_t w = blockIdx.z;
     const uint32_t n = ns ? ns[w] : n1;
+    float t1[9], t2[9];
+    norm_transforms(sums4, dsum2, w, n, t1, t2);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 9) {
+        ws_all[18 * w + threadIdx.x] = t1[threadIdx.x];
+        ws_all[18 * w + 9 + threadIdx.x] = t2[threadIdx.x];
+    }
     const uint32_t blk = blockIdx.x * 64 + threadIdx.x;
     if ((FUND ? n <= 8 : 2 * n <= 9) || blk * kAtaBlock >= n) return;
+    const NormXf xf = norm_xf(t1, t2);
     const float4 *q = q_all + w * q_stride;
     const uint32_t b0 = blk * kAtaBlock;
     const uint32_t b1 = b0 + kAtaBlock < n ? b0 + kAtaBlock : n;
     double *out = partial_all + w * p_stride + (size_t)blk * 45;
     switch (blockIdx.y) {
-        case 0: ata_group<FUND, 0>(q, b0, b1, out); break;
-        case 1: ata_group<FUND, 1>(q, b0, b1, out); break;
-        case 2: ata_group<FUND, 2>(q, b0, b1, out); break;
-        case 3: ata_group<FUND, 3>(q, b0, b1, out); break;
-        default: ata_group<FUND, 4>(q, b0, b1, out); break;
+        case 0: ata_group<FUND, 0>(q, xf, b0, b1, out); break;
+        case 1: ata_group<FUND, 1>(q, xf, b0, b1, out); break;
+        case 2: ata_group<FUND, 2>(q, xf, b0, b1, out); break;
+        case 3: ata_group<FUND, 3>(q, xf, b0, b1, out); break;
+        default: ata_group<FUND, 4>(q, xf, b0, b1, out); break;
     }
 }
 
@@ -186,18 +244,18 @@ __global__ __launch_bounds__(64) void k_ata_partial(const float4 *__restrict__ q
 //                (eight_points.cpp:76-99);
 // cast to float.
 template <int R, bool FUND>
-__device__ void thin_solve(const float4 *q, double *v) {
+__device__ void thin_solve(const float4 *q, const NormXf xf, double *v) {
     double W[R][9];
     if (FUND) {
 #pragma unroll
         for (int i = 0; i < R; i++) {
-            const float4 p = q[i];
+            const float4 p = xf(q[i]);
             fund_row(p.x, p.y, p.z, p.w, W[i]);
         }
     } else {
 #pragma unroll
         for (int i = 0; i < R / 2; i++) {
-            const float4 p = q[i];
+            const float4 p = xf(q[i]);
             dlt_rows(p.x, p.y, p.z, p.w, W[2 * i], W[2 * i + 1]);
         }
     }
@@ -228,23 +286,24 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
     }
     if (FUND ? n <= 8 : 2 * n <= 9) {
         if (t == 0) {
+            const NormXf xf = norm_xf(ws, ws + 9);
             double v[9];
             if (FUND) {
                 switch (n) {
-                    case 1: thin_solve<1, true>(q, v); break;
-                    case 2: thin_solve<2, true>(q, v); break;
-                    case 3: thin_solve<3, true>(q, v); break;
-                    case 4: thin_solve<4, true>(q, v); break;
-                    case 5: thin_solve<5, true>(q, v); break;
-                    case 6: thin_solve<6, true>(q, v); break;
-                    case 7: thin_solve<7, true>(q, v); break;
-                    default: thin_solve<8, true>(q, v); break;
+                    case 1: thin_solve<1, true>(q, xf, v); break;
+                    case 2: thin_solve<2, true>(q, xf, v); break;
+                    case 3: thin_solve<3, true>(q, xf, v); break;
+                    case 4: thin_solve<4, true>(q, xf, v); break;
+                    case 5: thin_solve<5, true>(q, xf, v); break;
+                    case 6: thin_solve<6, true>(q, xf, v); break;
+                    case 7: thin_solve<7, true>(q, xf, v); break;
+                    default: thin_solve<8, true>(q, xf, v); break;
                 }
             } else {
-                if (n == 1) thin_solve<2, false>(q, v);
-                else if (n == 2) thin_solve<4, false>(q, v);
-                else if (n == 3) thin_solve<6, false>(q, v);
-                else thin_solve<8, false>(q, v);
+                if (n == 1) thin_solve<2, false>(q, xf, v);
+                else if (n == 2) thin_solve<4, false>(q, xf, v);
+                else if (n == 3) thin_solve<6, false>(q, xf, v);
+                else thin_solve<8, false>(q, xf, v);
             }
             for (int k = 0; k < 9; k++) s_v[k] = v[k];
         }
@@ -278,11 +337,9 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
             for (int j = 0; j < 9; j++) V[j][t] = (j == (int)t) ? 1.0 : 0.0;
         __syncthreads();
         // round-robin Jacobi (the oracle's sym_eig_min spec): per round the rotations of 4
-        // disjoint planes from the matrix at the round's start (lanes 0-3), then all column
-        // updates (lane = (row, plane), V alongside), then all row updates (lane = (plane,
-        // column)) -- every lane owns disjoint element pairs, 3 barriers per round
-        __shared__ double s_cs[4][2];
-        __shared__ int s_on[4];
+        // disjoint planes from the matrix at the round's start, then all column updates (lane =
+        // (row, plane), V alongside), then all row updates (lane = (plane, column)) -- every
+        // lane owns disjoint element pairs, 3 barriers per round
         __shared__ signed char s_rounds[9][4][2];  // the schedule in LDS (not a global load per use)
         for (uint32_t i = t; i < 72; i += 64) (&s_rounds[0][0][0])[i] = (&kJacobiRounds[0][0][0])[i];
         __syncthreads();
@@ -294,29 +351,26 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
             }
             if (off <= 1e-30 * diag || off == 0.0) break;
             for (int r = 0; r < 9; r++) {
-                if (t < 4) {
-                    const int p = s_rounds[r][t][0], qq = s_rounds[r][t][1];
-                    const double apq = A[p][qq];
-                    s_on[t] = apq != 0.0;
-                    if (apq != 0.0) {
-                        const double theta = (A[qq][qq] - A[p][p]) / (2.0 * apq);
-                        const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-                        const double c = 1.0 / sqrt(tt * tt + 1.0);
-                        s_cs[t][0] = c;
-                        s_cs[t][1] = tt * c;
-                    }
-                }
-                __syncthreads();
-                const int k = (int)t / 9, e = (int)t - 9 * k;  // 36 lanes: plane k, row / column e
-                const bool act = t < 36 && s_on[k < 4 ? k : 0];
+                // lanes (plane k, row / column e), 36 of them: each computes its plane's
+                // rotation itself (the same expressions, so the same bits in the 9 lanes of a
+                // plane) -- no LDS exchange of (c, s) between the rotation and the updates
+                const int k = (int)t / 9, e = (int)t - 9 * k;
+                bool act = false;
                 int p = 0, qq = 0;
                 double c = 0.0, sn = 0.0;
                 if (t < 36) {
                     p = s_rounds[r][k][0];
                     qq = s_rounds[r][k][1];
-                    c = s_cs[k][0];
-                    sn = s_cs[k][1];
+                    const double apq = A[p][qq];
+                    act = apq != 0.0;
+                    if (act) {
+                        const double theta = (A[qq][qq] - A[p][p]) / (2.0 * apq);
+                        const double tt = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                        c = 1.0 / sqrt(tt * tt + 1.0);
+                        sn = tt * c;
+                    }
                 }
+                __syncthreads();  // every lane read its plane's entries before any update
                 if (act) {  // columns p, q of row e; V likewise
                     const double aip = A[e][p], aiq = A[e][qq];
                     A[e][p] = c * aip - sn * aiq;
@@ -452,30 +506,38 @@ hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pt
         return hipGetLastError();
     }
     float4 *q = static_cast<float4 *>(b.q);
-    hipLaunchKernelGGL(k_gather<float4>, gg, dim3(256), 0, st, static_cast<const float4 *>(pts), b.base,
-                       b.base_stride, b.pos, b.pos_stride, b.ns, b.n1, q, b.q_stride);
-    {  // normalising transforms: sequential sums (seqsum), distance terms, apply
+    {  // gather; normalising transforms: sequential sums (seqsum), distance terms
         char *seq = static_cast<char *>(b.seq);
         const size_t ss = seq_stride(b.nmax);
         float *sums4 = reinterpret_cast<float *>(seq + b.W * ss), *dsum2 = sums4 + 4 * b.W;
-        hipError_t e = launch_seqsum(st, 4, false, q, 4 * b.q_stride, b.ns, b.n1, b.W, nullptr, seq, ss, false, sums4);
+        const bool fused = b.nmax <= kFusedGatherMax;
+        if (fused)
+            hipLaunchKernelGGL(k_gather_psum4, dim3(seq::kSegMax, b.W), dim3(256), 0, st,
+                               static_cast<const float4 *>(pts), b.base, b.base_stride, b.pos, b.pos_stride, b.ns,
+                               b.n1, q, b.q_stride, seq, ss);
+        else
+            hipLaunchKernelGGL(k_gather<float4>, gg, dim3(256), 0, st, static_cast<const float4 *>(pts), b.base,
+                               b.base_stride, b.pos, b.pos_stride, b.ns, b.n1, q, b.q_stride);
+        hipError_t e = launch_seqsum(st, 4, false, q, 4 * b.q_stride, b.ns, b.n1, b.W, nullptr, seq, ss, fused, sums4);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_norm_dist, dim3(seq::kSegMax, b.W), dim3(256), 0, st, q, b.q_stride, b.ns, b.n1, seq, ss,
                            sums4);
         e = launch_seqsum(st, 2, true, reinterpret_cast<const double *>(seq + kSeqA), ss / sizeof(double), b.ns, b.n1,
                           b.W, nullptr, seq, ss, true, dsum2);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_norm_apply, dim3((b.nmax + 255) / 256 ? (b.nmax + 255) / 256 : 1, b.W), dim3(256), 0, st,
-                           q, b.q_stride, b.ns, b.n1, sums4, dsum2, b.ws);
     }
+    const char *seq = static_cast<const char *>(b.seq);
+    const float *sums4 = reinterpret_cast<const float *>(seq + b.W * seq_stride(b.nmax)), *dsum2 = sums4 + 4 * b.W;
     const uint32_t nblk = (b.nmax + kAtaBlock - 1) / kAtaBlock;
     const dim3 ga(nblk ? (nblk + 63) / 64 : 1, kAtaGroups, b.W);
     if (estimator == USAC_HOMOGRAPHY) {
-        hipLaunchKernelGGL(k_ata_partial<false>, ga, dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial, b.p_stride);
+        hipLaunchKernelGGL(k_ata_partial<false>, ga, dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial, b.p_stride,
+                           sums4, dsum2, b.ws);
         hipLaunchKernelGGL(k_dlt_finish<false>, dim3(b.W), dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial,
                            b.p_stride, b.ws, b.model_out, b.ok);
     } else {
-        hipLaunchKernelGGL(k_ata_partial<true>, ga, dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial, b.p_stride);
+        hipLaunchKernelGGL(k_ata_partial<true>, ga, dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial, b.p_stride,
+                           sums4, dsum2, b.ws);
         hipLaunchKernelGGL(k_dlt_finish<true>, dim3(b.W), dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial,
                            b.p_stride, b.ws, b.model_out, b.ok);
     }
