@@ -180,30 +180,57 @@ __device__ __forceinline__ NormXf norm_xf(const float *t1, const float *t2) {
 // a compile-time constant in the body; each entry accumulated in registers over the block's
 // points in order (the spec's unit and order; the grouping only spreads the entries over
 // lanes).  FUND: one 8-point row per correspondence (eight_points.cpp:26-45), else two DLT rows.
-constexpr int kAtaGroups = 5;  // 45 = 5 x 9 entries
+constexpr int kAtaGroups = 5;                  // 45 = 5 x 9 entries
+constexpr int kAtaPer = 45 / kAtaGroups;
 
 template <bool FUND, int G>
 __device__ __forceinline__ void ata_group(const float4 *q, const NormXf xf, uint32_t b0, uint32_t b1, double *out) {
-    double acc[9];
+    double acc[kAtaPer];
 #pragma unroll
-    for (int e = 0; e < 9; e++) acc[e] = 0.0;
-    for (uint32_t i = b0; i < b1; i++) {
-        const float4 p = xf(q[i]);
-        double r0[9], r1[9];
-        if (FUND) fund_row(p.x, p.y, p.z, p.w, r0);
-        else dlt_rows(p.x, p.y, p.z, p.w, r0, r1);
-        int e = 0;
+    for (int e = 0; e < kAtaPer; e++) acc[e] = 0.0;
+    // the block's points in batches of 8, the next batch's loads in flight while the current
+    // one is accumulated (one point at a time would wait a memory latency per point)
+    constexpr uint32_t kB = 8;
+    float4 cur[kB], nxt[kB];
+    auto load = [&](float4 (&x)[kB], uint32_t i0) {
 #pragma unroll
-        for (int j = 0; j < 9; j++)
+        for (uint32_t u = 0; u < kB; u++) x[u] = i0 + u < b1 ? q[i0 + u] : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    load(cur, b0);
+    for (uint32_t i0 = b0; i0 < b1; i0 += kB) {
+        if (i0 + kB < b1) load(nxt, i0 + kB);
 #pragma unroll
-            for (int k = j; k < 9; k++, e++) {
-                if (e < 9 * G || e >= 9 * G + 9) continue;
-                if (FUND) acc[e - 9 * G] += r0[j] * r0[k];
-                else acc[e - 9 * G] += r0[j] * r0[k] + r1[j] * r1[k];
-            }
+        for (uint32_t u = 0; u < kB; u++) {
+            if (i0 + u >= b1) break;
+            const float4 p = xf(cur[u]);
+            double r0[9], r1[9];
+            if (FUND) fund_row(p.x, p.y, p.z, p.w, r0);
+            else dlt_rows(p.x, p.y, p.z, p.w, r0, r1);
+            int e = 0;
+#pragma unroll
+            for (int j = 0; j < 9; j++)
+#pragma unroll
+                for (int k = j; k < 9; k++, e++) {
+                    if (e < kAtaPer * G || e >= kAtaPer * (G + 1)) continue;
+                    if (FUND) acc[e - kAtaPer * G] += r0[j] * r0[k];
+                    else acc[e - kAtaPer * G] += r0[j] * r0[k] + r1[j] * r1[k];
+                }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kB; u++) cur[u] = nxt[u];
     }
 #pragma unroll
-    for (int e = 0; e < 9; e++) out[9 * G + e] = acc[e];
+    for (int e = 0; e < kAtaPer; e++) out[kAtaPer * G + e] = acc[e];
+}
+
+// group g (wave-uniform) to its compile-time instance
+template <bool FUND, int G = 0>
+__device__ __forceinline__ void ata_dispatch(int g, const float4 *q, const NormXf xf, uint32_t b0, uint32_t b1,
+                                             double *out) {
+    if constexpr (G + 1 < kAtaGroups) {
+        if (g != G) return ata_dispatch<FUND, G + 1>(g, q, xf, b0, b1, out);
+    }
+    ata_group<FUND, G>(q, xf, b0, b1, out);
 }
 
 template <bool FUND>
@@ -227,13 +254,7 @@ __global__ __launch_bounds__(64) void k_ata_partial(const float4 *__restrict__ q
     const uint32_t b0 = blk * kAtaBlock;
     const uint32_t b1 = b0 + kAtaBlock < n ? b0 + kAtaBlock : n;
     double *out = partial_all + w * p_stride + (size_t)blk * 45;
-    switch (blockIdx.y) {
-        case 0: ata_group<FUND, 0>(q, xf, b0, b1, out); break;
-        case 1: ata_group<FUND, 1>(q, xf, b0, b1, out); break;
-        case 2: ata_group<FUND, 2>(q, xf, b0, b1, out); break;
-        case 3: ata_group<FUND, 3>(q, xf, b0, b1, out); break;
-        default: ata_group<FUND, 4>(q, xf, b0, b1, out); break;
-    }
+    ata_dispatch<FUND>((int)blockIdx.y, q, xf, b0, b1, out);
 }
 
 // Final solve, one wave: A^T A from the partials (lane e), round-robin Jacobi eigen over
