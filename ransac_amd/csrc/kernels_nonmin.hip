@@ -364,6 +364,15 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
         __shared__ signed char s_rounds[9][4][2];  // the schedule in LDS (not a global load per use)
         for (uint32_t i = t; i < 72; i += 64) (&s_rounds[0][0][0])[i] = (&kJacobiRounds[0][0][0])[i];
         __syncthreads();
+        // lanes (plane k, row / column e), 36 of them; each lane's plane of every round in
+        // registers (the round loop unrolls), so a round starts with one LDS read, not two
+        const int k = (int)t / 9, e = (int)t - 9 * k;
+        int rp[9], rq[9];
+#pragma unroll
+        for (int r = 0; r < 9; r++) {
+            rp[r] = t < 36 ? s_rounds[r][k][0] : 0;
+            rq[r] = t < 36 ? s_rounds[r][k][1] : 0;
+        }
         for (int sweep = 0; sweep < 50; sweep++) {
             double off = 0.0, diag = 0.0;
             for (int p = 0; p < 9; p++) {
@@ -371,18 +380,21 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
                 for (int qq = p + 1; qq < 9; qq++) off += A[p][qq] * A[p][qq];
             }
             if (off <= 1e-30 * diag || off == 0.0) break;
+#pragma unroll
             for (int r = 0; r < 9; r++) {
-                // lanes (plane k, row / column e), 36 of them: each computes its plane's
-                // rotation itself (the same expressions, so the same bits in the 9 lanes of a
-                // plane) -- no LDS exchange of (c, s) between the rotation and the updates
-                const int k = (int)t / 9, e = (int)t - 9 * k;
+                // each lane computes its plane's rotation itself (the same expressions, so the
+                // same bits in the 9 lanes of a plane: no LDS exchange of (c, s)); the column
+                // update's operands are the round-start values, so they are read here too and
+                // their LDS latency overlaps the rotation's fp64 chain
+                const int p = rp[r], qq = rq[r];
                 bool act = false;
-                int p = 0, qq = 0;
-                double c = 0.0, sn = 0.0;
+                double c = 0.0, sn = 0.0, aip = 0.0, aiq = 0.0, vip = 0.0, viq = 0.0;
                 if (t < 36) {
-                    p = s_rounds[r][k][0];
-                    qq = s_rounds[r][k][1];
                     const double apq = A[p][qq];
+                    aip = A[e][p];
+                    aiq = A[e][qq];
+                    vip = V[e][p];
+                    viq = V[e][qq];
                     act = apq != 0.0;
                     if (act) {
                         const double theta = (A[qq][qq] - A[p][p]) / (2.0 * apq);
@@ -391,12 +403,10 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
                         sn = tt * c;
                     }
                 }
-                __syncthreads();  // every lane read its plane's entries before any update
+                __syncthreads();  // every lane read its entries before any update
                 if (act) {  // columns p, q of row e; V likewise
-                    const double aip = A[e][p], aiq = A[e][qq];
                     A[e][p] = c * aip - sn * aiq;
                     A[e][qq] = sn * aip + c * aiq;
-                    const double vip = V[e][p], viq = V[e][qq];
                     V[e][p] = c * vip - sn * viq;
                     V[e][qq] = sn * vip + c * viq;
                 }
