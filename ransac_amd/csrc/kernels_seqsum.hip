@@ -69,7 +69,7 @@ __global__ __launch_bounds__(kCand) void k_seq_seg(const typename Op<F64>::V *__
                                                    const uint32_t *__restrict__ ns, uint32_t n1,
                                                    const uint32_t *__restrict__ slots, char *scratch, size_t sstride) {
     typedef typename Op<F64>::V V;
-    constexpr uint32_t kChunk = NCH == 1 ? 2048 : 1024;  // elements per LDS chunk
+    constexpr uint32_t kChunk = (NCH == 1 ? 8 : 4) * kCand;  // elements per LDS chunk (2048 / 1024 at 256 candidates)
     constexpr uint32_t kPer = kChunk * NCH / kCand;      // values per thread per chunk
     __shared__ V sv[2][kChunk * NCH];
     __shared__ double sp[kSegMax * NCH];

@@ -56,17 +56,19 @@ def test_residual_sum_adversarial(usac, kind):
     assert _residual_sum(usac, errs).view(np.int32) == _seq_sum(errs).view(np.int32)
 
 
-@pytest.mark.parametrize("n", [5000, 40000, 200000])
+@pytest.mark.parametrize("n", [5000, 40000, 65536, 65537, 200000])
 def test_normalization_long_chains(usac, oracle, n):
     """NormalizedDLT on n correspondences: its four coordinate means and two distance sums are
-    sequential chains of n elements (up to 32 segments of 6 k); model bits = the oracle's."""
+    sequential chains of n elements (up to 32 segments of 6 k); model bits = the oracle's.
+    65536 / 65537: either side of the fused gather + segment-sum kernel's limit
+    (kernels_nonmin.hip kFusedGatherMax)."""
     rng = np.random.default_rng(n)
     x1 = rng.uniform(0, 4000, (n, 2))
     H = np.array([[1.1, 0.05, 30.0], [-0.04, 0.95, -12.0], [1e-5, -2e-5, 1.0]])
     p = np.c_[x1, np.ones(n)] @ H.T
     x2 = p[:, :2] / p[:, 2:] + rng.normal(0, 0.5, (n, 2))
     pts = np.ascontiguousarray(np.c_[x1, x2], dtype=np.float32)
-    idx = np.arange(n, dtype=np.int32)
+    idx = rng.permutation(n).astype(np.int32) if n % 2 else np.arange(n, dtype=np.int32)
     est = oracle.Estimator(oracle.HOMOGRAPHY, pts)
     o = est.nonminimal(idx)
     with usac.Context(usac.ESTIMATOR.Homography, pts) as ctx:
