@@ -5,8 +5,9 @@
 // and PROSAC's termination scan.
 //
 //   k_inl_flags   grid over points: exact residual, per-block inlier count      (parallel)
-//   k_inl_scan    one workgroup: exclusive scan of the block counts -> offsets  (tiny)
-//   k_inl_compact grid over points: ordered compaction of indices and residuals (parallel)
+//   k_inl_compact grid over points: each block sums the earlier blocks' counts (its output
+//                 offset; the last block writes the total), ordered compaction of indices
+//                 and residuals                                                 (parallel)
 //   seqsum        the sequential fp32 sum over the compacted residuals
 //                 (the reference's order; evaluated in parallel, bit-exactly, by launch_seqsum)
 #include <hip/hip_runtime.h>
@@ -90,43 +91,16 @@ __global__ __launch_bounds__(kInlBlock) void k_inl_flags(const void *__restrict_
     }
 }
 
-__global__ __launch_bounds__(1024) void k_inl_scan(uint32_t *__restrict__ scratch, uint32_t n, uint32_t nblocks,
-                                                   const uint32_t *__restrict__ slots, int32_t *__restrict__ totals) {
-    // exclusive scan in place, 1024 threads, sequential chunks per thread
-    __shared__ uint32_t part[1024];
-    const uint32_t w = inl_slot(slots, blockIdx.x);
-    uint32_t *block_counts = scratch + w * inl_stride(n);
-    const uint32_t t = threadIdx.x;
-    const uint32_t per = (nblocks + 1023) / 1024;
-    const uint32_t b0 = t * per, b1 = b0 + per < nblocks ? b0 + per : nblocks;
-    uint32_t s = 0;
-    for (uint32_t b = b0; b < b1; b++) s += block_counts[b];
-    part[t] = s;
-    __syncthreads();
-    for (uint32_t off = 1; off < 1024; off <<= 1) {
-        const uint32_t v = t >= off ? part[t - off] : 0;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    uint32_t run = part[t] - s;  // exclusive prefix of this thread's chunk
-    for (uint32_t b = b0; b < b1; b++) {
-        const uint32_t c = block_counts[b];
-        block_counts[b] = run;
-        run += c;
-    }
-    if (t == 1023) totals[w] = (int32_t)part[1023];
-}
-
 template <int EST>
 __global__ __launch_bounds__(kInlBlock) void k_inl_compact(const void *__restrict__ pts, uint32_t n,
                                                            const float *__restrict__ models, float thr,
                                                            const float *__restrict__ thrs,
                                                            const uint32_t *__restrict__ slots,
                                                            uint32_t *__restrict__ scratch, int32_t *__restrict__ idx,
-                                                           size_t idx_stride, const int32_t *__restrict__ ok) {
+                                                           size_t idx_stride, const int32_t *__restrict__ ok,
+                                                           int32_t *__restrict__ totals) {
     __shared__ float sm[18];
-    __shared__ uint32_t wsum[kInlBlock / 64];
+    __shared__ uint32_t wsum[kInlBlock / 64], wpre[kInlBlock / 64];
     const uint32_t ws = inl_slot(slots, blockIdx.y);
     if (ok && !ok[ws]) return;  // a failed fit: its list is left as it was (workgroup-uniform)
     inl_model<EST>(models + 9 * (size_t)ws, sm);
@@ -136,7 +110,7 @@ __global__ __launch_bounds__(kInlBlock) void k_inl_compact(const void *__restric
     for (int k = 0; k < 18; k++) m[k] = sm[k];
     const size_t stride = inl_stride(n);
     const uint32_t nb = (n + kInlBlock - 1) / kInlBlock;
-    const uint32_t *block_offsets = scratch + ws * stride;
+    const uint32_t *block_counts = scratch + ws * stride;
     float *errs = reinterpret_cast<float *>(scratch + ws * stride + ((nb + 63) & ~63u));
     const uint32_t i = blockIdx.x * kInlBlock + threadIdx.x;
     const float e = i < n ? inl_error<EST>(m, pts, i) : 0.f;
@@ -145,7 +119,20 @@ __global__ __launch_bounds__(kInlBlock) void k_inl_compact(const void *__restric
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) wsum[wave] = (uint32_t)__popcll(bal);
     __syncthreads();
-    uint32_t base = block_offsets[blockIdx.x];
+    // this block's output offset: the sum of the earlier blocks' counts (k_inl_flags), summed
+    // here (integers: any order) -- no separate scan launch; the last block writes the total
+    uint32_t pre = 0;
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += kInlBlock) pre += block_counts[b];
+    for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
+    if (lane == 0) wpre[wave] = pre;
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t w = 0; w < kInlBlock / 64; w++) base += wpre[w];
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+        uint32_t tot = base;
+        for (uint32_t w = 0; w < kInlBlock / 64; w++) tot += wsum[w];
+        totals[ws] = (int32_t)tot;
+    }
     for (uint32_t w = 0; w < wave; w++) base += wsum[w];
     if (in) {
         const uint32_t r = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
@@ -164,9 +151,8 @@ hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, 
 #define INL(E)                                                                                                   \
     do {                                                                                                         \
         hipLaunchKernelGGL(k_inl_flags<E>, grid, dim3(kInlBlock), 0, st, pts, n, models, thr, thrs, slots, scr);        \
-        hipLaunchKernelGGL(k_inl_scan, dim3(W), dim3(1024), 0, st, scr, n, nb, slots, counts);                         \
         hipLaunchKernelGGL(k_inl_compact<E>, grid, dim3(kInlBlock), 0, st, pts, n, models, thr, thrs, slots, scr, \
-                           idx, idx_stride, ok);                                                                 \
+                           idx, idx_stride, ok, counts);                                                         \
     } while (0)
     switch (estimator) {
         case USAC_LINE2D: INL(USAC_LINE2D); break;
