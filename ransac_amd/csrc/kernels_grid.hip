@@ -22,6 +22,8 @@
 //   8. exclusive scan + k_grid_compact: the eligible points, ascending.
 #include <hip/hip_runtime.h>
 
+#include <thread>
+
 #include <string.h>
 
 #include <algorithm>
@@ -189,6 +191,16 @@ size_t grid_workspace_bytes(uint32_t n) {
         if (e_ != hipSuccess) return e_;    \
     } while (0)
 
+// wait for the stream by polling (a blocking synchronise adds a ~20 us wake-up; usac_api.cpp
+// stream_wait does the same for the loop's waits)
+static hipError_t poll_stream(hipStream_t st) {
+    for (uint32_t spins = 0;; spins++) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e != hipErrorNotReady) return e;
+        if ((spins & 1023u) == 1023u) std::this_thread::yield();
+    }
+}
+
 hipError_t build_grid(hipStream_t st, const float4 *pts, uint32_t n, int cell_size, int4 cmin, uint32_t m, void *ws,
                       uint32_t *cell, uint32_t *rank, uint32_t *start, int32_t *members, int32_t *eligible,
                       uint32_t *n_cells_out, uint32_t *n_elig_out) {
@@ -208,7 +220,7 @@ hipError_t build_grid(hipStream_t st, const float4 *pts, uint32_t n, int cell_si
     GRID_TRY(hipGetLastError());
     uint32_t nc = 0;
     GRID_TRY(hipMemcpyAsync(&nc, s.counts, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    GRID_TRY(hipStreamSynchronize(st));
+    GRID_TRY(poll_stream(st));
     tb = s.tmp_bytes;
     GRID_TRY(rocprim::radix_sort_pairs(s.tmp, tb, s.old_min, s.min_b, s.ord_a, s.ord_b, nc, 0, 32, st));
     hipLaunchKernelGGL(k_grid_renumber, dim3((nc + 1 + 255) / 256), b, 0, st, s.ord_b, s.old_start, nc, s.new_of_old,
@@ -225,7 +237,7 @@ hipError_t build_grid(hipStream_t st, const float4 *pts, uint32_t n, int cell_si
     GRID_TRY(hipGetLastError());
     uint32_t ne = 0;
     GRID_TRY(hipMemcpyAsync(&ne, s.counts + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    GRID_TRY(hipStreamSynchronize(st));
+    GRID_TRY(poll_stream(st));
     *n_cells_out = nc;
     *n_elig_out = ne;
     return hipSuccess;

@@ -1677,6 +1677,13 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     if (rc) return rc;
     rc = ensure_single(c);
     if (rc) return rc;
+    // sub-split of the setup (USAC_PROFILE): buffers, neighbours, LO / GC reservations
+    double tsub[3] = {0, 0, 0};
+    auto sub = [&](int k) {
+        const auto t = std::chrono::steady_clock::now();
+        tsub[k] = std::chrono::duration<double, std::milli>(t - tmark).count();
+    };
+    sub(0);
     const int saved_mode = c->dlt_mode;
     c->dlt_mode = prm->dlt_mode;
     const bool saved_sprt = c->sprt_on;  // the replay verifies exactly; the batch test is off
@@ -1716,6 +1723,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     } else {
         uni.reset(new usac::UniformSampler(grng, n, m));
     }
+    sub(1);
     std::unique_ptr<LoRansac> lo;
     if (use_lo) {
         lo.reset(new LoRansac(c, prm));
@@ -1732,6 +1740,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         gc.reset(new GcLo(c, prm, gc_knn ? knn_tab.data() : nullptr, prm->knn, grid.get()));
         if ((rc = gc->reserve())) return rc;
     }
+    sub(2);
     usac::StandardTerminationCriteria term(prm->desired_prob, m, n, prm->max_iterations);
     std::unique_ptr<usac::Sprt> sprt;
     const uint32_t nw = (n + 31) / 32;
@@ -1990,9 +1999,10 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     if (getenv("USAC_PROFILE"))
         fprintf(stderr,
                 "usac_ransac_run ms: setup %.3f draw %.3f device %.3f sums %.3f replay %.3f lo %.3f polish %.3f "
-                "(lo rounds %u stages %u)\n",
+                "(lo rounds %u stages %u; setup: buffers %.3f neighbours %.3f lo/gc %.3f)\n",
                 tsplit[T_SETUP], tsplit[T_DRAW], tsplit[T_DEVICE], tsplit[T_SUMS], tsplit[T_REPLAY], tsplit[T_LO],
-                tsplit[T_POLISH], lo ? lo->rounds : gc ? gc->labelings : 0u, lo ? lo->stages : gc ? gc->stages : 0u);
+                tsplit[T_POLISH], lo ? lo->rounds : gc ? gc->labelings : 0u, lo ? lo->stages : gc ? gc->stages : 0u,
+                tsub[0], tsub[1] - tsub[0], tsub[2] - tsub[1]);
     if ((rc = score_inliers(best_model))) return rc;  // ransac.cpp:214
     if (inliers_out && cnt > 0)
         HIP_TRY(c, hipMemcpy(inliers_out, c->inl_idx.p, sizeof(int32_t) * (size_t)cnt, hipMemcpyDeviceToHost));
