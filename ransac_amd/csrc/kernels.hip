@@ -395,17 +395,22 @@ __global__ __launch_bounds__(256) void k_score_ycombine(const int32_t *__restric
 
 // Hypothesis pre-sort for the fast score kernel: forward-distance hits of every hypothesis
 // on the first kPresortGroups point groups (fp32 with v_rcp -- a heuristic, it only
-// decides WHERE a hypothesis is scored, never its result).  Hypotheses with >= kPresortHits
-// hits go to the front of perm, the rest to the back (wave-aggregated atomics).
+// decides WHERE a hypothesis is scored, never its result).  Within each region of R
+// hypotheses (R a multiple of 64; the launch uses one region) those with >= kPresortHits hits
+// go to the front, the rest to the back: one packed 64-bit atomic per workgroup on the
+// region's counter ((good << 32) | bad); the workgroup that completes a region puts its
+// counter back to 0, so the next launch needs no memset (the counters are zeroed once, when
+// the buffer is allocated).
 constexpr uint32_t kPresortGroups = 32;  // 128 points
 constexpr int kPresortHits = 3;
 
 constexpr int kPresortWaves = 4;  // waves per 64 hypotheses, each on kPresortGroups / 4 groups
+constexpr uint32_t kPresortCtr = 256;  // region counters at the head of the pre-sort buffer
 
 __global__ __launch_bounds__(64 * kPresortWaves) void k_presort_h(const float4 *__restrict__ rec, uint32_t n,
                                                                   const float *__restrict__ models, uint32_t B,
                                                                   float thr, uint32_t *__restrict__ perm,
-                                                                  uint32_t *__restrict__ ends) {
+                                                                  unsigned long long *__restrict__ ctr, uint32_t R) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t h = blockIdx.x * 64 + lane;
@@ -442,16 +447,22 @@ __global__ __launch_bounds__(64 * kPresortWaves) void k_presort_h(const float4 *
     const bool good = valid && hits >= kPresortHits;
     const uint64_t bg = __ballot(good), bb = __ballot(valid && !good);
     const uint32_t below = (uint32_t)__popcll(good ? bg & ((1ull << lane) - 1) : bb & ((1ull << lane) - 1));
-    uint32_t fbase = 0, bbase = 0;
+    const uint32_t r = blockIdx.x * 64 / R, rs = r * R, re = rs + R < B ? rs + R : B;
+    const uint32_t ng = (uint32_t)__popcll(bg), nbad = (uint32_t)__popcll(bb);
+    unsigned long long old = 0;
     if (lane == 0) {
-        if (bg) fbase = atomicAdd(&ends[0], (uint32_t)__popcll(bg));
-        if (bb) bbase = atomicAdd(&ends[1], (uint32_t)__popcll(bb));
+        old = atomicAdd(&ctr[r], ((unsigned long long)ng << 32) | nbad);
+        const uint32_t done = (uint32_t)(old >> 32) + (uint32_t)old + ng + nbad;
+        if (done == re - rs) __hip_atomic_store(&ctr[r], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    fbase = __shfl(fbase, 0, 64);
-    bbase = __shfl(bbase, 0, 64);
-    const uint32_t at = good ? fbase + below : B - 1 - (bbase + below);
-    if (valid && at < B) perm[at] = h;  // (the counters reach B exactly: one grid row of workgroups)
+    old = __shfl(old, 0, 64);
+    const uint32_t fbase = rs + (uint32_t)(old >> 32), bbase = (uint32_t)old;
+    const uint32_t at = good ? fbase + below : re - 1 - (bbase + below);
+    if (valid && at < re) perm[at] = h;  // (each region's counts reach its size exactly)
 }
+
+size_t presort_bytes(uint32_t B) { return sizeof(unsigned long long) * kPresortCtr + sizeof(uint32_t) * (size_t)B; }
+size_t presort_counter_bytes() { return sizeof(unsigned long long) * kPresortCtr; }
 
 // ------------------------------------------------------------------------ line2d
 __global__ __launch_bounds__(256) void k_solve_line(const float2 *__restrict__ pts, uint32_t n,
@@ -651,11 +662,14 @@ hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const flo
     dim3 grid((B + 63) / 64, ysplit);
     int32_t *pc = ysplit > 1 ? static_cast<int32_t *>(yscratch) : nullptr;
     float *ps = ysplit > 1 ? reinterpret_cast<float *>(pc + (size_t)ysplit * B) : nullptr;
-    if (perm) {  // perm: B entries followed by 2 counters
-        uint32_t *ends = perm + B;
-        hipError_t e = hipMemsetAsync(ends, 0, 2 * sizeof(uint32_t), st);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_presort_h, dim3((B + 63) / 64), dim3(64 * kPresortWaves), 0, st, rec, n, models, B, thr, perm, ends);
+    if (perm) {  // the pre-sort buffer (presort_bytes): region counters, then the B entries
+        unsigned long long *ctr = reinterpret_cast<unsigned long long *>(perm);
+        perm += 2 * kPresortCtr;
+        // one region: the front-loaded order (stage-B-heavy hypotheses first) is what pays; a
+        // region per 4096 hypotheses measured 0.33 ms against 0.22 for the score kernel
+        const uint32_t R = (B + 63) & ~63u;
+        hipLaunchKernelGGL(k_presort_h, dim3((B + 63) / 64), dim3(64 * kPresortWaves), 0, st, rec, n, models, B, thr,
+                           perm, ctr, R);
     }
 #define SHF(C, E) \
     hipLaunchKernelGGL((k_score_hf<C, E>), grid, dim3(64 * C), 0, st, rec, n, ext, models, B, thr, perm, counts, sums, \

@@ -215,7 +215,8 @@ struct usac_ctx {
     uint32_t prosac_len = 0;  // its entries
     int dev_sampler = USAC_SAMPLER_UNIFORM;
     DevBuf tv_part;         // two-view scorer scratch: pre-sort permutation, chunk partials
-    DevBuf perm;            // hypothesis pre-sort order of the fast kernel (B + 2 uint32)
+    DevBuf perm;            // hypothesis pre-sort of the fast kernel (usac::presort_bytes)
+    void *perm_zeroed = nullptr;  // the perm block whose region counters were zeroed
     DevBuf hf_part;         // fast-kernel partials of a point range split over workgroups
     float rec_thr = -1.f;   // threshold the record bands were built for
     float4 ext = {0, 0, 0, 0};  // dataset box: max |x1|, |y1|, |x2|, |y2| (fast-kernel bounds)
@@ -446,8 +447,13 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
                                         c->counts.as<int32_t>(), c->sums.as<float>());
         uint32_t *perm = nullptr;
         if (c->score_variant == 0) {  // 2: fast kernel without the hypothesis pre-sort (A/B)
-            hipError_t e = c->perm.reserve(sizeof(uint32_t) * ((size_t)B + 2));
+            hipError_t e = c->perm.reserve(usac::presort_bytes(B));
             if (e != hipSuccess) return e;
+            if (c->perm_zeroed != c->perm.p) {  // a new block: its region counters start at 0
+                e = hipMemsetAsync(c->perm.p, 0, usac::presort_counter_bytes(), c->stream);
+                if (e != hipSuccess) return e;
+                c->perm_zeroed = c->perm.p;
+            }
             perm = c->perm.as<uint32_t>();
         }
         // small batches over many points (the loop's batches): split each tile's points over

@@ -56,6 +56,10 @@ hipError_t launch_prepare_rec(hipStream_t st, const float4 *pts, uint32_t n, flo
 // perm (nullable, B + 2 uint32): hypothesis pre-sort scratch (k_presort_h)
 // ysplit > 1 (throughput mode): every 64-hypothesis tile's points over chunks x ysplit waves in
 // ysplit workgroups, partials in yscratch (8 B x ysplit x B) added in order by a second launch
+// the fast scorer's hypothesis pre-sort buffer: region counters (zeroed once, when the buffer
+// is allocated: every launch leaves them at 0), then B permutation entries
+size_t presort_bytes(uint32_t B);
+size_t presort_counter_bytes();
 hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const float4 *rec, uint32_t n, float4 ext,
                            const float *models, uint32_t B, float thr, uint32_t *perm, int32_t *counts, float *sums,
                            uint32_t ysplit = 1, void *yscratch = nullptr);
