@@ -404,16 +404,19 @@ __global__ __launch_bounds__(256) void k_score_ycombine(const int32_t *__restric
 constexpr uint32_t kPresortGroups = 32;  // 128 points
 constexpr int kPresortHits = 3;
 
-constexpr int kPresortWaves = 4;  // waves per 64 hypotheses, each on kPresortGroups / 4 groups
+constexpr int kPresortWaves = 4;       // waves per workgroup, 64 hypotheses each
 constexpr uint32_t kPresortCtr = 256;  // region counters at the head of the pre-sort buffer
 
+// One workgroup = 4 x 64 hypotheses, each lane over all kPresortGroups groups; the four waves'
+// good / bad counts are combined in LDS so the workgroup takes its places with ONE atomic
+// (the atomics on the region counter, not the arithmetic, set this kernel's time).
 __global__ __launch_bounds__(64 * kPresortWaves) void k_presort_h(const float4 *__restrict__ rec, uint32_t n,
                                                                   const float *__restrict__ models, uint32_t B,
                                                                   float thr, uint32_t *__restrict__ perm,
                                                                   unsigned long long *__restrict__ ctr, uint32_t R) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t h = blockIdx.x * 64 + lane;
+    const uint32_t h = blockIdx.x * (64 * kPresortWaves) + threadIdx.x;
     const uint32_t hc = h < B ? h : B - 1;
     float m[9];
 #pragma unroll
@@ -421,10 +424,8 @@ __global__ __launch_bounds__(64 * kPresortWaves) void k_presort_h(const float4 *
     const float T2 = 4.0f * thr * thr;  // forward distance < 2 thr
     const uint32_t ngroups = (n + 3) / 4;
     const uint32_t g1 = ngroups < kPresortGroups ? ngroups : kPresortGroups;
-    constexpr uint32_t per = kPresortGroups / kPresortWaves;
-    const uint32_t gb = wave * per < g1 ? wave * per : g1, ge = gb + per < g1 ? gb + per : g1;
     int hits = 0;
-    for (uint32_t g = gb; g < ge; g++) {
+    for (uint32_t g = 0; g < g1; g++) {
         const float *p = reinterpret_cast<const float *>(rec + 8 * (size_t)g);
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -437,26 +438,38 @@ __global__ __launch_bounds__(64 * kPresortWaves) void k_presort_h(const float4 *
             hits += __builtin_fmaf(dx, dx, dy * dy) < T2 ? 1 : 0;
         }
     }
-    __shared__ int s_hits[kPresortWaves][64];
-    s_hits[wave][lane] = hits;
-    __syncthreads();
-    if (wave != 0) return;
-#pragma unroll
-    for (int w = 1; w < kPresortWaves; w++) hits += s_hits[w][lane];
     const bool valid = h < B;
     const bool good = valid && hits >= kPresortHits;
     const uint64_t bg = __ballot(good), bb = __ballot(valid && !good);
     const uint32_t below = (uint32_t)__popcll(good ? bg & ((1ull << lane) - 1) : bb & ((1ull << lane) - 1));
-    const uint32_t r = blockIdx.x * 64 / R, rs = r * R, re = rs + R < B ? rs + R : B;
-    const uint32_t ng = (uint32_t)__popcll(bg), nbad = (uint32_t)__popcll(bb);
-    unsigned long long old = 0;
+    __shared__ uint32_t s_g[kPresortWaves], s_b[kPresortWaves];
+    __shared__ unsigned long long s_old;
     if (lane == 0) {
-        old = atomicAdd(&ctr[r], ((unsigned long long)ng << 32) | nbad);
+        s_g[wave] = (uint32_t)__popcll(bg);
+        s_b[wave] = (uint32_t)__popcll(bb);
+    }
+    __syncthreads();
+    const uint32_t h0 = blockIdx.x * (64 * kPresortWaves);
+    const uint32_t r = h0 / R, rs = r * R, re = rs + R < B ? rs + R : B;
+    uint32_t ng = 0, nbad = 0, gw = 0, bw = 0;
+#pragma unroll
+    for (int w = 0; w < kPresortWaves; w++) {
+        if ((uint32_t)w < wave) {
+            gw += s_g[w];
+            bw += s_b[w];
+        }
+        ng += s_g[w];
+        nbad += s_b[w];
+    }
+    if (threadIdx.x == 0) {
+        const unsigned long long old = atomicAdd(&ctr[r], ((unsigned long long)ng << 32) | nbad);
         const uint32_t done = (uint32_t)(old >> 32) + (uint32_t)old + ng + nbad;
         if (done == re - rs) __hip_atomic_store(&ctr[r], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_old = old;
     }
-    old = __shfl(old, 0, 64);
-    const uint32_t fbase = rs + (uint32_t)(old >> 32), bbase = (uint32_t)old;
+    __syncthreads();
+    const unsigned long long old = s_old;
+    const uint32_t fbase = rs + (uint32_t)(old >> 32) + gw, bbase = (uint32_t)old + bw;
     const uint32_t at = good ? fbase + below : re - 1 - (bbase + below);
     if (valid && at < re) perm[at] = h;  // (each region's counts reach its size exactly)
 }
@@ -667,9 +680,9 @@ hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const flo
         perm += 2 * kPresortCtr;
         // one region: the front-loaded order (stage-B-heavy hypotheses first) is what pays; a
         // region per 4096 hypotheses measured 0.33 ms against 0.22 for the score kernel
-        const uint32_t R = (B + 63) & ~63u;
-        hipLaunchKernelGGL(k_presort_h, dim3((B + 63) / 64), dim3(64 * kPresortWaves), 0, st, rec, n, models, B, thr,
-                           perm, ctr, R);
+        const uint32_t R = (B + 255) & ~255u;  // a multiple of the workgroup's 256 hypotheses
+        hipLaunchKernelGGL(k_presort_h, dim3((B + 64 * kPresortWaves - 1) / (64 * kPresortWaves)),
+                           dim3(64 * kPresortWaves), 0, st, rec, n, models, B, thr, perm, ctr, R);
     }
 #define SHF(C, E) \
     hipLaunchKernelGGL((k_score_hf<C, E>), grid, dim3(64 * C), 0, st, rec, n, ext, models, B, thr, perm, counts, sums, \
