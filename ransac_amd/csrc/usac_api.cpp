@@ -244,7 +244,7 @@ struct usac_ctx {
     DevBuf sprt_pts, sprt_tested, sprt_surv, sprt_surv_n;
     uint32_t spk = 1;       // model slots per hypothesis (3 for the 7-point solver)
     // single-model / polish buffers
-    DevBuf one_model, inl_idx, inl_cnt, inl_sum, inl_scratch, q, partial, ws, nm_model, nm_ok;
+    DevBuf one_model, inl_idx, inl_idx2, inl_cnt, inl_sum, inl_scratch, q, partial, ws, nm_model, nm_ok;
     DevBuf nm_seq;          // normalisation scratch of the non-minimal fits (polish and LO)
     DevBuf lo_io;           // one LO stage's inputs and outputs, contiguous (one copy each way)
     // comm
@@ -309,6 +309,7 @@ int ensure_batch(usac_ctx *c, uint32_t B) {
 int ensure_single(usac_ctx *c) {
     HIP_TRY(c, c->one_model.reserve(sizeof(float) * 9));
     HIP_TRY(c, c->inl_idx.reserve(sizeof(int32_t) * (size_t)std::max<uint32_t>(c->n, 1)));
+    HIP_TRY(c, c->inl_idx2.reserve(sizeof(int32_t) * (size_t)std::max<uint32_t>(c->n, 1)));
     HIP_TRY(c, c->inl_cnt.reserve(sizeof(int32_t)));
     HIP_TRY(c, c->inl_sum.reserve(sizeof(float)));
     HIP_TRY(c, c->q.reserve(sizeof(float) * 4 * (size_t)std::max<uint32_t>(c->n, 1)));
@@ -1167,7 +1168,7 @@ void usac_destroy(usac_ctx *c) {
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
                       &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->inl_scratch, &c->e5_ws, &c->one_model,
-                      &c->inl_idx, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq, &c->lo_io,
+                      &c->inl_idx, &c->inl_idx2, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq, &c->lo_io,
                       &c->rec_send, &c->rec_all, &c->tv_part, &c->hf_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
                       &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2, &c->gc_err, &c->grid_cell, &c->grid_rank, &c->grid_start,
@@ -1981,23 +1982,36 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     }
 
     lap(T_REPLAY);
-    // ---- polish (ransac.cpp:157-207) on the device
+    // ---- polish (ransac.cpp:157-207) on the device.  Each pass is one submission: the fit on
+    // the current list, then the fitted model scored from device memory (compaction gated on
+    // the fit's ok) into the other list buffer -- one host wait per pass; an accepted model's
+    // list becomes the current one, so after the loop `cur` holds best_model's own inliers
+    // (the same kernels, model and threshold as the final getInliers would use).
     if ((rc = score_inliers(best_model))) return rc;  // quality->getInliers(best_model)
+    int32_t *cur = c->inl_idx.as<int32_t>(), *alt = c->inl_idx2.as<int32_t>();
+    int32_t cur_cnt = cnt;
     int prev = 0;
     float nm_model[9];
     for (int norm = 0; norm < 4; norm++) {
-        HIP_TRY(c, enqueue_nonminimal(c, c->inl_idx.as<int32_t>(), (uint32_t)best.inlier_number));
+        HIP_TRY(c, enqueue_nonminimal(c, cur, (uint32_t)best.inlier_number));
+        HIP_TRY(c, c->inl_scratch.reserve(usac::inliers_scratch_bytes(c->n, 1)));
+        HIP_TRY(c, usac::launch_inliers_batch(c->stream, c->estimator, c->pts.p, c->n, c->nm_model.as<float>(), 1, thr,
+                                              nullptr, nullptr, alt, 0, c->inl_cnt.as<int32_t>(),
+                                              c->inl_sum.as<float>(), c->inl_scratch.p, c->nm_ok.as<int32_t>()));
         HIP_TRY(c, hipMemcpyAsync(nm_model, c->nm_model.p, sizeof(float) * 9, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, hipMemcpyAsync(&ok, c->nm_ok.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(&cnt, c->inl_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(&s, c->inl_sum.p, sizeof(float), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, stream_wait(c->stream));
         if (!ok) break;
-        if ((rc = score_inliers(nm_model))) return rc;
         if ((double)((float)cnt / (float)best.inlier_number) < 0.8) break;
         if (cnt <= prev) break;
         prev = cnt;
         best.inlier_number = cnt;
         best.score = s;
         memcpy(best_model, nm_model, sizeof(best_model));
+        std::swap(cur, alt);
+        cur_cnt = cnt;
         out->polish_passes++;
     }
     const auto t1 = std::chrono::steady_clock::now();
@@ -2009,9 +2023,10 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                 tsplit[T_SETUP], tsplit[T_DRAW], tsplit[T_DEVICE], tsplit[T_SUMS], tsplit[T_REPLAY], tsplit[T_LO],
                 tsplit[T_POLISH], lo ? lo->rounds : gc ? gc->labelings : 0u, lo ? lo->stages : gc ? gc->stages : 0u,
                 tsub[0], tsub[1] - tsub[0], tsub[2] - tsub[1]);
-    if ((rc = score_inliers(best_model))) return rc;  // ransac.cpp:214
+    // ransac.cpp:214 getInliers(best_model): `cur` already is that list (see above)
+    cnt = cur_cnt;
     if (inliers_out && cnt > 0)
-        HIP_TRY(c, hipMemcpy(inliers_out, c->inl_idx.p, sizeof(int32_t) * (size_t)cnt, hipMemcpyDeviceToHost));
+        HIP_TRY(c, hipMemcpy(inliers_out, cur, sizeof(int32_t) * (size_t)cnt, hipMemcpyDeviceToHost));
     memcpy(out->model, best_model, sizeof(best_model));
     out->inliers = best.inlier_number;
     out->time_us = std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
