@@ -245,6 +245,9 @@ struct usac_ctx {
     uint32_t spk = 1;       // model slots per hypothesis (3 for the 7-point solver)
     // single-model / polish buffers
     DevBuf one_model, inl_idx, inl_idx2, inl_cnt, inl_sum, inl_scratch, q, partial, ws, nm_model, nm_ok;
+    DevBuf pol_res;                  // polish pass results (model, ok, count, sum; initial count, sum)
+    void *pol_pin = nullptr;         // their pinned host copy (PinnedPool)
+    size_t pol_pin_bytes = 0;
     DevBuf nm_seq;          // normalisation scratch of the non-minimal fits (polish and LO)
     DevBuf lo_io;           // one LO stage's inputs and outputs, contiguous (one copy each way)
     // comm
@@ -495,7 +498,8 @@ hipError_t enqueue_inliers(usac_ctx *c, const float *model_dev, float thr) {
                                 c->inl_cnt.as<int32_t>(), c->inl_sum.as<float>(), c->inl_scratch.p);
 }
 
-hipError_t enqueue_nonminimal(usac_ctx *c, const int32_t *idx_dev, uint32_t n) {
+hipError_t enqueue_nonminimal(usac_ctx *c, const int32_t *idx_dev, uint32_t n, float *model_out = nullptr,
+                              int32_t *ok_out = nullptr) {
     hipError_t e = c->nm_seq.reserve(usac::nonminimal_seq_bytes(n, 1));
     if (e != hipSuccess) return e;
     usac::NmBatch b{};
@@ -507,8 +511,8 @@ hipError_t enqueue_nonminimal(usac_ctx *c, const int32_t *idx_dev, uint32_t n) {
     b.q = c->q.p;
     b.partial = c->partial.as<double>();
     b.ws = c->ws.as<float>();
-    b.model_out = c->nm_model.as<float>();
-    b.ok = c->nm_ok.as<int32_t>();
+    b.model_out = model_out ? model_out : c->nm_model.as<float>();
+    b.ok = ok_out ? ok_out : c->nm_ok.as<int32_t>();
     return usac::launch_nonminimal_batch(c->stream, c->estimator, c->pts.p, b);
 }
 
@@ -1165,10 +1169,11 @@ void usac_destroy(usac_ctx *c) {
     (void)hipSetDevice(c->device);  // the pools are per device
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
+    if (c->pol_pin) PinnedPool::get().give_back(c->pol_pin, c->pol_pin_bytes);
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
                       &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->inl_scratch, &c->e5_ws, &c->one_model,
-                      &c->inl_idx, &c->inl_idx2, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq, &c->lo_io,
+                      &c->inl_idx, &c->inl_idx2, &c->pol_res, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq, &c->lo_io,
                       &c->rec_send, &c->rec_all, &c->tv_part, &c->hf_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
                       &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2, &c->gc_err, &c->grid_cell, &c->grid_rank, &c->grid_start,
@@ -1987,22 +1992,36 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     // the fit's ok) into the other list buffer -- one host wait per pass; an accepted model's
     // list becomes the current one, so after the loop `cur` holds best_model's own inliers
     // (the same kernels, model and threshold as the final getInliers would use).
-    if ((rc = score_inliers(best_model))) return rc;  // quality->getInliers(best_model)
+    // The results of a pass land in one device block (pol_res: model[9], ok, count, sum, and
+    // the initial getInliers' count, sum) copied with one D2H into pinned memory; the initial
+    // getInliers(best_model) rides in the first pass's submission.
+    HIP_TRY(c, c->pol_res.reserve(sizeof(float) * 16));
+    HIP_TRY(c, c->inl_scratch.reserve(usac::inliers_scratch_bytes(c->n, 1)));
+    if (!c->pol_pin && !(c->pol_pin = PinnedPool::get().take(sizeof(float) * 16, &c->pol_pin_bytes)))
+        return fail(c, USAC_ERR_HIP, "pinned host allocation failed");
+    float *dres = c->pol_res.as<float>();
+    const float *hres = static_cast<const float *>(c->pol_pin);
     int32_t *cur = c->inl_idx.as<int32_t>(), *alt = c->inl_idx2.as<int32_t>();
-    int32_t cur_cnt = cnt;
+    HIP_TRY(c, hipMemcpyAsync(c->one_model.p, best_model, sizeof(float) * 9, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, usac::launch_inliers_batch(c->stream, c->estimator, c->pts.p, c->n, c->one_model.as<float>(), 1, thr,
+                                          nullptr, nullptr, cur, 0, reinterpret_cast<int32_t *>(dres + 12), dres + 13,
+                                          c->inl_scratch.p));  // quality->getInliers(best_model)
+    int32_t cur_cnt = 0;
     int prev = 0;
     float nm_model[9];
     for (int norm = 0; norm < 4; norm++) {
-        HIP_TRY(c, enqueue_nonminimal(c, cur, (uint32_t)best.inlier_number));
-        HIP_TRY(c, c->inl_scratch.reserve(usac::inliers_scratch_bytes(c->n, 1)));
-        HIP_TRY(c, usac::launch_inliers_batch(c->stream, c->estimator, c->pts.p, c->n, c->nm_model.as<float>(), 1, thr,
-                                              nullptr, nullptr, alt, 0, c->inl_cnt.as<int32_t>(),
-                                              c->inl_sum.as<float>(), c->inl_scratch.p, c->nm_ok.as<int32_t>()));
-        HIP_TRY(c, hipMemcpyAsync(nm_model, c->nm_model.p, sizeof(float) * 9, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipMemcpyAsync(&ok, c->nm_ok.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipMemcpyAsync(&cnt, c->inl_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipMemcpyAsync(&s, c->inl_sum.p, sizeof(float), hipMemcpyDeviceToHost, c->stream));
+        int32_t *dok = reinterpret_cast<int32_t *>(dres + 9);
+        HIP_TRY(c, enqueue_nonminimal(c, cur, (uint32_t)best.inlier_number, dres, dok));
+        HIP_TRY(c, usac::launch_inliers_batch(c->stream, c->estimator, c->pts.p, c->n, dres, 1, thr, nullptr, nullptr,
+                                              alt, 0, reinterpret_cast<int32_t *>(dres + 10), dres + 11,
+                                              c->inl_scratch.p, dok));
+        HIP_TRY(c, hipMemcpyAsync(c->pol_pin, dres, sizeof(float) * 14, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, stream_wait(c->stream));
+        memcpy(nm_model, hres, sizeof(nm_model));
+        memcpy(&ok, hres + 9, sizeof(int32_t));
+        memcpy(&cnt, hres + 10, sizeof(int32_t));
+        memcpy(&s, hres + 11, sizeof(float));
+        if (norm == 0) memcpy(&cur_cnt, hres + 12, sizeof(int32_t));
         if (!ok) break;
         if ((double)((float)cnt / (float)best.inlier_number) < 0.8) break;
         if (cnt <= prev) break;
