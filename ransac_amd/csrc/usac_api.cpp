@@ -188,6 +188,30 @@ struct PinnedPool {
     }
 };
 
+// std::vector storage in pinned host memory (PinnedPool), for the loop's DMA sources and
+// targets: a copy from / to pageable memory goes through a staging buffer and holds the host
+// for the copy; these copies sit between every device step and the host replay.
+template <class T>
+struct PinnedAlloc {
+    typedef T value_type;
+    PinnedAlloc() = default;
+    template <class U>
+    PinnedAlloc(const PinnedAlloc<U> &) {}
+    T *allocate(size_t k) {
+        size_t got = 0;
+        void *p = PinnedPool::get().take(sizeof(T) * (k ? k : 1), &got);
+        if (!p) throw std::bad_alloc();
+        return static_cast<T *>(p);
+    }
+    void deallocate(T *p, size_t k) { PinnedPool::get().give_back(p, DevPool::size_class(sizeof(T) * (k ? k : 1))); }
+    template <class U>
+    bool operator==(const PinnedAlloc<U> &) const { return true; }
+    template <class U>
+    bool operator!=(const PinnedAlloc<U> &) const { return false; }
+};
+template <class T>
+using pinned_vector = std::vector<T, PinnedAlloc<T>>;
+
 // Wait for a stream by polling it: the loop's host replay waits on the device dozens of
 // times per run (LO stages, batches, polish), and a blocking hipStreamSynchronize adds a wake-up
 // latency of ~20 us each time; polling returns within about a microsecond of completion.
@@ -889,9 +913,9 @@ int exact_sums(usac_ctx *c, float thr, int best_count, const int32_t *hc, const 
     }
     if (cand.empty()) return USAC_OK;
     const int nc = ncomp(c);
-    std::vector<float> am(9 * (size_t)kMax);
-    std::vector<int32_t> cc(kMax);
-    std::vector<float> cs(kMax);
+    pinned_vector<float> am(9 * (size_t)kMax);
+    pinned_vector<int32_t> cc(kMax);
+    pinned_vector<float> cs(kMax);
     HIP_TRY(c, c->lo_models.reserve(sizeof(float) * 9 * kMax));
     HIP_TRY(c, c->lo_cnts.reserve(sizeof(int32_t) * kMax));
     HIP_TRY(c, c->lo_sums.reserve(sizeof(float) * kMax));
@@ -1769,8 +1793,10 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
 
     const size_t SB = (size_t)batch * spk;  // slot stride of the host copies
     std::vector<uint8_t> xbuf;               // sharded runs: all-gather send + receive buffers
-    std::vector<int32_t> hs((size_t)batch * m, 0), hc(SB), slot_row(SB);
-    std::vector<float> hsum(SB), hmod((size_t)ncomp(c) * SB);
+    pinned_vector<int32_t> hs((size_t)batch * m, 0), hc(SB);
+    std::vector<int32_t> slot_row(SB);
+    std::vector<float> hsum(SB);
+    pinned_vector<float> hmod((size_t)ncomp(c) * SB);
     std::vector<uint32_t> hlist(SB), hmask(sprt ? (size_t)nw * SB : 0);
     std::vector<uint32_t> subset_at(batch), largest_at(batch);
     std::vector<int32_t> last_sample(m, 0);
