@@ -1810,12 +1810,22 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     // exact inliers of a model on the device -> (cnt, s) and c->inl_idx
     int32_t cnt = 0, ok = 0;
     float s = 0.f;
+    // (count, sum) of a host model through one pinned D2H (polish result block, slots 12-13)
+    HIP_TRY(c, c->pol_res.reserve(sizeof(float) * 16));
+    if (!c->pol_pin && !(c->pol_pin = PinnedPool::get().take(sizeof(float) * 16, &c->pol_pin_bytes)))
+        return fail(c, USAC_ERR_HIP, "pinned host allocation failed");
     auto score_inliers = [&](const float *model_host) -> int {
+        float *dres = c->pol_res.as<float>();
         HIP_TRY(c, hipMemcpyAsync(c->one_model.p, model_host, sizeof(float) * 9, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(c, enqueue_inliers(c, c->one_model.as<float>(), thr));
-        HIP_TRY(c, hipMemcpyAsync(&cnt, c->inl_cnt.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, hipMemcpyAsync(&s, c->inl_sum.p, sizeof(float), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, c->inl_scratch.reserve(usac::inliers_scratch_bytes(c->n, 1)));
+        HIP_TRY(c, usac::launch_inliers_batch(c->stream, c->estimator, c->pts.p, c->n, c->one_model.as<float>(), 1, thr,
+                                              nullptr, nullptr, c->inl_idx.as<int32_t>(), 0,
+                                              reinterpret_cast<int32_t *>(dres + 12), dres + 13, c->inl_scratch.p));
+        HIP_TRY(c, hipMemcpyAsync(static_cast<float *>(c->pol_pin) + 12, dres + 12, sizeof(float) * 2,
+                                  hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, stream_wait(c->stream));
+        memcpy(&cnt, static_cast<const float *>(c->pol_pin) + 12, sizeof(int32_t));
+        memcpy(&s, static_cast<const float *>(c->pol_pin) + 13, sizeof(float));
         return USAC_OK;
     };
 
@@ -2070,8 +2080,12 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                 tsub[0], tsub[1] - tsub[0], tsub[2] - tsub[1]);
     // ransac.cpp:214 getInliers(best_model): `cur` already is that list (see above)
     cnt = cur_cnt;
-    if (inliers_out && cnt > 0)
-        HIP_TRY(c, hipMemcpy(inliers_out, cur, sizeof(int32_t) * (size_t)cnt, hipMemcpyDeviceToHost));
+    if (inliers_out && cnt > 0) {  // DMA into pinned memory, then into the caller's buffer
+        pinned_vector<int32_t> stage((size_t)cnt);
+        HIP_TRY(c, hipMemcpyAsync(stage.data(), cur, sizeof(int32_t) * (size_t)cnt, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, stream_wait(c->stream));
+        memcpy(inliers_out, stage.data(), sizeof(int32_t) * (size_t)cnt);
+    }
     memcpy(out->model, best_model, sizeof(best_model));
     out->inliers = best.inlier_number;
     out->time_us = std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
