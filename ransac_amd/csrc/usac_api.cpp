@@ -399,15 +399,18 @@ int ensure_grid(usac_ctx *c, int cs) {
 int download_grid(usac_ctx *c, int cs, std::unique_ptr<usac::GridNeighbors> &out) {
     int rc = ensure_grid(c, cs);
     if (rc) return rc;
-    std::vector<uint32_t> cell(c->n), rank(c->n), start((size_t)c->grid_n_cells + 1);
-    std::vector<int32_t> members(c->n);
-    HIP_TRY(c, hipMemcpyAsync(cell.data(), c->grid_cell.p, sizeof(uint32_t) * c->n, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(rank.data(), c->grid_rank.p, sizeof(uint32_t) * c->n, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(start.data(), c->grid_start.p, sizeof(uint32_t) * start.size(), hipMemcpyDeviceToHost,
-                              c->stream));
-    HIP_TRY(c, hipMemcpyAsync(members.data(), c->grid_members.p, sizeof(int32_t) * c->n, hipMemcpyDeviceToHost,
-                              c->stream));
+    // DMA into one pinned block, then into the host vectors (the sampler reads them at random:
+    // they should be cache-warm, which DMA-written pinned memory is not)
+    const size_t n = c->n, nc1 = (size_t)c->grid_n_cells + 1;
+    pinned_vector<uint32_t> stage(3 * n + nc1);
+    uint32_t *w = stage.data();
+    HIP_TRY(c, hipMemcpyAsync(w, c->grid_cell.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(w + n, c->grid_rank.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(w + 2 * n, c->grid_members.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(w + 3 * n, c->grid_start.p, sizeof(uint32_t) * nc1, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, stream_wait(c->stream));
+    std::vector<uint32_t> cell(w, w + n), rank(w + n, w + 2 * n), start(w + 3 * n, w + 3 * n + nc1);
+    std::vector<int32_t> members(reinterpret_cast<const int32_t *>(w + 2 * n), reinterpret_cast<const int32_t *>(w + 3 * n));
     out.reset(new usac::GridNeighbors(std::move(cell), std::move(rank), std::move(start), std::move(members)));
     return USAC_OK;
 }
@@ -594,6 +597,7 @@ struct LoRansac {
     uint32_t *hns = nullptr, *hslots = nullptr;
     int32_t *hpos = nullptr, *hcnt = nullptr, *hok = nullptr;
     float *hthr = nullptr, *hsum = nullptr, *hmod = nullptr;
+    float *hmodel = nullptr;  // pinned slot of the model a round starts from (its H2D copy)
     uint32_t *dns = nullptr, *dslots = nullptr;
     int32_t *dpos = nullptr, *dcnt = nullptr, *dok = nullptr;
     float *dthr = nullptr, *dsum = nullptr, *dmod = nullptr;
@@ -625,8 +629,9 @@ struct LoRansac {
         in_bytes = sizeof(uint32_t) * (3 * W + W * L);
         out_bytes = sizeof(float) * 12 * W;
         HIP_TRY(c, c->lo_io.reserve(in_bytes + out_bytes));
-        pin = PinnedPool::get().take(in_bytes + out_bytes, &pin_bytes);
+        pin = PinnedPool::get().take(in_bytes + out_bytes + sizeof(float) * 16, &pin_bytes);
         if (!pin) return fail(c, USAC_ERR_HIP, "hipHostMalloc (LO staging) failed");
+        hmodel = reinterpret_cast<float *>(static_cast<char *>(pin) + in_bytes + out_bytes);
         uint32_t *hw = static_cast<uint32_t *>(pin), *dw = c->lo_io.as<uint32_t>();
         hns = hw;
         hthr = reinterpret_cast<float *>(hw + W);
@@ -810,7 +815,8 @@ struct LoRansac {
     void run(float *model, int &cnt, float &sum) {
         if (cnt < 12 || rc) return;
         // quality->getInliers(best_model) -> max_inliers (device)
-        hipError_t e = hipMemcpyAsync(c->one_model.p, model, sizeof(float) * 9, hipMemcpyHostToDevice, c->stream);
+        memcpy(hmodel, model, sizeof(float) * 9);  // (the previous round's copy has completed)
+        hipError_t e = hipMemcpyAsync(c->one_model.p, hmodel, sizeof(float) * 9, hipMemcpyHostToDevice, c->stream);
         if (e == hipSuccess) e = c->inl_scratch.reserve(usac::inliers_scratch_bytes(n, 1));
         if (e == hipSuccess)
             e = usac::launch_inliers(c->stream, c->estimator, c->pts.p, n, c->one_model.as<float>(), theta,
