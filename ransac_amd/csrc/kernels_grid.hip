@@ -11,8 +11,8 @@
 // members[start[cell[i]] + (k < rank[i] ? k : k + 1)].
 //
 // Pipeline (rocPRIM device primitives for the sort and scans):
-//   1. k_grid_keys     per point: the packed 64-bit cell key (16 bits per dimension, offset
-//                      by the dataset box's lowest cell) and its index;
+//   1. k_grid_keys     per point: the packed cell key (per dimension just the bits of the
+//                      box's cell range plus a sentinel, offset by its lowest cell) and index;
 //   2. radix sort      (key, index) pairs -- stable, so a cell's members stay ascending;
 //   3. k_grid_heads    1 where the sorted key changes; inclusive scan -> cell id (key order);
 //   4. k_grid_cells    per key-order cell: first position and first (= smallest) member;
@@ -34,18 +34,20 @@
 namespace usac {
 
 __global__ __launch_bounds__(256) void k_grid_keys(const float4 *__restrict__ pts, uint32_t n, float cs, int4 cmin,
-                                                   uint64_t *__restrict__ keys, uint32_t *__restrict__ idx) {
+                                                   int4 bits, uint64_t *__restrict__ keys, uint32_t *__restrict__ idx) {
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const float4 p = pts[i];
     const float v[4] = {p.x, p.y, p.z, p.w};
     const int lo[4] = {cmin.x, cmin.y, cmin.z, cmin.w};
+    const int bw[4] = {bits.x, bits.y, bits.z, bits.w};
     uint64_t k = 0;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
+        const int top = (1 << bw[j]) - 1;  // above every cell of the box: the out-of-box sentinel
         int c = (int)(v[j] / cs) - lo[j];  // IEEE fp32 division, truncation (as the reference)
-        c = c < 0 ? 0 : c > 65535 ? 65535 : c;  // only non-finite coordinates leave the box
-        k = (k << 16) | (uint64_t)c;
+        c = c < 0 ? 0 : c > top ? top : c;  // only non-finite coordinates leave the box
+        k = (k << bw[j]) | (uint64_t)c;
     }
     keys[i] = k;
     idx[i] = i;
@@ -201,16 +203,18 @@ static hipError_t poll_stream(hipStream_t st) {
     }
 }
 
-hipError_t build_grid(hipStream_t st, const float4 *pts, uint32_t n, int cell_size, int4 cmin, uint32_t m, void *ws,
-                      uint32_t *cell, uint32_t *rank, uint32_t *start, int32_t *members, int32_t *eligible,
-                      uint32_t *n_cells_out, uint32_t *n_elig_out) {
+hipError_t build_grid(hipStream_t st, const float4 *pts, uint32_t n, int cell_size, int4 cmin, int4 bits, uint32_t m,
+                      void *ws, uint32_t *cell, uint32_t *rank, uint32_t *start, int32_t *members, int32_t *eligible,
+                      uint32_t *pinned2, uint32_t *n_cells_out, uint32_t *n_elig_out) {
     if (n == 0) return hipErrorInvalidValue;
     GridScratch s = carve(ws, n);
     const dim3 b(256), g((n + 255) / 256);
-    hipLaunchKernelGGL(k_grid_keys, g, b, 0, st, pts, n, (float)cell_size, cmin, s.keys_a, s.idx_a);
+    hipLaunchKernelGGL(k_grid_keys, g, b, 0, st, pts, n, (float)cell_size, cmin, bits, s.keys_a, s.idx_a);
     GRID_TRY(hipGetLastError());
     size_t tb = s.tmp_bytes;
-    GRID_TRY(rocprim::radix_sort_pairs(s.tmp, tb, s.keys_a, s.keys_b, s.idx_a, s.idx_b, n, 0, 64, st));
+    // only the key's used bits (per dimension: the box's cell range and a sentinel) are sorted
+    const int key_bits = bits.x + bits.y + bits.z + bits.w;
+    GRID_TRY(rocprim::radix_sort_pairs(s.tmp, tb, s.keys_a, s.keys_b, s.idx_a, s.idx_b, n, 0, key_bits, st));
     hipLaunchKernelGGL(k_grid_heads, g, b, 0, st, s.keys_b, n, s.head);
     GRID_TRY(hipGetLastError());
     tb = s.tmp_bytes;
@@ -218,11 +222,13 @@ hipError_t build_grid(hipStream_t st, const float4 *pts, uint32_t n, int cell_si
     hipLaunchKernelGGL(k_grid_cells, g, b, 0, st, s.head, s.cellid, s.idx_b, n, s.old_start, s.old_min, s.ord_a,
                        s.counts);
     GRID_TRY(hipGetLastError());
-    uint32_t nc = 0;
-    GRID_TRY(hipMemcpyAsync(&nc, s.counts, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    GRID_TRY(hipMemcpyAsync(pinned2, s.counts, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     GRID_TRY(poll_stream(st));
+    const uint32_t nc = pinned2[0];
     tb = s.tmp_bytes;
-    GRID_TRY(rocprim::radix_sort_pairs(s.tmp, tb, s.old_min, s.min_b, s.ord_a, s.ord_b, nc, 0, 32, st));
+    int min_bits = 1;  // the smallest members are point indices < n
+    while (min_bits < 32 && (n - 1) >> min_bits) min_bits++;
+    GRID_TRY(rocprim::radix_sort_pairs(s.tmp, tb, s.old_min, s.min_b, s.ord_a, s.ord_b, nc, 0, min_bits, st));
     hipLaunchKernelGGL(k_grid_renumber, dim3((nc + 1 + 255) / 256), b, 0, st, s.ord_b, s.old_start, nc, s.new_of_old,
                        s.size_new);
     GRID_TRY(hipGetLastError());
@@ -235,9 +241,9 @@ hipError_t build_grid(hipStream_t st, const float4 *pts, uint32_t n, int cell_si
     GRID_TRY(rocprim::exclusive_scan(s.tmp, tb, s.elig, s.pos, 0u, (size_t)n, rocprim::plus<uint32_t>(), st));
     hipLaunchKernelGGL(k_grid_compact, g, b, 0, st, s.elig, s.pos, n, eligible, s.counts + 1);
     GRID_TRY(hipGetLastError());
-    uint32_t ne = 0;
-    GRID_TRY(hipMemcpyAsync(&ne, s.counts + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    GRID_TRY(hipMemcpyAsync(pinned2 + 1, s.counts + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     GRID_TRY(poll_stream(st));
+    const uint32_t ne = pinned2[1];
     *n_cells_out = nc;
     *n_elig_out = ne;
     return hipSuccess;

@@ -269,6 +269,8 @@ struct usac_ctx {
     uint32_t spk = 1;       // model slots per hypothesis (3 for the 7-point solver)
     // single-model / polish buffers
     DevBuf one_model, inl_idx, inl_idx2, inl_cnt, inl_sum, inl_scratch, q, partial, ws, nm_model, nm_ok;
+    uint32_t *grid_pin = nullptr;    // pinned words the grid build reads its two counts into
+    size_t grid_pin_bytes = 0;
     DevBuf pol_res;                  // polish pass results (model, ok, count, sum; initial count, sum)
     void *pol_pin = nullptr;         // their pinned host copy (PinnedPool)
     size_t pol_pin_bytes = 0;
@@ -372,12 +374,18 @@ int ensure_grid(usac_ctx *c, int cs) {
     if (c->cols != 4) return fail(c, USAC_ERR_ARG, "grid neighbours need 4-column points (SURVEY Q17)");
     if (cs <= 0) return fail(c, USAC_ERR_ARG, "grid cell_size must be > 0");
     const float e[4] = {c->ext.x, c->ext.y, c->ext.z, c->ext.w};
-    int lo[4];
+    int lo[4], bits[4];
     for (int j = 0; j < 4; j++) {
         lo[j] = (int)(-e[j] / (float)cs);
-        if ((long long)(int)(e[j] / (float)cs) - lo[j] > 65535)
-            return fail(c, USAC_ERR_UNSUPPORTED, "grid: more than 65536 cells along one dimension");
+        const long long range = (long long)(int)(e[j] / (float)cs) - lo[j];
+        if (range > 65535) return fail(c, USAC_ERR_UNSUPPORTED, "grid: more than 65536 cells along one dimension");
+        bits[j] = 1;  // 2^bits - 1 > range: room for the out-of-box sentinel
+        while ((1ll << bits[j]) - 1 <= range) bits[j]++;
     }
+    if (bits[0] + bits[1] + bits[2] + bits[3] > 64)  // only at >= 32768 cells in every dimension
+        for (int j = 0; j < 4; j++) bits[j] = std::min(bits[j], 16);
+    if (!c->grid_pin && !(c->grid_pin = static_cast<uint32_t *>(PinnedPool::get().take(64, &c->grid_pin_bytes))))
+        return fail(c, USAC_ERR_HIP, "pinned host allocation failed");
     const size_t n = c->n;
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, c->grid_cell.reserve(sizeof(uint32_t) * n));
@@ -387,10 +395,11 @@ int ensure_grid(usac_ctx *c, int cs) {
     HIP_TRY(c, c->grid_elig.reserve(sizeof(int32_t) * n));
     HIP_TRY(c, c->grid_ws.reserve(usac::grid_workspace_bytes(c->n)));
     c->grid_cs = 0;
-    HIP_TRY(c, usac::build_grid(c->stream, c->pts.as<float4>(), c->n, cs, make_int4(lo[0], lo[1], lo[2], lo[3]), c->m,
-                                c->grid_ws.p, c->grid_cell.as<uint32_t>(), c->grid_rank.as<uint32_t>(),
-                                c->grid_start.as<uint32_t>(), c->grid_members.as<int32_t>(),
-                                c->grid_elig.as<int32_t>(), &c->grid_n_cells, &c->grid_n_elig));
+    HIP_TRY(c, usac::build_grid(c->stream, c->pts.as<float4>(), c->n, cs, make_int4(lo[0], lo[1], lo[2], lo[3]),
+                                make_int4(bits[0], bits[1], bits[2], bits[3]), c->m, c->grid_ws.p,
+                                c->grid_cell.as<uint32_t>(), c->grid_rank.as<uint32_t>(), c->grid_start.as<uint32_t>(),
+                                c->grid_members.as<int32_t>(), c->grid_elig.as<int32_t>(), c->grid_pin,
+                                &c->grid_n_cells, &c->grid_n_elig));
     c->grid_cs = cs;
     return USAC_OK;
 }
@@ -1200,6 +1209,7 @@ void usac_destroy(usac_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->pol_pin) PinnedPool::get().give_back(c->pol_pin, c->pol_pin_bytes);
+    if (c->grid_pin) PinnedPool::get().give_back(c->grid_pin, c->grid_pin_bytes);
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
                       &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->inl_scratch, &c->e5_ws, &c->one_model,

@@ -36,9 +36,9 @@ struct DevSampler {
 // cell of the dataset box per dimension (every cell - cmin must fit 16 bits).  Synchronises
 // `st` twice (cell and eligible counts).
 size_t grid_workspace_bytes(uint32_t n);
-hipError_t build_grid(hipStream_t st, const float4 *pts, uint32_t n, int cell_size, int4 cmin, uint32_t m, void *ws,
-                      uint32_t *cell, uint32_t *rank, uint32_t *start, int32_t *members, int32_t *eligible,
-                      uint32_t *n_cells, uint32_t *n_eligible);
+hipError_t build_grid(hipStream_t st, const float4 *pts, uint32_t n, int cell_size, int4 cmin, int4 bits, uint32_t m,
+                      void *ws, uint32_t *cell, uint32_t *rank, uint32_t *start, int32_t *members, int32_t *eligible,
+                      uint32_t *pinned2, uint32_t *n_cells_out, uint32_t *n_elig_out);
 
 // device-drawn samples only (B x m int32), the stream the solve kernels use
 hipError_t launch_draw_samples(hipStream_t st, int m, uint32_t n, uint32_t B, DevSampler ds, uint64_t first_hyp,
