@@ -465,6 +465,13 @@ def set_f8_rank2(on):
     lib().orc_set_f8_rank2(1 if on else 0)
 
 
+def set_sprt_file_order(on):
+    """SPRT point order of the revision that produced results/line2d/*_001.csv: every model
+    tested on the points in file order from point 0 (no shuffled pool, no rolling index; the
+    current sprt.hpp:93-107,211-223 shuffles and rolls).  Test-only."""
+    lib().orc_set_sprt_file_order(1 if on else 0)
+
+
 def hypothesis_loop_mt(kind, points, thr, seed, count, threads, dlt_mode=DLT_THIN):
     """All-cores CPU baseline: `count` hypotheses of the reference-style loop on `threads`
     pthreads (disjoint ranges, one estimator each) -> (wall seconds, best inlier count)."""

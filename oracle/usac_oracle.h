@@ -150,6 +150,8 @@ void orc_napsac_sample(orc_napsac *s, int *sample);
  * mt19937 is seeded with cfg->seed instead of std::random_device). */
 /* test switch: rank-2 enforcement in the 8-point polish (older reference revision) */
 void orc_set_f8_rank2(int on);
+/* test switch: SPRT tests points in file order from point 0 (revision of results/line2d/uniform_001.csv) */
+void orc_set_sprt_file_order(int on);
 /* all-cores CPU baseline: wall seconds of `count` hypotheses on `threads` workers */
 double orc_hypothesis_loop_mt(int kind, const float *points, unsigned int n, int dlt_mode, float thr,
                               unsigned int seed, int count, int threads, int *best_cnt);

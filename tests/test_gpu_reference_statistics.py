@@ -102,3 +102,29 @@ def test_evd_gc_knn_statistics_device(usac, oracle, rel, sprt):
             inl.append(out.getNumberOfInliers())
         results[scene] = {INL: inl}
     assert len(check(rel, results, [(INL, SD_INL)], {INL: inl_floor})) >= 14
+
+
+def test_line2d_sprt_statistics_device(usac, oracle, line2d_scenes):
+    """results/line2d/uniform_001.csv through usac_ransac_run: SPRT as sprt.hpp is written
+    (shuffled, rolling pool), every run identical to the oracle's (iterations, model bits,
+    inlier list), and the four I=200 scenes' averages inside the harness lens
+    (test_line2d_sprt_statistics_current_pool; the file-order revision that reproduces all
+    eight rows is an oracle switch only)."""
+    from test_reference_statistics import ITS, STATS, lens_p
+    rel = "line2d/uniform_001.csv"
+    runs = int(STATS[rel]["settings"]["Runs for each image"])
+    for name, (pts, _, _) in sorted(line2d_scenes.items()):
+        if "I=200" not in name:
+            continue
+        inl, its = [], []
+        for seed in range(1, 41):
+            out = _run(usac, pts, usac.ESTIMATOR.Line2d, 2, 10.0, 0.99, seed, sprt=True)
+            ref = oracle.ransac_run(oracle.LINE2D, pts, 10.0, 0.99, seed, sprt=True)
+            assert out.getNumberOfMainIterations() == ref["iters"], (name, seed)
+            assert (_bits(out.getModel()) == _bits(ref["model"])).all(), (name, seed)
+            assert (out.getInliers() == ref["inlier_idx"]).all(), (name, seed)
+            inl.append(out.getNumberOfInliers())
+            its.append(out.getNumberOfMainIterations())
+        row = STATS[rel]["scenes"][name]
+        assert lens_p(inl, row, INL, runs) >= 0.005, name
+        assert lens_p(its, row, ITS, runs) >= 0.005, name

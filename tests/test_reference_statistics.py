@@ -26,8 +26,21 @@ What is pinned, and what is not (DESIGN.md §3 lists the same):
   * homography, EVD (results/EVD, 15 wide-baseline scenes): graph-cut LO with KNN or grid
     neighbours, Uniform and PROSAC, with and without SPRT -- final inliers (PROSAC: 14 of 15
     scenes, EVD_SKIP).
-  * line2d (results/line2d): Uniform (inliers + iterations), LO-RANSAC and NAPSAC (inliers).
-    Not pinned: SPRT, PROSAC and the iteration counts with LO -- see the EXCEPTIONS notes.
+  * line2d (results/line2d): Uniform (inliers + iterations), LO-RANSAC and NAPSAC (inliers),
+    SPRT (inliers + iterations, below), graph-cut LO (inliers).  Not pinned: PROSAC and the
+    iteration counts with LO / graph cut (LINE2D_NOT_PINNED).
+
+Time-seeded runs (the "harness lens").  Every Ransac the reference's harness constructs calls
+srand(time(NULL)) (model.hpp:45 reset_random_generator defaults to true; uniform_sampler.hpp:22-26,
+sprt.hpp:90), and getStatisticalResults builds one Ransac per run back to back (tests.h:144-147).
+All runs that start within the same wall-clock second therefore draw the same glibc stream and
+return the same result: a CSV row of R runs at an average of tau seconds each holds only about
+R*tau + 1 distinct runs.  The CSVs show it -- kusvod2 `shout` (100 runs at 6.9 ms) publishes
+78.0 +- 0.0 inliers and 137 +- 0 iterations, identical runs.  Where that matters (fast runs, so
+one to three distinct runs per row) the pins below simulate the harness: runs start at
+phase + i*tau (phase uniform in [0, 1) s, tau = the row's "Avg time"), runs in the same second
+share one oracle run drawn from a pool of seeded oracle runs, and the published average must lie
+within the central 99 % of the simulated 50- / 100-run averages (lens_p >= 0.005).
 """
 import json
 import os
@@ -76,6 +89,34 @@ def check(rel, results, keys, floors):
             (pinned if ok else failures).append((scene, key, round(m, 4), row[key], row[sdk]))
     assert not failures, (rel, failures)
     return pinned
+
+
+def lens_p(vals, row, key, runs, sims=4000, seed=0):
+    """Harness lens (module docstring): two-sided tail probability of the published average
+    `row[key]` among simulated time-seeded averages of `runs` runs built from `vals` (one
+    value per independent seeded oracle run)."""
+    rng = np.random.default_rng(seed)
+    vals = np.asarray(vals, dtype=np.float64)
+    tau = row["Avg time (mcs)"] * 1e-6
+    means = np.empty(sims)
+    for i in range(sims):
+        grp = np.floor(rng.random() + tau * np.arange(runs)).astype(np.int64)
+        grp -= grp[0]
+        pick = rng.choice(len(vals), grp[-1] + 1, replace=len(vals) <= grp[-1])
+        means[i] = vals[pick[grp]].mean()
+    x = row[key]
+    return min(float((means <= x + 1e-9).mean()), float((means >= x - 1e-9).mean()))
+
+
+def lens_check(rel, results, keys, min_p=0.005):
+    """results: scene -> {key: per-run values}; returns {(scene, key): p}, asserting p >= min_p."""
+    table = STATS[rel]
+    runs = int(table["settings"]["Runs for each image"])
+    ps = {(scene, key): lens_p(vals[key], table["scenes"][scene], key, runs)
+          for scene, vals in results.items() for key in keys}
+    bad = {k: v for k, v in ps.items() if v < min_p}
+    assert not bad, (rel, bad)
+    return ps
 
 
 def inl_floor(mean):
@@ -265,3 +306,107 @@ def test_dlt4_thin_row_matches_numpy_svd(oracle, homography_scenes):
     assert len(rels) > 1900
     assert np.median(rels) < 1e-6, np.median(rels)
     assert np.quantile(rels, 0.99) < 1e-4, np.quantile(rels, 0.99)
+
+
+@pytest.fixture(scope="module")
+def line2d_sprt_pools(oracle, line2d_scenes):
+    """100 seeded oracle runs per scene, SPRT on (sprt.hpp semantics as written: shuffled,
+    rolling pool) and with the CSV revision's point order (oracle.set_sprt_file_order)."""
+    pools = {}
+    for file_order in (False, True):
+        oracle.set_sprt_file_order(file_order)
+        try:
+            pools[file_order] = {name: _line2d_runs(oracle, pts, 100, sprt=True)
+                                 for name, (pts, _, _) in sorted(line2d_scenes.items())}
+        finally:
+            oracle.set_sprt_file_order(False)
+    return pools
+
+
+def test_line2d_sprt_statistics(line2d_sprt_pools):
+    """results/line2d/uniform_001.csv (Uniform + SPRT, 50 runs of 14-40 ms: 2-3 distinct runs
+    per row under the harness's time seeding).  With the points tested in file order from
+    point 0 -- the SPRT of the revision that wrote this CSV (oracle.set_sprt_file_order) --
+    all 8 scenes' average inliers and iterations are pinned under the harness lens: the
+    published SPRT runs are longer and worse than without SPRT (2628 vs 2548 iterations,
+    411.6 +- 45 vs 438.2 inliers on the first scene) because the line2d files hold their
+    inliers last, so a true line is often rejected on the outlier prefix."""
+    ps = lens_check("line2d/uniform_001.csv", line2d_sprt_pools[True], [INL, ITS])
+    assert len(ps) == 16
+
+
+def test_line2d_sprt_statistics_current_pool(line2d_sprt_pools):
+    """The same CSV against sprt.hpp as written (shuffled pool, rolling index: the semantics
+    the product and its bit-exact parity tests follow).  The four I=200 scenes agree under
+    the harness lens; the four I=500 scenes cannot: with a shuffled pool the true line
+    (6.7-7.1 % inliers) is almost never rejected, so runs end at ~700-725 inliers after
+    ~700 iterations, while the CSV's rows sit at 473-702 +- 83-168 inliers and 1313-2734
+    iterations -- outside the central 99 % of the simulated 50-run averages (the file-order
+    revision above reproduces them).  Asserted both ways so a change on either side shows."""
+    rel = "line2d/uniform_001.csv"
+    pools = line2d_sprt_pools[False]
+    i200 = {k: v for k, v in pools.items() if "I=200" in k}
+    i500 = {k: v for k, v in pools.items() if "I=500" in k}
+    assert len(lens_check(rel, i200, [INL, ITS])) == 8
+    runs = int(STATS[rel]["settings"]["Runs for each image"])
+    rejected = [scene for scene, vals in i500.items()
+                if min(lens_p(vals[k], STATS[rel]["scenes"][scene], k, runs) for k in (INL, ITS)) < 0.005]
+    assert len(rejected) >= 2, rejected
+
+
+# line2d CSVs (results/line2d) with numbers the oracle does not reproduce, and why.
+LINE2D_NOT_PINNED = {
+    "prosac_000.csv iterations": "seed-insensitive in the CSV (5, 1.04, 4, 1.04, 9, 1.04, 7.02, 1.02 "
+                                 "per scene, std 0-0.28) but 2-9 here with the densitySort order "
+                                 "(utils.cpp:8-32 restated with the exact KNN, k = 13): the PROSAC "
+                                 "termination of that revision stops after one sample on the I=500 "
+                                 "scenes, the current prosac_termination_criteria.hpp does not",
+    "uniform_010.csv iterations": "graph-cut runs 3-9 % shorter here (2418 vs 2507 on the first scene) "
+                                  "-- a graph-cut revision difference; inliers are pinned",
+    "uniform_010.csv w=1200_h=1000_I=200 inliers": "468.0 +- 3.0 vs 457.2 +- 7.2",
+    "uniform_100.csv iterations": "LO runs longer than no-LO in the CSV (2608 vs 2548): that revision "
+                                  "counted differently",
+}
+
+
+def test_line2d_gc_statistics(oracle, line2d_scenes):
+    """results/line2d/uniform_010.csv: Uniform + graph-cut LO (KNN neighbours, k = 8 as the
+    line2d harness; Grid is invalid for 2-D points, Q17).  Average inliers pinned by the plain
+    rule (four combined standard errors + floor; ~230 ms per published run, so ~12 distinct
+    runs per row), one scene excepted (LINE2D_NOT_PINNED)."""
+    rel = "line2d/uniform_010.csv"
+    results = {}
+    for name, (pts, _, _) in sorted(line2d_scenes.items()):
+        if "uniform_010.csv %s inliers" % name.replace("_n=3.000000", "").replace("_N=10200", "") in LINE2D_NOT_PINNED:
+            continue
+        results[name] = _line2d_runs(oracle, pts, 5, lo=oracle.LO_GC, neighbors=oracle.NEIGHBORS_NANOFLANN, knn=8)
+    assert len(results) == 7
+    assert len(check(rel, results, [(INL, SD_INL)], {INL: inl_floor})) == 7
+
+
+# kusvod2 scenes excluded from the plain pins above, re-examined under the harness lens: 100
+# runs of 3-8 ms are one or two distinct runs per row, so the published average is one or two
+# draws of the run distribution (box / castle / leafs / shout / kampa).  Still not pinned:
+# graff (10 000 iterations per run, ~10-14 distinct runs; 10.7 vs 12.9 inliers) and castle
+# with SPRT (147.75 published, the oracle's runs give 150-156).
+KUSVOD2_LENS = [("kusvod2/uniform_gc_Grid_c_sz_50.csv", ["box", "castle", "leafs", "shout"]),
+                ("kusvod2/uniform_gc_sprt_Grid_c_sz_50.csv", ["box", "leafs", "shout", "kampa"])]
+
+
+@pytest.mark.parametrize("rel,scenes", KUSVOD2_LENS)
+def test_fundamental_gc_statistics_lens(oracle, kusvod2_scenes, rel, scenes):
+    sprt = "sprt" in rel
+    results = {}
+    oracle.set_f8_rank2(True)
+    try:
+        for scene in scenes:
+            pts, _ = kusvod2_scenes[scene]
+            inl = []
+            for seed in range(1, 31):
+                r = oracle.ransac_run(oracle.FUNDAMENTAL, pts, 2.0, 0.95, seed, lo=oracle.LO_GC,
+                                      neighbors=oracle.NEIGHBORS_GRID, cell_size=50, sprt=sprt)
+                inl.append(r["inliers"] if r["ret"] == 0 else 0)
+            results[scene] = {INL: inl}
+    finally:
+        oracle.set_f8_rank2(False)
+    assert len(lens_check(rel, results, [INL])) == len(scenes)
