@@ -437,6 +437,7 @@ def main():
     dlt_mode = 0 if args.dlt == "thin" else 1
     est_id = usac.ESTIMATOR.Fundamental if fund else usac.ESTIMATOR.Essential if ess else usac.ESTIMATOR.Homography
     P = max(1, args.pipeline)
+    assert P <= usac.Context.XRING, "at most %d batches in flight (exchange ring)" % usac.Context.XRING
     ctxs = [usac.Context(est_id, pts, device=local_rank) for _ in range(P)]
     for c in ctxs:
         c.set_dlt_mode(dlt_mode)
@@ -480,13 +481,20 @@ def main():
     def launch(i):
         first = (i * world + rank) * B
         ctxs[i % P].hypothesize_async(B, args.seed, first, args.threshold)
+        if exchange == "rccl_allgather":
+            # the batch best is all-gathered on ctx's exchange stream, ordered after this
+            # batch's stream by an event: finish(i) then waits for batch i's exchange only
+            ctx.exchange_best_async(ctxs[i % P], i % ctx.XRING)
 
     def finish(i):
         c = ctxs[i % P]
-        best = c.fetch_best()
+        if exchange == "rccl_allgather":
+            best = usac.merge_records(ctx.exchange_best_wait(i % ctx.XRING))
+        else:
+            best = c.fetch_best()
+            if world > 1:
+                best = usac.merge_records(allgather(best))
         t = c.last_timings()
-        if world > 1:
-            best = usac.merge_records(allgather(best))
         return best, t
 
     def run(first_step, count, sink):

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define USAC_ABI_VERSION 8
+#define USAC_ABI_VERSION 9
 
 /* = enum ESTIMATOR (usac/model.hpp:10) */
 enum { USAC_LINE2D = 1, USAC_HOMOGRAPHY = 2, USAC_FUNDAMENTAL = 3, USAC_ESSENTIAL = 4 };
@@ -279,6 +279,17 @@ int usac_comm_unique_id(uint8_t *id128);
 int usac_comm_init(usac_ctx *ctx, int nranks, int rank, const uint8_t *id128);
 /* All-gather of one usac_record per rank on the context stream: all[nranks]. */
 int usac_allgather_records(usac_ctx *ctx, const usac_record *local, usac_record *all);
+/* The per-batch best exchange of the throughput pipeline, off the compute streams: the record
+ * usac_hypothesize_async(batch) leaves on the device is all-gathered over ctx's communicator
+ * on ctx's own exchange stream, ordered after `batch`'s stream by an event (neither stream
+ * waits for the other's later work; no host staging), then copied to pinned host memory.
+ * `slot` (< USAC_XRING) names the exchange in a ring; usac_exchange_best_wait(slot) returns
+ * the nranks records (rank order) and frees the slot: at most USAC_XRING exchanges may be
+ * outstanding.  Every rank must issue the exchanges in the same order.
+ * batch may be ctx itself or another context on the same device. */
+#define USAC_XRING 8
+int usac_exchange_best_async(usac_ctx *ctx, usac_ctx *batch, uint32_t slot);
+int usac_exchange_best_wait(usac_ctx *ctx, uint32_t slot, usac_record *all);
 /* Merge n records by Score::bigger, earliest hyp_index on exact ties. */
 int usac_merge_records(const usac_record *recs, uint32_t n, usac_record *best);
 

@@ -109,7 +109,7 @@ typedef struct {
     int cell_size; /* model.hpp:43 */
     int neighbors;        /* ORC_NEIGHBORS_* (model.hpp:12,42): Grid, else nanoflann KNN */
     unsigned int knn;     /* model.hpp:23 k_nearest_neighbors (NAPSAC KNN, GC) */
-    float spatial_coherence_gc; /* model.hpp:33 (0.1); <= 0 selects 0.1 */
+    float spatial_coherence_gc; /* model.hpp:33 (0.1): used as given, 0 = no pairwise term -- set it */
 } orc_config;
 enum { ORC_NEIGHBORS_NULL = 0, ORC_NEIGHBORS_NANOFLANN = 1, ORC_NEIGHBORS_GRID = 2 }; /* = NeighborsSearch */
 

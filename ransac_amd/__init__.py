@@ -103,6 +103,7 @@ ABI_SYMBOLS = [
     "usac_prosac_samples", "usac_sprt_pool", "usac_set_sprt", "usac_sprt_tested", "usac_set_device_sampler",
     "usac_draw_samples", "usac_set_cell_size", "usac_grid_neighbors",
     "usac_comm_unique_id", "usac_comm_init", "usac_allgather_records", "usac_merge_records",
+    "usac_exchange_best_async", "usac_exchange_best_wait",
 ]
 
 
@@ -170,6 +171,8 @@ def lib():
         "usac_comm_unique_id": (ctypes.c_int, [u8p]),
         "usac_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, u8p]),
         "usac_allgather_records": (ctypes.c_int, [_vp, _P(Record), _P(Record)]),
+        "usac_exchange_best_async": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32]),
+        "usac_exchange_best_wait": (ctypes.c_int, [_vp, ctypes.c_uint32, _P(Record)]),
         "usac_merge_records": (ctypes.c_int, [_P(Record), ctypes.c_uint32, _P(Record)]),
     }
     for name, (res, args) in sig.items():
@@ -444,6 +447,19 @@ class Context:
     def allgather_record(self, rec):
         allr = (Record * self.nranks)()
         self._check(lib().usac_allgather_records(self._h, ctypes.byref(rec), allr), "allgather_records")
+        return list(allr)
+
+    XRING = 8  # USAC_XRING
+
+    def exchange_best_async(self, batch_ctx, slot):
+        """All-gather the batch best that hypothesize_async left on batch_ctx (same device) over
+        this context's communicator, on its exchange stream, after batch_ctx's stream (no host
+        staging, no wait on any compute stream); slot < XRING names it for exchange_best_wait."""
+        self._check(lib().usac_exchange_best_async(self._h, batch_ctx._h, slot), "exchange_best_async")
+
+    def exchange_best_wait(self, slot):
+        allr = (Record * self.nranks)()
+        self._check(lib().usac_exchange_best_wait(self._h, slot, allr), "exchange_best_wait")
         return list(allr)
 
 

@@ -762,6 +762,23 @@ hipError_t launch_score_line(hipStream_t st, int chunks, const float2 *pts, uint
     return LAUNCH_CHECK();
 }
 
+__global__ __launch_bounds__(256) void k_pack_slice(const int32_t *__restrict__ counts, const float *__restrict__ models,
+                                                    uint32_t S, uint32_t P, int ncomp, int32_t status,
+                                                    int32_t *__restrict__ out) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i == 0) out[0] = status;
+    if (i >= P) return;
+    out[1 + i] = i < S ? counts[i] : -1;
+    for (int k = 0; k < ncomp; k++)
+        out[1 + (size_t)(1 + k) * P + i] = i < S ? __float_as_int(models[(size_t)k * S + i]) : 0;
+}
+
+hipError_t launch_pack_slice(hipStream_t st, const int32_t *counts, const float *models, uint32_t S, uint32_t P,
+                             int ncomp, int32_t status, int32_t *out) {
+    hipLaunchKernelGGL(k_pack_slice, dim3(P / 256 + 1), dim3(256), 0, st, counts, models, S, P, ncomp, status, out);
+    return LAUNCH_CHECK();
+}
+
 hipError_t launch_argmax(hipStream_t st, const int32_t *counts, const float *sums, uint32_t B, const float *models,
                          int ncomp, uint64_t first_hyp, uint32_t spk, void *scratch, usac_record *out) {
     const uint32_t nparts = (B + 2047) / 2048;

@@ -102,7 +102,11 @@ __global__ __launch_bounds__(kInlBlock) void k_inl_compact(const void *__restric
     __shared__ float sm[18];
     __shared__ uint32_t wsum[kInlBlock / 64], wpre[kInlBlock / 64];
     const uint32_t ws = inl_slot(slots, blockIdx.y);
-    if (ok && !ok[ws]) return;  // a failed fit: its list is left as it was (workgroup-uniform)
+    if (ok && !ok[ws]) {  // a failed fit: its list is left as it was (workgroup-uniform) and its
+        // count reads 0, so the Σ pass over this slot (launch_seqsum) sums nothing
+        if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) totals[ws] = 0;
+        return;
+    }
     inl_model<EST>(models + 9 * (size_t)ws, sm);
     const float t = thrs ? thrs[ws] : thr;
     float m[18];

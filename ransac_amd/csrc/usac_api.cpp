@@ -280,7 +280,16 @@ struct usac_ctx {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     DevBuf rec_send, rec_all;
-    DevBuf x_send, x_recv;  // sharded-run all-gather staging (RCCL path)
+    DevBuf x_send, x_recv;  // sharded-run all-gather buffers (RCCL path, device-packed)
+    void *x_pin = nullptr;  // their pinned host copy (the replay's counts / model words)
+    size_t x_pin_bytes = 0;
+    // batch-best exchange (usac_exchange_best_async / _wait): a dedicated stream ordered after
+    // each batch by an event, a ring of in-flight all-gathers (device + pinned host records)
+    hipStream_t xstream = nullptr;
+    hipEvent_t xev_batch[USAC_XRING] = {}, xev_done[USAC_XRING] = {};
+    DevBuf xring;
+    usac_record *xring_host = nullptr;
+    size_t xring_host_bytes = 0;
     // timing
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float last_ms[3] = {0, 0, 0};
@@ -382,8 +391,11 @@ int ensure_grid(usac_ctx *c, int cs) {
         bits[j] = 1;  // 2^bits - 1 > range: room for the out-of-box sentinel
         while ((1ll << bits[j]) - 1 <= range) bits[j]++;
     }
-    if (bits[0] + bits[1] + bits[2] + bits[3] > 64)  // only at >= 32768 cells in every dimension
-        for (int j = 0; j < 4; j++) bits[j] = std::min(bits[j], 16);
+    // each dimension keeps its range plus the out-of-box sentinel; a key wider than 64 bits
+    // (e.g. 17 + 17 + 17 + 14 bits) is refused rather than clamped (a clamped dimension would
+    // give the sentinel a real cell's value)
+    if (bits[0] + bits[1] + bits[2] + bits[3] > 64)
+        return fail(c, USAC_ERR_UNSUPPORTED, "grid: the four cell ranges need more than 64 key bits");
     if (!c->grid_pin && !(c->grid_pin = static_cast<uint32_t *>(PinnedPool::get().take(64, &c->grid_pin_bytes))))
         return fail(c, USAC_ERR_HIP, "pinned host allocation failed");
     const size_t n = c->n;
@@ -705,23 +717,26 @@ struct LoRansac {
     // outcome and, if the fit succeeded, the score.  (A chain in a SCORE phase only arises
     // without a fused fit -- never here -- so it is scored on its own.)
     int stage(uint32_t W, int inner_cnt) {
-        bool fit = false, score = false, inner_fit = false, pos = false;
+        bool fit = false, score = false, inner_fit = false, iter_fit = false, pos = false;
         uint32_t nmax = 0, ns = 0;
         for (uint32_t w = 0; w < W; w++) {
             const Chain &h = ch[w];
             hns[w] = 0;
             if (h.phase == INNER_FIT || h.phase == ITER_FIT) {
                 fit = true;
-                inner_fit = h.phase == INNER_FIT;
-                if (inner_fit) {
-                    pos = inner_cnt > (int)limit;
-                    hns[w] = pos ? limit : (uint32_t)inner_cnt;
+                bool p;
+                if (h.phase == INNER_FIT) {
+                    inner_fit = true;
+                    p = inner_cnt > (int)limit;
+                    hns[w] = p ? limit : (uint32_t)inner_cnt;
                     hthr[w] = (float)mult * h.thr;
                 } else {
-                    pos = h.fit_pos;
-                    hns[w] = pos ? limit : (uint32_t)h.lo_cnt;
+                    iter_fit = true;
+                    p = h.fit_pos;
+                    hns[w] = p ? limit : (uint32_t)h.lo_cnt;
                     hthr[w] = h.thr;
                 }
+                pos = pos || p;
                 hslots[ns++] = w;
                 nmax = std::max(nmax, hns[w]);
             } else if (h.phase == INNER_SCORE || h.phase == ITER_SCORE) {
@@ -730,7 +745,20 @@ struct LoRansac {
                 hthr[w] = h.thr;
             }
         }
-        if (fit && score) return fail(c, USAC_ERR_HIP, "LO chains out of lockstep");  // never: fit, score alternate
+        // never: fit and score stages alternate, and inner fits only open a round
+        if ((fit && score) || (inner_fit && iter_fit)) return fail(c, USAC_ERR_HIP, "LO chains out of lockstep");
+        if (pos) {
+            // the position list is per launch: a fitting chain without its own positions
+            // (GetScoreLimited with lo_cnt <= limit, or an inner fit of <= limit points) fits
+            // its first hns[w] list entries -- identity positions (hns[w] <= limit)
+            for (uint32_t w = 0; w < W; w++) {
+                const Chain &h = ch[w];
+                const bool fitting = h.phase == INNER_FIT || h.phase == ITER_FIT;
+                const bool own = h.phase == INNER_FIT ? inner_cnt > (int)limit : h.fit_pos;
+                if (fitting && !own)
+                    for (uint32_t i = 0; i < hns[w]; i++) hpos[(size_t)w * limit + i] = (int32_t)i;
+            }
+        }
         hipStream_t st = c->stream;
         HIP_TRY(c, hipMemcpyAsync(c->lo_io.p, pin, in_bytes, hipMemcpyHostToDevice, st));
         if (fit) {
@@ -1207,8 +1235,16 @@ void usac_destroy(usac_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);  // the pools are per device
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->xstream) (void)hipStreamSynchronize(c->xstream);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->pol_pin) PinnedPool::get().give_back(c->pol_pin, c->pol_pin_bytes);
+    if (c->x_pin) PinnedPool::get().give_back(c->x_pin, c->x_pin_bytes);
+    if (c->xring_host) PinnedPool::get().give_back(c->xring_host, c->xring_host_bytes);
+    for (int k = 0; k < USAC_XRING; k++) {
+        if (c->xev_batch[k]) StreamPool::get().give_back(c->xev_batch[k]);
+        if (c->xev_done[k]) StreamPool::get().give_back(c->xev_done[k]);
+    }
+    if (c->xstream) StreamPool::get().give_back(c->xstream);
     if (c->grid_pin) PinnedPool::get().give_back(c->grid_pin, c->grid_pin_bytes);
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
@@ -1218,7 +1254,7 @@ void usac_destroy(usac_ctx *c) {
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
                       &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2, &c->gc_err, &c->grid_cell, &c->grid_rank, &c->grid_start,
                       &c->grid_members, &c->grid_elig, &c->grid_ws, &c->x_send,
-                      &c->x_recv})
+                      &c->x_recv, &c->xring})
         b->release();
     for (auto &ev : c->ev)
         if (ev) StreamPool::get().give_back(ev);
@@ -1622,9 +1658,14 @@ int usac_sprt_pool(uint32_t seed, int estimator, uint32_t n_points, uint32_t m, 
 // sampler is rewound to just after the current sample.  Then the <= 4-pass non-minimal
 // polish on the device.
 // One batch of a sharded run: rank r solves and scores slots of samples [r P, r P + P) (P =
-// ceil(B / nranks); the last slices may be short or empty), packs its counts and model words
-// (int32 / fp32, padded to P x spk slots, counts -1 on padding) and all-gathers them; every rank
-// unpacks all slices into hc / hmod exactly as the unsharded batch leaves them.
+// ceil(B / nranks); the last slices may be short or empty), packs its status word, counts and
+// model words (int32 / fp32, padded to P x spk slots, counts -1 on padding) and all-gathers
+// them; every rank unpacks all slices into hc / hmod exactly as the unsharded batch leaves
+// them.  A rank whose local part failed still joins the all-gather with its error as status,
+// and every rank then fails with the first failing rank's status: no rank is left blocked in
+// a collective its peers never enter.  The RCCL path packs on the device (no host staging on
+// the way out) and brings the gathered words back with one copy into pinned memory; a gather
+// callback (e.g. gloo) receives host buffers.
 static int sharded_batch(usac_ctx *c, const int32_t *hs, uint32_t B, uint32_t iters, float thr, int nranks, int rank,
                          usac_allgather_fn gather, void *user, std::vector<uint8_t> &xbuf, int32_t *hc, float *hmod,
                          size_t SB) {
@@ -1634,37 +1675,64 @@ static int sharded_batch(usac_ctx *c, const int32_t *hs, uint32_t B, uint32_t it
     const uint32_t lo = std::min<uint32_t>(B, (uint32_t)rank * P);
     const uint32_t Bs = std::min<uint32_t>(B, lo + P) - lo;
     const size_t Ps = (size_t)P * spk, Ss = (size_t)Bs * spk;
-    const size_t words = (1 + (size_t)nc) * Ps, bytes = 4 * words;
-    xbuf.resize(bytes * (1 + (size_t)nranks));
-    int32_t *send = reinterpret_cast<int32_t *>(xbuf.data());
-    uint8_t *recv = xbuf.data() + bytes;
-    std::fill(send, send + Ps, -1);
-    std::fill(send + Ps, send + words, 0);
-    if (Bs) {
+    const size_t words = 1 + (1 + (size_t)nc) * Ps, bytes = 4 * words;
+    // the local part: its first error becomes this rank's status (the message stays in c->err)
+    auto local = [&]() -> int {
+        if (!Bs) return USAC_OK;
         HIP_TRY(c, hipMemcpyAsync(c->samples.p, hs + (size_t)lo * m, sizeof(int32_t) * (size_t)Bs * m,
                                   hipMemcpyHostToDevice, c->stream));
         HIP_TRY(c, enqueue_solve(c, c->samples.as<int32_t>(), Bs, 0, (uint64_t)iters + lo, nullptr));
         HIP_TRY(c, enqueue_score(c, Bs, thr, loop_chunks(c, Bs)));
-        HIP_TRY(c, hipMemcpyAsync(send, c->counts.p, sizeof(int32_t) * Ss, hipMemcpyDeviceToHost, c->stream));
-        for (int k = 0; k < nc; k++)
-            HIP_TRY(c, hipMemcpyAsync(send + (1 + (size_t)k) * Ps, c->models.as<float>() + (size_t)k * Ss,
-                                      sizeof(float) * Ss, hipMemcpyDeviceToHost, c->stream));
-    }
-    HIP_TRY(c, stream_wait(c->stream));
+        return USAC_OK;
+    };
+    const int status = local();
+    const std::string local_err = c->err;
+    const uint8_t *recv = nullptr;
     if (gather) {
-        if (gather(user, send, bytes, recv) != 0) return fail(c, USAC_ERR_ARG, "all-gather callback failed");
+        xbuf.resize(bytes * (1 + (size_t)nranks));
+        int32_t *send = reinterpret_cast<int32_t *>(xbuf.data());
+        std::fill(send + 1, send + 1 + Ps, -1);
+        std::fill(send + 1 + Ps, send + words, 0);
+        send[0] = status;
+        if (status == USAC_OK && Bs) {
+            HIP_TRY(c, hipMemcpyAsync(send + 1, c->counts.p, sizeof(int32_t) * Ss, hipMemcpyDeviceToHost, c->stream));
+            for (int k = 0; k < nc; k++)
+                HIP_TRY(c, hipMemcpyAsync(send + 1 + (1 + (size_t)k) * Ps, c->models.as<float>() + (size_t)k * Ss,
+                                          sizeof(float) * Ss, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(c, stream_wait(c->stream));
+        }
+        if (gather(user, send, bytes, xbuf.data() + bytes) != 0)
+            return fail(c, USAC_ERR_ARG, "all-gather callback failed (gather callbacks must fail on every rank)");
+        recv = xbuf.data() + bytes;
     } else {
         HIP_TRY(c, c->x_send.reserve(bytes));
         HIP_TRY(c, c->x_recv.reserve(bytes * (size_t)nranks));
-        HIP_TRY(c, hipMemcpyAsync(c->x_send.p, send, bytes, hipMemcpyHostToDevice, c->stream));
+        if (c->x_pin_bytes < bytes * (size_t)nranks) {
+            if (c->x_pin) PinnedPool::get().give_back(c->x_pin, c->x_pin_bytes);
+            c->x_pin = PinnedPool::get().take(bytes * (size_t)nranks, &c->x_pin_bytes);
+            if (!c->x_pin) {
+                c->x_pin_bytes = 0;
+                return fail(c, USAC_ERR_HIP, "pinned host allocation failed");
+            }
+        }
+        HIP_TRY(c, usac::launch_pack_slice(c->stream, c->counts.as<int32_t>(), c->models.as<float>(),
+                                           status == USAC_OK ? (uint32_t)Ss : 0u, (uint32_t)Ps, nc, status,
+                                           c->x_send.as<int32_t>()));
         NCCL_TRY(c, ncclAllGather(c->x_send.p, c->x_recv.p, bytes, ncclUint8, c->comm, c->stream));
-        HIP_TRY(c, hipMemcpyAsync(recv, c->x_recv.p, bytes * (size_t)nranks, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(c->x_pin, c->x_recv.p, bytes * (size_t)nranks, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, stream_wait(c->stream));
+        recv = static_cast<const uint8_t *>(c->x_pin);
+    }
+    for (int r = 0; r < nranks; r++) {
+        const int32_t st = *reinterpret_cast<const int32_t *>(recv + (size_t)r * bytes);
+        if (st != USAC_OK)
+            return fail(c, st, r == rank ? local_err : "sharded run: rank " + std::to_string(r) + " failed (status " +
+                                                           std::to_string(st) + ")");
     }
     for (int r = 0; r < nranks; r++) {
         const uint32_t lr = std::min<uint32_t>(B, (uint32_t)r * P);
         const size_t Sr = (size_t)(std::min<uint32_t>(B, lr + P) - lr) * spk;
-        const int32_t *rc_ = reinterpret_cast<const int32_t *>(recv + (size_t)r * bytes);
+        const int32_t *rc_ = reinterpret_cast<const int32_t *>(recv + (size_t)r * bytes) + 1;
         memcpy(hc + (size_t)lr * spk, rc_, sizeof(int32_t) * Sr);
         for (int k = 0; k < nc; k++)
             memcpy(hmod + (size_t)k * SB + (size_t)lr * spk, rc_ + (1 + (size_t)k) * Ps, sizeof(float) * Sr);
@@ -2138,6 +2206,50 @@ int usac_comm_init(usac_ctx *c, int nranks, int rank, const uint8_t *id128) {
     c->rank = rank;
     HIP_TRY(c, c->rec_send.reserve(sizeof(usac_record)));
     HIP_TRY(c, c->rec_all.reserve(sizeof(usac_record) * (size_t)nranks));
+    return USAC_OK;
+}
+
+int usac_exchange_best_async(usac_ctx *c, usac_ctx *batch, uint32_t slot) {
+    if (!c || !batch || slot >= USAC_XRING) return USAC_ERR_ARG;
+    if (!c->comm) return fail(c, USAC_ERR_ARG, "usac_comm_init not called");
+    if (batch->device != c->device) return fail(c, USAC_ERR_ARG, "exchange: batch context on another device");
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (!c->xstream) {
+        HIP_TRY(c, StreamPool::get().stream(&c->xstream));
+        for (int k = 0; k < USAC_XRING; k++) {
+            HIP_TRY(c, StreamPool::get().event(&c->xev_batch[k]));
+            HIP_TRY(c, StreamPool::get().event(&c->xev_done[k]));
+        }
+        HIP_TRY(c, c->xring.reserve(sizeof(usac_record) * (size_t)USAC_XRING * (size_t)(c->nranks + 1)));
+        c->xring_host = static_cast<usac_record *>(
+            PinnedPool::get().take(sizeof(usac_record) * (size_t)USAC_XRING * (size_t)c->nranks, &c->xring_host_bytes));
+        if (!c->xring_host) return fail(c, USAC_ERR_HIP, "pinned host allocation failed");
+    }
+    // the batch's argmax record is copied into the ring's send slot on the batch stream (the
+    // batch's next use of that stream overwrites its record); the exchange stream waits for
+    // that copy only (neither stream waits for the other's later work)
+    usac_record *dsend = c->xring.as<usac_record>() + (size_t)USAC_XRING * c->nranks + slot;
+    usac_record *dall = c->xring.as<usac_record>() + (size_t)slot * c->nranks;
+    HIP_TRY(c, hipMemcpyAsync(dsend, batch->best.p, sizeof(usac_record), hipMemcpyDeviceToDevice, batch->stream));
+    HIP_TRY(c, hipEventRecord(c->xev_batch[slot], batch->stream));
+    HIP_TRY(c, hipStreamWaitEvent(c->xstream, c->xev_batch[slot], 0));
+    NCCL_TRY(c, ncclAllGather(dsend, dall, sizeof(usac_record), ncclUint8, c->comm, c->xstream));
+    HIP_TRY(c, hipMemcpyAsync(c->xring_host + (size_t)slot * c->nranks, dall, sizeof(usac_record) * (size_t)c->nranks,
+                              hipMemcpyDeviceToHost, c->xstream));
+    HIP_TRY(c, hipEventRecord(c->xev_done[slot], c->xstream));
+    return USAC_OK;
+}
+
+int usac_exchange_best_wait(usac_ctx *c, uint32_t slot, usac_record *all) {
+    if (!c || !all || slot >= USAC_XRING || !c->xstream) return USAC_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    for (uint32_t spins = 0;; spins++) {  // poll (as stream_wait): returns within ~1 us
+        const hipError_t e = hipEventQuery(c->xev_done[slot]);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) return fail(c, USAC_ERR_HIP, std::string("exchange: ") + hipGetErrorString(e));
+        if ((spins & 1023u) == 1023u) std::this_thread::yield();
+    }
+    memcpy(all, c->xring_host + (size_t)slot * c->nranks, sizeof(usac_record) * (size_t)c->nranks);
     return USAC_OK;
 }
 

@@ -75,6 +75,12 @@ hipError_t launch_argmax(hipStream_t st, const int32_t *counts, const float *sum
                          int ncomp, uint64_t first_hyp, uint32_t spk, void *scratch /* 12 B x ceil(B/2048) */,
                          usac_record *out);
 
+// One rank's slice of a sharded batch packed for the all-gather (device to device): word 0 =
+// the rank's status, then counts (S of P slots, -1 on padding) and ncomp model words per slot
+// (component k of slot i at models[k * S + i], zero on padding): 1 + (1 + ncomp) * P words.
+hipError_t launch_pack_slice(hipStream_t st, const int32_t *counts, const float *models, uint32_t S, uint32_t P,
+                             int ncomp, int32_t status, int32_t *out);
+
 // fundamental (kernels_fund.hip): slots 3*b + j, counts -1 on empty slots, list/list_n =
 // occupied slots (list_n zeroed by the launcher)
 hipError_t launch_solve_f7(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
