@@ -17,7 +17,7 @@
  *                                  models (usac/quality/quality.hpp:60-101)
  *   usac_get_inliers               Quality::getNumberInliers(..., get_inliers=true, inliers)
  *                                  / Quality::getInliers (quality.hpp:80-87, 108-121)
- *   usac_nonminimal                Estimator::EstimateModelNonMinimalSample
+ *   usac_nonminimal / usac_lsq_fit Estimator::EstimateModelNonMinimalSample (weighted: estimator.hpp:26)
  *                                  (estimator.hpp:21; normalized_dlt.cpp:7-23;
  *                                  eight_points.cpp:4-100;
  *                                  line2d_estimator.hpp:59-107)
@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define USAC_ABI_VERSION 9
+#define USAC_ABI_VERSION 10
 
 /* = enum ESTIMATOR (usac/model.hpp:10) */
 enum { USAC_LINE2D = 1, USAC_HOMOGRAPHY = 2, USAC_FUNDAMENTAL = 3, USAC_ESSENTIAL = 4 };
@@ -170,6 +170,14 @@ float usac_bk_label(int n, const float *unary, int m, const int32_t *ei, const i
 int usac_knn(usac_ctx *ctx, uint32_t k, int32_t *idx, float *d2);
 /* Non-minimal least squares on the listed points; returns USAC_OK and writes model. */
 int usac_nonminimal(usac_ctx *ctx, const int32_t *idx, uint32_t n, float *model);
+/* Estimator::EstimateModelNonMinimalSample with optional weights (estimator.hpp:21,26):
+ * weights == NULL is usac_nonminimal; otherwise weights[i] belongs to point i of the context
+ * (n_points floats, indexed by point index as the reference's weights[sample[i]]) and the fit
+ * is the weighted overload -- homography: weighted NormalizedDLT (normalized_dlt.cpp:25-36),
+ * fundamental: weighted EightPointsAlgorithm (eight_points.cpp:176-228), both through the
+ * weighted GetNormalizingTransformation (normalizing_transformation.cpp:117-166).  Line and
+ * essential estimators have no weighted overload (USAC_ERR_UNSUPPORTED). */
+int usac_lsq_fit(usac_ctx *ctx, const int32_t *idx, uint32_t n, const float *weights, float *model);
 
 /* Fused batch: samples (B x m host int32) or NULL => device xorshift sampler keyed by
  * (seed, first_hyp + i).  Per-model counts/sums (host, nullable, B x S entries: slot
@@ -258,7 +266,10 @@ typedef int (*usac_allgather_fn)(void *user, const void *send, size_t bytes, voi
  * `gather` when non-null (e.g. a torch.distributed gloo group), else RCCL on the communicator of
  * usac_comm_init(ctx, nranks, rank, id).  Termination, LO, graph cut and polish are then replayed
  * on the merged batch identically on every rank, so every rank's output equals usac_ransac_run's.
- * Not with SPRT (its sequential replay reads pool-order flag words of every model). */
+ * With SPRT each rank also computes its slice's pool-order inlier words (the words the sequential
+ * SPRT walk reads, sprt.hpp:191-317), all-gathered with the models; every rank replays the walk.
+ * A rank that fails joins the all-gather with its status and every rank fails with it; a gather
+ * callback must therefore fail (return non-zero) on every rank or on none. */
 int usac_ransac_run_sharded(usac_ctx *ctx, const usac_params *params, int nranks, int rank, usac_allgather_fn gather,
                             void *gather_user, usac_run_output *out, int32_t *inliers_out, usac_record *records,
                             uint32_t rec_cap);

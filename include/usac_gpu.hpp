@@ -205,6 +205,14 @@ public:
         ctx_.check(rc, "EstimateModelNonMinimalSample");
         return true;
     }
+    // the weighted overload (estimator.hpp:26): weights[point index], homography / fundamental
+    bool EstimateModelNonMinimalSample(const int *const sample, unsigned int sample_size, const float *const weights,
+                                       Descriptor &model) {
+        const int rc = usac_lsq_fit(ctx_.get(), sample, sample_size, weights, model.data());
+        if (rc == USAC_ERR_NO_MODEL) return false;
+        ctx_.check(rc, "EstimateModelNonMinimalSample(weights)");
+        return true;
+    }
     bool LeastSquaresFitting(const int *const sample, unsigned int sample_size, Descriptor &model) {
         return EstimateModelNonMinimalSample(sample, sample_size, model);
     }

@@ -82,6 +82,7 @@ def lib():
         L.orc_est_free.argtypes = [ctypes.c_void_p]
         L.orc_est_estimate.argtypes = [ctypes.c_void_p, _i32p, _f32p]
         L.orc_est_nonminimal.argtypes = [ctypes.c_void_p, _i32p, ctypes.c_uint, _f32p]
+        L.orc_est_nonminimal_weighted.argtypes = [ctypes.c_void_p, _i32p, ctypes.c_uint, _f32p, _f32p]
         L.orc_est_set_model.argtypes = [ctypes.c_void_p, _f32p]
         L.orc_est_error.argtypes = [ctypes.c_void_p, ctypes.c_uint]
         L.orc_est_error.restype = ctypes.c_float
@@ -209,6 +210,17 @@ class Estimator:
         idx = np.ascontiguousarray(idx, dtype=np.int32)
         out = np.zeros(9, dtype=np.float32)
         ok = lib().orc_est_nonminimal(self._h, _p(idx, _i32p), len(idx), _p(out, _f32p))
+        return out if ok else None
+
+    def nonminimal_weighted(self, idx, weights):
+        """weights: one float per point of the set (indexed by point index, as the reference)."""
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        weights = np.ascontiguousarray(weights, dtype=np.float32)
+        assert weights.size >= self.n
+        out = np.zeros(9, dtype=np.float32)
+        ok = lib().orc_est_nonminimal_weighted(self._h, _p(idx, _i32p), len(idx), _p(weights, _f32p), _p(out, _f32p))
+        if ok < 0:
+            raise NotImplementedError("weighted non-minimal fit: homography / fundamental only")
         return out if ok else None
 
     def errors(self, model):

@@ -356,27 +356,48 @@ static int homography_dlt4(const orc_est *e, const int *sample, float *H) {
 
 /* GetNormalizingTransformation (normalizing_transformation.cpp:7-113): fp32 sums in
  * sample order; the distance accumulation adds a double sqrt into a float (:45-46);
- * scale = M_SQRT2 / (avg / n) in double, rounded to float (:50-51). */
-static void normalizing_transform(const float *pts, const int *sample, unsigned int n, float *T1, float *T2,
-                                  float *norm /* n x 4 */) {
+ * scale = M_SQRT2 / (avg / n) in double, rounded to float (:50-51).
+ * With weights (weights[point index], the weighted overload :117-166): the sums run over the
+ * weighted coordinates w*x, and the distances are those of the weighted points from the origin
+ * (not from the mean, :130-141); the transform is then applied to the unweighted points. */
+static void normalizing_transform(const float *pts, const int *sample, unsigned int n, const float *weights,
+                                  float *T1, float *T2, float *norm /* n x 4 */) {
     float m1x = 0, m1y = 0, m2x = 0, m2y = 0;
-    for (unsigned int i = 0; i < n; i++) {
-        const float *p = pts + 4 * (size_t)sample[i];
-        m1x += p[0];
-        m1y += p[1];
-        m2x += p[2];
-        m2y += p[3];
-    }
-    m1x /= (float)n;
-    m1y /= (float)n;
-    m2x /= (float)n;
-    m2y /= (float)n;
     float d1 = 0, d2 = 0;
-    for (unsigned int i = 0; i < n; i++) {
-        const float *p = pts + 4 * (size_t)sample[i];
-        float x1m = p[0] - m1x, y1m = p[1] - m1y, x2m = p[2] - m2x, y2m = p[3] - m2y;
-        d1 = (float)((double)d1 + sqrt((double)(x1m * x1m + y1m * y1m)));
-        d2 = (float)((double)d2 + sqrt((double)(x2m * x2m + y2m * y2m)));
+    if (weights) {
+        for (unsigned int i = 0; i < n; i++) {
+            const float *p = pts + 4 * (size_t)sample[i];
+            const float w = weights[sample[i]];
+            const float x1 = w * p[0], y1 = w * p[1], x2 = w * p[2], y2 = w * p[3];
+            m1x += x1;
+            m1y += y1;
+            m2x += x2;
+            m2y += y2;
+            d1 = (float)((double)d1 + sqrt((double)(x1 * x1 + y1 * y1)));
+            d2 = (float)((double)d2 + sqrt((double)(x2 * x2 + y2 * y2)));
+        }
+        m1x /= (float)n;
+        m1y /= (float)n;
+        m2x /= (float)n;
+        m2y /= (float)n;
+    } else {
+        for (unsigned int i = 0; i < n; i++) {
+            const float *p = pts + 4 * (size_t)sample[i];
+            m1x += p[0];
+            m1y += p[1];
+            m2x += p[2];
+            m2y += p[3];
+        }
+        m1x /= (float)n;
+        m1y /= (float)n;
+        m2x /= (float)n;
+        m2y /= (float)n;
+        for (unsigned int i = 0; i < n; i++) {
+            const float *p = pts + 4 * (size_t)sample[i];
+            float x1m = p[0] - m1x, y1m = p[1] - m1y, x2m = p[2] - m2x, y2m = p[3] - m2y;
+            d1 = (float)((double)d1 + sqrt((double)(x1m * x1m + y1m * y1m)));
+            d2 = (float)((double)d2 + sqrt((double)(x2m * x2m + y2m * y2m)));
+        }
     }
     float s1 = (float)(M_SQRT2 / (double)(d1 / (float)n));
     float s2 = (float)(M_SQRT2 / (double)(d2 / (float)n));
@@ -397,11 +418,12 @@ static void normalizing_transform(const float *pts, const int *sample, unsigned 
  * points, then H = T2^-1 * H * T1, H /= H33.  2n <= 8 rows keep the thin-SVD semantics
  * (SURVEY Q2); 2n >= 10 rows take the smallest right singular vector via the fp64
  * normal matrix. */
-static int homography_normalized_dlt(const orc_est *e, const int *sample, unsigned int n, float *H) {
+static int homography_normalized_dlt(const orc_est *e, const int *sample, unsigned int n, const float *weights,
+                                     float *H) {
     if (n == 0) return 0;
     float T1[9], T2[9], T2i[9];
     float *norm = (float *)malloc(sizeof(float) * 4 * n);
-    normalizing_transform(e->pts, sample, n, T1, T2, norm);
+    normalizing_transform(e->pts, sample, n, weights, T1, T2, norm);
     double v[9];
     if (2 * n <= 9) {
         double W[9][9];
@@ -759,11 +781,11 @@ static void rank2_project(double v[9]) {
         }
 }
 
-static int fundamental_8pt(const orc_est *e, const int *sample, unsigned int n, float *F) {
+static int fundamental_8pt(const orc_est *e, const int *sample, unsigned int n, const float *weights, float *F) {
     if (n == 0) return 0;
     float T1[9], T2[9];
     float *norm = (float *)malloc(sizeof(float) * 4 * n);
-    normalizing_transform(e->pts, sample, n, T1, T2, norm);
+    normalizing_transform(e->pts, sample, n, weights, T1, T2, norm);
     double v[9];
     if (n <= 8) {
         double W[9][9];
@@ -1364,8 +1386,18 @@ int orc_est_estimate(orc_est *e, const int *sample, float *models) {
 
 int orc_est_nonminimal(orc_est *e, const int *sample, unsigned int n, float *model) {
     if (e->kind == ORC_LINE2D) return line2d_nonminimal(e, sample, n, model);
-    if (e->kind == ORC_FUNDAMENTAL || e->kind == ORC_ESSENTIAL) return fundamental_8pt(e, sample, n, model);
-    return homography_normalized_dlt(e, sample, n, model);
+    if (e->kind == ORC_FUNDAMENTAL || e->kind == ORC_ESSENTIAL) return fundamental_8pt(e, sample, n, NULL, model);
+    return homography_normalized_dlt(e, sample, n, NULL, model);
+}
+
+/* Estimator::EstimateModelNonMinimalSample(sample, n, weights, model) (estimator.hpp:26):
+ * homography_estimator.hpp:69-77 (weighted NormalizedDLT, normalized_dlt.cpp:25-36) and
+ * fundamental_estimator.hpp:78-86 (weighted EightPointsAlgorithm, eight_points.cpp:176-228);
+ * the other estimators inherit the base's "NOT IMPLEMENTED": -1. */
+int orc_est_nonminimal_weighted(orc_est *e, const int *sample, unsigned int n, const float *weights, float *model) {
+    if (e->kind == ORC_FUNDAMENTAL) return fundamental_8pt(e, sample, n, weights, model);
+    if (e->kind == ORC_HOMOGRAPHY) return homography_normalized_dlt(e, sample, n, weights, model);
+    return -1;
 }
 
 /* test hook: the cubic solver spec */

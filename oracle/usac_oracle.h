@@ -59,6 +59,8 @@ int orc_cubic_roots(double c0, double c1, double c2, double c3, double *roots);
 int orc_est_estimate(orc_est *e, const int *sample, float *models);
 /* EstimateModelNonMinimalSample: returns 1 on success */
 int orc_est_nonminimal(orc_est *e, const int *sample, unsigned int n, float *model);
+/* the weighted overload (weights[point index]): homography / fundamental; -1 for the others */
+int orc_est_nonminimal_weighted(orc_est *e, const int *sample, unsigned int n, const float *weights, float *model);
 void orc_est_set_model(orc_est *e, const float *model);
 float orc_est_error(const orc_est *e, unsigned int pidx);
 

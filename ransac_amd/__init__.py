@@ -97,7 +97,7 @@ class _RunOutput(ctypes.Structure):
 ABI_SYMBOLS = [
     "usac_create", "usac_destroy", "usac_last_error", "usac_abi_version", "usac_set_dlt_mode", "usac_sample_size",
     "usac_num_points", "usac_estimate_models", "usac_score_models", "usac_get_inliers", "usac_knn", "usac_bk_label",
-    "usac_nonminimal",
+    "usac_nonminimal", "usac_lsq_fit",
     "usac_hypothesize_score", "usac_hypothesize_async", "usac_fetch_best", "usac_sync", "usac_last_timings",
     "usac_set_score_chunks", "usac_set_score_variant", "usac_last_counts", "usac_std_termination", "usac_ransac_run", "usac_ransac_run_sharded", "usac_uniform_samples",
     "usac_prosac_samples", "usac_sprt_pool", "usac_set_sprt", "usac_sprt_tested", "usac_set_device_sampler",
@@ -144,6 +144,7 @@ def lib():
         "usac_knn": (ctypes.c_int, [_vp, ctypes.c_uint32, i32p, f32p]),
         "usac_bk_label": (ctypes.c_float, [ctypes.c_int, f32p, ctypes.c_int, i32p, i32p, f32p, f32p, f32p, f32p, i32p]),
         "usac_nonminimal": (ctypes.c_int, [_vp, i32p, ctypes.c_uint32, f32p]),
+        "usac_lsq_fit": (ctypes.c_int, [_vp, i32p, ctypes.c_uint32, f32p, f32p]),
         "usac_hypothesize_score": (ctypes.c_int, [_vp, i32p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
                                                   ctypes.c_float, i32p, f32p, _P(Record)]),
         "usac_hypothesize_async": (ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
@@ -349,6 +350,22 @@ class Context:
         out = np.zeros(9, dtype=np.float32)
         self._check(lib().usac_nonminimal(self._h, _ptr(i, ctypes.c_int32), i.size, _ptr(out, ctypes.c_float)),
                     "nonminimal")
+        return out
+
+    def lsq_fit(self, idx, weights=None):
+        """usac_lsq_fit: EstimateModelNonMinimalSample(sample, n[, weights], model) -- weights (one
+        float per point of the context, by point index) select the weighted overload
+        (estimator.hpp:26; homography and fundamental)."""
+        i = np.ascontiguousarray(idx, dtype=np.int32)
+        out = np.zeros(9, dtype=np.float32)
+        wp = None
+        if weights is not None:
+            w = np.ascontiguousarray(weights, dtype=np.float32)
+            if w.size != self.n:
+                raise ValueError("weights: one per point (%d), got %d" % (self.n, w.size))
+            wp = _ptr(w, ctypes.c_float)
+        self._check(lib().usac_lsq_fit(self._h, _ptr(i, ctypes.c_int32), i.size, wp, _ptr(out, ctypes.c_float)),
+                    "lsq_fit")
         return out
 
     def hypothesize_score(self, B=None, samples=None, seed=0, first_hyp=0, thr=2.0, per_hypothesis=True):

@@ -141,6 +141,29 @@ __global__ __launch_bounds__(256) void k_norm_dist(const float4 *__restrict__ q_
     if (threadIdx.x < 2) reinterpret_cast<double *>(seq)[j * 2 + threadIdx.x] = red[threadIdx.x][0];
 }
 
+// the weighted overload's inputs (normalizing_transformation.cpp:117-146): q[i] = the point,
+// qw[i] = its weighted coordinates w*x (the mean chains' addends) and the distance terms
+// sqrt((double)(x*x + y*y)) of the weighted points from the origin (not from the mean)
+__global__ __launch_bounds__(256) void k_gather_weighted(const float4 *__restrict__ pts, const float *__restrict__ wts,
+                                                         const int32_t *__restrict__ base, size_t base_stride,
+                                                         const int32_t *__restrict__ pos, size_t pos_stride,
+                                                         const uint32_t *__restrict__ ns, uint32_t n1,
+                                                         float4 *__restrict__ q_all, float4 *__restrict__ qw_all,
+                                                         size_t q_stride, char *seq_all, size_t sstride) {
+    const uint32_t w = blockIdx.y;
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= (ns ? ns[w] : n1)) return;
+    const int32_t *list = base + w * base_stride;
+    const int32_t k = list[pos ? pos[w * pos_stride + i] : (int32_t)i];
+    const float4 p = pts[k];
+    const float g = wts[k];
+    const float x1 = g * p.x, y1 = g * p.y, x2 = g * p.z, y2 = g * p.w;
+    q_all[w * q_stride + i] = p;
+    qw_all[w * q_stride + i] = make_float4(x1, y1, x2, y2);
+    reinterpret_cast<double2 *>(seq_all + w * sstride + kSeqA)[i] =
+        make_double2(sqrt((double)(x1 * x1 + y1 * y1)), sqrt((double)(x2 * x2 + y2 * y2)));
+}
+
 // T1, T2 from the sums (the reference's expressions; ws layout (floats): [0..8] T1, [9..17]
 // T2).  The normalised points are never stored: the A^T A pass (and the thin solve) apply
 // x' = T[0] x + T[2], y' = T[4] y + T[5] on the fly -- the same float operations.
@@ -526,10 +549,13 @@ __global__ __launch_bounds__(64) void k_line_pca(const float2 *__restrict__ q_al
 // EstimateModelNonMinimalSample for W fits: homography (normalized_dlt.cpp:7-23), F and E
 // (EightPointsAlgorithm, fundamental_estimator.hpp:65-76, essential_estimator.hpp:64-74,
 // eight_points.cpp:4-100), line (line2d_estimator.hpp:59-107).  nmax >= every ns[w].
+// With b.weights: the weighted overload (normalized_dlt.cpp:25-36, eight_points.cpp:176-228),
+// which differs only in the normalising transformation.
 hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pts, const NmBatch &b) {
     if (b.W == 0) return hipSuccess;
     const dim3 gg((b.nmax + 255) / 256 ? (b.nmax + 255) / 256 : 1, b.W);
     if (estimator == USAC_LINE2D) {
+        if (b.weights) return hipErrorInvalidValue;  // the reference has no weighted line fit
         float2 *q = static_cast<float2 *>(b.q);
         hipLaunchKernelGGL(k_gather<float2>, gg, dim3(256), 0, st, static_cast<const float2 *>(pts), b.base,
                            b.base_stride, b.pos, b.pos_stride, b.ns, b.n1, q, b.q_stride);
@@ -537,7 +563,20 @@ hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pt
         return hipGetLastError();
     }
     float4 *q = static_cast<float4 *>(b.q);
-    {  // gather; normalising transforms: sequential sums (seqsum), distance terms
+    if (b.weights) {  // the weighted overload: six independent sequential chains, then as below
+        if (!b.qw) return hipErrorInvalidValue;
+        char *seq = static_cast<char *>(b.seq);
+        const size_t ss = seq_stride(b.nmax);
+        float *sums4 = reinterpret_cast<float *>(seq + b.W * ss), *dsum2 = sums4 + 4 * b.W;
+        float4 *qw = static_cast<float4 *>(b.qw);
+        hipLaunchKernelGGL(k_gather_weighted, gg, dim3(256), 0, st, static_cast<const float4 *>(pts), b.weights, b.base,
+                           b.base_stride, b.pos, b.pos_stride, b.ns, b.n1, q, qw, b.q_stride, seq, ss);
+        hipError_t e = launch_seqsum(st, 4, false, qw, 4 * b.q_stride, b.ns, b.n1, b.W, nullptr, seq, ss, false, sums4);
+        if (e != hipSuccess) return e;
+        e = launch_seqsum(st, 2, true, reinterpret_cast<const double *>(seq + kSeqA), ss / sizeof(double), b.ns, b.n1,
+                          b.W, nullptr, seq, ss, false, dsum2);
+        if (e != hipSuccess) return e;
+    } else {  // gather; normalising transforms: sequential sums (seqsum), distance terms
         char *seq = static_cast<char *>(b.seq);
         const size_t ss = seq_stride(b.nmax);
         float *sums4 = reinterpret_cast<float *>(seq + b.W * ss), *dsum2 = sums4 + 4 * b.W;

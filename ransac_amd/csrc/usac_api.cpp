@@ -275,6 +275,7 @@ struct usac_ctx {
     void *pol_pin = nullptr;         // their pinned host copy (PinnedPool)
     size_t pol_pin_bytes = 0;
     DevBuf nm_seq;          // normalisation scratch of the non-minimal fits (polish and LO)
+    DevBuf nm_w, nm_qw;     // usac_lsq_fit with weights: the weights, the weighted points
     DevBuf lo_io;           // one LO stage's inputs and outputs, contiguous (one copy each way)
     // comm
     ncclComm_t comm = nullptr;
@@ -547,7 +548,7 @@ hipError_t enqueue_inliers(usac_ctx *c, const float *model_dev, float thr) {
 }
 
 hipError_t enqueue_nonminimal(usac_ctx *c, const int32_t *idx_dev, uint32_t n, float *model_out = nullptr,
-                              int32_t *ok_out = nullptr) {
+                              int32_t *ok_out = nullptr, const float *weights_dev = nullptr) {
     hipError_t e = c->nm_seq.reserve(usac::nonminimal_seq_bytes(n, 1));
     if (e != hipSuccess) return e;
     usac::NmBatch b{};
@@ -561,6 +562,11 @@ hipError_t enqueue_nonminimal(usac_ctx *c, const int32_t *idx_dev, uint32_t n, f
     b.ws = c->ws.as<float>();
     b.model_out = model_out ? model_out : c->nm_model.as<float>();
     b.ok = ok_out ? ok_out : c->nm_ok.as<int32_t>();
+    if (weights_dev) {
+        if ((e = c->nm_qw.reserve(sizeof(float) * 4 * (size_t)n)) != hipSuccess) return e;
+        b.weights = weights_dev;
+        b.qw = c->nm_qw.p;
+    }
     return usac::launch_nonminimal_batch(c->stream, c->estimator, c->pts.p, b);
 }
 
@@ -1249,7 +1255,7 @@ void usac_destroy(usac_ctx *c) {
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
                       &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->inl_scratch, &c->e5_ws, &c->one_model,
-                      &c->inl_idx, &c->inl_idx2, &c->pol_res, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq, &c->lo_io,
+                      &c->inl_idx, &c->inl_idx2, &c->pol_res, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq, &c->nm_w, &c->nm_qw, &c->lo_io,
                       &c->rec_send, &c->rec_all, &c->tv_part, &c->hf_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
                       &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2, &c->gc_err, &c->grid_cell, &c->grid_rank, &c->grid_start,
@@ -1408,8 +1414,15 @@ int usac_knn(usac_ctx *c, uint32_t k, int32_t *idx, float *d2) {
 }
 
 int usac_nonminimal(usac_ctx *c, const int32_t *idx, uint32_t n, float *model) {
+    return usac_lsq_fit(c, idx, n, nullptr, model);
+}
+
+int usac_lsq_fit(usac_ctx *c, const int32_t *idx, uint32_t n, const float *weights, float *model) {
     if (!c || !idx || !model) return USAC_ERR_ARG;
     if (n == 0) return fail(c, USAC_ERR_ARG, "empty sample");
+    if (weights && c->estimator != USAC_HOMOGRAPHY && c->estimator != USAC_FUNDAMENTAL)
+        return fail(c, USAC_ERR_UNSUPPORTED, "weighted non-minimal fit: homography / fundamental only "
+                                             "(the other estimators inherit estimator.hpp:26's NOT IMPLEMENTED)");
     for (uint32_t i = 0; i < n; i++)
         if (idx[i] < 0 || (uint32_t)idx[i] >= c->n) return fail(c, USAC_ERR_ARG, "index out of range");
     int rc = ensure_single(c);
@@ -1419,7 +1432,12 @@ int usac_nonminimal(usac_ctx *c, const int32_t *idx, uint32_t n, float *model) {
     HIP_TRY(c, c->q.reserve(sizeof(float) * 4 * (size_t)n));
     HIP_TRY(c, c->partial.reserve(sizeof(double) * 45 * ((size_t)n / 64 + 2)));
     HIP_TRY(c, hipMemcpyAsync(c->inl_idx.p, idx, sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, enqueue_nonminimal(c, c->inl_idx.as<int32_t>(), n));
+    if (weights) {
+        HIP_TRY(c, c->nm_w.reserve(sizeof(float) * (size_t)c->n));
+        HIP_TRY(c, hipMemcpyAsync(c->nm_w.p, weights, sizeof(float) * c->n, hipMemcpyHostToDevice, c->stream));
+    }
+    HIP_TRY(c, enqueue_nonminimal(c, c->inl_idx.as<int32_t>(), n, nullptr, nullptr,
+                                  weights ? c->nm_w.as<float>() : nullptr));
     int32_t ok = 0;
     HIP_TRY(c, hipMemcpyAsync(model, c->nm_model.p, sizeof(float) * 9, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipMemcpyAsync(&ok, c->nm_ok.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
@@ -1668,21 +1686,27 @@ int usac_sprt_pool(uint32_t seed, int estimator, uint32_t n_points, uint32_t m, 
 // callback (e.g. gloo) receives host buffers.
 static int sharded_batch(usac_ctx *c, const int32_t *hs, uint32_t B, uint32_t iters, float thr, int nranks, int rank,
                          usac_allgather_fn gather, void *user, std::vector<uint8_t> &xbuf, int32_t *hc, float *hmod,
-                         size_t SB) {
+                         size_t SB, bool sprt, uint32_t *hmask) {
     const uint32_t m = c->m, spk = c->spk;
     const int nc = ncomp(c);
     const uint32_t P = (B + (uint32_t)nranks - 1) / (uint32_t)nranks;
     const uint32_t lo = std::min<uint32_t>(B, (uint32_t)rank * P);
     const uint32_t Bs = std::min<uint32_t>(B, lo + P) - lo;
     const size_t Ps = (size_t)P * spk, Ss = (size_t)Bs * spk;
-    const size_t words = 1 + (1 + (size_t)nc) * Ps, bytes = 4 * words;
+    // SPRT: every slot's pool-order inlier words follow the models ([nw][Ps], row = slot)
+    const size_t nw = sprt ? (c->n + 31) / 32 : 0, moff = 1 + (1 + (size_t)nc) * Ps;
+    const size_t words = moff + nw * Ps, bytes = 4 * words;
+    auto pool_mask = [&](uint32_t *out) -> hipError_t {
+        return usac::launch_pool_mask(c->stream, c->estimator, c->pool_pts.p, c->n, c->models.as<float>(), Ss, nullptr,
+                                      nullptr, (uint32_t)Ss, thr, out, (uint32_t)Ps);
+    };
     // the local part: its first error becomes this rank's status (the message stays in c->err)
     auto local = [&]() -> int {
         if (!Bs) return USAC_OK;
         HIP_TRY(c, hipMemcpyAsync(c->samples.p, hs + (size_t)lo * m, sizeof(int32_t) * (size_t)Bs * m,
                                   hipMemcpyHostToDevice, c->stream));
         HIP_TRY(c, enqueue_solve(c, c->samples.as<int32_t>(), Bs, 0, (uint64_t)iters + lo, nullptr));
-        HIP_TRY(c, enqueue_score(c, Bs, thr, loop_chunks(c, Bs)));
+        if (!sprt) HIP_TRY(c, enqueue_score(c, Bs, thr, loop_chunks(c, Bs)));
         return USAC_OK;
     };
     const int status = local();
@@ -1699,6 +1723,11 @@ static int sharded_batch(usac_ctx *c, const int32_t *hs, uint32_t B, uint32_t it
             for (int k = 0; k < nc; k++)
                 HIP_TRY(c, hipMemcpyAsync(send + 1 + (1 + (size_t)k) * Ps, c->models.as<float>() + (size_t)k * Ss,
                                           sizeof(float) * Ss, hipMemcpyDeviceToHost, c->stream));
+            if (sprt) {
+                HIP_TRY(c, pool_mask(c->masks.as<uint32_t>()));
+                HIP_TRY(c, hipMemcpyAsync(send + moff, c->masks.p, sizeof(uint32_t) * nw * Ps, hipMemcpyDeviceToHost,
+                                          c->stream));
+            }
             HIP_TRY(c, stream_wait(c->stream));
         }
         if (gather(user, send, bytes, xbuf.data() + bytes) != 0)
@@ -1718,6 +1747,7 @@ static int sharded_batch(usac_ctx *c, const int32_t *hs, uint32_t B, uint32_t it
         HIP_TRY(c, usac::launch_pack_slice(c->stream, c->counts.as<int32_t>(), c->models.as<float>(),
                                            status == USAC_OK ? (uint32_t)Ss : 0u, (uint32_t)Ps, nc, status,
                                            c->x_send.as<int32_t>()));
+        if (sprt && status == USAC_OK && Bs) HIP_TRY(c, pool_mask(c->x_send.as<uint32_t>() + moff));
         NCCL_TRY(c, ncclAllGather(c->x_send.p, c->x_recv.p, bytes, ncclUint8, c->comm, c->stream));
         HIP_TRY(c, hipMemcpyAsync(c->x_pin, c->x_recv.p, bytes * (size_t)nranks, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, stream_wait(c->stream));
@@ -1736,7 +1766,12 @@ static int sharded_batch(usac_ctx *c, const int32_t *hs, uint32_t B, uint32_t it
         memcpy(hc + (size_t)lr * spk, rc_, sizeof(int32_t) * Sr);
         for (int k = 0; k < nc; k++)
             memcpy(hmod + (size_t)k * SB + (size_t)lr * spk, rc_ + (1 + (size_t)k) * Ps, sizeof(float) * Sr);
+        // mask rows = slots of the whole batch: hmask[w * S + slot]
+        for (size_t w = 0; w < nw; w++)
+            memcpy(hmask + w * (size_t)B * spk + (size_t)lr * spk, rc_ + (moff - 1) + w * Ps, sizeof(uint32_t) * Sr);
     }
+    // without a slot list a model's count is never -1 (ransac_run_impl's unsharded SPRT path)
+    if (sprt && !listed(c)) std::fill(hc, hc + (size_t)B * spk, 0);
     return USAC_OK;
 }
 
@@ -1750,8 +1785,6 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                            uint32_t rec_cap) {
     if (!c || !prm || !out || nranks < 1 || rank < 0 || rank >= nranks) return USAC_ERR_ARG;
     memset(out, 0, sizeof(*out));
-    if (nranks > 1 && prm->sprt)
-        return fail(c, USAC_ERR_UNSUPPORTED, "sharded run with SPRT: the sequential SPRT replay is not sharded");
     if (nranks > 1 && !gather && (!c->comm || c->nranks != nranks || c->rank != rank))
         return fail(c, USAC_ERR_ARG, "sharded run without a gather callback needs usac_comm_init(nranks, rank)");
     const bool prosac = prm->sampler == USAC_SAMPLER_PROSAC;
@@ -1945,7 +1978,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         uint32_t rows = (uint32_t)S;
         if (nranks > 1) {  // this rank's slice, then the all-gather of every slice's counts and models
             if ((rc = sharded_batch(c, hs.data(), B, iters, thr, nranks, rank, gather, gather_user, xbuf, hc.data(),
-                                    hmod.data(), SB)))
+                                    hmod.data(), SB, sprt != nullptr, hmask.data())))
                 return rc;
         } else {
         HIP_TRY(c, hipMemcpyAsync(c->samples.p, hs.data(), sizeof(int32_t) * (size_t)B * m, hipMemcpyHostToDevice,
@@ -1985,7 +2018,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         HIP_TRY(c, stream_wait(c->stream));
         }
         if (sprt) {
-            if (listed(c)) {
+            if (listed(c) && nranks == 1) {
                 std::fill(slot_row.begin(), slot_row.begin() + S, -1);
                 for (uint32_t r = 0; r < rows; r++) slot_row[hlist[r]] = (int32_t)r;
             } else {

@@ -173,6 +173,10 @@ struct NmBatch {
     float *ws, *model_out;
     int32_t *ok;
     void *seq;  // normalisation scratch, nonminimal_seq_bytes(nmax, W) (not used by line fits)
+    // weighted normalisation (homography / fundamental only; nullable): weights[point index],
+    // qw = W x q_stride float4 scratch for the weighted points
+    const float *weights;
+    void *qw;
 };
 hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pts, const NmBatch &b);
 size_t nonminimal_partial_stride(uint32_t nmax);

@@ -1,7 +1,9 @@
 """Hypothesis-sharded Ransac::run (usac_ransac_run_sharded): two fresh child
 processes share the GPU, each solving and scoring half of every batch, with the per-batch
-all-gather over gloo; both ranks' outputs -- iterations, best-score records, LO counters, model
-bits, inlier list -- must equal the single-rank run's."""
+all-gather over gloo; both ranks' outputs -- iterations, best-score records, LO counters, SPRT
+rejections / histories, model bits, inlier list -- must equal the single-rank run's.  With SPRT
+each rank computes the pool-order inlier words of its slice and every rank replays the
+sequential SPRT walk over the gathered words."""
 import os
 import socket
 import subprocess
@@ -25,6 +27,14 @@ def make_case(usac, case):
         pts, _, _ = synthetic.fundamental_points(n=5000, inlier_ratio=0.5, seed=9, normalized=True,
                                                  prosac_order=False)
         mdl = usac.Model(0.002, 5, 0.95, 7, usac.ESTIMATOR.Essential, usac.SAMPLER.Uniform)
+    elif case == "f_prosac_sprt":  # cfg3 shape at reduced size: F 7-pt + PROSAC + SPRT
+        pts, _, _ = synthetic.fundamental_points(n=4000, inlier_ratio=0.3, seed=4, prosac_order=True)
+        mdl = usac.Model(2.0, 7, 0.99, 7, usac.ESTIMATOR.Fundamental, usac.SAMPLER.Prosac)
+        mdl.setSprt(True)
+    elif case == "h_uniform_sprt":  # homography + Uniform + SPRT (unlisted slots)
+        pts, _, _ = synthetic.homography_points(n=5000, inlier_ratio=0.15, seed=8)
+        mdl = usac.Model(2.0, 4, 0.99, 7, usac.ESTIMATOR.Homography, usac.SAMPLER.Uniform)
+        mdl.setSprt(True)
     else:  # "f_gc": fundamental, uniform, graph-cut LO with KNN neighbours
         pts, _, _ = synthetic.fundamental_points(n=3000, inlier_ratio=0.4, seed=5, prosac_order=False)
         mdl = usac.Model(2.0, 7, 0.95, 7, usac.ESTIMATOR.Fundamental, usac.SAMPLER.Uniform)
@@ -33,6 +43,8 @@ def make_case(usac, case):
     mdl.setSeed(3)
     mdl.max_iterations = 3000
     mdl.batch = 1000  # several batches, each split 500 / 500 across the two ranks
+    if case.endswith("_sprt"):
+        mdl.batch = 250  # SPRT runs end early: still several batches (125 / 125 samples per rank)
     return pts, mdl
 
 
@@ -43,7 +55,7 @@ def _free_port():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["h_napsac_lo", "e_uniform", "f_gc"])
+@pytest.mark.parametrize("case", ["h_napsac_lo", "e_uniform", "f_gc", "f_prosac_sprt", "h_uniform_sprt"])
 def test_sharded_run_equals_single_rank(usac, tmp_path, case):
     pts, mdl = make_case(usac, case)
     r = usac.Ransac(mdl, pts)
@@ -64,12 +76,19 @@ def test_sharded_run_equals_single_rank(usac, tmp_path, case):
         assert (z["model"].view(np.int32) == np.asarray(ref.getModel(), np.float32).view(np.int32)).all()
         assert np.array_equal(z["inliers"], ref.getInliers())
         assert int(z["batches"]) == ref.raw["batches"]
+        assert int(z["sprt_rejected"]) == ref.raw["sprt_rejected"]
+        assert int(z["sprt_histories"]) == ref.raw["sprt_histories"]
+    if case.endswith("_sprt"):  # the SPRT walk actually rejected models
+        assert ref.raw["sprt_rejected"] > 0
 
 
 @pytest.mark.gpu
-def test_sharded_run_rejects_sprt(usac):
+def test_sharded_run_failing_gather_fails(usac):
+    """A gather callback that raises fails the run (usac_last_error), never hangs it."""
     pts, mdl = make_case(usac, "e_uniform")
-    mdl.setSprt(True)
     r = usac.Ransac(mdl, pts)
+
+    def bad(b):
+        raise RuntimeError("peer lost")
     with pytest.raises(usac.UsacError):
-        r.run(shard=(2, 0, lambda b: [b, b]))
+        r.run(shard=(2, 0, bad))

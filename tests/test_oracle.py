@@ -110,3 +110,54 @@ def test_line2d_generator_reproduces_reference_dataset(oracle, line2d_scenes):
         assert pts.shape == ref_pts.shape, name
         assert (fmt(pts.astype(np.float64)) == fmt(ref_pts.astype(np.float64))).all(), name
         assert (fmt(gt.astype(np.float64)) == fmt(ref_model.astype(np.float64))).all(), name
+
+
+def _weighted_T(pts, idx, w):
+    """normalizing_transformation.cpp:117-146 in numpy, fp32 sequential chains as written."""
+    m = np.zeros(4, np.float32)
+    d = np.zeros(2, np.float32)
+    for i in idx:
+        q = (w[i] * pts[i]).astype(np.float32)
+        m = (m + q).astype(np.float32)
+        d[0] = np.float32(np.float64(d[0]) + np.sqrt(np.float64(np.float32(q[0] * q[0] + q[1] * q[1]))))
+        d[1] = np.float32(np.float64(d[1]) + np.sqrt(np.float64(np.float32(q[2] * q[2] + q[3] * q[3]))))
+    m = (m / np.float32(len(idx))).astype(np.float32)
+    s = [np.float32(np.sqrt(2.0) / np.float64(np.float32(d[k] / np.float32(len(idx))))) for k in range(2)]
+    T = [np.array([[s[k], 0, -m[2 * k] * s[k]], [0, s[k], -m[2 * k + 1] * s[k]], [0, 0, 1]], np.float64)
+         for k in range(2)]
+    return T
+
+
+@pytest.mark.parametrize("kind", ["H", "F"])
+def test_weighted_nonminimal_matches_numpy(oracle, kind):
+    """The weighted overload (normalized_dlt.cpp:25-36, eight_points.cpp:176-228): the oracle's
+    model equals an fp64 numpy least-squares fit under the weighted normalisation (rel 1e-3), and the
+    unweighted fit does not (the data hold outliers, so the normalisation moves the algebraic fit)."""
+    rng = np.random.default_rng(3)
+    if kind == "H":
+        pts, _, _ = synthetic.homography_points(n=600, inlier_ratio=0.7, seed=5, noise=2.0)
+    else:
+        pts, _, _ = synthetic.fundamental_points(n=600, inlier_ratio=0.7, seed=5, noise=1.0, prosac_order=False)
+    idx = np.sort(rng.choice(600, 300, replace=False)).astype(np.int32)
+    w = (1.0 / (1.0 + rng.exponential(1.0, 600))).astype(np.float32)
+    est = oracle.Estimator(oracle.HOMOGRAPHY if kind == "H" else oracle.FUNDAMENTAL, pts)
+    got = est.nonminimal_weighted(idx, w)
+    T1, T2 = _weighted_T(pts, idx, w)
+    p = pts[idx].astype(np.float64)
+    a = np.c_[p[:, :2], np.ones(len(idx))] @ T1.T
+    b = np.c_[p[:, 2:], np.ones(len(idx))] @ T2.T
+    x1, y1, x2, y2 = a[:, 0], a[:, 1], b[:, 0], b[:, 1]
+    o, z = np.ones_like(x1), np.zeros_like(x1)
+    if kind == "H":
+        A = np.r_[np.c_[-x1, -y1, -o, z, z, z, x2 * x1, x2 * y1, x2],
+                  np.c_[z, z, z, -x1, -y1, -o, y2 * x1, y2 * y1, y2]]
+    else:
+        A = np.c_[x2 * x1, x2 * y1, x2, y2 * x1, y2 * y1, y2, x1, y1, o]
+    v = np.linalg.svd(A)[2][-1].reshape(3, 3)
+    M = np.linalg.inv(T2) @ v @ T1 if kind == "H" else T2.T @ v @ T1
+    M = M / M[2, 2]
+    tol = dict(rtol=1e-3, atol=1e-5 * np.abs(M).max())
+    assert np.allclose(got.reshape(3, 3), M, **tol)
+    assert not np.allclose(est.nonminimal(idx).reshape(3, 3), M, **tol)
+    with pytest.raises(NotImplementedError):
+        oracle.Estimator(oracle.LINE2D, synthetic.line_points(200)[0]).nonminimal_weighted(idx[:10], w[:200])
