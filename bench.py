@@ -222,6 +222,54 @@ def valu_roofline(kernel_prefix, n_points, batch, kernel_ms):
     return out
 
 
+def _stage_kernels(estimator, sprt, chunks, stage):
+    """The kernels of one timed stage of a batch (usac_hypothesize_async: solve = ev0..ev1,
+    score = ev1..ev2), as rocprofv3 names them (prefixes, spaces ignored)."""
+    est = {"fundamental": 3, "essential": 4}.get(estimator, 2)
+    if stage == "solve":
+        return {2: ["usac::k_solve_h4("], 3: ["usac::k_solve_f7("],
+                4: ["usac::k_e5_basis(", "usac::k_e5_dets(", "usac::k_e5_roots(", "usac::k_e5_check(",
+                    "usac::k_e5_select("]}[est]
+    if sprt:
+        return ["void usac::k_sprt_head<%d>(" % est, "void usac::k_sprt_tail<%d>(" % est]
+    if est == 2:
+        return ["usac::k_presort_h(", "void usac::k_score_hf<%d, false>(" % chunks]
+    return ["usac::k_prepare_rec(", "void usac::k_presort_tv<%d>(" % est, "void usac::k_score_f2<%d>(" % est,
+            "usac::k_tv_combine("]
+
+
+def stage_roofline(prefixes, n_points, batch, stage_ms):
+    """VALU roofline of a stage of kernels: the VALU-busy SIMD-cycles of all its kernels per
+    batch (PMC SQ_ACTIVE_INST_VALU x 4, committed summary of the same workload shape) over the
+    stage's time measured live with HIP events on the context stream, against 1024 SIMDs x
+    2.4 GHz; per kernel, the same fraction against its own rocprofv3 duration, the wave-cycle
+    split and the counter-measured HBM bytes.  None without a summary for every kernel."""
+    ents = [(p, _profile_entry(p, n_points, batch)) for p in prefixes]
+    if not stage_ms or any(e is None or "SQ_ACTIVE_INST_VALU" not in e[0].get("pmc", {}) for _, e in ents):
+        return None
+    t = stage_ms * 1e-3
+    busy = sum(e[0]["pmc"]["SQ_ACTIVE_INST_VALU"] * 4 for _, e in ents)
+    hbm = sum(e[0].get("hbm_bytes_per_launch", 0.0) for _, e in ents)
+    out = {"bound": "valu", "unit": "SIMD-cycles/s", "peak": SIMD_CYCLES_S, "achieved": busy / t,
+           "frac": busy / t / SIMD_CYCLES_S, "valu_busy_cycles_per_launch": busy, "stage_ms": stage_ms,
+           "sources": sorted({e[1] for _, e in ents}),
+           "hbm": {"traffic_bytes_per_launch": hbm, "achieved_gbs": hbm / t / 1e9, "peak_gbs": HBM_PEAK_GBS,
+                   "frac": hbm / t / 1e9 / HBM_PEAK_GBS}, "kernels": {}}
+    for p, (v, _) in ents:
+        pmc = v["pmc"]
+        k = {"rocprof_avg_us": v.get("trace", {}).get("avg_ns", 0.0) / 1e3,
+             "valu_busy_cycles": pmc["SQ_ACTIVE_INST_VALU"] * 4}
+        if k["rocprof_avg_us"]:
+            k["valu_frac"] = k["valu_busy_cycles"] / (k["rocprof_avg_us"] * 1e-6) / SIMD_CYCLES_S
+        if pmc.get("SQ_WAVE_CYCLES"):
+            k["wave_cycle_split"] = {c.lower(): pmc[c] / pmc["SQ_WAVE_CYCLES"]
+                                     for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY") if c in pmc}
+        if "hbm_bytes_per_launch" in v:
+            k["hbm_bytes"] = v["hbm_bytes_per_launch"]
+        out["kernels"][p.replace("void ", "").replace("usac::", "").rstrip("(")] = k
+    return out
+
+
 _DEV = 0
 
 
@@ -554,27 +602,42 @@ def main():
         else:
             bytes_per_hyp = models_per_hyp * 16 * n + m * 4 + models_per_hyp * (36 + 8)
         avg_score_ms = float(np.mean(solo_score))
+        avg_solve_ms = float(np.mean(solo_solve))
         achieved = bytes_per_hyp * B / (avg_score_ms * 1e-3) / 1e9
-        kname = ("void usac::k_score_f2<%d>" if (fund or ess) else "void usac::k_score_hf<%d, false>") % args.chunks
-        kshort = ("k_sprt_head/tail<%d>" % (3 if fund else 4 if ess else 2)) if args.sprt else \
-            (("k_score_f2<%d,%s>" % (args.chunks, "E" if ess else "F")) if (fund or ess) else
-             ("k_score_hf<%d,false>" % args.chunks))
-        roof = valu_roofline(kname, n, B, avg_score_ms) if not args.sprt else None
+        # the dominant stage of a batch (solo HIP-event times): its kernels' VALU roofline
+        stage = "solve" if avg_solve_ms > avg_score_ms else "score"
+        other = "score" if stage == "solve" else "solve"
+        stage_ms = {"score": avg_score_ms, "solve": avg_solve_ms}
+        knames = {st: _stage_kernels(args.estimator, args.sprt, args.chunks, st) for st in ("score", "solve")}
+        roof = None
+        if not (fund or ess) and not args.sprt and stage == "score":  # cfg2: the score kernel alone (unchanged form)
+            roof = valu_roofline(knames["score"][1], n, B, avg_score_ms)
+            if roof is not None:
+                roof["stage"] = stage_roofline(knames["score"], n, B, avg_score_ms)
+        if roof is None:
+            roof = stage_roofline(knames[stage], n, B, stage_ms[stage])
         if roof is None:
             roof = {"bound": "valu", "achieved": None, "peak": SIMD_CYCLES_S, "unit": "SIMD-cycles/s", "frac": None,
-                    "note": "no committed PMC summary (profiles/r*_summary.json) for this kernel and workload"}
+                    "note": "no committed PMC summary (profiles/r*_summary.json) for these kernels and workload"}
+        roof["other_stage"] = {"stage": other, "ms": stage_ms[other],
+                               "roofline": stage_roofline(knames[other], n, B, stage_ms[other])}
+        kshort = "+".join(k.replace("void ", "").replace("usac::", "").rstrip("(").replace(" ", "")
+                          for k in knames[stage])
         roof.update({
             "traffic": roof.get("hbm", {}).get("traffic_bytes_per_launch"), "traffic_unit": "bytes/launch",
-            "kernel": kshort, "kernel_ms": avg_score_ms, "hypotheses_per_launch": B, "sprt": bool(args.sprt),
+            "dominant_stage": stage,
+            "kernel": kshort, "kernel_ms": stage_ms[stage], "hypotheses_per_launch": B, "sprt": bool(args.sprt),
             "sprt_points_tested_per_batch": tested_per_batch, "models_per_hypothesis": models_per_hyp,
             "algorithmic_bytes_per_hypothesis": bytes_per_hyp,
             "algorithmic_equiv_gbs": achieved,
             "note": "frac = VALU-busy SIMD-cycles per launch (PMC SQ_ACTIVE_INST_VALU x 4, packed FMAs at their two "
-                    "issue slots) / measured kernel time / (1024 SIMDs x 2.4 GHz): the score kernel is "
+                    "issue slots; summed over the dominant stage's kernels) / the stage's HIP-event time / (1024 "
+                    "SIMDs x 2.4 GHz); other_stage: the same for the other stage of the batch.  The score kernel is "
                     "fp32-VALU-issue bound with its point records L2/scalar-cache resident, so `hbm` (counter-"
                     "measured bytes) is a small fraction of HBM peak; algorithmic_equiv_gbs = SURVEY §8(d) bytes "
                     "(16 B x N per hypothesis) / kernel time, a re-read-equivalent rate, not a roofline fraction",
-            "solve_kernel_ms": float(np.mean(solo_solve)), "kernel_ms_in_pipeline": float(np.mean(score_ms)),
+            "score_kernel_ms": avg_score_ms,
+            "solve_kernel_ms": avg_solve_ms, "kernel_ms_in_pipeline": float(np.mean(score_ms)),
             "solve_kernel_ms_in_pipeline": float(np.mean(solve_ms)),
             "batch_device_ms_in_pipeline": float(np.mean(batch_ms))})
         smp_name = {"prosac": "Prosac (reference subset schedule, T_N = 200000)",

@@ -132,6 +132,8 @@ typedef struct usac_run_output {
     uint32_t lo_rounds;         /* LO speculation rounds (batches of inner iterations run at once) */
     uint32_t lo_stages;         /* LO device stages (one batched fit or one batched scoring each) */
     uint32_t sum_models;        /* models whose exact sequential Σerr the replay needed */
+    uint32_t lo_fits;           /* LO least-squares fits this rank ran (a sharded run splits the
+                                   inner-iteration chains: the ranks' counts add up to the 1-rank run's) */
 } usac_run_output;
 
 /* ---- lifetime ----------------------------------------------------------------- */

@@ -90,7 +90,8 @@ class _RunOutput(ctypes.Structure):
                 ("batches", ctypes.c_uint32), ("sprt_rejected", ctypes.c_int32), ("sprt_histories", ctypes.c_int32),
                 ("prosac_term_len", ctypes.c_uint32), ("rollbacks", ctypes.c_uint32),
                 ("lo_inner_iters", ctypes.c_uint32), ("lo_iterative_iters", ctypes.c_uint32),
-                ("lo_rounds", ctypes.c_uint32), ("lo_stages", ctypes.c_uint32), ("sum_models", ctypes.c_uint32)]
+                ("lo_rounds", ctypes.c_uint32), ("lo_stages", ctypes.c_uint32), ("sum_models", ctypes.c_uint32),
+                ("lo_fits", ctypes.c_uint32)]
 
 
 # every symbol include/usac_gpu.h declares (checked by tests/test_abi.py)
@@ -662,7 +663,8 @@ class Ransac:
                "n_records": out.n_records, "batches": out.batches, "sprt_rejected": out.sprt_rejected,
                "sprt_histories": out.sprt_histories, "prosac_term_len": out.prosac_term_len,
                "rollbacks": out.rollbacks, "lo_iterative_iters": out.lo_iterative_iters,
-               "lo_rounds": out.lo_rounds, "lo_stages": out.lo_stages, "sum_models": out.sum_models}
+               "lo_rounds": out.lo_rounds, "lo_stages": out.lo_stages, "sum_models": out.sum_models,
+               "lo_fits": out.lo_fits}
         self._out = RansacOutput(np.array(out.model[:], dtype=np.float32), inl[: out.inliers].copy(), out.time_us,
                                  out.inliers, out.iters, raw, out.lo_inner_iters)
 

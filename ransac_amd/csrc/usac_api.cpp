@@ -570,6 +570,52 @@ hipError_t enqueue_nonminimal(usac_ctx *c, const int32_t *idx_dev, uint32_t n, f
     return usac::launch_nonminimal_batch(c->stream, c->estimator, c->pts.p, b);
 }
 
+// The ranks of a sharded run and their all-gather of host bytes: the gather callback when one
+// is given, else RCCL on the context's communicator (staged through device buffers).  Every
+// payload is prefixed by the sender's status word, so a rank whose local part failed still
+// joins the collective and every rank then fails with the first failing rank's status.
+struct Shard {
+    int nranks = 1, rank = 0;
+    usac_allgather_fn gather = nullptr;
+    void *user = nullptr;
+};
+
+int shard_allgather(usac_ctx *c, const Shard &sh, int status, const void *send, size_t bytes,
+                    std::vector<uint8_t> &recv) {
+    const size_t rb = 8 + ((bytes + 7) & ~(size_t)7);  // status word padded to 8, payload
+    std::vector<uint8_t> mine(rb, 0);
+    memcpy(mine.data(), &status, sizeof(status));
+    if (bytes) memcpy(mine.data() + 8, send, bytes);
+    recv.resize(rb * (size_t)sh.nranks);
+    if (sh.gather) {
+        if (sh.gather(sh.user, mine.data(), rb, recv.data()) != 0)
+            return fail(c, USAC_ERR_ARG, "all-gather callback failed (gather callbacks must fail on every rank)");
+    } else {
+        if (!c->comm) return fail(c, USAC_ERR_ARG, "sharded run without a communicator");
+        HIP_TRY(c, c->x_send.reserve(rb));
+        HIP_TRY(c, c->x_recv.reserve(rb * (size_t)sh.nranks));
+        pinned_vector<uint8_t> st(rb * (size_t)(sh.nranks + 1));
+        memcpy(st.data(), mine.data(), rb);
+        HIP_TRY(c, hipMemcpyAsync(c->x_send.p, st.data(), rb, hipMemcpyHostToDevice, c->stream));
+        NCCL_TRY(c, ncclAllGather(c->x_send.p, c->x_recv.p, rb, ncclUint8, c->comm, c->stream));
+        HIP_TRY(c, hipMemcpyAsync(st.data() + rb, c->x_recv.p, rb * (size_t)sh.nranks, hipMemcpyDeviceToHost,
+                                  c->stream));
+        HIP_TRY(c, stream_wait(c->stream));
+        memcpy(recv.data(), st.data() + rb, rb * (size_t)sh.nranks);
+    }
+    for (int r = 0; r < sh.nranks; r++) {
+        int32_t st;
+        memcpy(&st, recv.data() + (size_t)r * rb, sizeof(st));
+        if (st != USAC_OK)
+            return r == sh.rank ? st : fail(c, st, "sharded run: rank " + std::to_string(r) + " failed (status " +
+                                                        std::to_string(st) + ")");
+    }
+    // payloads only, rank after rank (bytes each)
+    for (int r = 0; r < sh.nranks; r++) memmove(recv.data() + (size_t)r * bytes, recv.data() + (size_t)r * rb + 8, bytes);
+    recv.resize(bytes * (size_t)sh.nranks);
+    return USAC_OK;
+}
+
 // LO-RANSAC: InnerLocalOptimization::GetModelScore (inner_local_optimization.hpp:74-133) with
 // IterativeLocalOptimization (iterative_local_optimization.hpp:61-136).  lo_model's threshold
 // persists across calls and compounds like the reference's; the LO mt19937 is
@@ -600,17 +646,22 @@ struct LoRansac {
         int lo_cnt = 0;
         float lo_sum = 0.f;
         uint32_t it = 0, iter_count = 0;
-        bool failed = false, fit_pos = false;
+        int32_t failed = 0, fit_pos = 0;
         float model[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        // the model and threshold that produced the chain's inlier list (its last successful
+        // fit's scoring): a rank that does not own the chain rebuilds the list from them
+        float list_model[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        float list_thr = 0.f;
     };
 
     usac_ctx *c;
+    Shard sh;  // sharded run: chain w runs on rank w % nranks (unlimited variant only)
     usac::Mt19937 g;
     bool limited;
     uint32_t inner, iters, limit, mult, m, n, wmax;
     float theta, lo_thr, step;
     uint32_t inner_count = 0, iterative_count = 0;
-    uint32_t rounds = 0, stages = 0;  // speculation rounds and device stages (statistics)
+    uint32_t rounds = 0, stages = 0, fits = 0;  // speculation rounds, device stages, fits (statistics)
     int rc = USAC_OK;
     // entry best of the current call
     int best_cnt = 0;
@@ -629,8 +680,9 @@ struct LoRansac {
     int32_t *dpos = nullptr, *dcnt = nullptr, *dok = nullptr;
     float *dthr = nullptr, *dsum = nullptr, *dmod = nullptr;
 
-    LoRansac(usac_ctx *ctx, const usac_params *p)
+    LoRansac(usac_ctx *ctx, const usac_params *p, const Shard &shard)
         : c(ctx),
+          sh(shard),
           g(p->seed + 1u),
           limited(p->lo == USAC_LO_INITFLORSC),
           inner(p->lo_inner_iterations),
@@ -685,6 +737,9 @@ struct LoRansac {
     }
 
     static bool bigger(int c1, float s1, int c2, float s2) { return c1 > c2 || (c1 == c2 && s1 > s2); }
+    // chains of this rank: all of them unless the run is sharded.  The limited variant draws
+    // inside its iterative stage (one chain, the generator moves), so it is never split.
+    bool own(uint32_t w) const { return sh.nranks == 1 || limited || (int)(w % (uint32_t)sh.nranks) == sh.rank; }
 
     // the threshold an inner iteration leaves when its iterative stage runs all its steps
     float predict(float t) const {
@@ -728,6 +783,7 @@ struct LoRansac {
         for (uint32_t w = 0; w < W; w++) {
             const Chain &h = ch[w];
             hns[w] = 0;
+            if (!own(w)) continue;
             if (h.phase == INNER_FIT || h.phase == ITER_FIT) {
                 fit = true;
                 bool p;
@@ -743,6 +799,7 @@ struct LoRansac {
                     hthr[w] = h.thr;
                 }
                 pos = pos || p;
+                fits++;
                 hslots[ns++] = w;
                 nmax = std::max(nmax, hns[w]);
             } else if (h.phase == INNER_SCORE || h.phase == ITER_SCORE) {
@@ -759,7 +816,7 @@ struct LoRansac {
             // its first hns[w] list entries -- identity positions (hns[w] <= limit)
             for (uint32_t w = 0; w < W; w++) {
                 const Chain &h = ch[w];
-                const bool fitting = h.phase == INNER_FIT || h.phase == ITER_FIT;
+                const bool fitting = own(w) && (h.phase == INNER_FIT || h.phase == ITER_FIT);
                 const bool own = h.phase == INNER_FIT ? inner_cnt > (int)limit : h.fit_pos;
                 if (fitting && !own)
                     for (uint32_t i = 0; i < hns[w]; i++) hpos[(size_t)w * limit + i] = (int32_t)i;
@@ -794,6 +851,7 @@ struct LoRansac {
         stages++;
         for (uint32_t w = 0; w < W; w++) {
             Chain &h = ch[w];
+            if (!own(w)) continue;
             switch (h.phase) {
                 case INNER_FIT:  // LeastSquaresFitting(lo_sample | max_inliers) -> lo_model
                     memcpy(h.model, hmod + 9 * (size_t)w, sizeof(h.model));
@@ -802,6 +860,7 @@ struct LoRansac {
                         h.phase = DONE;
                     } else {
                         h.thr = (float)mult * h.thr;  // K * theta
+                        scored_list(h, w);
                         inner_scored(h, w);
                     }
                     break;
@@ -811,6 +870,7 @@ struct LoRansac {
                 case ITER_FIT:
                     memcpy(h.model, hmod + 9 * (size_t)w, sizeof(h.model));
                     if (hok[w]) {
+                        scored_list(h, w);
                         iter_scored(h, w);
                     } else if (h.fit_pos) {  // GetScoreLimited: continue
                         h.it++;
@@ -827,6 +887,11 @@ struct LoRansac {
             }
         }
         return USAC_OK;
+    }
+    // a fitted model was scored: lo_lists[w] now holds its inliers at hthr[w]
+    void scored_list(Chain &h, uint32_t w) {
+        memcpy(h.list_model, h.model, sizeof(h.model));
+        h.list_thr = hthr[w];
     }
     // the inner iteration's scoring of lo_model at K * theta
     void inner_scored(Chain &h, uint32_t w) {
@@ -889,11 +954,22 @@ struct LoRansac {
                 t = predict(t);
             }
             rounds++;
+            int st = USAC_OK;
             for (;;) {
                 bool active = false;
-                for (uint32_t w = 0; w < W; w++) active |= ch[w].phase != DONE;
+                for (uint32_t w = 0; w < W; w++) active |= own(w) && ch[w].phase != DONE;
                 if (!active) break;
-                if ((rc = stage(W, cnt))) return;
+                if ((st = stage(W, cnt))) break;
+            }
+            if (sh.nranks > 1 && !limited) {  // every rank's chains, one all-gather per round
+                std::vector<uint8_t> all;
+                if ((rc = shard_allgather(c, sh, st, ch.data(), sizeof(Chain) * W, all))) return;
+                for (uint32_t w = 0; w < W; w++)
+                    if (!own(w))
+                        memcpy(&ch[w], all.data() + sizeof(Chain) * ((size_t)(w % (uint32_t)sh.nranks) * W + w),
+                               sizeof(Chain));
+            } else if ((rc = st)) {
+                return;
             }
             if (limited) g_after[0] = g;  // the iterative stage's draws
             // replay in order
@@ -920,8 +996,19 @@ struct LoRansac {
                     memcpy(model, h.model, sizeof(h.model));
                     cnt = h.lo_cnt;
                     sum = h.lo_sum;
-                    e = hipMemcpyAsync(c->lo_max.p, c->lo_lists.as<int32_t>() + (size_t)w * n,
-                                       sizeof(int32_t) * (size_t)cnt, hipMemcpyDeviceToDevice, c->stream);
+                    if (own(w)) {
+                        e = hipMemcpyAsync(c->lo_max.p, c->lo_lists.as<int32_t>() + (size_t)w * n,
+                                           sizeof(int32_t) * (size_t)cnt, hipMemcpyDeviceToDevice, c->stream);
+                    } else {  // another rank's chain: its list is the inliers of (list_model, list_thr)
+                        memcpy(hmodel, h.list_model, sizeof(float) * 9);
+                        e = hipMemcpyAsync(c->one_model.p, hmodel, sizeof(float) * 9, hipMemcpyHostToDevice, c->stream);
+                        if (e == hipSuccess)
+                            e = usac::launch_inliers(c->stream, c->estimator, c->pts.p, n, c->one_model.as<float>(),
+                                                     h.list_thr, c->lo_max.as<int32_t>(), c->inl_cnt.as<int32_t>(),
+                                                     c->inl_sum.as<float>(), c->inl_scratch.p);
+                        // hmodel is reused by the next H2D copy: that copy is queued behind this one
+                        if (e == hipSuccess) e = stream_wait(c->stream);
+                    }
                     if (e != hipSuccess) {
                         rc = fail(c, USAC_ERR_HIP, std::string("LO inliers copy: ") + hipGetErrorString(e));
                         return;
@@ -1879,7 +1966,12 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     sub(1);
     std::unique_ptr<LoRansac> lo;
     if (use_lo) {
-        lo.reset(new LoRansac(c, prm));
+        Shard shard;
+        shard.nranks = nranks;
+        shard.rank = rank;
+        shard.gather = gather;
+        shard.user = gather_user;
+        lo.reset(new LoRansac(c, prm, shard));
         if ((rc = lo->reserve())) return rc;
     }
     std::unique_ptr<GcLo> gc;
@@ -2121,6 +2213,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         out->lo_iterative_iters = lo ? lo->iterative_count : gc ? gc->labelings : 0;
         out->lo_rounds = lo ? lo->rounds : gc ? gc->labelings : 0;
         out->lo_stages = lo ? lo->stages : gc ? gc->stages : 0;
+        out->lo_fits = lo ? lo->fits : 0;
     };
     lo_counters();
     memcpy(out->minimal_model, best_model, sizeof(best_model));

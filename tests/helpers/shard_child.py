@@ -33,7 +33,7 @@ def main():
     o = r.getRansacOutput()
     np.savez(out_path, model=o.getModel(), inliers=o.getInliers(), iters=o.getNumberOfMainIterations(),
              lo=o.getLOIters(), records=np.array(r.records, dtype=np.float64).reshape(-1, 3),
-             batches=o.raw["batches"], sprt_rejected=o.raw["sprt_rejected"], sprt_histories=o.raw["sprt_histories"])
+             batches=o.raw["batches"], sprt_rejected=o.raw["sprt_rejected"], sprt_histories=o.raw["sprt_histories"], lo_fits=o.raw["lo_fits"], lo_rounds=o.raw["lo_rounds"])
     dist.barrier()
     dist.destroy_process_group()
 

@@ -80,6 +80,12 @@ def test_sharded_run_equals_single_rank(usac, tmp_path, case):
         assert int(z["sprt_histories"]) == ref.raw["sprt_histories"]
     if case.endswith("_sprt"):  # the SPRT walk actually rejected models
         assert ref.raw["sprt_rejected"] > 0
+    if case == "h_napsac_lo":  # LO chains split over the ranks: same rounds, the fits partitioned
+        z = [np.load(tmp_path / ("r%d.npz" % k)) for k in range(2)]
+        assert ref.raw["lo_fits"] > 0
+        assert all(int(zk["lo_rounds"]) == ref.raw["lo_rounds"] for zk in z)
+        assert sum(int(zk["lo_fits"]) for zk in z) == ref.raw["lo_fits"]
+        assert all(int(zk["lo_fits"]) < ref.raw["lo_fits"] for zk in z)
 
 
 @pytest.mark.gpu

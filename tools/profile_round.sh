@@ -1,21 +1,24 @@
 #!/bin/bash
-# Round-2 profiles: per workload a rocprofv3 kernel trace (--stats) of the bench at one batch in
+# Per-round profiles: per workload a rocprofv3 kernel trace (--stats) of the bench at one batch in
 # flight, then separate PMC passes (no PMC + trace mix; <= 8 SQ / 2 GRBM / 4 TCC counters each):
 # HBM bytes (FETCH_SIZE, WRITE_SIZE), VALU issue (SQ_ACTIVE_INST_VALU + GRBM_GUI_ACTIVE) and the
 # wave-cycle split.  Summaries (tools/summarize_profile.py, tagged with the workload shape the
-# bench matches on) go to gpurun_out/prof_r2/summaries; copy them into profiles/.
+# bench matches on) go to gpurun_out/prof_<tag>/summaries; copy them into profiles/.
+#   TAG=r3 WORKLOADS="h10k f10k_sprt e50k" bash tools/profile_round.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof_r2
+TAG=${TAG:-r3}
+OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT/summaries
-WORKLOADS=${WORKLOADS:-"h10k h100k e50k"}
+WORKLOADS=${WORKLOADS:-"h10k f10k_sprt e50k"}
 for w in $WORKLOADS; do
   case $w in
-    h10k)  ARGS=""; NPTS=10000 ;;
-    h100k) ARGS="--points 100000"; NPTS=100000 ;;
-    e50k)  ARGS="--estimator essential"; NPTS=50000 ;;
-    f10k)  ARGS="--estimator fundamental --no-sprt --sampler uniform"; NPTS=10000 ;;
+    h10k)      ARGS=""; NPTS=10000 ;;
+    h100k)     ARGS="--points 100000"; NPTS=100000 ;;
+    e50k)      ARGS="--estimator essential"; NPTS=50000 ;;
+    f10k)      ARGS="--estimator fundamental --no-sprt --sampler uniform"; NPTS=10000 ;;
+    f10k_sprt) ARGS="--estimator fundamental"; NPTS=10000 ;;   # cfg3: PROSAC + batch SPRT (bench default)
   esac
   D=$OUT/$w; mkdir -p $D
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $PWD/$D/trace -o run --output-format csv -- \
@@ -28,6 +31,6 @@ for w in $WORKLOADS; do
         python3 bench.py --steps 5 --warmup 1 --cpu-seconds 0 --pipeline 1 $ARGS > $D/bench_pmc_$name.json 2> $D/pmc_$name.err
     rc=$?; echo "== $w pmc $ctr rc=$rc"; [ $rc -eq 0 ] || { tail -5 $D/pmc_$name.err; exit $rc; }
   done
-  python3 tools/summarize_profile.py $D r2_$w $NPTS 65536 $OUT/summaries > /dev/null || exit 1
+  python3 tools/summarize_profile.py $D ${TAG}_$w $NPTS 65536 $OUT/summaries > /dev/null || exit 1
 done
 ls -la $OUT/summaries
