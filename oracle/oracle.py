@@ -83,6 +83,7 @@ def lib():
         L.orc_est_estimate.argtypes = [ctypes.c_void_p, _i32p, _f32p]
         L.orc_est_nonminimal.argtypes = [ctypes.c_void_p, _i32p, ctypes.c_uint, _f32p]
         L.orc_est_nonminimal_weighted.argtypes = [ctypes.c_void_p, _i32p, ctypes.c_uint, _f32p, _f32p]
+        L.orc_sym_eig_min.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double)]
         L.orc_est_set_model.argtypes = [ctypes.c_void_p, _f32p]
         L.orc_est_error.argtypes = [ctypes.c_void_p, ctypes.c_uint]
         L.orc_est_error.restype = ctypes.c_float
@@ -496,3 +497,13 @@ def hypothesis_loop_mt(kind, points, thr, seed, count, threads, dlt_mode=DLT_THI
     dt = L.orc_hypothesis_loop_mt(kind, _p(pts, _f32p), pts.shape[0], dlt_mode, thr, seed, count, threads,
                                   ctypes.byref(best))
     return dt, best.value
+
+
+def sym_eig_min(A):
+    """The LSQ fits' 9x9 eigen spec: (smallest-eigenvalue eigenvector, True if inverse iteration
+    converged / False if the Jacobi fall-back ran)."""
+    A = np.ascontiguousarray(A, dtype=np.float64).reshape(81)
+    v = np.zeros(9, dtype=np.float64)
+    dp = ctypes.POINTER(ctypes.c_double)
+    ok = lib().orc_sym_eig_min(A.ctypes.data_as(dp), v.ctypes.data_as(dp))
+    return v, bool(ok)

@@ -235,7 +235,7 @@ static const signed char kJacobiRounds[9][4][2] = {
     {{0, 6}, {1, 2}, {4, 8}, {5, 7}}, {{0, 5}, {2, 8}, {3, 7}, {4, 6}}, {{0, 4}, {1, 7}, {2, 6}, {3, 5}},
     {{0, 3}, {1, 5}, {2, 4}, {7, 8}}, {{0, 2}, {1, 3}, {5, 8}, {6, 7}}, {{0, 1}, {3, 8}, {4, 7}, {5, 6}}};
 
-static void sym_eig_min(double A[9][9], double *v) {
+static void sym_eig_min_jacobi(double A[9][9], double *v) {
     double V[9][9];
     for (int i = 0; i < 9; i++)
         for (int j = 0; j < 9; j++) V[i][j] = (i == j) ? 1.0 : 0.0;
@@ -296,6 +296,89 @@ static void sym_eig_min(double A[9][9], double *v) {
     for (int i = 1; i < 9; i++)
         if (A[i][i] < A[m][m]) m = i;
     for (int k = 0; k < 9; k++) v[k] = V[k][m];
+}
+
+/* Smallest-eigenvalue eigenvector of the symmetric 9x9 normal matrix (the LSQ fits'
+ * cv::SVD of a tall system, see sym_eig_min_jacobi): inverse iteration on A + mu I, with the
+ * two-sided Jacobi above as the fall-back.  Spec (identical on the device, kernels_nonmin.hip):
+ *   tr = sum of the diagonal (k = 0..8 in order); not (tr > 0) or not finite -> fall back;
+ *   mu = tr * 1e-12; Cholesky L of A + mu I column by column: d = (A[j][j] + mu) - L[j][0]^2 -
+ *   ... - L[j][j-1]^2 (left to right), not (d > 0) -> fall back, L[j][j] = sqrt(d),
+ *   inv[j] = 1 / L[j][j], L[i][j] = (A[i][j] - L[i][0] L[j][0] - ...) * inv[j];
+ *   x = (1/3, ..., 1/3); up to 30 times: L y = x (y[i] = (x[i] - L[i][0] y[0] - ...) * inv[i]),
+ *   L^T z = y (i = 8..0, z[i] = (y[i] - L[i+1][i] z[i+1] - ... - L[8][i] z[8]) * inv[i]),
+ *   nn = sum z[k]^2 (not (nn > 0) or not finite -> fall back), r = 1 / sqrt(nn), x' = z * r,
+ *   d = max |x' - x| (first of equal maxima irrelevant), x = x'; d <= 1e-13 -> done (v = x);
+ *   from the third step on, d > d_prev / 4 (slow: the two smallest eigenvalues are close, as
+ *   for an outlier-contaminated algebraic fit) -> fall back; 30 steps -> fall back.
+ * Converges in 5-7 steps on inlier sets (eigenvalue ratio ~1e-4); the fall-back keeps the
+ * old spec for degenerate systems.  The eigenvector is defined up to sign: inverse iteration
+ * from x keeps the sign with x . v > 0, the Jacobi the sign its rotations leave. */
+static int eig_min_invit(double A[9][9], double *v) {
+    double tr = 0.0;
+    for (int k = 0; k < 9; k++) tr += A[k][k];
+    if (!(tr > 0.0) || !isfinite(tr)) return 0;
+    const double mu = tr * 1e-12;
+    double L[9][9], inv[9];
+    for (int j = 0; j < 9; j++) {
+        double d = A[j][j] + mu;
+        for (int k = 0; k < j; k++) d -= L[j][k] * L[j][k];
+        if (!(d > 0.0)) return 0;
+        L[j][j] = sqrt(d);
+        inv[j] = 1.0 / L[j][j];
+        for (int i = j + 1; i < 9; i++) {
+            double s = A[i][j];
+            for (int k = 0; k < j; k++) s -= L[i][k] * L[j][k];
+            L[i][j] = s * inv[j];
+        }
+    }
+    double x[9], dprev = 0.0;
+    for (int k = 0; k < 9; k++) x[k] = 1.0 / 3.0;
+    for (int it = 0; it < 30; it++) {
+        double y[9], z[9];
+        for (int i = 0; i < 9; i++) {
+            double s = x[i];
+            for (int k = 0; k < i; k++) s -= L[i][k] * y[k];
+            y[i] = s * inv[i];
+        }
+        for (int i = 8; i >= 0; i--) {
+            double s = y[i];
+            for (int k = i + 1; k < 9; k++) s -= L[k][i] * z[k];
+            z[i] = s * inv[i];
+        }
+        double nn = 0.0;
+        for (int k = 0; k < 9; k++) nn += z[k] * z[k];
+        if (!(nn > 0.0) || !isfinite(nn)) return 0;
+        const double r = 1.0 / sqrt(nn);
+        double d = 0.0;
+        for (int k = 0; k < 9; k++) {
+            const double xn = z[k] * r;
+            const double e = fabs(xn - x[k]);
+            if (e > d) d = e;
+            x[k] = xn;
+        }
+        if (d <= 1e-13) {
+            for (int k = 0; k < 9; k++) v[k] = x[k];
+            return 1;
+        }
+        if (it >= 2 && d > 0.25 * dprev) return 0;
+        dprev = d;
+    }
+    return 0;
+}
+
+static void sym_eig_min(double A[9][9], double *v) {
+    if (!eig_min_invit(A, v)) sym_eig_min_jacobi(A, v);
+}
+
+/* test hook: the 9x9 eigen spec (returns 1 when inverse iteration converged, 0 = Jacobi) */
+int orc_sym_eig_min(const double *A81, double *v) {
+    double A[9][9];
+    for (int i = 0; i < 9; i++)
+        for (int j = 0; j < 9; j++) A[i][j] = A81[9 * i + j];
+    const int ok = eig_min_invit(A, v);
+    if (!ok) sym_eig_min_jacobi(A, v);
+    return ok;
 }
 
 /* ------------------------------------------------------------ estimators */
@@ -433,21 +516,29 @@ static int homography_normalized_dlt(const orc_est *e, const int *sample, unsign
         pick_vector(W, (int)(2 * n), ORC_DLT_THIN, v);
     } else {
         /* A^T A summation order (no reference order exists -- OpenCV's SVD hides it):
-         * 64-point blocks summed in point order, block partials summed in block order. */
+         * 64-point blocks summed in point order, 64 blocks (4096 points) summed in block order
+         * into a superblock partial, superblock partials summed in order. */
         double AtA[9][9];
         memset(AtA, 0, sizeof(AtA));
-        for (unsigned int b0 = 0; b0 < n; b0 += 64) {
-            double P[9][9];
-            memset(P, 0, sizeof(P));
-            unsigned int b1 = b0 + 64 < n ? b0 + 64 : n;
-            for (unsigned int i = b0; i < b1; i++) {
-                double r0[9], r1[9];
-                dlt_fill_rows(norm[4 * i], norm[4 * i + 1], norm[4 * i + 2], norm[4 * i + 3], r0, r1);
+        for (unsigned int s0 = 0; s0 < n; s0 += 4096) {
+            double SP[9][9];
+            memset(SP, 0, sizeof(SP));
+            unsigned int s1 = s0 + 4096 < n ? s0 + 4096 : n;
+            for (unsigned int b0 = s0; b0 < s1; b0 += 64) {
+                double P[9][9];
+                memset(P, 0, sizeof(P));
+                unsigned int b1 = b0 + 64 < n ? b0 + 64 : n;
+                for (unsigned int i = b0; i < b1; i++) {
+                    double r0[9], r1[9];
+                    dlt_fill_rows(norm[4 * i], norm[4 * i + 1], norm[4 * i + 2], norm[4 * i + 3], r0, r1);
+                    for (int j = 0; j < 9; j++)
+                        for (int k = j; k < 9; k++) P[j][k] += r0[j] * r0[k] + r1[j] * r1[k];
+                }
                 for (int j = 0; j < 9; j++)
-                    for (int k = j; k < 9; k++) P[j][k] += r0[j] * r0[k] + r1[j] * r1[k];
+                    for (int k = j; k < 9; k++) SP[j][k] += P[j][k];
             }
             for (int j = 0; j < 9; j++)
-                for (int k = j; k < 9; k++) AtA[j][k] += P[j][k];
+                for (int k = j; k < 9; k++) AtA[j][k] += SP[j][k];
         }
         for (int j = 0; j < 9; j++)
             for (int k = 0; k < j; k++) AtA[j][k] = AtA[k][j];
@@ -797,22 +888,29 @@ static int fundamental_8pt(const orc_est *e, const int *sample, unsigned int n, 
         row_jacobi(W, (int)n);
         pick_vector(W, (int)n, ORC_DLT_THIN, v);
     } else {
-        double AtA[9][9];
+        double AtA[9][9]; /* blocks / superblocks as homography_normalized_dlt */
         memset(AtA, 0, sizeof(AtA));
-        for (unsigned int b0 = 0; b0 < n; b0 += 64) {
-            double P[9][9];
-            memset(P, 0, sizeof(P));
-            unsigned int b1 = b0 + 64 < n ? b0 + 64 : n;
-            for (unsigned int i = b0; i < b1; i++) {
-                float x1 = norm[4 * i], y1 = norm[4 * i + 1], x2 = norm[4 * i + 2], y2 = norm[4 * i + 3];
-                float row[9] = {x2 * x1, x2 * y1, x2, y2 * x1, y2 * y1, y2, x1, y1, 1.f};
-                double rd[9];
-                for (int k = 0; k < 9; k++) rd[k] = (double)row[k];
+        for (unsigned int s0 = 0; s0 < n; s0 += 4096) {
+            double SP[9][9];
+            memset(SP, 0, sizeof(SP));
+            unsigned int s1 = s0 + 4096 < n ? s0 + 4096 : n;
+            for (unsigned int b0 = s0; b0 < s1; b0 += 64) {
+                double P[9][9];
+                memset(P, 0, sizeof(P));
+                unsigned int b1 = b0 + 64 < n ? b0 + 64 : n;
+                for (unsigned int i = b0; i < b1; i++) {
+                    float x1 = norm[4 * i], y1 = norm[4 * i + 1], x2 = norm[4 * i + 2], y2 = norm[4 * i + 3];
+                    float row[9] = {x2 * x1, x2 * y1, x2, y2 * x1, y2 * y1, y2, x1, y1, 1.f};
+                    double rd[9];
+                    for (int k = 0; k < 9; k++) rd[k] = (double)row[k];
+                    for (int j = 0; j < 9; j++)
+                        for (int k = j; k < 9; k++) P[j][k] += rd[j] * rd[k];
+                }
                 for (int j = 0; j < 9; j++)
-                    for (int k = j; k < 9; k++) P[j][k] += rd[j] * rd[k];
+                    for (int k = j; k < 9; k++) SP[j][k] += P[j][k];
             }
             for (int j = 0; j < 9; j++)
-                for (int k = j; k < 9; k++) AtA[j][k] += P[j][k];
+                for (int k = j; k < 9; k++) AtA[j][k] += SP[j][k];
         }
         for (int j = 0; j < 9; j++)
             for (int k = 0; k < j; k++) AtA[j][k] = AtA[k][j];

@@ -59,6 +59,9 @@ int orc_cubic_roots(double c0, double c1, double c2, double c3, double *roots);
 int orc_est_estimate(orc_est *e, const int *sample, float *models);
 /* EstimateModelNonMinimalSample: returns 1 on success */
 int orc_est_nonminimal(orc_est *e, const int *sample, unsigned int n, float *model);
+/* the LSQ fits' 9x9 eigen spec (inverse iteration, Jacobi fall-back): smallest-eigenvalue
+ * eigenvector of the symmetric A (row-major 81); returns 1 if inverse iteration converged */
+int orc_sym_eig_min(const double *A81, double *v);
 /* the weighted overload (weights[point index]): homography / fundamental; -1 for the others */
 int orc_est_nonminimal_weighted(orc_est *e, const int *sample, unsigned int n, const float *weights, float *model);
 void orc_est_set_model(orc_est *e, const float *model);

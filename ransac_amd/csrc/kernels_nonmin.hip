@@ -198,16 +198,18 @@ __device__ __forceinline__ NormXf norm_xf(const float *t1, const float *t2) {
     return NormXf{t1[0], t1[2], t1[4], t1[5], t2[0], t2[2], t2[4], t2[5]};
 }
 
-// block partials of A^T A: one lane per (64-point block, group of 9 of the 45 upper-triangle
+// partials of A^T A: one lane per (64-point block, group of 9 of the 45 upper-triangle
 // entries, row-major j <= k) -- five lanes per block, the group wave-uniform (blockIdx.y) and
 // a compile-time constant in the body; each entry accumulated in registers over the block's
-// points in order (the spec's unit and order; the grouping only spreads the entries over
-// lanes).  FUND: one 8-point row per correspondence (eight_points.cpp:26-45), else two DLT rows.
+// points in order; then the workgroup's 64 blocks (a 4096-point superblock) summed in block
+// order by one lane per entry, one partial per superblock (the spec's units and order; the
+// grouping only spreads the entries over lanes).  FUND: one 8-point row per correspondence
+// (eight_points.cpp:26-45), else two DLT rows.
 constexpr int kAtaGroups = 5;                  // 45 = 5 x 9 entries
 constexpr int kAtaPer = 45 / kAtaGroups;
 
 template <bool FUND, int G>
-__device__ __forceinline__ void ata_group(const float4 *q, const NormXf xf, uint32_t b0, uint32_t b1, double *out) {
+__device__ __forceinline__ void ata_group(const float4 *q, const NormXf xf, uint32_t b0, uint32_t b1, double *acc_out) {
     double acc[kAtaPer];
 #pragma unroll
     for (int e = 0; e < kAtaPer; e++) acc[e] = 0.0;
@@ -243,17 +245,17 @@ __device__ __forceinline__ void ata_group(const float4 *q, const NormXf xf, uint
         for (uint32_t u = 0; u < kB; u++) cur[u] = nxt[u];
     }
 #pragma unroll
-    for (int e = 0; e < kAtaPer; e++) out[kAtaPer * G + e] = acc[e];
+    for (int e = 0; e < kAtaPer; e++) acc_out[e] = acc[e];
 }
 
 // group g (wave-uniform) to its compile-time instance
 template <bool FUND, int G = 0>
 __device__ __forceinline__ void ata_dispatch(int g, const float4 *q, const NormXf xf, uint32_t b0, uint32_t b1,
-                                             double *out) {
+                                             double *acc) {
     if constexpr (G + 1 < kAtaGroups) {
-        if (g != G) return ata_dispatch<FUND, G + 1>(g, q, xf, b0, b1, out);
+        if (g != G) return ata_dispatch<FUND, G + 1>(g, q, xf, b0, b1, acc);
     }
-    ata_group<FUND, G>(q, xf, b0, b1, out);
+    ata_group<FUND, G>(q, xf, b0, b1, acc);
 }
 
 template <bool FUND>
@@ -270,14 +272,27 @@ __global__ __launch_bounds__(64) void k_ata_partial(const float4 *__restrict__ q
         ws_all[18 * w + threadIdx.x] = t1[threadIdx.x];
         ws_all[18 * w + 9 + threadIdx.x] = t2[threadIdx.x];
     }
+    if ((FUND ? n <= 8 : 2 * n <= 9) || blockIdx.x * 64 * kAtaBlock >= n) return;  // workgroup-uniform
+    __shared__ double red[64][kAtaPer + 1];
     const uint32_t blk = blockIdx.x * 64 + threadIdx.x;
-    if ((FUND ? n <= 8 : 2 * n <= 9) || blk * kAtaBlock >= n) return;
-    const NormXf xf = norm_xf(t1, t2);
-    const float4 *q = q_all + w * q_stride;
-    const uint32_t b0 = blk * kAtaBlock;
-    const uint32_t b1 = b0 + kAtaBlock < n ? b0 + kAtaBlock : n;
-    double *out = partial_all + w * p_stride + (size_t)blk * 45;
-    ata_dispatch<FUND>((int)blockIdx.y, q, xf, b0, b1, out);
+    double acc[kAtaPer];
+    if (blk * kAtaBlock < n) {
+        const NormXf xf = norm_xf(t1, t2);
+        const float4 *q = q_all + w * q_stride;
+        const uint32_t b0 = blk * kAtaBlock;
+        const uint32_t b1 = b0 + kAtaBlock < n ? b0 + kAtaBlock : n;
+        ata_dispatch<FUND>((int)blockIdx.y, q, xf, b0, b1, acc);
+#pragma unroll
+        for (int e = 0; e < kAtaPer; e++) red[threadIdx.x][e] = acc[e];
+    }
+    __syncthreads();
+    if (threadIdx.x < kAtaPer) {  // superblock sum, blocks in order
+        const uint32_t nblocks = (n + kAtaBlock - 1) / kAtaBlock, first = blockIdx.x * 64;
+        const uint32_t nb = nblocks - first < 64 ? nblocks - first : 64;
+        double sum = 0.0;
+        for (uint32_t b = 0; b < nb; b++) sum += red[b][threadIdx.x];
+        partial_all[w * p_stride + (size_t)blockIdx.x * 45 + kAtaPer * blockIdx.y + threadIdx.x] = sum;
+    }
 }
 
 // Final solve, one wave: A^T A from the partials (lane e), round-robin Jacobi eigen over
@@ -307,6 +322,77 @@ __device__ void thin_solve(const float4 *q, const NormXf xf, double *v) {
     pick_vector<R>(W, 0, v);
 }
 
+// Smallest-eigenvalue eigenvector of the symmetric 9x9 A (LDS, both triangles): inverse
+// iteration on A + 1e-12 tr(A) I through its Cholesky factor, in one lane with the factor in
+// registers -- the oracle's eig_min_invit spec operation for operation (usac_oracle.c).
+// Returns false when the spec falls back to the Jacobi (not positive definite, non-finite, or
+// the two smallest eigenvalues too close for fast convergence).
+__device__ bool eig_min_invit(const double (*A)[9], double *v) {
+    double tr = 0.0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) tr += A[k][k];
+    if (!(tr > 0.0) || !isfinite(tr)) return false;
+    const double mu = tr * 1e-12;
+    double L[9][9], inv[9];
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+        double d = A[j][j] + mu;
+#pragma unroll
+        for (int k = 0; k < j; k++) d -= L[j][k] * L[j][k];
+        if (!(d > 0.0)) return false;
+        L[j][j] = sqrt(d);
+        inv[j] = 1.0 / L[j][j];
+#pragma unroll
+        for (int i = j + 1; i < 9; i++) {
+            double s = A[i][j];
+#pragma unroll
+            for (int k = 0; k < j; k++) s -= L[i][k] * L[j][k];
+            L[i][j] = s * inv[j];
+        }
+    }
+    double x[9], dprev = 0.0;
+#pragma unroll
+    for (int k = 0; k < 9; k++) x[k] = 1.0 / 3.0;
+    for (int it = 0; it < 30; it++) {
+        double y[9], z[9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            double s = x[i];
+#pragma unroll
+            for (int k = 0; k < i; k++) s -= L[i][k] * y[k];
+            y[i] = s * inv[i];
+        }
+#pragma unroll
+        for (int i = 8; i >= 0; i--) {
+            double s = y[i];
+#pragma unroll
+            for (int k = i + 1; k < 9; k++) s -= L[k][i] * z[k];
+            z[i] = s * inv[i];
+        }
+        double nn = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) nn += z[k] * z[k];
+        if (!(nn > 0.0) || !isfinite(nn)) return false;
+        const double r = 1.0 / sqrt(nn);
+        double d = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            const double xn = z[k] * r;
+            const double e = fabs(xn - x[k]);
+            if (e > d) d = e;
+            x[k] = xn;
+        }
+        if (d <= 1e-13) {
+#pragma unroll
+            for (int k = 0; k < 9; k++) v[k] = x[k];
+            return true;
+        }
+        if (it >= 2 && d > 0.25 * dprev) return false;
+        dprev = d;
+    }
+    return false;
+}
+
 template <bool FUND>
 __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_all, size_t q_stride,
                                                    const uint32_t *__restrict__ ns, uint32_t n1,
@@ -320,7 +406,7 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
     const uint32_t n = ns ? ns[w] : n1;
     const float4 *q = q_all + w * q_stride;
     const double *partial = partial_all + w * p_stride;
-    const uint32_t nblocks = (n + kAtaBlock - 1) / kAtaBlock;
+    const uint32_t nblocks = (n + kAtaBlock * 64 - 1) / (kAtaBlock * 64);  // superblock partials
     const float *ws = ws_all + 18 * w;
     float *model_out = model_all + 9 * w;
     int32_t *ok = ok_all + w;
@@ -363,7 +449,7 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
                 }
                 rem -= 9 - r;
             }
-            // the block partials in block order (spec), sixteen loads in flight per sixteen adds
+            // the superblock partials in order (spec), sixteen loads in flight per sixteen adds
             double acc = 0.0;
             uint32_t c = 0;
             for (; c + 16 <= nblocks; c += 16) {
@@ -380,7 +466,17 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
         if (t < 9)
             for (int j = 0; j < 9; j++) V[j][t] = (j == (int)t) ? 1.0 : 0.0;
         __syncthreads();
-        // round-robin Jacobi (the oracle's sym_eig_min spec): per round the rotations of 4
+        // the spec's inverse iteration (lane 0); the Jacobi below only when it falls back
+        __shared__ int s_done;
+        if (t == 0) {
+            double v[9];
+            s_done = eig_min_invit(A, v) ? 1 : 0;
+            if (s_done)
+                for (int k = 0; k < 9; k++) s_v[k] = v[k];
+        }
+        __syncthreads();
+        if (!s_done) {
+        // round-robin Jacobi (the oracle's sym_eig_min_jacobi spec): per round the rotations of 4
         // disjoint planes from the matrix at the round's start, then all column updates (lane =
         // (row, plane), V alongside), then all row updates (lane = (plane, column)) -- every
         // lane owns disjoint element pairs, 3 barriers per round
@@ -449,6 +545,7 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
             for (int k = 0; k < 9; k++) s_v[k] = V[k][m];
         }
         __syncthreads();
+        }  // fall-back Jacobi
     }
     if (t == 0 && FUND) {
         double T1[9], tmp[9], Fd[9];
