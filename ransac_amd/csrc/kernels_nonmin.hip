@@ -393,23 +393,15 @@ __device__ bool eig_min_invit(const double (*A)[9], double *v) {
     return false;
 }
 
+// The end of a fit, one wave: the thin row-Jacobi when the system has <= 8 rows (homography
+// 2n <= 8, fundamental n <= 8: SURVEY Q1/Q2), else the smallest eigenvector of the normal
+// matrix A (LDS, both triangles, filled by the caller before the call) by the spec's inverse
+// iteration (lane 0) with the round-robin Jacobi as its fall-back; then the transform back and
+// the cast.  q: the fit's points (global or LDS), ws: T1, T2.
 template <bool FUND>
-__global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_all, size_t q_stride,
-                                                   const uint32_t *__restrict__ ns, uint32_t n1,
-                                                   const double *__restrict__ partial_all, size_t p_stride,
-                                                   const float *ws_all, float *model_all, int32_t *ok_all) {
-    __shared__ double A[9][9];
-    __shared__ double V[9][9];
-    __shared__ double s_v[9];
+__device__ __forceinline__ void fit_finish(const float4 *q, uint32_t n, const float *ws, double (*A)[9], double (*V)[9],
+                           double *s_v, float *model_out, int32_t *ok) {
     const uint32_t t = threadIdx.x;
-    const uint32_t w = blockIdx.x;
-    const uint32_t n = ns ? ns[w] : n1;
-    const float4 *q = q_all + w * q_stride;
-    const double *partial = partial_all + w * p_stride;
-    const uint32_t nblocks = (n + kAtaBlock * 64 - 1) / (kAtaBlock * 64);  // superblock partials
-    const float *ws = ws_all + 18 * w;
-    float *model_out = model_all + 9 * w;
-    int32_t *ok = ok_all + w;
     if (n == 0) {  // EstimateModelNonMinimalSample of no points fails
         if (t == 0) *ok = 0;
         return;
@@ -439,30 +431,6 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
         }
         __syncthreads();
     } else {
-        if (t < 45) {
-            int j = 0, k = t, rem = (int)t;
-            for (int r = 0; r < 9; r++) {
-                if (rem < 9 - r) {
-                    j = r;
-                    k = r + rem;
-                    break;
-                }
-                rem -= 9 - r;
-            }
-            // the superblock partials in order (spec), sixteen loads in flight per sixteen adds
-            double acc = 0.0;
-            uint32_t c = 0;
-            for (; c + 16 <= nblocks; c += 16) {
-                double x[16];
-#pragma unroll
-                for (int u = 0; u < 16; u++) x[u] = partial[(size_t)(c + u) * 45 + t];
-#pragma unroll
-                for (int u = 0; u < 16; u++) acc += x[u];
-            }
-            for (; c < nblocks; c++) acc += partial[(size_t)c * 45 + t];
-            A[j][k] = acc;
-            A[k][j] = acc;
-        }
         if (t < 9)
             for (int j = 0; j < 9; j++) V[j][t] = (j == (int)t) ? 1.0 : 0.0;
         __syncthreads();
@@ -594,6 +562,137 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
     }
 }
 
+
+// the entry (j, k), j <= k, of lane t < 45 of the upper triangle, row-major
+__device__ __forceinline__ void ata_entry(uint32_t t, int &j, int &k) {
+    int rem = (int)t;
+    j = 0;
+    k = (int)t;
+    for (int r = 0; r < 9; r++) {
+        if (rem < 9 - r) {
+            j = r;
+            k = r + rem;
+            return;
+        }
+        rem -= 9 - r;
+    }
+}
+
+template <bool FUND>
+__global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_all, size_t q_stride,
+                                                   const uint32_t *__restrict__ ns, uint32_t n1,
+                                                   const double *__restrict__ partial_all, size_t p_stride,
+                                                   const float *ws_all, float *model_all, int32_t *ok_all) {
+    __shared__ double A[9][9];
+    __shared__ double V[9][9];
+    __shared__ double s_v[9];
+    const uint32_t t = threadIdx.x;
+    const uint32_t w = blockIdx.x;
+    const uint32_t n = ns ? ns[w] : n1;
+    const double *partial = partial_all + w * p_stride;
+    const uint32_t nblocks = (n + kAtaBlock * 64 - 1) / (kAtaBlock * 64);  // superblock partials
+    if (n > 0 && !(FUND ? n <= 8 : 2 * n <= 9) && t < 45) {
+        int j, k;
+        ata_entry(t, j, k);
+        // the superblock partials in order (spec), sixteen loads in flight per sixteen adds
+        double acc = 0.0;
+        uint32_t c = 0;
+        for (; c + 16 <= nblocks; c += 16) {
+            double x[16];
+#pragma unroll
+            for (int u = 0; u < 16; u++) x[u] = partial[(size_t)(c + u) * 45 + t];
+#pragma unroll
+            for (int u = 0; u < 16; u++) acc += x[u];
+        }
+        for (; c < nblocks; c++) acc += partial[(size_t)c * 45 + t];
+        A[j][k] = acc;
+        A[k][j] = acc;
+    }
+    fit_finish<FUND>(q_all + w * q_stride, n, ws_all + 18 * w, A, V, s_v, model_all + 9 * w, ok_all + w);
+}
+
+// A whole fit of <= kSmallFit points in one workgroup (the LO inner fits of lo_sample_size
+// points, small polish lists): the points gathered into LDS; the four coordinate sums and the
+// two distance sums as the reference's sequential chains, one lane each (they are short);
+// T1, T2; the normal matrix in the spec's order (64-point blocks in point order, blocks in
+// order: one superblock), lane = entry; fit_finish.  Bit-identical to the multi-launch path.
+constexpr uint32_t kSmallFit = 256;
+
+template <bool FUND>
+__global__ __launch_bounds__(64) void k_fit_small(const float4 *__restrict__ pts, const int32_t *__restrict__ base,
+                                                  size_t base_stride, const int32_t *__restrict__ pos,
+                                                  size_t pos_stride, const uint32_t *__restrict__ ns, uint32_t n1,
+                                                  float *__restrict__ ws_all, float *__restrict__ model_all,
+                                                  int32_t *__restrict__ ok_all) {
+    __shared__ float4 q[kSmallFit];
+    __shared__ double A[9][9];
+    __shared__ double V[9][9];
+    __shared__ double s_v[9];
+    __shared__ float s_sums[6];
+    __shared__ float s_ws[18];
+    const uint32_t t = threadIdx.x;
+    const uint32_t w = blockIdx.x;
+    const uint32_t n = ns ? ns[w] : n1;
+    if (n == 0) {  // EstimateModelNonMinimalSample of no points fails
+        if (t == 0) ok_all[w] = 0;
+        return;
+    }
+    const int32_t *list = base + w * base_stride;
+    for (uint32_t i = t; i < n; i += 64) q[i] = pts[list[pos ? pos[w * pos_stride + i] : (int32_t)i]];
+    __syncthreads();
+    if (t < 4) {  // mean chains (normalizing_transformation.cpp:13-20)
+        float s = 0.f;
+        for (uint32_t i = 0; i < n; i++) s += (&q[i].x)[t];
+        s_sums[t] = s;
+    }
+    __syncthreads();
+    if (t < 2) {  // distance chains (:28-47): float += double sqrt of the float expression
+        const float mx = s_sums[2 * t] / (float)n, my = s_sums[2 * t + 1] / (float)n;
+        float d = 0.f;
+        for (uint32_t i = 0; i < n; i++) {
+            const float xm = (&q[i].x)[2 * t] - mx, ym = (&q[i].x)[2 * t + 1] - my;
+            d = (float)((double)d + sqrt((double)(xm * xm + ym * ym)));
+        }
+        s_sums[4 + t] = d;
+    }
+    __syncthreads();
+    float t1[9], t2[9];
+    norm_transforms(s_sums, s_sums + 4, 0, n, t1, t2);
+    if (t < 9) {
+        s_ws[t] = t1[t];
+        s_ws[9 + t] = t2[t];
+        ws_all[18 * w + t] = t1[t];
+        ws_all[18 * w + 9 + t] = t2[t];
+    }
+    if (!(FUND ? n <= 8 : 2 * n <= 9) && t < 45) {
+        int j, k;
+        ata_entry(t, j, k);
+        const NormXf xf = norm_xf(t1, t2);
+        double sb = 0.0;  // the superblock (n <= 4096): blocks summed in order
+        for (uint32_t b0 = 0; b0 < n; b0 += kAtaBlock) {
+            const uint32_t b1 = b0 + kAtaBlock < n ? b0 + kAtaBlock : n;
+            double acc = 0.0;
+            for (uint32_t i = b0; i < b1; i++) {
+                const float4 p = xf(q[i]);
+                double r0[9], r1[9];
+                if (FUND) {
+                    fund_row(p.x, p.y, p.z, p.w, r0);
+                    acc += r0[j] * r0[k];
+                } else {
+                    dlt_rows(p.x, p.y, p.z, p.w, r0, r1);
+                    acc += r0[j] * r0[k] + r1[j] * r1[k];
+                }
+            }
+            sb += acc;
+        }
+        const double a = 0.0 + sb;  // the finish's sum over the (one) superblock partial
+        A[j][k] = a;
+        A[k][j] = a;
+    }
+    __syncthreads();
+    fit_finish<FUND>(q, n, s_ws, A, V, s_v, model_all + 9 * w, ok_all + w);
+}
+
 // Line PCA: one lane, sequential fp32 moments (sum_xy = 0 initialised),
 // closed-form eigenvector of the smaller eigenvalue of the 2x2 covariance (fp64).
 __global__ __launch_bounds__(64) void k_line_pca(const float2 *__restrict__ q_all, size_t q_stride,
@@ -660,6 +759,15 @@ hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pt
         return hipGetLastError();
     }
     float4 *q = static_cast<float4 *>(b.q);
+    if (b.nmax <= kSmallFit && !b.weights) {  // every fit in one workgroup, one launch
+        if (estimator == USAC_HOMOGRAPHY)
+            hipLaunchKernelGGL(k_fit_small<false>, dim3(b.W), dim3(64), 0, st, static_cast<const float4 *>(pts), b.base,
+                               b.base_stride, b.pos, b.pos_stride, b.ns, b.n1, b.ws, b.model_out, b.ok);
+        else
+            hipLaunchKernelGGL(k_fit_small<true>, dim3(b.W), dim3(64), 0, st, static_cast<const float4 *>(pts), b.base,
+                               b.base_stride, b.pos, b.pos_stride, b.ns, b.n1, b.ws, b.model_out, b.ok);
+        return hipGetLastError();
+    }
     if (b.weights) {  // the weighted overload: six independent sequential chains, then as below
         if (!b.qw) return hipErrorInvalidValue;
         char *seq = static_cast<char *>(b.seq);

@@ -249,3 +249,28 @@ def test_full_size_device_sampler_properties(usac, oracle):
     oc, os_ = est.quality(best["model"], 2.0)
     assert oc == n and np.float32(os_) == np.float32(ssum)
     assert (idx[1:] > idx[:-1]).all()                              # ascending, unique
+
+
+@pytest.mark.parametrize("kind", ["H", "F"])
+def test_nonminimal_sizes_bit_exact(usac, oracle, kind):
+    """Non-minimal fits on both sides of the one-workgroup small-fit kernel (<= 256 points), the
+    64-point block and 4096-point superblock edges, on clean inlier subsets (inverse iteration)
+    and on outlier-contaminated ones (the Jacobi fall-back of the eigen spec)."""
+    from ransac_amd import synthetic as syn
+    if kind == "H":
+        pts, _, inl = syn.homography_points(n=12000, inlier_ratio=0.5, seed=21)
+        est_o, est_u = oracle.HOMOGRAPHY, usac.ESTIMATOR.Homography
+    else:
+        pts, _, inl = syn.fundamental_points(n=12000, inlier_ratio=0.5, seed=21, prosac_order=False)
+        est_o, est_u = oracle.FUNDAMENTAL, usac.ESTIMATOR.Fundamental
+    inliers = np.flatnonzero(inl)
+    est = oracle.Estimator(est_o, pts)
+    rng = np.random.default_rng(5)
+    with usac.Context(est_u, pts) as ctx:
+        for k in (5, 9, 14, 63, 64, 65, 255, 256, 257, 4096, 4097, 9000):
+            for contaminated in (False, True):
+                pool = inliers if not contaminated else np.arange(12000)
+                idx = np.sort(rng.choice(pool, size=min(k, len(pool)), replace=False)).astype(np.int32)
+                g = ctx.nonminimal(idx)
+                o = est.nonminimal(idx)
+                np.testing.assert_array_equal(g.view(np.int32), o.view(np.int32), err_msg="%s %d %s" % (kind, k, contaminated))
