@@ -76,3 +76,50 @@ def test_normalization_long_chains(usac, oracle, n):
         g2 = ctx.nonminimal(idx[::-1].copy())  # another order: another chain
     np.testing.assert_array_equal(g.view(np.int32), o.view(np.int32))
     np.testing.assert_array_equal(g2.view(np.int32), est.nonminimal(idx[::-1].copy()).view(np.int32))
+
+
+@pytest.mark.parametrize("kind", ["signed", "integer", "half_integer", "around_zero", "binade_edges"])
+def test_normalization_chains_adversarial(usac, oracle, kind):
+    """The mean / distance chains of NormalizedDLT on data that defeats the binade-piece
+    speculation (kernels_seqsum.hip): mixed-sign coordinates whose running sums wander across
+    zero, integer and half-integer coordinates (ties at every ulp the running sum reaches),
+    sums parked at powers of two.  The device must still equal the oracle's sequential loops."""
+    rng = np.random.default_rng(11)
+    n = 40000
+    if kind == "signed":
+        x1 = rng.uniform(-2000, 2000, (n, 2))
+    elif kind == "integer":
+        x1 = rng.integers(0, 4000, (n, 2)).astype(np.float64)
+    elif kind == "half_integer":
+        x1 = rng.integers(0, 8000, (n, 2)) / 2.0
+    elif kind == "around_zero":  # +-v pairs: the running sum keeps returning to ~0
+        a = rng.uniform(0, 1000, (n // 2, 2))
+        x1 = np.empty((n, 2))
+        x1[0::2], x1[1::2] = a, -a + rng.normal(0, 1e-3, a.shape)
+    else:  # 2^k-valued coordinates: the sums sit on binade edges
+        x1 = 2.0 ** rng.integers(0, 12, (n, 2)).astype(np.float64)
+    H = np.array([[1.1, 0.05, 30.0], [-0.04, 0.95, -12.0], [1e-5, -2e-5, 1.0]])
+    p = np.c_[x1, np.ones(n)] @ H.T
+    x2 = p[:, :2] / p[:, 2:] + rng.normal(0, 0.5, (n, 2))
+    pts = np.ascontiguousarray(np.c_[x1, x2], dtype=np.float32)
+    idx = np.arange(n, dtype=np.int32)
+    est = oracle.Estimator(oracle.HOMOGRAPHY, pts)
+    with usac.Context(usac.ESTIMATOR.Homography, pts) as ctx:
+        for sub in (idx, idx[: n // 3], idx[::-1].copy()):
+            g = ctx.nonminimal(sub)
+            np.testing.assert_array_equal(g.view(np.int32), est.nonminimal(sub).view(np.int32), err_msg=kind)
+
+
+@pytest.mark.parametrize("kind", ["integer", "half_ulp", "powers_of_two"])
+def test_residual_sum_ties(usac, kind):
+    """Σerr chains whose addends are exact ties at the running sum's ulp (integers, 0.5s, powers
+    of two): rounding then depends on the parity of the running value -- the walk's job."""
+    rng = np.random.default_rng(3)
+    n = 50000
+    if kind == "integer":
+        errs = rng.integers(0, 4, n).astype(np.float32)
+    elif kind == "half_ulp":
+        errs = (rng.integers(0, 8, n) * 0.5 + 2 ** -6).astype(np.float32)
+    else:
+        errs = (2.0 ** rng.integers(-8, 3, n)).astype(np.float32)
+    assert _residual_sum(usac, errs).view(np.int32) == _seq_sum(errs).view(np.int32)
