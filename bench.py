@@ -158,6 +158,60 @@ def parity_check(usac, kind, pts, thr, dlt_mode, samples=None):
             "scores_bit_equal": bool((s.view(np.int32) == osum.view(np.int32)).all())}
 
 
+def timed_kernel_parity(usac, ctx, kind, pts, thr, dlt_mode, seed, sprt, first_hyp=0):
+    """The timed configuration itself (device sampler, multi-chunk fast score kernel, batch SPRT
+    when on) on one 256-sample batch against the CPU oracle on the same device-drawn samples:
+    counts exact (SPRT: every accepted model's count), Σ within the throughput kernel's declared
+    bound, and the batch record (Score::bigger + earliest index) against the oracle's exact
+    (count, Σ).  The Σ bound per model with c inliers: two-view (exact terms, sums re-associated
+    over point chunks) |Σ| c 2^-23; homography (stage-B terms from v_rcp / v_sqrt, DESIGN.md
+    "Guard band": |S - 2 e| <= 2^-21 Mp + 2^-18 S per pair, Mp <= the dataset's max |x1|+|y1|+
+    |x2|+|y2|) c (2^-22 Mp_max + 2^-18 thr) + |Σ| c 2^-23."""
+    from oracle import oracle as O
+
+    fund, ess = kind == "fundamental", kind == "essential"
+    B = 256
+    smp = ctx.draw_samples(B, seed, first_hyp)
+    ctx.hypothesize_async(B, seed, first_hyp, thr)
+    rec = ctx.fetch_best()
+    spk = 3 if fund else 1
+    c, s = ctx.last_counts(B * spk)
+    est = O.Estimator(O.FUNDAMENTAL if fund else O.ESSENTIAL if ess else O.HOMOGRAPHY, pts, dlt_mode)
+    om, onm = est.estimate_batch(smp)
+    if fund:
+        oc, osum = est.score_models(om.reshape(-1, 9), thr)
+        occ = (np.arange(3)[None, :] < onm[:, None]).reshape(-1)
+    else:
+        oc, osum = est.score_models(om, thr)
+        occ = onm == 1 if ess else np.ones(B, bool)
+    oc = np.where(occ, oc, -1)
+    chk = (c >= 0) if sprt else occ
+    counts_ok = bool((c[chk] == oc[chk]).all()) and (sprt or bool((c[~occ] < 0).all()))
+    cnt = np.maximum(oc[chk], 0).astype(np.float64)
+    ref = np.abs(osum[chk].astype(np.float64))
+    bound = ref * cnt * 2.0 ** -23
+    if not (fund or ess):
+        mp = float(np.abs(pts.astype(np.float64)).sum(1).max())
+        bound += cnt * (2.0 ** -22 * mp + 2.0 ** -18 * thr)
+    err = np.abs(s[chk].astype(np.float64) - osum[chk])
+    if sprt:  # an accepted model's score is (float)count (sprt.hpp:276-281), not a Σ
+        err, bound = np.zeros(0), np.zeros(0)
+    out = {"hypotheses": B, "models": int(occ.sum()), "counts_equal": counts_ok,
+           "sums_within_bound": bool((err <= bound).all()),
+           "sum_max_err_over_bound": float((err / np.maximum(bound, 1e-30)).max()) if err.size else 0.0}
+    if sprt:
+        out["sprt_accepted"] = int((c >= 0).sum())
+    else:  # the record: Score::bigger over the oracle's exact (count, Σ), earliest slot on ties
+        best = None
+        for sl in np.flatnonzero(occ):
+            if best is None or oc[sl] > oc[best] or (oc[sl] == oc[best] and osum[sl] > osum[best]):
+                best = sl
+        out["best_record_equal"] = bool(best is not None and int(rec.inliers) == int(oc[best]) and
+                                        int(rec.hyp_index) == first_hyp + int(best) // spk)
+    out["ok"] = bool(counts_ok and out["sums_within_bound"] and out.get("best_record_equal", True))
+    return out
+
+
 def _profile_entry(kernel_prefix, n_points, batch):
     """(summary entry, source) of `kernel_prefix` in the newest committed rocprofv3 summary
     (profiles/<round>_summary.json, made by tools/profile.sh + tools/summarize_profile.py)
@@ -681,6 +735,8 @@ def main():
         if world == 1:
             out["parity"] = parity_check(usac, args.estimator, pts, args.threshold, dlt_mode,
                                          samples=ctx.draw_samples(256, args.seed) if napsac else None)
+            out["parity"]["timed_kernel"] = timed_kernel_parity(usac, ctx, args.estimator, pts, args.threshold,
+                                                                dlt_mode, args.seed, bool(args.sprt))
             if args.cpu_seconds > 0:
                 out["cpu_baseline"] = cpu_baseline(args.estimator, pts, args.threshold, dlt_mode, args.cpu_seconds)
                 out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]

@@ -97,7 +97,7 @@ typedef struct usac_params {
     uint32_t seed;              /* glibc srandom(seed): ResetRandomGenerator(false) semantics;
                                    also seeds PROSAC's mt19937 (the reference uses random_device) */
     int32_t dlt_mode;           /* USAC_DLT_* */
-    uint32_t batch;             /* hypotheses per device batch (0 = default) */
+    uint32_t batch;             /* hypotheses per device batch (0 = default: 1024, 2048, ... up to 8192; SPRT 1024) */
     int32_t sampler;            /* USAC_SAMPLER_UNIFORM | _NAPSAC (grid) | _PROSAC (points sorted by quality) */
     int32_t sprt;               /* Model::setSprt (model.hpp:104): SPRT verification, sprt.hpp */
     int32_t lo;                 /* USAC_LO_* (model.hpp:26) */

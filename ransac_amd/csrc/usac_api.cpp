@@ -25,6 +25,7 @@
 namespace {
 
 constexpr uint32_t kDefaultBatch = 8192;
+constexpr uint32_t kRampFirst = 1024;  // first batch of a run with the default batch
 
 // Device memory of the contexts comes from a process-wide cache per device: a context is
 // typically created per Ransac::run (as the reference constructs its Ransac per run), and
@@ -2039,8 +2040,13 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     };
 
     lap(T_SETUP);
+    // with the library's default batch the batches ramp up (1024, 2048, ...): the termination
+    // bound drops once the loop has a good model, and a smaller first batch draws, solves and
+    // scores fewer hypotheses the run never reaches (the replay is exact for any partition)
+    uint32_t cap = prm->batch ? batch : std::min<uint32_t>(batch, kRampFirst);
     while (iters < max_iters) {
-        const uint32_t B = std::min(batch, max_iters - iters);
+        const uint32_t B = std::min(std::min(batch, max_iters - iters), cap);
+        if (!prm->batch) cap = std::min<uint32_t>(batch, 2 * cap);
         // ---- draw the batch (speculatively for PROSAC)
         std::unique_ptr<usac::ProsacSampler> snapshot;
         const uint32_t gen_term = prosac ? pterm->terminationLength() : n;
