@@ -393,11 +393,12 @@ int ensure_grid(usac_ctx *c, int cs) {
         bits[j] = 1;  // 2^bits - 1 > range: room for the out-of-box sentinel
         while ((1ll << bits[j]) - 1 <= range) bits[j]++;
     }
-    // each dimension keeps its range plus the out-of-box sentinel; a key wider than 64 bits
-    // (e.g. 17 + 17 + 17 + 14 bits) is refused rather than clamped (a clamped dimension would
-    // give the sentinel a real cell's value)
-    if (bits[0] + bits[1] + bits[2] + bits[3] > 64)
-        return fail(c, USAC_ERR_UNSUPPORTED, "grid: the four cell ranges need more than 64 key bits");
+    // each dimension keeps its range plus the out-of-box sentinel; a key wider than 63 bits
+    // (e.g. 17 + 17 + 17 + 13 bits; the build's hash table keeps the all-ones word as its empty
+    // slot) is refused rather than clamped (a clamped dimension would give the sentinel a real
+    // cell's value)
+    if (bits[0] + bits[1] + bits[2] + bits[3] > 63)
+        return fail(c, USAC_ERR_UNSUPPORTED, "grid: the four cell ranges need more than 63 key bits");
     if (!c->grid_pin && !(c->grid_pin = static_cast<uint32_t *>(PinnedPool::get().take(64, &c->grid_pin_bytes))))
         return fail(c, USAC_ERR_HIP, "pinned host allocation failed");
     const size_t n = c->n;

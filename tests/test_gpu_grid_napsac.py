@@ -1,10 +1,13 @@
-"""Grid neighbours built on the device (kernels_grid.hip: cell-key radix sort, segment heads,
-first-appearance renumbering) and the device NAPSAC sampler of the throughput batches
+"""Grid neighbours built on the device (kernels_grid.hip: cell keys grouped in a hash table,
+first-appearance numbering by a scan in point order, members ranked per cell) and the device
+NAPSAC sampler of the throughput batches
 (nearest_neighbors.cpp:160-202, napsac_sampler.hpp:100-138).
 
 * The device CSR equals, array for array, a numpy restatement of the host GridNeighbors
   (cells in order of first appearance, members ascending) and the oracle's per-point
-  neighbour lists (orc_grid).
+  neighbour lists (orc_grid); also on one 300 k-point cell (bitmap ranking over two LDS
+  chunks), every cell size 1..40 (one-lane / workgroup ranking split at 16), large cells whose
+  smallest member sits late, and a handful of points.
 * Device NAPSAC samples: the initial point has >= m neighbours, the other m - 1 points are
   consecutive entries of its neighbour list (distinct, same cell); uniform samples when no
   point qualifies.
@@ -45,6 +48,37 @@ def test_device_grid_equals_host_csr(usac, oracle, cs):
         e = g["start"][g["cell"][i] + 1]
         mine = g["members"][b:e]
         np.testing.assert_array_equal(mine[mine != i], lists[i])
+
+
+def _grid_case(case):
+    rng = np.random.default_rng(11)
+    if case == "one_cell_300k":  # one cell: the bitmap ranking over two LDS chunks
+        return rng.uniform(0, 49, (300000, 4)).astype(np.float32), 50
+    if case == "sizes_1_to_40":  # every cell size around the one-lane / workgroup split (16)
+        sizes = np.arange(1, 41)
+        ctr = np.repeat(np.arange(len(sizes)), sizes)
+        pts = np.empty((len(ctr), 4), np.float32)
+        for j in range(4):
+            pts[:, j] = 100.0 * ((ctr * (j + 3)) % 41) + rng.uniform(1, 49, len(ctr))
+        return pts[rng.permutation(len(pts))], 50
+    if case == "clustered_chunks":  # large cells whose smallest members sit late in the index range
+        pts = rng.uniform(0, 2000, (290000, 4)).astype(np.float32)
+        pts[280000:] = rng.uniform(0, 20, (10000, 4))
+        pts[5000:5100] = rng.uniform(0, 20, (100, 4))
+        return pts, 40
+    if case == "few_points":
+        return rng.uniform(0, 100, (6, 4)).astype(np.float32), 60
+    raise ValueError(case)
+
+
+@pytest.mark.parametrize("case", ["one_cell_300k", "sizes_1_to_40", "clustered_chunks", "few_points"])
+def test_device_grid_edge_cases(usac, case):
+    pts, cs = _grid_case(case)
+    ref = _grid_numpy(pts, cs, 4)
+    with usac.Context(usac.ESTIMATOR.Homography, pts) as ctx:
+        g = ctx.grid_neighbors(cs)
+    for k in ("cell", "rank", "start", "members", "eligible"):
+        np.testing.assert_array_equal(g[k], ref[k], err_msg=k)
 
 
 def test_device_napsac_samples(usac):
