@@ -167,8 +167,17 @@ hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, 
     }
 #undef INL
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    // the reference's sequential fp32 Σ in point order (quality.hpp:85) over the compacted residuals
+    if (e != hipSuccess || !sums) return e;
+    return launch_inliers_sums(st, n, W, slots, counts, sums, scratch);
+}
+
+// the reference's sequential fp32 Σ in point order (quality.hpp:85) over the residuals the
+// compaction left in scratch
+hipError_t launch_inliers_sums(hipStream_t st, uint32_t n, uint32_t W, const uint32_t *slots, const int32_t *counts,
+                               float *sums, void *scratch) {
+    if (W == 0) return hipSuccess;
+    const uint32_t nb = (n + kInlBlock - 1) / kInlBlock;
+    uint32_t *scr = static_cast<uint32_t *>(scratch);
     const size_t stride = inl_stride(n), res0 = (nb + 63) & ~63u;
     return launch_seqsum(st, 1, false, reinterpret_cast<const float *>(scr + res0), stride,
                          reinterpret_cast<const uint32_t *>(counts), 0, W, slots, scr + inl_res_words(n),

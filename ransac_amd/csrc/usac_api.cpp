@@ -277,7 +277,10 @@ struct usac_ctx {
     size_t pol_pin_bytes = 0;
     DevBuf nm_seq;          // normalisation scratch of the non-minimal fits (polish and LO)
     DevBuf nm_w, nm_qw;     // usac_lsq_fit with weights: the weights, the weighted points
-    DevBuf lo_io;           // one LO stage's inputs and outputs, contiguous (one copy each way)
+    DevBuf lo_io;           // one LO stage's inputs (two blocks, alternating) and outputs
+    // the LO stages' Σerr passes run on their own stream beside the next stage's fit
+    hipStream_t lo_stream = nullptr;
+    hipEvent_t lo_ev[3] = {nullptr, nullptr, nullptr};  // compaction done; Σ done (two, alternating)
     // comm
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -649,6 +652,7 @@ struct LoRansac {
         float lo_sum = 0.f;
         uint32_t it = 0, iter_count = 0;
         int32_t failed = 0, fit_pos = 0;
+        int32_t sum_buf = -1;  // lo_sum still on its way from that Σ buffer (settle)
         float model[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
         // the model and threshold that produced the chain's inlier list (its last successful
         // fit's scoring): a rank that does not own the chain rebuilds the list from them
@@ -676,11 +680,19 @@ struct LoRansac {
     size_t pin_bytes = 0, in_bytes = 0, out_bytes = 0;
     uint32_t *hns = nullptr, *hslots = nullptr;
     int32_t *hpos = nullptr, *hcnt = nullptr, *hok = nullptr;
-    float *hthr = nullptr, *hsum = nullptr, *hmod = nullptr;
+    float *hthr = nullptr, *hmod = nullptr;
+    float *hsig[2] = {nullptr, nullptr};  // the stages' Σ, alternating (the second block after hmodel)
     float *hmodel = nullptr;  // pinned slot of the model a round starts from (its H2D copy)
     uint32_t *dns = nullptr, *dslots = nullptr;
     int32_t *dpos = nullptr, *dcnt = nullptr, *dok = nullptr;
     float *dthr = nullptr, *dsum = nullptr, *dmod = nullptr;
+    // Σerr of a stage's scoring runs on c->lo_stream, ordered after the stage's compaction, so
+    // the host takes the stage's counts and launches the next stage without waiting for it; a
+    // chain whose decision compares Σ (a count tie with the best) waits for it (settle).  The
+    // input block alternates between two device copies, so a Σ pass still reading its slots
+    // is never overwritten by the next stage's upload.
+    uint32_t sig_k = 0;
+    bool sig_live[2] = {false, false};
 
     LoRansac(usac_ctx *ctx, const usac_params *p, const Shard &shard)
         : c(ctx),
@@ -709,9 +721,14 @@ struct LoRansac {
         HIP_TRY(c, c->lo_lists.reserve(sizeof(int32_t) * N * W));
         in_bytes = sizeof(uint32_t) * (3 * W + W * L);
         out_bytes = sizeof(float) * 12 * W;
-        HIP_TRY(c, c->lo_io.reserve(in_bytes + out_bytes));
-        pin = PinnedPool::get().take(in_bytes + out_bytes + sizeof(float) * 16, &pin_bytes);
+        // device: input block 0, outputs, input block 1; host: inputs, outputs, round model, Σ block 1
+        HIP_TRY(c, c->lo_io.reserve(2 * in_bytes + out_bytes));
+        pin = PinnedPool::get().take(in_bytes + out_bytes + sizeof(float) * (16 + W), &pin_bytes);
         if (!pin) return fail(c, USAC_ERR_HIP, "hipHostMalloc (LO staging) failed");
+        if (!c->lo_stream) {
+            HIP_TRY(c, StreamPool::get().stream(&c->lo_stream));
+            for (auto &ev : c->lo_ev) HIP_TRY(c, StreamPool::get().event(&ev));
+        }
         hmodel = reinterpret_cast<float *>(static_cast<char *>(pin) + in_bytes + out_bytes);
         uint32_t *hw = static_cast<uint32_t *>(pin), *dw = c->lo_io.as<uint32_t>();
         hns = hw;
@@ -721,11 +738,9 @@ struct LoRansac {
         hmod = reinterpret_cast<float *>(hw + 3 * W + W * L);
         hok = reinterpret_cast<int32_t *>(hmod + 9 * W);
         hcnt = hok + W;
-        hsum = reinterpret_cast<float *>(hcnt + W);
-        dns = dw;
-        dthr = reinterpret_cast<float *>(dw + W);
-        dslots = dw + 2 * W;
-        dpos = reinterpret_cast<int32_t *>(dw + 3 * W);
+        hsig[0] = reinterpret_cast<float *>(hcnt + W);
+        hsig[1] = hmodel + 16;
+        in_block(0);
         dmod = reinterpret_cast<float *>(dw + 3 * W + W * L);
         dok = reinterpret_cast<int32_t *>(dmod + 9 * W);
         dcnt = dok + W;
@@ -736,6 +751,37 @@ struct LoRansac {
         HIP_TRY(c, c->lo_ws.reserve(sizeof(float) * 18 * W));
         HIP_TRY(c, c->lo_scr.reserve(usac::inliers_scratch_bytes(n, wmax)));
         return USAC_OK;
+    }
+
+    // device input block b (of two) of a stage: ns, thresholds, slots, LSQ positions
+    void in_block(int b) {
+        const size_t W = wmax;
+        uint32_t *dw = c->lo_io.as<uint32_t>() + (b ? in_bytes + out_bytes : 0) / sizeof(uint32_t);
+        dns = dw;
+        dthr = reinterpret_cast<float *>(dw + W);
+        dslots = dw + 2 * W;
+        dpos = reinterpret_cast<int32_t *>(dw + 3 * W);
+    }
+    // the Σ of buffer b has arrived: hand it to the chains waiting for it
+    int settle(int b) {
+        if (!sig_live[b]) return USAC_OK;
+        for (uint32_t spins = 0;; spins++) {
+            const hipError_t e = hipEventQuery(c->lo_ev[1 + b]);
+            if (e == hipSuccess) break;
+            if (e != hipErrorNotReady) return fail(c, USAC_ERR_HIP, std::string("LO sums: ") + hipGetErrorString(e));
+            if ((spins & 1023u) == 1023u) std::this_thread::yield();
+        }
+        for (uint32_t w = 0; w < wmax; w++)
+            if (ch[w].sum_buf == b) {
+                ch[w].lo_sum = hsig[b][w];
+                ch[w].sum_buf = -1;
+            }
+        sig_live[b] = false;
+        return USAC_OK;
+    }
+    int settle_all() {
+        const int r = settle(0);
+        return r ? r : settle(1);
     }
 
     static bool bigger(int c1, float s1, int c2, float s2) { return c1 > c2 || (c1 == c2 && s1 > s2); }
@@ -825,7 +871,9 @@ struct LoRansac {
             }
         }
         hipStream_t st = c->stream;
-        HIP_TRY(c, hipMemcpyAsync(c->lo_io.p, pin, in_bytes, hipMemcpyHostToDevice, st));
+        const int sb = (int)(sig_k & 1u);  // this stage's input block, Σ buffer and Σ event
+        in_block(sb);
+        HIP_TRY(c, hipMemcpyAsync(dns, pin, in_bytes, hipMemcpyHostToDevice, st));
         if (fit) {
             usac::NmBatch b{};
             b.base = inner_fit ? c->lo_max.as<int32_t>() : c->lo_lists.as<int32_t>();
@@ -845,12 +893,32 @@ struct LoRansac {
             b.seq = c->nm_seq.p;
             HIP_TRY(c, usac::launch_nonminimal_batch(st, c->estimator, c->pts.p, b));
         }
+        // the compaction rewrites the residuals and counts the previous stage's Σ pass reads
+        if (sig_live[sb ^ 1]) HIP_TRY(c, hipStreamWaitEvent(st, c->lo_ev[1 + (sb ^ 1)], 0));
         HIP_TRY(c, usac::launch_inliers_batch(st, c->estimator, c->pts.p, n, dmod, ns, 0.f, dthr, dslots,
-                                              c->lo_lists.as<int32_t>(), n, dcnt, dsum, c->lo_scr.p,
+                                              c->lo_lists.as<int32_t>(), n, dcnt, nullptr, c->lo_scr.p,
                                               fit ? dok : nullptr));
-        HIP_TRY(c, hipMemcpyAsync(hmod, dmod, out_bytes, hipMemcpyDeviceToHost, st));
+        HIP_TRY(c, hipMemcpyAsync(hmod, dmod, out_bytes - sizeof(float) * wmax, hipMemcpyDeviceToHost, st));
+        HIP_TRY(c, hipEventRecord(c->lo_ev[0], st));
+        HIP_TRY(c, hipStreamWaitEvent(c->lo_stream, c->lo_ev[0], 0));
+        HIP_TRY(c, usac::launch_inliers_sums(c->lo_stream, n, ns, dslots, dcnt, dsum, c->lo_scr.p));
+        HIP_TRY(c, hipMemcpyAsync(hsig[sb], dsum, sizeof(float) * wmax, hipMemcpyDeviceToHost, c->lo_stream));
+        HIP_TRY(c, hipEventRecord(c->lo_ev[1 + sb], c->lo_stream));
+        sig_live[sb] = true;
+        sig_k++;
         HIP_TRY(c, stream_wait(st));
         stages++;
+        // the previous stage's Σ ran beside this stage's fit; this stage's is needed now only by
+        // a chain whose count ties the best's (GetScoreUnlimited's comparison)
+        int r = settle(sb ^ 1);
+        bool tie = false;
+        for (uint32_t w = 0; w < W && !limited; w++) {
+            const Chain &h = ch[w];
+            if (own(w) && ((h.phase == ITER_FIT && hok[w]) || h.phase == ITER_SCORE) && hcnt[w] == best_cnt) tie = true;
+        }
+        if (!r && tie) r = settle(sb);
+        if (r) return r;
+        cur_sb = sb;
         for (uint32_t w = 0; w < W; w++) {
             Chain &h = ch[w];
             if (!own(w)) continue;
@@ -895,10 +963,20 @@ struct LoRansac {
         memcpy(h.list_model, h.model, sizeof(h.model));
         h.list_thr = hthr[w];
     }
+    // a scoring's Σ: at hand if this stage's Σ buffer was settled, else pending
+    int cur_sb = 0;
+    void take_sum(Chain &h, uint32_t w) {
+        if (sig_live[cur_sb]) {
+            h.sum_buf = cur_sb;
+        } else {
+            h.lo_sum = hsig[cur_sb][w];
+            h.sum_buf = -1;
+        }
+    }
     // the inner iteration's scoring of lo_model at K * theta
     void inner_scored(Chain &h, uint32_t w) {
         h.lo_cnt = hcnt[w];
-        h.lo_sum = hsum[w];
+        take_sum(h, w);
         if (h.lo_cnt <= (int)m) {
             h.outcome = FEW;
             h.phase = DONE;
@@ -911,7 +989,7 @@ struct LoRansac {
     // an iterative step's scoring of its fit
     void iter_scored(Chain &h, uint32_t w) {
         h.lo_cnt = hcnt[w];
-        h.lo_sum = hsum[w];
+        take_sum(h, w);  // settled first when the count ties the best's: the comparison reads it
         if (!limited && bigger(best_cnt, best_sum, h.lo_cnt, h.lo_sum)) {
             finish(h);  // GetScoreUnlimited: the best is bigger -> break
         } else {
@@ -963,6 +1041,8 @@ struct LoRansac {
                 if (!active) break;
                 if ((st = stage(W, cnt))) break;
             }
+            if (!st) st = settle_all();  // every chain's Σ before the exchange and the replay
+            else (void)hipStreamSynchronize(c->lo_stream);
             if (sh.nranks > 1 && !limited) {  // every rank's chains, one all-gather per round
                 std::vector<uint8_t> all;
                 if ((rc = shard_allgather(c, sh, st, ch.data(), sizeof(Chain) * W, all))) return;
@@ -1331,6 +1411,7 @@ void usac_destroy(usac_ctx *c) {
     (void)hipSetDevice(c->device);  // the pools are per device
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->xstream) (void)hipStreamSynchronize(c->xstream);
+    if (c->lo_stream) (void)hipStreamSynchronize(c->lo_stream);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->pol_pin) PinnedPool::get().give_back(c->pol_pin, c->pol_pin_bytes);
     if (c->x_pin) PinnedPool::get().give_back(c->x_pin, c->x_pin_bytes);
@@ -1340,6 +1421,9 @@ void usac_destroy(usac_ctx *c) {
         if (c->xev_done[k]) StreamPool::get().give_back(c->xev_done[k]);
     }
     if (c->xstream) StreamPool::get().give_back(c->xstream);
+    for (auto &ev : c->lo_ev)
+        if (ev) StreamPool::get().give_back(ev);
+    if (c->lo_stream) StreamPool::get().give_back(c->lo_stream);
     if (c->grid_pin) PinnedPool::get().give_back(c->grid_pin, c->grid_pin_bytes);
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,

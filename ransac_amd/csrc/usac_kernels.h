@@ -132,11 +132,15 @@ hipError_t launch_inliers(hipStream_t st, int estimator, const void *pts, uint32
 // when thrs is null; list at idx + w * idx_stride, idx nullable = counts and sums only;
 // counts[w], sums[w]).  slots (nullable): the W launched rows are slots[0..W) of a larger
 // set, every other slot is left untouched.  ok (nullable): slots with ok[w] == 0 keep their
-// index list (their counts / sums are undefined).  scratch = inliers_scratch_bytes(n, max slot + 1)
+// index list (their counts / sums are undefined).  sums nullable: no Σ pass, which
+// launch_inliers_sums then runs from the same scratch (e.g. on another stream, ordered after
+// this launch, before the scratch is reused).  scratch = inliers_scratch_bytes(n, max slot + 1)
 hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *models,
                                 uint32_t W, float thr, const float *thrs, const uint32_t *slots, int32_t *idx,
                                 size_t idx_stride, int32_t *counts, float *sums, void *scratch,
                                 const int32_t *ok = nullptr);
+hipError_t launch_inliers_sums(hipStream_t st, uint32_t n, uint32_t W, const uint32_t *slots, const int32_t *counts,
+                               float *sums, void *scratch);
 size_t inliers_scratch_bytes(uint32_t n, uint32_t W);
 // every point's exact residual under one model (n floats)
 hipError_t launch_point_errors(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *model,
