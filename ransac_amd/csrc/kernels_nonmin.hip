@@ -785,7 +785,7 @@ hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pt
         char *seq = static_cast<char *>(b.seq);
         const size_t ss = seq_stride(b.nmax);
         float *sums4 = reinterpret_cast<float *>(seq + b.W * ss), *dsum2 = sums4 + 4 * b.W;
-        const bool fused = b.nmax <= kFusedGatherMax;
+        const bool fused = b.fused_any || b.nmax <= kFusedGatherMax;
         if (fused)
             hipLaunchKernelGGL(k_gather_psum4, dim3(seq::kSegMax, b.W), dim3(256), 0, st,
                                static_cast<const float4 *>(pts), b.base, b.base_stride, b.pos, b.pos_stride, b.ns,

@@ -280,7 +280,8 @@ struct usac_ctx {
     DevBuf lo_io;           // one LO stage's inputs (two blocks, alternating) and outputs
     // the LO stages' Σerr passes run on their own stream beside the next stage's fit
     hipStream_t lo_stream = nullptr;
-    hipEvent_t lo_ev[3] = {nullptr, nullptr, nullptr};  // compaction done; Σ done (two, alternating)
+    // per block parity: the stage's outputs in the host block (main), its Σ (side); round end
+    hipEvent_t lo_ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     // comm
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
@@ -652,7 +653,6 @@ struct LoRansac {
         float lo_sum = 0.f;
         uint32_t it = 0, iter_count = 0;
         int32_t failed = 0, fit_pos = 0;
-        int32_t sum_buf = -1;  // lo_sum still on its way from that Σ buffer (settle)
         float model[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
         // the model and threshold that produced the chain's inlier list (its last successful
         // fit's scoring): a rank that does not own the chain rebuilds the list from them
@@ -674,25 +674,20 @@ struct LoRansac {
     float best_sum = 0.f;
     std::vector<Chain> ch;
     std::vector<usac::Mt19937> g_after;  // generator after chain w's inner draw
-    // a stage's inputs (ns, thresholds, slots, LSQ positions) and outputs (models, fit flags,
-    // counts, sums) as one pinned host block mirrored by one device block: one copy each way
+    // A stage's inputs (ns, thresholds, slots, LSQ positions) and outputs (models, fit flags,
+    // counts, Σ) as one pinned host block mirrored by one device block, one copy each way; two
+    // such pairs (and two scoring scratch areas), by stage parity, so that a pipelined round
+    // can have stage k + 1 on the device while the host reads stage k.
     void *pin = nullptr;
-    size_t pin_bytes = 0, in_bytes = 0, out_bytes = 0;
+    size_t pin_bytes = 0, in_bytes = 0, out_bytes = 0, scr_bytes = 0;
     uint32_t *hns = nullptr, *hslots = nullptr;
     int32_t *hpos = nullptr, *hcnt = nullptr, *hok = nullptr;
-    float *hthr = nullptr, *hmod = nullptr;
-    float *hsig[2] = {nullptr, nullptr};  // the stages' Σ, alternating (the second block after hmodel)
+    float *hthr = nullptr, *hsum = nullptr, *hmod = nullptr;
     float *hmodel = nullptr;  // pinned slot of the model a round starts from (its H2D copy)
     uint32_t *dns = nullptr, *dslots = nullptr;
     int32_t *dpos = nullptr, *dcnt = nullptr, *dok = nullptr;
     float *dthr = nullptr, *dsum = nullptr, *dmod = nullptr;
-    // Σerr of a stage's scoring runs on c->lo_stream, ordered after the stage's compaction, so
-    // the host takes the stage's counts and launches the next stage without waiting for it; a
-    // chain whose decision compares Σ (a count tie with the best) waits for it (settle).  The
-    // input block alternates between two device copies, so a Σ pass still reading its slots
-    // is never overwritten by the next stage's upload.
-    uint32_t sig_k = 0;
-    bool sig_live[2] = {false, false};
+    int next_par = 0;  // block parity of the next pipelined stage (alternates across rounds too)
 
     LoRansac(usac_ctx *ctx, const usac_params *p, const Shard &shard)
         : c(ctx),
@@ -712,7 +707,11 @@ struct LoRansac {
           ch(wmax),
           g_after(wmax, usac::Mt19937(0)) {}
     ~LoRansac() {
-        if (pin) PinnedPool::get().give_back(pin, pin_bytes);
+        if (pin) {  // a pipelined round's unread last stage may still copy into the blocks
+            (void)hipStreamSynchronize(c->stream);
+            if (c->lo_stream) (void)hipStreamSynchronize(c->lo_stream);
+            PinnedPool::get().give_back(pin, pin_bytes);
+        }
     }
 
     int reserve() {
@@ -721,69 +720,51 @@ struct LoRansac {
         HIP_TRY(c, c->lo_lists.reserve(sizeof(int32_t) * N * W));
         in_bytes = sizeof(uint32_t) * (3 * W + W * L);
         out_bytes = sizeof(float) * 12 * W;
-        // device: input block 0, outputs, input block 1; host: inputs, outputs, round model, Σ block 1
-        HIP_TRY(c, c->lo_io.reserve(2 * in_bytes + out_bytes));
-        pin = PinnedPool::get().take(in_bytes + out_bytes + sizeof(float) * (16 + W), &pin_bytes);
+        HIP_TRY(c, c->lo_io.reserve(2 * (in_bytes + out_bytes)));
+        pin = PinnedPool::get().take(2 * (in_bytes + out_bytes) + sizeof(float) * 16, &pin_bytes);
         if (!pin) return fail(c, USAC_ERR_HIP, "hipHostMalloc (LO staging) failed");
-        if (!c->lo_stream) {
+        hmodel = reinterpret_cast<float *>(static_cast<char *>(pin) + 2 * (in_bytes + out_bytes));
+        if (!limited && !c->lo_stream) {
             HIP_TRY(c, StreamPool::get().stream(&c->lo_stream));
             for (auto &ev : c->lo_ev) HIP_TRY(c, StreamPool::get().event(&ev));
         }
-        hmodel = reinterpret_cast<float *>(static_cast<char *>(pin) + in_bytes + out_bytes);
-        uint32_t *hw = static_cast<uint32_t *>(pin), *dw = c->lo_io.as<uint32_t>();
-        hns = hw;
-        hthr = reinterpret_cast<float *>(hw + W);
-        hslots = hw + 2 * W;
-        hpos = reinterpret_cast<int32_t *>(hw + 3 * W);
-        hmod = reinterpret_cast<float *>(hw + 3 * W + W * L);
-        hok = reinterpret_cast<int32_t *>(hmod + 9 * W);
-        hcnt = hok + W;
-        hsig[0] = reinterpret_cast<float *>(hcnt + W);
-        hsig[1] = hmodel + 16;
-        in_block(0);
-        dmod = reinterpret_cast<float *>(dw + 3 * W + W * L);
-        dok = reinterpret_cast<int32_t *>(dmod + 9 * W);
-        dcnt = dok + W;
-        dsum = reinterpret_cast<float *>(dcnt + W);
+        set_block(0);
         HIP_TRY(c, c->lo_q.reserve(sizeof(float) * c->cols * N * W));
         HIP_TRY(c, c->lo_part.reserve(sizeof(double) * usac::nonminimal_partial_stride(n) * W));
         HIP_TRY(c, c->nm_seq.reserve(usac::nonminimal_seq_bytes(n, (uint32_t)W)));
         HIP_TRY(c, c->lo_ws.reserve(sizeof(float) * 18 * W));
-        HIP_TRY(c, c->lo_scr.reserve(usac::inliers_scratch_bytes(n, wmax)));
+        scr_bytes = usac::inliers_scratch_bytes(n, wmax);
+        HIP_TRY(c, c->lo_scr.reserve(2 * scr_bytes));
         return USAC_OK;
     }
 
-    // device input block b (of two) of a stage: ns, thresholds, slots, LSQ positions
-    void in_block(int b) {
-        const size_t W = wmax;
-        uint32_t *dw = c->lo_io.as<uint32_t>() + (b ? in_bytes + out_bytes : 0) / sizeof(uint32_t);
-        dns = dw;
-        dthr = reinterpret_cast<float *>(dw + W);
-        dslots = dw + 2 * W;
-        dpos = reinterpret_cast<int32_t *>(dw + 3 * W);
+    // the host and device blocks of parity b: inputs then outputs (layout of both)
+    void set_block(int b) {
+        const size_t W = wmax, L = std::max<uint32_t>(1u, limit);
+        auto lay = [&](uint32_t *w, uint32_t *&ns, float *&thr, uint32_t *&slots, int32_t *&pos, float *&mod,
+                       int32_t *&ok, int32_t *&cnt, float *&sum) {
+            ns = w;
+            thr = reinterpret_cast<float *>(w + W);
+            slots = w + 2 * W;
+            pos = reinterpret_cast<int32_t *>(w + 3 * W);
+            mod = reinterpret_cast<float *>(w + 3 * W + W * L);
+            ok = reinterpret_cast<int32_t *>(mod + 9 * W);
+            cnt = ok + W;
+            sum = reinterpret_cast<float *>(cnt + W);
+        };
+        const size_t off = (size_t)b * (in_bytes + out_bytes) / sizeof(uint32_t);
+        lay(static_cast<uint32_t *>(pin) + off, hns, hthr, hslots, hpos, hmod, hok, hcnt, hsum);
+        lay(c->lo_io.as<uint32_t>() + off, dns, dthr, dslots, dpos, dmod, dok, dcnt, dsum);
     }
-    // the Σ of buffer b has arrived: hand it to the chains waiting for it
-    int settle(int b) {
-        if (!sig_live[b]) return USAC_OK;
+    void *scr(int b) const { return static_cast<char *>(c->lo_scr.p) + (size_t)b * scr_bytes; }
+    int poll(hipEvent_t ev) {
         for (uint32_t spins = 0;; spins++) {
-            const hipError_t e = hipEventQuery(c->lo_ev[1 + b]);
-            if (e == hipSuccess) break;
-            if (e != hipErrorNotReady) return fail(c, USAC_ERR_HIP, std::string("LO sums: ") + hipGetErrorString(e));
+            const hipError_t e = hipEventQuery(ev);
+            if (e == hipSuccess) return USAC_OK;
+            if (e != hipErrorNotReady) return fail(c, USAC_ERR_HIP, std::string("LO stage: ") + hipGetErrorString(e));
             if ((spins & 1023u) == 1023u) std::this_thread::yield();
         }
-        for (uint32_t w = 0; w < wmax; w++)
-            if (ch[w].sum_buf == b) {
-                ch[w].lo_sum = hsig[b][w];
-                ch[w].sum_buf = -1;
-            }
-        sig_live[b] = false;
-        return USAC_OK;
     }
-    int settle_all() {
-        const int r = settle(0);
-        return r ? r : settle(1);
-    }
-
     static bool bigger(int c1, float s1, int c2, float s2) { return c1 > c2 || (c1 == c2 && s1 > s2); }
     // chains of this rank: all of them unless the run is sharded.  The limited variant draws
     // inside its iterative stage (one chain, the generator moves), so it is never split.
@@ -871,9 +852,7 @@ struct LoRansac {
             }
         }
         hipStream_t st = c->stream;
-        const int sb = (int)(sig_k & 1u);  // this stage's input block, Σ buffer and Σ event
-        in_block(sb);
-        HIP_TRY(c, hipMemcpyAsync(dns, pin, in_bytes, hipMemcpyHostToDevice, st));
+        HIP_TRY(c, hipMemcpyAsync(dns, hns, in_bytes, hipMemcpyHostToDevice, st));
         if (fit) {
             usac::NmBatch b{};
             b.base = inner_fit ? c->lo_max.as<int32_t>() : c->lo_lists.as<int32_t>();
@@ -893,32 +872,18 @@ struct LoRansac {
             b.seq = c->nm_seq.p;
             HIP_TRY(c, usac::launch_nonminimal_batch(st, c->estimator, c->pts.p, b));
         }
-        // the compaction rewrites the residuals and counts the previous stage's Σ pass reads
-        if (sig_live[sb ^ 1]) HIP_TRY(c, hipStreamWaitEvent(st, c->lo_ev[1 + (sb ^ 1)], 0));
         HIP_TRY(c, usac::launch_inliers_batch(st, c->estimator, c->pts.p, n, dmod, ns, 0.f, dthr, dslots,
-                                              c->lo_lists.as<int32_t>(), n, dcnt, nullptr, c->lo_scr.p,
-                                              fit ? dok : nullptr));
-        HIP_TRY(c, hipMemcpyAsync(hmod, dmod, out_bytes - sizeof(float) * wmax, hipMemcpyDeviceToHost, st));
-        HIP_TRY(c, hipEventRecord(c->lo_ev[0], st));
-        HIP_TRY(c, hipStreamWaitEvent(c->lo_stream, c->lo_ev[0], 0));
-        HIP_TRY(c, usac::launch_inliers_sums(c->lo_stream, n, ns, dslots, dcnt, dsum, c->lo_scr.p));
-        HIP_TRY(c, hipMemcpyAsync(hsig[sb], dsum, sizeof(float) * wmax, hipMemcpyDeviceToHost, c->lo_stream));
-        HIP_TRY(c, hipEventRecord(c->lo_ev[1 + sb], c->lo_stream));
-        sig_live[sb] = true;
-        sig_k++;
+                                              c->lo_lists.as<int32_t>(), n, dcnt, dsum, scr(0), fit ? dok : nullptr));
+        HIP_TRY(c, hipMemcpyAsync(hmod, dmod, out_bytes, hipMemcpyDeviceToHost, st));
         HIP_TRY(c, stream_wait(st));
         stages++;
-        // the previous stage's Σ ran beside this stage's fit; this stage's is needed now only by
-        // a chain whose count ties the best's (GetScoreUnlimited's comparison)
-        int r = settle(sb ^ 1);
-        bool tie = false;
-        for (uint32_t w = 0; w < W && !limited; w++) {
-            const Chain &h = ch[w];
-            if (own(w) && ((h.phase == ITER_FIT && hok[w]) || h.phase == ITER_SCORE) && hcnt[w] == best_cnt) tie = true;
-        }
-        if (!r && tie) r = settle(sb);
-        if (r) return r;
-        cur_sb = sb;
+        take(W, inner_cnt);
+        return USAC_OK;
+    }
+
+    // the chains' state machines take a stage's outputs (host block in use: hmod, hok, hcnt,
+    // hsum, hthr)
+    void take(uint32_t W, int inner_cnt) {
         for (uint32_t w = 0; w < W; w++) {
             Chain &h = ch[w];
             if (!own(w)) continue;
@@ -956,27 +921,17 @@ struct LoRansac {
                     break;
             }
         }
-        return USAC_OK;
     }
-    // a fitted model was scored: lo_lists[w] now holds its inliers at hthr[w]
-    void scored_list(Chain &h, uint32_t w) {
+    // a fitted model was scored: lo_lists[w] now holds its inliers at the chain's threshold
+    // (inner: K * theta, iterative: the already decremented one -- the stage's scoring threshold)
+    void scored_list(Chain &h, uint32_t) {
         memcpy(h.list_model, h.model, sizeof(h.model));
-        h.list_thr = hthr[w];
-    }
-    // a scoring's Σ: at hand if this stage's Σ buffer was settled, else pending
-    int cur_sb = 0;
-    void take_sum(Chain &h, uint32_t w) {
-        if (sig_live[cur_sb]) {
-            h.sum_buf = cur_sb;
-        } else {
-            h.lo_sum = hsig[cur_sb][w];
-            h.sum_buf = -1;
-        }
+        h.list_thr = h.thr;
     }
     // the inner iteration's scoring of lo_model at K * theta
     void inner_scored(Chain &h, uint32_t w) {
         h.lo_cnt = hcnt[w];
-        take_sum(h, w);
+        h.lo_sum = hsum[w];
         if (h.lo_cnt <= (int)m) {
             h.outcome = FEW;
             h.phase = DONE;
@@ -989,7 +944,7 @@ struct LoRansac {
     // an iterative step's scoring of its fit
     void iter_scored(Chain &h, uint32_t w) {
         h.lo_cnt = hcnt[w];
-        take_sum(h, w);  // settled first when the count ties the best's: the comparison reads it
+        h.lo_sum = hsum[w];
         if (!limited && bigger(best_cnt, best_sum, h.lo_cnt, h.lo_sum)) {
             finish(h);  // GetScoreUnlimited: the best is bigger -> break
         } else {
@@ -997,6 +952,106 @@ struct LoRansac {
             h.it++;
             iter_head(h, w);
         }
+    }
+
+    // ---- pipelined rounds (the unlimited variant): stage k + 1 is on the device while the
+    // host reads stage k.  Everything a stage needs is known before stage k's outputs are read
+    // except the point counts of its fits: each chain's threshold follows a fixed schedule
+    // (K * theta_start, then one step less per iterative fit), its list is on the device, and
+    // k_lo_prep derives its n from stage k's outputs on the device -- zero, i.e. a no-op fit
+    // and scoring that leave the chain's list alone, once the chain has certainly stopped
+    // (failed fit, <= m inliers, fewer inliers than the best).  A count tie with the best
+    // needs Σ to decide; the device continues such a chain, and if the host's state machine
+    // (which reads every stage in order, exactly as the sequential stages did) stops it, its
+    // later speculative fits are never read -- a chain stopped by the comparison never
+    // improves the best, so its list is never used either.  The scoring's Σ runs on the side
+    // stream beside the next stage's fit.  The stage after a round's last is usually already
+    // queued: it runs for nothing, ordered before every later use of the LO buffers.
+    int enqueue_pipe(uint32_t k, uint32_t W, int inner_cnt) {
+        const int b = next_par;
+        next_par ^= 1;
+        set_block(b ^ 1);  // the previous stage's device block (k_lo_prep's inputs)
+        const uint32_t *pns = dns;
+        const int32_t *pok = dok, *pcnt = dcnt;
+        const float *pthr = dthr;
+        set_block(b);
+        hipStream_t st = c->stream;
+        const bool pos = k == 0 && inner_cnt > (int)limit;
+        uint32_t nmax = 0;
+        if (k == 0) {  // the round's inner fits: inputs from the host
+            for (uint32_t w = 0; w < W; w++) {
+                hslots[w] = w;
+                hthr[w] = (float)mult * ch[w].thr_start;
+                hns[w] = own(w) ? (pos ? limit : (uint32_t)inner_cnt) : 0u;
+                nmax = std::max(nmax, hns[w]);
+            }
+            HIP_TRY(c, hipMemcpyAsync(dns, hns, in_bytes, hipMemcpyHostToDevice, st));
+        } else {  // iterative fits: inputs derived on the device from the previous stage
+            HIP_TRY(c, usac::launch_lo_prep(st, pns, pok, pcnt, pthr, W, (int32_t)m, best_cnt, k > 1 ? 1 : 0, step,
+                                            dns, dthr));
+        }
+        usac::NmBatch nb{};
+        nb.base = k == 0 ? c->lo_max.as<int32_t>() : c->lo_lists.as<int32_t>();
+        nb.base_stride = k == 0 ? 0 : n;
+        nb.pos = pos ? dpos : nullptr;
+        nb.pos_stride = limit;
+        nb.ns = dns;
+        nb.W = W;
+        nb.nmax = k == 0 ? nmax : n;  // iterative fits: n bounds the counts on the device
+        nb.fused_any = k > 0;
+        nb.q = c->lo_q.p;
+        nb.q_stride = n;
+        nb.partial = c->lo_part.as<double>();
+        nb.p_stride = usac::nonminimal_partial_stride(n);
+        nb.ws = c->lo_ws.as<float>();
+        nb.model_out = dmod;
+        nb.ok = dok;
+        nb.seq = c->nm_seq.p;
+        HIP_TRY(c, usac::launch_nonminimal_batch(st, c->estimator, c->pts.p, nb));
+        HIP_TRY(c, usac::launch_inliers_batch(st, c->estimator, c->pts.p, n, dmod, W, 0.f, dthr, nullptr,
+                                              c->lo_lists.as<int32_t>(), n, dcnt, nullptr, scr(b), dok));
+        // the side stream: Σ, then every output of the stage into the host block
+        HIP_TRY(c, hipEventRecord(c->lo_ev[b], st));
+        HIP_TRY(c, hipStreamWaitEvent(c->lo_stream, c->lo_ev[b], 0));
+        HIP_TRY(c, usac::launch_inliers_sums(c->lo_stream, n, W, nullptr, dcnt, dsum, scr(b)));
+        HIP_TRY(c, hipMemcpyAsync(hmod, dmod, out_bytes, hipMemcpyDeviceToHost, c->lo_stream));
+        HIP_TRY(c, hipEventRecord(c->lo_ev[2 + b], c->lo_stream));
+        return USAC_OK;
+    }
+
+    int round_pipe(uint32_t W, int inner_cnt) {
+        const int b0 = next_par;
+        uint32_t queued = 0;  // stages 0 .. queued - 1 are on the device
+        int r = enqueue_pipe(queued++, W, inner_cnt);
+        if (!r && iters > 0) r = enqueue_pipe(queued++, W, inner_cnt);
+        for (uint32_t k = 0; !r; k++) {
+            const int b = (b0 + (int)k) & 1;
+            if ((r = poll(c->lo_ev[2 + b]))) break;
+            set_block(b);
+            for (uint32_t w = 0; w < W; w++)
+                if (own(w) && (ch[w].phase == INNER_FIT || ch[w].phase == ITER_FIT)) fits++;
+            stages++;
+            take(W, inner_cnt);
+            bool active = false;
+            for (uint32_t w = 0; w < W; w++) active |= own(w) && ch[w].phase != DONE;
+            if (!active) break;
+            // an active chain fits again at stage k + 1 <= iters, which is queued
+            if (queued < k + 2) {
+                r = fail(c, USAC_ERR_HIP, "LO pipeline out of step");
+                break;
+            }
+            if (k + 2 <= iters && queued == k + 2) r = enqueue_pipe(queued++, W, inner_cnt);
+        }
+        // later main-stream users of the LO scratch wait for the side stream's last Σ pass
+        if (!r) {
+            hipError_t e = hipEventRecord(c->lo_ev[4], c->lo_stream);
+            if (e == hipSuccess) e = hipStreamWaitEvent(c->stream, c->lo_ev[4], 0);
+            if (e != hipSuccess) r = fail(c, USAC_ERR_HIP, std::string("LO stage: ") + hipGetErrorString(e));
+        } else {
+            (void)hipStreamSynchronize(c->stream);
+            (void)hipStreamSynchronize(c->lo_stream);
+        }
+        return r;
     }
 
     // GetModelScore(best_model, best_score): model / (cnt, sum) improved in place
@@ -1022,6 +1077,7 @@ struct LoRansac {
             best_cnt = cnt;
             best_sum = sum;
             float t = lo_thr;
+            set_block(limited ? 0 : next_par);  // the round's first stage block (its LSQ positions)
             for (uint32_t w = 0; w < W; w++) {
                 Chain &h = ch[w];
                 h = Chain();
@@ -1035,14 +1091,16 @@ struct LoRansac {
             }
             rounds++;
             int st = USAC_OK;
-            for (;;) {
-                bool active = false;
-                for (uint32_t w = 0; w < W; w++) active |= own(w) && ch[w].phase != DONE;
-                if (!active) break;
-                if ((st = stage(W, cnt))) break;
+            if (!limited) {
+                st = round_pipe(W, cnt);
+            } else {
+                for (;;) {
+                    bool active = false;
+                    for (uint32_t w = 0; w < W; w++) active |= own(w) && ch[w].phase != DONE;
+                    if (!active) break;
+                    if ((st = stage(W, cnt))) break;
+                }
             }
-            if (!st) st = settle_all();  // every chain's Σ before the exchange and the replay
-            else (void)hipStreamSynchronize(c->lo_stream);
             if (sh.nranks > 1 && !limited) {  // every rank's chains, one all-gather per round
                 std::vector<uint8_t> all;
                 if ((rc = shard_allgather(c, sh, st, ch.data(), sizeof(Chain) * W, all))) return;

@@ -33,8 +33,8 @@ struct DevSampler {
 // Grid neighbours on the device (kernels_grid.hip): CSR bit-identical to usac_host.hpp's
 // GridNeighbors -- cell[n] (first-appearance numbering), rank[n], start[n_cells + 1],
 // members[n] -- plus eligible[] = points with >= m neighbours, ascending.  cmin = the lowest
-// cell of the dataset box per dimension (every cell - cmin must fit 16 bits).  Synchronises
-// `st` twice (cell and eligible counts).
+// cell of the dataset box per dimension, bits = each dimension's key width (its cell range
+// plus an out-of-box sentinel; <= 63 bits in all).  Synchronises `st` once (the counts).
 size_t grid_workspace_bytes(uint32_t n);
 hipError_t build_grid(hipStream_t st, const float4 *pts, uint32_t n, int cell_size, int4 cmin, int4 bits, uint32_t m,
                       void *ws, uint32_t *cell, uint32_t *rank, uint32_t *start, int32_t *members, int32_t *eligible,
@@ -142,6 +142,14 @@ hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, 
 hipError_t launch_inliers_sums(hipStream_t st, uint32_t n, uint32_t W, const uint32_t *slots, const int32_t *counts,
                                float *sums, void *scratch);
 size_t inliers_scratch_bytes(uint32_t n, uint32_t W);
+// LO pipelined stages (usac_api.cpp LoRansac): the next iterative stage's inputs from the
+// previous stage's, on the device.  ns[w] = cnt[w] while chain w may continue -- it was
+// fitted (ns_prev > 0), its fit succeeded, it kept more than m inliers and (after an
+// iterative step) not fewer than the best's count -- else 0 (the chain's fit and scoring
+// become no-ops that leave its list alone); thr[w] = thr_prev[w] - step
+hipError_t launch_lo_prep(hipStream_t st, const uint32_t *ns_prev, const int32_t *ok_prev, const int32_t *cnt_prev,
+                          const float *thr_prev, uint32_t W, int32_t m, int32_t best_cnt, int compare, float step,
+                          uint32_t *ns, float *thr);
 // every point's exact residual under one model (n floats)
 hipError_t launch_point_errors(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *model,
                                float *errors);
@@ -181,6 +189,9 @@ struct NmBatch {
     // qw = W x q_stride float4 scratch for the weighted points
     const float *weights;
     void *qw;
+    // nmax is only a bound on ns (e.g. counts known on the device alone): take the fused
+    // gather + segment-sum path whatever its size (the results do not depend on the path)
+    bool fused_any;
 };
 hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pts, const NmBatch &b);
 size_t nonminimal_partial_stride(uint32_t nmax);
