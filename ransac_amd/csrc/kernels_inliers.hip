@@ -221,24 +221,4 @@ hipError_t launch_inliers(hipStream_t st, int estimator, const void *pts, uint32
 
 size_t inliers_scratch_bytes(uint32_t n, uint32_t W) { return sizeof(uint32_t) * inl_stride(n) * W; }
 
-__global__ __launch_bounds__(64) void k_lo_prep(const uint32_t *__restrict__ ns_prev, const int32_t *__restrict__ ok_prev,
-                                                const int32_t *__restrict__ cnt_prev, const float *__restrict__ thr_prev,
-                                                uint32_t W, int32_t m, int32_t best_cnt, int compare, float step,
-                                                uint32_t *__restrict__ ns, float *__restrict__ thr) {
-    for (uint32_t w = threadIdx.x; w < W; w += 64) {
-        const int32_t c = cnt_prev[w];
-        const bool go = ns_prev[w] > 0 && ok_prev[w] && c > m && (!compare || c >= best_cnt);
-        ns[w] = go ? (uint32_t)c : 0u;
-        thr[w] = thr_prev[w] - step;  // the host's `thr -= step` (fp32, no contraction)
-    }
-}
-
-hipError_t launch_lo_prep(hipStream_t st, const uint32_t *ns_prev, const int32_t *ok_prev, const int32_t *cnt_prev,
-                          const float *thr_prev, uint32_t W, int32_t m, int32_t best_cnt, int compare, float step,
-                          uint32_t *ns, float *thr) {
-    hipLaunchKernelGGL(k_lo_prep, dim3(1), dim3(64), 0, st, ns_prev, ok_prev, cnt_prev, thr_prev, W, m, best_cnt,
-                       compare, step, ns, thr);
-    return hipGetLastError();
-}
-
 }  // namespace usac

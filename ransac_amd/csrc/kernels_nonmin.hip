@@ -49,10 +49,22 @@ __global__ __launch_bounds__(256) void k_gather_psum4(const float4 *__restrict__
                                                       size_t base_stride, const int32_t *__restrict__ pos,
                                                       size_t pos_stride, const uint32_t *__restrict__ ns, uint32_t n1,
                                                       float4 *__restrict__ q_all, size_t q_stride, char *seq_all,
-                                                      size_t sstride) {
+                                                      size_t sstride, LoPrep prep, int has_prep) {
     __shared__ double red[4][256];
     const uint32_t j = blockIdx.x, w = blockIdx.y;
-    const uint32_t n = ns ? ns[w] : n1, L = seq::seg_len(n);
+    uint32_t n;
+    if (has_prep) {  // every segment of fit w derives the same n; segment 0 publishes it
+        const int32_t c = prep.cnt_prev[w];
+        const bool go = prep.ns_prev[w] > 0 && prep.ok_prev[w] && c > prep.m && (!prep.compare || c >= prep.best_cnt);
+        n = go ? (uint32_t)c : 0u;
+        if (j == 0 && threadIdx.x == 0) {
+            prep.ns[w] = n;
+            prep.thr[w] = prep.thr_prev[w] - prep.step;  // the host's `thr -= step` (fp32)
+        }
+    } else {
+        n = ns ? ns[w] : n1;
+    }
+    const uint32_t L = seq::seg_len(n);
     if (j * L >= n) return;
     const uint32_t e = (j + 1) * L < n ? (j + 1) * L : n;
     const int32_t *list = base + w * base_stride;
@@ -89,6 +101,17 @@ __global__ __launch_bounds__(256) void k_gather_psum4(const float4 *__restrict__
     if (threadIdx.x < 4) reinterpret_cast<double *>(seq_all + w * sstride)[j * 4 + threadIdx.x] = red[threadIdx.x][0];
 }
 constexpr uint32_t kFusedGatherMax = 64 * 1024;  // up to 8 points per thread and segment
+
+// the pipelined LO stages' count / threshold derivation (LoPrep) on its own, for the fit paths
+// without the fused gather
+__global__ __launch_bounds__(64) void k_lo_prep(LoPrep p, uint32_t W) {
+    for (uint32_t w = threadIdx.x; w < W; w += 64) {
+        const int32_t c = p.cnt_prev[w];
+        const bool go = p.ns_prev[w] > 0 && p.ok_prev[w] && c > p.m && (!p.compare || c >= p.best_cnt);
+        p.ns[w] = go ? (uint32_t)c : 0u;
+        p.thr[w] = p.thr_prev[w] - p.step;
+    }
+}
 
 // normalizing transformation (GetNormalizingTransformation, normalizing_transformation.cpp:
 // 7-113): the four coordinate means and the two average distances are the reference's
@@ -266,13 +289,19 @@ __global__ __launch_bounds__(64) void k_ata_partial(const float4 *__restrict__ q
                                                     float *__restrict__ ws_all) {
     const uint32_t w = blockIdx.z;
     const uint32_t n = ns ? ns[w] : n1;
+    // workgroup-uniform: past the fit's points (the grid is sized for a bound on n), or a
+    // system the finish solves from the points themselves; workgroup (0, 0) still writes the
+    // fit's transforms
+    const bool idle = (FUND ? n <= 8 : 2 * n <= 9) || blockIdx.x * 64 * kAtaBlock >= n;
+    const bool writer = blockIdx.x == 0 && blockIdx.y == 0;
+    if (idle && !writer) return;
     float t1[9], t2[9];
     norm_transforms(sums4, dsum2, w, n, t1, t2);
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 9) {
+    if (writer && threadIdx.x < 9) {
         ws_all[18 * w + threadIdx.x] = t1[threadIdx.x];
         ws_all[18 * w + 9 + threadIdx.x] = t2[threadIdx.x];
     }
-    if ((FUND ? n <= 8 : 2 * n <= 9) || blockIdx.x * 64 * kAtaBlock >= n) return;  // workgroup-uniform
+    if (idle) return;
     __shared__ double red[64][kAtaPer + 1];
     const uint32_t blk = blockIdx.x * 64 + threadIdx.x;
     double acc[kAtaPer];
@@ -749,6 +778,13 @@ __global__ __launch_bounds__(64) void k_line_pca(const float2 *__restrict__ q_al
 // which differs only in the normalising transformation.
 hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pts, const NmBatch &b) {
     if (b.W == 0) return hipSuccess;
+    // pipelined LO stages: the fused gather derives the counts; the other paths first run the
+    // derivation on its own (line fits; b.ns is the prep's output)
+    if (b.prep && (estimator == USAC_LINE2D || b.weights)) {
+        hipLaunchKernelGGL(k_lo_prep, dim3(1), dim3(64), 0, st, *b.prep, b.W);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     const dim3 gg((b.nmax + 255) / 256 ? (b.nmax + 255) / 256 : 1, b.W);
     if (estimator == USAC_LINE2D) {
         if (b.weights) return hipErrorInvalidValue;  // the reference has no weighted line fit
@@ -759,7 +795,7 @@ hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pt
         return hipGetLastError();
     }
     float4 *q = static_cast<float4 *>(b.q);
-    if (b.nmax <= kSmallFit && !b.weights) {  // every fit in one workgroup, one launch
+    if (b.nmax <= kSmallFit && !b.weights && !b.prep) {  // every fit in one workgroup, one launch
         if (estimator == USAC_HOMOGRAPHY)
             hipLaunchKernelGGL(k_fit_small<false>, dim3(b.W), dim3(64), 0, st, static_cast<const float4 *>(pts), b.base,
                                b.base_stride, b.pos, b.pos_stride, b.ns, b.n1, b.ws, b.model_out, b.ok);
@@ -785,11 +821,11 @@ hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pt
         char *seq = static_cast<char *>(b.seq);
         const size_t ss = seq_stride(b.nmax);
         float *sums4 = reinterpret_cast<float *>(seq + b.W * ss), *dsum2 = sums4 + 4 * b.W;
-        const bool fused = b.fused_any || b.nmax <= kFusedGatherMax;
+        const bool fused = b.fused_any || b.prep || b.nmax <= kFusedGatherMax;
         if (fused)
             hipLaunchKernelGGL(k_gather_psum4, dim3(seq::kSegMax, b.W), dim3(256), 0, st,
                                static_cast<const float4 *>(pts), b.base, b.base_stride, b.pos, b.pos_stride, b.ns,
-                               b.n1, q, b.q_stride, seq, ss);
+                               b.n1, q, b.q_stride, seq, ss, b.prep ? *b.prep : LoPrep{}, b.prep ? 1 : 0);
         else
             hipLaunchKernelGGL(k_gather<float4>, gg, dim3(256), 0, st, static_cast<const float4 *>(pts), b.base,
                                b.base_stride, b.pos, b.pos_stride, b.ns, b.n1, q, b.q_stride);

@@ -958,7 +958,7 @@ struct LoRansac {
     // host reads stage k.  Everything a stage needs is known before stage k's outputs are read
     // except the point counts of its fits: each chain's threshold follows a fixed schedule
     // (K * theta_start, then one step less per iterative fit), its list is on the device, and
-    // k_lo_prep derives its n from stage k's outputs on the device -- zero, i.e. a no-op fit
+    // the fit's gather derives its n from stage k's outputs on the device -- zero, a no-op fit
     // and scoring that leave the chain's list alone, once the chain has certainly stopped
     // (failed fit, <= m inliers, fewer inliers than the best).  A count tie with the best
     // needs Σ to decide; the device continues such a chain, and if the host's state machine
@@ -970,7 +970,7 @@ struct LoRansac {
     int enqueue_pipe(uint32_t k, uint32_t W, int inner_cnt) {
         const int b = next_par;
         next_par ^= 1;
-        set_block(b ^ 1);  // the previous stage's device block (k_lo_prep's inputs)
+        set_block(b ^ 1);  // the previous stage's device block (the count derivation's inputs)
         const uint32_t *pns = dns;
         const int32_t *pok = dok, *pcnt = dcnt;
         const float *pthr = dthr;
@@ -986,10 +986,10 @@ struct LoRansac {
                 nmax = std::max(nmax, hns[w]);
             }
             HIP_TRY(c, hipMemcpyAsync(dns, hns, in_bytes, hipMemcpyHostToDevice, st));
-        } else {  // iterative fits: inputs derived on the device from the previous stage
-            HIP_TRY(c, usac::launch_lo_prep(st, pns, pok, pcnt, pthr, W, (int32_t)m, best_cnt, k > 1 ? 1 : 0, step,
-                                            dns, dthr));
         }
+        // iterative fits: counts and thresholds derived on the device from the previous stage
+        // (by the fit's first kernel)
+        const usac::LoPrep prep{pns, pok, pcnt, pthr, dns, dthr, (int32_t)m, best_cnt, k > 1 ? 1 : 0, step};
         usac::NmBatch nb{};
         nb.base = k == 0 ? c->lo_max.as<int32_t>() : c->lo_lists.as<int32_t>();
         nb.base_stride = k == 0 ? 0 : n;
@@ -999,6 +999,7 @@ struct LoRansac {
         nb.W = W;
         nb.nmax = k == 0 ? nmax : n;  // iterative fits: n bounds the counts on the device
         nb.fused_any = k > 0;
+        nb.prep = k > 0 ? &prep : nullptr;
         nb.q = c->lo_q.p;
         nb.q_stride = n;
         nb.partial = c->lo_part.as<double>();

@@ -142,14 +142,6 @@ hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, 
 hipError_t launch_inliers_sums(hipStream_t st, uint32_t n, uint32_t W, const uint32_t *slots, const int32_t *counts,
                                float *sums, void *scratch);
 size_t inliers_scratch_bytes(uint32_t n, uint32_t W);
-// LO pipelined stages (usac_api.cpp LoRansac): the next iterative stage's inputs from the
-// previous stage's, on the device.  ns[w] = cnt[w] while chain w may continue -- it was
-// fitted (ns_prev > 0), its fit succeeded, it kept more than m inliers and (after an
-// iterative step) not fewer than the best's count -- else 0 (the chain's fit and scoring
-// become no-ops that leave its list alone); thr[w] = thr_prev[w] - step
-hipError_t launch_lo_prep(hipStream_t st, const uint32_t *ns_prev, const int32_t *ok_prev, const int32_t *cnt_prev,
-                          const float *thr_prev, uint32_t W, int32_t m, int32_t best_cnt, int compare, float step,
-                          uint32_t *ns, float *thr);
 // every point's exact residual under one model (n floats)
 hipError_t launch_point_errors(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *model,
                                float *errors);
@@ -192,6 +184,23 @@ struct NmBatch {
     // nmax is only a bound on ns (e.g. counts known on the device alone): take the fused
     // gather + segment-sum path whatever its size (the results do not depend on the path)
     bool fused_any;
+    // LO pipelined stages (usac_api.cpp LoRansac; nullable, implies fused_any): the fits' point
+    // counts and the stage's thresholds from the previous stage's outputs, computed by the
+    // gather itself (see LoPrep) and written to ns (then read by every later kernel) / thr
+    const struct LoPrep *prep;
+};
+// ns[w] = cnt[w] while chain w may continue -- it was fitted (ns_prev > 0), its fit
+// succeeded, it kept more than m inliers and (compare: after an iterative step) not fewer
+// than the best's count -- else 0 (the chain's fit and scoring become no-ops that leave its
+// list alone); thr[w] = thr_prev[w] - step
+struct LoPrep {
+    const uint32_t *ns_prev;
+    const int32_t *ok_prev, *cnt_prev;
+    const float *thr_prev;
+    uint32_t *ns;
+    float *thr;
+    int32_t m, best_cnt, compare;
+    float step;
 };
 hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pts, const NmBatch &b);
 size_t nonminimal_partial_stride(uint32_t nmax);
