@@ -229,6 +229,7 @@ __device__ __forceinline__ NormXf norm_xf(const float *t1, const float *t2) {
 // grouping only spreads the entries over lanes).  FUND: one 8-point row per correspondence
 // (eight_points.cpp:26-45), else two DLT rows.
 constexpr int kAtaGroups = 5;                  // 45 = 5 x 9 entries
+constexpr uint32_t kAtaGridBound = 8;          // superblock workgroups per fit at most, for a bound nmax
 constexpr int kAtaPer = 45 / kAtaGroups;
 
 template <bool FUND, int G>
@@ -289,7 +290,8 @@ __global__ __launch_bounds__(64) void k_ata_partial(const float4 *__restrict__ q
                                                     float *__restrict__ ws_all) {
     const uint32_t w = blockIdx.z;
     const uint32_t n = ns ? ns[w] : n1;
-    // workgroup-uniform: past the fit's points (the grid is sized for a bound on n), or a
+    // workgroup-uniform: no superblock of this workgroup within the fit's points (the grid is
+    // sized for a bound on n; workgroup x takes superblocks x, x + gridDim.x, ...), or a
     // system the finish solves from the points themselves; workgroup (0, 0) still writes the
     // fit's transforms
     const bool idle = (FUND ? n <= 8 : 2 * n <= 9) || blockIdx.x * 64 * kAtaBlock >= n;
@@ -303,24 +305,28 @@ __global__ __launch_bounds__(64) void k_ata_partial(const float4 *__restrict__ q
     }
     if (idle) return;
     __shared__ double red[64][kAtaPer + 1];
-    const uint32_t blk = blockIdx.x * 64 + threadIdx.x;
-    double acc[kAtaPer];
-    if (blk * kAtaBlock < n) {
-        const NormXf xf = norm_xf(t1, t2);
-        const float4 *q = q_all + w * q_stride;
-        const uint32_t b0 = blk * kAtaBlock;
-        const uint32_t b1 = b0 + kAtaBlock < n ? b0 + kAtaBlock : n;
-        ata_dispatch<FUND>((int)blockIdx.y, q, xf, b0, b1, acc);
+    const NormXf xf = norm_xf(t1, t2);
+    const float4 *q = q_all + w * q_stride;
+    const uint32_t nblocks = (n + kAtaBlock - 1) / kAtaBlock;
+    for (uint32_t sb = blockIdx.x; sb * 64 * kAtaBlock < n; sb += gridDim.x) {
+        const uint32_t blk = sb * 64 + threadIdx.x;
+        double acc[kAtaPer];
+        if (blk * kAtaBlock < n) {
+            const uint32_t b0 = blk * kAtaBlock;
+            const uint32_t b1 = b0 + kAtaBlock < n ? b0 + kAtaBlock : n;
+            ata_dispatch<FUND>((int)blockIdx.y, q, xf, b0, b1, acc);
 #pragma unroll
-        for (int e = 0; e < kAtaPer; e++) red[threadIdx.x][e] = acc[e];
-    }
-    __syncthreads();
-    if (threadIdx.x < kAtaPer) {  // superblock sum, blocks in order
-        const uint32_t nblocks = (n + kAtaBlock - 1) / kAtaBlock, first = blockIdx.x * 64;
-        const uint32_t nb = nblocks - first < 64 ? nblocks - first : 64;
-        double sum = 0.0;
-        for (uint32_t b = 0; b < nb; b++) sum += red[b][threadIdx.x];
-        partial_all[w * p_stride + (size_t)blockIdx.x * 45 + kAtaPer * blockIdx.y + threadIdx.x] = sum;
+            for (int e = 0; e < kAtaPer; e++) red[threadIdx.x][e] = acc[e];
+        }
+        __syncthreads();
+        if (threadIdx.x < kAtaPer) {  // superblock sum, blocks in order
+            const uint32_t first = sb * 64;
+            const uint32_t nb = nblocks - first < 64 ? nblocks - first : 64;
+            double sum = 0.0;
+            for (uint32_t b = 0; b < nb; b++) sum += red[b][threadIdx.x];
+            partial_all[w * p_stride + (size_t)sb * 45 + kAtaPer * blockIdx.y + threadIdx.x] = sum;
+        }
+        __syncthreads();  // red is reused by the next superblock
     }
 }
 
@@ -840,7 +846,11 @@ hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pt
     const char *seq = static_cast<const char *>(b.seq);
     const float *sums4 = reinterpret_cast<const float *>(seq + b.W * seq_stride(b.nmax)), *dsum2 = sums4 + 4 * b.W;
     const uint32_t nblk = (b.nmax + kAtaBlock - 1) / kAtaBlock;
-    const dim3 ga(nblk ? (nblk + 63) / 64 : 1, kAtaGroups, b.W);
+    // one workgroup per 4096-point superblock; when nmax is only a bound (pipelined LO stages)
+    // at most kAtaGridBound of them per fit, each looping over superblocks
+    uint32_t gx = nblk ? (nblk + 63) / 64 : 1;
+    if (b.prep && gx > kAtaGridBound) gx = kAtaGridBound;
+    const dim3 ga(gx, kAtaGroups, b.W);
     if (estimator == USAC_HOMOGRAPHY) {
         hipLaunchKernelGGL(k_ata_partial<false>, ga, dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial, b.p_stride,
                            sums4, dsum2, b.ws);
