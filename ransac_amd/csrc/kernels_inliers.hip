@@ -19,7 +19,9 @@
 
 namespace usac {
 
-constexpr uint32_t kInlBlock = 256;
+constexpr uint32_t kInlThreads = 256;               // threads per workgroup
+constexpr uint32_t kInlPer = 4;                     // points per thread
+constexpr uint32_t kInlBlock = kInlThreads * kInlPer;  // points per workgroup (block)
 
 template <int EST>
 __device__ __forceinline__ float inl_error(const float *m, const void *pts, uint32_t i) {
@@ -65,15 +67,17 @@ __host__ __device__ __forceinline__ size_t inl_stride(uint32_t n) { return inl_r
 // model slot of workgroup row b: slots[b] when a slot list is given (a subset of the W models)
 __device__ __forceinline__ uint32_t inl_slot(const uint32_t *slots, uint32_t b) { return slots ? slots[b] : b; }
 
+// Blocks of kInlBlock points in point order: thread t of block b takes points
+// b * kInlBlock + u * kInlThreads + t, u = 0 .. kInlPer - 1, so (u, wave, lane) is point order.
 template <int EST>
-__global__ __launch_bounds__(kInlBlock) void k_inl_flags(const void *__restrict__ pts, uint32_t n,
-                                                         const float *__restrict__ models, float thr,
-                                                         const float *__restrict__ thrs,
-                                                         const uint32_t *__restrict__ slots,
-                                                         uint32_t *__restrict__ scratch,
-                                                         const int32_t *__restrict__ ok) {
+__global__ __launch_bounds__(kInlThreads) void k_inl_flags(const void *__restrict__ pts, uint32_t n,
+                                                           const float *__restrict__ models, float thr,
+                                                           const float *__restrict__ thrs,
+                                                           const uint32_t *__restrict__ slots,
+                                                           uint32_t *__restrict__ scratch,
+                                                           const int32_t *__restrict__ ok) {
     __shared__ float sm[18];
-    __shared__ uint32_t wsum[kInlBlock / 64];
+    __shared__ uint32_t wsum[kInlThreads / 64];
     const uint32_t w = inl_slot(slots, blockIdx.y);
     if (ok && !ok[w]) return;  // a failed fit: k_inl_compact skips the slot too
     inl_model<EST>(models + 9 * (size_t)w, sm);
@@ -81,28 +85,32 @@ __global__ __launch_bounds__(kInlBlock) void k_inl_flags(const void *__restrict_
     float m[18];
 #pragma unroll
     for (int k = 0; k < 18; k++) m[k] = sm[k];
-    const uint32_t i = blockIdx.x * kInlBlock + threadIdx.x;
-    const bool in = i < n && inl_error<EST>(m, pts, i) < t;
-    const uint64_t bal = __ballot(in);
-    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = (uint32_t)__popcll(bal);
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < kInlPer; u++) {
+        const uint32_t i = blockIdx.x * kInlBlock + u * kInlThreads + threadIdx.x;
+        const bool in = i < n && inl_error<EST>(m, pts, i) < t;
+        cnt += (uint32_t)__popcll(__ballot(in));
+    }
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = cnt;
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t tot = 0;
-        for (uint32_t w = 0; w < kInlBlock / 64; w++) tot += wsum[w];
+        for (uint32_t v = 0; v < kInlThreads / 64; v++) tot += wsum[v];
         scratch[w * inl_stride(n) + blockIdx.x] = tot;
     }
 }
 
 template <int EST>
-__global__ __launch_bounds__(kInlBlock) void k_inl_compact(const void *__restrict__ pts, uint32_t n,
-                                                           const float *__restrict__ models, float thr,
-                                                           const float *__restrict__ thrs,
-                                                           const uint32_t *__restrict__ slots,
-                                                           uint32_t *__restrict__ scratch, int32_t *__restrict__ idx,
-                                                           size_t idx_stride, const int32_t *__restrict__ ok,
-                                                           int32_t *__restrict__ totals) {
+__global__ __launch_bounds__(kInlThreads) void k_inl_compact(const void *__restrict__ pts, uint32_t n,
+                                                             const float *__restrict__ models, float thr,
+                                                             const float *__restrict__ thrs,
+                                                             const uint32_t *__restrict__ slots,
+                                                             uint32_t *__restrict__ scratch, int32_t *__restrict__ idx,
+                                                             size_t idx_stride, const int32_t *__restrict__ ok,
+                                                             int32_t *__restrict__ totals) {
     __shared__ float sm[18];
-    __shared__ uint32_t wsum[kInlBlock / 64], wpre[kInlBlock / 64];
+    __shared__ uint32_t wsum[kInlPer][kInlThreads / 64], wpre[kInlThreads / 64];
     const uint32_t ws = inl_slot(slots, blockIdx.y);
     if (ok && !ok[ws]) {  // a failed fit: its list is left as it was (workgroup-uniform) and its
         // count reads 0, so the Σ pass over this slot (launch_seqsum) sums nothing
@@ -118,32 +126,41 @@ __global__ __launch_bounds__(kInlBlock) void k_inl_compact(const void *__restric
     const uint32_t nb = (n + kInlBlock - 1) / kInlBlock;
     const uint32_t *block_counts = scratch + ws * stride;
     float *errs = reinterpret_cast<float *>(scratch + ws * stride + ((nb + 63) & ~63u));
-    const uint32_t i = blockIdx.x * kInlBlock + threadIdx.x;
-    const float e = i < n ? inl_error<EST>(m, pts, i) : 0.f;
-    const bool in = i < n && e < t;
-    const uint64_t bal = __ballot(in);
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) wsum[wave] = (uint32_t)__popcll(bal);
-    __syncthreads();
+    float e[kInlPer];
+    uint64_t bal[kInlPer];
+#pragma unroll
+    for (uint32_t u = 0; u < kInlPer; u++) {
+        const uint32_t i = blockIdx.x * kInlBlock + u * kInlThreads + threadIdx.x;
+        e[u] = i < n ? inl_error<EST>(m, pts, i) : 0.f;
+        bal[u] = __ballot(i < n && e[u] < t);
+        if (lane == 0) wsum[u][wave] = (uint32_t)__popcll(bal[u]);
+    }
     // this block's output offset: the sum of the earlier blocks' counts (k_inl_flags), summed
     // here (integers: any order) -- no separate scan launch; the last block writes the total
     uint32_t pre = 0;
-    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += kInlBlock) pre += block_counts[b];
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += kInlThreads) pre += block_counts[b];
     for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o);
     if (lane == 0) wpre[wave] = pre;
     __syncthreads();
     uint32_t base = 0;
-    for (uint32_t w = 0; w < kInlBlock / 64; w++) base += wpre[w];
+    for (uint32_t v = 0; v < kInlThreads / 64; v++) base += wpre[v];
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
         uint32_t tot = base;
-        for (uint32_t w = 0; w < kInlBlock / 64; w++) tot += wsum[w];
+        for (uint32_t u = 0; u < kInlPer; u++)
+            for (uint32_t v = 0; v < kInlThreads / 64; v++) tot += wsum[u][v];
         totals[ws] = (int32_t)tot;
     }
-    for (uint32_t w = 0; w < wave; w++) base += wsum[w];
-    if (in) {
-        const uint32_t r = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
-        if (idx) idx[ws * idx_stride + r] = (int32_t)i;
-        errs[r] = e;
+#pragma unroll
+    for (uint32_t u = 0; u < kInlPer; u++) {
+        uint32_t r = base;
+        for (uint32_t v = 0; v < wave; v++) r += wsum[u][v];
+        if ((bal[u] >> lane) & 1ull) {
+            r += (uint32_t)__popcll(bal[u] & ((1ull << lane) - 1));
+            if (idx) idx[ws * idx_stride + r] = (int32_t)(blockIdx.x * kInlBlock + u * kInlThreads + threadIdx.x);
+            errs[r] = e[u];
+        }
+        for (uint32_t v = 0; v < kInlThreads / 64; v++) base += wsum[u][v];
     }
 }
 
@@ -156,8 +173,8 @@ hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, 
     const dim3 grid(nb, W);
 #define INL(E)                                                                                                   \
     do {                                                                                                         \
-        hipLaunchKernelGGL(k_inl_flags<E>, grid, dim3(kInlBlock), 0, st, pts, n, models, thr, thrs, slots, scr, ok);    \
-        hipLaunchKernelGGL(k_inl_compact<E>, grid, dim3(kInlBlock), 0, st, pts, n, models, thr, thrs, slots, scr, \
+        hipLaunchKernelGGL(k_inl_flags<E>, grid, dim3(kInlThreads), 0, st, pts, n, models, thr, thrs, slots, scr, ok);  \
+        hipLaunchKernelGGL(k_inl_compact<E>, grid, dim3(kInlThreads), 0, st, pts, n, models, thr, thrs, slots, scr, \
                            idx, idx_stride, ok, counts);                                                         \
     } while (0)
     switch (estimator) {
@@ -189,7 +206,7 @@ hipError_t launch_inliers_sums(hipStream_t st, uint32_t n, uint32_t W, const uin
 // every point's exact residual under one model (Estimator::GetError, e.g. for the graph-cut
 // LO's energies, graphcut.cpp:17-28)
 template <int EST>
-__global__ __launch_bounds__(kInlBlock) void k_point_errors(const void *__restrict__ pts, uint32_t n,
+__global__ __launch_bounds__(kInlThreads) void k_point_errors(const void *__restrict__ pts, uint32_t n,
                                                             const float *__restrict__ model,
                                                             float *__restrict__ errors) {
     __shared__ float sm[18];
@@ -197,18 +214,18 @@ __global__ __launch_bounds__(kInlBlock) void k_point_errors(const void *__restri
     float m[18];
 #pragma unroll
     for (int k = 0; k < 18; k++) m[k] = sm[k];
-    const uint32_t i = blockIdx.x * kInlBlock + threadIdx.x;
+    const uint32_t i = blockIdx.x * kInlThreads + threadIdx.x;
     if (i < n) errors[i] = inl_error<EST>(m, pts, i);
 }
 
 hipError_t launch_point_errors(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *model,
                                float *errors) {
-    const dim3 grid((n + kInlBlock - 1) / kInlBlock);
+    const dim3 grid((n + kInlThreads - 1) / kInlThreads);
     switch (estimator) {
-        case USAC_LINE2D: hipLaunchKernelGGL(k_point_errors<USAC_LINE2D>, grid, dim3(kInlBlock), 0, st, pts, n, model, errors); break;
-        case USAC_HOMOGRAPHY: hipLaunchKernelGGL(k_point_errors<USAC_HOMOGRAPHY>, grid, dim3(kInlBlock), 0, st, pts, n, model, errors); break;
-        case USAC_FUNDAMENTAL: hipLaunchKernelGGL(k_point_errors<USAC_FUNDAMENTAL>, grid, dim3(kInlBlock), 0, st, pts, n, model, errors); break;
-        case USAC_ESSENTIAL: hipLaunchKernelGGL(k_point_errors<USAC_ESSENTIAL>, grid, dim3(kInlBlock), 0, st, pts, n, model, errors); break;
+        case USAC_LINE2D: hipLaunchKernelGGL(k_point_errors<USAC_LINE2D>, grid, dim3(kInlThreads), 0, st, pts, n, model, errors); break;
+        case USAC_HOMOGRAPHY: hipLaunchKernelGGL(k_point_errors<USAC_HOMOGRAPHY>, grid, dim3(kInlThreads), 0, st, pts, n, model, errors); break;
+        case USAC_FUNDAMENTAL: hipLaunchKernelGGL(k_point_errors<USAC_FUNDAMENTAL>, grid, dim3(kInlThreads), 0, st, pts, n, model, errors); break;
+        case USAC_ESSENTIAL: hipLaunchKernelGGL(k_point_errors<USAC_ESSENTIAL>, grid, dim3(kInlThreads), 0, st, pts, n, model, errors); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

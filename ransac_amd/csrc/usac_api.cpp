@@ -430,8 +430,15 @@ int download_grid(usac_ctx *c, int cs, std::unique_ptr<usac::GridNeighbors> &out
     // DMA into one pinned block, then into the host vectors (the sampler reads them at random:
     // they should be cache-warm, which DMA-written pinned memory is not)
     const size_t n = c->n, nc1 = (size_t)c->grid_n_cells + 1;
-    pinned_vector<uint32_t> stage(3 * n + nc1);
-    uint32_t *w = stage.data();
+    // (a raw pooled block: a pinned_vector would zero-fill the 1.2 MB first)
+    size_t got = 0;
+    uint32_t *w = static_cast<uint32_t *>(PinnedPool::get().take(sizeof(uint32_t) * (3 * n + nc1), &got));
+    if (!w) return fail(c, USAC_ERR_HIP, "pinned host allocation failed");
+    struct Back {
+        void *p;
+        size_t b;
+        ~Back() { PinnedPool::get().give_back(p, b); }
+    } back{w, got};
     HIP_TRY(c, hipMemcpyAsync(w, c->grid_cell.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipMemcpyAsync(w + n, c->grid_rank.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipMemcpyAsync(w + 2 * n, c->grid_members.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
