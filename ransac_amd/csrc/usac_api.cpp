@@ -205,6 +205,16 @@ struct PinnedAlloc {
         return static_cast<T *>(p);
     }
     void deallocate(T *p, size_t k) { PinnedPool::get().give_back(p, DevPool::size_class(sizeof(T) * (k ? k : 1))); }
+    // default-initialise (no zero fill of staging that a copy overwrites anyway); explicit
+    // values as usual
+    template <class U>
+    void construct(U *p) noexcept {
+        ::new (static_cast<void *>(p)) U;
+    }
+    template <class U, class... A>
+    void construct(U *p, A &&...a) {
+        ::new (static_cast<void *>(p)) U(std::forward<A>(a)...);
+    }
     template <class U>
     bool operator==(const PinnedAlloc<U> &) const { return true; }
     template <class U>
@@ -256,7 +266,12 @@ struct usac_ctx {
         lo_ws, lo_scr;
     DevBuf knn_idx, knn_d2;  // KNN neighbour table (usac_knn, NAPSAC KNN)
     // grid neighbours (build_grid): CSR of the cells of size grid_cs, NAPSAC-eligible points
-    DevBuf grid_cell, grid_rank, grid_start, grid_members, grid_elig, grid_ws;
+    // grid CSR in one block, downloaded by one copy: cell[n], rank[n], members[n], start[n + 1]
+    DevBuf grid_csr, grid_elig, grid_ws;
+    uint32_t *grid_cell() const { return grid_csr.as<uint32_t>(); }
+    uint32_t *grid_rank() const { return grid_csr.as<uint32_t>() + n; }
+    int32_t *grid_members() const { return reinterpret_cast<int32_t *>(grid_csr.as<uint32_t>() + 2 * (size_t)n); }
+    uint32_t *grid_start() const { return grid_csr.as<uint32_t>() + 3 * (size_t)n; }
     int grid_cs = 0;        // cell size the grid was built for (0 = none)
     int cell_size = 50;     // model.hpp:43, the device NAPSAC sampler's grid
     uint32_t grid_n_cells = 0, grid_n_elig = 0;
@@ -372,10 +387,10 @@ usac::DevSampler dev_sampler(const usac_ctx *c, uint64_t seed) {
     ds.prosac_len = prosac ? c->prosac_len : 0u;
     if (c->dev_sampler == USAC_SAMPLER_NAPSAC) {
         ds.nap_n_eligible = c->grid_n_elig;
-        ds.nap_cell = c->grid_cell.as<uint32_t>();
-        ds.nap_rank = c->grid_rank.as<uint32_t>();
-        ds.nap_start = c->grid_start.as<uint32_t>();
-        ds.nap_members = c->grid_members.as<int32_t>();
+        ds.nap_cell = c->grid_cell();
+        ds.nap_rank = c->grid_rank();
+        ds.nap_start = c->grid_start();
+        ds.nap_members = c->grid_members();
         ds.nap_eligible = c->grid_elig.as<int32_t>();
     }
     return ds;
@@ -407,17 +422,14 @@ int ensure_grid(usac_ctx *c, int cs) {
         return fail(c, USAC_ERR_HIP, "pinned host allocation failed");
     const size_t n = c->n;
     HIP_TRY(c, hipSetDevice(c->device));
-    HIP_TRY(c, c->grid_cell.reserve(sizeof(uint32_t) * n));
-    HIP_TRY(c, c->grid_rank.reserve(sizeof(uint32_t) * n));
-    HIP_TRY(c, c->grid_start.reserve(sizeof(uint32_t) * (n + 1)));
-    HIP_TRY(c, c->grid_members.reserve(sizeof(int32_t) * n));
+    HIP_TRY(c, c->grid_csr.reserve(sizeof(uint32_t) * (4 * n + 1)));
     HIP_TRY(c, c->grid_elig.reserve(sizeof(int32_t) * n));
     HIP_TRY(c, c->grid_ws.reserve(usac::grid_workspace_bytes(c->n)));
     c->grid_cs = 0;
     HIP_TRY(c, usac::build_grid(c->stream, c->pts.as<float4>(), c->n, cs, make_int4(lo[0], lo[1], lo[2], lo[3]),
                                 make_int4(bits[0], bits[1], bits[2], bits[3]), c->m, c->grid_ws.p,
-                                c->grid_cell.as<uint32_t>(), c->grid_rank.as<uint32_t>(), c->grid_start.as<uint32_t>(),
-                                c->grid_members.as<int32_t>(), c->grid_elig.as<int32_t>(), c->grid_pin,
+                                c->grid_cell(), c->grid_rank(), c->grid_start(), c->grid_members(),
+                                c->grid_elig.as<int32_t>(), c->grid_pin,
                                 &c->grid_n_cells, &c->grid_n_elig));
     c->grid_cs = cs;
     return USAC_OK;
@@ -439,10 +451,7 @@ int download_grid(usac_ctx *c, int cs, std::unique_ptr<usac::GridNeighbors> &out
         size_t b;
         ~Back() { PinnedPool::get().give_back(p, b); }
     } back{w, got};
-    HIP_TRY(c, hipMemcpyAsync(w, c->grid_cell.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(w + n, c->grid_rank.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(w + 2 * n, c->grid_members.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(c, hipMemcpyAsync(w + 3 * n, c->grid_start.p, sizeof(uint32_t) * nc1, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(w, c->grid_csr.p, sizeof(uint32_t) * (3 * n + nc1), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, stream_wait(c->stream));
     std::vector<uint32_t> cell(w, w + n), rank(w + n, w + 2 * n), start(w + 3 * n, w + 3 * n + nc1);
     std::vector<int32_t> members(reinterpret_cast<const int32_t *>(w + 2 * n), reinterpret_cast<const int32_t *>(w + 3 * n));
@@ -1497,8 +1506,8 @@ void usac_destroy(usac_ctx *c) {
                       &c->inl_idx, &c->inl_idx2, &c->pol_res, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq, &c->nm_w, &c->nm_qw, &c->lo_io,
                       &c->rec_send, &c->rec_all, &c->tv_part, &c->hf_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
-                      &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2, &c->gc_err, &c->grid_cell, &c->grid_rank, &c->grid_start,
-                      &c->grid_members, &c->grid_elig, &c->grid_ws, &c->x_send,
+                      &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2, &c->gc_err, &c->grid_csr,
+                      &c->grid_elig, &c->grid_ws, &c->x_send,
                       &c->x_recv, &c->xring})
         b->release();
     for (auto &ev : c->ev)
@@ -1819,12 +1828,12 @@ int usac_grid_neighbors(usac_ctx *c, int cell_size, uint32_t *n_cells, uint32_t 
     const size_t n = c->n;
     if (n_cells) *n_cells = c->grid_n_cells;
     if (n_eligible) *n_eligible = c->grid_n_elig;
-    if (cell) HIP_TRY(c, hipMemcpyAsync(cell, c->grid_cell.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
-    if (rank) HIP_TRY(c, hipMemcpyAsync(rank, c->grid_rank.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    if (cell) HIP_TRY(c, hipMemcpyAsync(cell, c->grid_cell(), 4 * n, hipMemcpyDeviceToHost, c->stream));
+    if (rank) HIP_TRY(c, hipMemcpyAsync(rank, c->grid_rank(), 4 * n, hipMemcpyDeviceToHost, c->stream));
     if (start)
-        HIP_TRY(c, hipMemcpyAsync(start, c->grid_start.p, 4 * ((size_t)c->grid_n_cells + 1), hipMemcpyDeviceToHost,
+        HIP_TRY(c, hipMemcpyAsync(start, c->grid_start(), 4 * ((size_t)c->grid_n_cells + 1), hipMemcpyDeviceToHost,
                                   c->stream));
-    if (members) HIP_TRY(c, hipMemcpyAsync(members, c->grid_members.p, 4 * n, hipMemcpyDeviceToHost, c->stream));
+    if (members) HIP_TRY(c, hipMemcpyAsync(members, c->grid_members(), 4 * n, hipMemcpyDeviceToHost, c->stream));
     if (eligible && c->grid_n_elig)
         HIP_TRY(c, hipMemcpyAsync(eligible, c->grid_elig.p, 4 * (size_t)c->grid_n_elig, hipMemcpyDeviceToHost,
                                   c->stream));
@@ -2224,6 +2233,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         lap(T_DRAW);
         // ---- device: solve, then exact scores or pool-order flags
         const size_t S = (size_t)B * spk;
+        size_t hst = SB;  // host stride of hmod's components this batch
         uint32_t rows = (uint32_t)S;
         if (nranks > 1) {  // this rank's slice, then the all-gather of every slice's counts and models
             if ((rc = sharded_batch(c, hs.data(), B, iters, thr, nranks, rank, gather, gather_user, xbuf, hc.data(),
@@ -2243,13 +2253,12 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
             HIP_TRY(c, enqueue_score(c, B, thr, loop_chunks(c, B)));
             HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
         }
-        if (SB == S)  // the device's component-major [ncomp][S] block in one copy
-            HIP_TRY(c, hipMemcpyAsync(hmod.data(), c->models.p, sizeof(float) * S * ncomp(c), hipMemcpyDeviceToHost,
-                                      c->stream));
-        else
-            for (int k = 0; k < ncomp(c); k++)
-                HIP_TRY(c, hipMemcpyAsync(hmod.data() + (size_t)k * SB, c->models.as<float>() + (size_t)k * S,
-                                          sizeof(float) * S, hipMemcpyDeviceToHost, c->stream));
+        // the device's component-major [ncomp][S] block in one copy (host stride S this batch:
+        // every copy costs a fixed overhead, 18 per-component copies of a ramp batch cost more
+        // than the batch's kernels)
+        hst = S;
+        HIP_TRY(c, hipMemcpyAsync(hmod.data(), c->models.p, sizeof(float) * S * ncomp(c), hipMemcpyDeviceToHost,
+                                  c->stream));
         if (sprt) {
             if (listed(c)) {  // occupied slots -> mask rows
                 HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
@@ -2275,7 +2284,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
             }
         }
         lap(T_DEVICE);
-        if (!sprt && (rc = exact_sums(c, thr, best.inlier_number, hc.data(), hmod.data(), SB, S, hsum.data(),
+        if (!sprt && (rc = exact_sums(c, thr, best.inlier_number, hc.data(), hmod.data(), hst, S, hsum.data(),
                                       &out->sum_models)))
             return rc;
         lap(T_SUMS);
@@ -2307,7 +2316,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                 }
                 if (!cur.bigger(best)) continue;
                 float model[9];
-                for (int k = 0; k < 9; k++) model[k] = k < ncomp(c) ? hmod[(size_t)k * SB + sl] : 0.f;
+                for (int k = 0; k < 9; k++) model[k] = k < ncomp(c) ? hmod[(size_t)k * hst + sl] : 0.f;
                 if (lo) {  // ransac.cpp:110-112, before the best is replaced
                     lap(T_REPLAY);
                     lo->run(model, cur.inlier_number, cur.score);
