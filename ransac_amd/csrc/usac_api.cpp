@@ -295,6 +295,9 @@ struct usac_ctx {
     DevBuf lo_io;           // one LO stage's inputs (two blocks, alternating) and outputs
     // the LO stages' Σerr passes run on their own stream beside the next stage's fit
     hipStream_t lo_stream = nullptr;
+    // the loop's next batch drawn and run ahead of the current batch's replay (usac_ransac_run)
+    hipStream_t spec_stream = nullptr;
+    hipEvent_t spec_ev = nullptr;
     // per block parity: the stage's outputs in the host block (main), its Σ (side); round end
     hipEvent_t lo_ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     // comm
@@ -1487,6 +1490,7 @@ void usac_destroy(usac_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->xstream) (void)hipStreamSynchronize(c->xstream);
     if (c->lo_stream) (void)hipStreamSynchronize(c->lo_stream);
+    if (c->spec_stream) (void)hipStreamSynchronize(c->spec_stream);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->pol_pin) PinnedPool::get().give_back(c->pol_pin, c->pol_pin_bytes);
     if (c->x_pin) PinnedPool::get().give_back(c->x_pin, c->x_pin_bytes);
@@ -1499,6 +1503,8 @@ void usac_destroy(usac_ctx *c) {
     for (auto &ev : c->lo_ev)
         if (ev) StreamPool::get().give_back(ev);
     if (c->lo_stream) StreamPool::get().give_back(c->lo_stream);
+    if (c->spec_ev) StreamPool::get().give_back(c->spec_ev);
+    if (c->spec_stream) StreamPool::get().give_back(c->spec_stream);
     if (c->grid_pin) PinnedPool::get().give_back(c->grid_pin, c->grid_pin_bytes);
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
@@ -2170,6 +2176,49 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     std::vector<uint32_t> hlist(SB), hmask(sprt ? (size_t)nw * SB : 0);
     std::vector<uint32_t> subset_at(batch), largest_at(batch);
     std::vector<int32_t> last_sample(m, 0);
+    // Speculation: the next batch is drawn and solved / scored on its own stream while the
+    // current batch is replayed (its LO fits run meanwhile).  Its size assumes the replay
+    // leaves max_iterations alone; a smaller actual batch takes the prefix of its results (the
+    // same samples, the same kernels per hypothesis), and the sampler's extra draws are undone
+    // (journal rollback, then a redraw of the kept prefix) before the sampler is used again.
+    // Uniform / NAPSAC-grid without SPRT on one rank only (PROSAC's draws depend on the replay).
+    const bool spec_ok = !prosac && !prm->sprt && nranks == 1 && !napk && (nap || uni) && !getenv("USAC_NO_SPECULATION");
+    pinned_vector<int32_t> hs2(spec_ok ? (size_t)batch * m : 0), hc2(spec_ok ? SB : 0);
+    pinned_vector<float> hmod2(spec_ok ? (size_t)ncomp(c) * SB : 0);
+    std::vector<int32_t> spec_last(m, 0);
+    bool spec = false;          // a speculative batch is on the spec stream
+    uint32_t spec_B = 0;        // its size
+    uint32_t sampler_keep = 0;  // > 0: roll the sampler back and redraw this many samples
+    if (spec_ok) {
+        if (!c->spec_stream) HIP_TRY(c, StreamPool::get().stream(&c->spec_stream));
+        if (!c->spec_ev) HIP_TRY(c, StreamPool::get().event(&c->spec_ev));
+        // every buffer a batch of `batch` samples grows into, now: a reserve() that grows a
+        // block synchronises the device, which must not happen under the speculation
+        HIP_TRY(c, c->perm.reserve(usac::presort_bytes(batch)));
+        HIP_TRY(c, c->hf_part.reserve(sizeof(int32_t) * 2 * 16 * (size_t)batch));
+        if (listed(c)) HIP_TRY(c, c->tv_part.reserve(usac::tv_scratch_bytes(batch * c->spk, c->chunks)));
+        if (is_e(c)) HIP_TRY(c, c->e5_ws.reserve(usac::e5_workspace_bytes(batch)));
+    }
+    // every exit waits for a speculative batch still copying into hs2 / hc2 / hmod2
+    struct SpecDrain {
+        usac_ctx *c;
+        const bool &pending;
+        ~SpecDrain() {
+            if (pending) (void)hipStreamSynchronize(c->spec_stream);
+        }
+    } spec_drain{c, spec};
+    auto sampler_mark = [&]() {
+        if (nap) nap->mark();
+        else uni->mark();
+    };
+    auto sampler_commit = [&]() {
+        if (nap) nap->commit();
+        else uni->commit();
+    };
+    auto sampler_rollback = [&]() {
+        if (nap) nap->rollback();
+        else uni->rollback();
+    };
     std::vector<uint8_t> flags(prosac ? n : 0);
     std::vector<int32_t> inl_list(prosac ? n : 0);
     usac::Score best;
@@ -2204,24 +2253,18 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     // bound drops once the loop has a good model, and a smaller first batch draws, solves and
     // scores fewer hypotheses the run never reaches (the replay is exact for any partition)
     uint32_t cap = prm->batch ? batch : std::min<uint32_t>(batch, kRampFirst);
-    while (iters < max_iters) {
-        const uint32_t B = std::min(std::min(batch, max_iters - iters), cap);
-        if (!prm->batch) cap = std::min<uint32_t>(batch, 2 * cap);
-        // ---- draw the batch (speculatively for PROSAC)
-        std::unique_ptr<usac::ProsacSampler> snapshot;
-        const uint32_t gen_term = prosac ? pterm->terminationLength() : n;
-        if (prosac) snapshot.reset(new usac::ProsacSampler(*pro));
+    // draws B samples into buf (the reference's sample array reuse for NAPSAC: a sample the
+    // sampler leaves (partly) unwritten keeps the previous sample's entries)
+    auto draw_into = [&](int32_t *buf, uint32_t B, usac::ProsacSampler *pro_, uint32_t gen_term) {
         for (uint32_t j = 0; j < B; j++) {
-            int32_t *smp = hs.data() + (size_t)j * m;
-            if (prosac) {
-                subset_at[j] = pro->subset();
-                pro->generateSample(smp, gen_term);
-                largest_at[j] = pro->largest();
+            int32_t *smp = buf + (size_t)j * m;
+            if (pro_) {
+                subset_at[j] = pro_->subset();
+                pro_->generateSample(smp, gen_term);
+                largest_at[j] = pro_->largest();
             } else if (napk) {
                 napk->generateSample(smp);
             } else if (napsac) {
-                // the reference reuses one sample array: a sample the sampler leaves
-                // (partly) unwritten keeps the previous sample's entries
                 if (j > 0) memcpy(smp, smp - m, sizeof(int32_t) * m);
                 else memcpy(smp, last_sample.data(), sizeof(int32_t) * m);
                 nap->generateSample(smp);
@@ -2230,12 +2273,59 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                 uni->generateSample(smp);
             }
         }
+    };
+    // the sampler exactly after the batches consumed so far (undo a speculation's extra draws)
+    auto settle_sampler = [&]() {
+        if (!sampler_keep) return;
+        sampler_rollback();
+        last_sample = spec_last;
+        draw_into(hs2.data(), sampler_keep, nullptr, n);  // hs2 is free again: the kept batch moved to hs
+        sampler_keep = 0;
+    };
+    auto spec_wait = [&]() -> hipError_t {
+        for (uint32_t spins = 0;; spins++) {
+            const hipError_t e = hipEventQuery(c->spec_ev);
+            if (e != hipErrorNotReady) return e;
+            if ((spins & 1023u) == 1023u) std::this_thread::yield();
+        }
+    };
+    while (iters < max_iters) {
+        const uint32_t B = std::min(std::min(batch, max_iters - iters), cap);
+        if (!prm->batch) cap = std::min<uint32_t>(batch, 2 * cap);
+        bool have = false;  // this batch's device results are already on the host (speculation)
+        size_t spec_hst = 0;
+        if (spec) {
+            spec = false;
+            HIP_TRY(c, spec_wait());
+            if (B <= spec_B) {  // its first B samples are this batch
+                std::swap(hs, hs2);
+                std::swap(hc, hc2);
+                std::swap(hmod, hmod2);
+                spec_hst = (size_t)spec_B * spk;
+                have = true;
+                if (B < spec_B) sampler_keep = B;  // undone lazily, before the next draw
+                else sampler_commit();
+            } else {  // (max_iterations grew) the speculation is dropped
+                sampler_rollback();
+                last_sample = spec_last;
+            }
+        }
+        // ---- draw the batch (speculatively for PROSAC)
+        std::unique_ptr<usac::ProsacSampler> snapshot;
+        const uint32_t gen_term = prosac ? pterm->terminationLength() : n;
+        if (!have) {
+            settle_sampler();
+            if (prosac) snapshot.reset(new usac::ProsacSampler(*pro));
+            draw_into(hs.data(), B, prosac ? pro.get() : nullptr, gen_term);
+        }
         lap(T_DRAW);
         // ---- device: solve, then exact scores or pool-order flags
         const size_t S = (size_t)B * spk;
         size_t hst = SB;  // host stride of hmod's components this batch
         uint32_t rows = (uint32_t)S;
-        if (nranks > 1) {  // this rank's slice, then the all-gather of every slice's counts and models
+        if (have) {
+            hst = spec_hst;
+        } else if (nranks > 1) {  // this rank's slice, then the all-gather of every slice's counts and models
             if ((rc = sharded_batch(c, hs.data(), B, iters, thr, nranks, rank, gather, gather_user, xbuf, hc.data(),
                                     hmod.data(), SB, sprt != nullptr, hmask.data())))
                 return rc;
@@ -2282,6 +2372,33 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
             } else {
                 for (size_t sl = 0; sl < S; sl++) slot_row[sl] = (int32_t)sl;
             }
+        }
+        // ---- speculation: the next batch, as if the replay leaves max_iterations alone
+        if (spec_ok && iters + B < max_iters) {
+            settle_sampler();
+            const uint32_t B2 = std::min(std::min(batch, max_iters - (iters + B)), cap);
+            sampler_mark();
+            spec_last = last_sample;
+            draw_into(hs2.data(), B2, nullptr, n);
+            const size_t S2 = (size_t)B2 * spk;
+            std::swap(c->stream, c->spec_stream);  // the launchers enqueue on c->stream
+            hipError_t e = hipMemcpyAsync(c->samples.p, hs2.data(), sizeof(int32_t) * (size_t)B2 * m,
+                                          hipMemcpyHostToDevice, c->stream);
+            if (e == hipSuccess) e = enqueue_solve(c, c->samples.as<int32_t>(), B2, 0, iters + B, nullptr);
+            if (e == hipSuccess) e = enqueue_score(c, B2, thr, loop_chunks(c, B2));
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(hc2.data(), c->counts.p, sizeof(int32_t) * S2, hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(hmod2.data(), c->models.p, sizeof(float) * S2 * ncomp(c), hipMemcpyDeviceToHost,
+                                   c->stream);
+            if (e == hipSuccess) e = hipEventRecord(c->spec_ev, c->stream);
+            std::swap(c->stream, c->spec_stream);
+            if (e != hipSuccess) {
+                (void)hipStreamSynchronize(c->spec_stream);
+                return fail(c, USAC_ERR_HIP, std::string("speculative batch: ") + hipGetErrorString(e));
+            }
+            spec = true;
+            spec_B = B2;
         }
         lap(T_DEVICE);
         if (!sprt && (rc = exact_sums(c, thr, best.inlier_number, hc.data(), hmod.data(), hst, S, hsum.data(),

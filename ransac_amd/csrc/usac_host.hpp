@@ -50,6 +50,20 @@ class GlibcRandom {
         random_r(&data_, &r);
         return (uint32_t)r;
     }
+    // the generator's state, saved and restored in place (random_data points into state_,
+    // so a state only goes back into the object it came from)
+    struct Saved {
+        char state[128];
+        struct random_data data;
+    };
+    void save(Saved &o) const {
+        memcpy(o.state, state_, sizeof(state_));
+        o.data = data_;
+    }
+    void restore(const Saved &o) {
+        memcpy(state_, o.state, sizeof(state_));
+        data_ = o.data;
+    }
 
    private:
     char state_[128];
@@ -79,7 +93,27 @@ class UniformSampler {
             pool_[idx] = pool_[max_];
             pool_[max_] = v;
             sample[i] = (int32_t)v;
+            if (journal_on_) journal_.push_back({idx, (uint32_t)max_});
         }
+    }
+    // speculative draws (the loop's next batch drawn ahead): mark the state, draw, and either
+    // keep the draws (commit) or undo them (rollback: the pool swaps in reverse order, the
+    // generator and the pool size restored)
+    void mark() {
+        rng_.save(mark_rng_);
+        mark_max_ = max_;
+        journal_.clear();
+        journal_on_ = true;
+    }
+    void commit() {
+        journal_on_ = false;
+        journal_.clear();
+    }
+    void rollback() {
+        for (auto it = journal_.rbegin(); it != journal_.rend(); ++it) std::swap(pool_[it->first], pool_[it->second]);
+        max_ = mark_max_;
+        rng_.restore(mark_rng_);
+        commit();
     }
 
    private:
@@ -88,6 +122,10 @@ class UniformSampler {
     std::vector<uint32_t> pool_;
     int max_;
     uint32_t n_, m_;
+    bool journal_on_ = false;
+    std::vector<std::pair<uint32_t, uint32_t>> journal_;
+    GlibcRandom::Saved mark_rng_;
+    int mark_max_ = 0;
 };
 
 // standard_termination_criteria.hpp:24-31, 52-62 (fp32 ratio power, 0.0005f floor,
@@ -554,10 +592,33 @@ class NapsacSampler {
         }
         sample[0] = init;
         const uint32_t sz = g_.count((uint32_t)init);
+        if (journal_on_) cursor_.push_back({(uint32_t)init, next_[init]});
         for (uint32_t k = 1; k < m_; k++) {
             sample[k] = g_.at((uint32_t)init, next_[init]);
             if (++next_[init] >= sz) next_[init] = 0;
         }
+    }
+    // speculative draws, as UniformSampler: the pool swaps and the cursors undone in reverse
+    void mark() {
+        rng_.save(mark_rng_);
+        mark_max_ = max_;
+        mark_uniform_ = uniform_;
+        swaps_.clear();
+        cursor_.clear();
+        journal_on_ = true;
+    }
+    void commit() {
+        journal_on_ = false;
+        swaps_.clear();
+        cursor_.clear();
+    }
+    void rollback() {
+        for (auto it = cursor_.rbegin(); it != cursor_.rend(); ++it) next_[it->first] = it->second;
+        for (auto it = swaps_.rbegin(); it != swaps_.rend(); ++it) std::swap(array_[it->first], array_[it->second]);
+        max_ = mark_max_;
+        uniform_ = mark_uniform_;
+        rng_.restore(mark_rng_);
+        commit();
     }
 
    private:
@@ -568,6 +629,7 @@ class NapsacSampler {
         max_--;
         array_[k] = array_[max_];
         array_[max_] = v;
+        if (journal_on_) swaps_.push_back({k, max_});
         return v;
     }
     GlibcRandom &rng_;
@@ -576,6 +638,10 @@ class NapsacSampler {
     std::vector<uint32_t> next_;
     uint32_t n_, m_, max_ = 0;
     bool uniform_ = false;
+    bool journal_on_ = false, mark_uniform_ = false;
+    std::vector<std::pair<uint32_t, uint32_t>> swaps_, cursor_;
+    GlibcRandom::Saved mark_rng_;
+    uint32_t mark_max_ = 0;
 };
 
 // NapsacSampler::generateSampleKNN (napsac_sampler.hpp:76-98): the initial point from the
