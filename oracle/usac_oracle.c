@@ -109,9 +109,15 @@ int orc_inv3x3(const float *m, float *dst) {
  *   0..r-1 (odd r gets a bye slot), R-1 rounds of disjoint pairs, each pair as (min, max);
  *   row norms n_i = sum_k W[i][k]^2 (k = 0..8 in order) recomputed at each sweep start;
  *   per pair: a = n_p, b = n_q, g = sum_k W[p][k] W[q][k]; skip when g*g <= 1e-28*(a*b);
- *   d = b - a, t = 2g / (|d| + sqrt(d*d + (2g)^2)), negated when d < 0;
- *   c = 1/sqrt(1+t*t); s = c*t; row_p <- c*row_p - s*row_q; row_q <- s*row_p + c*row_q;
- *   n_p <- a - t*g, n_q <- b + t*g;  stop after a sweep with no rotation. */
+ *   d = b - a, g2 = 2g, r = sqrt(d^2 + g2^2), u = |d| + r, inv = 1/sqrt(2 r u),
+ *   c = u inv, s = g2 inv (negated when d < 0), t = s (2 r inv) -- the classical
+ *   t = sign(zeta)/(|zeta| + sqrt(1+zeta^2)), zeta = d/2g, c = 1/sqrt(1+t^2), s = c t with
+ *   one division instead of two ((c, s) = (u, g2)/|(u, g2)|, |(u, g2)|^2 = 2 r u);
+ *   row_p <- c*row_p - s*row_q; row_q <- s*row_p + c*row_q;
+ *   n_p <- a - t*g, n_q <- b + t*g;  stop after a sweep with no rotation.
+ * Round 3: the sums of products and the rotations are fused (fma(), one rounding, =
+ * v_fma_f64 on the device): the norms and g are fma chains over k = 0..8, row_p =
+ * fma(c, wp, -(s wq)), row_q = fma(s, wp, c wq), r = sqrt(fma(d, d, g2 g2)). */
 #define ORC_JAC_SWEEPS 30
 #define ORC_JAC_EPS2 1e-28 /* skip when g^2 <= 1e-28 a b  (|g| <= 1e-14 sqrt(a b)) */
 static int tournament_pairs(int r, int pairs[][2]) {
@@ -143,27 +149,28 @@ static void row_jacobi(double W[][9], int r) {
         double nrm[9];
         for (int i = 0; i < r; i++) {
             double a = 0.0;
-            for (int k = 0; k < 9; k++) a += W[i][k] * W[i][k];
+            for (int k = 0; k < 9; k++) a = fma(W[i][k], W[i][k], a);
             nrm[i] = a;
         }
         for (int pi = 0; pi < np; pi++) {
             const int p = pairs[pi][0], q = pairs[pi][1];
             const double a = nrm[p], b = nrm[q];
             double g = 0.0;
-            for (int k = 0; k < 9; k++) g += W[p][k] * W[q][k];
+            for (int k = 0; k < 9; k++) g = fma(W[p][k], W[q][k], g);
             if (g * g <= ORC_JAC_EPS2 * (a * b)) continue;
             rotated = 1;
-            /* t = sign(zeta)/(|zeta| + sqrt(1+zeta^2)), zeta = (b-a)/(2g), written as
-             * t = sign(d) 2g / (|d| + sqrt(d^2 + 4g^2)), d = b - a */
             const double d = b - a, g2 = 2.0 * g;
-            double t = g2 / (fabs(d) + sqrt(d * d + g2 * g2));
-            if (d < 0.0) t = -t;
-            const double c = 1.0 / sqrt(1.0 + t * t);
-            const double s = c * t;
+            const double rr = sqrt(fma(d, d, g2 * g2));
+            const double u = fabs(d) + rr, r2 = 2.0 * rr;
+            const double inv = 1.0 / sqrt(r2 * u);
+            const double c = u * inv;
+            double s = g2 * inv;
+            if (d < 0.0) s = -s;
+            const double t = s * (r2 * inv);
             for (int k = 0; k < 9; k++) {
                 double wp = W[p][k], wq = W[q][k];
-                W[p][k] = c * wp - s * wq;
-                W[q][k] = s * wp + c * wq;
+                W[p][k] = fma(c, wp, -(s * wq));
+                W[q][k] = fma(s, wp, c * wq);
             }
             nrm[p] = a - t * g;
             nrm[q] = b + t * g;
@@ -428,11 +435,98 @@ static void dlt_fill_rows(float x1, float y1, float x2, float y2, double *r0, do
     }
 }
 
+/* Thin-row spec of the 4-pt DLT (round 3; the device's k_solve_h4, usac_device.hpp dlt4_thin_qr):
+ * the row of vt wanted by dlt.cpp:48 is v8, the right singular vector of the smallest of A's
+ * eight singular values.  With the Householder QR of A^T = Q R (Q 9x8, R 8x8 upper),
+ * A = R^T Q^T and v8 = Q w8, w8 the eigenvector of the smallest eigenvalue of R R^T, found by
+ * inverse iteration (two triangular solves per step, R R^T never formed).  All fp64, fma() =
+ * one rounding:
+ *   QR, column j = row j of W (k = j..8): s2 = fma chain of W[j][k]^2, sig = sqrt(s2)
+ *     (sig not > 0 -> fall back); x0 = W[j][j]; alpha_j = x0 >= 0 ? -sig : sig;
+ *     beta_j = 1/(sig (sig + |x0|)); W[j][j] = x0 - alpha_j (the reflector is W[j][j..8]);
+ *     rows i = j+1..7: f = beta_j * (fma chain of W[j][k] W[i][k]), W[i][k] = fma(-f, W[j][k], W[i][k]);
+ *     then R[j][j] = alpha_j, R[j][i] = W[i][j] (i > j); rd_j = 1/alpha_j.
+ *   inverse iteration from w = e_7, at most ORC_QR_ITERS steps: back substitution
+ *     z_k = (fma chain w_k - R[k][i] z_i, i = k+1..7) * rd_k for k = 7..0; forward substitution
+ *     y_k = (fma chain z_k - R[i][k] y_i, i = 0..k-1) * rd_k for k = 0..7; n2 = fma chain of y_k^2
+ *     (not finite and > 0 -> fall back); inv = 1/sqrt(n2); w'_k = y_k inv; stop when
+ *     max_k |w'_k - w_k| <= 1e-13 (compare-select in k order); no stop -> fall back.
+ *   v = H_0 (H_1 (... H_7 [w; 0])), H_j x = x - beta_j (v_j . x) v_j  (fma chains over k = j..8).
+ * Fall-back (~2.4e-4 of cfg2's samples: sigma_8 / sigma_7 > ~0.6, a degenerate or non-finite
+ * system): row_jacobi + pick_vector on the same rows, the pre-round-3 spec.  Median 3 - 4
+ * steps; H agrees with LAPACK's vt[7] as the Jacobi did (tests/test_reference_statistics.py). */
+#define ORC_QR_ITERS 32
+static int dlt4_thin_qr(const double A[8][9], double *v) {
+    double W[8][9], be[8], rd[8];
+    memcpy(W, A, sizeof(W));
+    for (int j = 0; j < 8; j++) {
+        double s2 = 0.0;
+        for (int k = j; k < 9; k++) s2 = fma(W[j][k], W[j][k], s2);
+        const double sig = sqrt(s2);
+        if (!(sig > 0.0) || !(sig < INFINITY)) return 0;
+        const double x0 = W[j][j];
+        const double alpha = x0 >= 0.0 ? -sig : sig;
+        be[j] = 1.0 / (sig * (sig + fabs(x0)));
+        W[j][j] = x0 - alpha;
+        for (int i = j + 1; i < 8; i++) {
+            double s = 0.0;
+            for (int k = j; k < 9; k++) s = fma(W[j][k], W[i][k], s);
+            const double f = be[j] * s;
+            for (int k = j; k < 9; k++) W[i][k] = fma(-f, W[j][k], W[i][k]);
+        }
+        rd[j] = 1.0 / alpha;
+    }
+    double w[8] = {0, 0, 0, 0, 0, 0, 0, 1.0}, z[8];
+    int conv = 0;
+    for (int it = 0; it < ORC_QR_ITERS && !conv; it++) {
+        for (int k = 7; k >= 0; k--) {
+            double t = w[k];
+            for (int i = k + 1; i < 8; i++) t = fma(-W[i][k], z[i], t);
+            z[k] = t * rd[k];
+        }
+        for (int k = 0; k < 8; k++) { /* y in place of z */
+            double t = z[k];
+            for (int i = 0; i < k; i++) t = fma(-W[k][i], z[i], t);
+            z[k] = t * rd[k];
+        }
+        double n2 = 0.0;
+        for (int k = 0; k < 8; k++) n2 = fma(z[k], z[k], n2);
+        if (!(n2 > 0.0) || !(n2 < INFINITY)) return 0;
+        const double inv = 1.0 / sqrt(n2);
+        double dmax = 0.0;
+        for (int k = 0; k < 8; k++) {
+            const double y = z[k] * inv, dk = fabs(y - w[k]);
+            if (dk > dmax) dmax = dk;
+            w[k] = y;
+        }
+        conv = dmax <= 1e-13;
+    }
+    if (!conv) return 0;
+    double x[9];
+    for (int k = 0; k < 8; k++) x[k] = w[k];
+    x[8] = 0.0;
+    for (int j = 7; j >= 0; j--) {
+        double s = 0.0;
+        for (int k = j; k < 9; k++) s = fma(W[j][k], x[k], s);
+        const double f = be[j] * s;
+        for (int k = j; k < 9; k++) x[k] = fma(-f, W[j][k], x[k]);
+    }
+    for (int k = 0; k < 9; k++) v[k] = x[k];
+    return 1;
+}
+
 static int homography_dlt4(const orc_est *e, const int *sample, float *H) {
     double W[8][9];
     for (int i = 0; i < 4; i++) {
         const float *p = e->pts + 4 * (size_t)sample[i];
         dlt_fill_rows(p[0], p[1], p[2], p[3], W[2 * i], W[2 * i + 1]);
+    }
+    if (e->dlt_mode == ORC_DLT_THIN) {
+        double v[9];
+        if (dlt4_thin_qr((const double(*)[9])W, v)) {
+            for (int k = 0; k < 9; k++) H[k] = (float)(v[k] / v[8]);
+            return 1;
+        }
     }
     return dlt_rows_solve(W, 8, e->dlt_mode, H);
 }
@@ -976,7 +1070,8 @@ static inline float fundamental_error(const orc_est *e, unsigned int pidx) {
  *      see triangulate()), CalcDepth; the
  *      first root whose E puts all five points in front of both cameras is returned. */
 
-/* row Jacobi on r rows of `cols` (<= 4) columns, same rules as row_jacobi; J (nullable,
+/* row Jacobi on r rows of `cols` (<= 4) columns, the round-1 row_jacobi rules (unfused
+ * products, t and c by two divisions); J (nullable,
  * r x r) accumulates the rotations applied to the rows */
 static void row_jacobi_small(double W[][4], int r, int cols, double J[][4]) {
     int pairs[6][2];

@@ -23,32 +23,7 @@
 namespace usac {
 
 // ------------------------------------------------------------------------ solve (H, 4-pt)
-__global__ __launch_bounds__(64) void k_solve_h4(const float4 *__restrict__ pts, uint32_t n,
-                                                 const int32_t *__restrict__ samples_in, int32_t *samples_out,
-                                                 uint32_t B, DevSampler ds, uint64_t first_hyp, int nullspace,
-                                                 float *__restrict__ models) {
-    const uint32_t h = blockIdx.x * 64 + threadIdx.x;
-    if (h >= B) return;
-    int32_t s[4];
-    if (samples_in) {
-#pragma unroll
-        for (int i = 0; i < 4; i++) s[i] = samples_in[4 * (size_t)h + i];
-    } else {
-        draw_sample<4>(ds, first_hyp + h, n, s);
-        if (samples_out) {
-#pragma unroll
-            for (int i = 0; i < 4; i++) samples_out[4 * (size_t)h + i] = s[i];
-        }
-    }
-    double W[8][9];
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        float4 p = pts[s[i]];
-        dlt_rows(p.x, p.y, p.z, p.w, W[2 * i], W[2 * i + 1]);
-    }
-    row_jacobi<8>(W);
-    double v[9];
-    pick_vector<8>(W, nullspace, v);
+__device__ __forceinline__ void store_h(float *__restrict__ models, uint32_t B, uint32_t h, const double *v) {
     float H[9], Hi[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) H[k] = (float)(v[k] / v[8]);
@@ -57,6 +32,97 @@ __global__ __launch_bounds__(64) void k_solve_h4(const float4 *__restrict__ pts,
     for (int k = 0; k < 9; k++) {
         models[(size_t)k * B + h] = H[k];
         models[(size_t)(9 + k) * B + h] = Hi[k];
+    }
+}
+
+// Thin 4-pt DLT by QR + inverse iteration (dlt4_thin_qr).  A lane whose system falls back is
+// appended to fb_list (wave-aggregated atomic on fb_n[0]); k_solve_h4_jac then solves it by the
+// row Jacobi.  The sample is written to samples_out here for every lane.
+__global__ __launch_bounds__(64) void k_solve_h4(const float4 *__restrict__ pts, uint32_t n,
+                                                 const int32_t *__restrict__ samples_in, int32_t *samples_out,
+                                                 uint32_t B, DevSampler ds, uint64_t first_hyp,
+                                                 float *__restrict__ models, uint32_t *__restrict__ fb_list,
+                                                 uint32_t *__restrict__ fb_n) {
+    const uint32_t h = blockIdx.x * 64 + threadIdx.x;
+    bool fb = false;
+    if (h < B) {
+        int32_t s[4];
+        if (samples_in) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) s[i] = samples_in[4 * (size_t)h + i];
+        } else {
+            draw_sample<4>(ds, first_hyp + h, n, s);
+            if (samples_out) {
+#pragma unroll
+                for (int i = 0; i < 4; i++) samples_out[4 * (size_t)h + i] = s[i];
+            }
+        }
+        double W[8][9];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            float4 p = pts[s[i]];
+            dlt_rows(p.x, p.y, p.z, p.w, W[2 * i], W[2 * i + 1]);
+        }
+        double v[9];
+        if (dlt4_thin_qr(W, v)) store_h(models, B, h, v);
+        else fb = true;
+    }
+    const uint64_t m = __ballot(fb);
+    if (m) {
+        const uint32_t lane = threadIdx.x;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(fb_n, (uint32_t)__popcll(m));
+        base = __shfl(base, 0, 64);
+        if (fb) fb_list[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = h;
+    }
+}
+
+// Row-Jacobi 4-pt DLT (row_jacobi + pick_vector): every hypothesis (fb_list == nullptr: the
+// nullspace mode; it also writes samples_out) or the fb_n[0] listed fall-backs of k_solve_h4
+// (a grid-stride loop over the list: the grid is sized before the count is known).  With a list, the last
+// workgroup to finish (fb_n[1] counts them) resets both counters, so the next solve on this
+// buffer starts from zero without a memset.
+__global__ __launch_bounds__(64) void k_solve_h4_jac(const float4 *__restrict__ pts, uint32_t n,
+                                                     const int32_t *__restrict__ samples_in, int32_t *samples_out,
+                                                     uint32_t B, DevSampler ds, uint64_t first_hyp, int nullspace,
+                                                     float *__restrict__ models, const uint32_t *__restrict__ fb_list,
+                                                     uint32_t *__restrict__ fb_n) {
+    const uint32_t K = fb_list ? __builtin_amdgcn_readfirstlane(__atomic_load_n(fb_n, __ATOMIC_RELAXED)) : B;
+    for (uint32_t base = blockIdx.x * 64; base < K; base += gridDim.x * 64) {
+        const uint32_t i = base + threadIdx.x;
+        if (i >= K) continue;
+        const uint32_t h = fb_list ? fb_list[i] : i;
+        int32_t s[4];
+        if (samples_in) {
+#pragma unroll
+            for (int k = 0; k < 4; k++) s[k] = samples_in[4 * (size_t)h + k];
+        } else {
+            draw_sample<4>(ds, first_hyp + h, n, s);
+            if (samples_out && !fb_list) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) samples_out[4 * (size_t)h + k] = s[k];
+            }
+        }
+        double W[8][9];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            float4 p = pts[s[k]];
+            dlt_rows(p.x, p.y, p.z, p.w, W[2 * k], W[2 * k + 1]);
+        }
+        row_jacobi<8>(W);
+        double v[9];
+        pick_vector<8>(W, nullspace, v);
+        store_h(models, B, h, v);
+    }
+    if (fb_list) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            if (atomicAdd(fb_n + 1, 1u) == gridDim.x - 1) {
+                __atomic_store_n(fb_n, 0u, __ATOMIC_RELAXED);
+                __atomic_store_n(fb_n + 1, 0u, __ATOMIC_RELAXED);
+            }
+        }
     }
 }
 
@@ -637,9 +703,20 @@ __global__ __launch_bounds__(256) void k_argmax_final(const BestEntry *__restric
 
 hipError_t launch_solve_h4(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
                            int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, int nullspace,
-                           float *models) {
-    hipLaunchKernelGGL(k_solve_h4, dim3((B + 63) / 64), dim3(64), 0, st, pts, n, samples_in, samples_out, B, ds,
-                       first_hyp, nullspace, models);
+                           float *models, uint32_t *fb_list, uint32_t *fb_n) {
+    const uint32_t blocks = (B + 63) / 64;
+    if (nullspace) {
+        hipLaunchKernelGGL(k_solve_h4_jac, dim3(blocks), dim3(64), 0, st, pts, n, samples_in, samples_out, B, ds,
+                           first_hyp, 1, models, (const uint32_t *)nullptr, (uint32_t *)nullptr);
+        return LAUNCH_CHECK();
+    }
+    if (!fb_list || !fb_n) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_solve_h4, dim3(blocks), dim3(64), 0, st, pts, n, samples_in, samples_out, B, ds, first_hyp,
+                       models, fb_list, fb_n);
+    hipError_t e = LAUNCH_CHECK();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_solve_h4_jac, dim3(blocks < 256 ? blocks : 256), dim3(64), 0, st, pts, n, samples_in,
+                       samples_out, B, ds, first_hyp, 0, models, (const uint32_t *)fb_list, fb_n);
     return LAUNCH_CHECK();
 }
 

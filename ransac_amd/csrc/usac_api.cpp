@@ -258,6 +258,7 @@ struct usac_ctx {
     // batch buffers
     DevBuf samples, models, counts, sums, best, hostmodels, argmax_part;
     DevBuf list, list_n;    // fundamental: occupied model slots (compacted) and their number
+    DevBuf h4_fb, h4_fb_n;  // homography thin DLT: QR fall-back hypotheses and two counters (zeroed once)
     DevBuf pool_idx, pool_pts, masks;  // SPRT parity path: pool order, permuted points, flag words
     // LO-RANSAC (LoRansac): W speculative inner iterations in flight -- their inlier lists
     // (W x N), LSQ sample positions (W x lo_sample_size), point counts, thresholds, models,
@@ -364,6 +365,13 @@ int ensure_batch(usac_ctx *c, uint32_t B) {
     if (listed(c)) {
         HIP_TRY(c, c->list.reserve(sizeof(uint32_t) * S));
         HIP_TRY(c, c->list_n.reserve(sizeof(uint32_t)));
+    }
+    if (is_h(c)) {
+        HIP_TRY(c, c->h4_fb.reserve(sizeof(uint32_t) * (size_t)B));
+        if (!c->h4_fb_n.p) {  // the kernels reset the counters after each use; a pooled block is not zero
+            HIP_TRY(c, c->h4_fb_n.reserve(2 * sizeof(uint32_t)));
+            HIP_TRY(c, hipMemsetAsync(c->h4_fb_n.p, 0, 2 * sizeof(uint32_t), c->stream));
+        }
     }
     return USAC_OK;
 }
@@ -479,7 +487,8 @@ hipError_t enqueue_solve(usac_ctx *c, const int32_t *samples_dev, uint32_t B, ui
                                      c->list.as<uint32_t>(), c->list_n.as<uint32_t>());
     if (is_h(c))
         return usac::launch_solve_h4(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, ds,
-                                     first_hyp, c->dlt_mode == USAC_DLT_NULLSPACE, c->models.as<float>());
+                                     first_hyp, c->dlt_mode == USAC_DLT_NULLSPACE, c->models.as<float>(),
+                                     c->h4_fb.as<uint32_t>(), c->h4_fb_n.as<uint32_t>());
     return usac::launch_solve_line(c->stream, c->pts.as<float2>(), c->n, samples_dev, samples_out, B, ds, first_hyp,
                                    c->models.as<float>());
 }
@@ -1507,7 +1516,7 @@ void usac_destroy(usac_ctx *c) {
     if (c->spec_stream) StreamPool::get().give_back(c->spec_stream);
     if (c->grid_pin) PinnedPool::get().give_back(c->grid_pin, c->grid_pin_bytes);
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
-                      &c->argmax_part, &c->list, &c->list_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
+                      &c->argmax_part, &c->list, &c->list_n, &c->h4_fb, &c->h4_fb_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
                       &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->inl_scratch, &c->e5_ws, &c->one_model,
                       &c->inl_idx, &c->inl_idx2, &c->pol_res, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq, &c->nm_w, &c->nm_qw, &c->lo_io,
                       &c->rec_send, &c->rec_all, &c->tv_part, &c->hf_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,

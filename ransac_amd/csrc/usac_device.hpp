@@ -133,11 +133,15 @@ struct Tournament {
 };
 
 // One-sided (Hestenes) Jacobi on the R rows of W (fp64), the row-space part of the thin
-// cv::SVD::compute of dlt.cpp:43.  Spec (identical in the oracle): sweeps < 30, pairs in
-// tournament order (above); row norms n_i (sum over k = 0..8 in order) recomputed at
-// each sweep start; per pair a = n_p, b = n_q, g = sum_k W[p][k] W[q][k], skip when
-// g*g <= 1e-28*(a*b); d = b - a, t = 2g/(|d| + sqrt(d*d + (2g)^2)) negated when d < 0
-// (= sign(zeta)/(|zeta|+sqrt(1+zeta^2)), zeta = d/2g), c = 1/sqrt(1+t*t), s = c*t;
+// cv::SVD::compute of dlt.cpp:43.  Spec (identical in the oracle's row_jacobi; fused
+// operations written out, fma = one rounding): sweeps < 30, pairs in tournament order
+// (above); row norms n_i = fma chain over k = 0..8 recomputed at each sweep start; per pair
+// a = n_p, b = n_q, g = fma chain of W[p][k] W[q][k]; skip when g*g <= 1e-28*(a*b);
+// d = b - a, g2 = 2g, r = sqrt(fma(d, d, g2*g2)), u = |d| + r, inv = 1/sqrt((2r)*u),
+// c = u*inv, s = g2*inv negated when d < 0, t = s*((2r)*inv)  (the classical
+// t = sign(zeta)/(|zeta|+sqrt(1+zeta^2)), zeta = d/2g, c = 1/sqrt(1+t^2), s = c t with
+// one division instead of two: (c, s) = (u, g2)/|(u, g2)| and |(u, g2)|^2 = 2 r u);
+// row_p <- fma(c, row_p, -(s*row_q)), row_q <- fma(s, row_p, c*row_q);
 // n_p <- a - t g, n_q <- b + t g; stop after a sweep without rotation.  Fully unrolled
 // so W stays in VGPRs.
 template <int R>
@@ -150,7 +154,7 @@ __device__ __forceinline__ void row_jacobi(double (&W)[R][9]) {
         for (int i = 0; i < R; i++) {
             double a = 0.0;
 #pragma unroll
-            for (int k = 0; k < 9; k++) a += W[i][k] * W[i][k];
+            for (int k = 0; k < 9; k++) a = fma(W[i][k], W[i][k], a);
             nrm[i] = a;
         }
 #pragma unroll
@@ -159,19 +163,22 @@ __device__ __forceinline__ void row_jacobi(double (&W)[R][9]) {
             const double a = nrm[p], b = nrm[q];
             double g = 0.0;
 #pragma unroll
-            for (int k = 0; k < 9; k++) g += W[p][k] * W[q][k];
+            for (int k = 0; k < 9; k++) g = fma(W[p][k], W[q][k], g);
             if (!(g * g <= 1e-28 * (a * b))) {
                 rotated = true;
                 const double d = b - a, g2 = 2.0 * g;
-                double t = g2 / (fabs(d) + sqrt(d * d + g2 * g2));
-                if (d < 0.0) t = -t;
-                const double c = 1.0 / sqrt(1.0 + t * t);
-                const double s = c * t;
+                const double r = sqrt(fma(d, d, g2 * g2));
+                const double u = fabs(d) + r, r2 = 2.0 * r;
+                const double inv = 1.0 / sqrt(r2 * u);
+                const double c = u * inv;
+                double s = g2 * inv;
+                if (d < 0.0) s = -s;
+                const double t = s * (r2 * inv);
 #pragma unroll
                 for (int k = 0; k < 9; k++) {
-                    double wp = W[p][k], wq = W[q][k];
-                    W[p][k] = c * wp - s * wq;
-                    W[q][k] = s * wp + c * wq;
+                    const double wp = W[p][k], wq = W[q][k];
+                    W[p][k] = fma(c, wp, -(s * wq));
+                    W[q][k] = fma(s, wp, c * wq);
                 }
                 nrm[p] = a - t * g;
                 nrm[q] = b + t * g;
@@ -179,6 +186,88 @@ __device__ __forceinline__ void row_jacobi(double (&W)[R][9]) {
         }
         if (!rotated) break;
     }
+}
+
+// Thin row of the 4-pt DLT by Householder QR of A^T + inverse iteration on R R^T (the oracle's
+// dlt4_thin_qr, spec there; fma = one rounding on both sides).  Returns false when the spec
+// falls back to row_jacobi + pick_vector (zero / non-finite column norm or iterate, or no
+// convergence within 32 steps).  W is consumed (reflectors in place, R above them).
+__device__ __forceinline__ bool dlt4_thin_qr(double (&W)[8][9], double *v) {
+    double be[8], rd[8];
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        double s2 = 0.0;
+#pragma unroll
+        for (int k = j; k < 9; k++) s2 = fma(W[j][k], W[j][k], s2);
+        const double sig = sqrt(s2);
+        ok = ok && (sig > 0.0) && (sig < INFINITY);
+        const double x0 = W[j][j];
+        const double alpha = x0 >= 0.0 ? -sig : sig;
+        be[j] = 1.0 / (sig * (sig + fabs(x0)));
+        W[j][j] = x0 - alpha;
+#pragma unroll
+        for (int i = j + 1; i < 8; i++) {
+            double s = 0.0;
+#pragma unroll
+            for (int k = j; k < 9; k++) s = fma(W[j][k], W[i][k], s);
+            const double f = be[j] * s;
+#pragma unroll
+            for (int k = j; k < 9; k++) W[i][k] = fma(-f, W[j][k], W[i][k]);
+        }
+        rd[j] = 1.0 / alpha;
+    }
+    if (!ok) return false;
+    double w[8], z[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) w[k] = k == 7 ? 1.0 : 0.0;
+    bool conv = false;
+    for (int it = 0; it < 32 && !conv; it++) {
+#pragma unroll
+        for (int k = 7; k >= 0; k--) {
+            double t = w[k];
+#pragma unroll
+            for (int i = k + 1; i < 8; i++) t = fma(-W[i][k], z[i], t);
+            z[k] = t * rd[k];
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            double t = z[k];
+#pragma unroll
+            for (int i = 0; i < k; i++) t = fma(-W[k][i], z[i], t);
+            z[k] = t * rd[k];
+        }
+        double n2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) n2 = fma(z[k], z[k], n2);
+        if (!(n2 > 0.0) || !(n2 < INFINITY)) return false;
+        const double inv = 1.0 / sqrt(n2);
+        double dmax = 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const double y = z[k] * inv, dk = fabs(y - w[k]);
+            dmax = dk > dmax ? dk : dmax;
+            w[k] = y;
+        }
+        conv = dmax <= 1e-13;
+    }
+    if (!conv) return false;
+    double x[9];
+#pragma unroll
+    for (int k = 0; k < 8; k++) x[k] = w[k];
+    x[8] = 0.0;
+#pragma unroll
+    for (int j = 7; j >= 0; j--) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = j; k < 9; k++) s = fma(W[j][k], x[k], s);
+        const double f = be[j] * s;
+#pragma unroll
+        for (int k = j; k < 9; k++) x[k] = fma(-f, W[j][k], x[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 9; k++) v[k] = x[k];
+    return true;
 }
 
 // Model vector from the converged rows (oracle pick_vector):

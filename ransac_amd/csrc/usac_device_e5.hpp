@@ -18,7 +18,8 @@
 namespace usac {
 namespace e5 {
 
-// row Jacobi on R rows of C (<= 4) columns with the row_jacobi rules; ACC: also rotate the
+// row Jacobi on R rows of C (<= 4) columns with the round-1 row_jacobi rules (unfused
+// products, t and c by two divisions; the oracle's row_jacobi_small); ACC: also rotate the
 // rows of J (R x R)
 template <int R, int C, bool ACC>
 __device__ __forceinline__ void jacobi_small(double (&W)[R][C], double (&J)[R][R]) {

@@ -81,6 +81,29 @@ def test_dlt4_models_bit_exact(usac, oracle, homography_scenes, mode):
         assert same.all(), "first mismatch at sample %d" % int(np.argmin(same.all(1)))
 
 
+def test_dlt4_qr_fallbacks_bit_exact(usac, oracle):
+    """The thin DLT's QR + inverse-iteration spec and its row-Jacobi fall-back (k_solve_h4 ->
+    k_solve_h4_jac over the fall-back list): a full cfg2-size batch (~2.4e-4 of its samples fall
+    back on a close sigma_7 / sigma_8 pair) plus degenerate samples (repeated points: rank-
+    deficient rows; all-zero points: a zero column norm; a non-finite point)."""
+    pts, _ = _cfg2(10000, seed=4)
+    pts = pts.copy()
+    pts[17] = 0.0
+    pts[18] = 0.0
+    pts[19] = [np.inf, 1.0, 2.0, 3.0]
+    samples = oracle.uniform_samples(11, len(pts), 4, 65536)
+    samples[:64] = [[5, 5, 9, 13], [17, 18, 17, 18], [17, 18, 20, 21], [19, 1, 2, 3]] * 16
+    samples[64:128, 1] = samples[64:128, 0]
+    est = oracle.Estimator(oracle.HOMOGRAPHY, pts)
+    om, _ = est.estimate_batch(samples)
+    with usac.Context(usac.ESTIMATOR.Homography, pts) as ctx:
+        for _ in range(2):  # the second solve starts from the counters the first one reset
+            gm, nm = ctx.estimate_models(samples)
+            assert (nm == 1).all()
+            same = (gm.view(np.int32) == om.view(np.int32)) | (np.isnan(gm) & np.isnan(om))
+            assert same.all(), "first mismatch at sample %d" % int(np.argmin(same.all(1)))
+
+
 def test_fused_batch_matches_oracle(usac, oracle):
     pts, _ = _cfg2(4000)
     samples = oracle.uniform_samples(21, len(pts), 4, 4096)
