@@ -438,24 +438,55 @@ static void dlt_fill_rows(float x1, float y1, float x2, float y2, double *r0, do
 /* Thin-row spec of the 4-pt DLT (round 3; the device's k_solve_h4, usac_device.hpp dlt4_thin_qr):
  * the row of vt wanted by dlt.cpp:48 is v8, the right singular vector of the smallest of A's
  * eight singular values.  With the Householder QR of A^T = Q R (Q 9x8, R 8x8 upper),
- * A = R^T Q^T and v8 = Q w8, w8 the eigenvector of the smallest eigenvalue of R R^T, found by
- * inverse iteration (two triangular solves per step, R R^T never formed).  All fp64, fma() =
- * one rounding:
+ * A = R^T Q^T and v8 = Q w8, w8 the eigenvector of the smallest eigenvalue of R R^T.  w8 is found
+ * by two-vector subspace inverse iteration with a Rayleigh-Ritz step (R R^T never formed: two
+ * triangular solves per vector; the Ritz vector converges at the rate sigma_8^2 / sigma_6^2, so a
+ * close sigma_7 does not slow it -- NAPSAC's neighbourhood samples have sigma_8 / sigma_7 up to
+ * 0.9).  All fp64, fma() = one rounding:
  *   QR, column j = row j of W (k = j..8): s2 = fma chain of W[j][k]^2, sig = sqrt(s2)
- *     (sig not > 0 -> fall back); x0 = W[j][j]; alpha_j = x0 >= 0 ? -sig : sig;
+ *     (sig not finite and > 0 -> fall back); x0 = W[j][j]; alpha_j = x0 >= 0 ? -sig : sig;
  *     beta_j = 1/(sig (sig + |x0|)); W[j][j] = x0 - alpha_j (the reflector is W[j][j..8]);
  *     rows i = j+1..7: f = beta_j * (fma chain of W[j][k] W[i][k]), W[i][k] = fma(-f, W[j][k], W[i][k]);
  *     then R[j][j] = alpha_j, R[j][i] = W[i][j] (i > j); rd_j = 1/alpha_j.
- *   inverse iteration from w = e_7, at most ORC_QR_ITERS steps: back substitution
- *     z_k = (fma chain w_k - R[k][i] z_i, i = k+1..7) * rd_k for k = 7..0; forward substitution
- *     y_k = (fma chain z_k - R[i][k] y_i, i = 0..k-1) * rd_k for k = 0..7; n2 = fma chain of y_k^2
- *     (not finite and > 0 -> fall back); inv = 1/sqrt(n2); w'_k = y_k inv; stop when
- *     max_k |w'_k - w_k| <= 1e-13 (compare-select in k order); no stop -> fall back.
- *   v = H_0 (H_1 (... H_7 [w; 0])), H_j x = x - beta_j (v_j . x) v_j  (fma chains over k = j..8).
- * Fall-back (~2.4e-4 of cfg2's samples: sigma_8 / sigma_7 > ~0.6, a degenerate or non-finite
- * system): row_jacobi + pick_vector on the same rows, the pre-round-3 spec.  Median 3 - 4
- * steps; H agrees with LAPACK's vt[7] as the Jacobi did (tests/test_reference_statistics.py). */
+ *   back(q): y_k = (fma chain q_k - R[k][i] y_i, i = k+1..7) * rd_k, k = 7..0   (R y = q)
+ *   fwd(u):  y_k = (fma chain u_k - R[i][k] y_i, i = 0..k-1) * rd_k, k = 0..7   (R^T y = u)
+ *   q1 = e_7, q2 = e_6, w0 = 0; at most ORC_QR_ITERS steps:
+ *     y1 = back(q1), y2 = back(q2); a = y1.y1, b = y1.y2, d = y2.y2 (fma chains, k = 0..7);
+ *     h = (a - d) * 0.5, r = sqrt(fma(h, h, b b)); (c1, c2) = h >= 0 ? (h + r, b) : (b, r - h)
+ *     (the larger eigenvalue's eigenvector of [[a, b], [b, d]]); nn = sqrt(fma(c1, c1, c2 c2))
+ *     (not finite and > 0 -> fall back), c1 *= 1/nn, c2 *= 1/nn;
+ *     w_k = fma(c1, q1_k, c2 q2_k); dt = w.w0; e_k = |w_k - (dt < 0 ? -w0_k : w0_k)|;
+ *     w0 = w; stop when max_k e_k <= 1e-13 (compare-select in k order);
+ *     u1_k = fma(c1, y1_k, c2 y2_k), u2_k = fma(c1, y2_k, -(c2 y1_k)); z1 = fwd(u1), z2 = fwd(u2);
+ *     Gram-Schmidt: q1 = z1 * (1/sqrt(z1.z1)); p = q1.z2, z2_k = fma(-p, q1_k, z2_k),
+ *     q2 = z2 * (1/sqrt(z2.z2))  (either norm not finite and > 0 -> fall back);
+ *   no stop -> fall back;  v = H_0 (H_1 (... H_7 [w0; 0])), H_j x = x - beta_j (v_j . x) v_j
+ *   (fma chains over k = j..8).
+ * Fall-back (degenerate / non-finite systems; none of 32768 cfg2 samples, 6e-5 of NAPSAC's):
+ * row_jacobi + pick_vector on the same rows, the pre-round-3 spec.  4 - 5 steps on average;
+ * H agrees with LAPACK's vt[7] as the Jacobi did (tests/test_reference_statistics.py). */
 #define ORC_QR_ITERS 32
+static void qr_back(double W[8][9], const double *rd, const double *q, double *y) {
+    for (int k = 7; k >= 0; k--) {
+        double t = q[k];
+        for (int i = k + 1; i < 8; i++) t = fma(-W[i][k], y[i], t);
+        y[k] = t * rd[k];
+    }
+}
+static void qr_fwd(double W[8][9], const double *rd, const double *u, double *y) {
+    for (int k = 0; k < 8; k++) {
+        double t = u[k];
+        for (int i = 0; i < k; i++) t = fma(-W[k][i], y[i], t);
+        y[k] = t * rd[k];
+    }
+}
+static double dot8(const double *x, const double *y) {
+    double t = 0.0;
+    for (int k = 0; k < 8; k++) t = fma(x[k], y[k], t);
+    return t;
+}
+static int pos_finite(double x) { return x > 0.0 && x < INFINITY; }
+
 static int dlt4_thin_qr(const double A[8][9], double *v) {
     double W[8][9], be[8], rd[8];
     memcpy(W, A, sizeof(W));
@@ -463,7 +494,7 @@ static int dlt4_thin_qr(const double A[8][9], double *v) {
         double s2 = 0.0;
         for (int k = j; k < 9; k++) s2 = fma(W[j][k], W[j][k], s2);
         const double sig = sqrt(s2);
-        if (!(sig > 0.0) || !(sig < INFINITY)) return 0;
+        if (!pos_finite(sig)) return 0;
         const double x0 = W[j][j];
         const double alpha = x0 >= 0.0 ? -sig : sig;
         be[j] = 1.0 / (sig * (sig + fabs(x0)));
@@ -476,34 +507,53 @@ static int dlt4_thin_qr(const double A[8][9], double *v) {
         }
         rd[j] = 1.0 / alpha;
     }
-    double w[8] = {0, 0, 0, 0, 0, 0, 0, 1.0}, z[8];
+    double q1[8] = {0, 0, 0, 0, 0, 0, 0, 1.0}, q2[8] = {0, 0, 0, 0, 0, 0, 1.0, 0}, w0[8] = {0};
+    double y1[8], y2[8], u1[8], u2[8];
     int conv = 0;
     for (int it = 0; it < ORC_QR_ITERS && !conv; it++) {
-        for (int k = 7; k >= 0; k--) {
-            double t = w[k];
-            for (int i = k + 1; i < 8; i++) t = fma(-W[i][k], z[i], t);
-            z[k] = t * rd[k];
-        }
-        for (int k = 0; k < 8; k++) { /* y in place of z */
-            double t = z[k];
-            for (int i = 0; i < k; i++) t = fma(-W[k][i], z[i], t);
-            z[k] = t * rd[k];
-        }
-        double n2 = 0.0;
-        for (int k = 0; k < 8; k++) n2 = fma(z[k], z[k], n2);
-        if (!(n2 > 0.0) || !(n2 < INFINITY)) return 0;
-        const double inv = 1.0 / sqrt(n2);
+        qr_back(W, rd, q1, y1);
+        qr_back(W, rd, q2, y2);
+        const double a = dot8(y1, y1), b = dot8(y1, y2), d = dot8(y2, y2);
+        const double h = (a - d) * 0.5, r = sqrt(fma(h, h, b * b));
+        double c1 = h >= 0.0 ? h + r : b, c2 = h >= 0.0 ? b : r - h;
+        const double nn = sqrt(fma(c1, c1, c2 * c2));
+        if (!pos_finite(nn)) return 0;
+        const double inn = 1.0 / nn;
+        c1 = c1 * inn;
+        c2 = c2 * inn;
+        double w[8];
+        for (int k = 0; k < 8; k++) w[k] = fma(c1, q1[k], c2 * q2[k]);
+        const double dt = dot8(w, w0);
         double dmax = 0.0;
         for (int k = 0; k < 8; k++) {
-            const double y = z[k] * inv, dk = fabs(y - w[k]);
-            if (dk > dmax) dmax = dk;
-            w[k] = y;
+            const double ek = fabs(w[k] - (dt < 0.0 ? -w0[k] : w0[k]));
+            if (ek > dmax) dmax = ek;
+            w0[k] = w[k];
         }
-        conv = dmax <= 1e-13;
+        if (dmax <= 1e-13) {
+            conv = 1;
+            break;
+        }
+        for (int k = 0; k < 8; k++) {
+            u1[k] = fma(c1, y1[k], c2 * y2[k]);
+            u2[k] = fma(c1, y2[k], -(c2 * y1[k]));
+        }
+        qr_fwd(W, rd, u1, y1);
+        qr_fwd(W, rd, u2, y2);
+        const double n1 = dot8(y1, y1);
+        if (!pos_finite(n1)) return 0;
+        const double i1 = 1.0 / sqrt(n1);
+        for (int k = 0; k < 8; k++) q1[k] = y1[k] * i1;
+        const double p = dot8(q1, y2);
+        for (int k = 0; k < 8; k++) y2[k] = fma(-p, q1[k], y2[k]);
+        const double n2 = dot8(y2, y2);
+        if (!pos_finite(n2)) return 0;
+        const double i2 = 1.0 / sqrt(n2);
+        for (int k = 0; k < 8; k++) q2[k] = y2[k] * i2;
     }
     if (!conv) return 0;
     double x[9];
-    for (int k = 0; k < 8; k++) x[k] = w[k];
+    for (int k = 0; k < 8; k++) x[k] = w0[k];
     x[8] = 0.0;
     for (int j = 7; j >= 0; j--) {
         double s = 0.0;

@@ -188,10 +188,37 @@ __device__ __forceinline__ void row_jacobi(double (&W)[R][9]) {
     }
 }
 
-// Thin row of the 4-pt DLT by Householder QR of A^T + inverse iteration on R R^T (the oracle's
-// dlt4_thin_qr, spec there; fma = one rounding on both sides).  Returns false when the spec
-// falls back to row_jacobi + pick_vector (zero / non-finite column norm or iterate, or no
-// convergence within 32 steps).  W is consumed (reflectors in place, R above them).
+// Thin row of the 4-pt DLT by Householder QR of A^T + two-vector subspace inverse iteration on
+// R R^T with a Rayleigh-Ritz step (the oracle's dlt4_thin_qr, spec there; fma = one rounding on
+// both sides).  Returns false when the spec falls back to row_jacobi + pick_vector (a zero /
+// non-finite norm, or no convergence within 32 steps).  W is consumed (reflectors in place,
+// R above them).
+__device__ __forceinline__ void qr_back(const double (&W)[8][9], const double *rd, const double *q, double *y) {
+#pragma unroll
+    for (int k = 7; k >= 0; k--) {
+        double t = q[k];
+#pragma unroll
+        for (int i = k + 1; i < 8; i++) t = fma(-W[i][k], y[i], t);
+        y[k] = t * rd[k];
+    }
+}
+__device__ __forceinline__ void qr_fwd(const double (&W)[8][9], const double *rd, const double *u, double *y) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        double t = u[k];
+#pragma unroll
+        for (int i = 0; i < k; i++) t = fma(-W[k][i], y[i], t);
+        y[k] = t * rd[k];
+    }
+}
+__device__ __forceinline__ double dot8(const double *x, const double *y) {
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) t = fma(x[k], y[k], t);
+    return t;
+}
+__device__ __forceinline__ bool pos_finite(double x) { return x > 0.0 && x < INFINITY; }
+
 __device__ __forceinline__ bool dlt4_thin_qr(double (&W)[8][9], double *v) {
     double be[8], rd[8];
     bool ok = true;
@@ -201,7 +228,7 @@ __device__ __forceinline__ bool dlt4_thin_qr(double (&W)[8][9], double *v) {
 #pragma unroll
         for (int k = j; k < 9; k++) s2 = fma(W[j][k], W[j][k], s2);
         const double sig = sqrt(s2);
-        ok = ok && (sig > 0.0) && (sig < INFINITY);
+        ok = ok && pos_finite(sig);
         const double x0 = W[j][j];
         const double alpha = x0 >= 0.0 ? -sig : sig;
         be[j] = 1.0 / (sig * (sig + fabs(x0)));
@@ -218,43 +245,66 @@ __device__ __forceinline__ bool dlt4_thin_qr(double (&W)[8][9], double *v) {
         rd[j] = 1.0 / alpha;
     }
     if (!ok) return false;
-    double w[8], z[8];
+    double q1[8], q2[8], w0[8], y1[8], y2[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) w[k] = k == 7 ? 1.0 : 0.0;
+    for (int k = 0; k < 8; k++) {
+        q1[k] = k == 7 ? 1.0 : 0.0;
+        q2[k] = k == 6 ? 1.0 : 0.0;
+        w0[k] = 0.0;
+    }
     bool conv = false;
-    for (int it = 0; it < 32 && !conv; it++) {
+    for (int it = 0; it < 32; it++) {
+        qr_back(W, rd, q1, y1);
+        qr_back(W, rd, q2, y2);
+        const double a = dot8(y1, y1), b = dot8(y1, y2), d = dot8(y2, y2);
+        const double h = (a - d) * 0.5, r = sqrt(fma(h, h, b * b));
+        double c1 = h >= 0.0 ? h + r : b, c2 = h >= 0.0 ? b : r - h;
+        const double nn = sqrt(fma(c1, c1, c2 * c2));
+        if (!pos_finite(nn)) return false;
+        const double inn = 1.0 / nn;
+        c1 = c1 * inn;
+        c2 = c2 * inn;
+        double w[8];
 #pragma unroll
-        for (int k = 7; k >= 0; k--) {
-            double t = w[k];
-#pragma unroll
-            for (int i = k + 1; i < 8; i++) t = fma(-W[i][k], z[i], t);
-            z[k] = t * rd[k];
-        }
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            double t = z[k];
-#pragma unroll
-            for (int i = 0; i < k; i++) t = fma(-W[k][i], z[i], t);
-            z[k] = t * rd[k];
-        }
-        double n2 = 0.0;
-#pragma unroll
-        for (int k = 0; k < 8; k++) n2 = fma(z[k], z[k], n2);
-        if (!(n2 > 0.0) || !(n2 < INFINITY)) return false;
-        const double inv = 1.0 / sqrt(n2);
+        for (int k = 0; k < 8; k++) w[k] = fma(c1, q1[k], c2 * q2[k]);
+        const double dt = dot8(w, w0);
         double dmax = 0.0;
 #pragma unroll
         for (int k = 0; k < 8; k++) {
-            const double y = z[k] * inv, dk = fabs(y - w[k]);
-            dmax = dk > dmax ? dk : dmax;
-            w[k] = y;
+            const double ek = fabs(w[k] - (dt < 0.0 ? -w0[k] : w0[k]));
+            dmax = ek > dmax ? ek : dmax;
+            w0[k] = w[k];
         }
-        conv = dmax <= 1e-13;
+        if (dmax <= 1e-13) {
+            conv = true;
+            break;
+        }
+        double u1[8], u2[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            u1[k] = fma(c1, y1[k], c2 * y2[k]);
+            u2[k] = fma(c1, y2[k], -(c2 * y1[k]));
+        }
+        qr_fwd(W, rd, u1, y1);
+        qr_fwd(W, rd, u2, y2);
+        const double n1 = dot8(y1, y1);
+        if (!pos_finite(n1)) return false;
+        const double i1 = 1.0 / sqrt(n1);
+#pragma unroll
+        for (int k = 0; k < 8; k++) q1[k] = y1[k] * i1;
+        const double p = dot8(q1, y2);
+#pragma unroll
+        for (int k = 0; k < 8; k++) y2[k] = fma(-p, q1[k], y2[k]);
+        const double n2 = dot8(y2, y2);
+        if (!pos_finite(n2)) return false;
+        const double i2 = 1.0 / sqrt(n2);
+#pragma unroll
+        for (int k = 0; k < 8; k++) q2[k] = y2[k] * i2;
     }
     if (!conv) return false;
     double x[9];
 #pragma unroll
-    for (int k = 0; k < 8; k++) x[k] = w[k];
+    for (int k = 0; k < 8; k++) x[k] = w0[k];
     x[8] = 0.0;
 #pragma unroll
     for (int j = 7; j >= 0; j--) {
