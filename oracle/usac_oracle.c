@@ -819,6 +819,81 @@ static void null_complement(double W[][9], int r, int count, double N[][9]) {
     }
 }
 
+/* Null-space basis of an r x 9 system (r < 9) in the same completion order, by Householder QR
+ * (round 3; the device's qr_null<R>, shared by the 7-pt F and 5-pt E solvers): QR of W^T as in
+ * dlt4_thin_qr (s2 = fma chain, sig = sqrt(s2) -- not finite and > 0 -> return 0 and the caller
+ * falls back to row_jacobi + null_complement --, alpha, beta, reflector in W[j][j..8], rows
+ * i = j+1..r-1 updated by fma); null columns q_m = H_0 (... H_{r-1} e_{r+m}), m = 0..8-r
+ * (fma chains over k = j..8); then for vector j: c_k = (fma chain over l < j of N[l][k]^2) -
+ * (fma chain over m of q_m[k]^2) -- the row space's share of axis k minus 1, plus the earlier
+ * vectors' --, start axis ks = first argmin; x_k = fma chain over m of q_m[ks] q_m[k] (the
+ * projection of e_ks onto the null space); two passes of d = fma chain N[l].x,
+ * x_k = fma(-d, N[l][k], x_k) over l < j; N[j][k] = x_k / sqrt(fma chain of x_k^2).
+ * In exact arithmetic this is null_complement's result (the projector onto the row space and
+ * its diagonal do not depend on the basis that spans it); the QR replaces the ~8-sweep row
+ * Jacobi (k_solve_f7 0.10 ms -> see DESIGN.md). */
+static int qr_null(double W[][9], int r, double N[][9]) {
+    const int C = 9 - r;
+    double be[9], Q[9][9];
+    for (int j = 0; j < r; j++) {
+        double s2 = 0.0;
+        for (int k = j; k < 9; k++) s2 = fma(W[j][k], W[j][k], s2);
+        const double sig = sqrt(s2);
+        if (!pos_finite(sig)) return 0;
+        const double x0 = W[j][j];
+        const double alpha = x0 >= 0.0 ? -sig : sig;
+        be[j] = 1.0 / (sig * (sig + fabs(x0)));
+        W[j][j] = x0 - alpha;
+        for (int i = j + 1; i < r; i++) {
+            double s = 0.0;
+            for (int k = j; k < 9; k++) s = fma(W[j][k], W[i][k], s);
+            const double f = be[j] * s;
+            for (int k = j; k < 9; k++) W[i][k] = fma(-f, W[j][k], W[i][k]);
+        }
+    }
+    for (int m = 0; m < C; m++) {
+        for (int k = 0; k < 9; k++) Q[m][k] = k == r + m ? 1.0 : 0.0;
+        for (int j = r - 1; j >= 0; j--) {
+            double s = 0.0;
+            for (int k = j; k < 9; k++) s = fma(W[j][k], Q[m][k], s);
+            const double f = be[j] * s;
+            for (int k = j; k < 9; k++) Q[m][k] = fma(-f, W[j][k], Q[m][k]);
+        }
+    }
+    for (int j = 0; j < C; j++) {
+        int ks = 0;
+        double best = 0.0;
+        for (int k = 0; k < 9; k++) {
+            double t = 0.0, u = 0.0;
+            for (int m = 0; m < C; m++) t = fma(Q[m][k], Q[m][k], t);
+            for (int l = 0; l < j; l++) u = fma(N[l][k], N[l][k], u);
+            const double c = u - t;
+            if (k == 0 || c < best) {
+                best = c;
+                ks = k;
+            }
+        }
+        double x[9];
+        for (int k = 0; k < 9; k++) {
+            double t = 0.0;
+            for (int m = 0; m < C; m++) t = fma(Q[m][ks], Q[m][k], t);
+            x[k] = t;
+        }
+        for (int pass = 0; pass < 2; pass++) {
+            for (int l = 0; l < j; l++) {
+                double d = 0.0;
+                for (int k = 0; k < 9; k++) d = fma(N[l][k], x[k], d);
+                for (int k = 0; k < 9; k++) x[k] = fma(-d, N[l][k], x[k]);
+            }
+        }
+        double nrm = 0.0;
+        for (int k = 0; k < 9; k++) nrm = fma(x[k], x[k], nrm);
+        nrm = sqrt(nrm);
+        for (int k = 0; k < 9; k++) N[j][k] = x[k] / nrm;
+    }
+    return 1;
+}
+
 /* Real roots of c0 x^3 + c1 x^2 + c2 x + c3, ascending -- restates the contract of
  * cv::solveCubic (seven_points.cpp:131) with IEEE basic operations only (OpenCV's
  * closed form uses acos/cos/pow, which are not correctly rounded; this spec is shared
@@ -911,7 +986,8 @@ static int fund_is_valid(const float *pts, const float *F, const int *sample) {
 
 /* FundamentalSolver::SevenPointsAlgorithm (seven_points.cpp:49-156) + the validity filter
  * of FundamentalEstimator::EstimateModel (fundamental_estimator.hpp:48-63): 7x9 fp32
- * rows, fp64 row Jacobi + null complement (f1, f2 = the two null rows, cast to float),
+ * rows, fp64 null basis by qr_null (f1, f2 = the two null rows, cast to float; row Jacobi +
+ * null complement when it falls back),
  * fp32 cubic coefficients exactly as :98-128, roots (cubic_roots) cast to float, fp32
  * F assembly with F33 normalisation (:138-154); valid models kept in root order. */
 static int fundamental_7pt(const orc_est *e, const int *sample, float *models) {
@@ -922,9 +998,12 @@ static int fundamental_7pt(const orc_est *e, const int *sample, float *models) {
         float row[9] = {x2 * x1, x2 * y1, x2, y2 * x1, y2 * y1, y2, x1, y1, 1.f};
         for (int k = 0; k < 9; k++) W[i][k] = (double)row[k];
     }
-    row_jacobi(W, 7);
-    double N[2][9];
-    null_complement(W, 7, 2, N);
+    double N[2][9], W0[7][9];
+    memcpy(W0, W, sizeof(W0));
+    if (!qr_null(W, 7, N)) {
+        row_jacobi(W0, 7);
+        null_complement(W0, 7, 2, N);
+    }
     float f1[9], f2[9];
     for (int k = 0; k < 9; k++) {
         f1[k] = (float)N[0][k];
@@ -1525,9 +1604,12 @@ static int essential_5pt_all(const orc_est *e, const int *sample, float *Eout, f
         const double row[9] = {x1 * x2, x2 * y1, x2, x1 * y2, y1 * y2, y2, x1, y1, 1.0};
         for (int k = 0; k < 9; k++) W[i][k] = row[k];
     }
-    row_jacobi(W, 5);
-    double N[4][9];
-    null_complement(W, 5, 4, N);
+    double N[4][9], W0[5][9];
+    memcpy(W0, W, sizeof(W0));
+    if (!qr_null(W, 5, N)) {
+        row_jacobi(W0, 5);
+        null_complement(W0, 5, 4, N);
+    }
     double Mz[10][10], dets[11], z[11];
     for (int k = 0; k < 11; k++) {
         z[k] = (double)(k - 5);

@@ -83,8 +83,18 @@ __global__ __launch_bounds__(64) void k_e5_basis(const float4 *__restrict__ pts,
         W[i][3] = x1 * y2; W[i][4] = y1 * y2; W[i][5] = y2;
         W[i][6] = x1; W[i][7] = y1; W[i][8] = 1.0;
     }
-    row_jacobi<5>(W);
-    e5::null_basis4(W, N);
+    if (!qr_null<5>(W, N)) {  // a zero / non-finite column: the row-Jacobi completion
+#pragma unroll
+        for (int i = 0; i < 5; i++) {
+            const float4 p = pts[s[i]];
+            const double x1 = p.x, y1 = p.y, x2 = p.z, y2 = p.w;
+            W[i][0] = x1 * x2; W[i][1] = x2 * y1; W[i][2] = x2;
+            W[i][3] = x1 * y2; W[i][4] = y1 * y2; W[i][5] = y2;
+            W[i][6] = x1; W[i][7] = y1; W[i][8] = 1.0;
+        }
+        row_jacobi<5>(W);
+        e5::null_basis4(W, N);
+    }
 #pragma unroll
     for (int j = 0; j < 4; j++)
 #pragma unroll

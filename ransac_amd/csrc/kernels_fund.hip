@@ -17,7 +17,8 @@
 namespace usac {
 
 // SevenPointsAlgorithm + EstimateModel validity filter for one sample per lane:
-// 7 x 9 fp64 rows -> row Jacobi -> null complement (f1, f2) -> fp32 cubic coefficients ->
+// 7 x 9 fp64 rows -> QR null basis (f1, f2; row Jacobi + null complement as the fall-back) ->
+// fp32 cubic coefficients ->
 // IEEE cubic roots -> F per root -> oriented filter -> slot write + compaction.
 __global__ __launch_bounds__(64) void k_solve_f7(const float4 *__restrict__ pts, uint32_t n,
                                                  const int32_t *__restrict__ samples_in, int32_t *samples_out,
@@ -47,9 +48,16 @@ __global__ __launch_bounds__(64) void k_solve_f7(const float4 *__restrict__ pts,
             const float4 p = pts[s[i]];
             fund_row(p.x, p.y, p.z, p.w, W[i]);
         }
-        row_jacobi<7>(W);
         double N[2][9];
-        null_complement7(W, N);
+        if (!qr_null<7>(W, N)) {  // a zero / non-finite column: the row-Jacobi completion
+#pragma unroll
+            for (int i = 0; i < 7; i++) {
+                const float4 p = pts[s[i]];
+                fund_row(p.x, p.y, p.z, p.w, W[i]);
+            }
+            row_jacobi<7>(W);
+            null_complement7(W, N);
+        }
         float f1[9], f2[9];
 #pragma unroll
         for (int k = 0; k < 9; k++) {

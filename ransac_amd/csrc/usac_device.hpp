@@ -320,6 +320,105 @@ __device__ __forceinline__ bool dlt4_thin_qr(double (&W)[8][9], double *v) {
     return true;
 }
 
+// Null-space basis of an R x 9 system (R < 9) in the FULL_UV completion order (the oracle's
+// qr_null, spec there): Householder QR of W^T as in dlt4_thin_qr, the 9 - R null columns
+// Q e_R.. Q e_8, then vector j from the axis least represented by the row space and the earlier
+// vectors, projected onto the null space and twice Gram-Schmidt'ed against the earlier vectors.
+// False (fall back to row_jacobi + the row-based completion) on a zero / non-finite column norm.
+template <int R>
+__device__ __forceinline__ bool qr_null(double (&W)[R][9], double (&N)[9 - R][9]) {
+    constexpr int C = 9 - R;
+    double be[R];
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+        double s2 = 0.0;
+#pragma unroll
+        for (int k = j; k < 9; k++) s2 = fma(W[j][k], W[j][k], s2);
+        const double sig = sqrt(s2);
+        ok = ok && pos_finite(sig);
+        const double x0 = W[j][j];
+        const double alpha = x0 >= 0.0 ? -sig : sig;
+        be[j] = 1.0 / (sig * (sig + fabs(x0)));
+        W[j][j] = x0 - alpha;
+#pragma unroll
+        for (int i = j + 1; i < R; i++) {
+            double s = 0.0;
+#pragma unroll
+            for (int k = j; k < 9; k++) s = fma(W[j][k], W[i][k], s);
+            const double f = be[j] * s;
+#pragma unroll
+            for (int k = j; k < 9; k++) W[i][k] = fma(-f, W[j][k], W[i][k]);
+        }
+    }
+    if (!ok) return false;
+    double Q[C][9];
+#pragma unroll
+    for (int m = 0; m < C; m++) {
+#pragma unroll
+        for (int k = 0; k < 9; k++) Q[m][k] = k == R + m ? 1.0 : 0.0;
+#pragma unroll
+        for (int j = R - 1; j >= 0; j--) {
+            double s = 0.0;
+#pragma unroll
+            for (int k = j; k < 9; k++) s = fma(W[j][k], Q[m][k], s);
+            const double f = be[j] * s;
+#pragma unroll
+            for (int k = j; k < 9; k++) Q[m][k] = fma(-f, W[j][k], Q[m][k]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < C; j++) {
+        int ks = 0;
+        double best = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            double t = 0.0, u = 0.0;
+#pragma unroll
+            for (int m = 0; m < C; m++) t = fma(Q[m][k], Q[m][k], t);
+#pragma unroll
+            for (int l = 0; l < j; l++) u = fma(N[l][k], N[l][k], u);
+            const double c = u - t;
+            if (k == 0 || c < best) {
+                best = c;
+                ks = k;
+            }
+        }
+        double qk[C], x[9];
+#pragma unroll
+        for (int m = 0; m < C; m++) {
+            qk[m] = Q[m][0];
+#pragma unroll
+            for (int k = 1; k < 9; k++) qk[m] = ks == k ? Q[m][k] : qk[m];
+        }
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            double t = 0.0;
+#pragma unroll
+            for (int m = 0; m < C; m++) t = fma(qk[m], Q[m][k], t);
+            x[k] = t;
+        }
+#pragma unroll
+        for (int pass = 0; pass < 2; pass++) {
+#pragma unroll
+            for (int l = 0; l < j; l++) {
+                double d = 0.0;
+#pragma unroll
+                for (int k = 0; k < 9; k++) d = fma(N[l][k], x[k], d);
+#pragma unroll
+                for (int k = 0; k < 9; k++) x[k] = fma(-d, N[l][k], x[k]);
+            }
+        }
+        double nrm = 0.0;
+#pragma unroll
+        for (int k = 0; k < 9; k++) nrm = fma(x[k], x[k], nrm);
+        nrm = sqrt(nrm);
+#pragma unroll
+        for (int k = 0; k < 9; k++) N[j][k] = x[k] / nrm;
+    }
+    return true;
+}
+
 // Model vector from the converged rows (oracle pick_vector):
 //  thin      -> row of smallest squared norm, first on ties  (vt.row(vt.rows-1))
 //  nullspace -> unit vector orthogonal to all non-zero rows: rows normalised in place,
