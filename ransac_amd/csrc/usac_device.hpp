@@ -3,8 +3,9 @@
 // Every routine states the reference code it computes and the exact floating-point
 // recipe (DESIGN.md "Numerics"); the CPU oracle (oracle/usac_oracle.c) restates the same
 // reference independently, and the parity tests compare the two bit for bit.
-// Compiled with -ffp-contract=off: no FMA contraction, IEEE fp32/fp64 division and
-// square root (hipcc's default correctly-rounded lowering), denormals kept.
+// Compiled with -ffp-contract=off: no FMA contraction (a fused operation is an explicit fma()
+// in both this file and the oracle), IEEE fp32/fp64 division and square root (hipcc's default
+// correctly-rounded lowering), denormals kept.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
