@@ -4,7 +4,7 @@
 // Used by the polish (ransac.cpp:157-214), LO-RANSAC (inner_local_optimization.hpp:74-133)
 // and PROSAC's termination scan.
 //
-//   k_inl_flags   grid over points: exact residual, per-block inlier count      (parallel)
+//   k_inl_flags   grid over points: exact residual (kept in scratch), per-block inlier count
 //   k_inl_compact grid over points: each block sums the earlier blocks' counts (its output
 //                 offset; the last block writes the total), ordered compaction of indices
 //                 and residuals                                                 (parallel)
@@ -51,14 +51,20 @@ __device__ __forceinline__ void inl_model(const float *model, float *sm) {
 }
 
 // Batched over W models: blockIdx.y = model w (model w at models + 9 w, threshold thrs[w]
-// or the scalar thr).  Per model the scratch holds its block counts (nb padded to 64)
-// followed by its compacted residuals (n floats): inl_stride(n) words.  Every model's
+// or the scalar thr).  Per model the scratch holds its block counts (nb padded to 64),
+// its compacted residuals (n floats) and every point's residual (n floats): inl_stride(n) words.  Every model's
 // result is exactly the single-model one (the kernels never mix models).
 // The residuals are followed by the model's seqsum scratch (one chain, 8-byte aligned: every
 // part of the stride is even).
 constexpr size_t kInlSeqWords = seq::scratch_bytes(1) / sizeof(uint32_t);
 
 __host__ __device__ __forceinline__ size_t inl_res_words(uint32_t n) {
+    const uint32_t nb = (n + kInlBlock - 1) / kInlBlock;
+    return (size_t)((nb + 63) & ~63u) + 2 * (size_t)((n + 1) & ~1u);
+}
+// every point's residual (k_inl_flags writes them, k_inl_compact reads them back instead of
+// evaluating the model again), after the compacted residuals
+__host__ __device__ __forceinline__ size_t inl_all_offset(uint32_t n) {
     const uint32_t nb = (n + kInlBlock - 1) / kInlBlock;
     return (size_t)((nb + 63) & ~63u) + ((n + 1) & ~1u);
 }
@@ -85,12 +91,14 @@ __global__ __launch_bounds__(kInlThreads) void k_inl_flags(const void *__restric
     float m[18];
 #pragma unroll
     for (int k = 0; k < 18; k++) m[k] = sm[k];
+    float *all_e = reinterpret_cast<float *>(scratch + w * inl_stride(n) + inl_all_offset(n));
     uint32_t cnt = 0;
 #pragma unroll
     for (uint32_t u = 0; u < kInlPer; u++) {
         const uint32_t i = blockIdx.x * kInlBlock + u * kInlThreads + threadIdx.x;
-        const bool in = i < n && inl_error<EST>(m, pts, i) < t;
-        cnt += (uint32_t)__popcll(__ballot(in));
+        const float e = i < n ? inl_error<EST>(m, pts, i) : 0.f;
+        if (i < n) all_e[i] = e;
+        cnt += (uint32_t)__popcll(__ballot(i < n && e < t));
     }
     if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = cnt;
     __syncthreads();
@@ -109,7 +117,6 @@ __global__ __launch_bounds__(kInlThreads) void k_inl_compact(const void *__restr
                                                              uint32_t *__restrict__ scratch, int32_t *__restrict__ idx,
                                                              size_t idx_stride, const int32_t *__restrict__ ok,
                                                              int32_t *__restrict__ totals) {
-    __shared__ float sm[18];
     __shared__ uint32_t wsum[kInlPer][kInlThreads / 64], wpre[kInlThreads / 64];
     const uint32_t ws = inl_slot(slots, blockIdx.y);
     if (ok && !ok[ws]) {  // a failed fit: its list is left as it was (workgroup-uniform) and its
@@ -117,22 +124,19 @@ __global__ __launch_bounds__(kInlThreads) void k_inl_compact(const void *__restr
         if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) totals[ws] = 0;
         return;
     }
-    inl_model<EST>(models + 9 * (size_t)ws, sm);
     const float t = thrs ? thrs[ws] : thr;
-    float m[18];
-#pragma unroll
-    for (int k = 0; k < 18; k++) m[k] = sm[k];
     const size_t stride = inl_stride(n);
     const uint32_t nb = (n + kInlBlock - 1) / kInlBlock;
     const uint32_t *block_counts = scratch + ws * stride;
     float *errs = reinterpret_cast<float *>(scratch + ws * stride + ((nb + 63) & ~63u));
+    const float *all_e = reinterpret_cast<const float *>(scratch + ws * stride + inl_all_offset(n));
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     float e[kInlPer];
     uint64_t bal[kInlPer];
 #pragma unroll
     for (uint32_t u = 0; u < kInlPer; u++) {
         const uint32_t i = blockIdx.x * kInlBlock + u * kInlThreads + threadIdx.x;
-        e[u] = i < n ? inl_error<EST>(m, pts, i) : 0.f;
+        e[u] = i < n ? all_e[i] : 0.f;
         bal[u] = __ballot(i < n && e[u] < t);
         if (lane == 0) wsum[u][wave] = (uint32_t)__popcll(bal[u]);
     }
