@@ -131,7 +131,11 @@ namespace usac {
 //            256 contiguous chunks; each thread reduces its chunk to (count, ΣΔL, max prefix
 //            of ΔL); thread 0 combines the chunks in pool order -- rejected iff some prefix
 //            exceeds log A, the sequential test re-associated (fp32).
-constexpr uint32_t kHead = 256;
+// kHead = 64 (round 3; was 256): a wave of phase 1 runs until its last lane decides, and on
+// cfg3 most waves hold one of the few good models, so the head is as long as the wave walks;
+// 64 points reject nearly every bad model and the survivors' tails run in parallel
+// (cfg3 883-894 -> 1065-1069 M hyp/s same-box; 32: 961-1088)
+constexpr uint32_t kHead = 64;
 
 template <int EST>
 __device__ __forceinline__ float sprt_error(const float *m, const void *pts, uint32_t p) {
