@@ -57,6 +57,10 @@ def parse():
     ap.add_argument("--lo", type=int, default=1, help="cfg5 LO variant: 1 InItLORsc (unlimited), 2 InItFLORsc")
     ap.add_argument("--cfg5-replicas", action="store_true",
                     help="cfg5 with N > 1: independent runs per rank instead of hypothesis-sharded runs")
+    ap.add_argument("--prewarm-ms", type=float, default=150.0,
+                    help="untimed device warm-up before the warmup steps (throughput lines): batches are run "
+                         "for this long first, so the timed steps see the GPU at its sustained clocks even when "
+                         "--warmup is a handful of steps (0 = off)")
     ap.add_argument("--pipeline", type=int, default=3,
                     help="batches in flight: one context (stream + buffers) per in-flight batch, so batch i+1's "
                          "solve overlaps batch i's scoring")
@@ -608,6 +612,22 @@ def main():
         for j in range(max(0, count - P + 1), count):
             sink(*finish(first_step + j))
 
+    # untimed device warm-up (clocks, caches, queues): batches of the same workload beyond every
+    # timed index, until --prewarm-ms has passed; then the W warmup steps as before
+    pre_batches = 0
+    if args.prewarm_ms > 0 and torch.cuda.is_available():
+        base = args.warmup + args.steps + 1000
+        tw = time.perf_counter()
+        while True:
+            go = (time.perf_counter() - tw) * 1e3 < args.prewarm_ms
+            if world > 1:  # every rank runs the same batches (each launch may be a collective)
+                flag = torch.tensor([1 if go else 0], dtype=torch.int32)
+                dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+                go = bool(flag.item())
+            if not go:
+                break
+            run(base + pre_batches, 4 * P, lambda rec, t: None)
+            pre_batches += 4 * P
     run(0, args.warmup, lambda rec, t: None)
     if world > 1:
         dist.barrier()
@@ -702,7 +722,7 @@ def main():
             "unit": "hypotheses/s",
             "n_gpus": world,
             "steps": args.steps,
-            "warmup": args.warmup,
+            "warmup": args.warmup, "prewarm": {"ms": args.prewarm_ms, "batches": pre_batches},
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
             "scaling": "weak",
