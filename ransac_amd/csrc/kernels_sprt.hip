@@ -260,26 +260,50 @@ __global__ __launch_bounds__(256) void k_sprt_tail(const void *__restrict__ pool
         s_sum[threadIdx.x] = acc;
         s_max[threadIdx.x] = mx;
         __syncthreads();
-        if (threadIdx.x == 0) {
+        if (threadIdx.x < 64) {
+            // the chunks combined in pool order by wave 0: lane l holds chunks 4l..4l+3 in
+            // registers (one LDS round trip), and the sequential walk reads them with
+            // v_readlane (wave-uniform lane index) instead of three dependent LDS reads per
+            // chunk; every lane runs the same fp32 chain as a single thread did
+            const uint32_t l = threadIdx.x;
+            int rc[4];
+            float rs[4], rm[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                rc[u] = s_cnt[4 * l + u];
+                rs[u] = s_sum[4 * l + u];
+                rm[u] = s_max[4 * l + u];
+            }
             float L = sv.L;
             int c = sv.cnt;
-            bool good = true;
+            bool good = true, end = false;
             uint32_t tested = kHead;
-            for (int j = 0; j < 256; j++) {
-                const uint32_t cb = j * per, ce = cb + per < rest ? cb + per : rest;
-                if (cb >= ce) break;
-                if (L + s_max[j] > log_A) {  // rejected inside chunk j
-                    good = false;
-                    tested += ce - cb;  // upper bound of the points the sequential test reads
-                    break;
+            for (int src = 0; src < 64 && !end; src++) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t j = 4 * src + u;
+                    const uint32_t cb = j * per, ce = cb + per < rest ? cb + per : rest;
+                    if (cb >= ce) {
+                        end = true;
+                        break;
+                    }
+                    const float mj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rm[u]), src));
+                    if (L + mj > log_A) {  // rejected inside chunk j
+                        good = false;
+                        tested += ce - cb;  // upper bound of the points the sequential test reads
+                        end = true;
+                        break;
+                    }
+                    L += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rs[u]), src));
+                    c += __builtin_amdgcn_readlane(rc[u], src);
+                    tested += ce - cb;
                 }
-                L += s_sum[j];
-                c += s_cnt[j];
-                tested += ce - cb;
             }
-            counts[sv.slot] = good ? c : -1;
-            sums[sv.slot] = good ? (float)c : 0.f;
-            if (tested_total) atomicAdd(tested_total, tested - kHead);
+            if (l == 0) {
+                counts[sv.slot] = good ? c : -1;
+                sums[sv.slot] = good ? (float)c : 0.f;
+                if (tested_total) atomicAdd(tested_total, tested - kHead);
+            }
         }
         __syncthreads();
     }
