@@ -11,6 +11,10 @@ scaling "weak", each rank owns disjoint hypothesis index ranges).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Without a launcher, --gpus N > 1 starts the N rank processes itself (launch_ranks: one per GPU,
+RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rank 0's line relayed, non-zero exit when any
+rank fails); under torchrun --gpus must equal WORLD_SIZE.
 """
 import argparse
 import json
@@ -511,9 +515,100 @@ def init_exchange(ctx, usac, dist, torch, world, rank, uid):
     sys.exit(3)
 
 
+def launch_plan(gpus, env):
+    """How `bench.py --gpus N` runs, decided before anything touches the GPU:
+    ("self", 1) -- one process, one GPU (no WORLD_SIZE, N = 1);
+    ("rank", W) -- this process is one rank of a launcher's W (torchrun, or launch_ranks below);
+    ("spawn", N) -- no launcher: start N rank processes here (launch_ranks);
+    ("refuse", msg) -- --gpus disagrees with the launcher's WORLD_SIZE."""
+    if gpus < 1:
+        return "refuse", "--gpus must be >= 1"
+    ws = env.get("WORLD_SIZE")
+    if ws is None or ws == "":
+        return ("spawn", gpus) if gpus > 1 else ("self", 1)
+    try:
+        world = int(ws)
+    except ValueError:
+        return "refuse", "WORLD_SIZE=%r is not an integer" % ws
+    if world != gpus:
+        return "refuse", "--gpus %d but the launcher's WORLD_SIZE is %d: refusing to report a %d-GPU line" % (
+            gpus, world, gpus)
+    return "rank", world
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv, env=None, script=None):
+    """One process per GPU without torchrun: N fresh children of this (GPU-untouched) parent, each
+    with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT, running this script
+    with the same arguments.  Rank 0's stdout (the JSON line) is relayed; the other ranks' stdout
+    goes to stderr.  When a child fails the others are ended (they would wait in a collective) and
+    the launcher exits with the failing child's status; 0 only when every rank exits 0."""
+    import subprocess
+    import threading
+
+    base = dict(os.environ if env is None else env)
+    base.update({"WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_free_port()),
+                 "LOCAL_WORLD_SIZE": str(n)})
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, "-u", script or os.path.abspath(__file__)] + list(argv),
+                                      env=e, stdout=subprocess.PIPE, text=True))
+
+    def relay(p, out):
+        for ln in p.stdout:
+            out.write(ln)
+            out.flush()
+    th = [threading.Thread(target=relay, args=(p, sys.stdout if r == 0 else sys.stderr), daemon=True)
+          for r, p in enumerate(procs)]
+    for t in th:
+        t.start()
+    status = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        failed = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if failed and status == 0:
+            r, status = failed[0]
+            print("bench: rank %d exited with status %d; ending the other ranks" % (r, status), file=sys.stderr)
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+        if all(c is not None for c in codes):
+            break
+        time.sleep(0.05)
+    for t in th:
+        t.join(timeout=5)
+    return status
+
+
 def main():
     global _DEV
     args = parse()
+    how, what = launch_plan(args.gpus, os.environ)
+    if how == "refuse":
+        print("bench: " + what, file=sys.stderr)
+        sys.exit(2)
+    if how == "spawn":  # no HIP call has happened in this process
+        sys.exit(launch_ranks(what, sys.argv[1:]))
+    if os.environ.get("USAC_BENCH_DRY_RUN"):  # launcher plumbing test: report the rank's view and stop
+        r = int(os.environ.get("RANK", "0"))
+        if os.environ.get("USAC_BENCH_FAIL_RANK") == str(r):
+            sys.exit(5)
+        if r == 0:
+            print(json.dumps({"n_gpus": what, "rank": r, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                              "master": "%s:%s" % (os.environ.get("MASTER_ADDR"), os.environ.get("MASTER_PORT"))}))
+        else:  # a failing rank 0 must not leave the others waiting forever (they wait here briefly)
+            time.sleep(float(os.environ.get("USAC_BENCH_DRY_SLEEP", "0")))
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -53,7 +53,7 @@
 extern "C" {
 #endif
 
-#define USAC_ABI_VERSION 10
+#define USAC_ABI_VERSION 11
 
 /* = enum ESTIMATOR (usac/model.hpp:10) */
 enum { USAC_LINE2D = 1, USAC_HOMOGRAPHY = 2, USAC_FUNDAMENTAL = 3, USAC_ESSENTIAL = 4 };
@@ -285,6 +285,127 @@ int usac_prosac_samples(uint32_t seed, uint32_t n_points, uint32_t m, uint32_t c
 /* SPRT random pool after srandom(seed) (sprt.hpp:89-104; n_points glibc draws) and the
  * first test's threshold A (sprt.hpp:332-355) for `estimator`.  For parity tests. */
 int usac_sprt_pool(uint32_t seed, int estimator, uint32_t n_points, uint32_t m, uint32_t *pool, double *A0);
+
+/* ---- stateful plugins: the reference's per-call surface (ABI 11) ----------------------
+ * Handles that keep the reference's plugin state between calls, so a caller that keeps its
+ * own Ransac::run loop (ransac.cpp:58-139) swaps each plugin for the device one:
+ *   usac_random       the global glibc random() stream after srandom(seed) -- UniformSampler and
+ *                     NapsacSampler draw from it, the SPRT ctor shuffles its pool with it
+ *                     (uniform_sampler.hpp:22-54, array_random_generator.hpp:21-49, sprt.hpp:93-104)
+ *   usac_sampler      Sampler::generateSample (sampler.hpp:11-35): Uniform (persistent pool),
+ *                     PROSAC (growth function, termination length), NAPSAC (grid / KNN neighbours
+ *                     built on the context's device)
+ *   usac_termination  TerminationCriteria::getUpBoundIterations (termination_criteria.hpp:16-17) and
+ *                     ProsacTerminationCriteria::getUpBoundIterations(hypCount, model)
+ *                     (prosac_termination_criteria.hpp:148-201)
+ *   usac_sprt         SPRT::verifyModelAndGetModelScore (sprt.hpp:191-317), getUpperBoundIterations
+ *                     (sprt.hpp:371-393) and the batch replay of the loop body with SPRT
+ *   usac_lo           LocalOptimization::GetModelScore (local_optimization.hpp:19): inner + iterative
+ *                     LO-RANSAC or graph-cut LO
+ * A handle created on a context uses that context's device, stream and buffers: it must be
+ * destroyed before the context, and -- like the reference's plugins -- is not thread-safe.
+ * Handles drawing from a usac_random keep a pointer to it (destroy them first). */
+typedef struct usac_random usac_random;
+typedef struct usac_sampler usac_sampler;
+typedef struct usac_termination usac_termination;
+typedef struct usac_sprt usac_sprt;
+typedef struct usac_lo usac_lo;
+
+int usac_random_create(uint32_t seed, usac_random **out);
+uint32_t usac_random_next(usac_random *rng); /* random() */
+void usac_random_destroy(usac_random *rng);
+
+/* initSampler (ransac/init.cpp) for params->sampler:
+ *   USAC_SAMPLER_UNIFORM  UniformSampler on rng: m draws without replacement from a persistent
+ *                         pool, idx = random() % max, refilled when max reaches 0 (Q5)
+ *   USAC_SAMPLER_PROSAC   ProsacSampler, its mt19937 seeded with params->seed (the reference:
+ *                         std::random_device); points sorted by quality; sampling is limited to the
+ *                         termination length of the PROSAC termination criteria created on it
+ *                         (usac_termination_create), n before that (prosac_sampler.hpp:117-172)
+ *   USAC_SAMPLER_NAPSAC   NapsacSampler on rng with grid neighbours (params->neighbors ==
+ *                         USAC_NEIGHBORS_GRID, cell params->cell_size; 4-column points) or KNN
+ *                         (params->knn), both built on ctx's device (napsac_sampler.hpp:40-158)
+ * rng: required for Uniform / NAPSAC, ignored for PROSAC. */
+int usac_sampler_create(usac_ctx *ctx, const usac_params *params, usac_random *rng, usac_sampler **out);
+/* generateSample(sample): m indices into `sample`.  NAPSAC rewrites only sample[0] once it has
+ * turned uniform (as the reference), so pass the same array every call, as the loop does. */
+int usac_sampler_generate(usac_sampler *s, int32_t *sample);
+/* count successive generateSample calls into samples (count x m; each row starts as a copy of
+ * the previous one, the reference's reused sample array) */
+int usac_sampler_generate_batch(usac_sampler *s, uint32_t count, int32_t *samples);
+/* samples drawn so far; PROSAC: subset_size and largest_sample_size (else n, n) -- nullable */
+int usac_sampler_state(const usac_sampler *s, uint64_t *drawn, uint32_t *subset_size, uint32_t *largest_sample_size);
+void usac_sampler_destroy(usac_sampler *s);
+
+/* initTerminationCriteria: StandardTerminationCriteria (params->desired_prob, ->max_iterations;
+ * m and n from ctx), or -- prosac != NULL, a USAC_SAMPLER_PROSAC sampler -- ProsacTerminationCriteria
+ * linked to it both ways as in the reference (the sampler reads its termination length, it reads
+ * the sampler's growth function and largest sample size; prosac_termination_criteria.hpp:44-119). */
+int usac_termination_create(usac_ctx *ctx, const usac_params *params, usac_sampler *prosac, usac_termination **out);
+/* getUpBoundIterations(inlier_size) / (inlier_size, points_size) (standard_termination_criteria.hpp:
+ * 52-74); points_size 0 = the context's n */
+uint32_t usac_termination_bound(const usac_termination *t, uint32_t inlier_size, uint32_t points_size);
+/* ProsacTerminationCriteria::getUpBoundIterations(hypCount, model): the model's inlier flags at
+ * params->threshold over the quality-sorted points from the device, the non-randomness /
+ * maximality scan on the host.  *max_iters = the new bound, *termination_length (nullable) = the
+ * updated termination length (the linked sampler uses it from its next sample on). */
+int usac_prosac_termination(usac_termination *t, uint32_t hyp_count, const float *model, uint32_t *max_iters,
+                            uint32_t *termination_length);
+void usac_termination_destroy(usac_termination *t);
+
+/* SPRT ctor (sprt.hpp:89-175): the random pool from n draws of rng (the Ransac ctor creates it after
+ * the sampler, before the sampler's first draw), the reference's initial epsilon / delta / t_M / m_S
+ * for ctx's estimator; params->threshold, ->max_iterations. */
+int usac_sprt_create(usac_ctx *ctx, const usac_params *params, usac_random *rng, usac_sprt **out);
+/* verifyModelAndGetModelScore(model, current_hypothese, maximum_score, score), one model (9 floats;
+ * line: 3): the model's inlier flags in pool order from the device, the reference's fp64 lambda walk
+ * over the rolling pool index on the host.  *good = the decision; *count / *score written as the
+ * reference writes them (accepted: inliers, (float)inliers; rejected while current_hypothese <
+ * max_hypothesis_test_before_sprt = 20: the full count; otherwise left untouched). */
+int usac_sprt_verify(usac_sprt *s, const float *model, int32_t current_hypothese, uint32_t maximum_score,
+                     int32_t *good, int32_t *count, float *score);
+/* getUpperBoundIterations(inlier_size) (sprt.hpp:371-393) */
+uint32_t usac_sprt_upper_bound(const usac_sprt *s, uint32_t inlier_size);
+/* tests designed so far (sprt_histories.size()) and models rejected by this handle */
+int usac_sprt_stats(const usac_sprt *s, uint32_t *histories, uint32_t *rejected);
+
+/* The loop body of ransac.cpp:58-139 with SPRT over a batch of minimal samples (SURVEY §8(b)
+ * usac_sprt_replay).  State in / out: */
+typedef struct usac_sprt_state {
+    uint32_t iters;        /* in/out: the loop's iteration counter (ransac.cpp:55) */
+    uint32_t max_iters;    /* in: the bound in force (`while (iters < max_iters)`) */
+    int32_t best_inliers;  /* in: best_score->inlier_number */
+    float best_score;      /* in: best_score->score */
+    uint32_t sample;       /* in/out cursor: the next sample of the batch ... */
+    uint32_t slot;         /* ... and model slot to verify; (0, 0) starts a new batch */
+    int32_t found;         /* out: 1 = stopped after a model bigger than the best (Score::bigger) */
+    int32_t inliers;       /* out: that model's score (the caller updates its best, runs LO and */
+    float score;           /*      the termination, sets max_iters / best_* and calls again) */
+    uint32_t found_sample, found_slot;
+    uint32_t rejected;     /* out: models rejected during this call */
+} usac_sprt_state;
+/* models: B x slots x 9 floats and n_models[B] (usac_estimate_models' layout; slots = 3 for the
+ * 7-point solver, else 1).  From the cursor, in loop order: verify(model, iters, best_inliers); a
+ * rejected model at iters >= 20 counts an iteration and is skipped (Q9); every other model is
+ * compared with the best; after each sample iters++; before each sample `iters < max_iters` is
+ * checked.  Returns with found = 1 at the first model bigger than the best (the cursor then points
+ * past it), or found = 0 when the batch is exhausted (sample == B) or the loop bound is reached
+ * (iters >= max_iters).  The batch's inlier words are computed on the device when the cursor is at
+ * (0, 0); later calls for the same batch must pass the same models. */
+int usac_sprt_replay(usac_sprt *s, const float *models, const int32_t *n_models, uint32_t B, usac_sprt_state *st);
+void usac_sprt_destroy(usac_sprt *s);
+
+/* initLocalOptimization for params->lo: USAC_LO_INITLORSC / _INITFLORSC (InnerLocalOptimization with
+ * IterativeLocalOptimization, unlimited / limited; inner_local_optimization.hpp:40-133,
+ * iterative_local_optimization.hpp:28-136; its mt19937 seeded with params->seed + 1) or USAC_LO_GC
+ * (GraphCut, graphcut.hpp:99-153, KNN or grid neighbours built on ctx's device; params->neighbors,
+ * ->knn, ->cell_size, ->spatial_coherence_gc).  The LO threshold persists across calls (Q11). */
+int usac_lo_create(usac_ctx *ctx, const usac_params *params, usac_lo **out);
+/* GetModelScore(best_model, best_score): model (9 floats), inliers and score improved in place */
+int usac_lo_get_model_score(usac_lo *lo, float *model, int32_t *inliers, float *score);
+/* lo_inner_iters / lo_iterative_iters (InnerLocalOptimization), or gc_iterations / labellings (GC) */
+int usac_lo_iters(const usac_lo *lo, uint32_t *inner, uint32_t *iterative);
+void usac_lo_destroy(usac_lo *lo);
 
 /* ---- multi-GPU (RCCL over xGMI) --------------------------------------------------- */
 /* 128-byte RCCL unique id (rank 0 creates, everyone receives it out of band). */

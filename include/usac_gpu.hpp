@@ -15,6 +15,13 @@
  *                            points); run(); getRansacOutput()), the loop on the device
  *                            (usac_ransac_run), or hypothesis-sharded over ranks (runSharded)
  *   usac_gpu::Context        one usac_ctx (device, HIP stream, resident points)
+ *   usac_gpu::RandomGenerator  the global glibc random() stream the samplers / SPRT share
+ *   usac_gpu::Sampler        usac/sampler/sampler.hpp:11-35 (Uniform / Prosac / Napsac)
+ *   usac_gpu::TerminationCriteria, ProsacTerminationCriteria
+ *                            termination_criteria.hpp:16-17, prosac_termination_criteria.hpp:44-201
+ *   usac_gpu::SPRT           usac/sprt.hpp:89-491 (verifyModelAndGetModelScore,
+ *                            getUpperBoundIterations; replay = usac_sprt_replay)
+ *   usac_gpu::LocalOptimization  local_optimization.hpp:19 (InItLORsc / InItFLORsc / GC)
  *
  * Errors: the C-ABI's negative status codes become usac_gpu::Error (code + usac_last_error);
  * USAC_ERR_NO_MODEL (-111) is the reference's exit(111) of ransac.cpp:143-147.
@@ -84,6 +91,7 @@ public:
     ESTIMATOR estimator = NullE;
     SAMPLER sampler = NullS;
     bool sprt = false;
+    unsigned int max_hypothesis_test_before_sprt = 20;
     NeighborsSearch neighborsType = NullN;
     int cell_size = 50;
     bool reset_random_generator = true;
@@ -280,6 +288,161 @@ public:
 
 private:
     unsigned int modelFloats() const { return estimator->context().estimator() == Line2d ? 3u : 9u; }
+};
+
+// ---- the stateful plugins (usac_gpu.h ABI 11): what a caller keeping its own loop swaps in ----
+
+// The reference's global glibc random() stream (srand(seed)): UniformSampler / NapsacSampler draw
+// from it and the SPRT ctor shuffles its pool with it (uniform_sampler.hpp:22-54, sprt.hpp:93-104).
+class RandomGenerator {
+public:
+    explicit RandomGenerator(uint32_t seed) {
+        if (usac_random_create(seed, &h_) != USAC_OK) throw Error(USAC_ERR_ARG, "usac_random_create");
+    }
+    ~RandomGenerator() { usac_random_destroy(h_); }
+    RandomGenerator(const RandomGenerator &) = delete;
+    RandomGenerator &operator=(const RandomGenerator &) = delete;
+    uint32_t next() { return usac_random_next(h_); }
+    usac_random *get() const { return h_; }
+
+private:
+    usac_random *h_ = nullptr;
+};
+
+// usac/sampler/sampler.hpp:11-35, built as initSampler builds it for model.sampler: UniformSampler
+// (persistent pool on rng), ProsacSampler (mt19937 seeded with model.seed), NapsacSampler (grid or KNN
+// neighbours built on the device, on rng)
+class Sampler {
+public:
+    Sampler(Context &ctx, const Model &model, RandomGenerator *rng) : ctx_(ctx) {
+        const usac_params p = model.params();
+        ctx_.check(usac_sampler_create(ctx_.get(), &p, rng ? rng->get() : nullptr, &h_), "Sampler");
+    }
+    virtual ~Sampler() { usac_sampler_destroy(h_); }
+    Sampler(const Sampler &) = delete;
+    Sampler &operator=(const Sampler &) = delete;
+    void generateSample(int *sample) { ctx_.check(usac_sampler_generate(h_, sample), "generateSample"); }
+    // count samples in a row (count x m; each row starts from the previous one, as the reused array)
+    void generateSamples(unsigned int count, int *samples) {
+        ctx_.check(usac_sampler_generate_batch(h_, count, samples), "generateSamples");
+    }
+    unsigned int getNumberOfIterations() const {
+        uint64_t d = 0;
+        usac_sampler_state(h_, &d, nullptr, nullptr);
+        return (unsigned int)d;
+    }
+    bool isInit() const { return h_ != nullptr; }
+    usac_sampler *get() const { return h_; }
+
+private:
+    Context &ctx_;
+    usac_sampler *h_ = nullptr;
+};
+
+// usac/termination_criteria/termination_criteria.hpp:16-17 (StandardTerminationCriteria)
+class TerminationCriteria {
+public:
+    TerminationCriteria(Context &ctx, const Model &model, Sampler *prosac_sampler = nullptr) : ctx_(ctx) {
+        const usac_params p = model.params();
+        ctx_.check(usac_termination_create(ctx_.get(), &p, prosac_sampler ? prosac_sampler->get() : nullptr, &h_),
+                   "TerminationCriteria");
+    }
+    virtual ~TerminationCriteria() { usac_termination_destroy(h_); }
+    TerminationCriteria(const TerminationCriteria &) = delete;
+    TerminationCriteria &operator=(const TerminationCriteria &) = delete;
+    unsigned int getUpBoundIterations(unsigned int inlier_size) { return usac_termination_bound(h_, inlier_size, 0); }
+    unsigned int getUpBoundIterations(unsigned int inlier_size, unsigned int points_size) {
+        return usac_termination_bound(h_, inlier_size, points_size);
+    }
+
+protected:
+    Context &ctx_;
+    usac_termination *h_ = nullptr;
+};
+
+// usac/termination_criteria/prosac_termination_criteria.hpp:44-201, linked to its PROSAC sampler
+class ProsacTerminationCriteria : public TerminationCriteria {
+public:
+    ProsacTerminationCriteria(Context &ctx, const Model &model, Sampler &prosac_sampler)
+        : TerminationCriteria(ctx, model, &prosac_sampler), termination_length(ctx.pointsSize()) {}
+    using TerminationCriteria::getUpBoundIterations;
+    // getUpBoundIterations(hypCount, model): the model's inliers over the quality-sorted points
+    unsigned int getUpBoundIterations(unsigned int hypCount, const Descriptor &model) {
+        uint32_t max_samples = 0;
+        ctx_.check(usac_prosac_termination(h_, hypCount, model.data(), &max_samples, &termination_length),
+                   "ProsacTerminationCriteria::getUpBoundIterations");
+        return max_samples;
+    }
+    unsigned int *getStoppingLength() { return &termination_length; }
+
+private:
+    unsigned int termination_length;
+};
+
+// usac/sprt.hpp:89-491
+class SPRT {
+public:
+    SPRT(Context &ctx, const Model &model, RandomGenerator &rng) : ctx_(ctx) {
+        const usac_params p = model.params();
+        ctx_.check(usac_sprt_create(ctx_.get(), &p, rng.get(), &h_), "SPRT");
+    }
+    ~SPRT() { usac_sprt_destroy(h_); }
+    SPRT(const SPRT &) = delete;
+    SPRT &operator=(const SPRT &) = delete;
+    // verifyModelAndGetModelScore(model, current_hypothese, maximum_score, score) (sprt.hpp:191-317)
+    bool verifyModelAndGetModelScore(const Descriptor &model, int current_hypothese, unsigned int maximum_score,
+                                     Score *score) {
+        int32_t good = 0;
+        ctx_.check(usac_sprt_verify(h_, model.data(), current_hypothese, maximum_score, &good, &score->inlier_number,
+                                    &score->score),
+                   "SPRT::verifyModelAndGetModelScore");
+        return good != 0;
+    }
+    unsigned int getUpperBoundIterations(int inlier_size) { return usac_sprt_upper_bound(h_, (uint32_t)inlier_size); }
+    // the batch form of the loop body (usac_sprt_replay): models B x slots x 9, n_models[B]
+    bool replay(const float *models, const int *n_models, unsigned int B, usac_sprt_state &state) {
+        ctx_.check(usac_sprt_replay(h_, models, n_models, B, &state), "SPRT::replay");
+        return state.found != 0;
+    }
+    unsigned int histories() const {
+        uint32_t h = 0;
+        usac_sprt_stats(h_, &h, nullptr);
+        return h;
+    }
+
+private:
+    Context &ctx_;
+    usac_sprt *h_ = nullptr;
+};
+
+// usac/local_optimization/local_optimization.hpp:19, built as initLocalOptimization builds it for
+// model.lo (InItLORsc / InItFLORsc: inner + iterative LO-RANSAC; GC: graph cut)
+class LocalOptimization {
+public:
+    LocalOptimization(Context &ctx, const Model &model) : ctx_(ctx) {
+        const usac_params p = model.params();
+        ctx_.check(usac_lo_create(ctx_.get(), &p, &h_), "LocalOptimization");
+    }
+    ~LocalOptimization() { usac_lo_destroy(h_); }
+    LocalOptimization(const LocalOptimization &) = delete;
+    LocalOptimization &operator=(const LocalOptimization &) = delete;
+    void GetModelScore(Model *best_model, Score *best_score) {
+        Descriptor d = best_model->returnDescriptor();
+        ctx_.check(usac_lo_get_model_score(h_, d.data(), &best_score->inlier_number, &best_score->score),
+                   "LocalOptimization::GetModelScore");
+        best_model->setDescriptor(d.data());
+    }
+    // (lo_inner_iters, lo_iterative_iters) -- GC: (gc_iterations, labellings)
+    void iters(unsigned int &inner, unsigned int &iterative) const {
+        uint32_t a = 0, b = 0;
+        usac_lo_iters(h_, &a, &b);
+        inner = a;
+        iterative = b;
+    }
+
+private:
+    Context &ctx_;
+    usac_lo *h_ = nullptr;
 };
 
 // usac/ransac/ransac_output.hpp:11-99

@@ -16,6 +16,7 @@ import subprocess
 import numpy as np
 
 __all__ = ["ESTIMATOR", "SAMPLER", "LocOpt", "NeighborsSearch", "DLT", "Model", "Ransac", "RansacOutput", "Score", "Context", "Record",
+           "RandomGenerator", "Sampler", "TerminationCriteria", "SPRT", "LocalOptimization", "SprtState",
            "build", "lib", "std_termination", "uniform_samples", "prosac_samples", "sprt_pool", "UsacError"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -83,6 +84,14 @@ class _Params(ctypes.Structure):
                 ("spatial_coherence_gc", ctypes.c_float)]
 
 
+class SprtState(ctypes.Structure):
+    """usac_sprt_state (include/usac_gpu.h): the loop state in / out of usac_sprt_replay."""
+    _fields_ = [("iters", ctypes.c_uint32), ("max_iters", ctypes.c_uint32), ("best_inliers", ctypes.c_int32),
+                ("best_score", ctypes.c_float), ("sample", ctypes.c_uint32), ("slot", ctypes.c_uint32),
+                ("found", ctypes.c_int32), ("inliers", ctypes.c_int32), ("score", ctypes.c_float),
+                ("found_sample", ctypes.c_uint32), ("found_slot", ctypes.c_uint32), ("rejected", ctypes.c_uint32)]
+
+
 class _RunOutput(ctypes.Structure):
     _fields_ = [("model", ctypes.c_float * 9), ("inliers", ctypes.c_int32), ("iters", ctypes.c_uint32),
                 ("time_us", ctypes.c_int64), ("n_records", ctypes.c_int32), ("polish_passes", ctypes.c_int32),
@@ -105,6 +114,11 @@ ABI_SYMBOLS = [
     "usac_draw_samples", "usac_set_cell_size", "usac_grid_neighbors",
     "usac_comm_unique_id", "usac_comm_init", "usac_allgather_records", "usac_merge_records",
     "usac_exchange_best_async", "usac_exchange_best_wait",
+    "usac_random_create", "usac_random_next", "usac_random_destroy", "usac_sampler_create", "usac_sampler_generate",
+    "usac_sampler_generate_batch", "usac_sampler_state", "usac_sampler_destroy", "usac_termination_create",
+    "usac_termination_bound", "usac_prosac_termination", "usac_termination_destroy", "usac_sprt_create",
+    "usac_sprt_verify", "usac_sprt_upper_bound", "usac_sprt_stats", "usac_sprt_replay", "usac_sprt_destroy",
+    "usac_lo_create", "usac_lo_get_model_score", "usac_lo_iters", "usac_lo_destroy",
 ]
 
 
@@ -176,6 +190,28 @@ def lib():
         "usac_exchange_best_async": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32]),
         "usac_exchange_best_wait": (ctypes.c_int, [_vp, ctypes.c_uint32, _P(Record)]),
         "usac_merge_records": (ctypes.c_int, [_P(Record), ctypes.c_uint32, _P(Record)]),
+        "usac_random_create": (ctypes.c_int, [ctypes.c_uint32, _P(_vp)]),
+        "usac_random_next": (ctypes.c_uint32, [_vp]),
+        "usac_random_destroy": (None, [_vp]),
+        "usac_sampler_create": (ctypes.c_int, [_vp, _P(_Params), _vp, _P(_vp)]),
+        "usac_sampler_generate": (ctypes.c_int, [_vp, i32p]),
+        "usac_sampler_generate_batch": (ctypes.c_int, [_vp, ctypes.c_uint32, i32p]),
+        "usac_sampler_state": (ctypes.c_int, [_vp, _P(ctypes.c_uint64), u32p, u32p]),
+        "usac_sampler_destroy": (None, [_vp]),
+        "usac_termination_create": (ctypes.c_int, [_vp, _P(_Params), _vp, _P(_vp)]),
+        "usac_termination_bound": (ctypes.c_uint32, [_vp, ctypes.c_uint32, ctypes.c_uint32]),
+        "usac_prosac_termination": (ctypes.c_int, [_vp, ctypes.c_uint32, f32p, u32p, u32p]),
+        "usac_termination_destroy": (None, [_vp]),
+        "usac_sprt_create": (ctypes.c_int, [_vp, _P(_Params), _vp, _P(_vp)]),
+        "usac_sprt_verify": (ctypes.c_int, [_vp, f32p, ctypes.c_int32, ctypes.c_uint32, i32p, i32p, f32p]),
+        "usac_sprt_upper_bound": (ctypes.c_uint32, [_vp, ctypes.c_uint32]),
+        "usac_sprt_stats": (ctypes.c_int, [_vp, u32p, u32p]),
+        "usac_sprt_replay": (ctypes.c_int, [_vp, f32p, i32p, ctypes.c_uint32, _P(SprtState)]),
+        "usac_sprt_destroy": (None, [_vp]),
+        "usac_lo_create": (ctypes.c_int, [_vp, _P(_Params), _P(_vp)]),
+        "usac_lo_get_model_score": (ctypes.c_int, [_vp, f32p, i32p, f32p]),
+        "usac_lo_iters": (ctypes.c_int, [_vp, u32p, u32p]),
+        "usac_lo_destroy": (None, [_vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -597,6 +633,17 @@ class RansacOutput:
         return self._lo
 
 
+def _params(m):
+    """usac_params of a Model (the fields the device loop and the plugins read)."""
+    seed = m.seed
+    if m.reset_random_generator and seed == 0:
+        seed = int.from_bytes(os.urandom(4), "little") or 1
+    return _Params(m.threshold, m.desired_prob, m.max_iterations, seed, int(m.dlt_mode), m.batch, int(m.sampler),
+                   1 if m.sprt else 0, int(m.lo), m.lo_sample_size, m.lo_iterative_iterations,
+                   m.lo_inner_iterations, m.lo_threshold_multiplier, m.cell_size, int(m.neighborsType),
+                   m.k_nearest_neighbors, m.spatial_coherence_gc)
+
+
 # usac_allgather_fn (include/usac_gpu.h)
 _ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p)
 
@@ -621,14 +668,7 @@ class Ransac:
         gather(bytes) -> list of nranks bytes objects in rank order (e.g. a gloo all_gather), or
         gather = "rccl" for the communicator set up with Context.comm_init."""
         L = lib()
-        m = self.model
-        seed = m.seed
-        if m.reset_random_generator and seed == 0:
-            seed = int.from_bytes(os.urandom(4), "little") or 1
-        p = _Params(m.threshold, m.desired_prob, m.max_iterations, seed, int(m.dlt_mode), m.batch, int(m.sampler),
-                    1 if m.sprt else 0, int(m.lo), m.lo_sample_size, m.lo_iterative_iterations,
-                    m.lo_inner_iterations, m.lo_threshold_multiplier, m.cell_size, int(m.neighborsType),
-                    m.k_nearest_neighbors, m.spatial_coherence_gc)
+        p = _params(self.model)
         out = _RunOutput()
         inl = np.zeros(self.ctx.n, dtype=np.int32)
         recs = (Record * rec_cap)()
@@ -670,3 +710,179 @@ class Ransac:
 
     def getRansacOutput(self):
         return self._out
+
+
+# --------------------------------------------------------------------------- stateful plugins
+# The reference's per-call plugin surface (include/usac_gpu.h, ABI 11): a caller that keeps its own
+# Ransac::run loop (ransac.cpp:58-139) swaps plugin by plugin.  Every handle created on a Context
+# must be closed before it (close(), or garbage collection in creation-reverse order).
+class _Handle:
+    _destroy = None
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h:
+            getattr(lib(), self._destroy)(h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+class RandomGenerator(_Handle):
+    """The reference's global glibc random() stream after srandom(seed) (usac_random)."""
+    _destroy = "usac_random_destroy"
+
+    def __init__(self, seed):
+        h = _vp()
+        rc = lib().usac_random_create(int(seed), ctypes.byref(h))
+        if rc:
+            raise UsacError(rc, "usac_random_create")
+        self._h = h
+
+    def next(self):
+        return int(lib().usac_random_next(self._h))
+
+
+class Sampler(_Handle):
+    """Sampler::generateSample (sampler.hpp:11-35) as initSampler builds it for model.sampler: Uniform
+    (persistent pool on rng), Prosac (own mt19937 seeded with model.seed), Napsac (grid or KNN
+    neighbours built on the device, on rng)."""
+    _destroy = "usac_sampler_destroy"
+
+    def __init__(self, ctx, model, rng=None):
+        h = _vp()
+        self.ctx, self.rng = ctx, rng  # kept alive while the handle draws from them
+        self._p = _params(model)
+        ctx._check(lib().usac_sampler_create(ctx._h, ctypes.byref(self._p), rng._h if rng is not None else None,
+                                             ctypes.byref(h)), "sampler_create")
+        self._h = h
+        self.m = ctx.m
+        self._sample = np.zeros(self.m, dtype=np.int32)  # the loop's reused `int sample[m]`
+
+    def generateSample(self):
+        self.ctx._check(lib().usac_sampler_generate(self._h, _ptr(self._sample, ctypes.c_int32)), "generateSample")
+        return self._sample.copy()
+
+    def generateSamples(self, count):
+        out = np.zeros((int(count), self.m), dtype=np.int32)
+        self.ctx._check(lib().usac_sampler_generate_batch(self._h, int(count), _ptr(out, ctypes.c_int32)),
+                        "generateSamples")
+        return out
+
+    def state(self):
+        d, sub, lg = ctypes.c_uint64(0), ctypes.c_uint32(0), ctypes.c_uint32(0)
+        self.ctx._check(lib().usac_sampler_state(self._h, ctypes.byref(d), ctypes.byref(sub), ctypes.byref(lg)),
+                        "sampler_state")
+        return {"drawn": int(d.value), "subset_size": int(sub.value), "largest_sample_size": int(lg.value)}
+
+
+class TerminationCriteria(_Handle):
+    """StandardTerminationCriteria, or ProsacTerminationCriteria when built on a Prosac Sampler
+    (linked both ways as in the reference)."""
+    _destroy = "usac_termination_destroy"
+
+    def __init__(self, ctx, model, prosac_sampler=None):
+        h = _vp()
+        self.ctx, self.sampler = ctx, prosac_sampler
+        self._p = _params(model)
+        ctx._check(lib().usac_termination_create(ctx._h, ctypes.byref(self._p),
+                                                 prosac_sampler._h if prosac_sampler is not None else None,
+                                                 ctypes.byref(h)), "termination_create")
+        self._h = h
+        self.termination_length = ctx.n
+
+    def getUpBoundIterations(self, a, b=None):
+        """(inlier_size[, points_size]) -> standard bound; (hypCount, model array) -> PROSAC's
+        getUpBoundIterations(hypCount, model) (prosac_termination_criteria.hpp:148-201)."""
+        if b is None or np.ndim(b) == 0:
+            return int(lib().usac_termination_bound(self._h, int(a), int(b or 0)))
+        m = np.zeros(9, dtype=np.float32)
+        mm = np.asarray(b, dtype=np.float32).reshape(-1)
+        m[: mm.size] = mm
+        mi, tl = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        self.ctx._check(lib().usac_prosac_termination(self._h, int(a), _ptr(m, ctypes.c_float), ctypes.byref(mi),
+                                                      ctypes.byref(tl)), "prosac_termination")
+        self.termination_length = int(tl.value)
+        return int(mi.value)
+
+
+class SPRT(_Handle):
+    """SPRT (sprt.hpp:89-491): pool shuffled from rng at construction, verifyModelAndGetModelScore,
+    getUpperBoundIterations, and the batch replay of the loop body (usac_sprt_replay)."""
+    _destroy = "usac_sprt_destroy"
+
+    def __init__(self, ctx, model, rng):
+        h = _vp()
+        self.ctx, self.rng = ctx, rng
+        self._p = _params(model)
+        ctx._check(lib().usac_sprt_create(ctx._h, ctypes.byref(self._p), rng._h, ctypes.byref(h)), "sprt_create")
+        self._h = h
+
+    def verifyModelAndGetModelScore(self, model, current_hypothese, maximum_score, score):
+        m = np.zeros(9, dtype=np.float32)
+        mm = np.asarray(model, dtype=np.float32).reshape(-1)
+        m[: mm.size] = mm
+        good = ctypes.c_int32(0)
+        cnt = ctypes.c_int32(score.inlier_number)
+        sc = ctypes.c_float(score.score)
+        self.ctx._check(lib().usac_sprt_verify(self._h, _ptr(m, ctypes.c_float), int(current_hypothese),
+                                               int(maximum_score), ctypes.byref(good), ctypes.byref(cnt),
+                                               ctypes.byref(sc)), "sprt_verify")
+        score.inlier_number, score.score = int(cnt.value), float(sc.value)
+        return bool(good.value)
+
+    def getUpperBoundIterations(self, inlier_size):
+        return int(lib().usac_sprt_upper_bound(self._h, int(inlier_size)))
+
+    def stats(self):
+        h, r = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        self.ctx._check(lib().usac_sprt_stats(self._h, ctypes.byref(h), ctypes.byref(r)), "sprt_stats")
+        return {"histories": int(h.value), "rejected": int(r.value)}
+
+    def replay(self, models, n_models, state):
+        """usac_sprt_replay over a batch (models B x slots x 9, n_models[B]); `state` a SprtState,
+        updated in place; returns state.found."""
+        m = np.ascontiguousarray(models, dtype=np.float32)
+        nm = np.ascontiguousarray(n_models, dtype=np.int32)
+        self.ctx._check(lib().usac_sprt_replay(self._h, _ptr(m, ctypes.c_float), _ptr(nm, ctypes.c_int32), len(nm),
+                                               ctypes.byref(state)), "sprt_replay")
+        return bool(state.found)
+
+
+class LocalOptimization(_Handle):
+    """LocalOptimization::GetModelScore (local_optimization.hpp:19) as initLocalOptimization builds it
+    for model.lo: InItLORsc / InItFLORsc (inner + iterative LO-RANSAC) or GC (graph cut)."""
+    _destroy = "usac_lo_destroy"
+
+    def __init__(self, ctx, model):
+        h = _vp()
+        self.ctx = ctx
+        self._p = _params(model)
+        ctx._check(lib().usac_lo_create(ctx._h, ctypes.byref(self._p), ctypes.byref(h)), "lo_create")
+        self._h = h
+
+    def GetModelScore(self, best_model, best_score):
+        """best_model: float32 array of 9 (line: 3) improved in place; best_score: a Score."""
+        m = np.zeros(9, dtype=np.float32)
+        m[: best_model.size] = best_model.reshape(-1)
+        cnt = ctypes.c_int32(best_score.inlier_number)
+        sc = ctypes.c_float(best_score.score)
+        self.ctx._check(lib().usac_lo_get_model_score(self._h, _ptr(m, ctypes.c_float), ctypes.byref(cnt),
+                                                      ctypes.byref(sc)), "lo_get_model_score")
+        best_model.reshape(-1)[:] = m[: best_model.size]
+        best_score.inlier_number, best_score.score = int(cnt.value), float(sc.value)
+
+    def iters(self):
+        a, b = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        self.ctx._check(lib().usac_lo_iters(self._h, ctypes.byref(a), ctypes.byref(b)), "lo_iters")
+        return int(a.value), int(b.value)

@@ -2693,3 +2693,439 @@ int usac_merge_records(const usac_record *recs, uint32_t n, usac_record *best) {
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- stateful plugins (ABI 11)
+// The reference's per-call plugin surface: handles that keep each plugin's state
+// between calls, so a caller that keeps its own Ransac::run loop swaps plugin by plugin.  The
+// state machines are usac_host.hpp's (the same ones ransac_run_impl replays with); every inlier
+// test, least-squares fit and neighbour build runs on the context's device.
+
+struct usac_random {
+    usac::GlibcRandom g;
+    explicit usac_random(uint32_t seed) : g(seed) {}
+};
+
+struct usac_sampler {
+    usac_ctx *c = nullptr;
+    int kind = USAC_SAMPLER_UNIFORM;
+    uint32_t n = 0, m = 0;
+    std::unique_ptr<usac::UniformSampler> uni;
+    std::unique_ptr<usac::ProsacSampler> pro;
+    std::unique_ptr<usac::GridNeighbors> grid;
+    std::unique_ptr<usac::NapsacSampler> nap;
+    std::vector<int32_t> knn_tab;
+    std::unique_ptr<usac::NapsacKnnSampler> napk;
+    usac_termination *term = nullptr;  // the linked ProsacTerminationCriteria (PROSAC)
+    uint64_t drawn = 0;
+    std::vector<int32_t> last;  // generate_batch: the reference's reused sample array
+};
+
+struct usac_termination {
+    usac_ctx *c = nullptr;
+    float thr = 0.f;
+    usac::StandardTerminationCriteria std_;
+    std::unique_ptr<usac::ProsacTerminationCriteria> pro;
+    usac_sampler *sampler = nullptr;
+    std::vector<uint8_t> flags;
+    std::vector<int32_t> inl;
+    usac_termination(usac_ctx *ctx, const usac_params *p)
+        : c(ctx), thr(p->threshold), std_(p->desired_prob, ctx->m, ctx->n, p->max_iterations) {}
+};
+
+struct usac_sprt {
+    usac_ctx *c = nullptr;
+    float thr = 0.f;
+    uint32_t nw = 0;
+    std::unique_ptr<usac::Sprt> s;
+    DevBuf pool_idx, pool_pts, masks;
+    std::vector<uint32_t> hmask;  // the current batch's words [nw][rows]
+    uint32_t rows = 0;
+    std::vector<int32_t> row_of;  // batch slot -> row (-1: empty slot)
+    uint32_t batch_B = 0, batch_slots = 0;
+    std::vector<uint32_t> wbuf;
+    uint32_t rejected = 0;
+    ~usac_sprt() {
+        (void)hipSetDevice(c->device);
+        (void)hipStreamSynchronize(c->stream);
+        pool_idx.release();
+        pool_pts.release();
+        masks.release();
+    }
+};
+
+struct usac_lo {
+    usac_ctx *c = nullptr;
+    std::unique_ptr<LoRansac> lo;
+    std::unique_ptr<GcLo> gc;
+    std::vector<int32_t> knn_tab;
+    std::unique_ptr<usac::GridNeighbors> grid;
+};
+
+namespace {
+
+// host models (K x 9, line: first 3 of each row) into the context's device model layout (H: H
+// and H^-1, [18][K]; F / E: [9][K]; line [3][K]), the layout the solve kernels leave
+int upload_models(usac_ctx *c, const float *models, uint32_t K) {
+    int rc = ensure_batch(c, K);
+    if (rc) return rc;
+    HIP_TRY(c, hipMemcpyAsync(c->hostmodels.p, models, sizeof(float) * 9 * (size_t)K, hipMemcpyHostToDevice,
+                              c->stream));
+    if (listed(c)) HIP_TRY(c, usac::launch_prepare_f(c->stream, c->hostmodels.as<float>(), K, c->models.as<float>()));
+    else if (is_h(c)) HIP_TRY(c, usac::launch_prepare_h(c->stream, c->hostmodels.as<float>(), K, c->models.as<float>()));
+    else HIP_TRY(c, usac::launch_prepare_line(c->stream, c->hostmodels.as<float>(), K, c->models.as<float>()));
+    return USAC_OK;
+}
+
+// pool-order inlier words of K host models into s->hmask ([nw][K], row = model)
+int sprt_masks(usac_sprt *s, const float *models, uint32_t K) {
+    usac_ctx *c = s->c;
+    HIP_TRY(c, hipSetDevice(c->device));
+    int rc = upload_models(c, models, K);
+    if (rc) return rc;
+    HIP_TRY(c, s->masks.reserve(sizeof(uint32_t) * s->nw * (size_t)K));
+    HIP_TRY(c, usac::launch_pool_mask(c->stream, c->estimator, s->pool_pts.p, c->n, c->models.as<float>(), K, nullptr,
+                                      nullptr, K, s->thr, s->masks.as<uint32_t>(), K));
+    s->hmask.resize((size_t)s->nw * K);
+    HIP_TRY(c, hipMemcpyAsync(s->hmask.data(), s->masks.p, sizeof(uint32_t) * s->nw * (size_t)K, hipMemcpyDeviceToHost,
+                              c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
+    s->rows = K;
+    return USAC_OK;
+}
+
+// the host walk of row r (sprt.hpp:191-317)
+bool sprt_walk(usac_sprt *s, uint32_t r, int32_t current_hypothese, uint32_t maximum_score, int &count, float &score) {
+    s->wbuf.resize(s->nw);
+    for (uint32_t w = 0; w < s->nw; w++) s->wbuf[w] = s->hmask[(size_t)w * s->rows + r];
+    const bool good = s->s->verify(s->wbuf.data(), current_hypothese, maximum_score, count, score);
+    if (!good) s->rejected++;
+    return good;
+}
+
+}  // namespace
+
+extern "C" {
+
+int usac_random_create(uint32_t seed, usac_random **out) {
+    if (!out) return USAC_ERR_ARG;
+    *out = new usac_random(seed);
+    return USAC_OK;
+}
+
+uint32_t usac_random_next(usac_random *rng) { return rng ? rng->g.next() : 0u; }
+
+void usac_random_destroy(usac_random *rng) { delete rng; }
+
+int usac_sampler_create(usac_ctx *c, const usac_params *p, usac_random *rng, usac_sampler **out) {
+    if (!c || !p || !out) return USAC_ERR_ARG;
+    *out = nullptr;
+    const int kind = p->sampler == 0 ? USAC_SAMPLER_UNIFORM : p->sampler;
+    if (kind != USAC_SAMPLER_UNIFORM && kind != USAC_SAMPLER_PROSAC && kind != USAC_SAMPLER_NAPSAC)
+        return fail(c, USAC_ERR_UNSUPPORTED, "sampler: Uniform, Napsac or Prosac");
+    if (kind != USAC_SAMPLER_PROSAC && !rng) return fail(c, USAC_ERR_ARG, "sampler: Uniform / NAPSAC draw from a usac_random");
+    std::unique_ptr<usac_sampler> s(new usac_sampler());
+    s->c = c;
+    s->kind = kind;
+    s->n = c->n;
+    s->m = c->m;
+    s->last.assign(c->m, 0);
+    if (kind == USAC_SAMPLER_PROSAC) {
+        if (c->n < c->m || c->m < 2) return fail(c, USAC_ERR_ARG, "PROSAC needs n >= sample size");
+        s->pro.reset(new usac::ProsacSampler(p->seed, c->n, c->m));
+    } else if (kind == USAC_SAMPLER_NAPSAC) {
+        HIP_TRY(c, hipSetDevice(c->device));
+        if (p->neighbors == USAC_NEIGHBORS_GRID) {
+            if (c->cols != 4) return fail(c, USAC_ERR_ARG, "NAPSAC grid neighbours need 4-column points (SURVEY Q17)");
+            if (p->cell_size <= 0) return fail(c, USAC_ERR_ARG, "NAPSAC cell_size must be > 0");
+            int rc = download_grid(c, p->cell_size, s->grid);
+            if (rc) return rc;
+            s->nap.reset(new usac::NapsacSampler(rng->g, *s->grid, c->n, c->m));
+        } else {
+            if (p->knn == 0 || p->knn > usac::kKnnMax || p->knn + 1 < c->m)
+                return fail(c, USAC_ERR_ARG, "NAPSAC KNN: k_nearest_neighbors must be in [sample_size - 1, 32]");
+            s->knn_tab.resize((size_t)c->n * p->knn);
+            int rc = usac_knn(c, p->knn, s->knn_tab.data(), nullptr);
+            if (rc) return rc;
+            s->napk.reset(new usac::NapsacKnnSampler(rng->g, s->knn_tab.data(), c->n, c->m, p->knn));
+        }
+    } else {
+        s->uni.reset(new usac::UniformSampler(rng->g, c->n, c->m));
+    }
+    *out = s.release();
+    return USAC_OK;
+}
+
+int usac_sampler_generate(usac_sampler *s, int32_t *sample) {
+    if (!s || !sample) return USAC_ERR_ARG;
+    if (s->pro) {
+        if (s->drawn >= usac::ProsacSampler::kGrowthMax)
+            return fail(s->c, USAC_ERR_UNSUPPORTED, "PROSAC: more than T_N = 200000 samples (the reference then "
+                                                    "draws outside the point range)");
+        s->pro->generateSample(sample, s->term && s->term->pro ? s->term->pro->terminationLength() : s->n);
+    } else if (s->nap) {
+        s->nap->generateSample(sample);
+    } else if (s->napk) {
+        s->napk->generateSample(sample);
+    } else {
+        s->uni->generateSample(sample);
+    }
+    s->drawn++;
+    return USAC_OK;
+}
+
+int usac_sampler_generate_batch(usac_sampler *s, uint32_t count, int32_t *samples) {
+    if (!s || (!samples && count)) return USAC_ERR_ARG;
+    for (uint32_t j = 0; j < count; j++) {
+        int32_t *smp = samples + (size_t)j * s->m;
+        memcpy(smp, s->last.data(), sizeof(int32_t) * s->m);
+        int rc = usac_sampler_generate(s, smp);
+        if (rc) return rc;
+        memcpy(s->last.data(), smp, sizeof(int32_t) * s->m);
+    }
+    return USAC_OK;
+}
+
+int usac_sampler_state(const usac_sampler *s, uint64_t *drawn, uint32_t *subset_size, uint32_t *largest) {
+    if (!s) return USAC_ERR_ARG;
+    if (drawn) *drawn = s->drawn;
+    if (subset_size) *subset_size = s->pro ? s->pro->subset() : s->n;
+    if (largest) *largest = s->pro ? s->pro->largest() : s->n;
+    return USAC_OK;
+}
+
+void usac_sampler_destroy(usac_sampler *s) {
+    if (!s) return;
+    if (s->term) s->term->sampler = nullptr;
+    delete s;
+}
+
+int usac_termination_create(usac_ctx *c, const usac_params *p, usac_sampler *prosac, usac_termination **out) {
+    if (!c || !p || !out) return USAC_ERR_ARG;
+    *out = nullptr;
+    if (prosac && (!prosac->pro || prosac->c != c))
+        return fail(c, USAC_ERR_ARG, "termination: the linked sampler must be a PROSAC sampler of this context");
+    if (prosac && prosac->term) return fail(c, USAC_ERR_ARG, "termination: the sampler is linked already");
+    if (prosac && c->n <= 20)
+        return fail(c, USAC_ERR_ARG, "PROSAC termination needs > 20 points (prosac_termination_criteria.hpp:158-163)");
+    std::unique_ptr<usac_termination> t(new usac_termination(c, p));
+    if (prosac) {
+        t->pro.reset(new usac::ProsacTerminationCriteria(prosac->pro->growth(), p->desired_prob, c->m, c->n,
+                                                         p->max_iterations));
+        t->sampler = prosac;
+        prosac->term = t.get();
+        t->flags.assign(c->n, 0);
+        t->inl.resize(c->n);
+    }
+    *out = t.release();
+    return USAC_OK;
+}
+
+uint32_t usac_termination_bound(const usac_termination *t, uint32_t inlier_size, uint32_t points_size) {
+    if (!t) return 0;
+    return t->std_.getUpBoundIterations(inlier_size, points_size ? points_size : t->c->n);
+}
+
+int usac_prosac_termination(usac_termination *t, uint32_t hyp_count, const float *model, uint32_t *max_iters,
+                            uint32_t *termination_length) {
+    if (!t || !model || !max_iters) return USAC_ERR_ARG;
+    usac_ctx *c = t->c;
+    if (!t->pro) return fail(c, USAC_ERR_ARG, "not a PROSAC termination criteria");
+    if (!t->sampler) return fail(c, USAC_ERR_ARG, "PROSAC termination: its sampler was destroyed");
+    uint32_t n = 0;
+    int rc = usac_get_inliers(c, model, t->thr, t->inl.data(), &n, nullptr);
+    if (rc) return rc;
+    std::fill(t->flags.begin(), t->flags.end(), 0);
+    for (uint32_t k = 0; k < n; k++) t->flags[t->inl[k]] = 1;
+    const std::vector<uint8_t> &f = t->flags;
+    *max_iters = t->pro->getUpBoundIterations(hyp_count, [&](uint32_t i) { return f[i] != 0; },
+                                              t->sampler->pro->largest());
+    if (termination_length) *termination_length = t->pro->terminationLength();
+    return USAC_OK;
+}
+
+void usac_termination_destroy(usac_termination *t) {
+    if (!t) return;
+    if (t->sampler) t->sampler->term = nullptr;
+    delete t;
+}
+
+int usac_sprt_create(usac_ctx *c, const usac_params *p, usac_random *rng, usac_sprt **out) {
+    if (!c || !p || !rng || !out) return USAC_ERR_ARG;
+    *out = nullptr;
+    HIP_TRY(c, hipSetDevice(c->device));
+    std::unique_ptr<usac_sprt> s(new usac_sprt());
+    s->c = c;
+    s->thr = p->threshold;
+    s->nw = (c->n + 31) / 32;
+    s->s.reset(new usac::Sprt(rng->g, c->estimator, c->n, c->m, p->max_iterations));
+    HIP_TRY(c, s->pool_idx.reserve(sizeof(uint32_t) * c->n));
+    HIP_TRY(c, s->pool_pts.reserve(sizeof(float) * c->cols * (size_t)c->n));
+    HIP_TRY(c, hipMemcpyAsync(s->pool_idx.p, s->s->pool().data(), sizeof(uint32_t) * c->n, hipMemcpyHostToDevice,
+                              c->stream));
+    HIP_TRY(c, usac::launch_gather_points(c->stream, c->pts.p, c->cols, s->pool_idx.as<uint32_t>(), c->n,
+                                          s->pool_pts.p));
+    HIP_TRY(c, stream_wait(c->stream));
+    *out = s.release();
+    return USAC_OK;
+}
+
+int usac_sprt_verify(usac_sprt *s, const float *model, int32_t current_hypothese, uint32_t maximum_score,
+                     int32_t *good, int32_t *count, float *score) {
+    if (!s || !model || !good || !count || !score) return USAC_ERR_ARG;
+    float m9[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    memcpy(m9, model, sizeof(float) * (size_t)ncomp(s->c));
+    s->batch_B = 0;  // a batch replay's words are gone
+    int rc = sprt_masks(s, m9, 1);
+    if (rc) return rc;
+    int cnt = *count;
+    float sc = *score;
+    *good = sprt_walk(s, 0, current_hypothese, maximum_score, cnt, sc) ? 1 : 0;
+    *count = cnt;
+    *score = sc;
+    return USAC_OK;
+}
+
+uint32_t usac_sprt_upper_bound(const usac_sprt *s, uint32_t inlier_size) {
+    return s ? s->s->getUpperBoundIterations((int)inlier_size) : 0u;
+}
+
+int usac_sprt_stats(const usac_sprt *s, uint32_t *histories, uint32_t *rejected) {
+    if (!s) return USAC_ERR_ARG;
+    if (histories) *histories = (uint32_t)s->s->histories();
+    if (rejected) *rejected = s->rejected;
+    return USAC_OK;
+}
+
+int usac_sprt_replay(usac_sprt *s, const float *models, const int32_t *n_models, uint32_t B, usac_sprt_state *st) {
+    if (!s || !models || !n_models || !st) return USAC_ERR_ARG;
+    usac_ctx *c = s->c;
+    const uint32_t S = c->spk;
+    if (st->sample > B || (st->sample < B && st->slot > S)) return fail(c, USAC_ERR_ARG, "sprt_replay: cursor out of range");
+    st->found = 0;
+    st->rejected = 0;
+    if (st->sample == 0 && st->slot == 0) {  // a new batch: every model's pool-order inlier words
+        std::vector<float> list;
+        s->row_of.assign((size_t)B * S, -1);
+        uint32_t K = 0;
+        for (uint32_t b = 0; b < B; b++) {
+            if (n_models[b] < 0 || (uint32_t)n_models[b] > S) return fail(c, USAC_ERR_ARG, "sprt_replay: n_models out of range");
+            for (uint32_t q = 0; q < (uint32_t)n_models[b]; q++) {
+                s->row_of[(size_t)b * S + q] = (int32_t)K++;
+                list.insert(list.end(), models + ((size_t)b * S + q) * 9, models + ((size_t)b * S + q + 1) * 9);
+            }
+        }
+        if (K) {
+            int rc = sprt_masks(s, list.data(), K);
+            if (rc) return rc;
+        }
+        s->batch_B = B;
+    } else if (s->batch_B != B) {
+        return fail(c, USAC_ERR_ARG, "sprt_replay: a batch resumes with the models it started with");
+    }
+    const uint32_t rej0 = s->rejected;
+    uint32_t b = st->sample, q = st->slot;
+    while (b < B) {
+        if (q == 0 && st->iters >= st->max_iters) break;  // while (iters < max_iters)
+        for (; q < (uint32_t)n_models[b]; q++) {
+            int cnt = 0;
+            float sc = 0.f;
+            const bool good = sprt_walk(s, (uint32_t)s->row_of[(size_t)b * S + q], (int)st->iters,
+                                        (uint32_t)st->best_inliers, cnt, sc);
+            if (!good && st->iters >= 20) {  // max_hypothesis_test_before_sprt (model.hpp:40), Q9
+                st->iters++;
+                continue;
+            }
+            usac::Score cur, best;
+            cur.inlier_number = cnt;
+            cur.score = sc;
+            best.inlier_number = st->best_inliers;
+            best.score = st->best_score;
+            if (cur.bigger(best)) {
+                st->found = 1;
+                st->inliers = cnt;
+                st->score = sc;
+                st->found_sample = b;
+                st->found_slot = q;
+                st->sample = b;
+                st->slot = q + 1;
+                st->rejected = s->rejected - rej0;
+                return USAC_OK;
+            }
+        }
+        st->iters++;
+        b++;
+        q = 0;
+    }
+    st->sample = b;
+    st->slot = 0;
+    st->rejected = s->rejected - rej0;
+    return USAC_OK;
+}
+
+void usac_sprt_destroy(usac_sprt *s) { delete s; }
+
+int usac_lo_create(usac_ctx *c, const usac_params *p, usac_lo **out) {
+    if (!c || !p || !out) return USAC_ERR_ARG;
+    *out = nullptr;
+    HIP_TRY(c, hipSetDevice(c->device));
+    int rc = ensure_single(c);
+    if (rc) return rc;
+    std::unique_ptr<usac_lo> h(new usac_lo());
+    h->c = c;
+    if (p->lo == USAC_LO_INITLORSC || p->lo == USAC_LO_INITFLORSC) {
+        if (p->lo_sample_size == 0 || p->lo_iterative_iterations == 0)
+            return fail(c, USAC_ERR_ARG, "LO parameters must be > 0");
+        h->lo.reset(new LoRansac(c, p, Shard()));
+        if ((rc = h->lo->reserve())) return rc;
+    } else if (p->lo == USAC_LO_GC) {
+        const bool knn = p->neighbors != USAC_NEIGHBORS_GRID;
+        if (knn) {
+            if (p->knn == 0 || p->knn > usac::kKnnMax) return fail(c, USAC_ERR_ARG, "GC KNN: k_nearest_neighbors must be in [1, 32]");
+            h->knn_tab.resize((size_t)c->n * p->knn);
+            if ((rc = usac_knn(c, p->knn, h->knn_tab.data(), nullptr))) return rc;
+        } else {
+            if (c->cols != 4 || p->cell_size <= 0)
+                return fail(c, USAC_ERR_ARG, "GC grid neighbours need 4-column points and cell_size > 0");
+            if ((rc = download_grid(c, p->cell_size, h->grid))) return rc;
+        }
+        h->gc.reset(new GcLo(c, p, knn ? h->knn_tab.data() : nullptr, p->knn, h->grid.get()));
+        if ((rc = h->gc->reserve())) return rc;
+    } else {
+        return fail(c, USAC_ERR_UNSUPPORTED, "LO: InItLORsc / InItFLORsc / GC only");
+    }
+    *out = h.release();
+    return USAC_OK;
+}
+
+int usac_lo_get_model_score(usac_lo *h, float *model, int32_t *inliers, float *score) {
+    if (!h || !model || !inliers || !score) return USAC_ERR_ARG;
+    HIP_TRY(h->c, hipSetDevice(h->c->device));
+    int cnt = *inliers;
+    float sum = *score;
+    if (h->lo) {
+        h->lo->run(model, cnt, sum);
+        if (h->lo->rc) return h->lo->rc;
+    } else {
+        h->gc->run(model, cnt, sum);
+        if (h->gc->rc) return h->gc->rc;
+    }
+    *inliers = cnt;
+    *score = sum;
+    return USAC_OK;
+}
+
+int usac_lo_iters(const usac_lo *h, uint32_t *inner, uint32_t *iterative) {
+    if (!h) return USAC_ERR_ARG;
+    if (inner) *inner = h->lo ? h->lo->inner_count : h->gc->gc_iters;
+    if (iterative) *iterative = h->lo ? h->lo->iterative_count : h->gc->labelings;
+    return USAC_OK;
+}
+
+void usac_lo_destroy(usac_lo *h) {
+    if (!h) return;
+    (void)hipSetDevice(h->c->device);
+    (void)hipStreamSynchronize(h->c->stream);
+    delete h;
+}
+
+}  // extern "C"

@@ -72,3 +72,13 @@ def test_cpp_consumer_compiles_and_links(usac):
     assert r.returncode == 0, r.stderr
     d = json.loads(r.stdout)
     assert d["abi"] == d["header"] == usac.lib().usac_abi_version()
+
+
+def test_random_handle_is_the_glibc_stream(usac, oracle):
+    """usac_random (the reference's global random() after srandom(seed)) needs no GPU."""
+    for seed in (1, 7, 123456):
+        with usac.RandomGenerator(seed) as r:
+            got = [r.next() for _ in range(500)]
+        assert got == oracle.glibc_stream(seed, 500).tolist()
+    with usac.RandomGenerator(1) as r:
+        assert [r.next(), r.next()] == [1804289383, 846930886]  # glibc KAT (SURVEY §8(c) 1)

@@ -103,3 +103,48 @@ def test_cpp_quality_and_estimator_equal_oracle(oracle, tmp_path, kind):
     assert out["nonminimal"] == _bits(o.nonminimal(idx0)).tolist()
     assert out["est_n"] == onm.tolist() == out["batch_est_n"]
     assert out["est_models"] == _bits(om).reshape(-1).tolist() == out["batch_est_models"]
+
+
+# the reference's own loop body (ransac.cpp:58-139 + the polish :157-214) in
+# C++ against usac_gpu::Sampler / GpuEstimator / GpuQuality / SPRT / TerminationCriteria /
+# ProsacTerminationCriteria / LocalOptimization -- one plugin call per model ("loop"), or samples
+# drawn and solved 64 at a time with SPRT::replay walking the batch ("batched").
+LOOP_CASES = {  # estimator id, data, threshold, sampler, sprt, lo, neighbors
+    "H_uniform": (2, "H", 2.0, 1, 0, 0, 0),
+    "H_uniform_sprt": (2, "H", 2.0, 1, 1, 0, 0),
+    "H_prosac": (2, "H", 2.0, 4, 0, 0, 0),
+    "F_prosac_sprt": (3, "F", 2.0, 4, 1, 0, 0),
+    "F_uniform_sprt": (3, "F", 2.0, 1, 1, 0, 0),
+    "L_uniform_lo": (1, "L", 8.0, 1, 0, 1, 0),
+    "L_uniform_sprt_lo": (1, "L", 8.0, 1, 1, 1, 0),
+    "H_napsac_lo": (2, "Hc", 2.0, 3, 0, 1, 2),
+    "H_uniform_gc_knn": (2, "H", 2.0, 1, 0, 3, 1),
+}
+
+
+@pytest.mark.parametrize("mode", ["loop", "batched"])
+@pytest.mark.parametrize("case", sorted(LOOP_CASES))
+def test_cpp_reference_loop_body_equals_oracle(oracle, tmp_path, case, mode):
+    est, kind, thr, sampler, sprt, lo, nb = LOOP_CASES[case]
+    pts = np.ascontiguousarray(_data(kind), dtype=np.float32)
+    pts.tofile(tmp_path / "pts.f32")
+    seed = 4
+    out = _consumer(["loop", est, len(pts), "pts.f32", thr, 0.95, seed, sampler, sprt, lo, nb, mode], tmp_path)
+    okind = {1: oracle.LINE2D, 2: oracle.HOMOGRAPHY, 3: oracle.FUNDAMENTAL}[est]
+    osmp = {1: oracle.SAMPLER_UNIFORM, 3: oracle.SAMPLER_NAPSAC, 4: oracle.SAMPLER_PROSAC}[sampler]
+    ref = oracle.ransac_run(okind, pts, thr, 0.95, seed, sampler=osmp, sprt=bool(sprt), lo=lo,
+                            neighbors=oracle.NEIGHBORS_GRID if nb == 2 else oracle.NEIGHBORS_NANOFLANN)
+    recs = np.array(out["records"], dtype=np.int64).reshape(-1, 3)
+    assert [(int(i), int(c)) for i, c, _ in recs] == [(i, c) for i, c, _ in ref["records"]]
+    assert [int(b) for b in recs[:, 2]] == [int(np.float32(s).view(np.int32)) for _, _, s in ref["records"]]
+    assert out["iters"] == ref["iters"]
+    assert out["inliers"] == ref["inliers"]
+    nm = 3 if est == 1 else 9
+    assert out["model"] == _bits(ref["model"][:nm]).tolist()
+    assert out["inlier_idx"] == ref["inlier_idx"].tolist()
+    if lo:
+        assert out["lo_inner"] == ref["lo_inner_iters"] and out["lo_iterative"] == ref["lo_iterative_iters"]
+    if sprt:
+        assert out["sprt_histories"] == ref["sprt_histories"]
+    if sampler == 4:
+        assert out["termination_length"] == ref["prosac_term_len"]
