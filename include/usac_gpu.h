@@ -39,6 +39,12 @@
  *                                  ransac_output.hpp:29-97), Uniform sampler
  *   usac_ransac_run_sharded        Ransac::run with hypothesis-sharded batches
  *   usac_comm_*                    new: one RCCL all-gather of best records per batch
+ *   usac_random / usac_sampler /   the per-call plugin state (ABI 11): the glibc random() stream,
+ *   usac_termination / usac_sprt / Sampler::generateSample (sampler.hpp:11-35), TerminationCriteria
+ *   usac_lo                        (termination_criteria.hpp:16-17, prosac_termination_criteria.hpp:
+ *                                  148-201), SPRT (sprt.hpp:191-393, + the batch replay
+ *                                  usac_sprt_replay), LocalOptimization::GetModelScore
+ *                                  (local_optimization.hpp:19)
  *
  * Threading: a context is bound to one device and one HIP stream and is not
  * thread-safe (one host thread / process per GPU).  Calls are synchronous with respect
@@ -134,6 +140,9 @@ typedef struct usac_run_output {
     uint32_t sum_models;        /* models whose exact sequential Σerr the replay needed */
     uint32_t lo_fits;           /* LO least-squares fits this rank ran (a sharded run splits the
                                    inner-iteration chains: the ranks' counts add up to the 1-rank run's) */
+    uint32_t spec_batches;      /* batches drawn and solved ahead of the replay (speculation) */
+    uint32_t spec_rollbacks;    /* of those, cut short by a smaller termination bound (sampler rolled back) */
+    uint32_t spec_wasted;       /* hypotheses solved and scored ahead that the run never reached */
 } usac_run_output;
 
 /* ---- lifetime ----------------------------------------------------------------- */
@@ -193,7 +202,8 @@ int usac_hypothesize_score(usac_ctx *ctx, const int32_t *samples, uint32_t B, ui
 int usac_hypothesize_async(usac_ctx *ctx, uint32_t B, uint64_t seed, uint64_t first_hyp, float thr);
 int usac_fetch_best(usac_ctx *ctx, usac_record *best);
 /* Per-slot counts / sums (sums nullable) of the last batch as the score kernel left them (the
- * throughput kernels' chunked sums included): n <= B x slots.  Waits for the stream.  For tests. */
+ * throughput kernels' chunked sums included): n <= B x slots.  Waits for the stream.  For tests.
+ * USAC_ERR_ARG after a usac_ransac_run until the next batch (the run's buffers are not a batch's). */
 int usac_last_counts(usac_ctx *ctx, int32_t *counts, float *sums, uint32_t n);
 int usac_sync(usac_ctx *ctx);
 /* Device time of the last async batch's kernels, measured with HIP events on the
@@ -419,7 +429,10 @@ int usac_allgather_records(usac_ctx *ctx, const usac_record *local, usac_record 
  * waits for the other's later work; no host staging), then copied to pinned host memory.
  * `slot` (< USAC_XRING) names the exchange in a ring; usac_exchange_best_wait(slot) returns
  * the nranks records (rank order) and frees the slot: at most USAC_XRING exchanges may be
- * outstanding.  Every rank must issue the exchanges in the same order.
+ * outstanding.  Every rank must issue the exchanges -- and the context's other collectives
+ * (usac_allgather_records, sharded runs on its communicator) -- in the same order; the two kinds
+ * may be mixed: a collective on the context stream waits for the exchanges issued before it, an
+ * exchange for the context-stream collectives issued before it (events, no host wait).
  * batch may be ctx itself or another context on the same device. */
 #define USAC_XRING 8
 int usac_exchange_best_async(usac_ctx *ctx, usac_ctx *batch, uint32_t slot);

@@ -100,7 +100,8 @@ class _RunOutput(ctypes.Structure):
                 ("prosac_term_len", ctypes.c_uint32), ("rollbacks", ctypes.c_uint32),
                 ("lo_inner_iters", ctypes.c_uint32), ("lo_iterative_iters", ctypes.c_uint32),
                 ("lo_rounds", ctypes.c_uint32), ("lo_stages", ctypes.c_uint32), ("sum_models", ctypes.c_uint32),
-                ("lo_fits", ctypes.c_uint32)]
+                ("lo_fits", ctypes.c_uint32), ("spec_batches", ctypes.c_uint32), ("spec_rollbacks", ctypes.c_uint32),
+                ("spec_wasted", ctypes.c_uint32)]
 
 
 # every symbol include/usac_gpu.h declares (checked by tests/test_abi.py)
@@ -704,7 +705,8 @@ class Ransac:
                "sprt_histories": out.sprt_histories, "prosac_term_len": out.prosac_term_len,
                "rollbacks": out.rollbacks, "lo_iterative_iters": out.lo_iterative_iters,
                "lo_rounds": out.lo_rounds, "lo_stages": out.lo_stages, "sum_models": out.sum_models,
-               "lo_fits": out.lo_fits}
+               "lo_fits": out.lo_fits, "spec_batches": out.spec_batches, "spec_rollbacks": out.spec_rollbacks,
+               "spec_wasted": out.spec_wasted}
         self._out = RansacOutput(np.array(out.model[:], dtype=np.float32), inl[: out.inliers].copy(), out.time_us,
                                  out.inliers, out.iters, raw, out.lo_inner_iters)
 

@@ -44,6 +44,11 @@ constexpr uint32_t kPartPts = 1024;      // points per K2/K3 block (4 per thread
 constexpr uint32_t kSmallCell = 16;      // cells up to this size are ranked by one lane
 constexpr uint32_t kBmWords = 8192;      // LDS bitmap chunk of K6: 262 144 indices
 constexpr uint32_t kBigBlocks = 256;
+// k_grid_big holds the bitmap and its per-word prefix (2 x 32 KiB) plus 16 B in LDS: 65 552 B per
+// workgroup, above the 64 KiB of gfx90a / gfx942 and within gfx950's 160 KiB (MI355X_MICROARCH.md).
+// This build targets gfx950 only (ransac_amd/Makefile ARCH); the bound is checked here.
+static_assert(2 * kBmWords * sizeof(uint32_t) + 4 * sizeof(uint32_t) <= 160 * 1024,
+              "k_grid_big's LDS exceeds gfx950's 160 KiB per workgroup");
 
 __device__ __forceinline__ uint32_t hash_slot(uint64_t k, uint32_t mask) {
     k ^= k >> 33;

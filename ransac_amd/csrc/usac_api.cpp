@@ -315,9 +315,16 @@ struct usac_ctx {
     DevBuf xring;
     usac_record *xring_host = nullptr;
     size_t xring_host_bytes = 0;
+    // collectives on one communicator must run in one order on every rank: the two streams
+    // that issue them are ordered by events -- a collective on `stream` waits for the last
+    // exchange (x_last), an exchange waits for the last collective on `stream` (coll_ev)
+    int x_last = -1;
+    hipEvent_t coll_ev = nullptr;
+    bool coll_pending = false;
     // timing
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float last_ms[3] = {0, 0, 0};
+    bool batch_valid = false;  // counts / sums hold a batch's scores (usac_last_counts)
     bool timed_pending = false;
     std::string err;
 };
@@ -342,6 +349,19 @@ int fail(usac_ctx *c, int code, const std::string &msg) {
         if (r_ != ncclSuccess)                                                                     \
             return fail((ctx), USAC_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
     } while (0)
+
+// before a collective on c->stream: after every exchange issued on the exchange stream
+hipError_t order_after_exchanges(usac_ctx *c) {
+    if (c->xstream && c->x_last >= 0) return hipStreamWaitEvent(c->stream, c->xev_done[c->x_last], 0);
+    return hipSuccess;
+}
+// after a collective on c->stream: later exchanges wait for it
+hipError_t mark_collective(usac_ctx *c) {
+    if (!c->coll_ev) return hipSuccess;
+    hipError_t e = hipEventRecord(c->coll_ev, c->stream);
+    if (e == hipSuccess) c->coll_pending = true;
+    return e;
+}
 
 bool is_h(const usac_ctx *c) { return c->estimator == USAC_HOMOGRAPHY; }
 bool is_f(const usac_ctx *c) { return c->estimator == USAC_FUNDAMENTAL; }
@@ -407,34 +427,71 @@ usac::DevSampler dev_sampler(const usac_ctx *c, uint64_t seed) {
     return ds;
 }
 
+// The grid of a dataset whose cell key does not fit the device build's 63-bit packed key (more
+// than 65536 cells along a dimension, or four ranges wider than 63 bits in all): built on the host
+// (usac::GridNeighbors' hash map takes any key) from the device's points, then uploaded in the
+// device CSR layout -- the same cells, numbering and member order as the device build.
+int host_grid(usac_ctx *c, int cs) {
+    const size_t n = c->n;
+    std::vector<float> pts(4 * n);
+    HIP_TRY(c, hipMemcpyAsync(pts.data(), c->pts.p, sizeof(float) * 4 * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
+    const usac::GridNeighbors g(pts.data(), c->n, cs);
+    std::vector<uint32_t> csr(4 * n + 1);
+    const uint32_t nc = (uint32_t)g.starts().size() - 1;
+    memcpy(csr.data(), g.cells().data(), 4 * n);
+    memcpy(csr.data() + n, g.ranks().data(), 4 * n);
+    memcpy(csr.data() + 2 * n, g.members().data(), 4 * n);
+    memcpy(csr.data() + 3 * n, g.starts().data(), 4 * ((size_t)nc + 1));
+    std::vector<int32_t> elig;
+    for (uint32_t i = 0; i < c->n; i++)
+        if (g.count(i) >= c->m) elig.push_back((int32_t)i);
+    HIP_TRY(c, hipMemcpyAsync(c->grid_csr.p, csr.data(), sizeof(uint32_t) * (3 * n + nc + 1), hipMemcpyHostToDevice,
+                              c->stream));
+    if (!elig.empty())
+        HIP_TRY(c, hipMemcpyAsync(c->grid_elig.p, elig.data(), sizeof(int32_t) * elig.size(), hipMemcpyHostToDevice,
+                                  c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
+    c->grid_n_cells = nc;
+    c->grid_n_elig = (uint32_t)elig.size();
+    c->grid_cs = cs;
+    return USAC_OK;
+}
+
 // NearestNeighbors::getGridNearestNeighbors (nearest_neighbors.cpp:160-202) on the device for
-// cell size cs (kept until another size is asked for).  Cells are packed 16 bits per
-// dimension relative to the dataset box's lowest cell.
+// cell size cs (kept until another size is asked for).  Cells are packed per dimension relative
+// to the dataset box's lowest cell; a box too wide for the packed key takes host_grid instead.
 int ensure_grid(usac_ctx *c, int cs) {
     if (c->grid_cs == cs) return USAC_OK;
     if (c->cols != 4) return fail(c, USAC_ERR_ARG, "grid neighbours need 4-column points (SURVEY Q17)");
     if (cs <= 0) return fail(c, USAC_ERR_ARG, "grid cell_size must be > 0");
     const float e[4] = {c->ext.x, c->ext.y, c->ext.z, c->ext.w};
     int lo[4], bits[4];
+    bool packable = true;
     for (int j = 0; j < 4; j++) {
+        lo[j] = bits[j] = 0;
+        if (!(e[j] / (float)cs < 1.0e9f)) {  // the int cell index itself is out of range
+            packable = false;
+            continue;
+        }
         lo[j] = (int)(-e[j] / (float)cs);
         const long long range = (long long)(int)(e[j] / (float)cs) - lo[j];
-        if (range > 65535) return fail(c, USAC_ERR_UNSUPPORTED, "grid: more than 65536 cells along one dimension");
+        packable &= range <= 65535;
         bits[j] = 1;  // 2^bits - 1 > range: room for the out-of-box sentinel
-        while ((1ll << bits[j]) - 1 <= range) bits[j]++;
+        while (bits[j] < 40 && (1ll << bits[j]) - 1 <= range) bits[j]++;
     }
-    // each dimension keeps its range plus the out-of-box sentinel; a key wider than 63 bits
-    // (e.g. 17 + 17 + 17 + 13 bits; the build's hash table keeps the all-ones word as its empty
-    // slot) is refused rather than clamped (a clamped dimension would give the sentinel a real
-    // cell's value)
-    if (bits[0] + bits[1] + bits[2] + bits[3] > 63)
-        return fail(c, USAC_ERR_UNSUPPORTED, "grid: the four cell ranges need more than 63 key bits");
-    if (!c->grid_pin && !(c->grid_pin = static_cast<uint32_t *>(PinnedPool::get().take(64, &c->grid_pin_bytes))))
-        return fail(c, USAC_ERR_HIP, "pinned host allocation failed");
+    // each dimension keeps its range plus the out-of-box sentinel; the build's hash table keeps
+    // the all-ones word as its empty slot, so the key must fit 63 bits (clamping a dimension
+    // would give the sentinel a real cell's value)
+    packable &= bits[0] + bits[1] + bits[2] + bits[3] <= 63;
     const size_t n = c->n;
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, c->grid_csr.reserve(sizeof(uint32_t) * (4 * n + 1)));
     HIP_TRY(c, c->grid_elig.reserve(sizeof(int32_t) * n));
+    c->grid_cs = 0;
+    if (!packable) return host_grid(c, cs);
+    if (!c->grid_pin && !(c->grid_pin = static_cast<uint32_t *>(PinnedPool::get().take(64, &c->grid_pin_bytes))))
+        return fail(c, USAC_ERR_HIP, "pinned host allocation failed");
     HIP_TRY(c, c->grid_ws.reserve(usac::grid_workspace_bytes(c->n)));
     c->grid_cs = 0;
     HIP_TRY(c, usac::build_grid(c->stream, c->pts.as<float4>(), c->n, cs, make_int4(lo[0], lo[1], lo[2], lo[3]),
@@ -631,7 +688,9 @@ int shard_allgather(usac_ctx *c, const Shard &sh, int status, const void *send, 
         pinned_vector<uint8_t> st(rb * (size_t)(sh.nranks + 1));
         memcpy(st.data(), mine.data(), rb);
         HIP_TRY(c, hipMemcpyAsync(c->x_send.p, st.data(), rb, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(c, order_after_exchanges(c));
         NCCL_TRY(c, ncclAllGather(c->x_send.p, c->x_recv.p, rb, ncclUint8, c->comm, c->stream));
+        HIP_TRY(c, mark_collective(c));
         HIP_TRY(c, hipMemcpyAsync(st.data() + rb, c->x_recv.p, rb * (size_t)sh.nranks, hipMemcpyDeviceToHost,
                                   c->stream));
         HIP_TRY(c, stream_wait(c->stream));
@@ -1509,6 +1568,7 @@ void usac_destroy(usac_ctx *c) {
         if (c->xev_done[k]) StreamPool::get().give_back(c->xev_done[k]);
     }
     if (c->xstream) StreamPool::get().give_back(c->xstream);
+    if (c->coll_ev) StreamPool::get().give_back(c->coll_ev);
     for (auto &ev : c->lo_ev)
         if (ev) StreamPool::get().give_back(ev);
     if (c->lo_stream) StreamPool::get().give_back(c->lo_stream);
@@ -1725,6 +1785,7 @@ int usac_hypothesize_score(usac_ctx *c, const int32_t *samples, uint32_t B, uint
     // per-hypothesis outputs requested -> exact sequential sums (one chunk)
     const int chunks = (counts || sums) ? 1 : c->chunks;
     HIP_TRY(c, enqueue_score(c, B, thr, chunks));
+    c->batch_valid = true;
     const uint32_t S = B * c->spk;
     HIP_TRY(c, usac::launch_argmax(c->stream, c->counts.as<int32_t>(), c->sums.as<float>(), S, c->models.as<float>(),
                                    ncomp(c), first_hyp, c->spk, c->argmax_part.p, c->best.as<usac_record>()));
@@ -1744,6 +1805,7 @@ int usac_hypothesize_async(usac_ctx *c, uint32_t B, uint64_t seed, uint64_t firs
     HIP_TRY(c, enqueue_solve(c, nullptr, B, seed, first_hyp, nullptr));
     HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
     HIP_TRY(c, enqueue_score(c, B, thr, c->chunks));
+    c->batch_valid = true;
     HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
     HIP_TRY(c, usac::launch_argmax(c->stream, c->counts.as<int32_t>(), c->sums.as<float>(), B * c->spk,
                                    c->models.as<float>(), ncomp(c), first_hyp, c->spk, c->argmax_part.p,
@@ -1755,6 +1817,7 @@ int usac_hypothesize_async(usac_ctx *c, uint32_t B, uint64_t seed, uint64_t firs
 
 int usac_last_counts(usac_ctx *c, int32_t *counts, float *sums, uint32_t n) {
     if (!c || !counts || n == 0) return USAC_ERR_ARG;
+    if (!c->batch_valid) return fail(c, USAC_ERR_ARG, "no batch since the last usac_ransac_run");
     if ((size_t)n * sizeof(int32_t) > c->counts.bytes) return fail(c, USAC_ERR_ARG, "more slots than the last batch");
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipMemcpyAsync(counts, c->counts.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
@@ -2011,7 +2074,9 @@ static int sharded_batch(usac_ctx *c, const int32_t *hs, uint32_t B, uint32_t it
                                            status == USAC_OK ? (uint32_t)Ss : 0u, (uint32_t)Ps, nc, status,
                                            c->x_send.as<int32_t>()));
         if (sprt && status == USAC_OK && Bs) HIP_TRY(c, pool_mask(c->x_send.as<uint32_t>() + moff));
+        HIP_TRY(c, order_after_exchanges(c));
         NCCL_TRY(c, ncclAllGather(c->x_send.p, c->x_recv.p, bytes, ncclUint8, c->comm, c->stream));
+        HIP_TRY(c, mark_collective(c));
         HIP_TRY(c, hipMemcpyAsync(c->x_pin, c->x_recv.p, bytes * (size_t)nranks, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, stream_wait(c->stream));
         recv = static_cast<const uint8_t *>(c->x_pin);
@@ -2088,6 +2153,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         tmark = t;
     };
     HIP_TRY(c, hipSetDevice(c->device));
+    c->batch_valid = false;  // the run's batches, LO and polish reuse the batch buffers
     const uint32_t batch = prm->batch ? prm->batch : (prm->sprt ? 1024u : kDefaultBatch);
     int rc = ensure_batch(c, batch);
     if (rc) return rc;
@@ -2312,9 +2378,15 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                 std::swap(hmod, hmod2);
                 spec_hst = (size_t)spec_B * spk;
                 have = true;
-                if (B < spec_B) sampler_keep = B;  // undone lazily, before the next draw
-                else sampler_commit();
+                if (B < spec_B) {
+                    sampler_keep = B;  // undone lazily, before the next draw
+                    out->spec_rollbacks++;
+                    out->spec_wasted += spec_B - B;
+                } else {
+                    sampler_commit();
+                }
             } else {  // (max_iterations grew) the speculation is dropped
+                out->spec_wasted += spec_B;
                 sampler_rollback();
                 last_sample = spec_last;
             }
@@ -2382,8 +2454,17 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                 for (size_t sl = 0; sl < S; sl++) slot_row[sl] = (int32_t)sl;
             }
         }
-        // ---- speculation: the next batch, as if the replay leaves max_iterations alone
-        if (spec_ok && iters + B < max_iters) {
+        // ---- speculation: the next batch, as if the replay leaves max_iterations alone -- unless
+        // this batch certainly ends the run: the replay leaves max_iters <= the termination bound
+        // of its final best, whose count is at least every count of this batch (Score::bigger
+        // orders by count first; LO only adds inliers) and the bound does not grow with the count
+        bool spec_next = spec_ok && iters + B < max_iters;
+        if (spec_next) {
+            int maxc = best.inlier_number;
+            for (size_t sl = 0; sl < S; sl++) maxc = std::max(maxc, hc[sl]);
+            spec_next = term.getUpBoundIterations((uint32_t)maxc) > iters + B;
+        }
+        if (spec_next) {
             settle_sampler();
             const uint32_t B2 = std::min(std::min(batch, max_iters - (iters + B)), cap);
             sampler_mark();
@@ -2408,6 +2489,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
             }
             spec = true;
             spec_B = B2;
+            out->spec_batches++;
         }
         lap(T_DEVICE);
         if (!sprt && (rc = exact_sums(c, thr, best.inlier_number, hc.data(), hmod.data(), hst, S, hsum.data(),
@@ -2496,6 +2578,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
             out->rollbacks++;
         }
     }
+    if (spec) out->spec_wasted += spec_B;  // the run ended before the batch drawn ahead
     out->iters = iters;
     out->n_records = nrec;
     out->sprt_histories = sprt ? (int32_t)sprt->histories() : 0;
@@ -2620,6 +2703,7 @@ int usac_comm_init(usac_ctx *c, int nranks, int rank, const uint8_t *id128) {
     ncclUniqueId id;
     memcpy(&id, id128, sizeof(id) < 128 ? sizeof(id) : 128);
     NCCL_TRY(c, ncclCommInitRank(&c->comm, nranks, id, rank));
+    if (!c->coll_ev) HIP_TRY(c, StreamPool::get().event(&c->coll_ev));
     c->nranks = nranks;
     c->rank = rank;
     HIP_TRY(c, c->rec_send.reserve(sizeof(usac_record)));
@@ -2651,10 +2735,15 @@ int usac_exchange_best_async(usac_ctx *c, usac_ctx *batch, uint32_t slot) {
     HIP_TRY(c, hipMemcpyAsync(dsend, batch->best.p, sizeof(usac_record), hipMemcpyDeviceToDevice, batch->stream));
     HIP_TRY(c, hipEventRecord(c->xev_batch[slot], batch->stream));
     HIP_TRY(c, hipStreamWaitEvent(c->xstream, c->xev_batch[slot], 0));
+    if (c->coll_pending) {  // after the last collective issued on c->stream
+        HIP_TRY(c, hipStreamWaitEvent(c->xstream, c->coll_ev, 0));
+        c->coll_pending = false;
+    }
     NCCL_TRY(c, ncclAllGather(dsend, dall, sizeof(usac_record), ncclUint8, c->comm, c->xstream));
     HIP_TRY(c, hipMemcpyAsync(c->xring_host + (size_t)slot * c->nranks, dall, sizeof(usac_record) * (size_t)c->nranks,
                               hipMemcpyDeviceToHost, c->xstream));
     HIP_TRY(c, hipEventRecord(c->xev_done[slot], c->xstream));
+    c->x_last = (int)slot;
     return USAC_OK;
 }
 
@@ -2676,7 +2765,9 @@ int usac_allgather_records(usac_ctx *c, const usac_record *local, usac_record *a
     if (!c->comm) return fail(c, USAC_ERR_ARG, "usac_comm_init not called");
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipMemcpyAsync(c->rec_send.p, local, sizeof(usac_record), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, order_after_exchanges(c));
     NCCL_TRY(c, ncclAllGather(c->rec_send.p, c->rec_all.p, sizeof(usac_record), ncclUint8, c->comm, c->stream));
+    HIP_TRY(c, mark_collective(c));
     HIP_TRY(c, hipMemcpyAsync(all, c->rec_all.p, sizeof(usac_record) * (size_t)c->nranks, hipMemcpyDeviceToHost,
                               c->stream));
     HIP_TRY(c, stream_wait(c->stream));

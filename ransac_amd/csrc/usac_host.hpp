@@ -557,6 +557,11 @@ class GridNeighbors {
                   std::vector<int32_t> members)
         : cell_(std::move(cell)), rank_(std::move(rank)), start_(std::move(start)), members_(std::move(members)) {}
     uint32_t count(uint32_t i) const { return start_[cell_[i] + 1] - start_[cell_[i]] - 1; }
+    // the CSR itself (cells in order of first appearance, members ascending)
+    const std::vector<uint32_t> &cells() const { return cell_; }
+    const std::vector<uint32_t> &ranks() const { return rank_; }
+    const std::vector<uint32_t> &starts() const { return start_; }
+    const std::vector<int32_t> &members() const { return members_; }
     int32_t at(uint32_t i, uint32_t k) const { return members_[start_[cell_[i]] + (k < rank_[i] ? k : k + 1)]; }
 
    private:

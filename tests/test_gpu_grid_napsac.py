@@ -154,3 +154,31 @@ def test_device_napsac_throughput_batch(usac, oracle):
     # (their models are not better on their own: a 4-point sample inside one 50 px cell
     # extrapolates badly -- the uniform batch's best has more inliers -- hence LO in cfg5)
     assert 0 < bf["inliers"] and 0 < bu["inliers"]
+
+
+@pytest.mark.parametrize("case", ["wide_x", "wide_all"])
+def test_wide_range_grid_host_fallback(usac, oracle, case):
+    """A coordinate range the device build's packed cell key cannot hold (> 65536 cells along a
+    dimension, or more than 63 key bits in all): the grid is built on the host from
+    the device's points and uploaded in the device layout -- same CSR as the numpy restatement,
+    and the NAPSAC loop equals the oracle's."""
+    pts = _cfg5(n=20000, seed=3)[0].copy()
+    if case == "wide_x":
+        pts[::97, 0] += 4.0e6  # x1 spans 80 000 cells of 50
+    else:
+        pts[::31] *= np.float32(3000.0)  # every dimension ~60 000 cells: 4 x 17 bits
+    ref = _grid_numpy(pts, 50, 4)
+    with usac.Context(usac.ESTIMATOR.Homography, pts) as ctx:
+        g = ctx.grid_neighbors(50)
+    for k in ("cell", "rank", "start", "members", "eligible"):
+        np.testing.assert_array_equal(g[k], ref[k], err_msg=k)
+    mdl = usac.Model(2.0, 4, 0.95, 7, usac.ESTIMATOR.Homography, usac.SAMPLER.Napsac)
+    mdl.ResetRandomGenerator(False)
+    mdl.setSeed(9)
+    mdl.setNeighborsType(usac.NeighborsSearch.Grid)
+    r = usac.Ransac(mdl, pts)
+    r.run()
+    out = r.getRansacOutput()
+    o = oracle.ransac_run(oracle.HOMOGRAPHY, pts, 2.0, 0.95, 9, sampler=oracle.SAMPLER_NAPSAC)
+    assert out.getNumberOfMainIterations() == o["iters"]
+    assert np.array_equal(out.getInliers(), o["inlier_idx"])

@@ -101,3 +101,54 @@ def test_cfg1_generator_loop_identical(usac, oracle, seed):
     # the generator's line is found: |cos| between normals ~1
     mdl = out.getModel()[:2]
     assert abs(float(np.dot(mdl, gt[:2]))) / float(np.linalg.norm(mdl)) > 0.99
+
+
+def _run_loop(usac, pts, est, sampler, thr, seed, lo, spec):
+    import os
+    mdl = usac.Model(thr, 4 if est == usac.ESTIMATOR.Homography else 2, 0.99, 7, est, sampler)
+    mdl.ResetRandomGenerator(False)
+    mdl.setSeed(seed)
+    mdl.lo = usac.LocOpt(lo)
+    mdl.max_iterations = 20000
+    mdl.setNeighborsType(usac.NeighborsSearch.Grid)
+    if spec:
+        os.environ.pop("USAC_NO_SPECULATION", None)
+    else:
+        os.environ["USAC_NO_SPECULATION"] = "1"
+    try:
+        r = usac.Ransac(mdl, pts)
+        r.run()
+    finally:
+        os.environ.pop("USAC_NO_SPECULATION", None)
+    return r.getRansacOutput(), r.records
+
+
+def test_speculation_on_off_identical(usac):
+    """The loop's next batch drawn and solved ahead of the replay: with the library's
+    ramping batches, runs with and without the speculation give the same records, iterations,
+    model bits and inliers -- Uniform and NAPSAC, with and without LO -- and the journal rollback
+    (a speculative batch cut short by a new termination bound) is exercised."""
+    rollbacks = batches = 0
+    for kind, sampler, lo in [("H", usac.SAMPLER.Uniform, 0), ("H", usac.SAMPLER.Uniform, 1),
+                              ("Hc", usac.SAMPLER.Napsac, 0), ("Hc", usac.SAMPLER.Napsac, 1),
+                              ("L", usac.SAMPLER.Uniform, 0)]:
+        for seed in (1, 2, 3):
+            if kind == "H":
+                pts = synthetic.homography_points(n=6000, inlier_ratio=0.25, seed=seed)[0]
+            elif kind == "Hc":
+                pts = synthetic.homography_points(n=20000, inlier_ratio=0.15, seed=seed, cluster=(500, 500, 150))[0]
+            else:
+                pts = synthetic.line_points(n=3000, inlier_ratio=0.05, seed=seed)[0]
+            est = usac.ESTIMATOR.Line2d if kind == "L" else usac.ESTIMATOR.Homography
+            thr = 8.0 if kind == "L" else 2.0
+            a, ra = _run_loop(usac, pts, est, sampler, thr, seed, lo, True)
+            b, rb = _run_loop(usac, pts, est, sampler, thr, seed, lo, False)
+            assert ra == rb, (kind, lo, seed)
+            assert a.getNumberOfMainIterations() == b.getNumberOfMainIterations()
+            assert (_bits(a.getModel()) == _bits(b.getModel())).all()
+            assert np.array_equal(a.getInliers(), b.getInliers())
+            assert a.getLOIters() == b.getLOIters()
+            assert b.raw["spec_batches"] == 0
+            batches += a.raw["spec_batches"]
+            rollbacks += a.raw["spec_rollbacks"]
+    assert batches > 0 and rollbacks > 0, (batches, rollbacks)
