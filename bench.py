@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--cfg5", action="store_true",
                     help="BASELINE configs[4]: full USAC runs (homography + NAPSAC grid sampler + LO-RANSAC) "
                          "over 100k correspondences; one step = one run, value = main-loop hypotheses/s")
+    ap.add_argument("--sprt-exact", action="store_true",
+                    help="cfg3 with the reference's sequential SPRT: whole Ransac::run calls (Fundamental + PROSAC "
+                         "+ SPRT, rolling pool index, adaptive history); one step = one run")
     ap.add_argument("--lo", type=int, default=1, help="cfg5 LO variant: 1 InItLORsc (unlimited), 2 InItFLORsc")
     ap.add_argument("--cfg5-replicas", action="store_true",
                     help="cfg5 with N > 1: independent runs per rank instead of hypothesis-sharded runs")
@@ -273,6 +276,24 @@ def valu_roofline(kernel_prefix, n_points, batch, kernel_ms):
     if n_instr:
         out["instructions_per_launch"] = n_instr
         out["instr_issue_frac"] = n_instr / t / VALU_PEAK_INSTR_S
+        # the guide's issue costs (MI355X_MICROARCH.md: a wave64 VALU op 2 SIMD cycles, packed /
+        # transcendental 4) over the hot loop's instruction mix from the ISA (tools/isa_mix.py): the
+        # x4 model above charges every instruction 4 cycles (SQ_ACTIVE_INST_VALU counts ~1 per
+        # instruction, packed or not), which overstates the VALU time of the plain ones
+        import re
+        mixf = os.path.join(ROOT, "profiles", "r4", "isa_%s.json" % re.sub(
+            r"[^A-Za-z0-9]+", "_", kernel_prefix.replace("void usac::", "")).strip("_"))
+        if os.path.exists(mixf):
+            mx = json.load(open(mixf))
+            cyc = float(mx["issue_cycles_per_valu_instruction"])
+            out["frac_x4"] = out.get("frac")
+            out["achieved"] = n_instr * cyc / t
+            out["frac"] = out["achieved"] / SIMD_CYCLES_S
+            out["issue_model"] = {"cycles_per_valu_instruction": cyc, "loop_mix": mx["mix"],
+                                  "source": os.path.relpath(mixf, ROOT),
+                                  "note": "frac = SQ_INSTS_VALU x the hot loop's mean issue cycles (plain 2, packed / "
+                                          "transcendental 4) / kernel time / (1024 SIMDs x 2.4 GHz); frac_x4 = the "
+                                          "SQ_ACTIVE_INST_VALU x 4 form"}
     if pmc.get("SQ_WAVE_CYCLES"):
         wc = pmc["SQ_WAVE_CYCLES"]
         out["wave_cycle_split"] = {k.lower(): pmc[k] / wc for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
@@ -307,8 +328,12 @@ def stage_roofline(prefixes, n_points, batch, stage_ms):
     2.4 GHz; per kernel, the same fraction against its own rocprofv3 duration, the wave-cycle
     split and the counter-measured HBM bytes.  None without a summary for every kernel."""
     ents = [(p, _profile_entry(p, n_points, batch)) for p in prefixes]
-    if not stage_ms or any(e is None or "SQ_ACTIVE_INST_VALU" not in e[0].get("pmc", {}) for _, e in ents):
+    if any(e is None or "SQ_ACTIVE_INST_VALU" not in e[0].get("pmc", {}) for _, e in ents):
         return None
+    if not stage_ms:  # no live stage time: the kernels' own rocprofv3 durations, back to back
+        stage_ms = sum(e[0].get("trace", {}).get("avg_ns", 0.0) for _, e in ents) * 1e-6
+        if not stage_ms:
+            return None
     t = stage_ms * 1e-3
     busy = sum(e[0]["pmc"]["SQ_ACTIVE_INST_VALU"] * 4 for _, e in ents)
     hbm = sum(e[0].get("hbm_bytes_per_launch", 0.0) for _, e in ents)
@@ -494,6 +519,118 @@ def cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank):
     print(json.dumps(line))
 
 
+def cfg3_exact_main(args, usac, synthetic, dist, torch, world, rank, local_rank):
+    """cfg3 with the reference's own SPRT (--sprt-exact): whole Ransac::run calls (BASELINE
+    configs[2]: Fundamental 7-pt + PROSAC + SPRT, 10 k quality-sorted correspondences) through
+    usac_ransac_run, whose SPRT is the reference's sequential fp64 lambda walk over the rolling pool
+    index with the adaptive history (sprt.hpp:191-317, on device-computed pool-order inlier words).
+    One step = one run per rank (seeds differ), value = main-loop hypotheses (SPRT double counting
+    included, ransac.cpp:81-83) / wall time; N > 1: replicas (weak scaling).  Parity: runs compared
+    with the oracle -- iterations, records, SPRT rejections and history length, PROSAC termination
+    length, model bits, inlier list."""
+    from oracle import oracle as O
+
+    n = args.points
+    pts, _, _ = synthetic.fundamental_points(n=n, inlier_ratio=0.3, seed=args.seed)  # quality-sorted (PROSAC)
+
+    def model(seed):
+        mdl = usac.Model(args.threshold, 7, 0.95, 7, usac.ESTIMATOR.Fundamental, usac.SAMPLER.Prosac)
+        mdl.ResetRandomGenerator(False)
+        mdl.setSeed(seed)
+        mdl.setSprt(True)
+        return mdl
+
+    ctx = usac.Context(usac.ESTIMATOR.Fundamental, pts, device=local_rank)  # one context, runs back to back
+
+    def one_run(seed):
+        r = usac.Ransac(model(seed), pts, ctx=ctx)
+        r.run()
+        return r
+
+    for i in range(args.warmup):
+        one_run(10_000 + i)
+    if world > 1:
+        dist.barrier()
+    iters, rejected, batches = 0, 0, 0
+    t0 = time.perf_counter()
+    for step in range(args.steps):
+        r = one_run(args.seed + step * world + rank)
+        out = r.getRansacOutput()
+        iters += out.getNumberOfMainIterations()
+        rejected += out.raw["sprt_rejected"]
+        batches += out.raw["batches"]
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed, float(iters)], dtype=torch.float64)
+        dist.all_reduce(tt[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
+        elapsed, iters = float(tt[0]), int(tt[1])
+    if rank != 0:
+        ctx.close()
+        return
+    # parity: the first runs of the timed seeds against the oracle
+    checks = []
+    for k in range(min(args.steps, 8)):
+        seed = args.seed + k * world
+        r = one_run(seed)
+        out = r.getRansacOutput()
+        ref = O.ransac_run(O.FUNDAMENTAL, pts, args.threshold, 0.95, seed, sampler=O.SAMPLER_PROSAC, sprt=True)
+        checks.append({
+            "iterations_equal": out.getNumberOfMainIterations() == ref["iters"],
+            "records_equal": [(i, c, float(np.float32(s))) for i, c, s in r.records] ==
+                             [(i, c, float(np.float32(s))) for i, c, s in ref["records"]],
+            "sprt_rejected_equal": out.raw["sprt_rejected"] == ref["sprt_rejected"],
+            "sprt_histories_equal": out.raw["sprt_histories"] == ref["sprt_histories"],
+            "prosac_term_len_equal": out.raw["prosac_term_len"] == ref["prosac_term_len"],
+            "model_bit_equal": bool((np.asarray(out.getModel(), np.float32).view(np.int32) ==
+                                     np.asarray(ref["model"], np.float32).view(np.int32)).all()),
+            "inliers_equal": bool(np.array_equal(out.getInliers(), ref["inlier_idx"]))})
+    parity = {"runs": len(checks)}
+    for key in checks[0]:
+        parity[key] = all(c[key] for c in checks)
+    # roofline of the run's dominant kernel: the SPRT pool-order inlier words of one batch
+    roof = stage_roofline(["void usac::k_pool_mask<3>(", "usac::k_solve_f7("], n, 1024, None) or {
+        "bound": "valu", "achieved": None, "peak": SIMD_CYCLES_S, "unit": "SIMD-cycles/s", "frac": None}
+    roof.update({"traffic": roof.get("hbm", {}).get("traffic_bytes_per_launch"),
+                 "note": "a run is the host's sequential SPRT walk over device-computed pool-order inlier words "
+                         "(k_pool_mask) of batches of 1024 PROSAC samples (k_solve_f7), with host round trips per "
+                         "batch; see DESIGN.md §7 (cfg3 exact line) for the per-run split"})
+    line = {
+        "metric": "model hypotheses/sec (sample+solve+score) and inlier-count match vs ref",
+        "value": iters / elapsed, "unit": "hypotheses/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (SURVEY §8(d) cfg3 generator: two views, 30% inliers, 0.5 px noise, quality-sorted)",
+        "config": {"workload": "cfg3 exact: Fundamental_estimator (7-pt) + Prosac_sampler + the reference's sequential "
+                               "SPRT (rolling pool index, adaptive history, fp64 lambda), full Ransac::run calls, "
+                               "%d correspondences; one step = one run per rank" % n,
+                   "n_points": n, "threshold": args.threshold, "sprt": "exact sequential (sprt.hpp:191-317)",
+                   "hypotheses_per_gpu": iters / world, "parallelism": "replicas x%d" % world},
+        "roofline": roof,
+        "parity": parity,
+        "run_stats": {"iterations_per_run": iters / world / args.steps, "sprt_rejected": rejected,
+                      "batches": batches},
+    }
+    if args.cpu_seconds > 0:
+        t1 = time.perf_counter()
+        runs, it = 0, 0
+        while runs == 0 or time.perf_counter() - t1 < args.cpu_seconds:
+            r = O.ransac_run(O.FUNDAMENTAL, pts, args.threshold, 0.95, args.seed + 1000 + runs,
+                             sampler=O.SAMPLER_PROSAC, sprt=True)
+            it += r["iters"]
+            runs += 1
+        dt = time.perf_counter() - t1
+        model_name, avail, _ = cpu_info()
+        line["cpu_baseline"] = {"value": it / dt, "unit": "hypotheses/s", "cores": 1, "kind": "port",
+                                "sample": "%d full runs (%d hypotheses, PROSAC + SPRT, N=%d), %.1f s on 1 core of %s"
+                                          % (runs, it, n, dt, model_name)}
+        line["gpu_over_cpu"] = line["value"] / line["cpu_baseline"]["value"]
+    ctx.close()
+    print(json.dumps(line))
+
+
 def init_exchange(ctx, usac, dist, torch, world, rank, uid):
     """RCCL communicator for the per-batch record exchange.  Ranks on distinct GPUs must get
     one: a failure ends the run (exit 3) instead of reporting a scaling line without RCCL.
@@ -625,6 +762,8 @@ def main():
         dist.init_process_group("gloo")
     if args.cfg5:
         return cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank)
+    if args.sprt_exact:
+        return cfg3_exact_main(args, usac, synthetic, dist, torch, world, rank, local_rank)
     fund = args.estimator == "fundamental"
     ess = args.estimator == "essential"
     napsac = args.sampler == "napsac"
@@ -799,9 +938,11 @@ def main():
             "sprt_points_tested_per_batch": tested_per_batch, "models_per_hypothesis": models_per_hyp,
             "algorithmic_bytes_per_hypothesis": bytes_per_hyp,
             "algorithmic_equiv_gbs": achieved,
-            "note": "frac = VALU-busy SIMD-cycles per launch (PMC SQ_ACTIVE_INST_VALU x 4, packed FMAs at their two "
-                    "issue slots; summed over the dominant stage's kernels) / the stage's HIP-event time / (1024 "
-                    "SIMDs x 2.4 GHz); other_stage: the same for the other stage of the batch.  The score kernel is "
+            "note": "frac = VALU-busy SIMD-cycles per launch / the dominant stage's HIP-event time / (1024 SIMDs x "
+                    "2.4 GHz): for the cfg2 score kernel SQ_INSTS_VALU x the ISA hot loop's mean issue cost (plain "
+                    "wave64 VALU 2 cycles, packed 4: issue_model; frac_x4 = the SQ_ACTIVE_INST_VALU x 4 form, which "
+                    "charges every instruction 4), for the other stages SQ_ACTIVE_INST_VALU x 4 summed over the "
+                    "stage's kernels; other_stage: the same for the other stage of the batch.  The score kernel is "
                     "fp32-VALU-issue bound with its point records L2/scalar-cache resident, so `hbm` (counter-"
                     "measured bytes) is a small fraction of HBM peak; algorithmic_equiv_gbs = SURVEY §8(d) bytes "
                     "(16 B x N per hypothesis) / kernel time, a re-read-equivalent rate, not a roofline fraction",

@@ -222,12 +222,21 @@ int usac_set_score_variant(usac_ctx *ctx, int variant);
  * batch (usac_hypothesize_score / _async) verifies each model by the SPRT with fixed
  * (epsilon, delta) -- <= 0 selects the reference's initial values for the estimator
  * (sprt.hpp:106-150) -- and threshold A = estimateThresholdA(epsilon, delta), over the
- * SPRT pool of srandom(seed) (sprt.hpp:93-104).  Rejected models get count -1; accepted
- * ones count = inliers over all points, score = (float)count (sprt.hpp:276-281).
- * usac_ransac_run always replays the exact sequential SPRT instead. */
+ * SPRT pool of srandom(seed) (sprt.hpp:93-104), each model from a pool position of its own
+ * (usac_batch_sprt_info) instead of the rolling index, without the history updates.  Each
+ * decision equals the reference's fp64 lambda product walk with those constants from that
+ * position (certified in log space from exact counts, the sequential product where the
+ * certificate fails; kernels_sprt.hip).  Rejected models get count -1; accepted ones count =
+ * inliers over all points, score = (float)count (sprt.hpp:276-281).  usac_ransac_run always
+ * replays the exact sequential SPRT (rolling index, history) instead. */
 int usac_set_sprt(usac_ctx *ctx, int enable, uint32_t seed, double epsilon, double delta);
 /* pool points the SPRT tested in the last batch (the scoring work actually done) */
 int usac_sprt_tested(usac_ctx *ctx, uint64_t *points_tested);
+/* The batch test's constants -- eps_delta_A[3] = epsilon, delta, A (nullable) -- and the first pool
+ * position each model slot of the last batch was tested from (starts, n slots, nullable; slots of
+ * the fundamental solver 3 per sample).  Every decision equals the reference's fp64 product walk
+ * (sprt.hpp:209-234) with these constants from that position.  For tests. */
+int usac_batch_sprt_info(usac_ctx *ctx, double *eps_delta_A, uint32_t *starts, uint32_t n);
 /* Sampler of the throughput batches' device stream (usac_hypothesize_score with samples ==
  * NULL, usac_hypothesize_async): USAC_SAMPLER_UNIFORM (default), USAC_SAMPLER_NAPSAC (grid
  * neighbours of usac_set_cell_size's cell, default 50, built on the device: the initial point

@@ -254,6 +254,58 @@ class Estimator:
         return c, s
 
 
+def sprt_fixed_batch(est, pool, thr, models, starts, epsilon, delta, A):
+    """The throughput SPRT's per-model test (sprt.hpp:209-234's fp64 lambda walk, fixed epsilon /
+    delta / A, each model from its own pool start) -> (good, count [-1 if rejected], tested)."""
+    L = lib()
+    models = np.ascontiguousarray(models, dtype=np.float32).reshape(-1, 9)
+    pool = np.ascontiguousarray(pool, dtype=np.uint32)
+    starts = np.ascontiguousarray(starts, dtype=np.uint32)
+    K = models.shape[0]
+    good = np.zeros(K, np.int32)
+    cnt = np.zeros(K, np.int32)
+    tested = np.zeros(K, np.uint32)
+    _u = ctypes.POINTER(ctypes.c_uint)
+    L.orc_sprt_fixed_batch.restype = None
+    L.orc_sprt_fixed_batch.argtypes = [ctypes.c_void_p, _u, ctypes.c_uint, ctypes.c_float, _f32p, _u, ctypes.c_int,
+                                       ctypes.c_double, ctypes.c_double, ctypes.c_double, _i32p, _i32p, _u]
+    L.orc_sprt_fixed_batch(est._h, pool.ctypes.data_as(_u), len(pool), ctypes.c_float(thr), _p(models, _f32p),
+                           starts.ctypes.data_as(_u), K, epsilon, delta, A, _p(good, _i32p), _p(cnt, _i32p),
+                           tested.ctypes.data_as(_u))
+    return good.astype(bool), cnt, tested
+
+
+def e5_matrix(N, z):
+    """The oracle's M(z) (usac_oracle.c e5_matrix) of a 4 x 9 null basis."""
+    L = lib()
+    N = np.ascontiguousarray(N, dtype=np.float64).reshape(36)
+    M = np.zeros(100, np.float64)
+    _d = ctypes.POINTER(ctypes.c_double)
+    L.orc_e5_matrix.restype = None
+    L.orc_e5_matrix.argtypes = [_d, ctypes.c_double, _d]
+    L.orc_e5_matrix(N.ctypes.data_as(_d), float(z), M.ctypes.data_as(_d))
+    return M.reshape(10, 10)
+
+
+MBLOCK_REF_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_ref", "libmblock_ref.so")
+
+
+def mblock_ref_available():
+    return os.path.exists(MBLOCK_REF_PATH)
+
+
+def mblock_ref_eval(N, z):
+    """The reference's own mblock.hpp (compiled where it lies into oracle/_ref) evaluated at z."""
+    L = ctypes.CDLL(MBLOCK_REF_PATH)
+    _d = ctypes.POINTER(ctypes.c_double)
+    L.mblock_ref_eval.restype = None
+    L.mblock_ref_eval.argtypes = [_d, ctypes.c_double, _d]
+    N = np.ascontiguousarray(N, dtype=np.float64).reshape(36)
+    M = np.zeros(100, np.float64)
+    L.mblock_ref_eval(N.ctypes.data_as(_d), float(z), M.ctypes.data_as(_d))
+    return M.reshape(10, 10)
+
+
 def real_roots(coeffs):
     """real roots (ascending) of sum coeffs[i] z^i (the 5-pt solver's root finder)"""
     a = np.ascontiguousarray(coeffs, dtype=np.float64)

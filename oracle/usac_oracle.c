@@ -1315,6 +1315,17 @@ static void e5_matrix(const double N[4][9], double z, double M[10][10]) {
     }
 }
 
+/* e5_matrix exported for the pin against the reference's own mblock.hpp (oracle/mblock_ref.cpp,
+ * tests/test_oracle_essential.py): N = 4 x 9 null basis, M = 10 x 10 row-major */
+void orc_e5_matrix(const double *N, double z, double *M) {
+    double Nb[4][9], Mb[10][10];
+    for (int i = 0; i < 4; i++)
+        for (int k = 0; k < 9; k++) Nb[i][k] = N[9 * i + k];
+    e5_matrix((const double(*)[9])Nb, z, Mb);
+    for (int r = 0; r < 10; r++)
+        for (int c = 0; c < 10; c++) M[10 * r + c] = Mb[r][c];
+}
+
 /* determinant by LU with partial pivoting (first maximal |pivot|) */
 static double det10(double A[10][10]) {
     double det = 1.0;
@@ -2228,6 +2239,41 @@ int orc_sprt_verify(orc_sprt *s, orc_est *e, float thr, int current_hypothese, u
         }
     }
     return good;
+}
+
+/* The throughput SPRT's test of one model (the loop of sprt.hpp:209-234 with a fixed epsilon, delta,
+ * A -- the batch's -- and a given pool start instead of the rolling index; no history update):
+ * lambda in fp64 as the reference multiplies it.  K models (K x 9), starts[k] = model k's first pool
+ * position; good[k], count[k] = inliers over all points when good (-1 when rejected), tested[k] =
+ * points read (nullable). */
+void orc_sprt_fixed_batch(orc_est *e, const unsigned int *pool, unsigned int n, float thr, const float *models,
+                          const unsigned int *starts, int K, double epsilon, double delta, double A, int *good,
+                          int *count, unsigned int *tested) {
+    for (int k = 0; k < K; k++) {
+        orc_est_set_model(e, models + 9 * (size_t)k);
+        double lambda_new, lambda = 1;
+        unsigned int t, inl = 0, idx = starts[k];
+        int g = 1;
+        for (t = 0; t < n; t++) {
+            if (idx >= n) idx = 0;
+            if (orc_est_error(e, pool[idx]) < thr) {
+                inl++;
+                lambda_new = lambda * (delta / epsilon);
+            } else {
+                lambda_new = lambda * ((1 - delta) / (1 - epsilon));
+            }
+            idx++;
+            if (lambda_new > A) {
+                g = 0;
+                t++;
+                break;
+            }
+            lambda = lambda_new;
+        }
+        good[k] = g;
+        count[k] = g ? (int)inl : -1;
+        if (tested) tested[k] = t;
+    }
 }
 
 /* SPRT::computeExponentH (sprt.hpp:442-491) */

@@ -190,6 +190,10 @@ unsigned int orc_prosac_term_length(const orc_prosac_term *t);
 unsigned int orc_prosac_term_update(orc_prosac_term *t, unsigned int hypCount, const unsigned char *flags,
                                     unsigned int largest);
 
+/* the 5-point solver's polynomial matrix M(z) of a null basis (4 x 9) -> 10 x 10 (pinned against
+ * the reference's mblock.hpp by tests/test_oracle_essential.py) */
+void orc_e5_matrix(const double *N, double z, double *M);
+
 /* SPRT (usac/sprt.hpp) */
 typedef struct orc_sprt orc_sprt;
 orc_sprt *orc_sprt_new(int kind, unsigned int points_size, unsigned int sample_size, unsigned int max_iterations,
@@ -201,6 +205,10 @@ unsigned int orc_sprt_histories(const orc_sprt *s);
 int orc_sprt_verify(orc_sprt *s, orc_est *e, float thr, int current_hypothese, unsigned int maximum_score,
                     int *count, float *score, unsigned int *tested_out);
 unsigned int orc_sprt_upper_bound(const orc_sprt *s, int inliers_size);
+/* the throughput SPRT's per-model test: fixed (epsilon, delta, A), given pool starts (tests) */
+void orc_sprt_fixed_batch(orc_est *e, const unsigned int *pool, unsigned int n, float thr, const float *models,
+                          const unsigned int *starts, int K, double epsilon, double delta, double A, int *good,
+                          int *count, unsigned int *tested);
 
 int orc_ransac_run(int kind, const float *points, unsigned int n, float threshold, float desired_prob,
                    unsigned int max_iterations, unsigned int seed, int dlt_mode, orc_result *out,

@@ -119,7 +119,7 @@ ABI_SYMBOLS = [
     "usac_sampler_generate_batch", "usac_sampler_state", "usac_sampler_destroy", "usac_termination_create",
     "usac_termination_bound", "usac_prosac_termination", "usac_termination_destroy", "usac_sprt_create",
     "usac_sprt_verify", "usac_sprt_upper_bound", "usac_sprt_stats", "usac_sprt_replay", "usac_sprt_destroy",
-    "usac_lo_create", "usac_lo_get_model_score", "usac_lo_iters", "usac_lo_destroy",
+    "usac_lo_create", "usac_lo_get_model_score", "usac_lo_iters", "usac_lo_destroy", "usac_batch_sprt_info",
 ]
 
 
@@ -185,6 +185,7 @@ def lib():
         "usac_set_cell_size": (ctypes.c_int, [_vp, ctypes.c_int]),
         "usac_grid_neighbors": (ctypes.c_int, [_vp, ctypes.c_int, u32p, u32p, u32p, u32p, i32p, i32p, u32p]),
         "usac_sprt_tested": (ctypes.c_int, [_vp, _P(ctypes.c_uint64)]),
+        "usac_batch_sprt_info": (ctypes.c_int, [_vp, _P(ctypes.c_double), u32p, ctypes.c_uint32]),
         "usac_comm_unique_id": (ctypes.c_int, [u8p]),
         "usac_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, u8p]),
         "usac_allgather_records": (ctypes.c_int, [_vp, _P(Record), _P(Record)]),
@@ -462,6 +463,15 @@ class Context:
         self._check(lib().usac_draw_samples(self._h, B, seed, first_hyp, out.ctypes.data_as(ctypes.c_void_p)),
                     "draw_samples")
         return out
+
+    def batch_sprt_info(self, n_slots=0):
+        """The batch SPRT's (epsilon, delta, A) and each slot's first pool position in the last batch."""
+        eda = np.zeros(3, dtype=np.float64)
+        st = np.zeros(max(n_slots, 1), dtype=np.uint32)
+        self._check(lib().usac_batch_sprt_info(self._h, _ptr(eda, ctypes.c_double),
+                                               _ptr(st, ctypes.c_uint32) if n_slots else None, n_slots),
+                    "batch_sprt_info")
+        return tuple(float(x) for x in eda), st[:n_slots]
 
     def sprt_tested(self):
         t = ctypes.c_uint64(0)

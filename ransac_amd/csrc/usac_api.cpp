@@ -26,6 +26,7 @@ namespace {
 
 constexpr uint32_t kDefaultBatch = 8192;
 constexpr uint32_t kRampFirst = 1024;  // first batch of a run with the default batch
+constexpr uint32_t kRampFirstProsac = 32;
 
 // Device memory of the contexts comes from a process-wide cache per device: a context is
 // typically created per Ransac::run (as the reference constructs its Ransac per run), and
@@ -280,9 +281,9 @@ struct usac_ctx {
     DevBuf e5_ws;                      // staged 5-point solver workspace
     // throughput SPRT (usac_set_sprt): batch-fixed test on the pool-ordered points
     bool sprt_on = false;
-    float sprt_log_up = 0.f, sprt_log_down = 0.f, sprt_log_A = 0.f;
-    double sprt_A = 0.0;
-    DevBuf sprt_pts, sprt_tested, sprt_surv, sprt_surv_n;
+    usac::SprtConsts sprt_k{};      // up, down, A and their logs (the reference's doubles)
+    double sprt_eps = 0.0, sprt_delta = 0.0;
+    DevBuf sprt_pts, sprt_tested, sprt_surv, sprt_surv_n, sprt_starts;
     uint32_t spk = 1;       // model slots per hypothesis (3 for the 7-point solver)
     // single-model / polish buffers
     DevBuf one_model, inl_idx, inl_idx2, inl_cnt, inl_sum, inl_scratch, q, partial, ws, nm_model, nm_ok;
@@ -559,11 +560,13 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
         const uint32_t S = B * c->spk;
         e = c->sprt_surv.reserve(usac::sprt_survivor_bytes() * (size_t)S);
         if (e != hipSuccess) return e;
+        e = c->sprt_starts.reserve(sizeof(uint32_t) * (size_t)S);
+        if (e != hipSuccess) return e;
         return usac::launch_score_sprt(c->stream, c->estimator, c->sprt_pts.p, c->n, c->models.as<float>(),
                                        (size_t)S, listed(c) ? c->list.as<uint32_t>() : nullptr,
-                                       listed(c) ? c->list_n.as<uint32_t>() : nullptr, S, thr, c->sprt_log_up,
-                                       c->sprt_log_down, c->sprt_log_A, c->counts.as<int32_t>(), c->sums.as<float>(),
-                                       c->sprt_tested.as<uint32_t>(), c->sprt_surv.p, c->sprt_surv_n.as<uint32_t>());
+                                       listed(c) ? c->list_n.as<uint32_t>() : nullptr, S, thr, c->sprt_k,
+                                       c->counts.as<int32_t>(), c->sums.as<float>(), c->sprt_tested.as<uint32_t>(),
+                                       c->sprt_surv.p, c->sprt_surv_n.as<uint32_t>(), c->sprt_starts.as<uint32_t>());
     }
     if ((listed(c) || is_h(c)) && c->score_variant != 1 && c->rec_thr != thr) {  // fast-kernel point records
         hipError_t e = c->rec.reserve(sizeof(float) * 32 * (((size_t)c->n + 3) / 4));
@@ -1577,7 +1580,7 @@ void usac_destroy(usac_ctx *c) {
     if (c->grid_pin) PinnedPool::get().give_back(c->grid_pin, c->grid_pin_bytes);
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->h4_fb, &c->h4_fb_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
-                      &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->inl_scratch, &c->e5_ws, &c->one_model,
+                      &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->sprt_starts, &c->inl_scratch, &c->e5_ws, &c->one_model,
                       &c->inl_idx, &c->inl_idx2, &c->pol_res, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq, &c->nm_w, &c->nm_qw, &c->lo_io,
                       &c->rec_send, &c->rec_all, &c->tv_part, &c->hf_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
@@ -1942,10 +1945,22 @@ int usac_set_sprt(usac_ctx *c, int enable, uint32_t seed, double epsilon, double
     usac::Sprt sp(g, c->estimator, c->n, c->m, 10000);
     const double eps = epsilon > 0 ? epsilon : sp.epsilon0(), del = delta > 0 ? delta : sp.delta0();
     if (!(eps < 1.0) || !(del < 1.0)) return fail(c, USAC_ERR_ARG, "SPRT: epsilon and delta must be in (0, 1)");
-    c->sprt_A = sp.thresholdA(eps, del);
-    c->sprt_log_up = (float)log(del / eps);
-    c->sprt_log_down = (float)log((1 - del) / (1 - eps));
-    c->sprt_log_A = (float)log(c->sprt_A);
+    // the reference's constants (sprt.hpp:219-224: lambda * (delta / epsilon), lambda * ((1 - delta) /
+    // (1 - epsilon)), compared with A), and their logs for the certified decisions (kernels_sprt.hip)
+    c->sprt_eps = eps;
+    c->sprt_delta = del;
+    c->sprt_k.up = del / eps;
+    c->sprt_k.down = (1 - del) / (1 - eps);
+    c->sprt_k.A = sp.thresholdA(eps, del);
+    c->sprt_k.lu = log(c->sprt_k.up);
+    c->sprt_k.ld = log(c->sprt_k.down);
+    c->sprt_k.lA = log(c->sprt_k.A);
+    // test hooks: a wider margin / a lower climb limit sends more walks down the sequential path
+    const char *em = getenv("USAC_SPRT_CERT_MARGIN"), *ec = getenv("USAC_SPRT_CERT_CLIMB");
+    c->sprt_k.margin = em ? atof(em) : 1e-7;
+    c->sprt_k.climb = ec ? atof(ec) : 700.0;
+    if (!(c->sprt_k.margin >= 1e-7) || !(c->sprt_k.climb > 0) || c->sprt_k.climb > 700.0)
+        return fail(c, USAC_ERR_ARG, "SPRT certificate: margin >= 1e-7 and 0 < climb <= 700");
     HIP_TRY(c, c->pool_idx.reserve(sizeof(uint32_t) * c->n));
     HIP_TRY(c, c->sprt_pts.reserve(sizeof(float) * c->cols * (size_t)c->n));
     HIP_TRY(c, c->sprt_tested.reserve(sizeof(uint32_t)));
@@ -1957,6 +1972,23 @@ int usac_set_sprt(usac_ctx *c, int enable, uint32_t seed, double epsilon, double
     HIP_TRY(c, hipMemsetAsync(c->sprt_tested.p, 0, sizeof(uint32_t), c->stream));
     HIP_TRY(c, stream_wait(c->stream));
     c->sprt_on = true;
+    return USAC_OK;
+}
+
+int usac_batch_sprt_info(usac_ctx *c, double *eps_delta_A, uint32_t *starts, uint32_t n) {
+    if (!c) return USAC_ERR_ARG;
+    if (!c->sprt_on) return fail(c, USAC_ERR_ARG, "SPRT not enabled");
+    if (eps_delta_A) {
+        eps_delta_A[0] = c->sprt_eps;
+        eps_delta_A[1] = c->sprt_delta;
+        eps_delta_A[2] = c->sprt_k.A;
+    }
+    if (starts && n) {
+        if (!c->batch_valid || (size_t)n * sizeof(uint32_t) > c->sprt_starts.bytes)
+            return fail(c, USAC_ERR_ARG, "no SPRT batch of that many slots");
+        HIP_TRY(c, hipMemcpyAsync(starts, c->sprt_starts.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, stream_wait(c->stream));
+    }
     return USAC_OK;
 }
 
@@ -2248,7 +2280,8 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     std::vector<int32_t> slot_row(SB);
     std::vector<float> hsum(SB);
     pinned_vector<float> hmod((size_t)ncomp(c) * SB);
-    std::vector<uint32_t> hlist(SB), hmask(sprt ? (size_t)nw * SB : 0);
+    std::vector<uint32_t> hlist(SB);
+    pinned_vector<uint32_t> hmask(sprt ? (size_t)nw * SB : 0);
     std::vector<uint32_t> subset_at(batch), largest_at(batch);
     std::vector<int32_t> last_sample(m, 0);
     // Speculation: the next batch is drawn and solved / scored on its own stream while the
@@ -2327,7 +2360,10 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     // with the library's default batch the batches ramp up (1024, 2048, ...): the termination
     // bound drops once the loop has a good model, and a smaller first batch draws, solves and
     // scores fewer hypotheses the run never reaches (the replay is exact for any partition)
-    uint32_t cap = prm->batch ? batch : std::min<uint32_t>(batch, kRampFirst);
+    // PROSAC on quality-sorted points finds its model within a few dozen samples and its
+    // termination bound then drops to about as many (cfg3: ~9 iterations a run), so its ramp
+    // starts at 32
+    uint32_t cap = prm->batch ? batch : std::min<uint32_t>(batch, prosac ? kRampFirstProsac : kRampFirst);
     // draws B samples into buf (the reference's sample array reuse for NAPSAC: a sample the
     // sampler leaves (partly) unwritten keeps the previous sample's entries)
     auto draw_into = [&](int32_t *buf, uint32_t B, usac::ProsacSampler *pro_, uint32_t gen_term) {
@@ -2440,9 +2476,12 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
             } else {
                 std::fill(hc.begin(), hc.begin() + S, 0);
             }
-            for (uint32_t w = 0; w < nw && rows; w++)
-                HIP_TRY(c, hipMemcpyAsync(hmask.data() + (size_t)w * rows, c->masks.as<uint32_t>() + (size_t)w * S,
-                                          sizeof(uint32_t) * rows, hipMemcpyDeviceToHost, c->stream));
+            // the [nw][S] words of the batch's rows, repacked [nw][rows], in one strided copy into
+            // pinned memory (a copy per word was ~nw fixed copy overheads per batch)
+            if (rows)
+                HIP_TRY(c, hipMemcpy2DAsync(hmask.data(), sizeof(uint32_t) * rows, c->masks.as<uint32_t>(),
+                                            sizeof(uint32_t) * S, sizeof(uint32_t) * rows, nw, hipMemcpyDeviceToHost,
+                                            c->stream));
         }
         HIP_TRY(c, stream_wait(c->stream));
         }
@@ -2498,7 +2537,6 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         lap(T_SUMS);
         out->batches++;
         // ---- sequential replay
-        std::vector<uint32_t> wbuf(sprt ? nw : 0);
         uint32_t j = 0;
         bool rewind = false;
         for (; j < B && iters < max_iters; j++) {
@@ -2508,9 +2546,8 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                 usac::Score cur;
                 if (sprt) {
                     const int32_t r = slot_row[sl];
-                    for (uint32_t w = 0; w < nw; w++) wbuf[w] = hmask[(size_t)w * rows + r];
-                    const bool good = sprt->verify(wbuf.data(), (int)iters, (uint32_t)best.inlier_number,
-                                                   cur.inlier_number, cur.score);
+                    const bool good = sprt->verify(hmask.data() + r, (int)iters, (uint32_t)best.inlier_number,
+                                                   cur.inlier_number, cur.score, rows);
                     if (!good) {
                         out->sprt_rejected++;
                         if ((int)iters >= 20) {  // max_hypothesis_test_before_sprt (model.hpp:40), Q9
@@ -2833,7 +2870,6 @@ struct usac_sprt {
     uint32_t rows = 0;
     std::vector<int32_t> row_of;  // batch slot -> row (-1: empty slot)
     uint32_t batch_B = 0, batch_slots = 0;
-    std::vector<uint32_t> wbuf;
     uint32_t rejected = 0;
     ~usac_sprt() {
         (void)hipSetDevice(c->device);
@@ -2886,9 +2922,7 @@ int sprt_masks(usac_sprt *s, const float *models, uint32_t K) {
 
 // the host walk of row r (sprt.hpp:191-317)
 bool sprt_walk(usac_sprt *s, uint32_t r, int32_t current_hypothese, uint32_t maximum_score, int &count, float &score) {
-    s->wbuf.resize(s->nw);
-    for (uint32_t w = 0; w < s->nw; w++) s->wbuf[w] = s->hmask[(size_t)w * s->rows + r];
-    const bool good = s->s->verify(s->wbuf.data(), current_hypothese, maximum_score, count, score);
+    const bool good = s->s->verify(s->hmask.data() + r, current_hypothese, maximum_score, count, score, s->rows);
     if (!good) s->rejected++;
     return good;
 }

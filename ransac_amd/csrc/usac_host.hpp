@@ -21,6 +21,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <map>
+#include <mutex>
 #include <unordered_map>
 #include <vector>
 
@@ -271,19 +273,37 @@ class ProsacTerminationCriteria {
                               uint32_t points_size, uint32_t max_iterations)
         : std_(desired_prob, sample_size, points_size, max_iterations),
           growth_(growth),
-          non_random_(points_size, 0),
+          non_random_(table(points_size, sample_size)),
           maximality_(points_size, 10000),
           n_(points_size),
-          m_(sample_size),
-          term_len_(points_size) {
+          term_len_(points_size) {}
+
+    // the non-random inlier minima depend on (n, m) alone: computed once per shape and kept (the
+    // reference recomputes them in every ctor, O(1000^2) pow / div, ~1.4 ms a run)
+    static std::vector<uint32_t> table(uint32_t points_size, uint32_t sample_size) {
+        static std::mutex mu;
+        static std::map<std::pair<uint32_t, uint32_t>, std::vector<uint32_t>> cache;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            auto it = cache.find({points_size, sample_size});
+            if (it != cache.end()) return it->second;
+        }
+        std::vector<uint32_t> t = non_random_table(points_size, sample_size);
+        std::lock_guard<std::mutex> g(mu);
+        if (cache.size() > 64) cache.clear();
+        cache[{points_size, sample_size}] = t;
+        return t;
+    }
+    static std::vector<uint32_t> non_random_table(uint32_t n_, uint32_t m_) {
+        std::vector<uint32_t> non_random_(n_, 0);
         const float psi = 0.95f, beta = 0.05f;
-        std::vector<double> pn(points_size);
+        std::vector<double> pn(n_);
         for (size_t n = m_ + 1; n <= n_; ++n) {
             if (n - 1 > 1000) {
                 non_random_[n - 1] = non_random_[n - 2];
                 continue;
             }
-            std::fill(pn.begin(), pn.end(), 0.0);
+            std::fill(pn.begin(), pn.begin() + n, 0.0);  // entries [0, n) are the ones read
             pn[m_] = beta * std::pow((double)1 - beta, (double)n - m_ - 1) * (n - m_);
             double prev = pn[m_];
             for (size_t i = m_ + 2; i <= n; ++i) {
@@ -303,6 +323,7 @@ class ProsacTerminationCriteria {
             }
             non_random_[n - 1] = imin;
         }
+        return non_random_;
     }
     uint32_t terminationLength() const { return term_len_; }
     // prosac_termination_criteria.hpp:148-201; inlier(i) = error of point i < threshold for
@@ -340,7 +361,7 @@ class ProsacTerminationCriteria {
     StandardTerminationCriteria std_;
     std::vector<uint32_t> growth_;  // the sampler's growth function (a copy: samplers are rewound by value)
     std::vector<uint32_t> non_random_, maximality_;
-    uint32_t n_, m_, term_len_;
+    uint32_t n_, term_len_;
 };
 
 // ---------------------------------------------------------------- SPRT
@@ -382,9 +403,11 @@ class Sprt {
     double epsilon0() const { return hist_[0].epsilon; }
     double delta0() const { return hist_[0].delta; }
 
-    // verifyModelAndGetModelScore (sprt.hpp:191-317).  words = the model's pool-order
-    // flags; count/score are written when the reference writes them.
-    bool verify(const uint32_t *words, int current_hypothese, uint32_t maximum_score, int &count, float &score) {
+    // verifyModelAndGetModelScore (sprt.hpp:191-317).  words = the model's pool-order flags, word
+    // w at words[w * stride] (the device's [word][model] layout read in place: a walk touches a
+    // few words, not all n / 32); count/score are written when the reference writes them.
+    bool verify(const uint32_t *words, int current_hypothese, uint32_t maximum_score, int &count, float &score,
+                size_t stride = 1) {
         const History &h = hist_[cur_];
         const double epsilon = h.epsilon, delta = h.delta, A = h.A;
         const double up = delta / epsilon, down = (1 - delta) / (1 - epsilon);
@@ -393,7 +416,7 @@ class Sprt {
         bool good = true;
         for (tested = 0; tested < n_; tested++) {
             if (idx_ >= n_) idx_ = 0;
-            const bool in = (words[idx_ >> 5] >> (idx_ & 31)) & 1u;
+            const bool in = (words[(idx_ >> 5) * stride] >> (idx_ & 31)) & 1u;
             const double next = in ? lambda * up : lambda * down;
             inl += in ? 1 : 0;
             idx_++;
@@ -411,7 +434,7 @@ class Sprt {
             uint32_t after = 0;
             for (uint32_t p = tested; p < n_; p++) {
                 if (idx_ >= n_) idx_ = 0;
-                after += (words[idx_ >> 5] >> (idx_ & 31)) & 1u;
+                after += (words[(idx_ >> 5) * stride] >> (idx_ & 31)) & 1u;
                 idx_++;
             }
             count = (int)(inl + after);

@@ -118,13 +118,20 @@ hipError_t launch_pool_mask(hipStream_t st, int estimator, const void *pool_pts,
                             size_t stride, const uint32_t *list, const uint32_t *list_n, uint32_t kmax, float thr,
                             uint32_t *words, uint32_t row_stride);
 
-// throughput SPRT (batch-fixed test): counts -1 for rejected models, tested_total (nullable)
-// accumulates the pool points tested
-// surv: kmax * sprt_survivor_bytes() scratch, surv_n: one uint32 (zeroed by the launcher)
+// throughput SPRT (batch-fixed test, decisions = the reference's fp64 product walk from each
+// model's start, kernels_sprt.hip): counts -1 for rejected models, tested_total (nullable)
+// accumulates the pool points tested; starts (nullable, one per slot) receives each model's
+// first pool position.  surv: kmax * sprt_survivor_bytes() scratch, surv_n: one uint32 (zeroed by
+// the launcher)
+struct SprtConsts {
+    double up, down, A;    // delta / epsilon, (1 - delta) / (1 - epsilon), A (the reference's doubles)
+    double lu, ld, lA;     // their natural logarithms
+    double margin, climb;  // the certificate: |P - log A| > margin, climbs < climb (1e-7, 700)
+};
 hipError_t launch_score_sprt(hipStream_t st, int estimator, const void *pool_pts, uint32_t n, const float *models,
                              size_t stride, const uint32_t *list, const uint32_t *list_n, uint32_t kmax, float thr,
-                             float log_up, float log_down, float log_A, int32_t *counts, float *sums,
-                             uint32_t *tested_total, void *surv, uint32_t *surv_n);
+                             const SprtConsts &kc, int32_t *counts, float *sums, uint32_t *tested_total, void *surv,
+                             uint32_t *surv_n, uint32_t *starts = nullptr);
 size_t sprt_survivor_bytes();
 
 // exact inliers of one model (kernels_inliers.hip): ascending idx, count, sequential Σ;

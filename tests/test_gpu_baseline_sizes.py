@@ -8,7 +8,8 @@ reach (VERDICT r1 "untested BASELINE sizes"):
   against the oracle (models, counts, sequential sums).
 * cfg3 -- Fundamental 7-pt + PROSAC + SPRT, 10 000 correspondences: the batch SPRT of a
   65 536-sample device batch accepts models with their exact full count (oracle recount of
-  every accepted model), and a whole Ransac::run with PROSAC + SPRT at 10 k equals the
+  every accepted model), every decision of the batch equals the reference's fp64 walk from the
+  model's start, and a whole Ransac::run with PROSAC + SPRT at 10 k equals the
   oracle's run (iterations, records, SPRT counters, PROSAC termination length, model bits,
   inlier list).
 """
@@ -103,6 +104,25 @@ def test_cfg3_batch_sprt_full_size(usac, oracle, cfg3_points):
     oc, _ = est.score_models(models, thr)
     np.testing.assert_array_equal(c[acc], oc)
     assert best["inliers"] == c.max() <= bf["inliers"]
+
+
+def test_cfg3_batch_sprt_decisions_equal_reference_walk(usac, oracle, cfg3_points):
+    """Every model of a 65 536-sample cfg3 batch (PROSAC device stream, 10 k points): the batch
+    SPRT's decision -- rejected, or accepted with its count -- equals the reference's fp64 lambda
+    product walk (sprt.hpp:209-234) from the pool position the device started it at, with the
+    batch's (epsilon, delta, A); rejected ones included."""
+    from tests.helpers.sprt_check import batch_sprt_vs_oracle
+    pts, thr, B = cfg3_points, 2.0, 65536
+    with usac.Context(usac.ESTIMATOR.Fundamental, pts) as ctx:
+        ctx.set_device_sampler(usac.SAMPLER.Prosac)
+        ctx.set_score_chunks(96)
+        samples = ctx.draw_samples(B, seed=1, first_hyp=0)
+        ctx.set_sprt(True, seed=1)
+        c, _, _ = ctx.hypothesize_score(B=B, seed=1, first_hyp=0, thr=thr)
+        r = batch_sprt_vs_oracle(oracle, ctx, oracle.FUNDAMENTAL, pts, thr, samples, c, 1, 7)
+    assert r["models"] > 5000 and 1 <= r["accepted"] <= 0.2 * r["models"]
+    np.testing.assert_array_equal(r["device"], r["oracle"])
+    assert r["empty_slots_ok"]
 
 
 @pytest.mark.parametrize("seed", [1, 2])

@@ -173,3 +173,38 @@ def test_batch_sprt_accepts_exact_counts(usac, oracle, kind):
     oc, _ = est.quality(best["model"], 2.0)
     assert oc == best["inliers"]
     assert tested < 0.2 * occupied.sum() * len(pts)
+
+
+@pytest.mark.parametrize("cert", ["default", "all_sequential", "low_climb"])
+@pytest.mark.parametrize("kind", ["F", "H", "L"])
+def test_batch_sprt_decisions_equal_reference_walk(usac, oracle, kind, cert, monkeypatch):
+    """Every batch-SPRT decision equals the reference's fp64 lambda product walk from the model's
+    start (kernels_sprt.hip's certificate): by default almost every walk is certified from counts;
+    with the margin widened to 1e9 every walk takes the sequential product path, with the climb
+    limit at 3 many do -- the decisions must not change."""
+    from tests.helpers.sprt_check import batch_sprt_vs_oracle
+    if cert == "all_sequential":
+        monkeypatch.setenv("USAC_SPRT_CERT_MARGIN", "1e9")
+    elif cert == "low_climb":
+        monkeypatch.setenv("USAC_SPRT_CERT_CLIMB", "3")
+    if kind == "F":
+        pts, _, inl = _cfg3(n=4000, seed=7)
+        est_id, okind, m, thr = usac.ESTIMATOR.Fundamental, oracle.FUNDAMENTAL, 7, 2.0
+    elif kind == "H":
+        pts, _, inl = synthetic.homography_points(n=4000, inlier_ratio=0.3, seed=7)
+        est_id, okind, m, thr = usac.ESTIMATOR.Homography, oracle.HOMOGRAPHY, 4, 2.0
+    else:
+        pts, M = synthetic.line_points(n=3000, inlier_ratio=0.3, seed=7)
+        inl = np.abs(pts @ M[:2] + M[2]) < 3.0
+        est_id, okind, m, thr = usac.ESTIMATOR.Line2d, oracle.LINE2D, 2, 8.0
+    rng = np.random.default_rng(2)
+    idx = np.where(inl)[0]
+    good = np.stack([rng.choice(idx, m, replace=False) for _ in range(48)]).astype(np.int32)
+    samples = np.concatenate([oracle.uniform_samples(23, len(pts), m, 1000), good])
+    with usac.Context(est_id, pts) as ctx:
+        ctx.set_sprt(True, seed=3)
+        c, _, _ = ctx.hypothesize_score(samples=samples, thr=thr)
+        r = batch_sprt_vs_oracle(oracle, ctx, okind, pts, thr, samples, c, 3, m)
+    assert r["accepted"] >= 1 and r["models"] > 100
+    np.testing.assert_array_equal(r["device"], r["oracle"])
+    assert r["empty_slots_ok"]

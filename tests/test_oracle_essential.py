@@ -98,3 +98,27 @@ def test_ransac_essential_finds_inliers(oracle):
     found = set(r["inlier_idx"].tolist())
     truth = set(np.where(inl)[0].tolist())
     assert len(found & truth) >= 0.9 * len(truth)
+
+
+def test_e5_matrix_pinned_against_reference_mblock(oracle):
+    """the oracle's M(z) -- the ten cubic constraints of E = x N0 + y N1 + z N2 + N3
+    over the monomials [x^3, y^3, x^2 y, x y^2, x^2, y^2, x y, x, y, 1] (usac_oracle.c e5_matrix; the
+    device's usac_device_e5.hpp follows it bit for bit) -- against the reference's own generated
+    matrix, usac/estimator/essential/mblock.hpp compiled where it lies into oracle/_ref by
+    oracle/Makefile (oracle/mblock_ref.cpp; the reference's Polynomial::Eval at z).  Every entry
+    within 1e-12 of its row's largest magnitude: same rows, same columns, same polynomials."""
+    if not oracle.mblock_ref_available():
+        pytest.skip("oracle/_ref/libmblock_ref.so not built (the reference is absent)")
+    rng = np.random.default_rng(5)
+    worst = 0.0
+    for t in range(300):
+        N = rng.standard_normal((4, 9))
+        if t % 3 == 0:  # null bases of real samples' scale: orthonormal rows
+            N = np.linalg.qr(N.T)[0].T
+        for z in (-5.0, -4.0, -1.0, 0.0, 0.25, 3.0, 5.0, float(rng.uniform(-20, 20))):
+            a = oracle.e5_matrix(N, z)
+            b = oracle.mblock_ref_eval(N, z)
+            scale = np.abs(b).max(axis=1, keepdims=True)
+            assert (scale > 0).all()
+            worst = max(worst, float((np.abs(a - b) / scale).max()))
+    assert worst <= 1e-12, worst
