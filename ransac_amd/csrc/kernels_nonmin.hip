@@ -55,7 +55,8 @@ __global__ __launch_bounds__(256) void k_gather_psum4(const float4 *__restrict__
     uint32_t n;
     if (has_prep) {  // every segment of fit w derives the same n; segment 0 publishes it
         const int32_t c = prep.cnt_prev[w];
-        const bool go = prep.ns_prev[w] > 0 && prep.ok_prev[w] && c > prep.m && (!prep.compare || c >= prep.best_cnt);
+        const int32_t best = prep.best_dev ? *prep.best_dev : prep.best_cnt;
+        const bool go = prep.ns_prev[w] > 0 && prep.ok_prev[w] && c > prep.m && (!prep.compare || c >= best);
         n = go ? (uint32_t)c : 0u;
         if (j == 0 && threadIdx.x == 0) {
             prep.ns[w] = n;
@@ -107,7 +108,8 @@ constexpr uint32_t kFusedGatherMax = 64 * 1024;  // up to 8 points per thread an
 __global__ __launch_bounds__(64) void k_lo_prep(LoPrep p, uint32_t W) {
     for (uint32_t w = threadIdx.x; w < W; w += 64) {
         const int32_t c = p.cnt_prev[w];
-        const bool go = p.ns_prev[w] > 0 && p.ok_prev[w] && c > p.m && (!p.compare || c >= p.best_cnt);
+        const int32_t best = p.best_dev ? *p.best_dev : p.best_cnt;
+        const bool go = p.ns_prev[w] > 0 && p.ok_prev[w] && c > p.m && (!p.compare || c >= best);
         p.ns[w] = go ? (uint32_t)c : 0u;
         p.thr[w] = p.thr_prev[w] - p.step;
     }

@@ -190,6 +190,22 @@ struct PinnedPool {
     }
 };
 
+// Captured LO stage graphs, process-wide: a context lives for one Ransac::run (as the reference
+// builds its Ransac per run), but its device blocks come from DevPool and recur from run to run,
+// so a graph keyed by the stage shape and every buffer address it touches is reused across runs
+// (a graph's kernels only reach what its key's shape implies, and every buffer of that key is
+// at least that large whenever the key matches).  The cache only grows, up to kMax entries;
+// past that, stages of new shapes are launched kernel by kernel.
+struct GraphCache {
+    static constexpr size_t kMax = 256;
+    std::mutex mu;
+    std::map<std::vector<uintptr_t>, hipGraphExec_t> g;
+    static GraphCache &get() {
+        static GraphCache *c = new GraphCache();
+        return *c;
+    }
+};
+
 // std::vector storage in pinned host memory (PinnedPool), for the loop's DMA sources and
 // targets: a copy from / to pageable memory goes through a staging buffer and holds the host
 // for the copy; these copies sit between every device step and the host replay.
@@ -297,6 +313,13 @@ struct usac_ctx {
     DevBuf lo_io;           // one LO stage's inputs (two blocks, alternating) and outputs
     // the LO stages' Σerr passes run on their own stream beside the next stage's fit
     hipStream_t lo_stream = nullptr;
+    // LO iterative stages replayed as HIP graphs (USAC_LO_GRAPH=1; one capture per stage shape and
+    // buffer set, process-wide).  Off by default: measured slower than the direct launches (same-
+    // process A/B over 60 cfg5 runs, tools/ab_lo_graph.py: 134 vs 127 us per LO stage)
+    bool lo_graph_on = false;
+    DevBuf lo_best;                  // the round's best count on the device (the graphs read it)
+    int32_t *lo_best_pin = nullptr;  // its pinned host word
+    size_t lo_best_pin_bytes = 0;
     // the loop's next batch drawn and run ahead of the current batch's replay (usac_ransac_run)
     hipStream_t spec_stream = nullptr;
     hipEvent_t spec_ev = nullptr;
@@ -758,6 +781,8 @@ struct LoRansac {
     float theta, lo_thr, step;
     uint32_t inner_count = 0, iterative_count = 0;
     uint32_t rounds = 0, stages = 0, fits = 0;  // speculation rounds, device stages, fits (statistics)
+    double t_enqueue = 0.0, t_poll = 0.0;          // host ms spent enqueuing stages / waiting for them (USAC_PROFILE)
+    uint32_t graphs_built = 0;                      // iterative-stage graphs captured (USAC_PROFILE)
     int rc = USAC_OK;
     // entry best of the current call
     int best_cnt = 0;
@@ -825,8 +850,16 @@ struct LoRansac {
         HIP_TRY(c, c->lo_ws.reserve(sizeof(float) * 18 * W));
         scr_bytes = usac::inliers_scratch_bytes(n, wmax);
         HIP_TRY(c, c->lo_scr.reserve(2 * scr_bytes));
+        if (graphs()) {
+            HIP_TRY(c, c->lo_best.reserve(sizeof(int32_t)));
+            if (!c->lo_best_pin &&
+                !(c->lo_best_pin = static_cast<int32_t *>(PinnedPool::get().take(sizeof(int32_t), &c->lo_best_pin_bytes))))
+                return fail(c, USAC_ERR_HIP, "hipHostMalloc (LO best word) failed");
+        }
         return USAC_OK;
     }
+    // iterative stages as HIP graphs: the unlimited variant's pipelined stages, non-line fits
+    bool graphs() const { return c->lo_graph_on && !limited && c->estimator != USAC_LINE2D; }
 
     // the host and device blocks of parity b: inputs then outputs (layout of both)
     void set_block(int b) {
@@ -1076,10 +1109,16 @@ struct LoRansac {
                 nmax = std::max(nmax, hns[w]);
             }
             HIP_TRY(c, hipMemcpyAsync(dns, hns, in_bytes, hipMemcpyHostToDevice, st));
+            if (graphs()) {  // the round's best count, read by the captured iterative stages
+                *c->lo_best_pin = best_cnt;
+                HIP_TRY(c, hipMemcpyAsync(c->lo_best.p, c->lo_best_pin, sizeof(int32_t), hipMemcpyHostToDevice, st));
+            }
         }
         // iterative fits: counts and thresholds derived on the device from the previous stage
         // (by the fit's first kernel)
-        const usac::LoPrep prep{pns, pok, pcnt, pthr, dns, dthr, (int32_t)m, best_cnt, k > 1 ? 1 : 0, step};
+        const bool graph = k > 0 && graphs();
+        const usac::LoPrep prep{pns,      pok, pcnt, pthr, dns, dthr, (int32_t)m, best_cnt, k > 1 ? 1 : 0, step,
+                                graph ? c->lo_best.as<int32_t>() : nullptr};
         usac::NmBatch nb{};
         nb.base = k == 0 ? c->lo_max.as<int32_t>() : c->lo_lists.as<int32_t>();
         nb.base_stride = k == 0 ? 0 : n;
@@ -1098,9 +1137,68 @@ struct LoRansac {
         nb.model_out = dmod;
         nb.ok = dok;
         nb.seq = c->nm_seq.p;
-        HIP_TRY(c, usac::launch_nonminimal_batch(st, c->estimator, c->pts.p, nb));
-        HIP_TRY(c, usac::launch_inliers_batch(st, c->estimator, c->pts.p, n, dmod, W, 0.f, dthr, nullptr,
-                                              c->lo_lists.as<int32_t>(), n, dcnt, nullptr, scr(b), dok));
+        auto launch = [&]() -> hipError_t {
+            hipError_t e = usac::launch_nonminimal_batch(st, c->estimator, c->pts.p, nb);
+            if (e == hipSuccess)
+                e = usac::launch_inliers_batch(st, c->estimator, c->pts.p, n, dmod, W, 0.f, dthr, nullptr,
+                                               c->lo_lists.as<int32_t>(), n, dcnt, nullptr, scr(b), dok);
+            return e;
+        };
+        if (graph) {  // the stage's ten kernels as one graph launch (captured once per shape)
+            float stepv = step;
+            uint32_t stepbits;
+            memcpy(&stepbits, &stepv, 4);
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            const std::vector<uintptr_t> key = {
+                (uintptr_t)dev, (uintptr_t)b, (uintptr_t)(k > 1), W, n, (uintptr_t)c->estimator, stepbits, m,
+                (uintptr_t)c->pts.p,
+                (uintptr_t)c->lo_io.p, (uintptr_t)c->lo_q.p, (uintptr_t)c->lo_part.p, (uintptr_t)c->lo_ws.p,
+                (uintptr_t)c->nm_seq.p, (uintptr_t)c->lo_lists.p, (uintptr_t)c->lo_max.p, (uintptr_t)c->lo_scr.p,
+                (uintptr_t)c->lo_best.p, scr_bytes, in_bytes, out_bytes};
+            GraphCache &gc = GraphCache::get();
+            hipGraphExec_t ex = nullptr;
+            {
+                std::lock_guard<std::mutex> lk(gc.mu);
+                auto it = gc.g.find(key);
+                if (it != gc.g.end()) ex = it->second;
+            }
+            bool full = false;
+            if (!ex) {
+                std::lock_guard<std::mutex> lk(gc.mu);
+                full = gc.g.size() >= GraphCache::kMax;
+            }
+            if (!ex && full) {
+                HIP_TRY(c, launch());
+            } else if (!ex) {
+                HIP_TRY(c, hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+                const hipError_t le = launch();
+                hipGraph_t g = nullptr;
+                const hipError_t ce = hipStreamEndCapture(st, &g);
+                if (le != hipSuccess || ce != hipSuccess) {
+                    if (g) (void)hipGraphDestroy(g);
+                    return fail(c, USAC_ERR_HIP, std::string("LO stage capture: ") +
+                                                     hipGetErrorString(le != hipSuccess ? le : ce));
+                }
+                const hipError_t ie = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+                (void)hipGraphDestroy(g);
+                if (ie != hipSuccess) return fail(c, USAC_ERR_HIP, std::string("LO stage graph: ") + hipGetErrorString(ie));
+                {
+                    std::lock_guard<std::mutex> lk(gc.mu);
+                    auto ins = gc.g.emplace(key, ex);
+                    if (!ins.second) {  // another thread captured the same stage meanwhile
+                        (void)hipGraphExecDestroy(ex);
+                        ex = ins.first->second;
+                    }
+                }
+                graphs_built++;
+                HIP_TRY(c, hipGraphLaunch(ex, st));
+            } else {
+                HIP_TRY(c, hipGraphLaunch(ex, st));
+            }
+        } else {
+            HIP_TRY(c, launch());
+        }
         // the side stream: Σ, then every output of the stage into the host block
         HIP_TRY(c, hipEventRecord(c->lo_ev[b], st));
         HIP_TRY(c, hipStreamWaitEvent(c->lo_stream, c->lo_ev[b], 0));
@@ -1113,11 +1211,20 @@ struct LoRansac {
     int round_pipe(uint32_t W, int inner_cnt) {
         const int b0 = next_par;
         uint32_t queued = 0;  // stages 0 .. queued - 1 are on the device
+        auto now = [] { return std::chrono::steady_clock::now(); };
+        auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+            return std::chrono::duration<double, std::milli>(b - a).count();
+        };
+        auto t0 = now();
         int r = enqueue_pipe(queued++, W, inner_cnt);
         if (!r && iters > 0) r = enqueue_pipe(queued++, W, inner_cnt);
+        t_enqueue += ms(t0, now());
         for (uint32_t k = 0; !r; k++) {
             const int b = (b0 + (int)k) & 1;
-            if ((r = poll(c->lo_ev[2 + b]))) break;
+            t0 = now();
+            r = poll(c->lo_ev[2 + b]);
+            t_poll += ms(t0, now());
+            if (r) break;
             set_block(b);
             for (uint32_t w = 0; w < W; w++)
                 if (own(w) && (ch[w].phase == INNER_FIT || ch[w].phase == ITER_FIT)) fits++;
@@ -1131,7 +1238,11 @@ struct LoRansac {
                 r = fail(c, USAC_ERR_HIP, "LO pipeline out of step");
                 break;
             }
-            if (k + 2 <= iters && queued == k + 2) r = enqueue_pipe(queued++, W, inner_cnt);
+            if (k + 2 <= iters && queued == k + 2) {
+                t0 = now();
+                r = enqueue_pipe(queued++, W, inner_cnt);
+                t_enqueue += ms(t0, now());
+            }
         }
         // later main-stream users of the LO scratch wait for the side stream's last Σ pass
         if (!r) {
@@ -1258,6 +1369,19 @@ struct LoRansac {
     }
 };
 
+constexpr uint32_t kExactSumsMax = 64;  // models per exact_sums launch
+
+// exact_sums' buffers at their full size, before the loop: growing a DevBuf synchronises the
+// device, and under the speculation that waited for the speculative batch (plus a hipMalloc) --
+// 0.47 ms a cfg5 run (USAC_PROFILE, round 4)
+int reserve_exact_sums(usac_ctx *c) {
+    HIP_TRY(c, c->lo_models.reserve(sizeof(float) * 9 * kExactSumsMax));
+    HIP_TRY(c, c->lo_cnts.reserve(sizeof(int32_t) * kExactSumsMax));
+    HIP_TRY(c, c->lo_sums.reserve(sizeof(float) * kExactSumsMax));
+    HIP_TRY(c, c->lo_scr.reserve(usac::inliers_scratch_bytes(c->n, kExactSumsMax)));
+    return USAC_OK;
+}
+
 // Σerr where the replay can read it.  The loop compares a model's Σ only against the running
 // best with an equal count, and stores it only when the model becomes the best (Score::bigger,
 // quality.hpp:22-31); both need count >= the running best count, which is at least
@@ -1268,7 +1392,7 @@ struct LoRansac {
 // never read.  The recount doubles as a check of the fast kernel's counts.
 int exact_sums(usac_ctx *c, float thr, int best_count, const int32_t *hc, const float *hmod, size_t SB, size_t S,
                float *hsum, uint32_t *n_models) {
-    constexpr uint32_t kMax = 64;
+    constexpr uint32_t kMax = kExactSumsMax;
     std::vector<uint32_t> cand;
     int run_max = best_count;
     for (size_t sl = 0; sl < S; sl++) {
@@ -1518,6 +1642,7 @@ int usac_create(usac_ctx **out, int device, int estimator, const float *pts, uin
     // two-view scoring: a batch yields few models (about 0.4-1.3 per sample) and the few with
     // many inliers are much slower to score, so their point ranges are cut finer
     if (estimator == USAC_FUNDAMENTAL || estimator == USAC_ESSENTIAL) c->chunks = 96;
+    if (const char *g = getenv("USAC_LO_GRAPH")) c->lo_graph_on = atoi(g) != 0;
     int rc = USAC_OK;
     do {
         hipError_t e = hipSetDevice(device);
@@ -1575,6 +1700,7 @@ void usac_destroy(usac_ctx *c) {
     for (auto &ev : c->lo_ev)
         if (ev) StreamPool::get().give_back(ev);
     if (c->lo_stream) StreamPool::get().give_back(c->lo_stream);
+    if (c->lo_best_pin) PinnedPool::get().give_back(c->lo_best_pin, c->lo_best_pin_bytes);
     if (c->spec_ev) StreamPool::get().give_back(c->spec_ev);
     if (c->spec_stream) StreamPool::get().give_back(c->spec_stream);
     if (c->grid_pin) PinnedPool::get().give_back(c->grid_pin, c->grid_pin_bytes);
@@ -1585,7 +1711,7 @@ void usac_destroy(usac_ctx *c) {
                       &c->rec_send, &c->rec_all, &c->tv_part, &c->hf_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
                       &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2, &c->gc_err, &c->grid_csr,
-                      &c->grid_elig, &c->grid_ws, &c->x_send,
+                      &c->grid_elig, &c->grid_ws, &c->x_send, &c->lo_best,
                       &c->x_recv, &c->xring})
         b->release();
     for (auto &ev : c->ev)
@@ -2259,6 +2385,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         gc.reset(new GcLo(c, prm, gc_knn ? knn_tab.data() : nullptr, prm->knn, grid.get()));
         if ((rc = gc->reserve())) return rc;
     }
+    if (!prm->sprt && (rc = reserve_exact_sums(c))) return rc;
     sub(2);
     usac::StandardTerminationCriteria term(prm->desired_prob, m, n, prm->max_iterations);
     std::unique_ptr<usac::Sprt> sprt;
@@ -2696,10 +2823,12 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     if (getenv("USAC_PROFILE"))
         fprintf(stderr,
                 "usac_ransac_run ms: setup %.3f draw %.3f device %.3f sums %.3f replay %.3f lo %.3f polish %.3f "
-                "(lo rounds %u stages %u; setup: buffers %.3f neighbours %.3f lo/gc %.3f)\n",
+                "(lo rounds %u stages %u enqueue %.3f poll %.3f graphs %u; setup: buffers %.3f neighbours %.3f "
+                "lo/gc %.3f)\n",
                 tsplit[T_SETUP], tsplit[T_DRAW], tsplit[T_DEVICE], tsplit[T_SUMS], tsplit[T_REPLAY], tsplit[T_LO],
                 tsplit[T_POLISH], lo ? lo->rounds : gc ? gc->labelings : 0u, lo ? lo->stages : gc ? gc->stages : 0u,
-                tsub[0], tsub[1] - tsub[0], tsub[2] - tsub[1]);
+                lo ? lo->t_enqueue : 0.0, lo ? lo->t_poll : 0.0, lo ? lo->graphs_built : 0u, tsub[0],
+                tsub[1] - tsub[0], tsub[2] - tsub[1]);
     // ransac.cpp:214 getInliers(best_model): `cur` already is that list (see above)
     cnt = cur_cnt;
     if (inliers_out && cnt > 0) {  // DMA into pinned memory, then into the caller's buffer

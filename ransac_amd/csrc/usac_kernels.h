@@ -211,6 +211,8 @@ struct LoPrep {
     float *thr;
     int32_t m, best_cnt, compare;
     float step;
+    const int32_t *best_dev;  // nullable: the best count read from device memory instead of best_cnt
+                              // (a captured stage graph keeps its arguments across rounds)
 };
 hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pts, const NmBatch &b);
 size_t nonminimal_partial_stride(uint32_t nmax);
