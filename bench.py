@@ -225,7 +225,7 @@ def timed_kernel_parity(usac, ctx, kind, pts, thr, dlt_mode, seed, sprt, first_h
 
 def _profile_entry(kernel_prefix, n_points, batch):
     """(summary entry, source) of `kernel_prefix` in the newest committed rocprofv3 summary
-    (profiles/<round>_summary.json, made by tools/profile.sh + tools/summarize_profile.py)
+    (profiles/<round>_summary.json, made by tools/archive/profile.sh + tools/summarize_profile.py)
     that ran the same workload shape; else None."""
     import glob
 
