@@ -276,24 +276,29 @@ def valu_roofline(kernel_prefix, n_points, batch, kernel_ms):
     if n_instr:
         out["instructions_per_launch"] = n_instr
         out["instr_issue_frac"] = n_instr / t / VALU_PEAK_INSTR_S
-        # the guide's issue costs (MI355X_MICROARCH.md: a wave64 VALU op 2 SIMD cycles, packed /
-        # transcendental 4) over the hot loop's instruction mix from the ISA (tools/isa_mix.py): the
-        # x4 model above charges every instruction 4 cycles (SQ_ACTIVE_INST_VALU counts ~1 per
-        # instruction, packed or not), which overstates the VALU time of the plain ones
+        # issue costs over the hot loop's instruction mix from the ISA (tools/isa_mix.py): the per-
+        # opcode costs measured on an MI355X (profiles/r4/valu_issue_costs.json, 8 waves per SIMD:
+        # v_fma/add/mul_f32 with VGPR operands ~2.4 SIMD cycles, v_pk_fma_f32 ~4.3, v_max / v_cmp /
+        # |.|-modified or SGPR-sourced plain ops ~3.9-4.3) give frac; frac_guide prices the same mix
+        # at the guide's 2 (plain) / 4 (packed, transcendental); frac_x4 = SQ_ACTIVE_INST_VALU x 4,
+        # which charges every instruction 4 (the counter counts ~1 per instruction, packed or not)
         import re
         mixf = os.path.join(ROOT, "profiles", "r4", "isa_%s.json" % re.sub(
             r"[^A-Za-z0-9]+", "_", kernel_prefix.replace("void usac::", "")).strip("_"))
         if os.path.exists(mixf):
             mx = json.load(open(mixf))
-            cyc = float(mx["issue_cycles_per_valu_instruction"])
+            guide = float(mx["issue_cycles_per_valu_instruction"])
+            cyc = float(mx.get("measured_cycles_per_valu_instruction", guide))
             out["frac_x4"] = out.get("frac")
+            out["frac_guide"] = n_instr * guide / t / SIMD_CYCLES_S
             out["achieved"] = n_instr * cyc / t
             out["frac"] = out["achieved"] / SIMD_CYCLES_S
-            out["issue_model"] = {"cycles_per_valu_instruction": cyc, "loop_mix": mx["mix"],
-                                  "source": os.path.relpath(mixf, ROOT),
-                                  "note": "frac = SQ_INSTS_VALU x the hot loop's mean issue cycles (plain 2, packed / "
-                                          "transcendental 4) / kernel time / (1024 SIMDs x 2.4 GHz); frac_x4 = the "
-                                          "SQ_ACTIVE_INST_VALU x 4 form"}
+            out["issue_model"] = {"cycles_per_valu_instruction": cyc, "guide_cycles_per_valu_instruction": guide,
+                                  "loop_mix": mx["mix"], "by_opcode": mx.get("measured_by_opcode"),
+                                  "source": os.path.relpath(mixf, ROOT), "costs": mx.get("measured_source"),
+                                  "note": "frac = SQ_INSTS_VALU x the hot loop's mean measured issue cycles / kernel "
+                                          "time / (1024 SIMDs x 2.4 GHz); frac_guide = the same with the guide's "
+                                          "2 / 4 cycles; frac_x4 = the SQ_ACTIVE_INST_VALU x 4 form"}
     if pmc.get("SQ_WAVE_CYCLES"):
         wc = pmc["SQ_WAVE_CYCLES"]
         out["wave_cycle_split"] = {k.lower(): pmc[k] / wc for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
@@ -939,9 +944,9 @@ def main():
             "algorithmic_bytes_per_hypothesis": bytes_per_hyp,
             "algorithmic_equiv_gbs": achieved,
             "note": "frac = VALU-busy SIMD-cycles per launch / the dominant stage's HIP-event time / (1024 SIMDs x "
-                    "2.4 GHz): for the cfg2 score kernel SQ_INSTS_VALU x the ISA hot loop's mean issue cost (plain "
-                    "wave64 VALU 2 cycles, packed 4: issue_model; frac_x4 = the SQ_ACTIVE_INST_VALU x 4 form, which "
-                    "charges every instruction 4), for the other stages SQ_ACTIVE_INST_VALU x 4 summed over the "
+                    "2.4 GHz): for the cfg2 score kernel SQ_INSTS_VALU x the ISA hot loop's mean issue cost per "
+                    "opcode as measured on an MI355X (issue_model; frac_guide = the guide's plain 2 / packed 4 "
+                    "cycles; frac_x4 = the SQ_ACTIVE_INST_VALU x 4 form), for the other stages SQ_ACTIVE_INST_VALU x 4 summed over the "
                     "stage's kernels; other_stage: the same for the other stage of the batch.  The score kernel is "
                     "fp32-VALU-issue bound with its point records L2/scalar-cache resident, so `hbm` (counter-"
                     "measured bytes) is a small fraction of HBM peak; algorithmic_equiv_gbs = SURVEY §8(d) bytes "

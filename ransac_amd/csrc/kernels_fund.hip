@@ -325,8 +325,12 @@ __device__ __forceinline__ void two_view_drain(const TwoViewModel<EST> &M, const
         if (!__builtin_amdgcn_ballot_w64(h0)) break;
         const float4 p0 = pts[i0];
         const float4 p1 = pts[i1];
+#ifdef TV_EXP_CHEAPDRAIN  // A/B hook: the drain's loads and queue walk, a trivial residual
+        const float e0 = fabsf(p0.x * M.f[0] + p0.w), e1 = fabsf(p1.x * M.f[0] + p1.w);
+#else
         const float e0 = two_view_error<EST>(M.f, p0.x, p0.y, p0.z, p0.w);
         const float e1 = two_view_error<EST>(M.f, p1.x, p1.y, p1.z, p1.w);
+#endif
         if (h0 && e0 < thr) {
             cnt++;
             sum += e0;
@@ -404,7 +408,13 @@ __global__ __launch_bounds__(64) void k_score_f2(const float4 *__restrict__ rec,
             const float4 d0 = pn[8], d1 = pn[9], d2 = pn[10], d3 = pn[11];
             const uint32_t ma = two_view_group<EST>(M, a0, a1, a2, a3);
             const uint32_t mb = two_view_group<EST>(M, b0, b1, b2, b3);
+#ifdef TV_EXP_NODRAIN  // A/B hook: stage A computed, nothing queued (stage-A cost alone)
+            uint32_t sink = ma | (mb << 4);
+            __asm__ volatile("" : "+v"(sink));
+            two_view_append(q, len, g, n, sink & 0u);
+#else
             two_view_append(q, len, g, n, ma | (mb << 4) | M.all);
+#endif
             if (__builtin_amdgcn_ballot_w64(len == kTvQueue)) two_view_drain<EST>(M, pts, q, len, thr, cnt, sum);
             a0 = c0; a1 = c1; a2 = c2; a3 = c3;
             b0 = d0; b1 = d1; b2 = d2; b3 = d3;
