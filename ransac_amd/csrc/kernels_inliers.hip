@@ -168,6 +168,29 @@ __global__ __launch_bounds__(kInlThreads) void k_inl_compact(const void *__restr
     }
 }
 
+// The polish's acceptance of pass k (ransac.cpp:170-200) on the device, so the four passes go
+// out in one submission: pass k+1 fits pass k's inlier list with ns[k + 1] points when pass k
+// was accepted -- its fit succeeded, (double)((float)cnt / (float)best) >= 0.8 and cnt > prev
+// -- else with 0 points (a no-op fit whose scoring leaves its list alone).  The host replays
+// the same decisions from the results and stops at the first rejection, so the passes after it
+// are never read.  res: the polish result block (polish_layout in usac_kernels.h).
+__global__ void k_polish_prep(int32_t *res, int k, int32_t best0) {
+    if (threadIdx.x != 0) return;
+    const int32_t *r = res + kPolPass * k;
+    const int32_t best = k == 0 ? best0 : res[kPolState];
+    const int32_t prev = k == 0 ? 0 : res[kPolState + 1];
+    const int32_t ok = r[9], cnt = r[10];
+    const bool accept = ok && !((double)((float)cnt / (float)best) < 0.8) && cnt > prev;
+    reinterpret_cast<uint32_t *>(res)[kPolNs + k + 1] = accept ? (uint32_t)cnt : 0u;
+    res[kPolState] = accept ? cnt : best;
+    res[kPolState + 1] = accept ? cnt : prev;
+}
+
+hipError_t launch_polish_prep(hipStream_t st, int32_t *res, int k, int32_t best0) {
+    hipLaunchKernelGGL(k_polish_prep, dim3(1), dim3(64), 0, st, res, k, best0);
+    return hipGetLastError();
+}
+
 hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *models,
                                 uint32_t W, float thr, const float *thrs, const uint32_t *slots, int32_t *idx,
                                 size_t idx_stride, int32_t *counts, float *sums, void *scratch, const int32_t *ok) {

@@ -26,6 +26,8 @@ namespace {
 
 constexpr uint32_t kDefaultBatch = 8192;
 constexpr uint32_t kRampFirst = 1024;  // first batch of a run with the default batch
+// the SPRT batch's whole [nw][S] word block copied with its list in one host wait up to this size
+constexpr size_t kMaskWholeCopy = 512 * 1024;
 constexpr uint32_t kRampFirstProsac = 32;
 
 // Device memory of the contexts comes from a process-wide cache per device: a context is
@@ -302,10 +304,11 @@ struct usac_ctx {
     DevBuf sprt_pts, sprt_tested, sprt_surv, sprt_surv_n, sprt_starts;
     uint32_t spk = 1;       // model slots per hypothesis (3 for the 7-point solver)
     // single-model / polish buffers
-    DevBuf one_model, inl_idx, inl_idx2, inl_cnt, inl_sum, inl_scratch, q, partial, ws, nm_model, nm_ok;
+    DevBuf one_model, inl_idx, inl_cnt, inl_sum, inl_scratch, q, partial, ws, nm_model, nm_ok;
     uint32_t *grid_pin = nullptr;    // pinned words the grid build reads its two counts into
     size_t grid_pin_bytes = 0;
-    DevBuf pol_res;                  // polish pass results (model, ok, count, sum; initial count, sum)
+    DevBuf pol_res;                  // polish pass results (usac_kernels.h kPol*: per pass model, ok, count, sum)
+    DevBuf pol_lists;                // the polish passes' inlier lists (4 x n)
     void *pol_pin = nullptr;         // their pinned host copy (PinnedPool)
     size_t pol_pin_bytes = 0;
     DevBuf nm_seq;          // normalisation scratch of the non-minimal fits (polish and LO)
@@ -423,7 +426,11 @@ int ensure_batch(usac_ctx *c, uint32_t B) {
 int ensure_single(usac_ctx *c) {
     HIP_TRY(c, c->one_model.reserve(sizeof(float) * 9));
     HIP_TRY(c, c->inl_idx.reserve(sizeof(int32_t) * (size_t)std::max<uint32_t>(c->n, 1)));
-    HIP_TRY(c, c->inl_idx2.reserve(sizeof(int32_t) * (size_t)std::max<uint32_t>(c->n, 1)));
+    HIP_TRY(c, c->pol_lists.reserve(sizeof(int32_t) * 4 * (size_t)std::max<uint32_t>(c->n, 1)));
+    // the polish's later passes fit with c->n as the bound on their device-side counts: their
+    // scratch reserved here, so no growth (a device synchronise) inside a run
+    HIP_TRY(c, c->nm_seq.reserve(usac::nonminimal_seq_bytes(std::max<uint32_t>(c->n, 1), 1)));
+    HIP_TRY(c, c->pol_res.reserve(sizeof(float) * usac::kPolWords));
     HIP_TRY(c, c->inl_cnt.reserve(sizeof(int32_t)));
     HIP_TRY(c, c->inl_sum.reserve(sizeof(float)));
     HIP_TRY(c, c->q.reserve(sizeof(float) * 4 * (size_t)std::max<uint32_t>(c->n, 1)));
@@ -664,8 +671,10 @@ hipError_t enqueue_inliers(usac_ctx *c, const float *model_dev, float thr) {
                                 c->inl_cnt.as<int32_t>(), c->inl_sum.as<float>(), c->inl_scratch.p);
 }
 
+// ns_dev (nullable): the fit's point count on the device, n then only a bound on it
 hipError_t enqueue_nonminimal(usac_ctx *c, const int32_t *idx_dev, uint32_t n, float *model_out = nullptr,
-                              int32_t *ok_out = nullptr, const float *weights_dev = nullptr) {
+                              int32_t *ok_out = nullptr, const float *weights_dev = nullptr,
+                              const uint32_t *ns_dev = nullptr) {
     hipError_t e = c->nm_seq.reserve(usac::nonminimal_seq_bytes(n, 1));
     if (e != hipSuccess) return e;
     usac::NmBatch b{};
@@ -674,6 +683,8 @@ hipError_t enqueue_nonminimal(usac_ctx *c, const int32_t *idx_dev, uint32_t n, f
     b.n1 = n;
     b.W = 1;
     b.nmax = n;
+    b.ns = ns_dev;
+    b.fused_any = ns_dev != nullptr;
     b.q = c->q.p;
     b.partial = c->partial.as<double>();
     b.ws = c->ws.as<float>();
@@ -1707,7 +1718,7 @@ void usac_destroy(usac_ctx *c) {
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->h4_fb, &c->h4_fb_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
                       &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->sprt_starts, &c->inl_scratch, &c->e5_ws, &c->one_model,
-                      &c->inl_idx, &c->inl_idx2, &c->pol_res, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq, &c->nm_w, &c->nm_qw, &c->lo_io,
+                      &c->inl_idx, &c->pol_lists, &c->pol_res, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq, &c->nm_w, &c->nm_qw, &c->lo_io,
                       &c->rec_send, &c->rec_all, &c->tv_part, &c->hf_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
                       &c->lo_q, &c->lo_part, &c->lo_ws, &c->lo_scr, &c->knn_idx, &c->knn_d2, &c->gc_err, &c->grid_csr,
@@ -2407,7 +2418,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     std::vector<int32_t> slot_row(SB);
     std::vector<float> hsum(SB);
     pinned_vector<float> hmod((size_t)ncomp(c) * SB);
-    std::vector<uint32_t> hlist(SB);
+    pinned_vector<uint32_t> hlist(SB + 1);  // the SPRT batch's occupied-slot list, its count at [SB]
     pinned_vector<uint32_t> hmask(sprt ? (size_t)nw * SB : 0);
     std::vector<uint32_t> subset_at(batch), largest_at(batch);
     std::vector<int32_t> last_sample(m, 0);
@@ -2465,8 +2476,8 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     int32_t cnt = 0, ok = 0;
     float s = 0.f;
     // (count, sum) of a host model through one pinned D2H (polish result block, slots 12-13)
-    HIP_TRY(c, c->pol_res.reserve(sizeof(float) * 16));
-    if (!c->pol_pin && !(c->pol_pin = PinnedPool::get().take(sizeof(float) * 16, &c->pol_pin_bytes)))
+    HIP_TRY(c, c->pol_res.reserve(sizeof(float) * usac::kPolWords));
+    if (!c->pol_pin && !(c->pol_pin = PinnedPool::get().take(sizeof(float) * usac::kPolWords, &c->pol_pin_bytes)))
         return fail(c, USAC_ERR_HIP, "pinned host allocation failed");
     auto score_inliers = [&](const float *model_host) -> int {
         float *dres = c->pol_res.as<float>();
@@ -2567,6 +2578,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         const size_t S = (size_t)B * spk;
         size_t hst = SB;  // host stride of hmod's components this batch
         uint32_t rows = (uint32_t)S;
+        uint32_t mask_stride = (uint32_t)S;  // host row stride of hmask (SPRT)
         if (have) {
             hst = spec_hst;
         } else if (nranks > 1) {  // this rank's slice, then the all-gather of every slice's counts and models
@@ -2594,23 +2606,42 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         HIP_TRY(c, hipMemcpyAsync(hmod.data(), c->models.p, sizeof(float) * S * ncomp(c), hipMemcpyDeviceToHost,
                                   c->stream));
         if (sprt) {
+            // small batches (the PROSAC ramp's first ones, where a cfg3 run ends): every slot's
+            // words [nw][S] with the list in the same submission -- one host wait; larger ones:
+            // the list count first, then only the occupied rows' words repacked [nw][rows]
+            const bool whole = !listed(c) || (size_t)nw * S * sizeof(uint32_t) <= kMaskWholeCopy;
             if (listed(c)) {  // occupied slots -> mask rows
                 HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
-                HIP_TRY(c, hipMemcpyAsync(&rows, c->list_n.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
-                HIP_TRY(c, stream_wait(c->stream));
-                if (rows) HIP_TRY(c, hipMemcpyAsync(hlist.data(), c->list.p, sizeof(uint32_t) * rows,
-                                                    hipMemcpyDeviceToHost, c->stream));
+                HIP_TRY(c, hipMemcpyAsync(hlist.data() + SB, c->list_n.p, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                          c->stream));
+                if (whole) {
+                    HIP_TRY(c, hipMemcpyAsync(hlist.data(), c->list.p, sizeof(uint32_t) * S, hipMemcpyDeviceToHost,
+                                              c->stream));
+                } else {
+                    HIP_TRY(c, stream_wait(c->stream));
+                    rows = hlist[SB];
+                    if (rows) HIP_TRY(c, hipMemcpyAsync(hlist.data(), c->list.p, sizeof(uint32_t) * rows,
+                                                        hipMemcpyDeviceToHost, c->stream));
+                }
             } else {
                 std::fill(hc.begin(), hc.begin() + S, 0);
             }
-            // the [nw][S] words of the batch's rows, repacked [nw][rows], in one strided copy into
-            // pinned memory (a copy per word was ~nw fixed copy overheads per batch)
-            if (rows)
-                HIP_TRY(c, hipMemcpy2DAsync(hmask.data(), sizeof(uint32_t) * rows, c->masks.as<uint32_t>(),
-                                            sizeof(uint32_t) * S, sizeof(uint32_t) * rows, nw, hipMemcpyDeviceToHost,
-                                            c->stream));
+            if (whole) {
+                mask_stride = (uint32_t)S;
+                HIP_TRY(c, hipMemcpyAsync(hmask.data(), c->masks.p, sizeof(uint32_t) * S * nw, hipMemcpyDeviceToHost,
+                                          c->stream));
+            } else {
+                mask_stride = rows;
+                // the [nw][S] words of the batch's rows, repacked [nw][rows], in one strided copy
+                // into pinned memory (a copy per word was ~nw fixed copy overheads per batch)
+                if (rows)
+                    HIP_TRY(c, hipMemcpy2DAsync(hmask.data(), sizeof(uint32_t) * rows, c->masks.as<uint32_t>(),
+                                                sizeof(uint32_t) * S, sizeof(uint32_t) * rows, nw,
+                                                hipMemcpyDeviceToHost, c->stream));
+            }
         }
         HIP_TRY(c, stream_wait(c->stream));
+        if (sprt && listed(c)) rows = hlist[SB];
         }
         if (sprt) {
             if (listed(c) && nranks == 1) {
@@ -2674,7 +2705,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                 if (sprt) {
                     const int32_t r = slot_row[sl];
                     const bool good = sprt->verify(hmask.data() + r, (int)iters, (uint32_t)best.inlier_number,
-                                                   cur.inlier_number, cur.score, rows);
+                                                   cur.inlier_number, cur.score, mask_stride);
                     if (!good) {
                         out->sprt_rejected++;
                         if ((int)iters >= 20) {  // max_hypothesis_test_before_sprt (model.hpp:40), Q9
@@ -2772,49 +2803,61 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     }
 
     lap(T_REPLAY);
-    // ---- polish (ransac.cpp:157-207) on the device.  Each pass is one submission: the fit on
-    // the current list, then the fitted model scored from device memory (compaction gated on
-    // the fit's ok) into the other list buffer -- one host wait per pass; an accepted model's
-    // list becomes the current one, so after the loop `cur` holds best_model's own inliers
-    // (the same kernels, model and threshold as the final getInliers would use).
-    // The results of a pass land in one device block (pol_res: model[9], ok, count, sum, and
-    // the initial getInliers' count, sum) copied with one D2H into pinned memory; the initial
-    // getInliers(best_model) rides in the first pass's submission.
-    HIP_TRY(c, c->pol_res.reserve(sizeof(float) * 16));
+    // ---- polish (ransac.cpp:157-207) on the device, the four passes in ONE submission: pass k
+    // fits the list pass k - 1 scored (the initial getInliers(best_model) list for pass 0) and
+    // scores the fitted model from device memory into list k + 1 (compaction gated on the fit's
+    // ok); between passes k_polish_prep takes the host's acceptance decision on the device and
+    // hands pass k + 1 its point count, or 0 after a rejection (a no-op pass).  All results land
+    // in one device block (usac_kernels.h kPol*) copied with one D2H; the host then replays the
+    // reference's loop on them and stops at the first rejection, so `cur` ends as best_model's
+    // own inlier list (the same kernels, model and threshold as the final getInliers would use).
+    HIP_TRY(c, c->pol_res.reserve(sizeof(float) * usac::kPolWords));
+    HIP_TRY(c, c->pol_lists.reserve(sizeof(int32_t) * 4 * (size_t)std::max<uint32_t>(c->n, 1)));
     HIP_TRY(c, c->inl_scratch.reserve(usac::inliers_scratch_bytes(c->n, 1)));
-    if (!c->pol_pin && !(c->pol_pin = PinnedPool::get().take(sizeof(float) * 16, &c->pol_pin_bytes)))
+    if (!c->pol_pin && !(c->pol_pin = PinnedPool::get().take(sizeof(float) * usac::kPolWords, &c->pol_pin_bytes)))
         return fail(c, USAC_ERR_HIP, "pinned host allocation failed");
     float *dres = c->pol_res.as<float>();
+    int32_t *dres_i = c->pol_res.as<int32_t>();
     const float *hres = static_cast<const float *>(c->pol_pin);
-    int32_t *cur = c->inl_idx.as<int32_t>(), *alt = c->inl_idx2.as<int32_t>();
+    int32_t *lists[5] = {c->inl_idx.as<int32_t>(), c->pol_lists.as<int32_t>(), nullptr, nullptr, nullptr};
+    for (int k = 2; k < 5; k++) lists[k] = lists[1] + (size_t)(k - 1) * std::max<uint32_t>(c->n, 1);
     HIP_TRY(c, hipMemcpyAsync(c->one_model.p, best_model, sizeof(float) * 9, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(c, usac::launch_inliers_batch(c->stream, c->estimator, c->pts.p, c->n, c->one_model.as<float>(), 1, thr,
-                                          nullptr, nullptr, cur, 0, reinterpret_cast<int32_t *>(dres + 12), dres + 13,
+                                          nullptr, nullptr, lists[0], 0, dres_i + 12, dres + 13,
                                           c->inl_scratch.p));  // quality->getInliers(best_model)
+    constexpr int kPasses = 4;
+    for (int k = 0; k < kPasses; k++) {
+        float *pres = dres + usac::kPolPass * k;
+        int32_t *dok = dres_i + usac::kPolPass * k + 9;
+        if (k == 0)
+            HIP_TRY(c, enqueue_nonminimal(c, lists[0], (uint32_t)best.inlier_number, pres, dok));
+        else  // the count pass k - 1's acceptance left on the device; c->n bounds it
+            HIP_TRY(c, enqueue_nonminimal(c, lists[k], c->n, pres, dok, nullptr,
+                                          reinterpret_cast<const uint32_t *>(dres_i + usac::kPolNs + k)));
+        HIP_TRY(c, usac::launch_inliers_batch(c->stream, c->estimator, c->pts.p, c->n, pres, 1, thr, nullptr, nullptr,
+                                              lists[k + 1], 0, dok + 1, pres + 11, c->inl_scratch.p, dok));
+        if (k + 1 < kPasses) HIP_TRY(c, usac::launch_polish_prep(c->stream, dres_i, k, best.inlier_number));
+    }
+    HIP_TRY(c, hipMemcpyAsync(c->pol_pin, dres, sizeof(float) * usac::kPolPass * kPasses, hipMemcpyDeviceToHost,
+                              c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
+    int32_t *cur = lists[0];
     int32_t cur_cnt = 0;
+    memcpy(&cur_cnt, hres + 12, sizeof(int32_t));
     int prev = 0;
-    float nm_model[9];
-    for (int norm = 0; norm < 4; norm++) {
-        int32_t *dok = reinterpret_cast<int32_t *>(dres + 9);
-        HIP_TRY(c, enqueue_nonminimal(c, cur, (uint32_t)best.inlier_number, dres, dok));
-        HIP_TRY(c, usac::launch_inliers_batch(c->stream, c->estimator, c->pts.p, c->n, dres, 1, thr, nullptr, nullptr,
-                                              alt, 0, reinterpret_cast<int32_t *>(dres + 10), dres + 11,
-                                              c->inl_scratch.p, dok));
-        HIP_TRY(c, hipMemcpyAsync(c->pol_pin, dres, sizeof(float) * 14, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(c, stream_wait(c->stream));
-        memcpy(nm_model, hres, sizeof(nm_model));
-        memcpy(&ok, hres + 9, sizeof(int32_t));
-        memcpy(&cnt, hres + 10, sizeof(int32_t));
-        memcpy(&s, hres + 11, sizeof(float));
-        if (norm == 0) memcpy(&cur_cnt, hres + 12, sizeof(int32_t));
+    for (int k = 0; k < kPasses; k++) {  // ransac.cpp:170-200, on the passes' results
+        const float *r = hres + usac::kPolPass * k;
+        memcpy(&ok, r + 9, sizeof(int32_t));
+        memcpy(&cnt, r + 10, sizeof(int32_t));
+        memcpy(&s, r + 11, sizeof(float));
         if (!ok) break;
         if ((double)((float)cnt / (float)best.inlier_number) < 0.8) break;
         if (cnt <= prev) break;
         prev = cnt;
         best.inlier_number = cnt;
         best.score = s;
-        memcpy(best_model, nm_model, sizeof(best_model));
-        std::swap(cur, alt);
+        memcpy(best_model, r, sizeof(best_model));
+        cur = lists[k + 1];
         cur_cnt = cnt;
         out->polish_passes++;
     }

@@ -152,6 +152,11 @@ hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, 
 hipError_t launch_inliers_sums(hipStream_t st, uint32_t n, uint32_t W, const uint32_t *slots, const int32_t *counts,
                                float *sums, void *scratch);
 size_t inliers_scratch_bytes(uint32_t n, uint32_t W);
+// the polish result block, int32 / float words: pass k's model[9], ok, count, sum at
+// kPolPass * k (pass 0's slots 12-13: the initial getInliers' count, sum), the fitted point
+// counts of passes 1..3 at kPolNs + k, the device's (best, prev) at kPolState
+constexpr int kPolPass = 16, kPolNs = 64, kPolState = 68, kPolWords = 72;
+hipError_t launch_polish_prep(hipStream_t st, int32_t *res, int k, int32_t best0);
 // every point's exact residual under one model (n floats)
 hipError_t launch_point_errors(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *model,
                                float *errors);
