@@ -370,13 +370,8 @@ __device__ __forceinline__ void score_group(const HModel &M, float4 X1, float4 Y
 // perm (nullable): lane i of the grid scores hypothesis perm[i] (k_presort_h groups the
 // hypotheses that survive stage A often into the same waves, so the other waves rarely
 // take the stage-B branch); results land at the hypothesis' own index.
-#ifdef HF_EXP_W8  // A/B hook: hold the scorer at 8 waves per SIMD (<= 64 VGPRs)
-#define HF_W8_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
-#else
-#define HF_W8_ATTR
-#endif
 template <int CHUNKS, bool EXACT_SUM>
-__global__ __launch_bounds__(64 * CHUNKS) HF_W8_ATTR void k_score_hf(const float4 *__restrict__ rec, uint32_t n, float4 ext,
+__global__ __launch_bounds__(64 * CHUNKS) void k_score_hf(const float4 *__restrict__ rec, uint32_t n, float4 ext,
                                                           const float *__restrict__ models, uint32_t B, float thr,
                                                           const uint32_t *__restrict__ perm,
                                                           int32_t *__restrict__ counts, float *__restrict__ sums,
@@ -407,89 +402,12 @@ __global__ __launch_bounds__(64 * CHUNKS) HF_W8_ATTR void k_score_hf(const float
     // its point pairs straight from the loaded registers (no copies); 8 waves per SIMD hide
     // the scalar-load latency
     uint32_t g = gbeg;
-#ifdef HF_EXP_QUAD  // A/B hook: one keep ballot per four groups; a hit re-runs the groups' stage A
-    for (; g + 4 <= gend; g += 4) {
-        const float4 *p = rec + 8 * (size_t)g;
-        uint64_t any;
-        {
-            const float4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], b0 = p[8], b1 = p[9], b2 = p[10], b3 = p[11];
-            bool k0, k1, k2, k3, k4, k5, k6, k7;
-            stage_a_keep2(M, v2f{a0.x, a0.y}, v2f{a1.x, a1.y}, v2f{a2.x, a2.y}, v2f{a3.x, a3.y}, k0, k1);
-            stage_a_keep2(M, v2f{a0.z, a0.w}, v2f{a1.z, a1.w}, v2f{a2.z, a2.w}, v2f{a3.z, a3.w}, k2, k3);
-            stage_a_keep2(M, v2f{b0.x, b0.y}, v2f{b1.x, b1.y}, v2f{b2.x, b2.y}, v2f{b3.x, b3.y}, k4, k5);
-            stage_a_keep2(M, v2f{b0.z, b0.w}, v2f{b1.z, b1.w}, v2f{b2.z, b2.w}, v2f{b3.z, b3.w}, k6, k7);
-            any = __builtin_amdgcn_ballot_w64(k0 | k1 | k2 | k3 | k4 | k5 | k6 | k7);
-        }
-        {
-            const float4 a0 = p[16], a1 = p[17], a2 = p[18], a3 = p[19], b0 = p[24], b1 = p[25], b2 = p[26],
-                         b3 = p[27];
-            bool k0, k1, k2, k3, k4, k5, k6, k7;
-            stage_a_keep2(M, v2f{a0.x, a0.y}, v2f{a1.x, a1.y}, v2f{a2.x, a2.y}, v2f{a3.x, a3.y}, k0, k1);
-            stage_a_keep2(M, v2f{a0.z, a0.w}, v2f{a1.z, a1.w}, v2f{a2.z, a2.w}, v2f{a3.z, a3.w}, k2, k3);
-            stage_a_keep2(M, v2f{b0.x, b0.y}, v2f{b1.x, b1.y}, v2f{b2.x, b2.y}, v2f{b3.x, b3.y}, k4, k5);
-            stage_a_keep2(M, v2f{b0.z, b0.w}, v2f{b1.z, b1.w}, v2f{b2.z, b2.w}, v2f{b3.z, b3.w}, k6, k7);
-            any |= __builtin_amdgcn_ballot_w64(k0 | k1 | k2 | k3 | k4 | k5 | k6 | k7);
-        }
-        if (__builtin_expect(any == 0, 1)) continue;
-#pragma unroll 1
-        for (int u = 0; u < 4; u++)
-            score_group<EXACT_SUM>(M, p[8 * u], p[8 * u + 1], p[8 * u + 2], p[8 * u + 3], p[8 * u + 4], p[8 * u + 5], T,
-                                   thr, cnt, sum);
-    }
-#endif
-#ifdef HF_EXP_DEFER  // A/B hook: a pair's keep ballot read one iteration later (its stage B, keeps
-                     // recomputed, after the next pair's stage A; cnt / sum keep point order)
-    {
-        const float4 *pp = rec;
-        uint64_t pend = 0;
-        for (; g + 2 <= gend; g += 2) {
-            const float4 *p = rec + 8 * (size_t)g;
-            const float4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], b0 = p[8], b1 = p[9], b2 = p[10], b3 = p[11];
-            bool k0, k1, k2, k3, k4, k5, k6, k7;
-            stage_a_keep2(M, v2f{a0.x, a0.y}, v2f{a1.x, a1.y}, v2f{a2.x, a2.y}, v2f{a3.x, a3.y}, k0, k1);
-            stage_a_keep2(M, v2f{a0.z, a0.w}, v2f{a1.z, a1.w}, v2f{a2.z, a2.w}, v2f{a3.z, a3.w}, k2, k3);
-            stage_a_keep2(M, v2f{b0.x, b0.y}, v2f{b1.x, b1.y}, v2f{b2.x, b2.y}, v2f{b3.x, b3.y}, k4, k5);
-            stage_a_keep2(M, v2f{b0.z, b0.w}, v2f{b1.z, b1.w}, v2f{b2.z, b2.w}, v2f{b3.z, b3.w}, k6, k7);
-            const uint64_t cur = __builtin_amdgcn_ballot_w64(k0 | k1 | k2 | k3 | k4 | k5 | k6 | k7);
-            if (__builtin_expect(pend != 0, 0)) {
-                score_group<EXACT_SUM>(M, pp[0], pp[1], pp[2], pp[3], pp[4], pp[5], T, thr, cnt, sum);
-                score_group<EXACT_SUM>(M, pp[8], pp[9], pp[10], pp[11], pp[12], pp[13], T, thr, cnt, sum);
-            }
-            pend = cur;
-            pp = p;
-        }
-        if (pend) {
-            score_group<EXACT_SUM>(M, pp[0], pp[1], pp[2], pp[3], pp[4], pp[5], T, thr, cnt, sum);
-            score_group<EXACT_SUM>(M, pp[8], pp[9], pp[10], pp[11], pp[12], pp[13], T, thr, cnt, sum);
-        }
-    }
-#endif
     for (; g + 2 <= gend; g += 2) {
         const float4 *p = rec + 8 * (size_t)g;
         const float4 a0 = p[0], a1 = p[1], a2 = p[2], a3 = p[3], ab = p[4], at = p[5];
         const float4 b0 = p[8], b1 = p[9], b2 = p[10], b3 = p[11], bb = p[12], bt = p[13];
-#ifdef HF_EXP_PAIR  // A/B hook: one keep ballot per two groups (half the VALU -> SALU -> branch turns)
-        bool k[8];
-        stage_a_keep2(M, v2f{a0.x, a0.y}, v2f{a1.x, a1.y}, v2f{a2.x, a2.y}, v2f{a3.x, a3.y}, k[0], k[1]);
-        stage_a_keep2(M, v2f{a0.z, a0.w}, v2f{a1.z, a1.w}, v2f{a2.z, a2.w}, v2f{a3.z, a3.w}, k[2], k[3]);
-        stage_a_keep2(M, v2f{b0.x, b0.y}, v2f{b1.x, b1.y}, v2f{b2.x, b2.y}, v2f{b3.x, b3.y}, k[4], k[5]);
-        stage_a_keep2(M, v2f{b0.z, b0.w}, v2f{b1.z, b1.w}, v2f{b2.z, b2.w}, v2f{b3.z, b3.w}, k[6], k[7]);
-        if (__builtin_expect(__builtin_amdgcn_ballot_w64(k[0] | k[1] | k[2] | k[3] | k[4] | k[5] | k[6] | k[7]) == 0, 1))
-            continue;
-        if (k[0]) stage_b<EXACT_SUM>(M, a0.x, a1.x, a2.x, a3.x, ab.x, T, thr, cnt, sum);
-        if (k[1]) stage_b<EXACT_SUM>(M, a0.y, a1.y, a2.y, a3.y, ab.y, T, thr, cnt, sum);
-        if (k[2]) stage_b<EXACT_SUM>(M, a0.z, a1.z, a2.z, a3.z, ab.z, T, thr, cnt, sum);
-        if (k[3]) stage_b<EXACT_SUM>(M, a0.w, a1.w, a2.w, a3.w, ab.w, T, thr, cnt, sum);
-        if (k[4]) stage_b<EXACT_SUM>(M, b0.x, b1.x, b2.x, b3.x, bb.x, T, thr, cnt, sum);
-        if (k[5]) stage_b<EXACT_SUM>(M, b0.y, b1.y, b2.y, b3.y, bb.y, T, thr, cnt, sum);
-        if (k[6]) stage_b<EXACT_SUM>(M, b0.z, b1.z, b2.z, b3.z, bb.z, T, thr, cnt, sum);
-        if (k[7]) stage_b<EXACT_SUM>(M, b0.w, b1.w, b2.w, b3.w, bb.w, T, thr, cnt, sum);
-        (void)at;
-        (void)bt;
-#else
         score_group<EXACT_SUM>(M, a0, a1, a2, a3, ab, at, T, thr, cnt, sum);
         score_group<EXACT_SUM>(M, b0, b1, b2, b3, bb, bt, T, thr, cnt, sum);
-#endif
     }
     if (g < gend) {
         const float4 *p = rec + 8 * (size_t)g;

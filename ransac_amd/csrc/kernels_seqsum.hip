@@ -22,6 +22,7 @@
 // Layout of one fit's scratch (seqsum_scratch_bytes(nch)): psum[kSegMax][nch] doubles (the
 // fp64 segment sums), then R[kSegMax][nch][kCand] floats (every candidate's segment end).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "usac_kernels.h"
 #include "usac_seqsum.hpp"
@@ -125,6 +126,72 @@ __global__ __launch_bounds__(kCand) void k_seq_seg(const typename Op<F64>::V *__
     for (int q = 0; q < NCH; q++) R[((size_t)j * NCH + q) * kCand + t] = s[q];
 }
 
+// The same segment ends with the chains split over the waves: workgroup (segment j, fit b) of
+// kCand * NCH threads, thread t runs chain q = t / kCand (wave-uniform) from candidate
+// c = t % kCand -- one dependent chain per lane instead of NCH interleaved ones, NCH times the
+// waves to hide its latency.  The chunk is staged transposed ([chain][element]) so a wave reads
+// its chain's next elements with 16-byte broadcast reads.  Same starts, same ops, same ends.
+template <int NCH, bool F64>
+__global__ __launch_bounds__(kCand *NCH) void k_seq_seg_split(const typename Op<F64>::V *__restrict__ vals,
+                                                              size_t vstride, const uint32_t *__restrict__ ns,
+                                                              uint32_t n1, const uint32_t *__restrict__ slots,
+                                                              char *scratch, size_t sstride) {
+    typedef typename Op<F64>::V V;
+    constexpr uint32_t kT = kCand * NCH;                 // threads
+    constexpr uint32_t kChunk = 1024;                    // elements per LDS chunk
+    constexpr uint32_t kPer = kChunk * NCH / kT;         // values per thread per chunk (4)
+    constexpr uint32_t kVec = 16 / sizeof(V);            // elements per 16-byte read
+    typedef V Vv __attribute__((ext_vector_type(kVec)));
+    __shared__ __attribute__((aligned(16))) V sv[2][NCH][kChunk + kVec];  // rows padded 16 B: no bank conflicts
+    __shared__ double sp[kSegMax * NCH];
+    const uint32_t j = blockIdx.x, w = fit_slot(slots, blockIdx.y);
+    const uint32_t n = fit_n(ns, n1, w), L = seg_len(n);
+    if (j * L >= n) return;
+    const uint32_t b = j * L, e = b + L < n ? b + L : n;
+    const double *psum = reinterpret_cast<const double *>(scratch + w * sstride);
+    float *R = reinterpret_cast<float *>(scratch + w * sstride + sizeof(double) * kSegMax * NCH);
+    const V *__restrict__ v = vals + w * vstride + (size_t)b * NCH;
+    const uint32_t tot = (e - b) * NCH;
+    const uint32_t t = threadIdx.x;
+    const uint32_t q = __builtin_amdgcn_readfirstlane(t / kCand), c = t % kCand;
+    V pre[kPer];
+    auto fetch = [&](uint32_t ch) {
+#pragma unroll
+        for (uint32_t u = 0; u < kPer; u++) {
+            const uint32_t i = ch * kChunk * NCH + t + kT * u;
+            pre[u] = i < tot ? v[i] : V(0);
+        }
+    };
+    fetch(0);
+    for (uint32_t i = t; i < j * NCH; i += kT) sp[i] = psum[i];
+    __syncthreads();
+    float s = cand_start(centre(sp, j, NCH, q), c);
+    const uint32_t nch = (e - b + kChunk - 1) / kChunk;
+    for (uint32_t ch = 0; ch < nch; ch++) {
+#pragma unroll
+        for (uint32_t u = 0; u < kPer; u++) {
+            const uint32_t i = t + kT * u;  // value i of the chunk: element i / NCH, chain i % NCH
+            sv[ch & 1][i % NCH][i / NCH] = pre[u];
+        }
+        __syncthreads();
+        if (ch + 1 < nch) fetch(ch + 1);
+        const V *buf = sv[ch & 1][q];
+        const uint32_t m = e - b - ch * kChunk < kChunk ? e - b - ch * kChunk : kChunk;
+        uint32_t k = 0;
+        for (; k + 8 <= m; k += 8) {
+            Vv x[8 / kVec];
+#pragma unroll
+            for (uint32_t u = 0; u < 8 / kVec; u++) x[u] = *reinterpret_cast<const Vv *>(buf + k + kVec * u);
+#pragma unroll
+            for (uint32_t u = 0; u < 8 / kVec; u++)
+#pragma unroll
+                for (uint32_t z = 0; z < kVec; z++) s = Op<F64>::step(s, x[u][z]);
+        }
+        for (; k < m; k++) s = Op<F64>::step(s, buf[k]);
+    }
+    R[((size_t)j * NCH + q) * kCand + c] = s;
+}
+
 // link: workgroup (chain q, fit b); the four waves stage the chain's candidate ends into
 // LDS, then wave 0 walks the segments (every lane the same value)
 template <int NCH, bool F64>
@@ -139,11 +206,11 @@ __global__ __launch_bounds__(256) void k_seq_link(const typename Op<F64>::V *__r
     const uint32_t S = (n + L - 1) / L;
     const double *psum = reinterpret_cast<const double *>(scratch + w * sstride);
     const float *R = reinterpret_cast<const float *>(scratch + w * sstride + sizeof(double) * kSegMax * NCH);
+    if (threadIdx.x < S) sp[threadIdx.x] = psum[threadIdx.x * NCH + q];
     for (uint32_t i = threadIdx.x; i < S * kCand; i += 256) {
         const uint32_t j = i / kCand, c = i % kCand;
         sR[j][c] = R[((size_t)j * NCH + q) * kCand + c];
     }
-    if (threadIdx.x < S) sp[threadIdx.x] = psum[threadIdx.x * NCH + q];
     __syncthreads();
     if (threadIdx.x >= 64) return;
     const typename Op<F64>::V *__restrict__ v = vals + w * vstride;
@@ -179,6 +246,16 @@ __global__ __launch_bounds__(256) void k_seq_link(const typename Op<F64>::V *__r
 
 size_t seqsum_scratch_bytes(int nch) { return scratch_bytes(nch); }
 
+// multi-chain segment kernel: chains split over waves (default) or interleaved per lane
+// (USAC_SEQ_SPLIT=0, the round-3 kernel; kept for A/B)
+static bool seg_split() {
+    static const bool on = [] {
+        const char *e = getenv("USAC_SEQ_SPLIT");
+        return !e || atoi(e) != 0;
+    }();
+    return on;
+}
+
 hipError_t launch_seqsum(hipStream_t st, int nch, bool f64, const void *vals, size_t vstride, const uint32_t *ns,
                          uint32_t n1, uint32_t W, const uint32_t *slots, void *scratch, size_t sstride,
                          bool have_psum, float *out) {
@@ -191,7 +268,11 @@ hipError_t launch_seqsum(hipStream_t st, int nch, bool f64, const void *vals, si
         const V_ *v_ = static_cast<const V_ *>(vals);                                                               \
         if (!have_psum)                                                                                             \
             hipLaunchKernelGGL((k_seq_psum<N, D>), gs, dim3(256), 0, st, v_, vstride, ns, n1, slots, scr, sstride); \
-        hipLaunchKernelGGL((k_seq_seg<N, D>), gs, dim3(kCand), 0, st, v_, vstride, ns, n1, slots, scr, sstride);    \
+        if (N > 1 && seg_split())                                                                                   \
+            hipLaunchKernelGGL((k_seq_seg_split<N, D>), gs, dim3(kCand * N), 0, st, v_, vstride, ns, n1, slots, scr,   \
+                               sstride);                                                                            \
+        else                                                                                                        \
+            hipLaunchKernelGGL((k_seq_seg<N, D>), gs, dim3(kCand), 0, st, v_, vstride, ns, n1, slots, scr, sstride);  \
         hipLaunchKernelGGL((k_seq_link<N, D>), gl, dim3(256), 0, st, v_, vstride, ns, n1, slots, scr, sstride, out); \
     } while (0)
     if (nch == 1 && !f64) SEQ(1, false);

@@ -2803,12 +2803,12 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     }
 
     lap(T_REPLAY);
-    // ---- polish (ransac.cpp:157-207) on the device, the four passes in ONE submission: pass k
+    // ---- polish (ransac.cpp:157-207) on the device, the passes submitted in groups: pass k
     // fits the list pass k - 1 scored (the initial getInliers(best_model) list for pass 0) and
     // scores the fitted model from device memory into list k + 1 (compaction gated on the fit's
     // ok); between passes k_polish_prep takes the host's acceptance decision on the device and
     // hands pass k + 1 its point count, or 0 after a rejection (a no-op pass).  All results land
-    // in one device block (usac_kernels.h kPol*) copied with one D2H; the host then replays the
+    // in one device block (usac_kernels.h kPol*) copied with one D2H per group; the host replays the
     // reference's loop on them and stops at the first rejection, so `cur` ends as best_model's
     // own inlier list (the same kernels, model and threshold as the final getInliers would use).
     HIP_TRY(c, c->pol_res.reserve(sizeof(float) * usac::kPolWords));
@@ -2825,41 +2825,53 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     HIP_TRY(c, usac::launch_inliers_batch(c->stream, c->estimator, c->pts.p, c->n, c->one_model.as<float>(), 1, thr,
                                           nullptr, nullptr, lists[0], 0, dres_i + 12, dres + 13,
                                           c->inl_scratch.p));  // quality->getInliers(best_model)
+    // passes go out in groups of G (USAC_POLISH_GROUP, default 2): a group is one submission and
+    // one host wait; the next group is submitted only while every pass so far was accepted
     constexpr int kPasses = 4;
-    for (int k = 0; k < kPasses; k++) {
-        float *pres = dres + usac::kPolPass * k;
-        int32_t *dok = dres_i + usac::kPolPass * k + 9;
-        if (k == 0)
-            HIP_TRY(c, enqueue_nonminimal(c, lists[0], (uint32_t)best.inlier_number, pres, dok));
-        else  // the count pass k - 1's acceptance left on the device; c->n bounds it
-            HIP_TRY(c, enqueue_nonminimal(c, lists[k], c->n, pres, dok, nullptr,
-                                          reinterpret_cast<const uint32_t *>(dres_i + usac::kPolNs + k)));
-        HIP_TRY(c, usac::launch_inliers_batch(c->stream, c->estimator, c->pts.p, c->n, pres, 1, thr, nullptr, nullptr,
-                                              lists[k + 1], 0, dok + 1, pres + 11, c->inl_scratch.p, dok));
-        if (k + 1 < kPasses) HIP_TRY(c, usac::launch_polish_prep(c->stream, dres_i, k, best.inlier_number));
-    }
-    HIP_TRY(c, hipMemcpyAsync(c->pol_pin, dres, sizeof(float) * usac::kPolPass * kPasses, hipMemcpyDeviceToHost,
-                              c->stream));
-    HIP_TRY(c, stream_wait(c->stream));
+    const int kGroup = [] {
+        const char *g = getenv("USAC_POLISH_GROUP");
+        const int v = g ? atoi(g) : 2;
+        return v < 1 ? 1 : v > kPasses ? kPasses : v;
+    }();
     int32_t *cur = lists[0];
     int32_t cur_cnt = 0;
-    memcpy(&cur_cnt, hres + 12, sizeof(int32_t));
     int prev = 0;
-    for (int k = 0; k < kPasses; k++) {  // ransac.cpp:170-200, on the passes' results
-        const float *r = hres + usac::kPolPass * k;
-        memcpy(&ok, r + 9, sizeof(int32_t));
-        memcpy(&cnt, r + 10, sizeof(int32_t));
-        memcpy(&s, r + 11, sizeof(float));
-        if (!ok) break;
-        if ((double)((float)cnt / (float)best.inlier_number) < 0.8) break;
-        if (cnt <= prev) break;
-        prev = cnt;
-        best.inlier_number = cnt;
-        best.score = s;
-        memcpy(best_model, r, sizeof(best_model));
-        cur = lists[k + 1];
-        cur_cnt = cnt;
-        out->polish_passes++;
+    bool stop = false;
+    for (int k0 = 0; k0 < kPasses && !stop; k0 += kGroup) {
+        const int k1 = std::min(k0 + kGroup, kPasses);
+        for (int k = k0; k < k1; k++) {
+            float *pres = dres + usac::kPolPass * k;
+            int32_t *dok = dres_i + usac::kPolPass * k + 9;
+            if (k == 0)
+                HIP_TRY(c, enqueue_nonminimal(c, lists[0], (uint32_t)best.inlier_number, pres, dok));
+            else  // the count pass k - 1's acceptance left on the device; c->n bounds it
+                HIP_TRY(c, enqueue_nonminimal(c, lists[k], c->n, pres, dok, nullptr,
+                                              reinterpret_cast<const uint32_t *>(dres_i + usac::kPolNs + k)));
+            HIP_TRY(c, usac::launch_inliers_batch(c->stream, c->estimator, c->pts.p, c->n, pres, 1, thr, nullptr,
+                                                  nullptr, lists[k + 1], 0, dok + 1, pres + 11, c->inl_scratch.p, dok));
+            if (k + 1 < kPasses) HIP_TRY(c, usac::launch_polish_prep(c->stream, dres_i, k, best.inlier_number));
+        }
+        HIP_TRY(c, hipMemcpyAsync(c->pol_pin, dres, sizeof(float) * usac::kPolPass * k1, hipMemcpyDeviceToHost,
+                                  c->stream));
+        HIP_TRY(c, stream_wait(c->stream));
+        if (k0 == 0) memcpy(&cur_cnt, hres + 12, sizeof(int32_t));
+        for (int k = k0; k < k1; k++) {  // ransac.cpp:170-200, on the passes' results
+            const float *r = hres + usac::kPolPass * k;
+            memcpy(&ok, r + 9, sizeof(int32_t));
+            memcpy(&cnt, r + 10, sizeof(int32_t));
+            memcpy(&s, r + 11, sizeof(float));
+            if (!ok || (double)((float)cnt / (float)best.inlier_number) < 0.8 || cnt <= prev) {
+                stop = true;
+                break;
+            }
+            prev = cnt;
+            best.inlier_number = cnt;
+            best.score = s;
+            memcpy(best_model, r, sizeof(best_model));
+            cur = lists[k + 1];
+            cur_cnt = cnt;
+            out->polish_passes++;
+        }
     }
     const auto t1 = std::chrono::steady_clock::now();
     lap(T_POLISH);

@@ -152,3 +152,34 @@ def test_speculation_on_off_identical(usac):
             batches += a.raw["spec_batches"]
             rollbacks += a.raw["spec_rollbacks"]
     assert batches > 0 and rollbacks > 0, (batches, rollbacks)
+
+
+@pytest.mark.parametrize("kind", ["H", "F", "L"])
+def test_polish_groups_identical(usac, oracle, kind):
+    """The polish passes go out in groups (USAC_POLISH_GROUP; k_polish_prep takes each pass's
+    acceptance on the device): one pass per submission, two, and all four give the oracle's
+    polish -- passes, final model bits, inlier list."""
+    import os
+    okind = {"H": oracle.HOMOGRAPHY, "F": oracle.FUNDAMENTAL, "L": oracle.LINE2D}[kind]
+    est = {"H": usac.ESTIMATOR.Homography, "F": usac.ESTIMATOR.Fundamental, "L": usac.ESTIMATOR.Line2d}[kind]
+    thr = 2.0 if kind != "L" else 8.0
+    passes = set()
+    for seed in (1, 2, 3, 4):
+        pts = _data(kind, seed, False)
+        ref = oracle.ransac_run(okind, pts, thr, 0.95, seed)
+        passes.add(ref["polish_passes"])
+        for g in ("1", "2", "4"):
+            os.environ["USAC_POLISH_GROUP"] = g
+            try:
+                m = usac.Model(thr, {"H": 4, "F": 7, "L": 2}[kind], 0.95, 7, est, usac.SAMPLER.Uniform)
+                m.ResetRandomGenerator(False)
+                m.setSeed(seed)
+                r = usac.Ransac(m, pts)
+                r.run()
+            finally:
+                os.environ.pop("USAC_POLISH_GROUP", None)
+            out = r.getRansacOutput()
+            assert out.raw["polish_passes"] == ref["polish_passes"], (seed, g)
+            assert (_bits(out.getModel()) == _bits(ref["model"])).all(), (seed, g)
+            assert (out.getInliers() == ref["inlier_idx"]).all(), (seed, g)
+    assert max(passes) >= 1
