@@ -175,9 +175,10 @@ def timed_kernel_parity(usac, ctx, kind, pts, thr, dlt_mode, seed, sprt, first_h
     counts exact (SPRT: every accepted model's count), Σ within the throughput kernel's declared
     bound, and the batch record (Score::bigger + earliest index) against the oracle's exact
     (count, Σ).  The Σ bound per model with c inliers: two-view (exact terms, sums re-associated
-    over point chunks) |Σ| c 2^-23; homography (stage-B terms from v_rcp / v_sqrt, DESIGN.md
-    "Guard band": |S - 2 e| <= 2^-21 Mp + 2^-18 S per pair, Mp <= the dataset's max |x1|+|y1|+
-    |x2|+|y2|) c (2^-22 Mp_max + 2^-18 thr) + |Σ| c 2^-23."""
+    over point chunks) |Σ| c 2^-23, essential plus c thr 2^-18 (its drains' guarded residual);
+    homography (stage-B terms from v_rcp / v_sqrt, DESIGN.md "Guard band": |S - 2 e| <= 2^-21 Mp
+    + 2^-18 S per pair, Mp <= the dataset's max |x1|+|y1|+|x2|+|y2|) c (2^-22 Mp_max + 2^-18 thr)
+    + |Σ| c 2^-23."""
     from oracle import oracle as O
 
     fund, ess = kind == "fundamental", kind == "essential"
@@ -201,6 +202,8 @@ def timed_kernel_parity(usac, ctx, kind, pts, thr, dlt_mode, seed, sprt, first_h
     cnt = np.maximum(oc[chk], 0).astype(np.float64)
     ref = np.abs(osum[chk].astype(np.float64))
     bound = ref * cnt * 2.0 ** -23
+    if ess:  # the guarded essential residual's terms (kernels_fund.hip essential_error_guarded)
+        bound += cnt * thr * 2.0 ** -18
     if not (fund or ess):
         mp = float(np.abs(pts.astype(np.float64)).sum(1).max())
         bound += cnt * (2.0 ** -22 * mp + 2.0 ** -18 * thr)

@@ -296,9 +296,43 @@ __device__ __forceinline__ void two_view_reject2(const TwoViewModel<EST> &M, v2f
 // branch would run the exact path nearly always; the queues run it only for kept pairs.
 constexpr int kTvQueue = 16;  // entries per lane (4 KB of LDS per wave)
 
+// The guarded essential residual of the throughput drains (C > 1: Σ is re-associated anyway and
+// its terms may carry a stated error; the counts stay exact).  The reference's l, t, a1, b1 and
+// squared norms (the same unfused operations), then e' = (|a1| rsq(a2²) + |b1| rsq(b2²)) / 2
+// with v_rsq_f32 (1 ulp) instead of two correctly rounded square roots and two IEEE divisions.
+// Per term the two differ by < 2^-21 relative (rsq 2^-23, the product and the reference's sqrt
+// and division 2^-24 each), so |e' - e| <= e' 2^-19: e' <= thr (1 - 2^-16) proves e < thr and
+// e' >= thr (1 + 2^-16) proves !(e < thr).  Pairs inside that band, squared norms outside
+// [2^-96, inf) (denormal / zero / overflowing rsq) and non-finite values take the exact
+// expression.  Returns the error added to Σ: e' for a proven inlier, else the exact e.
+__device__ __forceinline__ float essential_error_guarded(const float *E, float x1, float y1, float x2, float y2,
+                                                         float thr, float lo, float hi, bool &inl) {
+    const float l1 = E[0] * x2 + E[3] * y2 + E[6];
+    const float l2 = E[1] * x2 + E[4] * y2 + E[7];
+    const float l3 = E[2] * x2 + E[5] * y2 + E[8];
+    const float t1 = E[0] * x1 + E[1] * y1 + E[2];
+    const float t2 = E[3] * x1 + E[4] * y1 + E[5];
+    const float t3 = E[6] * x1 + E[7] * y1 + E[8];
+    const float a1 = l1 * x1 + l2 * y1 + l3;
+    const float qa = l1 * l1 + l2 * l2;
+    const float b1 = t1 * x2 + t2 * y2 + t3;
+    const float qb = t1 * t1 + t2 * t2;
+    const float ef = (fabsf(a1) * __builtin_amdgcn_rsqf(qa) + fabsf(b1) * __builtin_amdgcn_rsqf(qb)) * 0.5f;
+    const bool normal = qa >= 1.2621774483536189e-29f && qb >= 1.2621774483536189e-29f &&  // 2^-96
+                        qa < INFINITY && qb < INFINITY;
+    if (__builtin_expect(normal && (ef <= lo || ef >= hi), 1)) {
+        inl = ef <= lo;
+        return ef;
+    }
+    const float e = (fabsf(a1 / sqrtf(qa)) + fabsf(b1 / sqrtf(qb))) / 2;  // essential_error, bit for bit
+    inl = e < thr;
+    return e;
+}
+
 template <int EST>
 __device__ __forceinline__ void two_view_drain(const TwoViewModel<EST> &M, const float4 *__restrict__ pts,
-                                               const uint32_t *q, int &len, float thr, int &cnt, float &sum) {
+                                               const uint32_t *q, int &len, float thr, int &cnt, float &sum,
+                                               bool fast = false, float lo = 0.f, float hi = 0.f) {
     // each lane walks its kept points in order, two per trip: the two loads and exact
     // evaluations of a trip are independent (latency overlap), the adds stay in order
     int t = 0;
@@ -327,15 +361,25 @@ __device__ __forceinline__ void two_view_drain(const TwoViewModel<EST> &M, const
         const float4 p1 = pts[i1];
 #ifdef TV_EXP_CHEAPDRAIN  // A/B hook: the drain's loads and queue walk, a trivial residual
         const float e0 = fabsf(p0.x * M.f[0] + p0.w), e1 = fabsf(p1.x * M.f[0] + p1.w);
+        const bool in0 = e0 < thr, in1 = e1 < thr;
 #else
-        const float e0 = two_view_error<EST>(M.f, p0.x, p0.y, p0.z, p0.w);
-        const float e1 = two_view_error<EST>(M.f, p1.x, p1.y, p1.z, p1.w);
+        float e0, e1;
+        bool in0, in1;
+        if (EST == USAC_ESSENTIAL && fast) {  // wave-uniform
+            e0 = essential_error_guarded(M.f, p0.x, p0.y, p0.z, p0.w, thr, lo, hi, in0);
+            e1 = essential_error_guarded(M.f, p1.x, p1.y, p1.z, p1.w, thr, lo, hi, in1);
+        } else {
+            e0 = two_view_error<EST>(M.f, p0.x, p0.y, p0.z, p0.w);
+            e1 = two_view_error<EST>(M.f, p1.x, p1.y, p1.z, p1.w);
+            in0 = e0 < thr;
+            in1 = e1 < thr;
+        }
 #endif
-        if (h0 && e0 < thr) {
+        if (h0 && in0) {
             cnt++;
             sum += e0;
         }
-        if (h1 && e1 < thr) {
+        if (h1 && in1) {
             cnt++;
             sum += e1;
         }
@@ -391,6 +435,10 @@ __global__ __launch_bounds__(64) void k_score_f2(const float4 *__restrict__ rec,
     const uint32_t per = (ngroups + C - 1) / C;
     const uint32_t gbeg = chunk * per < ngroups ? chunk * per : ngroups;
     const uint32_t gend = gbeg + per < ngroups ? gbeg + per : ngroups;
+    // throughput launches (C > 1: Σ re-associated over chunks): the essential drains take the
+    // guarded residual (essential_error_guarded; counts exact, Σ terms within 2^-19 relative)
+    const bool fast = EST == USAC_ESSENTIAL && C > 1 && thr >= 7.888609052210118e-31f && thr < 1.0e30f;  // 2^-100
+    const float lo = thr * 0.9999847412109375f, hi = thr * 1.0000152587890625f;  // thr (1 -+ 2^-16)
     uint32_t *q = &s_q[lane];
     int len = 0, cnt = 0;
     float sum = 0.f;
@@ -415,7 +463,8 @@ __global__ __launch_bounds__(64) void k_score_f2(const float4 *__restrict__ rec,
 #else
             two_view_append(q, len, g, n, ma | (mb << 4) | M.all);
 #endif
-            if (__builtin_amdgcn_ballot_w64(len == kTvQueue)) two_view_drain<EST>(M, pts, q, len, thr, cnt, sum);
+            if (__builtin_amdgcn_ballot_w64(len == kTvQueue))
+                two_view_drain<EST>(M, pts, q, len, thr, cnt, sum, fast, lo, hi);
             a0 = c0; a1 = c1; a2 = c2; a3 = c3;
             b0 = d0; b1 = d1; b2 = d2; b3 = d3;
         }
@@ -424,7 +473,7 @@ __global__ __launch_bounds__(64) void k_score_f2(const float4 *__restrict__ rec,
         const float4 *p = rec + 8 * (size_t)g;
         two_view_append(q, len, g, n, (two_view_group<EST>(M, p[0], p[1], p[2], p[3]) | M.all) & 0xFu);
     }
-    two_view_drain<EST>(M, pts, q, len, thr, cnt, sum);
+    two_view_drain<EST>(M, pts, q, len, thr, cnt, sum, fast, lo, hi);
     if (!live) return;
     if (C == 1) {
         counts[slot] = cnt;

@@ -81,3 +81,41 @@ def test_fast_twoview_full_batch_equals_exact(usac, kind):
         ctx.hypothesize_async(65536, 7, 0, thr)
         rec = ctx.fetch_best()
         assert rec.inliers == be["inliers"]
+
+
+def test_essential_guarded_drain(usac, oracle):
+    """The throughput launches' essential drains take the guarded residual (kernels_fund.hip
+    essential_error_guarded: v_rsq_f32 instead of the correctly rounded square roots and IEEE
+    divisions, the exact expression inside a 2^-16 band around thr).  A device batch scored in
+    8 chunks: every count equals the oracle's -- also with thr placed exactly on a pair's error
+    and on the next float -- and each Σ is within the stated bound c thr 2^-18 + |Σ| c 2^-23."""
+    pts, _, _ = synthetic.fundamental_points(n=20000, inlier_ratio=0.3, seed=3, normalized=True)
+    B, seed = 512, 5
+    est = oracle.Estimator(oracle.ESSENTIAL, pts)
+    with usac.Context(usac.ESTIMATOR.Essential, pts) as ctx:
+        ctx.set_score_chunks(8)
+        smp = ctx.draw_samples(B, seed, 0)
+        om, onm = est.estimate_batch(smp)
+        occ = onm == 1
+        assert occ.sum() > 100
+        # thresholds on the exact errors of pairs of a model with many inliers, and the next floats
+        good = np.flatnonzero(occ)[np.argmax(est.score_models(om[occ], 0.002)[0])]
+        e = est.errors(om[good])
+        near = np.sort(e[(e > 0.001) & (e < 0.004)])[:: max(1, int(((e > 0.001) & (e < 0.004)).sum()) // 3)][:3]
+        thrs = [np.float32(0.002)]
+        for v in near:
+            thrs += [np.float32(v), np.nextafter(np.float32(v), np.float32(np.inf))]
+        differ = 0
+        for thr in thrs:
+            ctx.hypothesize_async(B, seed, 0, float(thr))
+            ctx.fetch_best()
+            c, s = ctx.last_counts(B)
+            oc, osum = est.score_models(om, float(thr))
+            np.testing.assert_array_equal(c[occ], oc[occ], err_msg=str(thr))
+            assert (c[~occ] < 0).all()
+            cnt = oc[occ].astype(np.float64)
+            bound = cnt * float(thr) * 2.0 ** -18 + np.abs(osum[occ].astype(np.float64)) * cnt * 2.0 ** -23
+            err = np.abs(s[occ].astype(np.float64) - osum[occ])
+            assert (err <= bound).all(), (thr, float((err / np.maximum(bound, 1e-30)).max()))
+            differ += int((s[occ] != osum[occ]).sum())
+        assert differ > 0  # the guarded terms are in use (Σ no longer bit-equal)
