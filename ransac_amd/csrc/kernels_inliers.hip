@@ -12,6 +12,8 @@
 //                 (the reference's order; evaluated in parallel, bit-exactly, by launch_seqsum)
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "usac_device.hpp"
 #include "usac_device_e5.hpp"
 #include "usac_kernels.h"
@@ -38,6 +40,15 @@ __device__ __forceinline__ float inl_error(const float *m, const void *pts, uint
         const float4 p = static_cast<const float4 *>(pts)[i];
         return essential_error(m, p.x, p.y, p.z, p.w);
     }
+}
+
+// the same residual of an already loaded point (k_inl_flags issues its points' loads first)
+template <int EST, class P>
+__device__ __forceinline__ float inl_error_p(const float *m, const P &p) {
+    if constexpr (EST == USAC_LINE2D) return line2d_error(m[0], m[1], m[2], p.x, p.y);
+    else if constexpr (EST == USAC_HOMOGRAPHY) return homography_error(m, m + 9, p.x, p.y, p.z, p.w);
+    else if constexpr (EST == USAC_FUNDAMENTAL) return fundamental_error(m, p.x, p.y, p.z, p.w);
+    else return essential_error(m, p.x, p.y, p.z, p.w);
 }
 
 // model parameters of one block (H also needs H^-1: cv::Mat::inv, homography_estimator.hpp:35)
@@ -82,8 +93,17 @@ __global__ __launch_bounds__(kInlThreads) void k_inl_flags(const void *__restric
                                                            const uint32_t *__restrict__ slots,
                                                            uint32_t *__restrict__ scratch,
                                                            const int32_t *__restrict__ ok) {
+    typedef typename std::conditional<EST == USAC_LINE2D, float2, float4>::type P;
     __shared__ float sm[18];
     __shared__ uint32_t wsum[kInlThreads / 64];
+    // the points' loads go out first: they do not depend on the model, whose slot, ok word and
+    // parameters are three dependent loads of their own
+    P pv[kInlPer];
+#pragma unroll
+    for (uint32_t u = 0; u < kInlPer; u++) {
+        const uint32_t i = blockIdx.x * kInlBlock + u * kInlThreads + threadIdx.x;
+        if (i < n) pv[u] = static_cast<const P *>(pts)[i];
+    }
     const uint32_t w = inl_slot(slots, blockIdx.y);
     if (ok && !ok[w]) return;  // a failed fit: k_inl_compact skips the slot too
     inl_model<EST>(models + 9 * (size_t)w, sm);
@@ -96,7 +116,7 @@ __global__ __launch_bounds__(kInlThreads) void k_inl_flags(const void *__restric
 #pragma unroll
     for (uint32_t u = 0; u < kInlPer; u++) {
         const uint32_t i = blockIdx.x * kInlBlock + u * kInlThreads + threadIdx.x;
-        const float e = i < n ? inl_error<EST>(m, pts, i) : 0.f;
+        const float e = i < n ? inl_error_p<EST>(m, pv[u]) : 0.f;
         if (i < n) all_e[i] = e;
         cnt += (uint32_t)__popcll(__ballot(i < n && e < t));
     }
@@ -119,24 +139,29 @@ __global__ __launch_bounds__(kInlThreads) void k_inl_compact(const void *__restr
                                                              int32_t *__restrict__ totals) {
     __shared__ uint32_t wsum[kInlPer][kInlThreads / 64], wpre[kInlThreads / 64];
     const uint32_t ws = inl_slot(slots, blockIdx.y);
+    const size_t stride = inl_stride(n);
+    const uint32_t nb = (n + kInlBlock - 1) / kInlBlock;
+    const uint32_t *block_counts = scratch + ws * stride;
+    float *errs = reinterpret_cast<float *>(scratch + ws * stride + ((nb + 63) & ~63u));
+    const float *all_e = reinterpret_cast<const float *>(scratch + ws * stride + inl_all_offset(n));
+    // the residual loads go out before the ok word is read (a failed fit's are never used)
+    float e[kInlPer];
+#pragma unroll
+    for (uint32_t u = 0; u < kInlPer; u++) {
+        const uint32_t i = blockIdx.x * kInlBlock + u * kInlThreads + threadIdx.x;
+        e[u] = i < n ? all_e[i] : 0.f;
+    }
     if (ok && !ok[ws]) {  // a failed fit: its list is left as it was (workgroup-uniform) and its
         // count reads 0, so the Σ pass over this slot (launch_seqsum) sums nothing
         if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) totals[ws] = 0;
         return;
     }
     const float t = thrs ? thrs[ws] : thr;
-    const size_t stride = inl_stride(n);
-    const uint32_t nb = (n + kInlBlock - 1) / kInlBlock;
-    const uint32_t *block_counts = scratch + ws * stride;
-    float *errs = reinterpret_cast<float *>(scratch + ws * stride + ((nb + 63) & ~63u));
-    const float *all_e = reinterpret_cast<const float *>(scratch + ws * stride + inl_all_offset(n));
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    float e[kInlPer];
     uint64_t bal[kInlPer];
 #pragma unroll
     for (uint32_t u = 0; u < kInlPer; u++) {
         const uint32_t i = blockIdx.x * kInlBlock + u * kInlThreads + threadIdx.x;
-        e[u] = i < n ? all_e[i] : 0.f;
         bal[u] = __ballot(i < n && e[u] < t);
         if (lane == 0) wsum[u][wave] = (uint32_t)__popcll(bal[u]);
     }
