@@ -16,6 +16,12 @@
 #define _DEFAULT_SOURCE
 #include "usac_oracle.h"
 
+/* The LSQ fits' A^T A order (the spec shared with kernels_nonmin.hip kAtaBlock): 16-point
+ * blocks, 64 blocks per superblock.  Round 4 session 2 shortened the block from 64 points: the
+ * device runs one lane per (block, entry group), so the block length is its dependent chain. */
+#define ORC_ATA_BLOCK 16u
+#define ORC_ATA_SUPER (64u * ORC_ATA_BLOCK)
+
 #include <float.h>
 #include <math.h>
 #include <stdlib.h>
@@ -660,18 +666,18 @@ static int homography_normalized_dlt(const orc_est *e, const int *sample, unsign
         pick_vector(W, (int)(2 * n), ORC_DLT_THIN, v);
     } else {
         /* A^T A summation order (no reference order exists -- OpenCV's SVD hides it):
-         * 64-point blocks summed in point order, 64 blocks (4096 points) summed in block order
-         * into a superblock partial, superblock partials summed in order. */
+         * ORC_ATA_BLOCK-point blocks summed in point order, 64 blocks (a superblock) summed in
+         * block order into a superblock partial, superblock partials summed in order. */
         double AtA[9][9];
         memset(AtA, 0, sizeof(AtA));
-        for (unsigned int s0 = 0; s0 < n; s0 += 4096) {
+        for (unsigned int s0 = 0; s0 < n; s0 += ORC_ATA_SUPER) {
             double SP[9][9];
             memset(SP, 0, sizeof(SP));
-            unsigned int s1 = s0 + 4096 < n ? s0 + 4096 : n;
-            for (unsigned int b0 = s0; b0 < s1; b0 += 64) {
+            unsigned int s1 = s0 + ORC_ATA_SUPER < n ? s0 + ORC_ATA_SUPER : n;
+            for (unsigned int b0 = s0; b0 < s1; b0 += ORC_ATA_BLOCK) {
                 double P[9][9];
                 memset(P, 0, sizeof(P));
-                unsigned int b1 = b0 + 64 < n ? b0 + 64 : n;
+                unsigned int b1 = b0 + ORC_ATA_BLOCK < n ? b0 + ORC_ATA_BLOCK : n;
                 for (unsigned int i = b0; i < b1; i++) {
                     double r0[9], r1[9];
                     dlt_fill_rows(norm[4 * i], norm[4 * i + 1], norm[4 * i + 2], norm[4 * i + 3], r0, r1);
@@ -1113,14 +1119,14 @@ static int fundamental_8pt(const orc_est *e, const int *sample, unsigned int n, 
     } else {
         double AtA[9][9]; /* blocks / superblocks as homography_normalized_dlt */
         memset(AtA, 0, sizeof(AtA));
-        for (unsigned int s0 = 0; s0 < n; s0 += 4096) {
+        for (unsigned int s0 = 0; s0 < n; s0 += ORC_ATA_SUPER) {
             double SP[9][9];
             memset(SP, 0, sizeof(SP));
-            unsigned int s1 = s0 + 4096 < n ? s0 + 4096 : n;
-            for (unsigned int b0 = s0; b0 < s1; b0 += 64) {
+            unsigned int s1 = s0 + ORC_ATA_SUPER < n ? s0 + ORC_ATA_SUPER : n;
+            for (unsigned int b0 = s0; b0 < s1; b0 += ORC_ATA_BLOCK) {
                 double P[9][9];
                 memset(P, 0, sizeof(P));
-                unsigned int b1 = b0 + 64 < n ? b0 + 64 : n;
+                unsigned int b1 = b0 + ORC_ATA_BLOCK < n ? b0 + ORC_ATA_BLOCK : n;
                 for (unsigned int i = b0; i < b1; i++) {
                     float x1 = norm[4 * i], y1 = norm[4 * i + 1], x2 = norm[4 * i + 2], y2 = norm[4 * i + 3];
                     float row[9] = {x2 * x1, x2 * y1, x2, y2 * x1, y2 * y1, y2, x1, y1, 1.f};

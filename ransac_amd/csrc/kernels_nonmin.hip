@@ -5,8 +5,9 @@
 //   line2d    : Line2DEstimator::EstimateModelNonMinimalSample PCA (line2d_estimator.hpp:59-107).
 // The reference's fp32 moment sums are sequential in sample order and stay sequential
 // here (one lane per accumulator).  The DLT normal matrix A^T A (fp64) has no reference
-// order (OpenCV's SVD hides it); its order is fixed by this build's spec: 64-point
-// blocks summed in order, block partials summed in block order -- shared with the oracle.
+// order (OpenCV's SVD hides it); its order is fixed by this build's spec: 16-point
+// blocks summed in order, 64 block partials per superblock in block order, superblocks in
+// order -- shared with the oracle.
 #include <hip/hip_runtime.h>
 
 #include "usac_device.hpp"
@@ -15,7 +16,7 @@
 
 namespace usac {
 
-constexpr uint32_t kAtaBlock = 64;
+constexpr uint32_t kAtaBlock = 16;  // A^T A spec block (oracle ORC_ATA_BLOCK); 64 blocks per superblock
 
 // round-robin Jacobi schedule: 9 rounds of 4 disjoint planes (oracle kJacobiRounds)
 __constant__ signed char kJacobiRounds[9][4][2] = {
@@ -223,15 +224,15 @@ __device__ __forceinline__ NormXf norm_xf(const float *t1, const float *t2) {
     return NormXf{t1[0], t1[2], t1[4], t1[5], t2[0], t2[2], t2[4], t2[5]};
 }
 
-// partials of A^T A: one lane per (64-point block, group of 9 of the 45 upper-triangle
+// partials of A^T A: one lane per (16-point block, group of 9 of the 45 upper-triangle
 // entries, row-major j <= k) -- five lanes per block, the group wave-uniform (blockIdx.y) and
 // a compile-time constant in the body; each entry accumulated in registers over the block's
-// points in order; then the workgroup's 64 blocks (a 4096-point superblock) summed in block
+// points in order; then the workgroup's 64 blocks (a 1024-point superblock) summed in block
 // order by one lane per entry, one partial per superblock (the spec's units and order; the
 // grouping only spreads the entries over lanes).  FUND: one 8-point row per correspondence
 // (eight_points.cpp:26-45), else two DLT rows.
 constexpr int kAtaGroups = 5;                  // 45 = 5 x 9 entries
-constexpr uint32_t kAtaGridBound = 8;          // superblock workgroups per fit at most, for a bound nmax
+constexpr uint32_t kAtaGridBound = 32;         // superblock workgroups per fit at most, for a bound nmax
 constexpr int kAtaPer = 45 / kAtaGroups;
 
 template <bool FUND, int G>
@@ -651,9 +652,10 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
 // A whole fit of <= kSmallFit points in one workgroup (the LO inner fits of lo_sample_size
 // points, small polish lists): the points gathered into LDS; the four coordinate sums and the
 // two distance sums as the reference's sequential chains, one lane each (they are short);
-// T1, T2; the normal matrix in the spec's order (64-point blocks in point order, blocks in
+// T1, T2; the normal matrix in the spec's order (16-point blocks in point order, blocks in
 // order: one superblock), lane = entry; fit_finish.  Bit-identical to the multi-launch path.
 constexpr uint32_t kSmallFit = 256;
+static_assert(kSmallFit <= 64 * kAtaBlock, "k_fit_small sums one A^T A superblock");
 
 template <bool FUND>
 __global__ __launch_bounds__(64) void k_fit_small(const float4 *__restrict__ pts, const int32_t *__restrict__ base,
@@ -705,7 +707,7 @@ __global__ __launch_bounds__(64) void k_fit_small(const float4 *__restrict__ pts
         int j, k;
         ata_entry(t, j, k);
         const NormXf xf = norm_xf(t1, t2);
-        double sb = 0.0;  // the superblock (n <= 4096): blocks summed in order
+        double sb = 0.0;  // the superblock (n <= kSmallFit <= 64 kAtaBlock): blocks summed in order
         for (uint32_t b0 = 0; b0 < n; b0 += kAtaBlock) {
             const uint32_t b1 = b0 + kAtaBlock < n ? b0 + kAtaBlock : n;
             double acc = 0.0;
@@ -848,7 +850,7 @@ hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pt
     const char *seq = static_cast<const char *>(b.seq);
     const float *sums4 = reinterpret_cast<const float *>(seq + b.W * seq_stride(b.nmax)), *dsum2 = sums4 + 4 * b.W;
     const uint32_t nblk = (b.nmax + kAtaBlock - 1) / kAtaBlock;
-    // one workgroup per 4096-point superblock; when nmax is only a bound (pipelined LO stages)
+    // one workgroup per 64-block superblock; when nmax is only a bound (pipelined LO stages)
     // at most kAtaGridBound of them per fit, each looping over superblocks
     uint32_t gx = nblk ? (nblk + 63) / 64 : 1;
     if (b.prep && gx > kAtaGridBound) gx = kAtaGridBound;
@@ -867,7 +869,7 @@ hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pt
     return hipGetLastError();
 }
 
-size_t nonminimal_partial_stride(uint32_t nmax) { return 45 * ((size_t)nmax / kAtaBlock + 2); }
+size_t nonminimal_partial_stride(uint32_t nmax) { return 45 * ((size_t)nmax / (64 * kAtaBlock) + 2); }
 
 size_t nonminimal_seq_bytes(uint32_t nmax, uint32_t W) {
     return seq_stride(nmax) * W + sizeof(float) * 6 * W;
