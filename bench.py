@@ -39,7 +39,10 @@ def parse():
                          "(50k correspondences in K^-1-normalised coordinates, threshold 0.002)")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--batch", type=int, default=None,
+                    help="hypotheses per batch and GPU: 65536 (cfg2's stated batch; cfg4), 262144 for the cfg3 "
+                         "batch-SPRT line (BASELINE configs[2] states none: at 65536 its step is the SPRT kernels' "
+                         "latency, measured 0.94 vs 3.3 G hyp/s, profiles/r4c/f_sweep.txt)")
     ap.add_argument("--points", type=int, default=None, help="default: 10000 (cfg2/cfg3), 50000 (cfg4)")
     ap.add_argument("--threshold", type=float, default=None,
                     help="default: 2.0 px (cfg2/cfg3), 0.002 (cfg4, normalised coordinates)")
@@ -84,6 +87,8 @@ def parse():
         args.sprt = fund
     if args.sampler is None:
         args.sampler = "prosac" if fund else "uniform"
+    if args.batch is None:
+        args.batch = 262144 if fund and args.sprt else 65536
     return args
 
 

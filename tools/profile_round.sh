@@ -21,7 +21,7 @@ for w in $WORKLOADS; do
     h100k)      ARGS="--points 100000"; NPTS=100000 ;;
     e50k)       ARGS="--estimator essential"; NPTS=50000 ;;
     f10k)       ARGS="--estimator fundamental --no-sprt --sampler uniform"; NPTS=10000 ;;
-    f10k_sprt)  ARGS="--estimator fundamental"; NPTS=10000 ;;   # cfg3: PROSAC + batch SPRT (bench default)
+    f10k_sprt)  ARGS="--estimator fundamental"; NPTS=10000; BATCH=262144 ;;   # cfg3: PROSAC + batch SPRT (bench default, B = 262144)
     f10k_exact) ARGS="--sprt-exact"; NPTS=10000; BATCH=1024; STEPS="--steps 20 --warmup 2"; PSTEPS="--steps 5 --warmup 1"; GRIDS=all ;;
   esac
   D=$OUT/$w; mkdir -p $D
