@@ -2466,7 +2466,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         else uni->rollback();
     };
     std::vector<uint8_t> flags(prosac ? n : 0);
-    std::vector<int32_t> inl_list(prosac ? n : 0);
+    pinned_vector<int32_t> inl_list(prosac ? n : 0);
     usac::Score best;
     float best_model[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t iters = 0, max_iters = prm->max_iterations;
@@ -2479,7 +2479,9 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     HIP_TRY(c, c->pol_res.reserve(sizeof(float) * usac::kPolWords));
     if (!c->pol_pin && !(c->pol_pin = PinnedPool::get().take(sizeof(float) * usac::kPolWords, &c->pol_pin_bytes)))
         return fail(c, USAC_ERR_HIP, "pinned host allocation failed");
-    auto score_inliers = [&](const float *model_host) -> int {
+    // list_pin (nullable): the whole n-word inlier list copied in the same submission (its
+    // first cnt words are the list) -- one host wait instead of a second, synchronous copy
+    auto score_inliers = [&](const float *model_host, int32_t *list_pin = nullptr) -> int {
         float *dres = c->pol_res.as<float>();
         HIP_TRY(c, hipMemcpyAsync(c->one_model.p, model_host, sizeof(float) * 9, hipMemcpyHostToDevice, c->stream));
         HIP_TRY(c, c->inl_scratch.reserve(usac::inliers_scratch_bytes(c->n, 1)));
@@ -2488,6 +2490,9 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                                               reinterpret_cast<int32_t *>(dres + 12), dres + 13, c->inl_scratch.p));
         HIP_TRY(c, hipMemcpyAsync(static_cast<float *>(c->pol_pin) + 12, dres + 12, sizeof(float) * 2,
                                   hipMemcpyDeviceToHost, c->stream));
+        if (list_pin)
+            HIP_TRY(c, hipMemcpyAsync(list_pin, c->inl_idx.p, sizeof(int32_t) * (size_t)c->n, hipMemcpyDeviceToHost,
+                                      c->stream));
         HIP_TRY(c, stream_wait(c->stream));
         memcpy(&cnt, static_cast<const float *>(c->pol_pin) + 12, sizeof(int32_t));
         memcpy(&s, static_cast<const float *>(c->pol_pin) + 13, sizeof(float));
@@ -2735,10 +2740,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                 best = cur;
                 memcpy(best_model, model, sizeof(best_model));
                 if (prosac) {
-                    if ((rc = score_inliers(best_model))) return rc;
-                    if (cnt > 0)
-                        HIP_TRY(c, hipMemcpy(inl_list.data(), c->inl_idx.p, sizeof(int32_t) * (size_t)cnt,
-                                             hipMemcpyDeviceToHost));
+                    if ((rc = score_inliers(best_model, inl_list.data()))) return rc;
                     std::fill(flags.begin(), flags.end(), 0);
                     for (int32_t t = 0; t < cnt; t++) flags[inl_list[t]] = 1;
                     max_iters = pterm->getUpBoundIterations(iters, [&](uint32_t i) { return flags[i] != 0; },
