@@ -540,9 +540,26 @@ __global__ __launch_bounds__(256) void k_tv_combine(const uint32_t *__restrict__
     const uint32_t K = list ? *list_n : kmax;
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
     if (i >= K) return;
+    // the chunks in order, 16 chunks' loads in flight per 16 adds (one thread per model: at a
+    // few hundred waves for the whole batch, a load per add would wait a memory latency each)
     int c = part_cnt[i];
     float s = part_sum[i];
-    for (uint32_t j = 1; j < C; j++) {
+    uint32_t j = 1;
+    for (; j + 16 <= C; j += 16) {
+        int pc[16];
+        float psv[16];
+#pragma unroll
+        for (uint32_t u = 0; u < 16; u++) {
+            pc[u] = part_cnt[(size_t)(j + u) * kmax + i];
+            psv[u] = part_sum[(size_t)(j + u) * kmax + i];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 16; u++) {
+            c += pc[u];
+            s += psv[u];
+        }
+    }
+    for (; j < C; j++) {
         c += part_cnt[(size_t)j * kmax + i];
         s += part_sum[(size_t)j * kmax + i];
     }
