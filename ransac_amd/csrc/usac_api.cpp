@@ -2465,7 +2465,6 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         if (nap) nap->rollback();
         else uni->rollback();
     };
-    std::vector<uint8_t> flags(prosac ? n : 0);
     pinned_vector<int32_t> inl_list(prosac ? n : 0);
     usac::Score best;
     float best_model[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -2741,10 +2740,8 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                 memcpy(best_model, model, sizeof(best_model));
                 if (prosac) {
                     if ((rc = score_inliers(best_model, inl_list.data()))) return rc;
-                    std::fill(flags.begin(), flags.end(), 0);
-                    for (int32_t t = 0; t < cnt; t++) flags[inl_list[t]] = 1;
-                    max_iters = pterm->getUpBoundIterations(iters, [&](uint32_t i) { return flags[i] != 0; },
-                                                            largest_at[j]);
+                    // (the list is ascending: the compaction keeps point order)
+                    max_iters = pterm->getUpBoundIterationsSorted(iters, inl_list.data(), (uint32_t)cnt, largest_at[j]);
                 } else {
                     max_iters = term.getUpBoundIterations((uint32_t)best.inlier_number);
                 }
@@ -3040,7 +3037,6 @@ struct usac_termination {
     usac::StandardTerminationCriteria std_;
     std::unique_ptr<usac::ProsacTerminationCriteria> pro;
     usac_sampler *sampler = nullptr;
-    std::vector<uint8_t> flags;
     std::vector<int32_t> inl;
     usac_termination(usac_ctx *ctx, const usac_params *p)
         : c(ctx), thr(p->threshold), std_(p->desired_prob, ctx->m, ctx->n, p->max_iterations) {}
@@ -3224,7 +3220,6 @@ int usac_termination_create(usac_ctx *c, const usac_params *p, usac_sampler *pro
                                                          p->max_iterations));
         t->sampler = prosac;
         prosac->term = t.get();
-        t->flags.assign(c->n, 0);
         t->inl.resize(c->n);
     }
     *out = t.release();
@@ -3245,11 +3240,7 @@ int usac_prosac_termination(usac_termination *t, uint32_t hyp_count, const float
     uint32_t n = 0;
     int rc = usac_get_inliers(c, model, t->thr, t->inl.data(), &n, nullptr);
     if (rc) return rc;
-    std::fill(t->flags.begin(), t->flags.end(), 0);
-    for (uint32_t k = 0; k < n; k++) t->flags[t->inl[k]] = 1;
-    const std::vector<uint8_t> &f = t->flags;
-    *max_iters = t->pro->getUpBoundIterations(hyp_count, [&](uint32_t i) { return f[i] != 0; },
-                                              t->sampler->pro->largest());
+    *max_iters = t->pro->getUpBoundIterationsSorted(hyp_count, t->inl.data(), n, t->sampler->pro->largest());
     if (termination_length) *termination_length = t->pro->terminationLength();
     return USAC_OK;
 }

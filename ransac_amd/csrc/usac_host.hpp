@@ -154,6 +154,25 @@ class StandardTerminationCriteria {
         double r = (double)log_1_p_ / std::log((double)(1 - inl_prob));
         return (uint32_t)r;
     }
+    // A lower bound of the two-argument getUpBoundIterations without its log: the value itself
+    // (exact = true) below the 0.0005 floor, else floor(|log(1-p)| y / (1 - y) (1 - 2^-40)) with
+    // y = the same float 1 - w^m: -ln y <= (1 - y) / y, and the log (< 1 ulp) and the two
+    // roundings of r are far inside the 2^-40 slack.
+    uint32_t lowerBound(uint32_t inlier_size, uint32_t points_size, bool &exact) const {
+        float inl_ratio = (float)inlier_size / (float)points_size;
+        float inl_prob = inl_ratio * inl_ratio;
+        int k = (int)m_;
+        while (k > 2) {
+            inl_prob *= inl_ratio;
+            k--;
+        }
+        exact = inl_prob < 0.0005f;
+        if (exact) return max_;
+        const double y = (double)(1 - inl_prob), x = 1.0 - y;  // (x exact: y is a float in (0, 1))
+        if (!(x > 0.0)) return 0;                             // (no bound: p rounded to 0 in 1 - p)
+        const double lb = -(double)log_1_p_ * y / x * (1.0 - 9.094947017729282e-13);  // 2^-40
+        return lb >= 4294967295.0 ? 4294967295u : (uint32_t)lb;
+    }
 
    private:
     float log_1_p_;
@@ -275,6 +294,7 @@ class ProsacTerminationCriteria {
           growth_(growth),
           non_random_(table(points_size, sample_size)),
           maximality_(points_size, 10000),
+          pend_(points_size, 0),
           n_(points_size),
           term_len_(points_size) {}
 
@@ -328,10 +348,16 @@ class ProsacTerminationCriteria {
     uint32_t terminationLength() const { return term_len_; }
     // prosac_termination_criteria.hpp:148-201; inlier(i) = error of point i < threshold for
     // the new best model, largest = the sampler's largest_sample_size at that iteration
+    //
+    // The standard-termination value of a candidate (a log each, ~1 800 on a first scan at
+    // n = 10 k) is computed only where it can decide something now: a candidate whose value is
+    // provably above the running max_samples (StandardTerminationCriteria::lowerBound) cannot
+    // move term_len / max_samples, and its maximality update -- min(maximality_[i], value) -- is
+    // recorded as pending (the count) and applied when maximality_[i] is next read.  The results
+    // and the state are the reference's, value for value (tests/test_prosac_scan.py runs both).
     template <class Flags>
     uint32_t getUpBoundIterations(uint32_t hypCount, const Flags &inlier, uint32_t largest) {
-        constexpr uint32_t kMin = 20;
-        uint32_t max_samples = maximality_[term_len_ - 1];
+        uint32_t max_samples = maximality(term_len_ - 1);
         uint32_t count = 0;
         for (uint32_t i = 0; i < kMin; i++) count += inlier(i) ? 1 : 0;
         bool cur = inlier(kMin), nxt = false;
@@ -340,27 +366,86 @@ class ProsacTerminationCriteria {
             count += cur ? 1 : 0;
             if (non_random_[i] < count) {
                 non_random_[i] = count;
-                if (i == n_ - 1 || (cur && !nxt)) {
-                    uint32_t samples = std_.getUpBoundIterations(count, i + 1);
-                    if (i + 1 < largest) samples += hypCount - growth_[i];
-                    if (samples < maximality_[i]) {
-                        maximality_[i] = samples;
-                        if (samples < max_samples || (samples == max_samples && i + 1 >= term_len_)) {
-                            term_len_ = i + 1;
-                            max_samples = samples;
-                        }
-                    }
-                }
+                if (i == n_ - 1 || (cur && !nxt)) candidate(i, count, hypCount, largest, max_samples);
             }
             cur = nxt;
         }
         return max_samples;
     }
+    // The same scan from the new best's inlier indices in ascending order (idx[0 .. cnt)): the
+    // count is constant between consecutive inliers, so each stretch of outliers is one max()
+    // pass over non_random_, and the candidates -- the last inlier of a run, and point n - 1 --
+    // are visited in the same order as above.
+    uint32_t getUpBoundIterationsSorted(uint32_t hypCount, const int32_t *idx, uint32_t cnt, uint32_t largest) {
+        uint32_t max_samples = maximality(term_len_ - 1);
+        uint32_t k = 0;  // inliers below i
+        while (k < cnt && (uint32_t)idx[k] < kMin) k++;
+        uint32_t i = kMin;
+        while (i < n_) {
+            if (k < cnt && (uint32_t)idx[k] == i) {  // an inlier: count k + 1
+                const uint32_t count = k + 1;
+                const bool last = i == n_ - 1 || k + 1 == cnt || (uint32_t)idx[k + 1] != i + 1;
+                if (non_random_[i] < count) {
+                    non_random_[i] = count;
+                    if (last) candidate(i, count, hypCount, largest, max_samples);
+                }
+                k++;
+                i++;
+                continue;
+            }
+            // outliers i .. e - 1 at count k; of them only point n - 1 can be a candidate
+            const uint32_t e = k < cnt ? (uint32_t)idx[k] : n_;
+            const uint32_t e1 = e == n_ ? n_ - 1 : e;
+            uint32_t *nr = non_random_.data();
+            for (uint32_t j = i; j < e1; j++) nr[j] = nr[j] < k ? k : nr[j];
+            if (e == n_ && nr[n_ - 1] < k) {
+                nr[n_ - 1] = k;
+                candidate(n_ - 1, k, hypCount, largest, max_samples);
+            }
+            i = e;
+        }
+        return max_samples;
+    }
 
    private:
+    static constexpr uint32_t kMin = 20;
+    // candidate i (count inliers up to it) after its non-random update: its standard-termination
+    // value, maximality and the running minimum (prosac_termination_criteria.hpp:170-195)
+    void candidate(uint32_t i, uint32_t count, uint32_t hypCount, uint32_t largest, uint32_t &max_samples) {
+        uint32_t samples;
+        if (i + 1 < largest) {
+            samples = std_.getUpBoundIterations(count, i + 1) + (hypCount - growth_[i]);
+        } else {
+            bool exact;
+            const uint32_t lb = std_.lowerBound(count, i + 1, exact);
+            if (!exact && lb > max_samples) {
+                if (pend_[i]) maximality(i);  // an older pending update first
+                pend_[i] = count;
+                return;
+            }
+            samples = exact ? lb : std_.getUpBoundIterations(count, i + 1);
+        }
+        if (samples < maximality(i)) {
+            maximality_[i] = samples;
+            if (samples < max_samples || (samples == max_samples && i + 1 >= term_len_)) {
+                term_len_ = i + 1;
+                max_samples = samples;
+            }
+        }
+    }
+    // maximality_[i] with its pending update applied
+    uint32_t maximality(uint32_t i) {
+        if (pend_[i]) {
+            const uint32_t v = std_.getUpBoundIterations(pend_[i], i + 1);
+            if (v < maximality_[i]) maximality_[i] = v;
+            pend_[i] = 0;
+        }
+        return maximality_[i];
+    }
     StandardTerminationCriteria std_;
     std::vector<uint32_t> growth_;  // the sampler's growth function (a copy: samplers are rewound by value)
     std::vector<uint32_t> non_random_, maximality_;
+    std::vector<uint32_t> pend_;    // a pending maximality update's inlier count (0: none)
     uint32_t n_, term_len_;
 };
 
