@@ -382,6 +382,7 @@ class ProsacTerminationCriteria {
         while (k < cnt && (uint32_t)idx[k] < kMin) k++;
         uint32_t i = kMin;
         while (i < n_) {
+            while (k < cnt && (uint32_t)idx[k] < i) k++;  // (only a list out of order: always progress)
             if (k < cnt && (uint32_t)idx[k] == i) {  // an inlier: count k + 1
                 const uint32_t count = k + 1;
                 const bool last = i == n_ - 1 || k + 1 == cnt || (uint32_t)idx[k + 1] != i + 1;
