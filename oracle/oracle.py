@@ -306,6 +306,43 @@ def mblock_ref_eval(N, z):
     return M.reshape(10, 10)
 
 
+RPOLY_REF_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_ref", "librpoly_ref.so")
+
+
+def rpoly_ref_available():
+    return os.path.exists(RPOLY_REF_PATH)
+
+
+def rpoly_ref_zeros(coeffs):
+    """The reference's own rpoly_ak1 (usac/estimator/essential/rpoly.cpp:7-230, compiled where it
+    lies into oracle/_ref by oracle/Makefile) on sum coeffs[i] z^i -> (real parts, imaginary
+    parts) of the zeros it reports, in the order it found them (its degree shrinks when it fails
+    after 20 shifts, rpoly.cpp:214-218)."""
+    L = ctypes.CDLL(RPOLY_REF_PATH)
+    _d = ctypes.POINTER(ctypes.c_double)
+    L.rpoly_ref_zeros.restype = ctypes.c_int
+    L.rpoly_ref_zeros.argtypes = [_d, ctypes.c_int, _d, _d]
+    a = np.ascontiguousarray(coeffs, dtype=np.float64)
+    zr = np.zeros(100)
+    zi = np.zeros(100)
+    k = L.rpoly_ref_zeros(a.ctypes.data_as(_d), len(a) - 1, zr.ctypes.data_as(_d), zi.ctypes.data_as(_d))
+    k = max(k, 0)
+    return zr[:k].copy(), zi[:k].copy()
+
+
+def e5_poly(est, sample):
+    """The degree-10 polynomial det M(z) of a 5-point sample, ascending powers: the input of the
+    root step (usac_oracle.c e5_poly; five_points.cpp:113-148 interpolates the same polynomial)."""
+    L = lib()
+    _d = ctypes.POINTER(ctypes.c_double)
+    L.orc_e5_poly.restype = None
+    L.orc_e5_poly.argtypes = [ctypes.c_void_p, _i32p, _d]
+    s = np.ascontiguousarray(sample, dtype=np.int32)
+    a = np.zeros(11)
+    L.orc_e5_poly(est._h, _p(s, _i32p), a.ctypes.data_as(_d))
+    return a
+
+
 def real_roots(coeffs):
     """real roots (ascending) of sum coeffs[i] z^i (the 5-pt solver's root finder)"""
     a = np.ascontiguousarray(coeffs, dtype=np.float64)

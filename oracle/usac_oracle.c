@@ -1605,6 +1605,37 @@ static void projections(const double E[9], double P[4][3][4]) {
     }
 }
 
+/* steps 1-3: the null basis N of the five rows W (destroyed) and the degree-10 coefficients a
+ * (ascending powers) of det M(z), interpolated at z = -5..5 (five_points.cpp:65-136) */
+static void e5_poly(double W[9][9], double N[4][9], double a[11]) {
+    double W0[5][9];
+    memcpy(W0, W, sizeof(W0));
+    if (!qr_null(W, 5, N)) {
+        row_jacobi(W0, 5);
+        null_complement(W0, 5, 4, N);
+    }
+    double Mz[10][10], dets[11], z[11];
+    for (int k = 0; k < 11; k++) {
+        z[k] = (double)(k - 5);
+        e5_matrix((const double(*)[9])N, z[k], Mz);
+        dets[k] = det10(Mz);
+    }
+    /* Newton divided differences, then monomial coefficients */
+    double c[11];
+    for (int k = 0; k < 11; k++) c[k] = dets[k];
+    for (int j = 1; j < 11; j++)
+        for (int i = 10; i >= j; i--) c[i] = (c[i] - c[i - 1]) / (z[i] - z[i - j]);
+    for (int i = 0; i < 11; i++) a[i] = 0.0;
+    a[0] = c[10];
+    int deg = 0;
+    for (int k = 9; k >= 0; k--) {
+        a[deg + 1] = 0.0;
+        for (int i = deg + 1; i >= 1; i--) a[i] = a[i - 1] - z[k] * a[i];
+        a[0] = c[k] - z[k] * a[0];
+        deg++;
+    }
+}
+
 /* returns 1 and writes E (9 floats) when a root passes the cheirality test; with
  * cand != NULL every root's E (10 x 9) and cheirality flag are reported (test hook) */
 static int essential_5pt_all(const orc_est *e, const int *sample, float *Eout, float *cand, int *cand_ok,
@@ -1621,32 +1652,8 @@ static int essential_5pt_all(const orc_est *e, const int *sample, float *Eout, f
         const double row[9] = {x1 * x2, x2 * y1, x2, x1 * y2, y1 * y2, y2, x1, y1, 1.0};
         for (int k = 0; k < 9; k++) W[i][k] = row[k];
     }
-    double N[4][9], W0[5][9];
-    memcpy(W0, W, sizeof(W0));
-    if (!qr_null(W, 5, N)) {
-        row_jacobi(W0, 5);
-        null_complement(W0, 5, 4, N);
-    }
-    double Mz[10][10], dets[11], z[11];
-    for (int k = 0; k < 11; k++) {
-        z[k] = (double)(k - 5);
-        e5_matrix((const double(*)[9])N, z[k], Mz);
-        dets[k] = det10(Mz);
-    }
-    /* Newton divided differences, then monomial coefficients */
-    double c[11], a[11];
-    for (int k = 0; k < 11; k++) c[k] = dets[k];
-    for (int j = 1; j < 11; j++)
-        for (int i = 10; i >= j; i--) c[i] = (c[i] - c[i - 1]) / (z[i] - z[i - j]);
-    for (int i = 0; i < 11; i++) a[i] = 0.0;
-    a[0] = c[10];
-    int deg = 0;
-    for (int k = 9; k >= 0; k--) {
-        a[deg + 1] = 0.0;
-        for (int i = deg + 1; i >= 1; i--) a[i] = a[i - 1] - z[k] * a[i];
-        a[0] = c[k] - z[k] * a[0];
-        deg++;
-    }
+    double N[4][9], a[11], Mz[10][10];
+    e5_poly(W, N, a);
     double roots[10];
     const int nr = real_roots(a, 10, roots);
     static const double Pref[3][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}};
@@ -1718,6 +1725,20 @@ static inline float essential_error(const orc_est *e, unsigned int pidx) {
 
 /* test hook: real roots of a polynomial (ascending) by the 5-pt solver's spec */
 int orc_real_roots(const double *a, int n, double *roots) { return real_roots(a, n, roots); }
+
+/* test hook: the degree-10 polynomial det M(z) of an essential sample (ascending powers), the
+ * input of the root step -- pinned against the reference's rpoly_ak1 (oracle/rpoly_ref.cpp) */
+void orc_e5_poly(orc_est *e, const int *sample, double *a) {
+    double W[9][9];
+    for (int i = 0; i < 5; i++) {
+        const float *p = e->pts + 4 * (size_t)sample[i];
+        const double x1 = p[0], y1 = p[1], x2 = p[2], y2 = p[3];
+        const double row[9] = {x1 * x2, x2 * y1, x2, x1 * y2, y1 * y2, y2, x1, y1, 1.0};
+        for (int k = 0; k < 9; k++) W[i][k] = row[k];
+    }
+    double N[4][9];
+    e5_poly(W, N, a);
+}
 
 int orc_est_estimate(orc_est *e, const int *sample, float *models) {
     if (e->kind == ORC_LINE2D) return line2d_estimate(e, sample, models);

@@ -1,9 +1,12 @@
 """CPU oracle, essential path, no GPU.
 
 The reference's 5-point solver goes through OpenCV SVD/determinant/inv and the rpoly
-Jenkins-Traub root finder (five_points.cpp:13-274) -- not reproducible here, so parity with
-the reference is end-to-end and the oracle's own restatement is pinned by
-identities: its root finder matches numpy on degree-10 polynomials, on exact two-view data
+Jenkins-Traub root finder (five_points.cpp:13-274).  Two of its steps are pinned against the
+reference's own code compiled where it lies (oracle/_ref): the polynomial matrix M(z)
+(mblock.hpp) and the root step (rpoly.cpp's rpoly_ak1, on the oracle's own polynomials).  The
+OpenCV steps (null basis, determinant interpolation, triangulation SVD) are not reproducible
+here, and the oracle's restatement of them is pinned by identities: its root finder matches
+numpy on degree-10 polynomials, on exact two-view data
 the generating E is among the solver's candidates and passes its cheirality test, the
 returned E satisfies the essential-matrix constraints, and the residual equals the textbook
 point-to-epipolar-line distance.
@@ -122,3 +125,76 @@ def test_e5_matrix_pinned_against_reference_mblock(oracle):
             assert (scale > 0).all()
             worst = max(worst, float((np.abs(a - b) / scale).max()))
     assert worst <= 1e-12, worst
+
+
+def _residual(a, x):
+    """|p(x)| / sum |a_i| |x|^i evaluated exactly (rationals): the backward error of a root."""
+    from fractions import Fraction
+
+    X, v, s = Fraction(float(x)), Fraction(0), Fraction(0)
+    for i, c in enumerate(a):
+        t = Fraction(float(c)) * X ** i
+        v += t
+        s += abs(t)
+    return float(abs(v) / s) if s else 0.0
+
+
+def test_e5_roots_pinned_against_reference_rpoly(oracle):
+    """the root step of the 5-point solver against the reference's own
+    rpoly_ak1 (usac/estimator/essential/rpoly.cpp:7-230, built by oracle/Makefile where it lies
+    with only the standard headers its precomp.hpp would include).  On the oracle's degree-10
+    polynomials of 10 000 cfg4 samples, the real zeros rpoly reports (zeroi == 0, the filter of
+    five_points.cpp:152-156) equal the oracle's real_roots:
+      * counts equal on >= 99.9 % of the samples; every difference is rpoly giving up after 20
+        shifts (rpoly.cpp:214-218, its degree comes back short) or a near-multiple cluster where a
+        complex pair sits within 1e-3 of the real axis (rpoly's deflation turns it into two "real"
+        zeros, or the other way round);
+      * values within rel 1e-9 on >= 99.8 % of the equal-count samples; where they differ by more,
+        the oracle's root has the smaller exact backward error (<= 1e-15: rounding level) -- rpoly's
+        deflated zeros carry the larger error.
+    The ORDER differs: rpoly returns zeros in the order it deflates them and five_points.cpp:239-273
+    keeps the first that passes cheirality, while this build's spec scans real roots ascending.  The
+    test measures how often that picks a different candidate (reported)."""
+    if not oracle.rpoly_ref_available():
+        pytest.skip("oracle/_ref/librpoly_ref.so not built (the reference is absent)")
+    pts, _, _ = synthetic.fundamental_points(n=50000, inlier_ratio=0.3, seed=1, normalized=True)
+    est = oracle.Estimator(oracle.ESSENTIAL, pts)
+    samples = oracle.uniform_samples(11, len(pts), 5, 10000)
+    n_cnt_diff, n_val, n_val_diff, n_sel, n_sel_diff, failures = 0, 0, 0, 0, 0, 0
+    for s in samples:
+        a = oracle.e5_poly(est, s)
+        ours = oracle.real_roots(a)
+        zr, zi = oracle.rpoly_ref_zeros(a)
+        if len(zr) < 10:
+            failures += 1
+        real = zr[zi == 0]
+        ref = np.sort(real)
+        if len(ref) != len(ours):
+            n_cnt_diff += 1
+            if len(zr) == 10:  # a cluster: numpy's companion roots show a pair within 1e-3 of the axis
+                cr = np.roots(a[::-1])
+                near = cr[(np.abs(cr.imag) > 0) & (np.abs(cr.imag) < 1e-3 * np.maximum(1.0, np.abs(cr.real)))]
+                odd = np.setxor1d(np.round(ref, 3), np.round(ours, 3))
+                assert len(near) or len(odd) == 0, (s, ours, ref)
+            continue
+        if not len(ref):
+            continue
+        n_val += 1
+        rel = np.abs(ref - ours) / np.abs(ours)
+        if rel.max() > 1e-9:
+            n_val_diff += 1
+            k = int(np.argmax(rel))
+            ro, rr = _residual(a, ours[k]), _residual(a, ref[k])
+            assert ro <= 1e-15 and ro <= rr, (s, ours[k], ref[k], ro, rr)
+        # the selection: first cheirality-passing candidate, ascending (this spec) vs rpoly's order
+        cand, ok = est.e5_candidates(s)
+        if len(cand) == len(ours) and ok.any():
+            n_sel += 1
+            pos = [int(np.argmin(np.abs(real - r))) for r in ours]
+            first_rp = min((k for k in range(len(ours)) if ok[k]), key=lambda k: pos[k])
+            n_sel_diff += first_rp != int(np.argmax(ok))
+    print("rpoly pin: count differences %d / %d (rpoly failures %d); values > 1e-9: %d / %d; selection differs "
+          "on %d of %d samples with a passing candidate" % (n_cnt_diff, len(samples), failures, n_val_diff, n_val,
+                                                            n_sel_diff, n_sel))
+    assert n_cnt_diff <= 10 and n_val_diff <= 0.002 * n_val
+    assert n_sel > 3000
