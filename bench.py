@@ -174,7 +174,7 @@ def parity_check(usac, kind, pts, thr, dlt_mode, samples=None):
             "scores_bit_equal": bool((s.view(np.int32) == osum.view(np.int32)).all())}
 
 
-def timed_kernel_parity(usac, ctx, kind, pts, thr, dlt_mode, seed, sprt, first_hyp=0):
+def timed_kernel_parity(usac, ctx, kind, pts, thr, dlt_mode, seed, sprt, first_hyp=0, xctx=None):
     """The timed configuration itself (device sampler, multi-chunk fast score kernel, batch SPRT
     when on) on one 256-sample batch against the CPU oracle on the same device-drawn samples:
     counts exact (SPRT: every accepted model's count), Σ within the throughput kernel's declared
@@ -190,6 +190,10 @@ def timed_kernel_parity(usac, ctx, kind, pts, thr, dlt_mode, seed, sprt, first_h
     B = 256
     smp = ctx.draw_samples(B, seed, first_hyp)
     ctx.hypothesize_async(B, seed, first_hyp, thr)
+    exchanged = None
+    if xctx is not None:  # N > 1: this batch's record through the line's own RCCL exchange as well
+        xctx.exchange_best_async(ctx, 0)
+        exchanged = xctx.exchange_best_wait(0)
     rec = ctx.fetch_best()
     spk = 3 if fund else 1
     c, s = ctx.last_counts(B * spk)
@@ -218,17 +222,84 @@ def timed_kernel_parity(usac, ctx, kind, pts, thr, dlt_mode, seed, sprt, first_h
     out = {"hypotheses": B, "models": int(occ.sum()), "counts_equal": counts_ok,
            "sums_within_bound": bool((err <= bound).all()),
            "sum_max_err_over_bound": float((err / np.maximum(bound, 1e-30)).max()) if err.size else 0.0}
-    if sprt:
+    if sprt:  # an accepted model scores (float)count: the record is the most inliers, earliest slot
         out["sprt_accepted"] = int((c >= 0).sum())
+        best = oracle_best(np.where(c >= 0, oc, -1), np.where(c >= 0, oc, 0).astype(np.float32), c >= 0)
     else:  # the record: Score::bigger over the oracle's exact (count, Σ), earliest slot on ties
-        best = None
-        for sl in np.flatnonzero(occ):
-            if best is None or oc[sl] > oc[best] or (oc[sl] == oc[best] and osum[sl] > osum[best]):
-                best = sl
+        best = oracle_best(oc, osum, occ)
+    if best is not None or not sprt:
         out["best_record_equal"] = bool(best is not None and int(rec.inliers) == int(oc[best]) and
                                         int(rec.hyp_index) == first_hyp + int(best) // spk)
+    out["expected_record"] = None if best is None else {"inliers": int(oc[best]),
+                                                         "hyp_index": first_hyp + int(best) // spk}
+    out["record"] = {"inliers": int(rec.inliers), "hyp_index": int(rec.hyp_index)}
+    if exchanged is not None:  # the exchange returned this rank's own record in its slot
+        out["exchanged"] = [{"inliers": int(r.inliers), "hyp_index": int(r.hyp_index)} for r in exchanged]
     out["ok"] = bool(counts_ok and out["sums_within_bound"] and out.get("best_record_equal", True))
     return out
+
+
+def oracle_best(counts, sums, occupied):
+    """Score::bigger (quality.hpp:22-31) over the occupied slots, earliest slot on exact ties
+    (the batch argmax and usac_merge_records); None when no slot is occupied."""
+    idx = np.flatnonzero(occupied)
+    if not idx.size:
+        return None
+    c, sm = counts[idx].astype(np.int64), sums[idx].astype(np.float32)
+    top = c == c.max()
+    s_top = sm[top]
+    return int(idx[top][int(np.flatnonzero(s_top == s_top.max())[0])])
+
+
+def oracle_batch(kind, pts, thr, dlt_mode, samples):
+    """The CPU oracle's models of `samples` (B x m) scored over all points: per slot (counts, Σ,
+    occupied), spk slots per sample (3 for the 7-point solver's roots, else 1; counts -1 and Σ 0 on
+    empty slots) -- the reference's per-hypothesis work, sample order."""
+    from oracle import oracle as O
+
+    fund, ess = kind == "fundamental", kind == "essential"
+    est = O.Estimator(O.FUNDAMENTAL if fund else O.ESSENTIAL if ess else O.HOMOGRAPHY, pts, dlt_mode)
+    om, onm = est.estimate_batch(samples)
+    if fund:
+        oc, osum = est.score_models(om.reshape(-1, 9), thr)
+        occ = (np.arange(3)[None, :] < onm[:, None]).reshape(-1)
+    else:
+        oc, osum = est.score_models(om, thr)
+        occ = onm == 1 if ess else np.ones(len(samples), bool)
+    return np.where(occ, oc, -1), np.where(occ, osum, 0).astype(np.float32), occ
+
+
+def oracle_batch_mt(kind, pts, thr, dlt_mode, samples, threads):
+    """oracle_batch over row blocks on `threads` host threads (one oracle estimator each; ctypes
+    releases the GIL), concatenated in sample order."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    parts = np.array_split(np.arange(len(samples)), max(1, min(threads, len(samples))))
+    with ThreadPoolExecutor(len(parts)) as ex:
+        res = list(ex.map(lambda ix: oracle_batch(kind, pts, thr, dlt_mode, samples[ix]), parts))
+    return tuple(np.concatenate([r[k] for r in res]) for k in range(3))
+
+
+def first_batch_parity(usac, ctx, kind, pts, thr, dlt_mode, seed, B, step, world, rec, threads):
+    """The first timed batch's merged record (every rank's B hypotheses, all-gathered and merged)
+    against the reference's best update over the union of all ranks' samples (ransac.cpp:103-132:
+    Score::bigger, the earliest hypothesis on exact ties).  Every rank's slice is keyed by (seed,
+    global index), so rank 0 redraws all of them with its own device sampler and the CPU oracle
+    scores them all (host threads)."""
+    t0 = time.perf_counter()
+    spk = 3 if kind == "fundamental" else 1
+    firsts = [(step * world + r) * B for r in range(world)]
+    smp = np.concatenate([ctx.draw_samples(B, seed, f) for f in firsts])
+    oc, osum, occ = oracle_batch_mt(kind, pts, thr, dlt_mode, smp, threads)
+    best = oracle_best(oc, osum, occ)
+    exp_hyp = None if best is None else firsts[best // spk // B] + (best // spk) % B
+    return {"hypotheses": int(len(smp)), "ranks": world, "models": int(occ.sum()),
+            "record": {"inliers": int(rec.inliers), "hyp_index": int(rec.hyp_index)},
+            "oracle_best": None if best is None else {"inliers": int(oc[best]), "hyp_index": int(exp_hyp)},
+            "ok": bool(best is not None and int(rec.inliers) == int(oc[best]) and int(rec.hyp_index) == exp_hyp),
+            "oracle_s": time.perf_counter() - t0,
+            "note": "the merged record of the first timed batch vs Score::bigger over the oracle's exact (count, "
+                    "Σ) of all %d ranks' samples, redrawn by rank 0 from (seed, global index)" % world}
 
 
 def _profile_entry(kernel_prefix, n_points, batch):
@@ -400,12 +471,13 @@ def cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank):
         return mdl
 
     sharded = world > 1 and not args.cfg5_replicas
-    comm_ctx = None
+    comm_ctx, rccl = None, None
     if sharded:  # the RCCL communicator lives on one context; each run's context borrows it via the bench
         comm_ctx = usac.Context(usac.ESTIMATOR.Homography, pts, device=local_rank)
         uid = [usac.Context.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         exchange = init_exchange(comm_ctx, usac, dist, torch, world, rank, uid[0])
+        rccl = rccl_report(comm_ctx, exchange, dist, world, rank)
 
     def gloo_gather(b):
         t = torch.frombuffer(bytearray(b), dtype=torch.uint8)
@@ -488,7 +560,7 @@ def cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank):
                    "n_points": n, "threshold": args.threshold, "max_iterations": max_iters,
                    "hypotheses_per_gpu": iters / world,
                    "parallelism": ("hypothesis-sharded runs x%d (%s)" % (world, exchange)) if sharded else
-                                  "replicas x%d" % world},
+                                  "replicas x%d" % world, "rccl": rccl},
         "roofline": roof,
         "parity": parity,
         "run_stats": {k: int(out.raw[k]) for k in ("batches", "n_records", "lo_rounds", "lo_stages", "sum_models",
@@ -665,6 +737,52 @@ def init_exchange(ctx, usac, dist, torch, world, rank, uid):
     sys.exit(3)
 
 
+def rccl_report(ctx, exchange, dist, world, rank):
+    """The rank count RCCL itself reports for the line's communicator (ncclCommCount /
+    ncclCommUserRank / ncclCommCuDevice through usac_comm_count), gathered from every rank; a line
+    whose communicator does not hold N ranks, or whose ranks do not sit on N distinct devices, is
+    refused (exit 4).  None without an RCCL exchange (N = 1, or the one-GPU gloo rehearsal)."""
+    if exchange != "rccl_allgather":
+        return None
+    n, r, dev = ctx.comm_count()
+    allv = [None] * world
+    dist.all_gather_object(allv, (n, r, dev))
+    bad = [v for k, v in enumerate(allv) if v[0] != world or v[1] != k]
+    if bad or len({v[2] for v in allv}) != world:
+        if rank == 0:
+            print("bench: RCCL reports %r for %d ranks; refusing to report the line" % (allv, world), file=sys.stderr)
+        sys.exit(4)
+    return {"ranks": n, "devices": [v[2] for v in allv], "source": "ncclCommCount / ncclCommUserRank / "
+                                                                     "ncclCommCuDevice"}
+
+
+def ranks_parity(usac, tk_all, exchange):
+    """N > 1: every rank's 256-sample timed-configuration check (counts exact, Σ within bound,
+    local record = the oracle's best), the merge of the ranks' records (usac_merge_records) equal
+    to Score::bigger over the ranks' oracle-expected records (ransac.cpp:103-132; earliest
+    hypothesis on ties), and -- with RCCL -- the exchange's all-gathered list equal to the records
+    the ranks hold."""
+    recs = [t["record"] for t in tk_all]
+    exp = [t["expected_record"] for t in tk_all]
+    merged = usac.merge_records([usac.Record(hyp_index=r["hyp_index"], inliers=r["inliers"],
+                                             score=float(r["inliers"]), valid=1) for r in recs]) \
+        if all(t.get("sprt_accepted") is not None for t in tk_all) else None
+    # the expected merge: the most inliers, then the earliest hypothesis (the slices are disjoint and
+    # ascending in rank order; with equal counts across ranks the exact Σ decides, which only the
+    # SPRT lines -- score = count -- leave to the index)
+    cand = [e for e in exp if e is not None]
+    out = {"per_rank_ok": [bool(t["ok"]) for t in tk_all], "records": recs}
+    if cand and merged is not None:
+        top = max(e["inliers"] for e in cand)
+        want = min((e for e in cand if e["inliers"] == top), key=lambda e: e["hyp_index"])
+        out["expected_merge"] = want
+        out["merge_equal"] = int(merged.inliers) == want["inliers"] and int(merged.hyp_index) == want["hyp_index"]
+    if exchange == "rccl_allgather":
+        out["exchange_equal"] = all(t.get("exchanged") == recs for t in tk_all)
+    out["ok"] = bool(all(out["per_rank_ok"]) and out.get("merge_equal", True) and out.get("exchange_equal", True))
+    return out
+
+
 def launch_plan(gpus, env):
     """How `bench.py --gpus N` runs, decided before anything touches the GPU:
     ("self", 1) -- one process, one GPU (no WORLD_SIZE, N = 1);
@@ -805,6 +923,7 @@ def main():
         uid = [usac.Context.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         exchange = init_exchange(ctx, usac, dist, torch, world, rank, uid[0])
+    rccl = rccl_report(ctx, exchange, dist, world, rank)
 
     def allgather(rec):
         if exchange == "rccl_allgather":
@@ -881,11 +1000,14 @@ def main():
     sync()
     score_ms, solve_ms, batch_ms = [], [], []
     best_box = [None]
+    first_box = []  # the first timed batch's merged record (checked against the oracle afterwards)
 
     def keep(rec, t):
         score_ms.append(t["score_ms"])
         solve_ms.append(t["solve_ms"])
         batch_ms.append(t["batch_ms"])
+        if not first_box:
+            first_box.append(rec)
         b = best_box[0]
         if b is None or usac.merge_records([rec, b]).hyp_index == rec.hyp_index:
             best_box[0] = rec
@@ -911,6 +1033,16 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+    # parity of the timed configuration on every rank (N > 1: each rank's own 256-sample slice, its
+    # record also through the line's exchange), gathered to rank 0
+    tk_all = None
+    if world > 1:
+        tk_first = (args.warmup + args.steps + 100) * world * B + rank * 256  # beyond every timed index
+        own = timed_kernel_parity(usac, ctx, args.estimator, pts, args.threshold, dlt_mode, args.seed,
+                                  bool(args.sprt), first_hyp=tk_first,
+                                  xctx=ctx if exchange == "rccl_allgather" else None)
+        tk_all = [None] * world
+        dist.all_gather_object(tk_all, own)
 
     if rank == 0:
         total = world * args.steps * B
@@ -1001,15 +1133,28 @@ def main():
             "roofline": roof,
             "best": {"inliers": int(best.inliers), "hyp_index": int(best.hyp_index)},
         }
+        out["config"]["rccl"] = rccl
+        par = parity_check(usac, args.estimator, pts, args.threshold, dlt_mode,
+                           samples=ctx.draw_samples(256, args.seed) if napsac else None)
         if world == 1:
-            out["parity"] = parity_check(usac, args.estimator, pts, args.threshold, dlt_mode,
-                                         samples=ctx.draw_samples(256, args.seed) if napsac else None)
-            out["parity"]["timed_kernel"] = timed_kernel_parity(usac, ctx, args.estimator, pts, args.threshold,
-                                                                dlt_mode, args.seed, bool(args.sprt))
-            if args.cpu_seconds > 0:
-                out["cpu_baseline"] = cpu_baseline(args.estimator, pts, args.threshold, dlt_mode, args.cpu_seconds)
-                out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+            par["timed_kernel"] = timed_kernel_parity(usac, ctx, args.estimator, pts, args.threshold, dlt_mode,
+                                                      args.seed, bool(args.sprt))
+        else:
+            par["timed_kernel"] = tk_all[0]
+            par["ranks"] = ranks_parity(usac, tk_all, exchange)
+        if not args.sprt:  # batch SPRT decisions depend on each rank's batch state: ranks_parity covers them
+            par["first_timed_batch"] = first_batch_parity(usac, ctx, args.estimator, pts, args.threshold, dlt_mode,
+                                                          args.seed, B, args.warmup, world, first_box[0],
+                                                          cpu_info()[2])
+        par["ok"] = bool(par["inlier_counts_equal"] and par["scores_bit_equal"] and par["timed_kernel"]["ok"] and
+                         par.get("ranks", {}).get("ok", True) and par.get("first_timed_batch", {}).get("ok", True))
+        out["parity"] = par
+        if args.cpu_seconds > 0:
+            out["cpu_baseline"] = cpu_baseline(args.estimator, pts, args.threshold, dlt_mode, args.cpu_seconds)
+            out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
         print(json.dumps(out), flush=True)
+    if world > 1:  # the other ranks wait for rank 0's checks and CPU baseline before tearing down
+        dist.barrier()
     for c in ctxs:
         c.close()
     if world > 1:

@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define USAC_ABI_VERSION 11
+#define USAC_ABI_VERSION 12
 
 /* = enum ESTIMATOR (usac/model.hpp:10) */
 enum { USAC_LINE2D = 1, USAC_HOMOGRAPHY = 2, USAC_FUNDAMENTAL = 3, USAC_ESSENTIAL = 4 };
@@ -116,6 +116,9 @@ typedef struct usac_params {
     uint32_t knn;                     /* model.hpp:23 k_nearest_neighbors (NAPSAC KNN / GC, 1..32) */
     float spatial_coherence_gc;       /* model.hpp:33 (0.1): GC pairwise weight, used as given
                                          (graphcut.hpp:43; 0 = no pairwise term) */
+    uint32_t max_hypothesis_test_before_sprt; /* model.hpp:40 (20; ABI 12): a rejected model still counts
+                                         as an iteration from this iteration on (ransac.cpp:81-83), and the
+                                         SPRT's adaptive history starts then (sprt.hpp:243); 0 = 20 */
 } usac_params;
 
 /* RansacOutput getters (ransac_output.hpp:57-97) */
@@ -234,8 +237,9 @@ int usac_set_sprt(usac_ctx *ctx, int enable, uint32_t seed, double epsilon, doub
 int usac_sprt_tested(usac_ctx *ctx, uint64_t *points_tested);
 /* The batch test's constants -- eps_delta_A[3] = epsilon, delta, A (nullable) -- and the first pool
  * position each model slot of the last batch was tested from (starts, n slots, nullable; slots of
- * the fundamental solver 3 per sample).  Every decision equals the reference's fp64 product walk
- * (sprt.hpp:209-234) with these constants from that position.  For tests. */
+ * the fundamental solver 3 per sample; n <= the last batch's slots; a slot the solver left empty
+ * reads UINT32_MAX).  Every decision equals the reference's fp64 product walk (sprt.hpp:209-234)
+ * with these constants from that position.  For tests. */
 int usac_batch_sprt_info(usac_ctx *ctx, double *eps_delta_A, uint32_t *starts, uint32_t n);
 /* Sampler of the throughput batches' device stream (usac_hypothesize_score with samples ==
  * NULL, usac_hypothesize_async): USAC_SAMPLER_UNIFORM (default), USAC_SAMPLER_NAPSAC (grid
@@ -374,13 +378,13 @@ void usac_termination_destroy(usac_termination *t);
 
 /* SPRT ctor (sprt.hpp:89-175): the random pool from n draws of rng (the Ransac ctor creates it after
  * the sampler, before the sampler's first draw), the reference's initial epsilon / delta / t_M / m_S
- * for ctx's estimator; params->threshold, ->max_iterations. */
+ * for ctx's estimator; params->threshold, ->max_iterations, ->max_hypothesis_test_before_sprt. */
 int usac_sprt_create(usac_ctx *ctx, const usac_params *params, usac_random *rng, usac_sprt **out);
 /* verifyModelAndGetModelScore(model, current_hypothese, maximum_score, score), one model (9 floats;
  * line: 3): the model's inlier flags in pool order from the device, the reference's fp64 lambda walk
  * over the rolling pool index on the host.  *good = the decision; *count / *score written as the
  * reference writes them (accepted: inliers, (float)inliers; rejected while current_hypothese <
- * max_hypothesis_test_before_sprt = 20: the full count; otherwise left untouched). */
+ * params->max_hypothesis_test_before_sprt (default 20): the full count; otherwise left untouched). */
 int usac_sprt_verify(usac_sprt *s, const float *model, int32_t current_hypothese, uint32_t maximum_score,
                      int32_t *good, int32_t *count, float *score);
 /* getUpperBoundIterations(inlier_size) (sprt.hpp:371-393) */
@@ -405,7 +409,8 @@ typedef struct usac_sprt_state {
 } usac_sprt_state;
 /* models: B x slots x 9 floats and n_models[B] (usac_estimate_models' layout; slots = 3 for the
  * 7-point solver, else 1).  From the cursor, in loop order: verify(model, iters, best_inliers); a
- * rejected model at iters >= 20 counts an iteration and is skipped (Q9); every other model is
+ * rejected model at iters >= max_hypothesis_test_before_sprt (the handle's params, default 20) counts an
+ * iteration and is skipped (Q9); every other model is
  * compared with the best; after each sample iters++; before each sample `iters < max_iters` is
  * checked.  Returns with found = 1 at the first model bigger than the best (the cursor then points
  * past it), or found = 0 when the batch is exhausted (sample == B) or the loop bound is reached
@@ -430,6 +435,9 @@ void usac_lo_destroy(usac_lo *lo);
 /* 128-byte RCCL unique id (rank 0 creates, everyone receives it out of band). */
 int usac_comm_unique_id(uint8_t *id128);
 int usac_comm_init(usac_ctx *ctx, int nranks, int rank, const uint8_t *id128);
+/* What RCCL itself reports for ctx's communicator (ABI 12): ncclCommCount / ncclCommUserRank /
+ * ncclCommCuDevice -- a multi-GPU bench line states the rank count RCCL saw, not the one asked for. */
+int usac_comm_count(usac_ctx *ctx, int *nranks, int *rank, int *device);
 /* All-gather of one usac_record per rank on the context stream: all[nranks]. */
 int usac_allgather_records(usac_ctx *ctx, const usac_record *local, usac_record *all);
 /* The per-batch best exchange of the throughput pipeline, off the compute streams: the record

@@ -144,6 +144,7 @@ public:
         p.neighbors = (int32_t)neighborsType;
         p.knn = k_nearest_neighbors;
         p.spatial_coherence_gc = spatial_coherence_gc;
+        p.max_hypothesis_test_before_sprt = max_hypothesis_test_before_sprt;
         return p;
     }
 

@@ -81,7 +81,7 @@ class _Params(ctypes.Structure):
                 ("lo_sample_size", ctypes.c_uint32), ("lo_iterative_iterations", ctypes.c_uint32),
                 ("lo_inner_iterations", ctypes.c_uint32), ("lo_threshold_multiplier", ctypes.c_uint32),
                 ("cell_size", ctypes.c_int32), ("neighbors", ctypes.c_int32), ("knn", ctypes.c_uint32),
-                ("spatial_coherence_gc", ctypes.c_float)]
+                ("spatial_coherence_gc", ctypes.c_float), ("max_hypothesis_test_before_sprt", ctypes.c_uint32)]
 
 
 class SprtState(ctypes.Structure):
@@ -113,7 +113,7 @@ ABI_SYMBOLS = [
     "usac_set_score_chunks", "usac_set_score_variant", "usac_last_counts", "usac_std_termination", "usac_ransac_run", "usac_ransac_run_sharded", "usac_uniform_samples",
     "usac_prosac_samples", "usac_sprt_pool", "usac_set_sprt", "usac_sprt_tested", "usac_set_device_sampler",
     "usac_draw_samples", "usac_set_cell_size", "usac_grid_neighbors",
-    "usac_comm_unique_id", "usac_comm_init", "usac_allgather_records", "usac_merge_records",
+    "usac_comm_unique_id", "usac_comm_init", "usac_comm_count", "usac_allgather_records", "usac_merge_records",
     "usac_exchange_best_async", "usac_exchange_best_wait",
     "usac_random_create", "usac_random_next", "usac_random_destroy", "usac_sampler_create", "usac_sampler_generate",
     "usac_sampler_generate_batch", "usac_sampler_state", "usac_sampler_destroy", "usac_termination_create",
@@ -188,6 +188,7 @@ def lib():
         "usac_batch_sprt_info": (ctypes.c_int, [_vp, _P(ctypes.c_double), u32p, ctypes.c_uint32]),
         "usac_comm_unique_id": (ctypes.c_int, [u8p]),
         "usac_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, u8p]),
+        "usac_comm_count": (ctypes.c_int, [_vp, i32p, i32p, i32p]),
         "usac_allgather_records": (ctypes.c_int, [_vp, _P(Record), _P(Record)]),
         "usac_exchange_best_async": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32]),
         "usac_exchange_best_wait": (ctypes.c_int, [_vp, ctypes.c_uint32, _P(Record)]),
@@ -509,6 +510,13 @@ class Context:
         self._check(lib().usac_comm_init(self._h, nranks, rank, buf), "comm_init")
         self.nranks = nranks
 
+    def comm_count(self):
+        """(nranks, rank, device) as RCCL reports them for this context's communicator."""
+        v = np.zeros(3, dtype=np.int32)
+        p = [v[i:].ctypes.data_as(ctypes.POINTER(ctypes.c_int32)) for i in range(3)]
+        self._check(lib().usac_comm_count(self._h, *p), "comm_count")
+        return int(v[0]), int(v[1]), int(v[2])
+
     def allgather_record(self, rec):
         allr = (Record * self.nranks)()
         self._check(lib().usac_allgather_records(self._h, ctypes.byref(rec), allr), "allgather_records")
@@ -581,6 +589,7 @@ class Model:
         self.cell_size = 50
         self.neighborsType = NeighborsSearch.NullN
         self.spatial_coherence_gc = 0.1
+        self.max_hypothesis_test_before_sprt = 20  # model.hpp:40
 
     def ResetRandomGenerator(self, reset):
         self.reset_random_generator = bool(reset)
@@ -652,7 +661,7 @@ def _params(m):
     return _Params(m.threshold, m.desired_prob, m.max_iterations, seed, int(m.dlt_mode), m.batch, int(m.sampler),
                    1 if m.sprt else 0, int(m.lo), m.lo_sample_size, m.lo_iterative_iterations,
                    m.lo_inner_iterations, m.lo_threshold_multiplier, m.cell_size, int(m.neighborsType),
-                   m.k_nearest_neighbors, m.spatial_coherence_gc)
+                   m.k_nearest_neighbors, m.spatial_coherence_gc, m.max_hypothesis_test_before_sprt)
 
 
 # usac_allgather_fn (include/usac_gpu.h)

@@ -44,11 +44,12 @@ __global__ __launch_bounds__(64) void k_pool_mask(const void *__restrict__ pool_
     float m[NC];
 #pragma unroll
     for (int k = 0; k < NC; k++) m[k] = models[(size_t)k * stride + slot];
-    // this block's word range (blockIdx.y): a lane walks kMaskWords words, not all n / 32 -- the
-    // loop's batches hold a few hundred models, so lanes = models alone is a handful of waves
+    // this block's word ranges (blockIdx.y, then every gridDim.y-th range: the y grid is capped at
+    // 65535 blocks, reached above 16.7 M points): a lane walks kMaskWords words at a time, not all
+    // n / 32 -- the loop's batches hold a few hundred models, so lanes = models alone is a handful of waves
     const uint32_t nw = (n + 31) / 32;
-    const uint32_t w0 = blockIdx.y * kMaskWords, w1 = w0 + kMaskWords < nw ? w0 + kMaskWords : nw;
-    for (uint32_t w = w0; w < w1; w++) {
+    for (uint32_t w0 = blockIdx.y * kMaskWords; w0 < nw; w0 += gridDim.y * kMaskWords)
+    for (uint32_t w = w0, w1 = w0 + kMaskWords < nw ? w0 + kMaskWords : nw; w < w1; w++) {
         uint32_t bits = 0;
         const uint32_t p0 = 32 * w;
         const uint32_t lim = n - p0 < 32 ? n - p0 : 32;
@@ -90,7 +91,8 @@ hipError_t launch_gather_points(hipStream_t st, const void *pts, uint32_t cols, 
 hipError_t launch_pool_mask(hipStream_t st, int estimator, const void *pool_pts, uint32_t n, const float *models,
                             size_t stride, const uint32_t *list, const uint32_t *list_n, uint32_t kmax, float thr,
                             uint32_t *words, uint32_t row_stride) {
-    const dim3 grid((kmax + 63) / 64, ((n + 31) / 32 + kMaskWords - 1) / kMaskWords);
+    const uint32_t ranges = ((n + 31) / 32 + kMaskWords - 1) / kMaskWords;
+    const dim3 grid((kmax + 63) / 64, ranges < 65535u ? ranges : 65535u);
     switch (estimator) {
         case USAC_LINE2D:
             hipLaunchKernelGGL(k_pool_mask<1>, grid, dim3(64), 0, st, pool_pts, n, models, stride, list, list_n, kmax,
@@ -131,10 +133,16 @@ namespace usac {
 // after a inliers and b outliers, log lambda = P = a log(up) + b log(down) exactly (for the fp64
 // up / down), and the fp64 product stays within a relative t 2^-53 of it while it is a normal
 // number.  The kernels evaluate P in fp64 from exact counts and decide "rejected at the first P >
-// log A" wherever that is certain: every prefix's |P - log A| > margin (1e-7, against evaluation
-// and product errors below 1e-9 for n < 2^26), and no climb P_t - min_{s<=t} P_s reaches climb =
-// 700 (so a walk that crosses log A > 0 never passed through subnormal lambda, and an accepted
-// walk's rounding inflation stays below 2^-1074 n e^700 << 1 <= A).  A model whose walk is not
+// log A" wherever that is certain: every prefix's |P - log A| > margin, and no climb P_t -
+// min_{s<=t} P_s reaches climb = 700 (so a walk that crosses log A > 0 never passed through
+// subnormal lambda, and an accepted walk's rounding inflation stays below 2^-1074 n e^700 << 1 <= A).
+// The margin is set per context from n (usac_set_sprt, sprt_margin): with L = max(|lu|, |ld|, 1),
+// the logs' roundings over n terms and the product's drift are <= n L 2^-51, P from the counts
+// (two products and a sum) <= n L 2^-51, a tail chunk's running sum over `per` = ceil((n - 64) /
+// 256) adds <= per^2 L 2^-53 (the head's 64 adds likewise), log A's rounding <= |lA| 2^-53; the
+// margin is 8x their sum and never below 1e-7 (1.3e-10 at cfg3's n = 10 k, so 1e-7 there; the
+// budget grows with n -- 2^26 points give ~4e-4 -- and more walks then take the sequential path,
+// which is exact for any n).  A model whose walk is not
 // certified (|P - log A| <= margin at the deciding prefix, or a climb >= climb) is decided by the
 // reference's own sequential fp64 product from its start (one lane; rare by construction).
 //

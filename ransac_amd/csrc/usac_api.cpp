@@ -9,6 +9,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <chrono>
 #include <map>
 #include <memory>
@@ -195,15 +197,26 @@ struct PinnedPool {
 // Captured LO stage graphs, process-wide: a context lives for one Ransac::run (as the reference
 // builds its Ransac per run), but its device blocks come from DevPool and recur from run to run,
 // so a graph keyed by the stage shape and every buffer address it touches is reused across runs
-// (a graph's kernels only reach what its key's shape implies, and every buffer of that key is
-// at least that large whenever the key matches).  The cache only grows, up to kMax entries;
-// past that, stages of new shapes are launched kernel by kernel.
+// (a graph's kernels only reach what its key's shape implies; the key also holds every buffer's
+// reserved byte count, so a block handed out again at the same address with a smaller backing
+// never matches an old graph).  The cache only grows, up to kMax entries; past that, stages of new
+// shapes are launched kernel by kernel.  The execs are destroyed at process exit by an atexit
+// handler registered after the HIP runtime's own (so it runs before the runtime's teardown).
 struct GraphCache {
     static constexpr size_t kMax = 256;
     std::mutex mu;
     std::map<std::vector<uintptr_t>, hipGraphExec_t> g;
     static GraphCache &get() {
-        static GraphCache *c = new GraphCache();
+        static GraphCache *c = [] {
+            GraphCache *gc = new GraphCache();
+            std::atexit([] {
+                GraphCache &cc = GraphCache::get();
+                std::lock_guard<std::mutex> lk(cc.mu);
+                for (auto &kv : cc.g) (void)hipGraphExecDestroy(kv.second);
+                cc.g.clear();
+            });
+            return gc;
+        }();
         return *c;
     }
 };
@@ -352,6 +365,7 @@ struct usac_ctx {
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
     float last_ms[3] = {0, 0, 0};
     bool batch_valid = false;  // counts / sums hold a batch's scores (usac_last_counts)
+    uint32_t sprt_S = 0;       // model slots of the last batch-SPRT launch (usac_batch_sprt_info)
     bool timed_pending = false;
     std::string err;
 };
@@ -588,6 +602,7 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
         hipError_t e = hipMemsetAsync(c->sprt_tested.p, 0, sizeof(uint32_t), c->stream);
         if (e != hipSuccess) return e;
         const uint32_t S = B * c->spk;
+        c->sprt_S = S;
         e = c->sprt_surv.reserve(usac::sprt_survivor_bytes() * (size_t)S);
         if (e != hipSuccess) return e;
         e = c->sprt_starts.reserve(sizeof(uint32_t) * (size_t)S);
@@ -1166,7 +1181,10 @@ struct LoRansac {
                 (uintptr_t)c->pts.p,
                 (uintptr_t)c->lo_io.p, (uintptr_t)c->lo_q.p, (uintptr_t)c->lo_part.p, (uintptr_t)c->lo_ws.p,
                 (uintptr_t)c->nm_seq.p, (uintptr_t)c->lo_lists.p, (uintptr_t)c->lo_max.p, (uintptr_t)c->lo_scr.p,
-                (uintptr_t)c->lo_best.p, scr_bytes, in_bytes, out_bytes};
+                (uintptr_t)c->lo_best.p, scr_bytes, in_bytes, out_bytes,
+                // the blocks' reserved sizes (DevPool may hand an address out again with less behind it)
+                c->pts.bytes, c->lo_io.bytes, c->lo_q.bytes, c->lo_part.bytes, c->lo_ws.bytes, c->nm_seq.bytes,
+                c->lo_lists.bytes, c->lo_max.bytes, c->lo_scr.bytes, c->lo_best.bytes};
             GraphCache &gc = GraphCache::get();
             hipGraphExec_t ex = nullptr;
             {
@@ -1620,6 +1638,11 @@ struct GcLo {
         return USAC_OK;
     }
 };
+
+// model.hpp:40 max_hypothesis_test_before_sprt (usac_params, ABI 12; 0 = the default 20)
+static int max_before_sprt(const usac_params *p) {
+    return p->max_hypothesis_test_before_sprt ? (int)p->max_hypothesis_test_before_sprt : 20;
+}
 
 bool rec_better(const usac_record &a, const usac_record &b) {
     if (!a.valid) return false;
@@ -2098,6 +2121,12 @@ int usac_set_sprt(usac_ctx *c, int enable, uint32_t seed, double epsilon, double
     c->sprt_k.climb = ec ? atof(ec) : 700.0;
     if (!(c->sprt_k.margin >= 1e-7) || !(c->sprt_k.climb > 0) || c->sprt_k.climb > 700.0)
         return fail(c, USAC_ERR_ARG, "SPRT certificate: margin >= 1e-7 and 0 < climb <= 700");
+    {  // the certificate's error budget at this n (kernels_sprt.hip): never a margin below it
+        const double L = std::max(std::max(fabs(c->sprt_k.lu), fabs(c->sprt_k.ld)), 1.0);
+        const double nn = (double)c->n, per = std::ceil(std::max(nn - 64.0, 0.0) / 256.0) + 64.0;
+        const double budget = 2.0 * nn * L * 0x1p-51 + per * per * L * 0x1p-53 + fabs(c->sprt_k.lA) * 0x1p-53;
+        c->sprt_k.margin = std::max(c->sprt_k.margin, 8.0 * budget);
+    }
     HIP_TRY(c, c->pool_idx.reserve(sizeof(uint32_t) * c->n));
     HIP_TRY(c, c->sprt_pts.reserve(sizeof(float) * c->cols * (size_t)c->n));
     HIP_TRY(c, c->sprt_tested.reserve(sizeof(uint32_t)));
@@ -2121,10 +2150,23 @@ int usac_batch_sprt_info(usac_ctx *c, double *eps_delta_A, uint32_t *starts, uin
         eps_delta_A[2] = c->sprt_k.A;
     }
     if (starts && n) {
-        if (!c->batch_valid || (size_t)n * sizeof(uint32_t) > c->sprt_starts.bytes)
-            return fail(c, USAC_ERR_ARG, "no SPRT batch of that many slots");
+        if (!c->batch_valid || n > c->sprt_S) return fail(c, USAC_ERR_ARG, "no SPRT batch of that many slots");
         HIP_TRY(c, hipMemcpyAsync(starts, c->sprt_starts.p, sizeof(uint32_t) * n, hipMemcpyDeviceToHost, c->stream));
+        uint32_t ln = 0;
+        if (listed(c)) HIP_TRY(c, hipMemcpyAsync(&ln, c->list_n.p, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, stream_wait(c->stream));
+        if (listed(c)) {  // k_sprt_head writes the listed (occupied) slots only: the others get UINT32_MAX
+            std::vector<uint32_t> lst(ln);
+            if (ln) {
+                HIP_TRY(c, hipMemcpyAsync(lst.data(), c->list.p, sizeof(uint32_t) * ln, hipMemcpyDeviceToHost, c->stream));
+                HIP_TRY(c, stream_wait(c->stream));
+            }
+            std::vector<char> occ(n, 0);
+            for (uint32_t k = 0; k < ln; k++)
+                if (lst[k] < n) occ[lst[k]] = 1;
+            for (uint32_t i = 0; i < n; i++)
+                if (!occ[i]) starts[i] = UINT32_MAX;
+        }
     }
     return USAC_OK;
 }
@@ -2400,9 +2442,10 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     sub(2);
     usac::StandardTerminationCriteria term(prm->desired_prob, m, n, prm->max_iterations);
     std::unique_ptr<usac::Sprt> sprt;
+    const int max_before = max_before_sprt(prm);
     const uint32_t nw = (n + 31) / 32;
     if (prm->sprt) {
-        sprt.reset(new usac::Sprt(grng, c->estimator, n, m, prm->max_iterations));
+        sprt.reset(new usac::Sprt(grng, c->estimator, n, m, prm->max_iterations, max_before_sprt(prm)));
         HIP_TRY(c, c->pool_idx.reserve(sizeof(uint32_t) * n));
         HIP_TRY(c, c->pool_pts.reserve(sizeof(float) * c->cols * (size_t)n));
         HIP_TRY(c, c->masks.reserve(sizeof(uint32_t) * nw * (size_t)batch * spk));
@@ -2712,7 +2755,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                                                    cur.inlier_number, cur.score, mask_stride);
                     if (!good) {
                         out->sprt_rejected++;
-                        if ((int)iters >= 20) {  // max_hypothesis_test_before_sprt (model.hpp:40), Q9
+                        if ((int)iters >= max_before) {  // max_hypothesis_test_before_sprt (model.hpp:40), Q9
                             iters++;
                             continue;
                         }
@@ -2931,6 +2974,15 @@ int usac_comm_init(usac_ctx *c, int nranks, int rank, const uint8_t *id128) {
     return USAC_OK;
 }
 
+int usac_comm_count(usac_ctx *c, int *nranks, int *rank, int *device) {
+    if (!c || !nranks || !rank || !device) return USAC_ERR_ARG;
+    if (!c->comm) return fail(c, USAC_ERR_ARG, "usac_comm_init not called");
+    NCCL_TRY(c, ncclCommCount(c->comm, nranks));
+    NCCL_TRY(c, ncclCommUserRank(c->comm, rank));
+    NCCL_TRY(c, ncclCommCuDevice(c->comm, device));
+    return USAC_OK;
+}
+
 int usac_exchange_best_async(usac_ctx *c, usac_ctx *batch, uint32_t slot) {
     if (!c || !batch || slot >= USAC_XRING) return USAC_ERR_ARG;
     if (!c->comm) return fail(c, USAC_ERR_ARG, "usac_comm_init not called");
@@ -3053,6 +3105,7 @@ struct usac_sprt {
     std::vector<int32_t> row_of;  // batch slot -> row (-1: empty slot)
     uint32_t batch_B = 0, batch_slots = 0;
     uint32_t rejected = 0;
+    int max_before = 20;  // usac_params::max_hypothesis_test_before_sprt
     ~usac_sprt() {
         (void)hipSetDevice(c->device);
         (void)hipStreamSynchronize(c->stream);
@@ -3259,7 +3312,8 @@ int usac_sprt_create(usac_ctx *c, const usac_params *p, usac_random *rng, usac_s
     s->c = c;
     s->thr = p->threshold;
     s->nw = (c->n + 31) / 32;
-    s->s.reset(new usac::Sprt(rng->g, c->estimator, c->n, c->m, p->max_iterations));
+    s->max_before = max_before_sprt(p);
+    s->s.reset(new usac::Sprt(rng->g, c->estimator, c->n, c->m, p->max_iterations, s->max_before));
     HIP_TRY(c, s->pool_idx.reserve(sizeof(uint32_t) * c->n));
     HIP_TRY(c, s->pool_pts.reserve(sizeof(float) * c->cols * (size_t)c->n));
     HIP_TRY(c, hipMemcpyAsync(s->pool_idx.p, s->s->pool().data(), sizeof(uint32_t) * c->n, hipMemcpyHostToDevice,
@@ -3333,7 +3387,7 @@ int usac_sprt_replay(usac_sprt *s, const float *models, const int32_t *n_models,
             float sc = 0.f;
             const bool good = sprt_walk(s, (uint32_t)s->row_of[(size_t)b * S + q], (int)st->iters,
                                         (uint32_t)st->best_inliers, cnt, sc);
-            if (!good && st->iters >= 20) {  // max_hypothesis_test_before_sprt (model.hpp:40), Q9
+            if (!good && (int)st->iters >= s->max_before) {  // max_hypothesis_test_before_sprt (model.hpp:40), Q9
                 st->iters++;
                 continue;
             }

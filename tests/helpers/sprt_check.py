@@ -19,4 +19,5 @@ def batch_sprt_vs_oracle(oracle, ctx, okind, pts, thr, samples, counts, pool_see
     pool, _ = oracle.sprt_pool(pool_seed, okind, len(pts), m)
     good, cnt, tested = oracle.sprt_fixed_batch(est, pool, thr, models, starts[occ], eps, delta, A)
     return {"device": np.asarray(counts)[occ], "oracle": cnt, "accepted": int(good.sum()), "models": int(occ.sum()),
-            "oracle_tested": int(tested.sum()), "empty_slots_ok": bool((np.asarray(counts)[~occ] < 0).all())}
+            "oracle_tested": int(tested.sum()), "empty_slots_ok": bool((np.asarray(counts)[~occ] < 0).all()) and
+            bool((starts[~occ] == 0xFFFFFFFF).all())}  # usac_batch_sprt_info: an empty slot has no start

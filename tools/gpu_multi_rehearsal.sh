@@ -1,12 +1,28 @@
 #!/bin/bash
-# N = 2 rehearsal of bench.py's multi-rank paths on ONE GPU (two ranks share the device; the
-# record exchange falls back to gloo there, RCCL refuses two ranks on one device): the
-# throughput line and the hypothesis-sharded cfg5 line.  Distinct GPUs use RCCL (driver runs).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
+# N = 2 rehearsal of bench.py's multi-rank paths on ONE GPU: `bench.py --gpus 2` starts its own two
+# rank processes, which share the device (USAC_BENCH_SAME_DEVICE; the record exchange falls back to
+# gloo there -- RCCL refuses two ranks on one device).  Lines: cfg2, cfg3 batch SPRT, cfg4, and the
+# hypothesis-sharded cfg5 run; each prints n_gpus, the parity verdicts (every rank's slice, the
+# first timed batch's merged record against the oracle over both ranks' samples) and the CPU baseline.
+# Usage (GPU box): bash tools/gpu_multi_rehearsal.sh [tag]; outputs gpurun_out/<tag>/.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+O=gpurun_out/${1:-multi}; mkdir -p $O
 export USAC_BENCH_SAME_DEVICE=1
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-    --master-port 29517 bench.py --gpus 2 --steps 30 --warmup 5 > gpurun_out/multi_h.json 2> gpurun_out/multi_h.err || { tail -20 gpurun_out/multi_h.err; exit 1; }
-cat gpurun_out/multi_h.json | cut -c1-400
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-    --master-port 29518 bench.py --cfg5 --gpus 2 --steps 20 --warmup 2 --cpu-seconds 0 > gpurun_out/multi_cfg5.json 2> gpurun_out/multi_cfg5.err || { tail -20 gpurun_out/multi_cfg5.err; exit 1; }
-cat gpurun_out/multi_cfg5.json | cut -c1-600
+run() {  # name, args...
+  local n=$1; shift
+  timeout -k 10 300 python bench.py --gpus 2 "$@" > $O/$n.json 2> $O/$n.err || { tail -20 $O/$n.err; exit 1; }
+  python3 - $O/$n.json <<'EOF'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+p = d.get("parity", {})
+print("%-14s n_gpus %d  %.4g %s  parity.ok %s  ranks %s  first_timed_batch %s  cpu_baseline %s" % (
+    sys.argv[1].split("/")[-1], d["n_gpus"], d["value"], d["unit"], p.get("ok", p),
+    (p.get("ranks") or {}).get("ok"), (p.get("first_timed_batch") or {}).get("ok"),
+    (d.get("cpu_baseline") or {}).get("value")))
+EOF
+}
+run cfg2 --steps 30 --warmup 5 --cpu-seconds 3
+run cfg3 --estimator fundamental --steps 30 --warmup 5 --cpu-seconds 3
+run cfg4 --estimator essential --steps 20 --warmup 3 --cpu-seconds 3
+run cfg5 --cfg5 --steps 10 --warmup 2 --cpu-seconds 3
