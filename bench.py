@@ -139,6 +139,75 @@ def cpu_baseline(kind, pts, thr, dlt_mode, seconds):
             "cpu_model": model, "nproc": os.cpu_count(), "cpus_available": avail}
 
 
+def cpu_baseline_batch_sprt(usac, ctx, kind, pts, thr, dlt_mode, seed, first_hyp, seconds):
+    """Like-for-like CPU baseline of a batch-SPRT line: the CPU oracle runs the
+    SAME hypotheses the timed batches run -- the device sampler's samples at the timed indices (the
+    PROSAC subset schedule, then uniform: prosac_sampler.hpp:117-172), the 7-point solve with the
+    oriented-constraint filter, and the batch SPRT with the same fixed (epsilon, delta, A) from the
+    same pool position per model (sprt.hpp:209-234 as a fixed walk: oracle sprt_fixed_batch) -- so its
+    models per hypothesis are the GPU's by construction and its accept / reject decisions are checked
+    equal.  The GPU supplies each chunk's samples and pool starts (untimed); only the oracle's solve +
+    verify is timed, on one core and on the box's threads."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import oracle as O
+
+    okind = {"fundamental": O.FUNDAMENTAL, "essential": O.ESSENTIAL}.get(kind, O.HOMOGRAPHY)
+    spk = 3 if kind == "fundamental" else 1
+    m = {"fundamental": 7, "essential": 5}.get(kind, 4)
+    pool, _ = O.sprt_pool(seed, okind, len(pts), m)
+
+    def gpu_chunk(first, K):  # the device's samples, decisions and pool starts of K hypotheses
+        ctx.hypothesize_async(K, seed, first, thr)
+        ctx.fetch_best()
+        (eps, delta, A), starts = ctx.batch_sprt_info(K * spk)
+        counts, _ = ctx.last_counts(K * spk)
+        return ctx.draw_samples(K, seed, first), starts, counts, (eps, delta, A)
+
+    def cpu_chunk(ch):  # the oracle's work on one chunk: solve, oriented filter, fixed SPRT walks
+        smp, starts, counts, (eps, delta, A) = ch
+        est = O.Estimator(okind, pts, dlt_mode)
+        om, onm = est.estimate_batch(smp)
+        om = np.asarray(om, np.float32).reshape(len(smp), -1, 9)
+        if spk == 3:
+            occ = (np.arange(3)[None, :] < onm[:, None]).reshape(-1)
+            models = om.reshape(-1, 9)[occ]
+        else:
+            occ = onm == 1 if okind == O.ESSENTIAL else np.ones(len(smp), bool)
+            models = om[:, 0][occ]
+        good, cnt, tested = O.sprt_fixed_batch(est, pool, thr, models, starts[occ], eps, delta, A)
+        return int(occ.sum()), bool((cnt == counts[occ]).all()), int(good.sum()), int(tested.sum())
+
+    # calibrate on one chunk, then a bounded sample of ~`seconds` of one core's work
+    K = 8192
+    c0 = gpu_chunk(first_hyp, K)
+    t0 = time.perf_counter()
+    cpu_chunk(c0)
+    per = max((time.perf_counter() - t0) / K, 1e-7)
+    nchunks = max(2, min(256, int(seconds / per / K)))
+    chunks = [gpu_chunk(first_hyp + i * K, K) for i in range(nchunks)]
+    t0 = time.perf_counter()
+    res = [cpu_chunk(ch) for ch in chunks]
+    dt = time.perf_counter() - t0
+    model, avail, threads = cpu_info()
+    t1 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(cpu_chunk, chunks))
+    dt_mt = time.perf_counter() - t1
+    hyps = nchunks * K
+    models = sum(r[0] for r in res)
+    return {"value": hyps / dt, "unit": "hypotheses/s", "cores": 1, "kind": "port",
+            "sample": "%d hypotheses of the timed stream (device sampler indices %d..%d: the same samples), 7-pt solve "
+                      "+ oriented filter + batch SPRT with the line's fixed (epsilon, delta, A) from the device's pool "
+                      "starts, %.1f s on 1 core of %s" % (hyps, first_hyp, first_hyp + hyps - 1, dt, model),
+            "models_per_hypothesis": models / hyps, "sprt_accepted": sum(r[2] for r in res),
+            "points_tested_per_hypothesis": sum(r[3] for r in res) / hyps,
+            "decisions_equal": all(r[1] for r in res),
+            "all_cores": {"value": hyps / dt_mt, "unit": "hypotheses/s", "cores": threads,
+                          "sample": "the same %d hypotheses, %.1f s on %d threads" % (hyps, dt_mt, threads)},
+            "cpu_model": model, "nproc": os.cpu_count(), "cpus_available": avail}
+
+
 def parity_check(usac, kind, pts, thr, dlt_mode, samples=None):
     """Inlier-count match vs the reference path (CPU oracle) on 256 host-drawn samples (or the
     given ones, e.g. the device NAPSAC stream's)."""
@@ -302,6 +371,31 @@ def first_batch_parity(usac, ctx, kind, pts, thr, dlt_mode, seed, B, step, world
                     "Σ) of all %d ranks' samples, redrawn by rank 0 from (seed, global index)" % world}
 
 
+def _kname_key(name):
+    """(identifier, template arguments) of a kernel name as rocprofv3 writes it -- demangled
+    ("void usac::k_score_hf<8, false>(...)") or, for kernels with vector-typed arguments, mangled
+    ("_ZN4usac11k_score_h16ILi2ELi1ELi8EEEv...") -- so either form matches the other."""
+    import re
+
+    name = name.strip()
+    m = re.match(r"_ZN4usac(\d+)", name)
+    if m:
+        ln, rest = int(m.group(1)), name[m.end():]
+        ident, rest = rest[:ln], rest[ln:]
+        args = tuple(int(v) for v in re.findall(r"L[ib](\d+)E", rest.split("EEv")[0])) if rest.startswith("I") else ()
+        return ident, args
+    m = re.search(r"usac::(\w+)\s*(<([^>]*)>)?", name)
+    if not m:
+        return name, ()
+    args = ()
+    if m.group(3):  # integer / bool template arguments (a type argument stays its text)
+        def arg(a):
+            a = a.strip()
+            return 1 if a == "true" else 0 if a == "false" else int(a) if re.fullmatch(r"-?\d+", a) else a
+        args = tuple(arg(a) for a in m.group(3).split(","))
+    return m.group(1), args
+
+
 def _profile_entry(kernel_prefix, n_points, batch):
     """(summary entry, source) of `kernel_prefix` in the newest committed rocprofv3 summary
     (profiles/<round>_summary.json, made by tools/archive/profile.sh + tools/summarize_profile.py)
@@ -318,7 +412,7 @@ def _profile_entry(kernel_prefix, n_points, batch):
         if shape.get("n_points") != n_points or shape.get("batch") != batch:
             continue
         for k, v in d.get("kernels", {}).items():
-            if k.replace(" ", "").startswith(kernel_prefix.replace(" ", "")):
+            if k.replace(" ", "").startswith(kernel_prefix.replace(" ", "")) or _kname_key(k) == _kname_key(kernel_prefix):
                 best = (v, os.path.relpath(f, ROOT))
     return best
 
@@ -329,6 +423,7 @@ def _profile_entry(kernel_prefix, n_points, batch):
 # wave, summed over waves) accounts for and SQ_INSTS_VALU (instructions) does not.
 SIMD_CYCLES_S = 1024 * 2.4e9
 VALU_PEAK_INSTR_S = SIMD_CYCLES_S / 2
+MFMA_F16_DENSE_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense BF16/FP16
 
 
 def valu_roofline(kernel_prefix, n_points, batch, kernel_ms):
@@ -362,8 +457,10 @@ def valu_roofline(kernel_prefix, n_points, batch, kernel_ms):
         # at the guide's 2 (plain) / 4 (packed, transcendental); frac_x4 = SQ_ACTIVE_INST_VALU x 4,
         # which charges every instruction 4 (the counter counts ~1 per instruction, packed or not)
         import re
-        mixf = os.path.join(ROOT, "profiles", "r4", "isa_%s.json" % re.sub(
-            r"[^A-Za-z0-9]+", "_", kernel_prefix.replace("void usac::", "")).strip("_"))
+        mixn = "isa_%s.json" % re.sub(r"[^A-Za-z0-9]+", "_", kernel_prefix.replace("void usac::", "")).strip("_")
+        mixf = os.path.join(ROOT, "profiles", "r5", mixn)
+        if not os.path.exists(mixf):
+            mixf = os.path.join(ROOT, "profiles", "r4", mixn)
         if os.path.exists(mixf):
             mx = json.load(open(mixf))
             guide = float(mx["issue_cycles_per_valu_instruction"])
@@ -378,6 +475,16 @@ def valu_roofline(kernel_prefix, n_points, batch, kernel_ms):
                                   "note": "frac = SQ_INSTS_VALU x the hot loop's mean measured issue cycles / kernel "
                                           "time / (1024 SIMDs x 2.4 GHz); frac_guide = the same with the guide's "
                                           "2 / 4 cycles; frac_x4 = the SQ_ACTIVE_INST_VALU x 4 form"}
+    if "k_score_h16" in kernel_prefix:  # the matrix-core prefilter: its MFMA work beside the VALU issue
+        # executed v_mfma_f32_32x32x16_f16 flops per launch: ceil(B / 20) waves (2 tiles of 10 hypotheses)
+        # x ceil(N / 32) point blocks x 2 MFMAs x 32 x 32 x 16 x 2
+        fl = -(-batch // 20) * -(-n_points // 32) * 2 * 32 * 32 * 16 * 2
+        out["mfma"] = {"executed_flops_per_launch": fl, "achieved_tflops": fl / t / 1e12,
+                       "peak_tflops": MFMA_F16_DENSE_TFLOPS, "frac": fl / t / 1e12 / MFMA_F16_DENSE_TFLOPS,
+                       "note": "dense fp16 MFMA peak (MI355X_MICROARCH.md: ~2.5 PF); the tiles carry 9 of 16 K "
+                               "columns and 30 of 32 rows, so useful flops are 0.53x the executed ones"}
+        if pmc.get("SQ_VALU_MFMA_BUSY_CYCLES"):
+            out["mfma"]["busy_frac_pmc"] = pmc["SQ_VALU_MFMA_BUSY_CYCLES"] / t / SIMD_CYCLES_S
     if pmc.get("SQ_WAVE_CYCLES"):
         wc = pmc["SQ_WAVE_CYCLES"]
         out["wave_cycle_split"] = {k.lower(): pmc[k] / wc for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
@@ -399,8 +506,10 @@ def _stage_kernels(estimator, sprt, chunks, stage):
                     "usac::k_e5_select("]}[est]
     if sprt:
         return ["void usac::k_sprt_head<%d>(" % est, "void usac::k_sprt_tail<%d>(" % est]
-    if est == 2:
-        return ["usac::k_presort_h(", "void usac::k_score_hf<%d, false>(" % chunks]
+    if est == 2:  # the matrix-core prefilter scorer (kernels_h16.hip; USAC_H16=0: k_presort_h + k_score_hf)
+        if os.environ.get("USAC_H16", "1") == "0":
+            return ["usac::k_presort_h(", "void usac::k_score_hf<%d, false>(" % chunks]
+        return ["usac::k_h16_rows(", "void usac::k_score_h16<2, 1, 8>(", "usac::k_h16_finish("]
     return ["usac::k_prepare_rec(", "void usac::k_presort_tv<%d>(" % est, "void usac::k_score_f2<%d>(" % est,
             "usac::k_tv_combine("]
 
@@ -937,9 +1046,10 @@ def main():
         for c in ctxs:
             c.set_sprt(True, seed=args.seed)
     models_per_hyp = 1.0
-    if fund or ess:  # occupied model slots per sample of the device sampler's stream (one batch)
+    timed_first = (args.warmup * world + rank) * B  # the first timed batch's first hypothesis
+    if fund or ess:  # occupied model slots per sample of the first timed batch (the device stream)
         ctx.set_sprt(False)
-        c0, _, _ = ctx.hypothesize_score(B=B, seed=args.seed + 1000, first_hyp=0, thr=args.threshold)
+        c0, _, _ = ctx.hypothesize_score(B=B, seed=args.seed, first_hyp=timed_first, thr=args.threshold)
         models_per_hyp = float((c0 >= 0).sum()) / B
         if args.sprt:
             ctx.set_sprt(True, seed=args.seed)
@@ -1037,7 +1147,7 @@ def main():
     # record also through the line's exchange), gathered to rank 0
     tk_all = None
     if world > 1:
-        tk_first = (args.warmup + args.steps + 100) * world * B + rank * 256  # beyond every timed index
+        tk_first = rank * 256  # the stream's head, as at N = 1 (PROSAC's early subsets: SPRT accepts models there)
         own = timed_kernel_parity(usac, ctx, args.estimator, pts, args.threshold, dlt_mode, args.seed,
                                   bool(args.sprt), first_hyp=tk_first,
                                   xctx=ctx if exchange == "rccl_allgather" else None)
@@ -1149,8 +1259,14 @@ def main():
         par["ok"] = bool(par["inlier_counts_equal"] and par["scores_bit_equal"] and par["timed_kernel"]["ok"] and
                          par.get("ranks", {}).get("ok", True) and par.get("first_timed_batch", {}).get("ok", True))
         out["parity"] = par
+        if fund or ess:  # occupied model slots per sample of the first timed batch (beside the value)
+            out["models_per_hypothesis"] = models_per_hyp
         if args.cpu_seconds > 0:
-            out["cpu_baseline"] = cpu_baseline(args.estimator, pts, args.threshold, dlt_mode, args.cpu_seconds)
+            if args.sprt:  # the same hypotheses through the oracle (same samples, models, SPRT decisions)
+                out["cpu_baseline"] = cpu_baseline_batch_sprt(usac, ctx, args.estimator, pts, args.threshold, dlt_mode,
+                                                              args.seed, timed_first, args.cpu_seconds)
+            else:
+                out["cpu_baseline"] = cpu_baseline(args.estimator, pts, args.threshold, dlt_mode, args.cpu_seconds)
             out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
         print(json.dumps(out), flush=True)
     if world > 1:  # the other ranks wait for rank 0's checks and CPU baseline before tearing down

@@ -216,9 +216,11 @@ int usac_last_timings(usac_ctx *ctx, float *ms3);
  * 1, 2, 4, 8, 16; any of 1..128 for the fundamental / essential estimators (their chunks are
  * separate workgroups, combined in chunk order; default 96). */
 int usac_set_score_chunks(usac_ctx *ctx, int chunks);
-/* Homography score kernel: 0 = guard-band fast path with the hypothesis pre-sort (default),
- * 1 = exact reference expression for every pair, 2 = fast path without the pre-sort (A/B and
- * debugging; all three give the same results). */
+/* Homography score kernel: 0 = guard-band fast path with the hypothesis pre-sort (default; multi-
+ * chunk batches -- the throughput and loop batches -- go through the matrix-core prefilter scorer
+ * unless USAC_H16=0), 1 = exact reference expression for every pair, 2 = fast path without the
+ * pre-sort, 3 = as 0, and usac_score_models also scores through the multi-chunk scorer (tests: exact
+ * counts, Σ within its bound).  Every variant gives the same counts. */
 int usac_set_score_variant(usac_ctx *ctx, int variant);
 
 /* Throughput SPRT (sprt.hpp:191-317 as a batch test): with enable != 0 every later

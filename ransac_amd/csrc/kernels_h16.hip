@@ -1,0 +1,461 @@
+// kernels_h16.hip -- the homography score with a matrix-core prefilter (gfx950 MFMA, fp16 in,
+// fp32 accumulate), exact counts (DESIGN.md §6 "h16").
+//
+// Every (hypothesis, point) pair of the reference's Quality::getNumberInliers scan
+// (quality.hpp:60-101, homography_estimator.hpp:85-110) needs e = (x2 Z - X, y2 Z - Y) and Z of
+// H p1.  Each of the three is a dot product of nine per-hypothesis coefficients with nine per-point
+// features f = (u, v, 1, p u, p v, p, q u, q v, q) of the centred, power-of-two-scaled coordinates
+// (x1 = cx1 + s1 u, ..., x2 = cx2 + s2 p, y2 = cy2 + s2 q):
+//   ex = x2 Z - X = sum over (u, v, 1) of (cx2 Z_k - X_k) f_k + sum over (p u, p v, p) of s2 Z_k f_k,
+// likewise ey with (q u, q v, q), and Z with (u, v, 1).  So a 32-row x 32-point tile of them is ONE
+// v_mfma_f32_32x32x16_f16: rows = (hypothesis, {ex, ey, Z}) for ten hypotheses (30 of 32 rows),
+// columns = 32 points, K = the nine features (of 16).  The fp16 coefficients and features carry a
+// rounding error, so the MFMA tile is a PREFILTER with a rigorous bound: per hypothesis a slack F_m
+// (k_h16_rows) such that
+//   max(|ex_m|, |ey_m|) > |zr_m| + F_m   ==>   max(|ex_fma|, |ey_fma|) > trm |Z_fma| + F,
+// the packed stage A of k_score_hf (usac_hscore.hpp stage_a_keep2), which proves the reference's
+// error is not below thr.  zr is the Z row times trm (1 + 2^-10).  The derivation: |f~ - f| <=
+// 2^-11 |f| + 2^-25 (fp16 rounding, subnormal floor), |g~ - g| likewise plus the coefficients' own
+// fp32 rounding (<= 2^-21 of the sum a_k of their terms' magnitudes), the MFMA's fp32 accumulation of 16
+// exact fp16 products <= 2^-19 sum |g~ f~|; |f| <= fmax (dataset constants), so per row
+// D = sum_k |g~_k| (2^-10 fmax_k + 2^-25) + fmax_k (2^-10 |g_k| + 2^-25 + 2^-21 a_k) + 2^-19 |g~_k| (fmax_k
+// + 2^-24), and with the FMA chains' own errors (|ex_fma - ex| <= c.z dZ + dX, |Z_fma - Z| <= dZ,
+// stage_a_bounds) F_m = [F + max(D_ex + c.z dZ + dX, D_ey + c.w dZ + dY) + trm' dZ + D_zr](1 + 2^-20),
+// everything in the hypothesis' power-of-two scale 2^-c.  The (1 + 2^-10) on trm dominates the
+// rounding of |zr_m| + F_m.  Non-finite hypotheses get zero rows and F_m = +inf (every pair goes to
+// the exact stage); padding and non-finite points get NaN features (never kept -- the reference
+// never counts them: their error is NaN or infinite).
+//
+// A kept pair goes to the exact stage B of k_score_hf (stage_b: v_rcp / v_sqrt with the guard band,
+// the reference's own expression inside it) through a per-wave LDS queue of (hypothesis, point)
+// entries, drained 64 at a time so every lane of the drain works (kept pairs are ~0.1 % of all).
+// Counts are exact; Σ adds stage B's terms as 2^-k fixed point (integer adds: deterministic, an
+// error of one unit per term), per point chunk, the chunks summed by k_h16_finish.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include <stdlib.h>
+
+#include <algorithm>
+
+#include "usac_device.hpp"
+#include "usac_hscore.hpp"
+#include "usac_kernels.h"
+
+namespace usac {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// queue entries per wave: a ring of < 64 waiting entries plus one iteration's appends (<= 64 per row)
+template <int NA, int U>
+constexpr uint32_t h16_queue() { return 64u * 5u * NA * U + 64u; }
+
+// ------------------------------------------------------------------------ dataset constants (host)
+bool h16_consts(const float *pts, uint32_t n, float4 ext, H16Consts *o) {
+    double lo[4] = {INFINITY, INFINITY, INFINITY, INFINITY}, hi[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    uint32_t nf = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const float *p = pts + 4 * (size_t)i;
+        if (!(std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2]) && std::isfinite(p[3]))) continue;
+        nf++;
+        for (int k = 0; k < 4; k++) {
+            lo[k] = std::min(lo[k], (double)p[k]);
+            hi[k] = std::max(hi[k], (double)p[k]);
+        }
+    }
+    if (!nf) return false;
+    // centres: midpoints of the box (exact in fp64); scales: the smallest powers of two >= the
+    // half-extents, so every centred coordinate lies in [-1, 1]
+    auto pow2_at_least = [](double v) { return v > 0 ? std::ldexp(1.0, std::ilogb(v) + 1) : 1.0; };
+    // (fp32 numbers: k_h16_rows works in fp32 and must use the very centres the features used)
+    o->cx1 = (float)(0.5 * (lo[0] + hi[0]));
+    o->cy1 = (float)(0.5 * (lo[1] + hi[1]));
+    o->cx2 = (float)(0.5 * (lo[2] + hi[2]));
+    o->cy2 = (float)(0.5 * (lo[3] + hi[3]));
+    o->s1 = pow2_at_least(std::max(std::max(hi[0] - o->cx1, o->cx1 - lo[0]), std::max(hi[1] - o->cy1, o->cy1 - lo[1])));
+    o->s2 = pow2_at_least(std::max(std::max(hi[2] - o->cx2, o->cx2 - lo[2]), std::max(hi[3] - o->cy2, o->cy2 - lo[3])));
+    for (int k = 0; k < 9; k++) o->fmax[k] = 0.0;
+    for (uint32_t i = 0; i < n; i++) {
+        const float *p = pts + 4 * (size_t)i;
+        if (!(std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2]) && std::isfinite(p[3]))) continue;
+        const double u = (p[0] - o->cx1) / o->s1, v = (p[1] - o->cy1) / o->s1;
+        const double pp = (p[2] - o->cx2) / o->s2, q = (p[3] - o->cy2) / o->s2;
+        const double f[9] = {u, v, 1.0, pp * u, pp * v, pp, q * u, q * v, q};
+        for (int k = 0; k < 9; k++) o->fmax[k] = std::max(o->fmax[k], std::fabs(f[k]));
+    }
+    for (int k = 0; k < 9; k++)  // the device's fp64 features may round up; k_h16_rows reads fmax as floats
+        o->fmax[k] = (double)std::nextafter((float)(o->fmax[k] * (1.0 + 0x1p-40)), INFINITY);
+    o->ext = ext;
+    return true;
+}
+
+size_t h16_feature_bytes(uint32_t n) { return (size_t)((n + 31) / 32) * 1024; }
+
+// one thread per (32-point block, lane): lane l holds B[k = 8 (l >> 5) + j][column l & 31]
+__global__ __launch_bounds__(256) void k_h16_points(const float4 *__restrict__ pts, uint32_t n, H16Consts k,
+                                                    half8 *__restrict__ feat) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t nblk = (n + 31) / 32;
+    if (t >= nblk * 64) return;
+    const uint32_t blk = t >> 6, l = t & 63, i = blk * 32 + (l & 31), hf = l >> 5;
+    half8 o;
+    bool ok = i < n;
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok) {
+        p = pts[i];
+        ok = isfinite(p.x) && isfinite(p.y) && isfinite(p.z) && isfinite(p.w);
+    }
+    if (!ok) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) o[j] = (_Float16)__builtin_nanf("");
+    } else {
+        const double u = ((double)p.x - k.cx1) / k.s1, v = ((double)p.y - k.cy1) / k.s1;
+        const double pp = ((double)p.z - k.cx2) / k.s2, q = ((double)p.w - k.cy2) / k.s2;
+        const double f[16] = {u, v, 1.0, pp * u, pp * v, pp, q * u, q * v, q, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 8; j++) o[j] = (_Float16)(float)f[8 * hf + j];
+    }
+    feat[t] = o;
+}
+
+hipError_t launch_h16_points(hipStream_t st, const float4 *pts, uint32_t n, const H16Consts &k, void *feat) {
+    const uint32_t threads = (n + 31) / 32 * 64;
+    hipLaunchKernelGGL(k_h16_points, dim3((threads + 255) / 256), dim3(256), 0, st, pts, n, k,
+                       static_cast<half8 *>(feat));
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------ per-hypothesis rows
+// rows[(3 h + r) * 2 + half]: row r (0 ex, 1 ey, 2 zr) of hypothesis h, coefficients 8 half .. 8 half + 7.
+// fp32 throughout (the dataset's centres are fp32 numbers, its scales powers of two): a coefficient's
+// own rounding is <= 2^-21 of the sum a_k of its terms' magnitudes, the bound's sums are rounded up by
+// (1 + 2^-18) -- both far inside the fp16 terms they sit beside.
+__global__ __launch_bounds__(256) void k_h16_rows(const float *__restrict__ models, uint32_t B, H16Consts k, float thr,
+                                                  half8 *__restrict__ rows, float *__restrict__ fm) {
+    const uint32_t h = blockIdx.x * 256 + threadIdx.x;
+    if (h >= B) return;
+    HModel M;
+#pragma unroll
+    for (int c = 0; c < 9; c++) M.h[c] = models[(size_t)c * B + h];
+    const float T = 2.0f * thr;
+    stage_a_bounds(M, k.ext, T);  // trm, F, dZ of the packed stage A (fp32, rounded up)
+    const float s20 = 9.5367431640625e-07f;  // 2^-20, as stage_a_bounds
+    const float dxf = s20 * (fabsf(M.h[0]) * k.ext.x + fabsf(M.h[1]) * k.ext.y + fabsf(M.h[2]));
+    const float dyf = s20 * (fabsf(M.h[3]) * k.ext.x + fabsf(M.h[4]) * k.ext.y + fabsf(M.h[5]));
+    const float cx1 = (float)k.cx1, cy1 = (float)k.cy1, cx2 = (float)k.cx2, cy2 = (float)k.cy2;
+    const float s1 = (float)k.s1, s2 = (float)k.s2;
+    // X, Y, Z over (u, v, 1) and the magnitudes of their terms
+    float P[3][3], aP[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        const float a0 = M.h[3 * r] * cx1, a1 = M.h[3 * r + 1] * cy1;
+        P[r][0] = M.h[3 * r] * s1;
+        P[r][1] = M.h[3 * r + 1] * s1;
+        P[r][2] = (a0 + a1) + M.h[3 * r + 2];
+        aP[r][0] = fabsf(P[r][0]);
+        aP[r][1] = fabsf(P[r][1]);
+        aP[r][2] = (fabsf(a0) + fabsf(a1)) + fabsf(M.h[3 * r + 2]);
+    }
+    const float trmi = M.trm * 1.0009765625f;  // trm (1 + 2^-10)
+    float g[3][9], a[3][9];
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int c = 0; c < 9; c++) g[r][c] = a[r][c] = 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        g[0][c] = cx2 * P[2][c] - P[0][c];
+        a[0][c] = fabsf(cx2) * aP[2][c] + aP[0][c];
+        g[0][3 + c] = s2 * P[2][c];
+        a[0][3 + c] = s2 * aP[2][c];
+        g[1][c] = cy2 * P[2][c] - P[1][c];
+        a[1][c] = fabsf(cy2) * aP[2][c] + aP[1][c];
+        g[1][6 + c] = s2 * P[2][c];
+        a[1][6 + c] = s2 * aP[2][c];
+        g[2][c] = trmi * P[2][c];
+        a[2][c] = trmi * aP[2][c];
+    }
+    float mx = 0.f;
+    bool fin = isfinite(trmi) && isfinite(M.F) && isfinite(M.dZ) && isfinite(dxf) && isfinite(dyf);
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int c = 0; c < 9; c++) {
+            fin = fin && isfinite(a[r][c]);  // a >= |g|: a finite a means a finite g
+            mx = fmaxf(mx, fabsf(g[r][c]));
+        }
+    fin = fin && mx > 0x1p-100f && mx < 0x1p100f;
+    half8 out[3][2];
+    float fmv = INFINITY;
+    if (!fin) {  // no prefilter for this hypothesis: zero rows, every pair to the exact stage
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+            for (int hf = 0; hf < 2; hf++)
+#pragma unroll
+                for (int j = 0; j < 8; j++) out[r][hf][j] = (_Float16)0.0f;
+    } else {
+        const int e = -(ilogbf(mx) + 1);  // max |g| 2^e in [0.5, 1)
+        float D[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            float d = 0x1p-100f;
+#pragma unroll
+            for (int c = 0; c < 16; c++) {
+                const float gh = c < 9 ? ldexpf(g[r][c], e) : 0.f;
+                const _Float16 gt = (_Float16)gh;
+                out[r][c >> 3][c & 7] = gt;
+                if (c < 9) {
+                    const float agt = fabsf((float)gt), fk = (float)k.fmax[c];
+                    d += agt * (0x1p-10f * fk + 0x1p-25f) +
+                         fk * (0x1p-10f * fabsf(gh) + 0x1p-25f + 0x1p-21f * ldexpf(a[r][c], e)) +
+                         0x1p-19f * agt * (fk + 0x1p-24f);
+                }
+            }
+            D[r] = d * 1.00000381469726562f;  // (1 + 2^-18): the sum's own roundings
+        }
+        const float sc = ldexpf(1.0f, e);
+        const float ex_fma = k.ext.z * M.dZ + dxf, ey_fma = k.ext.w * M.dZ + dyf;
+        const float Fm = (M.F * sc + fmaxf(D[0] + ex_fma * sc, D[1] + ey_fma * sc) + trmi * M.dZ * sc + D[2]) *
+                         1.00000381469726562f;
+        fmv = isfinite(Fm) ? Fm : INFINITY;
+    }
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int hf = 0; hf < 2; hf++) rows[((size_t)h * 3 + r) * 2 + hf] = out[r][hf];
+    fm[h] = fmv;
+}
+
+hipError_t launch_h16_rows(hipStream_t st, const float *models, uint32_t B, const H16Consts &k, float thr, void *rows,
+                           float *fm) {
+    hipLaunchKernelGGL(k_h16_rows, dim3((B + 255) / 256), dim3(256), 0, st, models, B, k, thr,
+                       static_cast<half8 *>(rows), fm);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------ the scorer
+// LDS ordering inside one wave (the queue, the model table, the counters): a workgroup-scope fence
+// waits for the wave's LDS operations and keeps the compiler from moving them across
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Drain `cnt` (<= 64) queue entries from `head`: lane i evaluates entry head + i exactly (stage_b,
+// throughput mode: S ~ 2 err, or the exact 2 err inside the band) and adds its inlier to the
+// hypothesis' LDS counters (count, Σ in 2^-fxs fixed point).
+template <uint32_t Q>
+__device__ __forceinline__ void h16_drain(uint32_t cnt, uint32_t head, uint32_t *q, const float (*sh)[20],
+                                          uint32_t *sc, unsigned long long *ss, const float4 *__restrict__ pts,
+                                          float T, float thr, double fxs) {
+    const uint32_t lane = threadIdx.x & 63;
+    wave_lds_sync();
+    if (lane < cnt) {
+        const uint32_t qi = head + lane;  // head < Q
+        const uint32_t e = q[qi >= Q ? qi - Q : qi];
+        const uint32_t hk = e >> 25, p = e & 0x1FFFFFFu;
+        const float4 pt = pts[p];
+        HModel M;
+#pragma unroll
+        for (int c = 0; c < 9; c++) {
+            M.h[c] = sh[hk][c];
+            M.hi[c] = sh[hk][9 + c];
+        }
+        // the point's guard band, as k_prepare_rec writes it
+        const float mp = fabsf(pt.x) + fabsf(pt.y) + fabsf(pt.z) + fabsf(pt.w);
+        const float band = kBandMp * mp + kBandT * T;
+        int c = 0;
+        float s = 0.f;
+        stage_b<false>(M, pt.x, pt.y, pt.z, pt.w, band, T, thr, c, s);
+        if (c) {
+            atomicAdd(&sc[hk], 1u);
+            atomicAdd(&ss[hk], (unsigned long long)llrint((double)s * fxs));
+        }
+    }
+    wave_lds_sync();
+}
+
+// Workgroup = 4 waves; wave w owns hypotheses [hb, hb + 10 NA) and point chunk blockIdx.y.
+// A fragments (lane l: row l & 31 of each 32-row tile, coefficients 8 (l >> 5) ..): row rho holds
+// (hypothesis t, component r) with i = (rho & 3) + 4 (rho >> 3), t = 5 ((rho >> 2) & 1) + i / 3, r = i % 3
+// (i < 15; row i = 15 of each lane half is spare), so that the D register q of lane half hf holds
+// (hypothesis 5 hf + q / 3, component q % 3): each lane owns whole (ex, ey, zr) triples of five
+// hypotheses of each tile for its point.
+template <int NA, int U, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_score_h16(const half8 *__restrict__ feat, const float4 *__restrict__ pts,
+                                                   uint32_t n, const half8 *__restrict__ rows,
+                                                   const float *__restrict__ fm, const float *__restrict__ models,
+                                                   uint32_t B, float thr, double fxs, uint32_t *__restrict__ cpart,
+                                                   unsigned long long *__restrict__ spart) {
+    constexpr int HW = 10 * NA;
+    __shared__ float sH[4][HW][20];
+    __shared__ uint32_t sC[4][HW];
+    __shared__ unsigned long long sS[4][HW];
+    constexpr uint32_t Q = h16_queue<NA, U>();
+    __shared__ uint32_t sQ[4][Q];
+    const uint32_t lane = threadIdx.x & 63, hf = lane >> 5;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t hb = (blockIdx.x * 4 + wave) * HW;
+    const float T = 2.0f * thr;
+    if (lane < HW) {
+        const uint32_t h = hb + lane;
+#pragma unroll
+        for (int c = 0; c < 18; c++) sH[wave][lane][c] = h < B ? models[(size_t)c * B + h] : 0.f;
+        sC[wave][lane] = 0;
+        sS[wave][lane] = 0;
+    }
+    half8 A[NA];
+    float F[NA][5];
+    {
+        const uint32_t rho = lane & 31, rh = (rho >> 2) & 1, i = (rho & 3) + 4 * (rho >> 3);
+        const uint32_t t = 5 * rh + i / 3, r = i % 3;
+#pragma unroll
+        for (int a = 0; a < NA; a++) {
+            const uint32_t h = hb + 10 * a + t;
+            half8 z;
+#pragma unroll
+            for (int j = 0; j < 8; j++) z[j] = (_Float16)0.0f;
+            A[a] = (i < 15 && h < B) ? rows[((size_t)h * 3 + r) * 2 + hf] : z;
+#pragma unroll
+            for (int j = 0; j < 5; j++) {
+                const uint32_t hj = hb + 10 * a + 5 * hf + j;
+                F[a][j] = hj < B ? fm[hj] : -1.0f;  // a missing hypothesis keeps nothing (0 <= -1 is false)
+            }
+        }
+    }
+    const uint32_t nblk = (n + 31) / 32, nch = gridDim.y, ch = blockIdx.y;
+    const uint32_t per = (nblk + nch - 1) / nch;
+    const uint32_t b0 = ch * per < nblk ? ch * per : nblk, b1 = b0 + per < nblk ? b0 + per : nblk;
+    uint32_t qn = 0, qh = 0;
+    const f32x16 zero = {};
+    wave_lds_sync();
+    // U 32-point blocks per iteration (their MFMAs issue back to back, then all the tests), the next
+    // iteration's blocks' features loaded while this iteration's tiles are tested
+    half8 bn[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) bn[u] = b0 + u < b1 ? feat[(size_t)(b0 + u) * 64 + lane] : half8{};
+    for (uint32_t blk = b0; blk < b1; blk += U) {
+        half8 bf[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            bf[u] = bn[u];
+            if (blk + U + u < b1) bn[u] = feat[(size_t)(blk + U + u) * 64 + lane];
+        }
+        f32x16 acc[U][NA];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int a = 0; a < NA; a++) acc[u][a] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[a], bf[u], zero, 0, 0, 0);
+        uint64_t msk[U][NA][5], any = 0;
+#pragma unroll
+        for (int u = 0; u < U; u++)
+#pragma unroll
+            for (int a = 0; a < NA; a++)
+#pragma unroll
+                for (int j = 0; j < 5; j++) {
+                    // keep iff |ex| <= R and |ey| <= R, R = |zr| + F: two compares with |.| source
+                    // modifiers (a max would first canonicalise both operands in IEEE mode); a block
+                    // past the chunk's end keeps nothing
+                    const float R = fabsf(acc[u][a][3 * j + 2]) + F[a][j];
+                    msk[u][a][j] = blk + u < b1 ? __builtin_amdgcn_ballot_w64(fabsf(acc[u][a][3 * j]) <= R) &
+                                                      __builtin_amdgcn_ballot_w64(fabsf(acc[u][a][3 * j + 1]) <= R)
+                                                : 0;
+                    any |= msk[u][a][j];
+                }
+        if (__builtin_expect(any != 0, 0)) {  // append the kept pairs, draining full groups of 64 per block
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint32_t point = (blk + u) * 32 + (lane & 31);
+#pragma unroll
+                for (int a = 0; a < NA; a++)
+#pragma unroll
+                    for (int j = 0; j < 5; j++) {
+                        const uint64_t mk = msk[u][a][j];
+                        if (mk) {
+                            const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+                                (uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+                            if ((mk >> lane) & 1) {
+                                const uint32_t qi = qh + qn + below;  // < 2 Q
+                                sQ[wave][qi >= Q ? qi - Q : qi] = ((uint32_t)(10 * a + 5 * hf + j) << 25) | point;
+                            }
+                            qn += (uint32_t)__builtin_popcountll(mk);
+                        }
+                    }
+                while (qn >= 64) {
+                    h16_drain<Q>(64, qh, sQ[wave], sH[wave], sC[wave], sS[wave], pts, T, thr, fxs);
+                    qh = qh + 64 >= Q ? qh + 64 - Q : qh + 64;
+                    qn -= 64;
+                }
+            }
+        }
+    }
+    while (qn) {
+        const uint32_t d = qn < 64 ? qn : 64;
+        h16_drain<Q>(d, qh, sQ[wave], sH[wave], sC[wave], sS[wave], pts, T, thr, fxs);
+        qh = qh + d >= Q ? qh + d - Q : qh + d;
+        qn -= d;
+    }
+    wave_lds_sync();
+    if (lane < HW && hb + lane < B) {
+        cpart[(size_t)ch * B + hb + lane] = sC[wave][lane];
+        spart[(size_t)ch * B + hb + lane] = sS[wave][lane];
+    }
+}
+
+// counts / sums from the chunk partials (integers: any order gives the same result)
+__global__ __launch_bounds__(256) void k_h16_finish(const uint32_t *__restrict__ cpart,
+                                                    const unsigned long long *__restrict__ spart, uint32_t B,
+                                                    uint32_t nch, double inv_fxs, int32_t *__restrict__ counts,
+                                                    float *__restrict__ sums) {
+    const uint32_t h = blockIdx.x * 256 + threadIdx.x;
+    if (h >= B) return;
+    uint32_t c = 0;
+    unsigned long long s = 0;
+    for (uint32_t y = 0; y < nch; y++) {
+        c += cpart[(size_t)y * B + h];
+        s += spart[(size_t)y * B + h];
+    }
+    counts[h] = (int32_t)c;
+    sums[h] = (float)((double)s * inv_fxs * 0.5);  // stage B adds S ~ 2 err (k_score_hf halves at the end)
+}
+
+size_t h16_part_bytes(uint32_t B, int chunks) { return (size_t)chunks * B * (sizeof(uint32_t) + sizeof(uint64_t)); }
+
+hipError_t launch_score_h16(hipStream_t st, const void *feat, const float4 *pts, uint32_t n, const void *rows,
+                            const float *fm, const float *models, uint32_t B, float thr, int chunks, void *part,
+                            int32_t *counts, float *sums) {
+    static const int na = getenv("USAC_H16_NA") ? atoi(getenv("USAC_H16_NA")) : 2;  // 10-hypothesis tiles per wave
+    if (chunks < 1 || n == 0 || n > 0x2000000u) return hipErrorInvalidValue;  // 25-bit point indices in the queue
+    // Σ in fixed point: a stage-B term is < 2 T (1 + 2^-15) (S ~ 2 err of an inlier, err < thr = T / 2), so
+    // 2^fx with 2 T 2^fx <= 2^40 leaves 2^23 terms per hypothesis and chunk below 2^63
+    const double T = 2.0 * (double)thr;
+    const int fx = T > 0 ? 39 - ilogb(T) : 40;
+    const double fxs = ldexp(1.0, fx);
+    unsigned long long *sp = static_cast<unsigned long long *>(part);  // 8-byte words first (alignment)
+    uint32_t *cp = reinterpret_cast<uint32_t *>(sp + (size_t)chunks * B);
+    static const int uu = getenv("USAC_H16_U") ? atoi(getenv("USAC_H16_U")) : 1;  // blocks per iteration
+    // min waves per SIMD: 8 (64 VGPRs, no spills) -- same-box cfg2 559-570 vs 551-555 M hyp/s at 7
+    static const int wpe = getenv("USAC_H16_WPE") ? atoi(getenv("USAC_H16_WPE")) : 8;
+#define H16(NA_, U_, W_)                                                                                            \
+    hipLaunchKernelGGL((k_score_h16<NA_, U_, W_>), dim3((B + 40 * NA_ - 1) / (40 * NA_), chunks), dim3(256), 0, st,   \
+                       static_cast<const half8 *>(feat), pts, n, static_cast<const half8 *>(rows), fm, models, B, thr, \
+                       fxs, cp, sp)
+    if (na == 4)
+        H16(4, 1, 1);
+    else if (uu == 2)
+        H16(2, 2, 1);
+    else if (wpe == 8)
+        H16(2, 1, 8);
+    else
+        H16(2, 1, 1);
+#undef H16
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_h16_finish, dim3((B + 255) / 256), dim3(256), 0, st, cp, sp, B, (uint32_t)chunks,
+                       ldexp(1.0, -fx), counts, sums);
+    return hipGetLastError();
+}
+
+}  // namespace usac

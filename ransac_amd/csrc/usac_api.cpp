@@ -274,7 +274,9 @@ struct usac_ctx {
     uint32_t n = 0, cols = 0, m = 0;
     int dlt_mode = USAC_DLT_THIN;
     int chunks = 4;
-    int score_variant = 0;  // 0 = guard-band fast path (+ pre-sort), 1 = exact expression only, 2 = fast, no pre-sort
+    int score_variant = 0;  // 0 = guard-band fast path (+ pre-sort; multi-chunk H: the matrix-core prefilter),
+                            // 1 = exact expression only, 2 = fast, no pre-sort, 3 = (tests) usac_score_models
+                            // of H through the multi-chunk scorer
     hipStream_t stream = nullptr;
     DevBuf pts;
     DevBuf rec;             // fast-kernel point records (32 B / point)
@@ -287,6 +289,14 @@ struct usac_ctx {
     DevBuf hf_part;         // fast-kernel partials of a point range split over workgroups
     float rec_thr = -1.f;   // threshold the record bands were built for
     float4 ext = {0, 0, 0, 0};  // dataset box: max |x1|, |y1|, |x2|, |y2| (fast-kernel bounds)
+    // the matrix-core prefilter scorer of homographies (kernels_h16.hip): dataset constants, fp16
+    // point features (built on first use), per-batch rows / slacks and chunk partials; h16 = 1 when
+    // usable (USAC_H16=0 turns it off: the lanes-over-hypotheses k_score_hf then scores every batch)
+    usac::H16Consts h16k{};
+    int h16 = 0;
+    bool h16_feat_ok = false;
+    bool h16_off = false;  // this batch scores with k_score_hf (the loop's speculative batches)
+    DevBuf h16_feat, h16_rows, h16_fm, h16_part;
     // batch buffers
     DevBuf samples, models, counts, sums, best, hostmodels, argmax_part;
     DevBuf list, list_n;    // fundamental: occupied model slots (compacted) and their number
@@ -595,6 +605,40 @@ hipError_t enqueue_solve(usac_ctx *c, const int32_t *samples_dev, uint32_t B, ui
                                    c->models.as<float>());
 }
 
+// point chunks of the matrix-core scorer for a batch of B: ~16 waves per SIMD over the launch
+// (20 hypotheses per wave; USAC_H16_CHUNKS overrides), at most one 32-point block per chunk and 256
+uint32_t h16_chunks(const usac_ctx *c, uint32_t B) {
+    static const int na = getenv("USAC_H16_NA") && atoi(getenv("USAC_H16_NA")) == 4 ? 4 : 2;
+    const uint32_t waves = (B + 10 * na - 1) / (10 * na), nblk = (c->n + 31) / 32;
+    static const int env_ch = getenv("USAC_H16_CHUNKS") ? atoi(getenv("USAC_H16_CHUNKS")) : 0;
+    const uint32_t ch = env_ch > 0 ? (uint32_t)env_ch : (16384u + waves - 1) / waves;
+    return std::max(1u, std::min(ch, std::min(nblk, 256u)));
+}
+
+// The matrix-core prefilter scorer (kernels_h16.hip): the point features once per context, each
+// hypothesis' fp16 rows and slack per batch, then the scorer over point chunks -- enough chunks for
+// ~16 waves per SIMD over the launch (20 hypotheses per wave; USAC_H16_CHUNKS overrides).
+hipError_t enqueue_score_h16(usac_ctx *c, uint32_t B, float thr) {
+    hipError_t e;
+    if (!c->h16_feat_ok) {
+        if ((e = c->h16_feat.reserve(usac::h16_feature_bytes(c->n))) != hipSuccess) return e;
+        if ((e = usac::launch_h16_points(c->stream, c->pts.as<float4>(), c->n, c->h16k, c->h16_feat.p)) != hipSuccess)
+            return e;
+        c->h16_feat_ok = true;
+    }
+    const uint32_t ch = h16_chunks(c, B);
+    if ((e = c->h16_rows.reserve((size_t)B * 96)) != hipSuccess) return e;
+    if ((e = c->h16_fm.reserve(sizeof(float) * (size_t)B)) != hipSuccess) return e;
+    if ((e = c->h16_part.reserve(usac::h16_part_bytes(B, (int)ch))) != hipSuccess) return e;
+    if ((e = usac::launch_h16_rows(c->stream, c->models.as<float>(), B, c->h16k, thr, c->h16_rows.p,
+                                   c->h16_fm.as<float>())) != hipSuccess)
+        return e;
+    e = usac::launch_score_h16(c->stream, c->h16_feat.p, c->pts.as<float4>(), c->n, c->h16_rows.p,
+                               c->h16_fm.as<float>(), c->models.as<float>(), B, thr, (int)ch, c->h16_part.p,
+                               c->counts.as<int32_t>(), c->sums.as<float>());
+    return e;
+}
+
 // chunks == 1 is the parity configuration: per-hypothesis sums are the exact sequential
 // fp32 sums of the reference.  chunks > 1 re-associates Σerr across chunks (counts exact).
 hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
@@ -637,6 +681,8 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
         if (c->score_variant == 1)
             return usac::launch_score_h(c->stream, chunks, c->pts.as<float4>(), c->n, c->models.as<float>(), B, thr,
                                         c->counts.as<int32_t>(), c->sums.as<float>());
+        if ((c->score_variant == 0 || c->score_variant == 3) && chunks > 1 && c->h16 == 1 && !c->h16_off)  // counts exact
+            return enqueue_score_h16(c, B, thr);
         uint32_t *perm = nullptr;
         if (c->score_variant == 0) {  // 2: fast kernel without the hypothesis pre-sort (A/B)
             hipError_t e = c->perm.reserve(usac::presort_bytes(B));
@@ -1454,7 +1500,8 @@ int exact_sums(usac_ctx *c, float thr, int best_count, const int32_t *hc, const 
         for (uint32_t k = 0; k < K; k++) {
             if (cc[k] != hc[cand[k0 + k]])
                 return fail(c, USAC_ERR_HIP, "score kernel count differs from the exact recount (slot " +
-                                                 std::to_string(cand[k0 + k]) + ")");
+                                                 std::to_string(cand[k0 + k]) + ": " + std::to_string(hc[cand[k0 + k]]) +
+                                                 " vs " + std::to_string(cc[k]) + ")");
             hsum[cand[k0 + k]] = cs[k];
         }
     }
@@ -1699,6 +1746,8 @@ int usac_create(usac_ctx **out, int device, int estimator, const float *pts, uin
                     if (v > mx[k]) mx[k] = v;
                 }
             c->ext = make_float4(mx[0], mx[1], mx[2], mx[3]);
+            const char *h16env = getenv("USAC_H16");
+            c->h16 = (!h16env || atoi(h16env) != 0) && usac::h16_consts(pts, n, c->ext, &c->h16k) ? 1 : 0;
         }
         if (e != hipSuccess) { rc = fail(c, USAC_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e)); break; }
     } while (0);
@@ -1741,6 +1790,7 @@ void usac_destroy(usac_ctx *c) {
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->h4_fb, &c->h4_fb_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
                       &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->sprt_starts, &c->inl_scratch, &c->e5_ws, &c->one_model,
+                      &c->h16_feat, &c->h16_rows, &c->h16_fm, &c->h16_part,
                       &c->inl_idx, &c->pol_lists, &c->pol_res, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq, &c->nm_w, &c->nm_qw, &c->lo_io,
                       &c->rec_send, &c->rec_all, &c->tv_part, &c->hf_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
@@ -1772,7 +1822,7 @@ int usac_set_score_chunks(usac_ctx *c, int chunks) {
 }
 
 int usac_set_score_variant(usac_ctx *c, int variant) {
-    if (!c || variant < 0 || variant > 2) return USAC_ERR_ARG;
+    if (!c || variant < 0 || variant > 3) return USAC_ERR_ARG;
     c->score_variant = variant;
     return USAC_OK;
 }
@@ -1847,7 +1897,8 @@ int usac_score_models(usac_ctx *c, const float *models, uint32_t nm, float thr, 
             HIP_TRY(c, usac::launch_prepare_h(c->stream, c->hostmodels.as<float>(), nm, c->models.as<float>()));
         else
             HIP_TRY(c, usac::launch_prepare_line(c->stream, c->hostmodels.as<float>(), nm, c->models.as<float>()));
-        HIP_TRY(c, enqueue_score(c, nm, thr, 1));
+        // variant 3 (tests): the throughput scorer on the given models -- counts exact, Σ within its bound
+        HIP_TRY(c, enqueue_score(c, nm, thr, c->score_variant == 3 ? std::max(c->chunks, 2) : 1));
     }
     HIP_TRY(c, hipMemcpyAsync(counts, c->counts.p, sizeof(int32_t) * nm, hipMemcpyDeviceToHost, c->stream));
     if (sums) HIP_TRY(c, hipMemcpyAsync(sums, c->sums.p, sizeof(float) * nm, hipMemcpyDeviceToHost, c->stream));
@@ -2324,6 +2375,16 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                            uint32_t rec_cap) {
     if (!c || !prm || !out || nranks < 1 || rank < 0 || rank >= nranks) return USAC_ERR_ARG;
     memset(out, 0, sizeof(*out));
+    // The loop scores with k_score_hf, never the matrix-core scorer: its batches are small (the
+    // ramp; h16's per-batch rows + finish launches cost more than they save: cfg5 3.30 ms per run
+    // with k_score_hf, 3.8-3.9 with h16), and its speculative batch runs beside the main stream's
+    // recount / LO kernels, where h16 was seen to corrupt a concurrent recount.
+    struct H16Off {
+        usac_ctx *c;
+        bool saved;
+        ~H16Off() { c->h16_off = saved; }
+    } h16_off{c, c->h16_off};
+    c->h16_off = true;
     if (nranks > 1 && !gather && (!c->comm || c->nranks != nranks || c->rank != rank))
         return fail(c, USAC_ERR_ARG, "sharded run without a gather callback needs usac_comm_init(nranks, rank)");
     const bool prosac = prm->sampler == USAC_SAMPLER_PROSAC;

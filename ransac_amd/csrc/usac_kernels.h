@@ -67,6 +67,31 @@ hipError_t launch_score_hf(hipStream_t st, int chunks, bool exact_sum, const flo
                            const float *models, uint32_t B, float thr, uint32_t *perm, int32_t *counts, float *sums,
                            uint32_t ysplit = 1, void *yscratch = nullptr);
 
+// Matrix-core prefilter scorer of homographies (kernels_h16.hip, DESIGN.md §6 "h16"): the dataset
+// constants -- every coordinate centred and scaled by a power of two, x1 = cx1 + s1 u, y1 = cy1 + s1 v,
+// x2 = cx2 + s2 p, y2 = cy2 + s2 q -- and fmax[k] >= |f_k| over the finite points for the nine features
+// f = (u, v, 1, p u, p v, p, q u, q v, q); ext = the dataset box of k_score_hf (its stage-A bounds).
+struct H16Consts {
+    double cx1, cy1, s1, cx2, cy2, s2;
+    double fmax[9];
+    float4 ext;
+};
+// host: the constants of n float4 points (false: no finite point)
+bool h16_consts(const float *pts, uint32_t n, float4 ext, H16Consts *out);
+// fp16 point features in the MFMA B-operand layout, 1 KB per 32 points (h16_feature_bytes(n));
+// points past n and non-finite points get NaN features (never kept)
+size_t h16_feature_bytes(uint32_t n);
+hipError_t launch_h16_points(hipStream_t st, const float4 *pts, uint32_t n, const H16Consts &k, void *feat);
+// per batch: each hypothesis' three fp16 rows (96 B) and its prefilter slack (rows: B x 96 B, fm: B floats)
+hipError_t launch_h16_rows(hipStream_t st, const float *models, uint32_t B, const H16Consts &k, float thr,
+                           void *rows, float *fm);
+// the scorer: counts / sums of B hypotheses (exact counts; Σ from fixed-point stage-B terms) over
+// `chunks` point chunks; part = h16_part_bytes(B, chunks) scratch
+size_t h16_part_bytes(uint32_t B, int chunks);
+hipError_t launch_score_h16(hipStream_t st, const void *feat, const float4 *pts, uint32_t n, const void *rows,
+                            const float *fm, const float *models, uint32_t B, float thr, int chunks, void *part,
+                            int32_t *counts, float *sums);
+
 hipError_t launch_solve_line(hipStream_t st, const float2 *pts, uint32_t n, const int32_t *samples_in,
                              int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, float *models);
 hipError_t launch_prepare_line(hipStream_t st, const float *in, uint32_t B, float *models);

@@ -12,8 +12,9 @@ cost in SIMD cycles, two ways:
             v_fma_f64 (4.7) take about twice that; v_rcp_f32 8.2, v_rcp_f64 16.3.
 
 The hot loop = the innermost backward-branching block range holding the most instructions of
-the chosen kind (default: the one with the most v_pk_fma_f32).
-  python3 tools/isa_mix.py <file.s> <mangled-name-substring> [json-out]
+the chosen kind (default: the one with the most v_pk_fma_f32; KIND=v_mfma for the matrix-core
+scorer).  MFMA instructions are counted apart (mix "mfma"), not as VALU issue.
+  [KIND=<opcode prefix>] python3 tools/isa_mix.py <file.s> <mangled-name-substring> [json-out]
 """
 import json
 import os
@@ -45,6 +46,8 @@ def function_body(lines, name):
 
 def classify(ins):
     op = ins.split()[0]
+    if op.startswith("v_mfma"):
+        return "mfma"
     if op.startswith("v_pk_"):
         return "valu_packed"
     if op.startswith(TRANS):
@@ -125,7 +128,7 @@ def main():
     best = None
     for lab, a, b in loops(body):
         seg = body[a:b + 1]
-        npk = sum(1 for ln in seg if ln.strip().startswith("v_pk_fma_f32"))
+        npk = sum(1 for ln in seg if ln.strip().startswith(os.environ.get("KIND", "v_pk_fma_f32")))
         if best is None or npk > best[0] or (npk == best[0] and b - a < best[2] - best[1]):
             best = (npk, a, b, lab)
     _, a, b, lab = best

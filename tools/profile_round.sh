@@ -30,6 +30,9 @@ for w in $WORKLOADS; do
   rc=$?; echo "== $w trace rc=$rc"; [ $rc -eq 0 ] || { tail -5 $D/trace.err; exit $rc; }
   PASSES=(FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
           "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVES")
+  if [ $w = h10k ] || [ $w = h100k ]; then  # the matrix-core scorer (kernels_h16.hip): MFMA busy, LDS / SALU issue
+    PASSES+=("SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE")
+  fi
   if [ $w = h10k ]; then
     PASSES+=("SQC_DCACHE_REQ SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_DCACHE_MISSES_DUPLICATE"
              "SQ_INSTS_SMEM SQ_INST_LEVEL_SMEM SQ_INST_CYCLES_SMEM SQ_INSTS_SALU SQ_WAVE_CYCLES")
