@@ -51,50 +51,116 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 template <int NA, int U>
 constexpr uint32_t h16_queue() { return 64u * 5u * NA * U + 64u; }
 
-// ------------------------------------------------------------------------ dataset constants (host)
-bool h16_consts(const float *pts, uint32_t n, float4 ext, H16Consts *o) {
-    double lo[4] = {INFINITY, INFINITY, INFINITY, INFINITY}, hi[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-    uint32_t nf = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        const float *p = pts + 4 * (size_t)i;
-        if (!(std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2]) && std::isfinite(p[3]))) continue;
-        nf++;
+// ------------------------------------------------------------------------ dataset constants
+// One workgroup (once per context, at its first h16 batch; no host pass over the points): the
+// box of the finite points, centres = the box midpoints rounded to fp32 (k_h16_rows works in
+// fp32 and must use the very centres the features used), scales = the smallest powers of two
+// >= the half-extents (every centred coordinate in [-1, 1]), then fmax[k] >= |f_k| over the
+// finite points for the nine features in fp64 -- rounded up to a float above fmax (1 + 2^-40):
+// k_h16_rows reads fmax as floats and the features' own fp64 evaluation may round up.
+constexpr int kConstThreads = 1024;
+
+__device__ __forceinline__ double h16_pow2_at_least(double v) { return v > 0 ? ldexp(1.0, ilogb(v) + 1) : 1.0; }
+
+__global__ __launch_bounds__(kConstThreads) void k_h16_consts(const float4 *__restrict__ pts, uint32_t n, float4 ext,
+                                                              H16Consts *__restrict__ out) {
+    __shared__ double red[kConstThreads / 64][9];
+    __shared__ double sc[6];
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    // pass 1: min / max of the four coordinates over the finite points (max of -x for the min)
+    double m[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) m[k] = -INFINITY;
+    for (uint32_t i = t; i < n; i += kConstThreads) {
+        const float4 p = pts[i];
+        if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z) && isfinite(p.w))) continue;
+        const double c[4] = {p.x, p.y, p.z, p.w};
+#pragma unroll
         for (int k = 0; k < 4; k++) {
-            lo[k] = std::min(lo[k], (double)p[k]);
-            hi[k] = std::max(hi[k], (double)p[k]);
+            m[k] = fmax(m[k], c[k]);
+            m[4 + k] = fmax(m[4 + k], -c[k]);
         }
     }
-    if (!nf) return false;
-    // centres: midpoints of the box (exact in fp64); scales: the smallest powers of two >= the
-    // half-extents, so every centred coordinate lies in [-1, 1]
-    auto pow2_at_least = [](double v) { return v > 0 ? std::ldexp(1.0, std::ilogb(v) + 1) : 1.0; };
-    // (fp32 numbers: k_h16_rows works in fp32 and must use the very centres the features used)
-    o->cx1 = (float)(0.5 * (lo[0] + hi[0]));
-    o->cy1 = (float)(0.5 * (lo[1] + hi[1]));
-    o->cx2 = (float)(0.5 * (lo[2] + hi[2]));
-    o->cy2 = (float)(0.5 * (lo[3] + hi[3]));
-    o->s1 = pow2_at_least(std::max(std::max(hi[0] - o->cx1, o->cx1 - lo[0]), std::max(hi[1] - o->cy1, o->cy1 - lo[1])));
-    o->s2 = pow2_at_least(std::max(std::max(hi[2] - o->cx2, o->cx2 - lo[2]), std::max(hi[3] - o->cy2, o->cy2 - lo[3])));
-    for (int k = 0; k < 9; k++) o->fmax[k] = 0.0;
-    for (uint32_t i = 0; i < n; i++) {
-        const float *p = pts + 4 * (size_t)i;
-        if (!(std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2]) && std::isfinite(p[3]))) continue;
-        const double u = (p[0] - o->cx1) / o->s1, v = (p[1] - o->cy1) / o->s1;
-        const double pp = (p[2] - o->cx2) / o->s2, q = (p[3] - o->cy2) / o->s2;
-        const double f[9] = {u, v, 1.0, pp * u, pp * v, pp, q * u, q * v, q};
-        for (int k = 0; k < 9; k++) o->fmax[k] = std::max(o->fmax[k], std::fabs(f[k]));
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m[k] = fmax(m[k], __shfl_xor(m[k], o));
+        if (lane == 0) red[w][k] = m[k];
     }
-    for (int k = 0; k < 9; k++)  // the device's fp64 features may round up; k_h16_rows reads fmax as floats
-        o->fmax[k] = (double)std::nextafter((float)(o->fmax[k] * (1.0 + 0x1p-40)), INFINITY);
-    o->ext = ext;
-    return true;
+    __syncthreads();
+    if (t == 0) {
+        double hi[4], lo[4];
+        for (int k = 0; k < 4; k++) {
+            hi[k] = lo[k] = -INFINITY;
+            for (int v = 0; v < kConstThreads / 64; v++) {
+                hi[k] = fmax(hi[k], red[v][k]);
+                lo[k] = fmax(lo[k], red[v][4 + k]);
+            }
+            lo[k] = -lo[k];
+        }
+        const bool any = hi[0] >= lo[0];  // a finite point exists
+        double cc[4];
+        for (int k = 0; k < 4; k++) cc[k] = any ? (double)(float)(0.5 * (lo[k] + hi[k])) : 0.0;
+        const double e1 = fmax(fmax(hi[0] - cc[0], cc[0] - lo[0]), fmax(hi[1] - cc[1], cc[1] - lo[1]));
+        const double e2 = fmax(fmax(hi[2] - cc[2], cc[2] - lo[2]), fmax(hi[3] - cc[3], cc[3] - lo[3]));
+        sc[0] = cc[0];
+        sc[1] = cc[1];
+        sc[2] = any ? h16_pow2_at_least(e1) : 1.0;
+        sc[3] = cc[2];
+        sc[4] = cc[3];
+        sc[5] = any ? h16_pow2_at_least(e2) : 1.0;
+    }
+    __syncthreads();
+    const double cx1 = sc[0], cy1 = sc[1], s1 = sc[2], cx2 = sc[3], cy2 = sc[4], s2 = sc[5];
+    // pass 2: max |f_k| (the same fp64 expressions as k_h16_points)
+    double f[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) f[k] = 0.0;
+    for (uint32_t i = t; i < n; i += kConstThreads) {
+        const float4 p = pts[i];
+        if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z) && isfinite(p.w))) continue;
+        const double u = ((double)p.x - cx1) / s1, v = ((double)p.y - cy1) / s1;
+        const double pp = ((double)p.z - cx2) / s2, q = ((double)p.w - cy2) / s2;
+        const double g[9] = {u, v, 1.0, pp * u, pp * v, pp, q * u, q * v, q};
+#pragma unroll
+        for (int k = 0; k < 9; k++) f[k] = fmax(f[k], fabs(g[k]));
+    }
+    __syncthreads();  // red[] is reused
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) f[k] = fmax(f[k], __shfl_xor(f[k], o));
+        if (lane == 0) red[w][k] = f[k];
+    }
+    __syncthreads();
+    if (t == 0) {
+        H16Consts k;
+        k.cx1 = cx1;
+        k.cy1 = cy1;
+        k.s1 = s1;
+        k.cx2 = cx2;
+        k.cy2 = cy2;
+        k.s2 = s2;
+        for (int q = 0; q < 9; q++) {
+            double mx = 0.0;
+            for (int v = 0; v < kConstThreads / 64; v++) mx = fmax(mx, red[v][q]);
+            k.fmax[q] = (double)nextafterf((float)(mx * (1.0 + 0x1p-40)), INFINITY);
+        }
+        k.ext = ext;
+        *out = k;
+    }
+}
+
+hipError_t launch_h16_consts(hipStream_t st, const float4 *pts, uint32_t n, float4 ext, H16Consts *out) {
+    hipLaunchKernelGGL(k_h16_consts, dim3(1), dim3(kConstThreads), 0, st, pts, n, ext, out);
+    return hipGetLastError();
 }
 
 size_t h16_feature_bytes(uint32_t n) { return (size_t)((n + 31) / 32) * 1024; }
 
 // one thread per (32-point block, lane): lane l holds B[k = 8 (l >> 5) + j][column l & 31]
-__global__ __launch_bounds__(256) void k_h16_points(const float4 *__restrict__ pts, uint32_t n, H16Consts k,
-                                                    half8 *__restrict__ feat) {
+__global__ __launch_bounds__(256) void k_h16_points(const float4 *__restrict__ pts, uint32_t n,
+                                                    const H16Consts *__restrict__ kc, half8 *__restrict__ feat) {
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
     const uint32_t nblk = (n + 31) / 32;
     if (t >= nblk * 64) return;
@@ -110,8 +176,8 @@ __global__ __launch_bounds__(256) void k_h16_points(const float4 *__restrict__ p
 #pragma unroll
         for (int j = 0; j < 8; j++) o[j] = (_Float16)__builtin_nanf("");
     } else {
-        const double u = ((double)p.x - k.cx1) / k.s1, v = ((double)p.y - k.cy1) / k.s1;
-        const double pp = ((double)p.z - k.cx2) / k.s2, q = ((double)p.w - k.cy2) / k.s2;
+        const double u = ((double)p.x - kc->cx1) / kc->s1, v = ((double)p.y - kc->cy1) / kc->s1;
+        const double pp = ((double)p.z - kc->cx2) / kc->s2, q = ((double)p.w - kc->cy2) / kc->s2;
         const double f[16] = {u, v, 1.0, pp * u, pp * v, pp, q * u, q * v, q, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
         for (int j = 0; j < 8; j++) o[j] = (_Float16)(float)f[8 * hf + j];
@@ -119,7 +185,7 @@ __global__ __launch_bounds__(256) void k_h16_points(const float4 *__restrict__ p
     feat[t] = o;
 }
 
-hipError_t launch_h16_points(hipStream_t st, const float4 *pts, uint32_t n, const H16Consts &k, void *feat) {
+hipError_t launch_h16_points(hipStream_t st, const float4 *pts, uint32_t n, const H16Consts *k, void *feat) {
     const uint32_t threads = (n + 31) / 32 * 64;
     hipLaunchKernelGGL(k_h16_points, dim3((threads + 255) / 256), dim3(256), 0, st, pts, n, k,
                        static_cast<half8 *>(feat));
@@ -131,20 +197,22 @@ hipError_t launch_h16_points(hipStream_t st, const float4 *pts, uint32_t n, cons
 // fp32 throughout (the dataset's centres are fp32 numbers, its scales powers of two): a coefficient's
 // own rounding is <= 2^-21 of the sum a_k of its terms' magnitudes, the bound's sums are rounded up by
 // (1 + 2^-18) -- both far inside the fp16 terms they sit beside.
-__global__ __launch_bounds__(256) void k_h16_rows(const float *__restrict__ models, uint32_t B, H16Consts k, float thr,
+__global__ __launch_bounds__(256) void k_h16_rows(const float *__restrict__ models, uint32_t B,
+                                                  const H16Consts *__restrict__ kc, float thr,
                                                   half8 *__restrict__ rows, float *__restrict__ fm) {
     const uint32_t h = blockIdx.x * 256 + threadIdx.x;
     if (h >= B) return;
+    const float4 ext = kc->ext;
     HModel M;
 #pragma unroll
     for (int c = 0; c < 9; c++) M.h[c] = models[(size_t)c * B + h];
     const float T = 2.0f * thr;
-    stage_a_bounds(M, k.ext, T);  // trm, F, dZ of the packed stage A (fp32, rounded up)
+    stage_a_bounds(M, ext, T);  // trm, F, dZ of the packed stage A (fp32, rounded up)
     const float s20 = 9.5367431640625e-07f;  // 2^-20, as stage_a_bounds
-    const float dxf = s20 * (fabsf(M.h[0]) * k.ext.x + fabsf(M.h[1]) * k.ext.y + fabsf(M.h[2]));
-    const float dyf = s20 * (fabsf(M.h[3]) * k.ext.x + fabsf(M.h[4]) * k.ext.y + fabsf(M.h[5]));
-    const float cx1 = (float)k.cx1, cy1 = (float)k.cy1, cx2 = (float)k.cx2, cy2 = (float)k.cy2;
-    const float s1 = (float)k.s1, s2 = (float)k.s2;
+    const float dxf = s20 * (fabsf(M.h[0]) * ext.x + fabsf(M.h[1]) * ext.y + fabsf(M.h[2]));
+    const float dyf = s20 * (fabsf(M.h[3]) * ext.x + fabsf(M.h[4]) * ext.y + fabsf(M.h[5]));
+    const float cx1 = (float)kc->cx1, cy1 = (float)kc->cy1, cx2 = (float)kc->cx2, cy2 = (float)kc->cy2;
+    const float s1 = (float)kc->s1, s2 = (float)kc->s2;
     // X, Y, Z over (u, v, 1) and the magnitudes of their terms
     float P[3][3], aP[3][3];
 #pragma unroll
@@ -207,7 +275,7 @@ __global__ __launch_bounds__(256) void k_h16_rows(const float *__restrict__ mode
                 const _Float16 gt = (_Float16)gh;
                 out[r][c >> 3][c & 7] = gt;
                 if (c < 9) {
-                    const float agt = fabsf((float)gt), fk = (float)k.fmax[c];
+                    const float agt = fabsf((float)gt), fk = (float)kc->fmax[c];
                     d += agt * (0x1p-10f * fk + 0x1p-25f) +
                          fk * (0x1p-10f * fabsf(gh) + 0x1p-25f + 0x1p-21f * ldexpf(a[r][c], e)) +
                          0x1p-19f * agt * (fk + 0x1p-24f);
@@ -216,7 +284,7 @@ __global__ __launch_bounds__(256) void k_h16_rows(const float *__restrict__ mode
             D[r] = d * 1.00000381469726562f;  // (1 + 2^-18): the sum's own roundings
         }
         const float sc = ldexpf(1.0f, e);
-        const float ex_fma = k.ext.z * M.dZ + dxf, ey_fma = k.ext.w * M.dZ + dyf;
+        const float ex_fma = ext.z * M.dZ + dxf, ey_fma = ext.w * M.dZ + dyf;
         const float Fm = (M.F * sc + fmaxf(D[0] + ex_fma * sc, D[1] + ey_fma * sc) + trmi * M.dZ * sc + D[2]) *
                          1.00000381469726562f;
         fmv = isfinite(Fm) ? Fm : INFINITY;
@@ -228,7 +296,7 @@ __global__ __launch_bounds__(256) void k_h16_rows(const float *__restrict__ mode
     fm[h] = fmv;
 }
 
-hipError_t launch_h16_rows(hipStream_t st, const float *models, uint32_t B, const H16Consts &k, float thr, void *rows,
+hipError_t launch_h16_rows(hipStream_t st, const float *models, uint32_t B, const H16Consts *k, float thr, void *rows,
                            float *fm) {
     hipLaunchKernelGGL(k_h16_rows, dim3((B + 255) / 256), dim3(256), 0, st, models, B, k, thr,
                        static_cast<half8 *>(rows), fm);

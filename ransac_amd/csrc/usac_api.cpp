@@ -292,11 +292,11 @@ struct usac_ctx {
     // the matrix-core prefilter scorer of homographies (kernels_h16.hip): dataset constants, fp16
     // point features (built on first use), per-batch rows / slacks and chunk partials; h16 = 1 when
     // usable (USAC_H16=0 turns it off: the lanes-over-hypotheses k_score_hf then scores every batch)
-    usac::H16Consts h16k{};
+
     int h16 = 0;
     bool h16_feat_ok = false;
     bool h16_off = false;  // this batch scores with k_score_hf (the loop's speculative batches)
-    DevBuf h16_feat, h16_rows, h16_fm, h16_part;
+    DevBuf h16_k, h16_feat, h16_rows, h16_fm, h16_part;  // h16_k: the dataset constants (usac::H16Consts)
     // batch buffers
     DevBuf samples, models, counts, sums, best, hostmodels, argmax_part;
     DevBuf list, list_n;    // fundamental: occupied model slots (compacted) and their number
@@ -621,8 +621,13 @@ uint32_t h16_chunks(const usac_ctx *c, uint32_t B) {
 hipError_t enqueue_score_h16(usac_ctx *c, uint32_t B, float thr) {
     hipError_t e;
     if (!c->h16_feat_ok) {
+        if ((e = c->h16_k.reserve(sizeof(usac::H16Consts))) != hipSuccess) return e;
         if ((e = c->h16_feat.reserve(usac::h16_feature_bytes(c->n))) != hipSuccess) return e;
-        if ((e = usac::launch_h16_points(c->stream, c->pts.as<float4>(), c->n, c->h16k, c->h16_feat.p)) != hipSuccess)
+        if ((e = usac::launch_h16_consts(c->stream, c->pts.as<float4>(), c->n, c->ext, c->h16_k.as<usac::H16Consts>())) !=
+            hipSuccess)
+            return e;
+        if ((e = usac::launch_h16_points(c->stream, c->pts.as<float4>(), c->n, c->h16_k.as<usac::H16Consts>(),
+                                         c->h16_feat.p)) != hipSuccess)
             return e;
         c->h16_feat_ok = true;
     }
@@ -630,7 +635,7 @@ hipError_t enqueue_score_h16(usac_ctx *c, uint32_t B, float thr) {
     if ((e = c->h16_rows.reserve((size_t)B * 96)) != hipSuccess) return e;
     if ((e = c->h16_fm.reserve(sizeof(float) * (size_t)B)) != hipSuccess) return e;
     if ((e = c->h16_part.reserve(usac::h16_part_bytes(B, (int)ch))) != hipSuccess) return e;
-    if ((e = usac::launch_h16_rows(c->stream, c->models.as<float>(), B, c->h16k, thr, c->h16_rows.p,
+    if ((e = usac::launch_h16_rows(c->stream, c->models.as<float>(), B, c->h16_k.as<usac::H16Consts>(), thr, c->h16_rows.p,
                                    c->h16_fm.as<float>())) != hipSuccess)
         return e;
     e = usac::launch_score_h16(c->stream, c->h16_feat.p, c->pts.as<float4>(), c->n, c->h16_rows.p,
@@ -1747,7 +1752,7 @@ int usac_create(usac_ctx **out, int device, int estimator, const float *pts, uin
                 }
             c->ext = make_float4(mx[0], mx[1], mx[2], mx[3]);
             const char *h16env = getenv("USAC_H16");
-            c->h16 = (!h16env || atoi(h16env) != 0) && usac::h16_consts(pts, n, c->ext, &c->h16k) ? 1 : 0;
+            c->h16 = !h16env || atoi(h16env) != 0 ? 1 : 0;
         }
         if (e != hipSuccess) { rc = fail(c, USAC_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e)); break; }
     } while (0);
@@ -1790,7 +1795,7 @@ void usac_destroy(usac_ctx *c) {
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->h4_fb, &c->h4_fb_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
                       &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->sprt_starts, &c->inl_scratch, &c->e5_ws, &c->one_model,
-                      &c->h16_feat, &c->h16_rows, &c->h16_fm, &c->h16_part,
+                      &c->h16_k, &c->h16_feat, &c->h16_rows, &c->h16_fm, &c->h16_part,
                       &c->inl_idx, &c->pol_lists, &c->pol_res, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq, &c->nm_w, &c->nm_qw, &c->lo_io,
                       &c->rec_send, &c->rec_all, &c->tv_part, &c->hf_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,

@@ -76,14 +76,15 @@ struct H16Consts {
     double fmax[9];
     float4 ext;
 };
-// host: the constants of n float4 points (false: no finite point)
-bool h16_consts(const float *pts, uint32_t n, float4 ext, H16Consts *out);
+// device (one workgroup, once per context at the first h16 batch): the constants of n float4
+// points into *out (no finite point: centres 0, scales 1, fmax 0 -- every feature is then NaN)
+hipError_t launch_h16_consts(hipStream_t st, const float4 *pts, uint32_t n, float4 ext, H16Consts *out);
 // fp16 point features in the MFMA B-operand layout, 1 KB per 32 points (h16_feature_bytes(n));
 // points past n and non-finite points get NaN features (never kept)
 size_t h16_feature_bytes(uint32_t n);
-hipError_t launch_h16_points(hipStream_t st, const float4 *pts, uint32_t n, const H16Consts &k, void *feat);
+hipError_t launch_h16_points(hipStream_t st, const float4 *pts, uint32_t n, const H16Consts *k, void *feat);
 // per batch: each hypothesis' three fp16 rows (96 B) and its prefilter slack (rows: B x 96 B, fm: B floats)
-hipError_t launch_h16_rows(hipStream_t st, const float *models, uint32_t B, const H16Consts &k, float thr,
+hipError_t launch_h16_rows(hipStream_t st, const float *models, uint32_t B, const H16Consts *k, float thr,
                            void *rows, float *fm);
 // the scorer: counts / sums of B hypotheses (exact counts; Σ from fixed-point stage-B terms) over
 // `chunks` point chunks; part = h16_part_bytes(B, chunks) scratch
