@@ -509,7 +509,9 @@ def _stage_kernels(estimator, sprt, chunks, stage):
     if est == 2:  # the matrix-core prefilter scorer (kernels_h16.hip; USAC_H16=0: k_presort_h + k_score_hf)
         if os.environ.get("USAC_H16", "1") == "0":
             return ["usac::k_presort_h(", "void usac::k_score_hf<%d, false>(" % chunks]
-        return ["usac::k_h16_rows(", "void usac::k_score_h16<2, 1, 8>(", "usac::k_h16_finish("]
+        if os.environ.get("USAC_H16_FUSE", "1") == "0":  # the rows by their own kernel, not the solver
+            return ["usac::k_h16_rows(", "void usac::k_score_h16<2, 1, 8>(", "usac::k_h16_finish("]
+        return ["void usac::k_score_h16<2, 1, 8>(", "usac::k_h16_finish("]
     return ["usac::k_prepare_rec(", "void usac::k_presort_tv<%d>(" % est, "void usac::k_score_f2<%d>(" % est,
             "usac::k_tv_combine("]
 
@@ -1174,7 +1176,7 @@ def main():
         knames = {st: _stage_kernels(args.estimator, args.sprt, args.chunks, st) for st in ("score", "solve")}
         roof = None
         if not (fund or ess) and not args.sprt and stage == "score":  # cfg2: the score kernel alone (unchanged form)
-            roof = valu_roofline(knames["score"][1], n, B, avg_score_ms)
+            roof = valu_roofline(next(k for k in knames["score"] if "k_score" in k), n, B, avg_score_ms)
             if roof is not None:
                 roof["stage"] = stage_roofline(knames["score"], n, B, avg_score_ms)
         if roof is None:

@@ -18,13 +18,15 @@
 #include <hip/hip_runtime.h>
 
 #include "usac_device.hpp"
+#include "usac_h16.hpp"
 #include "usac_hscore.hpp"
 #include "usac_kernels.h"
 
 namespace usac {
 
 // ------------------------------------------------------------------------ solve (H, 4-pt)
-__device__ __forceinline__ void store_h(float *__restrict__ models, uint32_t B, uint32_t h, const double *v) {
+__device__ __forceinline__ void store_h(float *__restrict__ models, uint32_t B, uint32_t h, const double *v,
+                                        const H16Emit &emit) {
     float H[9], Hi[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) H[k] = (float)(v[k] / v[8]);
@@ -34,6 +36,7 @@ __device__ __forceinline__ void store_h(float *__restrict__ models, uint32_t B, 
         models[(size_t)k * B + h] = H[k];
         models[(size_t)(9 + k) * B + h] = Hi[k];
     }
+    if (emit.rows) h16_rows_of(H, emit.k, emit.thr, h, static_cast<half8 *>(emit.rows), emit.fm);
 }
 
 // Thin 4-pt DLT by QR + inverse iteration (dlt4_thin_qr).  A lane whose system falls back is
@@ -43,7 +46,7 @@ __global__ __launch_bounds__(64) void k_solve_h4(const float4 *__restrict__ pts,
                                                  const int32_t *__restrict__ samples_in, int32_t *samples_out,
                                                  uint32_t B, DevSampler ds, uint64_t first_hyp,
                                                  float *__restrict__ models, uint32_t *__restrict__ fb_list,
-                                                 uint32_t *__restrict__ fb_n) {
+                                                 uint32_t *__restrict__ fb_n, H16Emit emit) {
     const uint32_t h = blockIdx.x * 64 + threadIdx.x;
     bool fb = false;
     if (h < B) {
@@ -65,7 +68,7 @@ __global__ __launch_bounds__(64) void k_solve_h4(const float4 *__restrict__ pts,
             dlt_rows(p.x, p.y, p.z, p.w, W[2 * i], W[2 * i + 1]);
         }
         double v[9];
-        if (dlt4_thin_qr(W, v)) store_h(models, B, h, v);
+        if (dlt4_thin_qr(W, v)) store_h(models, B, h, v, emit);
         else fb = true;
     }
     const uint64_t m = __ballot(fb);
@@ -87,7 +90,7 @@ __global__ __launch_bounds__(64) void k_solve_h4_jac(const float4 *__restrict__ 
                                                      const int32_t *__restrict__ samples_in, int32_t *samples_out,
                                                      uint32_t B, DevSampler ds, uint64_t first_hyp, int nullspace,
                                                      float *__restrict__ models, const uint32_t *__restrict__ fb_list,
-                                                     uint32_t *__restrict__ fb_n) {
+                                                     uint32_t *__restrict__ fb_n, H16Emit emit) {
     const uint32_t K = fb_list ? __builtin_amdgcn_readfirstlane(__atomic_load_n(fb_n, __ATOMIC_RELAXED)) : B;
     for (uint32_t base = blockIdx.x * 64; base < K; base += gridDim.x * 64) {
         const uint32_t i = base + threadIdx.x;
@@ -113,7 +116,7 @@ __global__ __launch_bounds__(64) void k_solve_h4_jac(const float4 *__restrict__ 
         row_jacobi<8>(W);
         double v[9];
         pick_vector<8>(W, nullspace, v);
-        store_h(models, B, h, v);
+        store_h(models, B, h, v, emit);
     }
     if (fb_list) {
         __syncthreads();
@@ -593,20 +596,21 @@ __global__ __launch_bounds__(256) void k_argmax_final(const BestEntry *__restric
 
 hipError_t launch_solve_h4(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
                            int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, int nullspace,
-                           float *models, uint32_t *fb_list, uint32_t *fb_n) {
+                           float *models, uint32_t *fb_list, uint32_t *fb_n, const H16Emit *emit) {
     const uint32_t blocks = (B + 63) / 64;
+    const H16Emit em = emit ? *emit : H16Emit{nullptr, 0.f, nullptr, nullptr};
     if (nullspace) {
         hipLaunchKernelGGL(k_solve_h4_jac, dim3(blocks), dim3(64), 0, st, pts, n, samples_in, samples_out, B, ds,
-                           first_hyp, 1, models, (const uint32_t *)nullptr, (uint32_t *)nullptr);
+                           first_hyp, 1, models, (const uint32_t *)nullptr, (uint32_t *)nullptr, em);
         return LAUNCH_CHECK();
     }
     if (!fb_list || !fb_n) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_solve_h4, dim3(blocks), dim3(64), 0, st, pts, n, samples_in, samples_out, B, ds, first_hyp,
-                       models, fb_list, fb_n);
+                       models, fb_list, fb_n, em);
     hipError_t e = LAUNCH_CHECK();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_solve_h4_jac, dim3(blocks < 256 ? blocks : 256), dim3(64), 0, st, pts, n, samples_in,
-                       samples_out, B, ds, first_hyp, 0, models, (const uint32_t *)fb_list, fb_n);
+                       samples_out, B, ds, first_hyp, 0, models, (const uint32_t *)fb_list, fb_n, em);
     return LAUNCH_CHECK();
 }
 

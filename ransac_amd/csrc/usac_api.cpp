@@ -295,7 +295,9 @@ struct usac_ctx {
 
     int h16 = 0;
     bool h16_feat_ok = false;
-    bool h16_off = false;  // this batch scores with k_score_hf (the loop's speculative batches)
+    bool h16_off = false;  // k_score_hf for every batch (usac_ransac_run sets it for its loop)
+    uint32_t h16_rows_for = 0;  // > 0: the solver wrote the rows of a batch of this size for h16_rows_thr
+    float h16_rows_thr = 0.f;
     DevBuf h16_k, h16_feat, h16_rows, h16_fm, h16_part;  // h16_k: the dataset constants (usac::H16Consts)
     // batch buffers
     DevBuf samples, models, counts, sums, best, hostmodels, argmax_part;
@@ -583,9 +585,14 @@ int download_grid(usac_ctx *c, int cs, std::unique_ptr<usac::GridNeighbors> &out
 }
 
 // solve (samples on device, or device RNG when samples_dev == nullptr) into c->models
+hipError_t h16_init(usac_ctx *c);
+
+// h16_thr >= 0: the batch will be scored by the matrix-core scorer (h16_scores) -- the homography
+// solvers then also write its rows and slacks (usac_h16.hpp), so enqueue_score_h16 skips k_h16_rows
 hipError_t enqueue_solve(usac_ctx *c, const int32_t *samples_dev, uint32_t B, uint64_t seed, uint64_t first_hyp,
-                         int32_t *samples_out) {
+                         int32_t *samples_out, float h16_thr = -1.f) {
     const usac::DevSampler ds = dev_sampler(c, seed);
+    c->h16_rows_for = 0;
     if (is_e(c)) {
         hipError_t e = c->e5_ws.reserve(usac::e5_workspace_bytes(B));
         if (e != hipSuccess) return e;
@@ -597,10 +604,25 @@ hipError_t enqueue_solve(usac_ctx *c, const int32_t *samples_dev, uint32_t B, ui
         return usac::launch_solve_f7(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, ds,
                                      first_hyp, c->models.as<float>(), c->counts.as<int32_t>(),
                                      c->list.as<uint32_t>(), c->list_n.as<uint32_t>());
-    if (is_h(c))
-        return usac::launch_solve_h4(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, ds,
-                                     first_hyp, c->dlt_mode == USAC_DLT_NULLSPACE, c->models.as<float>(),
-                                     c->h4_fb.as<uint32_t>(), c->h4_fb_n.as<uint32_t>());
+    if (is_h(c)) {
+        usac::H16Emit em{nullptr, 0.f, nullptr, nullptr};
+        if (h16_thr >= 0.f) {
+            hipError_t e = h16_init(c);
+            if (e == hipSuccess) e = c->h16_rows.reserve((size_t)B * 96);
+            if (e == hipSuccess) e = c->h16_fm.reserve(sizeof(float) * (size_t)B);
+            if (e != hipSuccess) return e;
+            em = usac::H16Emit{c->h16_k.as<usac::H16Consts>(), h16_thr, c->h16_rows.p, c->h16_fm.as<float>()};
+        }
+        const hipError_t e = usac::launch_solve_h4(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B,
+                                                   ds, first_hyp, c->dlt_mode == USAC_DLT_NULLSPACE,
+                                                   c->models.as<float>(), c->h4_fb.as<uint32_t>(),
+                                                   c->h4_fb_n.as<uint32_t>(), em.rows ? &em : nullptr);
+        if (e == hipSuccess && em.rows) {
+            c->h16_rows_for = B;
+            c->h16_rows_thr = h16_thr;
+        }
+        return e;
+    }
     return usac::launch_solve_line(c->stream, c->pts.as<float2>(), c->n, samples_dev, samples_out, B, ds, first_hyp,
                                    c->models.as<float>());
 }
@@ -618,26 +640,48 @@ uint32_t h16_chunks(const usac_ctx *c, uint32_t B) {
 // The matrix-core prefilter scorer (kernels_h16.hip): the point features once per context, each
 // hypothesis' fp16 rows and slack per batch, then the scorer over point chunks -- enough chunks for
 // ~16 waves per SIMD over the launch (20 hypotheses per wave; USAC_H16_CHUNKS overrides).
+// the dataset constants and the point features, once per context (on its stream)
+hipError_t h16_init(usac_ctx *c) {
+    if (c->h16_feat_ok) return hipSuccess;
+    hipError_t e;
+    if ((e = c->h16_k.reserve(sizeof(usac::H16Consts))) != hipSuccess) return e;
+    if ((e = c->h16_feat.reserve(usac::h16_feature_bytes(c->n))) != hipSuccess) return e;
+    if ((e = usac::launch_h16_consts(c->stream, c->pts.as<float4>(), c->n, c->ext, c->h16_k.as<usac::H16Consts>())) !=
+        hipSuccess)
+        return e;
+    if ((e = usac::launch_h16_points(c->stream, c->pts.as<float4>(), c->n, c->h16_k.as<usac::H16Consts>(),
+                                     c->h16_feat.p)) != hipSuccess)
+        return e;
+    c->h16_feat_ok = true;
+    return hipSuccess;
+}
+
+// will enqueue_score(c, B, thr, chunks) take the matrix-core scorer?
+bool h16_scores(const usac_ctx *c, int chunks);
+// ... and should the solver write its rows (USAC_H16_FUSE=0: k_h16_rows after the solve, A/B)
+float h16_solver_thr(const usac_ctx *c, int chunks, float thr) {
+    static const bool fuse = !getenv("USAC_H16_FUSE") || atoi(getenv("USAC_H16_FUSE")) != 0;
+    return fuse && h16_scores(c, chunks) ? thr : -1.f;
+}
+bool h16_scores(const usac_ctx *c, int chunks) {
+    return is_h(c) && !c->sprt_on && c->h16 == 1 && !c->h16_off && (c->score_variant == 0 || c->score_variant == 3) &&
+           chunks > 1;
+}
+
 hipError_t enqueue_score_h16(usac_ctx *c, uint32_t B, float thr) {
     hipError_t e;
-    if (!c->h16_feat_ok) {
-        if ((e = c->h16_k.reserve(sizeof(usac::H16Consts))) != hipSuccess) return e;
-        if ((e = c->h16_feat.reserve(usac::h16_feature_bytes(c->n))) != hipSuccess) return e;
-        if ((e = usac::launch_h16_consts(c->stream, c->pts.as<float4>(), c->n, c->ext, c->h16_k.as<usac::H16Consts>())) !=
-            hipSuccess)
-            return e;
-        if ((e = usac::launch_h16_points(c->stream, c->pts.as<float4>(), c->n, c->h16_k.as<usac::H16Consts>(),
-                                         c->h16_feat.p)) != hipSuccess)
-            return e;
-        c->h16_feat_ok = true;
-    }
+    if ((e = h16_init(c)) != hipSuccess) return e;
     const uint32_t ch = h16_chunks(c, B);
-    if ((e = c->h16_rows.reserve((size_t)B * 96)) != hipSuccess) return e;
-    if ((e = c->h16_fm.reserve(sizeof(float) * (size_t)B)) != hipSuccess) return e;
     if ((e = c->h16_part.reserve(usac::h16_part_bytes(B, (int)ch))) != hipSuccess) return e;
-    if ((e = usac::launch_h16_rows(c->stream, c->models.as<float>(), B, c->h16_k.as<usac::H16Consts>(), thr, c->h16_rows.p,
-                                   c->h16_fm.as<float>())) != hipSuccess)
-        return e;
+    const bool ready = c->h16_rows_for == B && c->h16_rows_thr == thr;  // written by the solver
+    c->h16_rows_for = 0;
+    if (!ready) {
+        if ((e = c->h16_rows.reserve((size_t)B * 96)) != hipSuccess) return e;
+        if ((e = c->h16_fm.reserve(sizeof(float) * (size_t)B)) != hipSuccess) return e;
+        if ((e = usac::launch_h16_rows(c->stream, c->models.as<float>(), B, c->h16_k.as<usac::H16Consts>(), thr,
+                                       c->h16_rows.p, c->h16_fm.as<float>())) != hipSuccess)
+            return e;
+    }
     e = usac::launch_score_h16(c->stream, c->h16_feat.p, c->pts.as<float4>(), c->n, c->h16_rows.p,
                                c->h16_fm.as<float>(), c->models.as<float>(), B, thr, (int)ch, c->h16_part.p,
                                c->counts.as<int32_t>(), c->sums.as<float>());
@@ -686,8 +730,7 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
         if (c->score_variant == 1)
             return usac::launch_score_h(c->stream, chunks, c->pts.as<float4>(), c->n, c->models.as<float>(), B, thr,
                                         c->counts.as<int32_t>(), c->sums.as<float>());
-        if ((c->score_variant == 0 || c->score_variant == 3) && chunks > 1 && c->h16 == 1 && !c->h16_off)  // counts exact
-            return enqueue_score_h16(c, B, thr);
+        if (h16_scores(c, chunks)) return enqueue_score_h16(c, B, thr);  // counts exact
         uint32_t *perm = nullptr;
         if (c->score_variant == 0) {  // 2: fast kernel without the hypothesis pre-sort (A/B)
             hipError_t e = c->perm.reserve(usac::presort_bytes(B));
@@ -1999,10 +2042,10 @@ int usac_hypothesize_score(usac_ctx *c, const int32_t *samples, uint32_t B, uint
     if (samples)
         HIP_TRY(c, hipMemcpyAsync(c->samples.p, samples, sizeof(int32_t) * (size_t)B * c->m, hipMemcpyHostToDevice,
                                   c->stream));
-    HIP_TRY(c, enqueue_solve(c, samples ? c->samples.as<int32_t>() : nullptr, B, seed, first_hyp,
-                             samples ? nullptr : c->samples.as<int32_t>()));
     // per-hypothesis outputs requested -> exact sequential sums (one chunk)
     const int chunks = (counts || sums) ? 1 : c->chunks;
+    HIP_TRY(c, enqueue_solve(c, samples ? c->samples.as<int32_t>() : nullptr, B, seed, first_hyp,
+                             samples ? nullptr : c->samples.as<int32_t>(), h16_solver_thr(c, chunks, thr)));
     HIP_TRY(c, enqueue_score(c, B, thr, chunks));
     c->batch_valid = true;
     const uint32_t S = B * c->spk;
@@ -2021,7 +2064,7 @@ int usac_hypothesize_async(usac_ctx *c, uint32_t B, uint64_t seed, uint64_t firs
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
     HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
-    HIP_TRY(c, enqueue_solve(c, nullptr, B, seed, first_hyp, nullptr));
+    HIP_TRY(c, enqueue_solve(c, nullptr, B, seed, first_hyp, nullptr, h16_solver_thr(c, c->chunks, thr)));
     HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
     HIP_TRY(c, enqueue_score(c, B, thr, c->chunks));
     c->batch_valid = true;

@@ -47,9 +47,18 @@ hipError_t launch_draw_samples(hipStream_t st, int m, uint32_t n, uint32_t B, De
 // thin mode: k_solve_h4 (QR + inverse iteration) then k_solve_h4_jac over its fall-back list
 // (fb_list: B entries; fb_n: two counters, zero before the first use, reset by the kernel);
 // nullspace mode: k_solve_h4_jac over all B (fb_list / fb_n unused)
+struct H16Consts;
+// emit (nullable): the solvers also write each hypothesis' matrix-core scorer rows and slack
+// (usac_h16.hpp h16_rows_of; rows = B x 96 B, fm = B floats) for threshold thr
+struct H16Emit {
+    const H16Consts *k;
+    float thr;
+    void *rows;
+    float *fm;
+};
 hipError_t launch_solve_h4(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
                            int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, int nullspace,
-                           float *models, uint32_t *fb_list, uint32_t *fb_n);
+                           float *models, uint32_t *fb_list, uint32_t *fb_n, const H16Emit *emit = nullptr);
 hipError_t launch_prepare_h(hipStream_t st, const float *in, uint32_t B, float *models);
 hipError_t launch_score_h(hipStream_t st, int chunks, const float4 *pts, uint32_t n, const float *models, uint32_t B,
                           float thr, int32_t *counts, float *sums);
