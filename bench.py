@@ -509,9 +509,12 @@ def _stage_kernels(estimator, sprt, chunks, stage):
     if est == 2:  # the matrix-core prefilter scorer (kernels_h16.hip; USAC_H16=0: k_presort_h + k_score_hf)
         if os.environ.get("USAC_H16", "1") == "0":
             return ["usac::k_presort_h(", "void usac::k_score_hf<%d, false>(" % chunks]
+        ks = ["void usac::k_score_h16<2, 1, 8>("]
         if os.environ.get("USAC_H16_FUSE", "1") == "0":  # the rows by their own kernel, not the solver
-            return ["usac::k_h16_rows(", "void usac::k_score_h16<2, 1, 8>(", "usac::k_h16_finish("]
-        return ["void usac::k_score_h16<2, 1, 8>(", "usac::k_h16_finish("]
+            ks = ["usac::k_h16_rows("] + ks
+        if os.environ.get("USAC_H16_DEFER", "1") == "0":  # the chunk sums by their own kernel, not the argmax
+            ks = ks + ["usac::k_h16_finish("]
+        return ks
     return ["usac::k_prepare_rec(", "void usac::k_presort_tv<%d>(" % est, "void usac::k_score_f2<%d>(" % est,
             "usac::k_tv_combine("]
 

@@ -537,19 +537,54 @@ __device__ __forceinline__ void tree_best(BestEntry *sh, uint32_t t, uint32_t wi
     }
 }
 
-__global__ __launch_bounds__(256) void k_argmax_part(const int32_t *__restrict__ counts,
-                                                     const float *__restrict__ sums, uint32_t B,
-                                                     BestEntry *__restrict__ part) {
+// H16: counts / sums first from the matrix-core scorer's chunk partials (cpart u32, spart u64 fixed
+// point, chunk-major), added in chunk order and written out exactly as k_h16_finish does
+template <bool H16>
+__global__ __launch_bounds__(256) void k_argmax_part(const int32_t *__restrict__ counts_in,
+                                                     const float *__restrict__ sums_in, uint32_t B,
+                                                     BestEntry *__restrict__ part, const uint32_t *__restrict__ cpart,
+                                                     const unsigned long long *__restrict__ spart, uint32_t nch,
+                                                     double inv_fxs, int32_t *__restrict__ counts_out,
+                                                     float *__restrict__ sums_out) {
     __shared__ BestEntry sh[256];
     const uint32_t t = threadIdx.x;
     const uint32_t base = blockIdx.x * 2048 + t;
     int c[8];
     float s[8];
+    if constexpr (H16) {
+        uint32_t cc[8];
+        unsigned long long ss[8];
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-        const uint32_t i = base + 256 * j;
-        c[j] = i < B ? counts[i] : -1;
-        s[j] = i < B ? sums[i] : 0.f;
+        for (int j = 0; j < 8; j++) {
+            cc[j] = 0;
+            ss[j] = 0;
+        }
+        for (uint32_t y = 0; y < nch; y++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint32_t i = base + 256 * j;
+                if (i < B) {
+                    cc[j] += cpart[(size_t)y * B + i];
+                    ss[j] += spart[(size_t)y * B + i];
+                }
+            }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t i = base + 256 * j;
+            c[j] = i < B ? (int32_t)cc[j] : -1;
+            s[j] = (float)((double)ss[j] * inv_fxs * 0.5);  // as k_h16_finish
+            if (i < B) {
+                counts_out[i] = c[j];
+                sums_out[i] = s[j];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t i = base + 256 * j;
+            c[j] = i < B ? counts_in[i] : -1;
+            s[j] = i < B ? sums_in[i] : 0.f;
+        }
     }
     BestEntry b{-1, 0.f, 0xFFFFFFFFu};
 #pragma unroll
@@ -754,7 +789,25 @@ hipError_t launch_argmax(hipStream_t st, const int32_t *counts, const float *sum
                          int ncomp, uint64_t first_hyp, uint32_t spk, void *scratch, usac_record *out) {
     const uint32_t nparts = (B + 2047) / 2048;
     BestEntry *part = static_cast<BestEntry *>(scratch);
-    hipLaunchKernelGGL(k_argmax_part, dim3(nparts), dim3(256), 0, st, counts, sums, B, part);
+    hipLaunchKernelGGL(k_argmax_part<false>, dim3(nparts), dim3(256), 0, st, counts, sums, B, part,
+                       (const uint32_t *)nullptr, (const unsigned long long *)nullptr, 0u, 0.0, (int32_t *)nullptr,
+                       (float *)nullptr);
+    hipLaunchKernelGGL(k_argmax_final, dim3(1), dim3(256), 0, st, part, nparts, B, models, ncomp, first_hyp, spk,
+                       out);
+    return LAUNCH_CHECK();
+}
+
+hipError_t launch_argmax_h16(hipStream_t st, const void *part16, uint32_t B, int chunks, float thr, int32_t *counts,
+                             float *sums, const float *models, int ncomp, uint64_t first_hyp, uint32_t spk,
+                             void *scratch, usac_record *out) {
+    const uint32_t nparts = (B + 2047) / 2048;
+    BestEntry *part = static_cast<BestEntry *>(scratch);
+    // the h16 partials' layout (launch_score_h16): u64 sums [chunks][B] first, then u32 counts
+    const unsigned long long *sp = static_cast<const unsigned long long *>(part16);
+    const uint32_t *cp = reinterpret_cast<const uint32_t *>(sp + (size_t)chunks * B);
+    hipLaunchKernelGGL(k_argmax_part<true>, dim3(nparts), dim3(256), 0, st, (const int32_t *)nullptr,
+                       (const float *)nullptr, B, part, cp, sp, (uint32_t)chunks, ldexp(1.0, -h16_fixed_point(thr)),
+                       counts, sums);
     hipLaunchKernelGGL(k_argmax_final, dim3(1), dim3(256), 0, st, part, nparts, B, models, ncomp, first_hyp, spk,
                        out);
     return LAUNCH_CHECK();

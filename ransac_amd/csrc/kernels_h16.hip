@@ -400,15 +400,19 @@ __global__ __launch_bounds__(256) void k_h16_finish(const uint32_t *__restrict__
 
 size_t h16_part_bytes(uint32_t B, int chunks) { return (size_t)chunks * B * (sizeof(uint32_t) + sizeof(uint64_t)); }
 
+int h16_fixed_point(float thr) {
+    const double T = 2.0 * (double)thr;
+    return T > 0 ? 39 - ilogb(T) : 40;
+}
+
 hipError_t launch_score_h16(hipStream_t st, const void *feat, const float4 *pts, uint32_t n, const void *rows,
                             const float *fm, const float *models, uint32_t B, float thr, int chunks, void *part,
-                            int32_t *counts, float *sums) {
+                            int32_t *counts, float *sums, bool finish) {
     static const int na = getenv("USAC_H16_NA") ? atoi(getenv("USAC_H16_NA")) : 2;  // 10-hypothesis tiles per wave
     if (chunks < 1 || n == 0 || n > 0x2000000u) return hipErrorInvalidValue;  // 25-bit point indices in the queue
     // Σ in fixed point: a stage-B term is < 2 T (1 + 2^-15) (S ~ 2 err of an inlier, err < thr = T / 2), so
     // 2^fx with 2 T 2^fx <= 2^40 leaves 2^23 terms per hypothesis and chunk below 2^63
-    const double T = 2.0 * (double)thr;
-    const int fx = T > 0 ? 39 - ilogb(T) : 40;
+    const int fx = h16_fixed_point(thr);
     const double fxs = ldexp(1.0, fx);
     unsigned long long *sp = static_cast<unsigned long long *>(part);  // 8-byte words first (alignment)
     uint32_t *cp = reinterpret_cast<uint32_t *>(sp + (size_t)chunks * B);
@@ -429,7 +433,7 @@ hipError_t launch_score_h16(hipStream_t st, const void *feat, const float4 *pts,
         H16(2, 1, 1);
 #undef H16
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess || !finish) return e;  // !finish: the caller's launch_argmax_h16 adds the chunks
     hipLaunchKernelGGL(k_h16_finish, dim3((B + 255) / 256), dim3(256), 0, st, cp, sp, B, (uint32_t)chunks,
                        ldexp(1.0, -fx), counts, sums);
     return hipGetLastError();

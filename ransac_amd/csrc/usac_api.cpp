@@ -298,6 +298,8 @@ struct usac_ctx {
     bool h16_off = false;  // k_score_hf for every batch (usac_ransac_run sets it for its loop)
     uint32_t h16_rows_for = 0;  // > 0: the solver wrote the rows of a batch of this size for h16_rows_thr
     float h16_rows_thr = 0.f;
+    uint32_t h16_deferred_ch = 0;  // > 0: the last h16 batch's chunk partials await batch_argmax
+    float h16_deferred_thr = 0.f;
     DevBuf h16_k, h16_feat, h16_rows, h16_fm, h16_part;  // h16_k: the dataset constants (usac::H16Consts)
     // batch buffers
     DevBuf samples, models, counts, sums, best, hostmodels, argmax_part;
@@ -668,8 +670,10 @@ bool h16_scores(const usac_ctx *c, int chunks) {
            chunks > 1;
 }
 
-hipError_t enqueue_score_h16(usac_ctx *c, uint32_t B, float thr) {
+// defer_finish: the chunk partials stay for the batch argmax (launch_argmax_h16, via batch_argmax)
+hipError_t enqueue_score_h16(usac_ctx *c, uint32_t B, float thr, bool defer_finish) {
     hipError_t e;
+    c->h16_deferred_ch = 0;
     if ((e = h16_init(c)) != hipSuccess) return e;
     const uint32_t ch = h16_chunks(c, B);
     if ((e = c->h16_part.reserve(usac::h16_part_bytes(B, (int)ch))) != hipSuccess) return e;
@@ -684,13 +688,17 @@ hipError_t enqueue_score_h16(usac_ctx *c, uint32_t B, float thr) {
     }
     e = usac::launch_score_h16(c->stream, c->h16_feat.p, c->pts.as<float4>(), c->n, c->h16_rows.p,
                                c->h16_fm.as<float>(), c->models.as<float>(), B, thr, (int)ch, c->h16_part.p,
-                               c->counts.as<int32_t>(), c->sums.as<float>());
+                               c->counts.as<int32_t>(), c->sums.as<float>(), !defer_finish);
+    if (e == hipSuccess && defer_finish) {
+        c->h16_deferred_ch = ch;
+        c->h16_deferred_thr = thr;
+    }
     return e;
 }
 
 // chunks == 1 is the parity configuration: per-hypothesis sums are the exact sequential
 // fp32 sums of the reference.  chunks > 1 re-associates Σerr across chunks (counts exact).
-hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
+hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks, bool defer_finish = false) {
     if (c->sprt_on) {
         hipError_t e = hipMemsetAsync(c->sprt_tested.p, 0, sizeof(uint32_t), c->stream);
         if (e != hipSuccess) return e;
@@ -730,7 +738,7 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks) {
         if (c->score_variant == 1)
             return usac::launch_score_h(c->stream, chunks, c->pts.as<float4>(), c->n, c->models.as<float>(), B, thr,
                                         c->counts.as<int32_t>(), c->sums.as<float>());
-        if (h16_scores(c, chunks)) return enqueue_score_h16(c, B, thr);  // counts exact
+        if (h16_scores(c, chunks)) return enqueue_score_h16(c, B, thr, defer_finish);  // counts exact
         uint32_t *perm = nullptr;
         if (c->score_variant == 0) {  // 2: fast kernel without the hypothesis pre-sort (A/B)
             hipError_t e = c->perm.reserve(usac::presort_bytes(B));
@@ -2030,6 +2038,26 @@ int usac_lsq_fit(usac_ctx *c, const int32_t *idx, uint32_t n, const float *weigh
     return ok ? USAC_OK : fail(c, USAC_ERR_NO_MODEL, "non-minimal estimation failed");
 }
 
+// USAC_H16_DEFER=0: the h16 scorer's own finish kernel, then the plain argmax (A/B)
+bool h16_defer() {
+    static const bool on = !getenv("USAC_H16_DEFER") || atoi(getenv("USAC_H16_DEFER")) != 0;
+    return on;
+}
+
+// the batch argmax (record of the batch) -- over the h16 scorer's chunk partials when it deferred
+// its finish (one launch fewer), else over counts / sums
+hipError_t batch_argmax(usac_ctx *c, uint32_t S, uint64_t first_hyp) {
+    if (c->h16_deferred_ch) {
+        const uint32_t ch = c->h16_deferred_ch;
+        c->h16_deferred_ch = 0;
+        return usac::launch_argmax_h16(c->stream, c->h16_part.p, S, (int)ch, c->h16_deferred_thr,
+                                       c->counts.as<int32_t>(), c->sums.as<float>(), c->models.as<float>(), ncomp(c),
+                                       first_hyp, c->spk, c->argmax_part.p, c->best.as<usac_record>());
+    }
+    return usac::launch_argmax(c->stream, c->counts.as<int32_t>(), c->sums.as<float>(), S, c->models.as<float>(),
+                               ncomp(c), first_hyp, c->spk, c->argmax_part.p, c->best.as<usac_record>());
+}
+
 int usac_hypothesize_score(usac_ctx *c, const int32_t *samples, uint32_t B, uint64_t seed, uint64_t first_hyp,
                            float thr, int32_t *counts, float *sums, usac_record *best) {
     if (!c || B == 0) return USAC_ERR_ARG;
@@ -2046,11 +2074,10 @@ int usac_hypothesize_score(usac_ctx *c, const int32_t *samples, uint32_t B, uint
     const int chunks = (counts || sums) ? 1 : c->chunks;
     HIP_TRY(c, enqueue_solve(c, samples ? c->samples.as<int32_t>() : nullptr, B, seed, first_hyp,
                              samples ? nullptr : c->samples.as<int32_t>(), h16_solver_thr(c, chunks, thr)));
-    HIP_TRY(c, enqueue_score(c, B, thr, chunks));
+    HIP_TRY(c, enqueue_score(c, B, thr, chunks, h16_defer()));
     c->batch_valid = true;
     const uint32_t S = B * c->spk;
-    HIP_TRY(c, usac::launch_argmax(c->stream, c->counts.as<int32_t>(), c->sums.as<float>(), S, c->models.as<float>(),
-                                   ncomp(c), first_hyp, c->spk, c->argmax_part.p, c->best.as<usac_record>()));
+    HIP_TRY(c, batch_argmax(c, S, first_hyp));
     if (counts) HIP_TRY(c, hipMemcpyAsync(counts, c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
     if (sums) HIP_TRY(c, hipMemcpyAsync(sums, c->sums.p, sizeof(float) * S, hipMemcpyDeviceToHost, c->stream));
     if (best) HIP_TRY(c, hipMemcpyAsync(best, c->best.p, sizeof(usac_record), hipMemcpyDeviceToHost, c->stream));
@@ -2066,12 +2093,10 @@ int usac_hypothesize_async(usac_ctx *c, uint32_t B, uint64_t seed, uint64_t firs
     HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(c, enqueue_solve(c, nullptr, B, seed, first_hyp, nullptr, h16_solver_thr(c, c->chunks, thr)));
     HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
-    HIP_TRY(c, enqueue_score(c, B, thr, c->chunks));
+    HIP_TRY(c, enqueue_score(c, B, thr, c->chunks, h16_defer()));
     c->batch_valid = true;
     HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
-    HIP_TRY(c, usac::launch_argmax(c->stream, c->counts.as<int32_t>(), c->sums.as<float>(), B * c->spk,
-                                   c->models.as<float>(), ncomp(c), first_hyp, c->spk, c->argmax_part.p,
-                                   c->best.as<usac_record>()));
+    HIP_TRY(c, batch_argmax(c, B * c->spk, first_hyp));
     HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
     c->timed_pending = true;
     return USAC_OK;

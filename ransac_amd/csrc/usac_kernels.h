@@ -98,9 +98,12 @@ hipError_t launch_h16_rows(hipStream_t st, const float *models, uint32_t B, cons
 // the scorer: counts / sums of B hypotheses (exact counts; Σ from fixed-point stage-B terms) over
 // `chunks` point chunks; part = h16_part_bytes(B, chunks) scratch
 size_t h16_part_bytes(uint32_t B, int chunks);
+// finish = false: the chunk partials are left for launch_argmax_h16 (the batch argmax adds them)
 hipError_t launch_score_h16(hipStream_t st, const void *feat, const float4 *pts, uint32_t n, const void *rows,
                             const float *fm, const float *models, uint32_t B, float thr, int chunks, void *part,
-                            int32_t *counts, float *sums);
+                            int32_t *counts, float *sums, bool finish = true);
+// Σ's fixed-point exponent of the h16 chunk partials for threshold thr
+int h16_fixed_point(float thr);
 
 hipError_t launch_solve_line(hipStream_t st, const float2 *pts, uint32_t n, const int32_t *samples_in,
                              int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, float *models);
@@ -109,6 +112,12 @@ hipError_t launch_score_line(hipStream_t st, int chunks, const float2 *pts, uint
                              uint32_t B, float thr, int32_t *counts, float *sums);
 
 // B = number of model slots; hyp_index = first_hyp + slot / spk (spk = slots per hypothesis)
+// launch_argmax over the h16 scorer's chunk partials (launch_score_h16 with finish = false): the
+// first pass also adds every hypothesis' chunks in chunk order and writes counts / sums, exactly as
+// k_h16_finish does -- one launch fewer per batch
+hipError_t launch_argmax_h16(hipStream_t st, const void *part, uint32_t B, int chunks, float thr, int32_t *counts,
+                             float *sums, const float *models, int ncomp, uint64_t first_hyp, uint32_t spk,
+                             void *scratch, usac_record *out);
 hipError_t launch_argmax(hipStream_t st, const int32_t *counts, const float *sums, uint32_t B, const float *models,
                          int ncomp, uint64_t first_hyp, uint32_t spk, void *scratch /* 12 B x ceil(B/2048) */,
                          usac_record *out);

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 O=gpurun_out/${1:-fuse}; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_h16.py tests/test_gpu_parity.py tests/test_gpu_edge.py -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; tail -1 $O/tests.log; [ $rc -eq 0 ] || { grep -E "^FAILED|Error" $O/tests.log | head; exit 1; }
-for v in "USAC_H16_FUSE=0" "USAC_H16_FUSE=1" "USAC_H16_FUSE=0" "USAC_H16_FUSE=1" "USAC_H16_FUSE=0" "USAC_H16_FUSE=1"; do
+for v in "USAC_H16_DEFER=0" "USAC_H16_DEFER=1" "USAC_H16_DEFER=0" "USAC_H16_DEFER=1" "USAC_H16_DEFER=0" "USAC_H16_DEFER=1"; do
   env $v timeout -k 10 300 python bench.py --cpu-seconds 0 > $O/b.json 2> $O/b.err || { tail -5 $O/b.err; exit 1; }
   python3 -c "import json; d=json.loads(open('$O/b.json').read().strip().splitlines()[-1]); print('$v', '%.1f M hyp/s ms/step %.4f parity %s' % (d['value']/1e6, d['ms_per_step'], d['parity']['ok']))"
 done
