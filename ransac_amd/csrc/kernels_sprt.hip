@@ -26,14 +26,14 @@ __global__ __launch_bounds__(256) void k_gather(const P *__restrict__ pts, const
 // 3 fundamental / 4 essential (float4, [9][stride]).  Lane = one model row; with `list` the rows are
 // list[0 .. *list_n) (model slot list[i] -> row i), else rows are slots 0 .. kmax-1.
 // words[w * row_stride + row], bit b = pool position 32 w + b.
-constexpr uint32_t kMaskWords = 8;  // pool words (256 points) per k_pool_mask lane
+constexpr uint32_t kMaskWords = 8;  // pool words (256 points) per k_pool_mask lane, at most
 
 template <int EST>
 __global__ __launch_bounds__(64) void k_pool_mask(const void *__restrict__ pool_pts, uint32_t n,
                                                   const float *__restrict__ models, size_t stride,
                                                   const uint32_t *__restrict__ list, const uint32_t *__restrict__ list_n,
                                                   uint32_t kmax, float thr, uint32_t *__restrict__ words,
-                                                  uint32_t row_stride) {
+                                                  uint32_t row_stride, uint32_t wpl) {
     constexpr int NC = EST == 1 ? 3 : EST == 2 ? 18 : 9;
     const uint32_t K = list ? __builtin_amdgcn_readfirstlane(*list_n) : kmax;
     const uint32_t i0 = blockIdx.x * 64;
@@ -45,11 +45,11 @@ __global__ __launch_bounds__(64) void k_pool_mask(const void *__restrict__ pool_
 #pragma unroll
     for (int k = 0; k < NC; k++) m[k] = models[(size_t)k * stride + slot];
     // this block's word ranges (blockIdx.y, then every gridDim.y-th range: the y grid is capped at
-    // 65535 blocks, reached above 16.7 M points): a lane walks kMaskWords words at a time, not all
-    // n / 32 -- the loop's batches hold a few hundred models, so lanes = models alone is a handful of waves
+    // 65535 blocks, reached above 16.7 M points): a lane walks wpl words at a time, not all n / 32 --
+    // the loop's batches hold a few hundred models, so lanes = models alone is a handful of waves
     const uint32_t nw = (n + 31) / 32;
-    for (uint32_t w0 = blockIdx.y * kMaskWords; w0 < nw; w0 += gridDim.y * kMaskWords)
-    for (uint32_t w = w0, w1 = w0 + kMaskWords < nw ? w0 + kMaskWords : nw; w < w1; w++) {
+    for (uint32_t w0 = blockIdx.y * wpl; w0 < nw; w0 += gridDim.y * wpl)
+    for (uint32_t w = w0, w1 = w0 + wpl < nw ? w0 + wpl : nw; w < w1; w++) {
         uint32_t bits = 0;
         const uint32_t p0 = 32 * w;
         const uint32_t lim = n - p0 < 32 ? n - p0 : 32;
@@ -91,24 +91,30 @@ hipError_t launch_gather_points(hipStream_t st, const void *pts, uint32_t cols, 
 hipError_t launch_pool_mask(hipStream_t st, int estimator, const void *pool_pts, uint32_t n, const float *models,
                             size_t stride, const uint32_t *list, const uint32_t *list_n, uint32_t kmax, float thr,
                             uint32_t *words, uint32_t row_stride) {
-    const uint32_t ranges = ((n + 31) / 32 + kMaskWords - 1) / kMaskWords;
-    const dim3 grid((kmax + 63) / 64, ranges < 65535u ? ranges : 65535u);
+    // words per lane: kMaskWords, fewer while the grid would hold under ~2048 workgroups (PROSAC's
+    // first batches: a few dozen samples, ~100 models -- round 5: all the pool's words at 8 per lane
+    // made two workgroup columns of 40 ranges, latency-bound)
+    const uint32_t nw = (n + 31) / 32, bx = (kmax + 63) / 64;
+    uint32_t wpl = kMaskWords;
+    while (wpl > 1 && (size_t)bx * ((nw + wpl - 1) / wpl) < 2048) wpl >>= 1;
+    const uint32_t ranges = (nw + wpl - 1) / wpl;
+    const dim3 grid(bx, ranges < 65535u ? ranges : 65535u);
     switch (estimator) {
         case USAC_LINE2D:
             hipLaunchKernelGGL(k_pool_mask<1>, grid, dim3(64), 0, st, pool_pts, n, models, stride, list, list_n, kmax,
-                               thr, words, row_stride);
+                               thr, words, row_stride, wpl);
             break;
         case USAC_HOMOGRAPHY:
             hipLaunchKernelGGL(k_pool_mask<2>, grid, dim3(64), 0, st, pool_pts, n, models, stride, list, list_n, kmax,
-                               thr, words, row_stride);
+                               thr, words, row_stride, wpl);
             break;
         case USAC_FUNDAMENTAL:
             hipLaunchKernelGGL(k_pool_mask<3>, grid, dim3(64), 0, st, pool_pts, n, models, stride, list, list_n, kmax,
-                               thr, words, row_stride);
+                               thr, words, row_stride, wpl);
             break;
         case USAC_ESSENTIAL:
             hipLaunchKernelGGL(k_pool_mask<4>, grid, dim3(64), 0, st, pool_pts, n, models, stride, list, list_n, kmax,
-                               thr, words, row_stride);
+                               thr, words, row_stride, wpl);
             break;
         default:
             return hipErrorInvalidValue;

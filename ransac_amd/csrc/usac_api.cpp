@@ -3001,12 +3001,15 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     HIP_TRY(c, usac::launch_inliers_batch(c->stream, c->estimator, c->pts.p, c->n, c->one_model.as<float>(), 1, thr,
                                           nullptr, nullptr, lists[0], 0, dres_i + 12, dres + 13,
                                           c->inl_scratch.p));  // quality->getInliers(best_model)
-    // passes go out in groups of G (USAC_POLISH_GROUP, default 2): a group is one submission and
-    // one host wait; the next group is submitted only while every pass so far was accepted
+    // passes go out in groups of G (USAC_POLISH_GROUP): a group is one submission and one host
+    // wait; the next group is submitted only while every pass so far was accepted.  Default: all
+    // four at once for a best model of <= 8192 inliers (cfg3 exact: 1.15 vs 1.20-1.28 ms per run
+    // with groups of 2), two above (cfg5's 17 k-inlier fits: a rejected pass's no-op successors
+    // cost 0.1 ms; profiles/r4c/ab_polish.txt, profiles/r5/polish_ab.txt)
     constexpr int kPasses = 4;
-    const int kGroup = [] {
+    const int kGroup = [&] {
         const char *g = getenv("USAC_POLISH_GROUP");
-        const int v = g ? atoi(g) : 2;
+        const int v = g ? atoi(g) : best.inlier_number <= 8192 ? 4 : 2;
         return v < 1 ? 1 : v > kPasses ? kPasses : v;
     }();
     int32_t *cur = lists[0];

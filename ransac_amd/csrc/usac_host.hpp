@@ -22,6 +22,7 @@
 #include <algorithm>
 #include <cmath>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -238,22 +239,40 @@ class ProsacSampler {
    public:
     // prosac_sampler.hpp:62-114 (T_N = 200000)
     ProsacSampler(uint32_t seed, uint32_t points_size, uint32_t sample_size)
-        : rng_(seed), growth_(points_size), n_(points_size), m_(sample_size) {
-        double T_n = kGrowthMax;
-        for (uint32_t i = 0; i < m_; ++i) T_n *= (double)(m_ - i) / (n_ - i);
-        uint32_t T_prime = 1;
-        for (uint32_t i = 0; i < n_; ++i) {
-            if (i + 1 <= m_) {
-                growth_[i] = T_prime;
-                continue;
-            }
-            const double T_next = (double)(i + 1) * T_n / (i + 1 - m_);
-            growth_[i] = T_prime + (uint32_t)std::ceil(T_next - T_n);
-            T_n = T_next;
-            T_prime = growth_[i];
-        }
+        : rng_(seed), growth_(growth_table(points_size, sample_size)), n_(points_size), m_(sample_size) {
         largest_ = subset_ = m_;
         hyp_ = 1;
+    }
+    // the growth function depends on (n, m) alone: computed once per shape and shared (a dependent
+    // chain of n fp64 divisions, ~0.1 ms at n = 10 k -- a tenth of a cfg3 run when rebuilt per run;
+    // snapshots of the sampler share it too)
+    static std::shared_ptr<const std::vector<uint32_t>> growth_table(uint32_t n, uint32_t m) {
+        static std::mutex mu;
+        static std::map<std::pair<uint32_t, uint32_t>, std::shared_ptr<const std::vector<uint32_t>>> cache;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            auto it = cache.find({n, m});
+            if (it != cache.end()) return it->second;
+        }
+        auto t = std::make_shared<std::vector<uint32_t>>(n);
+        std::vector<uint32_t> &growth = *t;
+        double T_n = kGrowthMax;
+        for (uint32_t i = 0; i < m; ++i) T_n *= (double)(m - i) / (n - i);
+        uint32_t T_prime = 1;
+        for (uint32_t i = 0; i < n; ++i) {
+            if (i + 1 <= m) {
+                growth[i] = T_prime;
+                continue;
+            }
+            const double T_next = (double)(i + 1) * T_n / (i + 1 - m);
+            growth[i] = T_prime + (uint32_t)std::ceil(T_next - T_n);
+            T_n = T_next;
+            T_prime = growth[i];
+        }
+        std::lock_guard<std::mutex> g(mu);
+        if (cache.size() > 64) cache.clear();
+        cache[{n, m}] = t;
+        return t;
     }
     // prosac_sampler.hpp:117-172 with the current termination_length
     void generateSample(int32_t *sample, uint32_t termination_length) {
@@ -265,7 +284,7 @@ class ProsacSampler {
             unique_set(rng_, sample, m_, termination_length);  // closed range, SURVEY Q15
             return;
         }
-        if (hyp_ > growth_[subset_ - 1]) {
+        if (hyp_ > (*growth_)[subset_ - 1]) {
             if (++subset_ > n_) subset_ = n_;
             largest_ = std::max(largest_, subset_);
         }
@@ -273,14 +292,14 @@ class ProsacSampler {
         sample[m_ - 1] = (int32_t)subset_ - 1;
         hyp_++;
     }
-    const std::vector<uint32_t> &growth() const { return growth_; }
+    const std::vector<uint32_t> &growth() const { return *growth_; }
     uint32_t largest() const { return largest_; }
     uint32_t subset() const { return subset_; }
     static constexpr uint32_t kGrowthMax = 200000;
 
    private:
     Mt19937 rng_;
-    std::vector<uint32_t> growth_;
+    std::shared_ptr<const std::vector<uint32_t>> growth_;
     uint32_t n_, m_, largest_, subset_, hyp_;
 };
 
