@@ -750,7 +750,7 @@ def cfg3_exact_main(args, usac, synthetic, dist, torch, world, rank, local_rank)
         one_run(10_000 + i)
     if world > 1:
         dist.barrier()
-    iters, rejected, batches = 0, 0, 0
+    iters, rejected, batches, lib_us = 0, 0, 0, 0
     t0 = time.perf_counter()
     for step in range(args.steps):
         r = one_run(args.seed + step * world + rank)
@@ -758,6 +758,7 @@ def cfg3_exact_main(args, usac, synthetic, dist, torch, world, rank, local_rank)
         iters += out.getNumberOfMainIterations()
         rejected += out.raw["sprt_rejected"]
         batches += out.raw["batches"]
+        lib_us += out.getTimeMicroSeconds()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -810,7 +811,10 @@ def cfg3_exact_main(args, usac, synthetic, dist, torch, world, rank, local_rank)
         "roofline": roof,
         "parity": parity,
         "run_stats": {"iterations_per_run": iters / world / args.steps, "sprt_rejected": rejected,
-                      "batches": batches},
+                      "batches": batches,
+                      # rank 0's usac_ransac_run wall time per run (RansacOutput.getTimeMicroSeconds:
+                      # argument checks to the polish's end) beside the line's per-run wall time
+                      "library_ms_per_run": lib_us / 1e3 / args.steps},
     }
     if args.cpu_seconds > 0:
         t1 = time.perf_counter()

@@ -32,3 +32,4 @@ if [ -n "${WITH_POLISH_AB:-}" ]; then
     python3 -c "import json; d=json.loads(open('$O/px.json').read().strip().splitlines()[-1]); print('polish group $g: cfg3 exact ms/run %.3f' % d['ms_per_step'], all(v for k,v in d['parity'].items() if k.endswith('equal')))"
   done
 fi
+python3 -c "import json; d=json.loads(open('$O/cfg3x.json').read().strip().splitlines()[-1]); print('cfg3x library ms/run', d['run_stats'].get('library_ms_per_run'))"
