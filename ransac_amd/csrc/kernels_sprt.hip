@@ -25,7 +25,8 @@ __global__ __launch_bounds__(256) void k_gather(const P *__restrict__ pts, const
 // EST: 1 line (float2 points, models [3][stride]), 2 homography (float4, [18][stride]: H, H^-1),
 // 3 fundamental / 4 essential (float4, [9][stride]).  Lane = one model row; with `list` the rows are
 // list[0 .. *list_n) (model slot list[i] -> row i), else rows are slots 0 .. kmax-1.
-// words[w * row_stride + row], bit b = pool position 32 w + b.
+// words[w * row_stride + row], bit b = pool position 32 w + b; row_stride 0: the row count itself
+// (the listed rows' words packed [nw][*list_n], one plain copy for the host).
 constexpr uint32_t kMaskWords = 8;  // pool words (256 points) per k_pool_mask lane, at most
 
 template <int EST>
@@ -39,6 +40,7 @@ __global__ __launch_bounds__(64) void k_pool_mask(const void *__restrict__ pool_
     const uint32_t i0 = blockIdx.x * 64;
     if (i0 >= K) return;
     const uint32_t row = i0 + threadIdx.x;
+    const size_t rs = row_stride ? row_stride : K;
     const uint32_t rc = row < K ? row : K - 1;
     const uint32_t slot = list ? list[rc] : rc;
     float m[NC];
@@ -70,7 +72,7 @@ __global__ __launch_bounds__(64) void k_pool_mask(const void *__restrict__ pool_
             }
             bits |= (e < thr ? 1u : 0u) << b;
         }
-        if (row < K) words[(size_t)w * row_stride + row] = bits;
+        if (row < K) words[(size_t)w * rs + row] = bits;
     }
 }
 

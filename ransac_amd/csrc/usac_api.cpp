@@ -2491,6 +2491,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     // wall-time split of the run, printed to stderr when USAC_PROFILE is set
     enum { T_SETUP, T_DRAW, T_DEVICE, T_SUMS, T_REPLAY, T_LO, T_POLISH, T_N };
     double tsplit[T_N] = {0, 0, 0, 0, 0, 0, 0};
+    double t_verify = 0.0, t_drawonly = 0.0;  // USAC_PROFILE detail: host SPRT walks, sample draws
     auto tmark = std::chrono::steady_clock::now();
     auto lap = [&](int k) {
         const auto t = std::chrono::steady_clock::now();
@@ -2675,6 +2676,30 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         return USAC_OK;
     };
 
+    // PROSAC + SPRT: a new best's inlier list (getUpBoundIterationsSorted's input) decoded from its
+    // pool-order mask row on the host instead of a device getInliers round trip per update.  An
+    // accepted model's row covers every point (Sprt::verify counts the rest of the pool for a
+    // model it keeps), and k_pool_mask evaluates the same residual (no contraction: Makefile) on
+    // copies of the same points with the same model words -- except H, whose mask uses the
+    // solver's H^-1 where getInliers inverts on the device.  USAC_CHECK_MASK_LIST=1 compares both.
+    const bool mask_list = prosac && sprt && c->estimator != USAC_HOMOGRAPHY && !getenv("USAC_DEVICE_INLIERS");
+    const bool mask_check = mask_list && getenv("USAC_CHECK_MASK_LIST");
+    std::vector<uint64_t> pt_bits(mask_list ? ((size_t)n + 63) / 64 : 0);
+    auto mask_inliers = [&](const uint32_t *row, size_t stride, int32_t *list) -> int32_t {
+        std::fill(pt_bits.begin(), pt_bits.end(), 0);
+        const uint32_t *pool = sprt->pool().data();
+        for (uint32_t w = 0; w < nw; w++)
+            for (uint32_t bits = row[(size_t)w * stride]; bits; bits &= bits - 1) {
+                const uint32_t p = pool[32 * w + (uint32_t)__builtin_ctz(bits)];
+                pt_bits[p >> 6] |= 1ull << (p & 63);
+            }
+        int32_t k = 0;
+        for (size_t w = 0; w < pt_bits.size(); w++)
+            for (uint64_t bits = pt_bits[w]; bits; bits &= bits - 1)
+                list[k++] = (int32_t)(64 * w + (uint32_t)__builtin_ctzll(bits));
+        return k;
+    };
+
     lap(T_SETUP);
     // with the library's default batch the batches ramp up (1024, 2048, ...): the termination
     // bound drops once the loop has a good model, and a smaller first batch draws, solves and
@@ -2751,8 +2776,10 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         const uint32_t gen_term = prosac ? pterm->terminationLength() : n;
         if (!have) {
             settle_sampler();
+            const auto td0 = std::chrono::steady_clock::now();
             if (prosac) snapshot.reset(new usac::ProsacSampler(*pro));
             draw_into(hs.data(), B, prosac ? pro.get() : nullptr, gen_term);
+            t_drawonly += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - td0).count();
         }
         lap(T_DRAW);
         // ---- device: solve, then exact scores or pool-order flags
@@ -2775,7 +2802,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
             HIP_TRY(c, usac::launch_pool_mask(c->stream, c->estimator, c->pool_pts.p, n, c->models.as<float>(), mstride,
                                               listed(c) ? c->list.as<uint32_t>() : nullptr,
                                               listed(c) ? c->list_n.as<uint32_t>() : nullptr, (uint32_t)S, thr,
-                                              c->masks.as<uint32_t>(), (uint32_t)S));
+                                              c->masks.as<uint32_t>(), listed(c) ? 0u : (uint32_t)S));
         } else {  // exact counts from the fast multi-chunk scorer; exact sums below, where needed
             HIP_TRY(c, enqueue_score(c, B, thr, loop_chunks(c, B)));
             HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
@@ -2787,9 +2814,11 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         HIP_TRY(c, hipMemcpyAsync(hmod.data(), c->models.p, sizeof(float) * S * ncomp(c), hipMemcpyDeviceToHost,
                                   c->stream));
         if (sprt) {
-            // small batches (the PROSAC ramp's first ones, where a cfg3 run ends): every slot's
-            // words [nw][S] with the list in the same submission -- one host wait; larger ones:
-            // the list count first, then only the occupied rows' words repacked [nw][rows]
+            // listed: the occupied rows' words packed [nw][rows] on the device (k_pool_mask, row
+            // stride 0).  Small batches (the PROSAC ramp's first ones, where a cfg3 run ends): the
+            // whole block with the list in the same submission -- one host wait; larger ones: the
+            // list count first, then only the rows' words (a plain copy: hipMemcpy2DAsync's first
+            // call in a process cost ~7 ms, round 5)
             const bool whole = !listed(c) || (size_t)nw * S * sizeof(uint32_t) <= kMaskWholeCopy;
             if (listed(c)) {  // occupied slots -> mask rows
                 HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
@@ -2808,21 +2837,16 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                 std::fill(hc.begin(), hc.begin() + S, 0);
             }
             if (whole) {
-                mask_stride = (uint32_t)S;
+                mask_stride = (uint32_t)S;  // listed: the row count, below
                 HIP_TRY(c, hipMemcpyAsync(hmask.data(), c->masks.p, sizeof(uint32_t) * S * nw, hipMemcpyDeviceToHost,
                                           c->stream));
-            } else {
-                mask_stride = rows;
-                // the [nw][S] words of the batch's rows, repacked [nw][rows], in one strided copy
-                // into pinned memory (a copy per word was ~nw fixed copy overheads per batch)
-                if (rows)
-                    HIP_TRY(c, hipMemcpy2DAsync(hmask.data(), sizeof(uint32_t) * rows, c->masks.as<uint32_t>(),
-                                                sizeof(uint32_t) * S, sizeof(uint32_t) * rows, nw,
-                                                hipMemcpyDeviceToHost, c->stream));
+            } else if (rows) {
+                HIP_TRY(c, hipMemcpyAsync(hmask.data(), c->masks.p, sizeof(uint32_t) * (size_t)rows * nw,
+                                          hipMemcpyDeviceToHost, c->stream));
             }
         }
         HIP_TRY(c, stream_wait(c->stream));
-        if (sprt && listed(c)) rows = hlist[SB];
+        if (sprt && listed(c)) mask_stride = rows = hlist[SB];
         }
         if (sprt) {
             if (listed(c) && nranks == 1) {
@@ -2883,10 +2907,13 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                 const size_t sl = (size_t)j * spk + q;
                 if (hc[sl] < 0) break;  // empty slot: the sample has no more models
                 usac::Score cur;
+                int32_t r = 0;
                 if (sprt) {
-                    const int32_t r = slot_row[sl];
+                    r = slot_row[sl];
+                    const auto tv0 = std::chrono::steady_clock::now();
                     const bool good = sprt->verify(hmask.data() + r, (int)iters, (uint32_t)best.inlier_number,
                                                    cur.inlier_number, cur.score, mask_stride);
+                    t_verify += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tv0).count();
                     if (!good) {
                         out->sprt_rejected++;
                         if ((int)iters >= max_before) {  // max_hypothesis_test_before_sprt (model.hpp:40), Q9
@@ -2915,7 +2942,20 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                 }
                 best = cur;
                 memcpy(best_model, model, sizeof(best_model));
-                if (prosac) {
+                if (prosac && mask_list) {
+                    cnt = mask_inliers(hmask.data() + r, mask_stride, inl_list.data());
+                    if (mask_check) {
+                        std::vector<int32_t> dl(n);
+                        const int32_t mc = cnt;
+                        if ((rc = score_inliers(best_model, dl.data()))) return rc;
+                        const std::vector<int32_t> tmp(inl_list.data(), inl_list.data() + mc);
+                        if (cnt != mc || cnt != cur.inlier_number ||
+                            !std::equal(tmp.begin(), tmp.end(), dl.begin()))
+                            return fail(c, USAC_ERR_HIP, "mask-decoded inlier list differs from getInliers");
+                        cnt = mc;
+                    }
+                    max_iters = pterm->getUpBoundIterationsSorted(iters, inl_list.data(), (uint32_t)cnt, largest_at[j]);
+                } else if (prosac) {
                     if ((rc = score_inliers(best_model, inl_list.data()))) return rc;
                     // (the list is ascending: the compaction keeps point order)
                     max_iters = pterm->getUpBoundIterationsSorted(iters, inl_list.data(), (uint32_t)cnt, largest_at[j]);
@@ -3058,11 +3098,11 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         fprintf(stderr,
                 "usac_ransac_run ms: setup %.3f draw %.3f device %.3f sums %.3f replay %.3f lo %.3f polish %.3f "
                 "(lo rounds %u stages %u enqueue %.3f poll %.3f graphs %u; setup: buffers %.3f neighbours %.3f "
-                "lo/gc %.3f)\n",
+                "lo/gc %.3f; sprt walks %.3f, draws %.3f; iters %u batches %u)\n",
                 tsplit[T_SETUP], tsplit[T_DRAW], tsplit[T_DEVICE], tsplit[T_SUMS], tsplit[T_REPLAY], tsplit[T_LO],
                 tsplit[T_POLISH], lo ? lo->rounds : gc ? gc->labelings : 0u, lo ? lo->stages : gc ? gc->stages : 0u,
                 lo ? lo->t_enqueue : 0.0, lo ? lo->t_poll : 0.0, lo ? lo->graphs_built : 0u, tsub[0],
-                tsub[1] - tsub[0], tsub[2] - tsub[1]);
+                tsub[1] - tsub[0], tsub[2] - tsub[1], t_verify, t_drawonly, iters, (uint32_t)out->batches);
     // ransac.cpp:214 getInliers(best_model): `cur` already is that list (see above)
     cnt = cur_cnt;
     if (inliers_out && cnt > 0) {  // DMA into pinned memory, then into the caller's buffer

@@ -183,3 +183,35 @@ def test_polish_groups_identical(usac, oracle, kind):
             assert (_bits(out.getModel()) == _bits(ref["model"])).all(), (seed, g)
             assert (out.getInliers() == ref["inlier_idx"]).all(), (seed, g)
     assert max(passes) >= 1
+
+
+@pytest.mark.parametrize("kind", ["F", "L"])
+def test_prosac_sprt_mask_inlier_lists(usac, oracle, kind):
+    """PROSAC + SPRT: a new best's inlier list (PROSAC's termination input) is decoded from the
+    model's SPRT mask row on the host; USAC_CHECK_MASK_LIST=1 makes the library also run the
+    device getInliers at every update and fail the run on any difference.  The runs equal the
+    oracle's, and the device-list path (USAC_DEVICE_INLIERS=1) gives the same runs."""
+    import os
+    okind = {"F": oracle.FUNDAMENTAL, "L": oracle.LINE2D}[kind]
+    est = {"F": usac.ESTIMATOR.Fundamental, "L": usac.ESTIMATOR.Line2d}[kind]
+    thr = 2.0 if kind != "L" else 8.0
+    for seed in (1, 2, 3):
+        pts = _data(kind, seed, True)
+        ref = oracle.ransac_run(okind, pts, thr, 0.95, seed, sampler=oracle.SAMPLER_PROSAC, sprt=True)
+        runs = []
+        for env in ("USAC_CHECK_MASK_LIST", "USAC_DEVICE_INLIERS"):
+            os.environ[env] = "1"
+            try:
+                m = usac.Model(thr, {"F": 7, "L": 2}[kind], 0.95, 7, est, usac.SAMPLER.Prosac)
+                m.ResetRandomGenerator(False)
+                m.setSeed(seed)
+                m.setSprt(True)
+                m.batch = 64
+                r = usac.Ransac(m, pts)
+                r.run()
+            finally:
+                os.environ.pop(env, None)
+            out = r.getRansacOutput()
+            runs.append((out.getNumberOfMainIterations(), r.records, out.raw["prosac_term_len"]))
+        assert runs[0] == runs[1], seed
+        assert runs[0][0] == ref["iters"] and runs[0][2] == ref["prosac_term_len"], seed
