@@ -513,6 +513,78 @@ class Sprt {
     // few words, not all n / 32); count/score are written when the reference writes them.
     bool verify(const uint32_t *words, int current_hypothese, uint32_t maximum_score, int &count, float &score,
                 size_t stride = 1) {
+        if (plain_) return verify_plain(words, current_hypothese, maximum_score, count, score, stride);
+        const History &h = hist_[cur_];
+        const double epsilon = h.epsilon, delta = h.delta, A = h.A;
+        const double up = delta / epsilon, down = (1 - delta) / (1 - epsilon);
+        double lambda = 1;
+        uint32_t tested = 0, inl = 0;
+        bool good = true;
+        // the reference's per-point walk, a word's run of positions at a time (the fp64 product
+        // chain is the same sequence of multiplications); at growing intervals the rest of the
+        // walk is tried for a certificate that lambda cannot pass A (no_crossing): then the
+        // remaining points are only counted -- the same decision, count and pool index
+        uint32_t next_cert = 32;
+        while (tested < n_) {
+            if (idx_ >= n_) idx_ = 0;
+            const uint32_t b = idx_ & 31;
+            const uint32_t len = std::min(std::min(32 - b, n_ - idx_), n_ - tested);
+            uint32_t bits = words[(size_t)(idx_ >> 5) * stride] >> b;
+            uint32_t k = 0;
+            for (; k < len; k++, bits >>= 1) {
+                const uint32_t in = bits & 1u;
+                const double next = lambda * (in ? up : down);
+                inl += in;
+                if (next > A) {
+                    good = false;
+                    k++;
+                    break;
+                }
+                lambda = next;
+            }
+            tested += k;
+            idx_ += k;
+            if (!good) break;
+            if (tested >= next_cert && tested < n_) {
+                if (idx_ >= n_) idx_ = 0;
+                if (no_crossing(words, stride, lambda, A, up, down, idx_, n_ - tested)) {
+                    inl += count_range(words, stride, idx_, n_ - tested);
+                    idx_ = last_of(idx_, n_ - tested) + 1;  // as the per-point walk leaves it
+                    tested = n_;
+                    break;
+                }
+                next_cert *= 4;
+            }
+        }
+        if (good) {
+            count = (int)inl;
+            score = (float)count;
+        } else if (current_hypothese < max_before_) {
+            uint32_t after = 0;
+            if (tested < n_) {
+                if (idx_ >= n_) idx_ = 0;
+                after = count_range(words, stride, idx_, n_ - tested);
+                idx_ = last_of(idx_, n_ - tested) + 1;
+            }
+            count = (int)(inl + after);
+            score = (float)count;
+        }
+        if (good) {
+            if (inl > maximum_score) {
+                const double eps = (float)inl / n_;
+                push(eps, delta, current_hypothese);
+            }
+        } else {
+            const float dest = (float)inl / tested;
+            if (dest > 0 && std::fabs(delta - dest) / delta > 0.05) push(epsilon, dest, current_hypothese);
+        }
+        return good;
+    }
+
+    // the same, one point per step throughout (the reference's loop as written): the check of
+    // verify()'s word runs and certificates (tests/test_sprt_walk.py), USAC_SPRT_PLAIN_WALK=1
+    bool verify_plain(const uint32_t *words, int current_hypothese, uint32_t maximum_score, int &count, float &score,
+                      size_t stride = 1) {
         const History &h = hist_[cur_];
         const double epsilon = h.epsilon, delta = h.delta, A = h.A;
         const double up = delta / epsilon, down = (1 - delta) / (1 - epsilon);
@@ -556,6 +628,9 @@ class Sprt {
         }
         return good;
     }
+    void set_plain_walk(bool v) { plain_ = v; }
+    uint32_t pool_index() const { return idx_; }
+    const std::vector<History> &history() const { return hist_; }
 
     // getUpperBoundIterations (sprt.hpp:371-393)
     uint32_t getUpperBoundIterations(int inliers_size) const {
@@ -588,6 +663,60 @@ class Sprt {
     }
 
    private:
+    // pool position of the last of r >= 1 positions walked from p (< n_), wrapping at n_
+    uint32_t last_of(uint32_t p, uint32_t r) const {
+        const uint64_t q = (uint64_t)p + r - 1;
+        return (uint32_t)(q < n_ ? q : q - n_);
+    }
+    // inlier bits at pool positions [lo, hi) (hi <= n_)
+    static uint32_t count_linear(const uint32_t *words, size_t stride, uint32_t lo, uint32_t hi) {
+        uint32_t c = 0;
+        while (lo < hi) {
+            const uint32_t b = lo & 31, len = std::min(32 - b, hi - lo);
+            const uint32_t w = words[(size_t)(lo >> 5) * stride] >> b;
+            c += (uint32_t)__builtin_popcount(len == 32 ? w : w & ((1u << len) - 1));
+            lo += len;
+        }
+        return c;
+    }
+    // inlier bits of the r positions from p, wrapping at n_
+    uint32_t count_range(const uint32_t *words, size_t stride, uint32_t p, uint32_t r) const {
+        const uint32_t first = std::min(r, n_ - p);
+        return count_linear(words, stride, p, p + first) + count_linear(words, stride, 0, r - first);
+    }
+    // Certificate that the per-point walk from lambda over the r positions from p never sees
+    // next > A.  L bounds log(computed lambda) step by step: a product rounds up by at most a
+    // factor (1 + 2^-53) while normal, and a subnormal or zero result is below T = 2^-1000, so
+    // L_j = max(L_{j-1} + log f_j + u, log T) holds (f = up | down, u >= log(1 + 2^-53)).
+    // Over a run of i inliers and o outliers the process stays below its start (floored at
+    // log T) plus the run's positive terms, and ends below max(start + run sum, log T + the
+    // positive terms).  Runs are the words; the test keeps a margin far above the bound's own
+    // rounding.  false: not proven (the exact walk continues).
+    bool no_crossing(const uint32_t *words, size_t stride, double lambda, double A, double up, double down,
+                     uint32_t p, uint32_t r) const {
+        if (!(A > 0) || !(lambda >= 0)) return false;
+        const double lu = std::log(up), ld = std::log(down), logT = -1000 * 0.6931471805599453;
+        const double la = std::log(A), u = 2.3e-16;
+        const double margin = 1e-6 + 1e-12 * (double)r * (std::fabs(lu) + std::fabs(ld) + 1);
+        if (!std::isfinite(ld) || std::isnan(lu)) return false;
+        double L = lambda > 0 ? std::max(std::log(lambda), logT) : logT;
+        auto runs = [&](uint32_t lo, uint32_t hi) -> bool {
+            while (lo < hi) {
+                const uint32_t b = lo & 31, len = std::min(32 - b, hi - lo);
+                const uint32_t w = words[(size_t)(lo >> 5) * stride] >> b;
+                const uint32_t i = (uint32_t)__builtin_popcount(len == 32 ? w : w & ((1u << len) - 1)), o = len - i;
+                const double pos = (o ? (ld > 0 ? o * ld : 0.0) : 0.0) + (i && lu > 0 ? i * lu : 0.0) + len * u;
+                const double start = std::max(L, logT);
+                if (!(start + pos + margin < la)) return false;
+                const double sum = (i ? i * lu : 0.0) + (o ? o * ld : 0.0) + len * u;  // lu may be -inf
+                L = std::max(start + sum, logT + pos);
+                lo += len;
+            }
+            return true;
+        };
+        const uint32_t first = std::min(r, n_ - p);
+        return runs(p, p + first) && runs(0, r - first);
+    }
     void push(double eps, double delta, int current_hypothese) {
         hist_.push_back(History{eps, delta, thresholdA(eps, delta), current_hypothese - last_update_});
         last_update_ = current_hypothese;
@@ -610,6 +739,7 @@ class Sprt {
     uint32_t n_, m_, max_iters_, idx_ = 0, cur_ = 0;
     int max_before_, last_update_ = 0;
     double t_M_ = 0, m_S_ = 0;
+    bool plain_ = getenv("USAC_SPRT_PLAIN_WALK") != nullptr;
 };
 
 // ---------------------------------------------------------------- NAPSAC (grid)
