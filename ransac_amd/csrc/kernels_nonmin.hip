@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include "usac_device.hpp"
+#include "usac_device_e5.hpp"
 #include "usac_kernels.h"
 #include "usac_seqsum.hpp"
 
@@ -873,6 +874,400 @@ size_t nonminimal_partial_stride(uint32_t nmax) { return 45 * ((size_t)nmax / (6
 
 size_t nonminimal_seq_bytes(uint32_t nmax, uint32_t W) {
     return seq_stride(nmax) * W + sizeof(float) * 6 * W;
+}
+
+// ---------------------------------------------------------------------------------------------
+// The post-loop polish (ransac.cpp:157-207) in ONE workgroup: 4 passes of fit + score + accept
+// were ~56 launches of a few microseconds each (cfg3 exact: 0.28 ms of a 0.72 ms run, round 5),
+// for lists of a few thousand points.  Every value is produced by the same operations in the same
+// order as the multi-launch path (which the oracle pins), so the results are bit-identical:
+//   gather      q[i] = pts[list[i]] into LDS
+//   seq chains  the reference's sequential fp32 sums (4 coordinate means, 2 average distances,
+//               Σerr) by the same speculation as kernels_seqsum.hip, workgroup-sized: a wave per
+//               (chain, segment), a lane per candidate start (64, centred on the fp64 prefix),
+//               a link walk that takes the candidate whose start has the running value's exact
+//               bits, or walks the segment itself
+//   A^T A       the spec's 16-point blocks (ata_group, a wave per group of 9 entries), block
+//               partials summed in order per 1024-point superblock, superblocks in order
+//   fit_finish  as k_dlt_finish / k_fit_small
+//   score       the residuals of all N points in point order (ballot compaction), the list and
+//               the residuals of the inliers, then the Σerr chain
+//   accept      k_polish_prep's decision, kept in registers (uniform over the workgroup)
+// 512 threads: fit_finish's lane-0 inverse iteration needs ~236 VGPRs (2 waves per SIMD).
+constexpr uint32_t kPolT = 512;
+constexpr uint32_t kPolC = 64;  // candidate starts per segment (a wave; 16 left ~25% of the starts outside)
+constexpr uint32_t kPolSbWin = 3;  // A^T A superblocks whose block partials are held at once
+
+struct PolShared {
+    float4 *Q;       // [kPolFitMax]
+    double *D;       // [2 kPolFitMax] distance terms; then A^T A block partials [64][45]; then residuals
+    float *E;        // (aliases D) the inliers' residuals [kPolPtsMax]
+    double *part;    // superblock partials [kPolFitMax / 1024][45]
+    double *psum;    // [8 * 64 / kPolC] fp64 segment sums
+    float *R;        // [kPolT] candidate ends
+    uint32_t *wc;    // [8][8] wave counts
+    uint64_t *dbg;   // USAC_PROFILE: [40 + NCH] link misses, [48 + NCH] segments linked
+};
+
+__device__ __forceinline__ float pol_cand(float ctr, uint32_t c) {
+    return seq::unkey((int32_t)((uint32_t)seq::key(ctr) + c - kPolC / 2));
+}
+
+// the sequential chains s = op(s, v[q * cstride + k]), k = 0 .. n-1, of NCH chains -> out[q]
+// (LDS; chain-major values, 16-byte aligned rows).  Wave w runs chain w % NCH; its lanes form
+// 64 / kPolC groups, a group per segment and a lane per candidate start (kPolC of them, centred
+// on the segment's fp64 prefix: the fp32 chain stayed within a few ulps of it in every cfg3
+// polish measured, round 5); each lane reads a group of its segment's next elements by 16-byte
+// reads issued a group ahead.  A start outside the window is walked by the link (exact either way).
+template <int NCH, bool F64>
+__device__ __forceinline__ void pol_seq(const typename seq::Op<F64>::V *vals, uint32_t cstride, uint32_t n,
+                                        const PolShared &sh, float *out) {
+    typedef seq::Op<F64> Op;
+    typedef typename Op::V V;
+    constexpr uint32_t GPW = 64 / kPolC, S = kPolT / (64 * NCH) * GPW;  // segments per chain
+    constexpr uint32_t kVec = 16 / sizeof(V), G = 8, NV = G / kVec;
+    typedef V Vv __attribute__((ext_vector_type(kVec)));
+    const uint32_t t = threadIdx.x, wave = t / 64, lane = t % 64, grp = lane / kPolC, c = lane % kPolC;
+    const uint32_t q = __builtin_amdgcn_readfirstlane(wave % NCH), jw = __builtin_amdgcn_readfirstlane(wave / NCH);
+    const uint32_t j = jw * GPW + grp;
+    const uint32_t L = ((n + S - 1) / S + G - 1) / G * G;  // a multiple of the group: aligned reads
+    const uint32_t b = j * L < n ? j * L : n, e = b + L < n ? b + L : n;
+    const V *v = vals + (size_t)q * cstride;
+    double a = 0.0;  // the segment's fp64 sum: only places the centres
+    for (uint32_t k = b + c; k < e; k += kPolC) a += Op::wide(v[k]);
+    for (uint32_t o = kPolC / 2; o > 0; o >>= 1) a += __shfl_xor(a, (int)o);
+    if (c == 0) sh.psum[j * NCH + q] = a;
+    __syncthreads();
+    double pre = 0.0;
+    for (uint32_t i = 0; i < j; i++) pre += sh.psum[i * NCH + q];
+    float s = pol_cand((float)pre, c);
+    uint32_t k = b;
+    auto load = [&](Vv (&x)[NV], uint32_t k0) {
+#pragma unroll
+        for (uint32_t u = 0; u < NV; u++) x[u] = *reinterpret_cast<const Vv *>(v + k0 + kVec * u);
+    };
+    if (k + G <= e) {
+        Vv x[NV];
+        load(x, k);
+        for (; k + 2 * G <= e; k += G) {
+            Vv y[NV];
+            load(y, k + G);
+#pragma unroll
+            for (uint32_t u = 0; u < NV; u++)
+#pragma unroll
+                for (uint32_t z = 0; z < kVec; z++) s = Op::step(s, x[u][z]);
+#pragma unroll
+            for (uint32_t u = 0; u < NV; u++) x[u] = y[u];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < NV; u++)
+#pragma unroll
+            for (uint32_t z = 0; z < kVec; z++) s = Op::step(s, x[u][z]);
+        k += G;
+    }
+    for (; k < e; k++) s = Op::step(s, v[k]);
+    sh.R[(j * NCH + q) * kPolC + c] = s;
+    __syncthreads();
+    if (wave < NCH) {  // link: wave q walks chain q's segments (every lane the same value)
+        const V *w = vals + (size_t)wave * cstride;
+        float r = 0.f;
+        double p2 = 0.0;
+        uint32_t miss = 0;
+        for (uint32_t jj = 0; jj < S; jj++) {
+            if (jj) p2 += sh.psum[(jj - 1) * NCH + wave];
+            const uint32_t bb = jj * L < n ? jj * L : n, ee = bb + L < n ? bb + L : n;
+            if (bb >= ee) break;
+            const float ctr = (float)p2;
+            const int64_t idx = (int64_t)seq::key(r) - (int64_t)seq::key(ctr) + (int64_t)(kPolC / 2);
+            bool hit = false;
+            if (idx >= 0 && idx < (int64_t)kPolC && __float_as_uint(pol_cand(ctr, (uint32_t)idx)) == __float_as_uint(r)) {
+                r = sh.R[(jj * NCH + wave) * kPolC + (uint32_t)idx];
+                hit = true;
+            }
+            if (!hit) {
+                miss++;
+                for (uint32_t kk = bb; kk < ee; kk++) r = Op::step(r, w[kk]);
+            }
+        }
+        if (lane == 0) out[wave] = r;
+        if (sh.dbg && lane == 0 && miss)  // USAC_PROFILE: walked segments
+            atomicAdd(reinterpret_cast<unsigned long long *>(sh.dbg + 40 + NCH), (unsigned long long)miss);
+    }
+    __syncthreads();
+}
+
+template <int EST>
+__device__ __forceinline__ float pol_error(const float *m, const float4 p) {
+    if constexpr (EST == USAC_HOMOGRAPHY) return homography_error(m, m + 9, p.x, p.y, p.z, p.w);
+    else if constexpr (EST == USAC_FUNDAMENTAL) return fundamental_error(m, p.x, p.y, p.z, p.w);
+    else return essential_error(m, p.x, p.y, p.z, p.w);
+}
+
+// getInliers of the model in sm_model (H: with its inverse) over all N points: list (global),
+// the residuals (sh.E) in point order; returns the count (uniform)
+template <int EST>
+__device__ __forceinline__ uint32_t pol_score(const float4 *__restrict__ pts, uint32_t N, const float *sm_model, float thr,
+                              int32_t *__restrict__ list, const PolShared &sh) {
+    const uint32_t t = threadIdx.x, wave = t / 64, lane = t % 64;
+    float m[18];
+#pragma unroll
+    for (int k = 0; k < 18; k++) m[k] = sm_model[k];
+    constexpr uint32_t U = 8, W = kPolT / 64;
+    uint32_t base = 0;
+    for (uint32_t c0 = 0; c0 < N; c0 += U * kPolT) {
+        float4 pv[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t i = c0 + u * kPolT + t;
+            pv[u] = i < N ? pts[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        float ev[U];
+        uint64_t bal[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            const uint32_t i = c0 + u * kPolT + t;
+            ev[u] = i < N ? pol_error<EST>(m, pv[u]) : 0.f;
+            bal[u] = __ballot(i < N && ev[u] < thr);
+            if (lane == 0) sh.wc[u * W + wave] = (uint32_t)__popcll(bal[u]);
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t u = 0; u < U; u++) {
+            uint32_t r = base, tot = 0;
+            for (uint32_t v = 0; v < W; v++) {
+                const uint32_t cv = sh.wc[u * W + v];
+                if (v < wave) r += cv;
+                tot += cv;
+            }
+            if ((bal[u] >> lane) & 1ull) {
+                r += (uint32_t)__popcll(bal[u] & ((1ull << lane) - 1));
+                list[r] = (int32_t)(c0 + u * kPolT + t);
+                sh.E[r] = ev[u];
+            }
+            base += tot;
+        }
+        __syncthreads();
+    }
+    return base;
+}
+
+// EstimateModelNonMinimalSample of the n points of list -> sm_model[0..8], *sm_ok (n <= kPolFitMax)
+template <bool FUND>
+__device__ __forceinline__ void pol_fit(const float4 *__restrict__ pts, const int32_t *__restrict__ list, uint32_t n,
+                        const PolShared &sh, float *sm_sums, float *sm_ws, double (*A)[9], double (*V)[9],
+                        double *s_v, float *sm_model, int32_t *sm_ok, uint64_t *st) {
+    const uint32_t t = threadIdx.x;
+    auto stamp = [&](int i) {
+        if (st && t == 0) st[i] = wall_clock64();
+    };
+    float *T = reinterpret_cast<float *>(sh.D);  // the coordinates chain-major [4][kPolFitMax]
+    for (uint32_t i0 = t; i0 < n; i0 += 8 * kPolT) {  // eight dependent loads in flight per thread
+        int32_t ix[8];
+#pragma unroll
+        for (uint32_t u = 0; u < 8; u++) ix[u] = i0 + u * kPolT < n ? list[i0 + u * kPolT] : 0;
+        float4 p[8];
+#pragma unroll
+        for (uint32_t u = 0; u < 8; u++) p[u] = i0 + u * kPolT < n ? pts[ix[u]] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (uint32_t u = 0; u < 8; u++) {
+            const uint32_t i = i0 + u * kPolT;
+            if (i < n) {
+                sh.Q[i] = p[u];
+                T[i] = p[u].x;
+                T[kPolFitMax + i] = p[u].y;
+                T[2 * kPolFitMax + i] = p[u].z;
+                T[3 * kPolFitMax + i] = p[u].w;
+            }
+        }
+    }
+    __syncthreads();
+    stamp(0);
+    if (n == 0) {
+        fit_finish<FUND>(sh.Q, 0, sm_ws, A, V, s_v, sm_model, sm_ok);
+        __syncthreads();
+        return;
+    }
+    const float4 *Q = sh.Q;
+    pol_seq<4, false>(T, kPolFitMax, n, sh, sm_sums);
+    stamp(1);
+    const float mx1 = sm_sums[0] / (float)n, my1 = sm_sums[1] / (float)n;
+    const float mx2 = sm_sums[2] / (float)n, my2 = sm_sums[3] / (float)n;
+    for (uint32_t i = t; i < n; i += kPolT) {  // k_norm_dist's terms
+        const float4 p = Q[i];
+        const float xm1 = p.x - mx1, ym1 = p.y - my1;
+        const float xm2 = p.z - mx2, ym2 = p.w - my2;
+        sh.D[i] = sqrt((double)(xm1 * xm1 + ym1 * ym1));  // chain-major [2][kPolFitMax]
+        sh.D[kPolFitMax + i] = sqrt((double)(xm2 * xm2 + ym2 * ym2));
+    }
+    __syncthreads();
+    stamp(2);
+    pol_seq<2, true>(sh.D, kPolFitMax, n, sh, sm_sums + 4);
+    stamp(3);
+    float t1[9], t2[9];
+    norm_transforms(sm_sums, sm_sums + 4, 0, n, t1, t2);
+    if (t < 9) {
+        sm_ws[t] = t1[t];
+        sm_ws[9 + t] = t2[t];
+    }
+    if (!(FUND ? n <= 8 : 2 * n <= 9)) {
+        const NormXf xf = norm_xf(t1, t2);
+        const uint32_t nblocks = (n + kAtaBlock - 1) / kAtaBlock, nsb = (nblocks + 63) / 64;
+        double *red = sh.D;  // [kPolSbWin][64][45] (the distance terms are consumed)
+        const uint32_t wave = __builtin_amdgcn_readfirstlane(t / 64), bl = t % 64;
+        for (uint32_t w0 = 0; w0 < nsb; w0 += kPolSbWin) {  // a window of superblocks: jobs (sb, group)
+            const uint32_t nwin = nsb - w0 < kPolSbWin ? nsb - w0 : kPolSbWin, jobs = kAtaGroups * nwin;
+            for (uint32_t jb = wave; jb < jobs; jb += kPolT / 64) {  // a wave per job, a lane per block
+                const uint32_t sbl = jb / kAtaGroups, g = jb % kAtaGroups, blk = (w0 + sbl) * 64 + bl;
+                if (blk < nblocks) {
+                    double acc[kAtaPer];
+                    const uint32_t b0 = blk * kAtaBlock, b1 = b0 + kAtaBlock < n ? b0 + kAtaBlock : n;
+                    ata_dispatch<FUND>((int)g, Q, xf, b0, b1, acc);
+#pragma unroll
+                    for (int e = 0; e < kAtaPer; e++) red[(sbl * 64 + bl) * 45 + kAtaPer * g + e] = acc[e];
+                }
+            }
+            __syncthreads();
+            if (t < 45 * nwin) {  // each superblock's blocks in order
+                const uint32_t sbl = t / 45, e = t % 45, sb = w0 + sbl;
+                const uint32_t nb = nblocks - sb * 64 < 64 ? nblocks - sb * 64 : 64;
+                double sum = 0.0;
+                for (uint32_t b = 0; b < nb; b++) sum += red[(sbl * 64 + b) * 45 + e];
+                sh.part[sb * 45 + e] = sum;
+            }
+            __syncthreads();
+        }
+        if (t < 45) {  // k_dlt_finish: the superblock partials in order
+            double acc = 0.0;
+            for (uint32_t c = 0; c < nsb; c++) acc += sh.part[c * 45 + t];
+            int j, k;
+            ata_entry(t, j, k);
+            A[j][k] = acc;
+            A[k][j] = acc;
+        }
+    }
+    __syncthreads();
+    stamp(4);
+    fit_finish<FUND>(Q, n, sm_ws, A, V, s_v, sm_model, sm_ok);
+    __syncthreads();
+    stamp(5);
+}
+
+template <int EST>
+__global__ __launch_bounds__(kPolT) void k_polish_fused(const float4 *__restrict__ pts, uint32_t N,
+                                                        const float *__restrict__ model0, float thr, int32_t best0,
+                                                        uint32_t fit_max, PolLists lists, int32_t *__restrict__ res,
+                                                        uint64_t *__restrict__ dbg) {
+    constexpr bool FUND = EST != USAC_HOMOGRAPHY;
+    __shared__ __attribute__((aligned(16))) float4 s_q[kPolFitMax];
+    __shared__ __attribute__((aligned(16))) double s_d[kPolSbWin * 64 * 45 > 2 * kPolFitMax ? kPolSbWin * 64 * 45
+                                                                                            : 2 * kPolFitMax];
+    __shared__ double s_part[(kPolFitMax / 1024) * 45];
+    __shared__ double A[9][9], V[9][9], s_v[9], s_psum[8 * 64 / kPolC];
+    __shared__ float s_R[kPolT], s_sums[8], s_ws[18], s_model[18], s_sum[1];
+    __shared__ uint32_t s_wc[8 * (kPolT / 64)];
+    __shared__ int32_t s_ok;
+    PolShared sh;  // (not a const aggregate: LDS addresses are no static initializer)
+    sh.Q = s_q;
+    sh.D = s_d;
+    sh.E = reinterpret_cast<float *>(s_d);
+    sh.part = s_part;
+    sh.psum = s_psum;
+    sh.R = s_R;
+    sh.wc = s_wc;
+    sh.dbg = dbg;
+    static_assert(sizeof(double) * 2 * kPolFitMax >= sizeof(float) * kPolPtsMax, "residuals alias the distance terms");
+    const uint32_t t = threadIdx.x;
+    float *resf = reinterpret_cast<float *>(res);
+    auto load_model = [&](const float *mdl) {  // inl_model: the model, H^-1 for H
+        if (t == 0) {
+            for (int k = 0; k < 9; k++) s_model[k] = mdl[k];
+            if (EST == USAC_HOMOGRAPHY) inv3x3(s_model, s_model + 9);
+        }
+        __syncthreads();
+    };
+    auto score = [&](int32_t *list, uint64_t *st) -> uint32_t {
+        const uint32_t cnt = pol_score<EST>(pts, N, s_model, thr, list, sh);
+        if (st && t == 0) st[0] = wall_clock64();
+        pol_seq<1, false>(sh.E, 0, cnt, sh, s_sum);
+        if (st && t == 0) st[1] = wall_clock64();
+        return cnt;
+    };
+    // USAC_PROFILE: wall-clock stamps (dbg[0] start, [1..2] the first getInliers, 8 per pass)
+    if (dbg && t == 0) dbg[0] = wall_clock64();
+    // quality->getInliers(best_model): lists[0], slots 12-13
+    load_model(model0);
+    {
+        const uint32_t c0 = score(lists.l[0], dbg ? dbg + 1 : nullptr);
+        if (t == 0) {
+            res[12] = (int32_t)c0;
+            resf[13] = s_sum[0];
+        }
+    }
+    int32_t best = best0, prev = 0;
+    uint32_t n = (uint32_t)best0;
+    constexpr int kPasses = 4;
+    for (int k = 0; k < kPasses; k++) {
+        if (n > fit_max) {  // workgroup-uniform: the host runs passes k.. the multi-launch way
+            if (t == 0) res[kPolStop] = k;
+            return;
+        }
+        float *pres = resf + kPolPass * k;
+        uint64_t *st = dbg ? dbg + 3 + 8 * k : nullptr;
+        pol_fit<FUND>(pts, lists.l[k], n, sh, s_sums, s_ws, A, V, s_v, s_model, &s_ok, st);
+        const int32_t ok = s_ok;
+        if (t == 0) {
+            if (n > 0)
+                for (int j = 0; j < 9; j++) pres[j] = s_model[j];
+            res[kPolPass * k + 9] = ok;
+        }
+        uint32_t cnt = 0;
+        float sum = 0.f;
+        if (ok) {
+            if (EST == USAC_HOMOGRAPHY && t == 0) inv3x3(s_model, s_model + 9);
+            __syncthreads();
+            cnt = score(lists.l[k + 1], st ? st + 6 : nullptr);
+            sum = s_sum[0];
+        }
+        if (t == 0) {
+            res[kPolPass * k + 10] = (int32_t)cnt;
+            pres[11] = sum;
+        }
+        if (k + 1 < kPasses) {  // k_polish_prep
+            const bool accept = ok && !((double)((float)(int32_t)cnt / (float)best) < 0.8) && (int32_t)cnt > prev;
+            if (t == 0) reinterpret_cast<uint32_t *>(res)[kPolNs + k + 1] = accept ? cnt : 0u;
+            best = accept ? (int32_t)cnt : best;
+            prev = accept ? (int32_t)cnt : prev;
+            if (t == 0) {
+                res[kPolState] = best;
+                res[kPolState + 1] = prev;
+            }
+            n = accept ? cnt : 0u;
+        }
+        __syncthreads();
+    }
+    if (t == 0) res[kPolStop] = kPasses;
+}
+
+hipError_t launch_polish_fused(hipStream_t st, int estimator, const void *pts, uint32_t N, const float *model0,
+                               float thr, int32_t best0, PolLists lists, int32_t *res, uint32_t fit_max,
+                               uint64_t *dbg) {
+    if (fit_max > kPolFitMax) fit_max = kPolFitMax;
+    if (N > kPolPtsMax || best0 < 0 || (uint32_t)best0 > fit_max) return hipErrorInvalidValue;
+    const float4 *p = static_cast<const float4 *>(pts);
+    switch (estimator) {
+        case USAC_HOMOGRAPHY:
+            hipLaunchKernelGGL(k_polish_fused<USAC_HOMOGRAPHY>, dim3(1), dim3(kPolT), 0, st, p, N, model0, thr, best0, fit_max, lists, res, dbg);
+            break;
+        case USAC_FUNDAMENTAL:
+            hipLaunchKernelGGL(k_polish_fused<USAC_FUNDAMENTAL>, dim3(1), dim3(kPolT), 0, st, p, N, model0, thr, best0, fit_max, lists, res, dbg);
+            break;
+        case USAC_ESSENTIAL:
+            hipLaunchKernelGGL(k_polish_fused<USAC_ESSENTIAL>, dim3(1), dim3(kPolT), 0, st, p, N, model0, thr, best0, fit_max, lists, res, dbg);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 }  // namespace usac

@@ -3038,9 +3038,30 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     int32_t *lists[5] = {c->inl_idx.as<int32_t>(), c->pol_lists.as<int32_t>(), nullptr, nullptr, nullptr};
     for (int k = 2; k < 5; k++) lists[k] = lists[1] + (size_t)(k - 1) * std::max<uint32_t>(c->n, 1);
     HIP_TRY(c, hipMemcpyAsync(c->one_model.p, best_model, sizeof(float) * 9, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(c, usac::launch_inliers_batch(c->stream, c->estimator, c->pts.p, c->n, c->one_model.as<float>(), 1, thr,
-                                          nullptr, nullptr, lists[0], 0, dres_i + 12, dres + 13,
-                                          c->inl_scratch.p));  // quality->getInliers(best_model)
+    // USAC_POLISH_FUSED=1: the whole polish in one workgroup (k_polish_fused) when the best
+    // model's list and the point set fit its LDS -- one launch instead of ~56, bit-identical, but
+    // not faster on cfg3 exact (0.30-0.33 vs 0.28 ms: the sequential sums' 64-candidate
+    // speculation needs more than one CU's issue rate), so off by default
+    // (USAC_POLISH_FUSED_MAX: a lower list bound, which makes the tests resume passes the
+    // multi-launch way)
+    const char *fe = getenv("USAC_POLISH_FUSED"), *fm = getenv("USAC_POLISH_FUSED_MAX");
+    const uint32_t fit_max = fm ? std::min<uint32_t>((uint32_t)atoi(fm), usac::kPolFitMax) : usac::kPolFitMax;
+    const bool fused = fe && atoi(fe) != 0 && c->estimator != USAC_LINE2D && c->n <= usac::kPolPtsMax &&
+                       (uint32_t)best.inlier_number <= fit_max;
+    const bool pol_prof = fused && getenv("USAC_PROFILE");
+    if (pol_prof) {
+        HIP_TRY(c, c->partial.reserve(sizeof(uint64_t) * 64));
+        HIP_TRY(c, hipMemsetAsync(c->partial.p, 0, sizeof(uint64_t) * 64, c->stream));
+    }
+    if (fused)
+        HIP_TRY(c, usac::launch_polish_fused(c->stream, c->estimator, c->pts.p, c->n, c->one_model.as<float>(), thr,
+                                             best.inlier_number, usac::PolLists{{lists[0], lists[1], lists[2], lists[3],
+                                                                                 lists[4]}},
+                                             dres_i, fit_max, pol_prof ? c->partial.as<uint64_t>() : nullptr));
+    else
+        HIP_TRY(c, usac::launch_inliers_batch(c->stream, c->estimator, c->pts.p, c->n, c->one_model.as<float>(), 1,
+                                              thr, nullptr, nullptr, lists[0], 0, dres_i + 12, dres + 13,
+                                              c->inl_scratch.p));  // quality->getInliers(best_model)
     // passes go out in groups of G (USAC_POLISH_GROUP): a group is one submission and one host
     // wait; the next group is submitted only while every pass so far was accepted.  Default: all
     // four at once for a best model of <= 8192 inliers (cfg3 exact: 1.15 vs 1.20-1.28 ms per run
@@ -3056,7 +3077,53 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     int32_t cur_cnt = 0;
     int prev = 0;
     bool stop = false;
-    for (int k0 = 0; k0 < kPasses && !stop; k0 += kGroup) {
+    // ransac.cpp:170-200 on the results of passes k0 .. k1 - 1 (pol_pin)
+    auto replay = [&](int k0, int k1) {
+        for (int k = k0; k < k1; k++) {
+            const float *r = hres + usac::kPolPass * k;
+            memcpy(&ok, r + 9, sizeof(int32_t));
+            memcpy(&cnt, r + 10, sizeof(int32_t));
+            memcpy(&s, r + 11, sizeof(float));
+            if (!ok || (double)((float)cnt / (float)best.inlier_number) < 0.8 || cnt <= prev) {
+                stop = true;
+                break;
+            }
+            prev = cnt;
+            best.inlier_number = cnt;
+            best.score = s;
+            memcpy(best_model, r, sizeof(best_model));
+            cur = lists[k + 1];
+            cur_cnt = cnt;
+            out->polish_passes++;
+        }
+    };
+    int k_first = 0;  // the first pass for the multi-launch path
+    if (fused) {
+        HIP_TRY(c, hipMemcpyAsync(c->pol_pin, dres, sizeof(float) * usac::kPolWords, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(c, stream_wait(c->stream));
+        memcpy(&cur_cnt, hres + 12, sizeof(int32_t));
+        memcpy(&k_first, hres + usac::kPolStop, sizeof(int32_t));
+        if (k_first < 0 || k_first > kPasses) return fail(c, USAC_ERR_HIP, "fused polish: bad pass count");
+        replay(0, k_first);
+        if (pol_prof) {  // the fused polish's phases (us): getInliers, then per pass gather, means,
+            // distance terms, distances, A^T A, finish, score, Σerr
+            uint64_t st[64] = {0};
+            HIP_TRY(c, hipMemcpy(st, c->partial.p, sizeof(st), hipMemcpyDeviceToHost));
+            fprintf(stderr, "polish_fused us: init %.1f %.1f |", (st[1] - st[0]) * 0.01, (st[2] - st[1]) * 0.01);
+            uint64_t last = st[2];
+            for (int k = 0; k < k_first; k++) {
+                for (int i = 0; i < 8; i++) {
+                    const uint64_t v = st[3 + 8 * k + i];
+                    fprintf(stderr, " %.1f", v >= last ? (v - last) * 0.01 : -1.0);
+                    if (v >= last) last = v;
+                }
+                fprintf(stderr, " |");
+            }
+            fprintf(stderr, " walked segments: 4ch %llu 2ch %llu 1ch %llu\n", (unsigned long long)st[44],
+                    (unsigned long long)st[42], (unsigned long long)st[41]);
+        }
+    }
+    for (int k0 = k_first; k0 < kPasses && !stop; k0 += kGroup) {
         const int k1 = std::min(k0 + kGroup, kPasses);
         for (int k = k0; k < k1; k++) {
             float *pres = dres + usac::kPolPass * k;
@@ -3074,23 +3141,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                                   c->stream));
         HIP_TRY(c, stream_wait(c->stream));
         if (k0 == 0) memcpy(&cur_cnt, hres + 12, sizeof(int32_t));
-        for (int k = k0; k < k1; k++) {  // ransac.cpp:170-200, on the passes' results
-            const float *r = hres + usac::kPolPass * k;
-            memcpy(&ok, r + 9, sizeof(int32_t));
-            memcpy(&cnt, r + 10, sizeof(int32_t));
-            memcpy(&s, r + 11, sizeof(float));
-            if (!ok || (double)((float)cnt / (float)best.inlier_number) < 0.8 || cnt <= prev) {
-                stop = true;
-                break;
-            }
-            prev = cnt;
-            best.inlier_number = cnt;
-            best.score = s;
-            memcpy(best_model, r, sizeof(best_model));
-            cur = lists[k + 1];
-            cur_cnt = cnt;
-            out->polish_passes++;
-        }
+        replay(k0, k1);
     }
     const auto t1 = std::chrono::steady_clock::now();
     lap(T_POLISH);

@@ -199,8 +199,20 @@ size_t inliers_scratch_bytes(uint32_t n, uint32_t W);
 // the polish result block, int32 / float words: pass k's model[9], ok, count, sum at
 // kPolPass * k (pass 0's slots 12-13: the initial getInliers' count, sum), the fitted point
 // counts of passes 1..3 at kPolNs + k, the device's (best, prev) at kPolState
-constexpr int kPolPass = 16, kPolNs = 64, kPolState = 68, kPolWords = 72;
+constexpr int kPolPass = 16, kPolNs = 64, kPolState = 68, kPolStop = 70, kPolWords = 72;
 hipError_t launch_polish_prep(hipStream_t st, int32_t *res, int k, int32_t best0);
+// The whole polish in one workgroup (kernels_nonmin.hip k_polish_fused): the initial
+// getInliers(model0) into lists[0] and slots 12-13, then passes 0..3 exactly as the multi-launch
+// passes + k_polish_prep write them (fit lists[k], score into lists[k + 1]), while a pass's
+// point count is <= fit_max (<= kPolFitMax); res[kPolStop] = the passes it ran (4: all; the host runs the
+// rest the multi-launch way).  H, F, E on <= kPolPtsMax points; else hipErrorInvalidValue.
+constexpr uint32_t kPolFitMax = 4096, kPolPtsMax = 16384;
+struct PolLists {
+    int32_t *l[5];
+};
+hipError_t launch_polish_fused(hipStream_t st, int estimator, const void *pts, uint32_t N, const float *model0,
+                               float thr, int32_t best0, PolLists lists, int32_t *res,
+                               uint32_t fit_max = kPolFitMax, uint64_t *dbg = nullptr);
 // every point's exact residual under one model (n floats)
 hipError_t launch_point_errors(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *model,
                                float *errors);
