@@ -34,8 +34,14 @@ __global__ __launch_bounds__(64) void k_pool_mask(const void *__restrict__ pool_
                                                   const float *__restrict__ models, size_t stride,
                                                   const uint32_t *__restrict__ list, const uint32_t *__restrict__ list_n,
                                                   uint32_t kmax, float thr, uint32_t *__restrict__ words,
-                                                  uint32_t row_stride, uint32_t wpl) {
+                                                  uint32_t row_stride, uint32_t wpl, PoolTail tail) {
     constexpr int NC = EST == 1 ? 3 : EST == 2 ? 18 : 9;
+    if (tail.dst && blockIdx.y == 0) {  // the batch's other results next to the words (PoolTail)
+        const uint32_t S = tail.S, T = 2 * S + 1 + tail.nmod;
+        for (uint32_t w = blockIdx.x * 64 + threadIdx.x; w < T; w += gridDim.x * 64)
+            tail.dst[w] = w < S ? tail.counts[w] : w == S ? *tail.list_n : w <= 2 * S ? tail.list[w - S - 1]
+                                                                                   : tail.models[w - 2 * S - 1];
+    }
     const uint32_t K = list ? __builtin_amdgcn_readfirstlane(*list_n) : kmax;
     const uint32_t i0 = blockIdx.x * 64;
     if (i0 >= K) return;
@@ -92,7 +98,8 @@ hipError_t launch_gather_points(hipStream_t st, const void *pts, uint32_t cols, 
 
 hipError_t launch_pool_mask(hipStream_t st, int estimator, const void *pool_pts, uint32_t n, const float *models,
                             size_t stride, const uint32_t *list, const uint32_t *list_n, uint32_t kmax, float thr,
-                            uint32_t *words, uint32_t row_stride) {
+                            uint32_t *words, uint32_t row_stride, const PoolTail *tail) {
+    const PoolTail tl = tail ? *tail : PoolTail{nullptr, nullptr, nullptr, nullptr, 0, 0, nullptr};
     // words per lane: kMaskWords, fewer while the grid would hold under ~2048 workgroups (PROSAC's
     // first batches: a few dozen samples, ~100 models -- round 5: all the pool's words at 8 per lane
     // made two workgroup columns of 40 ranges, latency-bound)
@@ -104,19 +111,19 @@ hipError_t launch_pool_mask(hipStream_t st, int estimator, const void *pool_pts,
     switch (estimator) {
         case USAC_LINE2D:
             hipLaunchKernelGGL(k_pool_mask<1>, grid, dim3(64), 0, st, pool_pts, n, models, stride, list, list_n, kmax,
-                               thr, words, row_stride, wpl);
+                               thr, words, row_stride, wpl, tl);
             break;
         case USAC_HOMOGRAPHY:
             hipLaunchKernelGGL(k_pool_mask<2>, grid, dim3(64), 0, st, pool_pts, n, models, stride, list, list_n, kmax,
-                               thr, words, row_stride, wpl);
+                               thr, words, row_stride, wpl, tl);
             break;
         case USAC_FUNDAMENTAL:
             hipLaunchKernelGGL(k_pool_mask<3>, grid, dim3(64), 0, st, pool_pts, n, models, stride, list, list_n, kmax,
-                               thr, words, row_stride, wpl);
+                               thr, words, row_stride, wpl, tl);
             break;
         case USAC_ESSENTIAL:
             hipLaunchKernelGGL(k_pool_mask<4>, grid, dim3(64), 0, st, pool_pts, n, models, stride, list, list_n, kmax,
-                               thr, words, row_stride, wpl);
+                               thr, words, row_stride, wpl, tl);
             break;
         default:
             return hipErrorInvalidValue;

@@ -2583,7 +2583,8 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         sprt.reset(new usac::Sprt(grng, c->estimator, n, m, prm->max_iterations, max_before_sprt(prm)));
         HIP_TRY(c, c->pool_idx.reserve(sizeof(uint32_t) * n));
         HIP_TRY(c, c->pool_pts.reserve(sizeof(float) * c->cols * (size_t)n));
-        HIP_TRY(c, c->masks.reserve(sizeof(uint32_t) * nw * (size_t)batch * spk));
+        // the words [nw][rows], then the batch's PoolTail (2 S + 1 + ncomp S words)
+        HIP_TRY(c, c->masks.reserve(sizeof(uint32_t) * ((size_t)nw + 2 + (size_t)ncomp(c)) * batch * spk + 4));
         HIP_TRY(c, hipMemcpyAsync(c->pool_idx.p, sprt->pool().data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice,
                                   c->stream));
         HIP_TRY(c, usac::launch_gather_points(c->stream, c->pts.p, c->cols, c->pool_idx.as<uint32_t>(), n,
@@ -2597,7 +2598,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     std::vector<float> hsum(SB);
     pinned_vector<float> hmod((size_t)ncomp(c) * SB);
     pinned_vector<uint32_t> hlist(SB + 1);  // the SPRT batch's occupied-slot list, its count at [SB]
-    pinned_vector<uint32_t> hmask(sprt ? (size_t)nw * SB : 0);
+    pinned_vector<uint32_t> hmask(sprt ? ((size_t)nw + 2 + (size_t)ncomp(c)) * SB + 4 : 0);  // words, PoolTail
     std::vector<uint32_t> subset_at(batch), largest_at(batch);
     std::vector<int32_t> last_sample(m, 0);
     // Speculation: the next batch is drawn and solved / scored on its own stream while the
@@ -2798,11 +2799,18 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                                   c->stream));
         HIP_TRY(c, enqueue_solve(c, c->samples.as<int32_t>(), B, 0, iters, nullptr));
         const size_t mstride = (size_t)B * spk;
+        // listed SPRT batches: the slot counts, list and models ride behind the words (PoolTail)
+        const bool tailed = sprt && listed(c) && !getenv("USAC_NO_POOL_TAIL");
+        const size_t tail_off = (size_t)nw * S, tail_words = (2 + (size_t)ncomp(c)) * S + 1;
         if (sprt) {
+            const usac::PoolTail tail{reinterpret_cast<const uint32_t *>(c->counts.p), c->list_n.as<uint32_t>(),
+                                      c->list.as<uint32_t>(), c->models.as<uint32_t>(), (uint32_t)S,
+                                      (uint32_t)(ncomp(c) * S), c->masks.as<uint32_t>() + tail_off};
             HIP_TRY(c, usac::launch_pool_mask(c->stream, c->estimator, c->pool_pts.p, n, c->models.as<float>(), mstride,
                                               listed(c) ? c->list.as<uint32_t>() : nullptr,
                                               listed(c) ? c->list_n.as<uint32_t>() : nullptr, (uint32_t)S, thr,
-                                              c->masks.as<uint32_t>(), listed(c) ? 0u : (uint32_t)S));
+                                              c->masks.as<uint32_t>(), listed(c) ? 0u : (uint32_t)S,
+                                              tailed ? &tail : nullptr));
         } else {  // exact counts from the fast multi-chunk scorer; exact sums below, where needed
             HIP_TRY(c, enqueue_score(c, B, thr, loop_chunks(c, B)));
             HIP_TRY(c, hipMemcpyAsync(hc.data(), c->counts.p, sizeof(int32_t) * S, hipMemcpyDeviceToHost, c->stream));
@@ -2811,9 +2819,38 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         // every copy costs a fixed overhead, 18 per-component copies of a ramp batch cost more
         // than the batch's kernels)
         hst = S;
-        HIP_TRY(c, hipMemcpyAsync(hmod.data(), c->models.p, sizeof(float) * S * ncomp(c), hipMemcpyDeviceToHost,
-                                  c->stream));
-        if (sprt) {
+        if (!tailed)
+            HIP_TRY(c, hipMemcpyAsync(hmod.data(), c->models.p, sizeof(float) * S * ncomp(c), hipMemcpyDeviceToHost,
+                                      c->stream));
+        const uint32_t *htail = nullptr;  // the batch's PoolTail on the host
+        auto untail = [&]() {
+            memcpy(hc.data(), htail, sizeof(int32_t) * S);
+            hlist[SB] = htail[S];
+            memcpy(hlist.data(), htail + S + 1, sizeof(uint32_t) * S);
+            memcpy(hmod.data(), htail + 2 * S + 1, sizeof(float) * S * ncomp(c));
+        };
+        if (tailed) {
+            // small batches (the PROSAC ramp's first ones, where a cfg3 run ends): words and tail in
+            // one copy, one host wait; larger ones: the tail first, then only the rows' words (the
+            // words are packed [nw][rows] on the device: k_pool_mask, row stride 0)
+            const bool whole = (size_t)nw * S * sizeof(uint32_t) <= kMaskWholeCopy;
+            if (whole) {
+                HIP_TRY(c, hipMemcpyAsync(hmask.data(), c->masks.p, sizeof(uint32_t) * (tail_off + tail_words),
+                                          hipMemcpyDeviceToHost, c->stream));
+                HIP_TRY(c, stream_wait(c->stream));
+                htail = hmask.data() + tail_off;
+                untail();
+            } else {
+                HIP_TRY(c, hipMemcpyAsync(hmask.data() + (size_t)nw * SB, c->masks.as<uint32_t>() + tail_off,
+                                          sizeof(uint32_t) * tail_words, hipMemcpyDeviceToHost, c->stream));
+                HIP_TRY(c, stream_wait(c->stream));
+                htail = hmask.data() + (size_t)nw * SB;
+                untail();
+                rows = hlist[SB];
+                if (rows) HIP_TRY(c, hipMemcpyAsync(hmask.data(), c->masks.p, sizeof(uint32_t) * (size_t)rows * nw,
+                                                    hipMemcpyDeviceToHost, c->stream));
+            }
+        } else if (sprt) {
             // listed: the occupied rows' words packed [nw][rows] on the device (k_pool_mask, row
             // stride 0).  Small batches (the PROSAC ramp's first ones, where a cfg3 run ends): the
             // whole block with the list in the same submission -- one host wait; larger ones: the

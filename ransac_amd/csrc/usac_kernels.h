@@ -158,9 +158,16 @@ size_t e5_workspace_bytes(uint32_t B);
 // pool-order inlier words (words[w * row_stride + row], bit b = position 32 w + b)
 hipError_t launch_gather_points(hipStream_t st, const void *pts, uint32_t cols, const uint32_t *idx, uint32_t n,
                                 void *out);
+// tail (optional): the batch's slot counts [S], list count [1], list [S] and models [nmod] copied
+// by the same launch into dst, so the host fetches a batch's results with one copy
+struct PoolTail {
+    const uint32_t *counts, *list_n, *list, *models;
+    uint32_t S, nmod;
+    uint32_t *dst;
+};
 hipError_t launch_pool_mask(hipStream_t st, int estimator, const void *pool_pts, uint32_t n, const float *models,
                             size_t stride, const uint32_t *list, const uint32_t *list_n, uint32_t kmax, float thr,
-                            uint32_t *words, uint32_t row_stride);
+                            uint32_t *words, uint32_t row_stride, const PoolTail *tail = nullptr);
 
 // throughput SPRT (batch-fixed test, decisions = the reference's fp64 product walk from each
 // model's start, kernels_sprt.hip): counts -1 for rejected models, tested_total (nullable)
