@@ -2579,16 +2579,24 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     std::unique_ptr<usac::Sprt> sprt;
     const int max_before = max_before_sprt(prm);
     const uint32_t nw = (n + 31) / 32;
-    if (prm->sprt) {
-        sprt.reset(new usac::Sprt(grng, c->estimator, n, m, prm->max_iterations, max_before_sprt(prm)));
-        HIP_TRY(c, c->pool_idx.reserve(sizeof(uint32_t) * n));
-        HIP_TRY(c, c->pool_pts.reserve(sizeof(float) * c->cols * (size_t)n));
-        // the words [nw][rows], then the batch's PoolTail (2 S + 1 + ncomp S words)
-        HIP_TRY(c, c->masks.reserve(sizeof(uint32_t) * ((size_t)nw + 2 + (size_t)ncomp(c)) * batch * spk + 4));
+    // PROSAC + SPRT on one rank: the pool shuffle (n glibc draws, the sampler has its own
+    // generator) runs after the first batch's solve is enqueued, overlapping it (pool_upload)
+    const bool defer_pool = prm->sprt && prosac && nranks == 1 && !getenv("USAC_NO_DEFER_POOL");
+    auto pool_upload = [&]() -> int {
+        sprt->shuffle_pool();
         HIP_TRY(c, hipMemcpyAsync(c->pool_idx.p, sprt->pool().data(), sizeof(uint32_t) * n, hipMemcpyHostToDevice,
                                   c->stream));
         HIP_TRY(c, usac::launch_gather_points(c->stream, c->pts.p, c->cols, c->pool_idx.as<uint32_t>(), n,
                                               c->pool_pts.p));
+        return USAC_OK;
+    };
+    if (prm->sprt) {
+        sprt.reset(new usac::Sprt(grng, c->estimator, n, m, prm->max_iterations, max_before_sprt(prm), defer_pool));
+        HIP_TRY(c, c->pool_idx.reserve(sizeof(uint32_t) * n));
+        HIP_TRY(c, c->pool_pts.reserve(sizeof(float) * c->cols * (size_t)n));
+        // the words [nw][rows], then the batch's PoolTail (2 S + 1 + ncomp S words)
+        HIP_TRY(c, c->masks.reserve(sizeof(uint32_t) * ((size_t)nw + 2 + (size_t)ncomp(c)) * batch * spk + 4));
+        if (!defer_pool && (rc = pool_upload())) return rc;
     }
 
     const size_t SB = (size_t)batch * spk;  // slot stride of the host copies
@@ -2802,6 +2810,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         // listed SPRT batches: the slot counts, list and models ride behind the words (PoolTail)
         const bool tailed = sprt && listed(c) && !getenv("USAC_NO_POOL_TAIL");
         const size_t tail_off = (size_t)nw * S, tail_words = (2 + (size_t)ncomp(c)) * S + 1;
+        if (sprt && !sprt->pool_ready() && (rc = pool_upload())) return rc;  // deferred: behind the solve
         if (sprt) {
             const usac::PoolTail tail{reinterpret_cast<const uint32_t *>(c->counts.p), c->list_n.as<uint32_t>(),
                                       c->list.as<uint32_t>(), c->models.as<uint32_t>(), (uint32_t)S,

@@ -480,19 +480,13 @@ class Sprt {
         int k;
     };
     // ctor (sprt.hpp:89-175): pool shuffle with points_size draws of the shared stream
+    // defer_pool: the shuffle waits for shuffle_pool() -- for a caller whose next draws of rng
+    // come after it anyway (PROSAC draws from its own generator), to overlap it with device work
     Sprt(GlibcRandom &rng, int estimator, uint32_t points_size, uint32_t sample_size, uint32_t max_iterations,
-         int max_hypothesis_test_before_sprt = 20)
+         int max_hypothesis_test_before_sprt = 20, bool defer_pool = false)
         : pool_(points_size), n_(points_size), m_(sample_size), max_iters_(max_iterations),
-          max_before_(max_hypothesis_test_before_sprt) {
-        for (uint32_t i = 0; i < n_; i++) pool_[i] = i;
-        int max = (int)n_;
-        for (uint32_t i = 0; i < n_; i++) {
-            const uint32_t r = rng.next() % (uint32_t)max;
-            const uint32_t t = pool_[r];
-            max--;
-            pool_[r] = pool_[max];
-            pool_[max] = t;
-        }
+          max_before_(max_hypothesis_test_before_sprt), rng_(&rng) {
+        if (!defer_pool) shuffle_pool();
         double eps0, delta0;
         switch (estimator) {
             case 2: delta0 = 0.01; eps0 = 0.1; t_M_ = 200; m_S_ = 1; break;        // homography
@@ -502,6 +496,20 @@ class Sprt {
         }
         hist_.push_back(History{eps0, delta0, thresholdA(eps0, delta0), 0});
     }
+    void shuffle_pool() {
+        if (!rng_) return;
+        for (uint32_t i = 0; i < n_; i++) pool_[i] = i;
+        int max = (int)n_;
+        for (uint32_t i = 0; i < n_; i++) {
+            const uint32_t r = rng_->next() % (uint32_t)max;
+            const uint32_t t = pool_[r];
+            max--;
+            pool_[r] = pool_[max];
+            pool_[max] = t;
+        }
+        rng_ = nullptr;
+    }
+    bool pool_ready() const { return rng_ == nullptr; }
     const std::vector<uint32_t> &pool() const { return pool_; }
     size_t histories() const { return hist_.size(); }
     double thresholdA0() const { return hist_[0].A; }
@@ -740,6 +748,7 @@ class Sprt {
     int max_before_, last_update_ = 0;
     double t_M_ = 0, m_S_ = 0;
     bool plain_ = getenv("USAC_SPRT_PLAIN_WALK") != nullptr;
+    GlibcRandom *rng_;  // set until the pool is shuffled
 };
 
 // ---------------------------------------------------------------- NAPSAC (grid)
