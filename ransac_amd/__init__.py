@@ -690,8 +690,13 @@ class Ransac:
         L = lib()
         p = _params(self.model)
         out = _RunOutput()
-        inl = np.zeros(self.ctx.n, dtype=np.int32)
-        recs = (Record * rec_cap)()
+        inl = np.empty(self.ctx.n, dtype=np.int32)
+        # the record array is the run's largest host allocation (rec_cap x 56 B, zero-filled): one
+        # per Context and capacity, reused (the records are copied out below)
+        cache = self.ctx.__dict__.setdefault("_rec_bufs", {})
+        recs = cache.get(rec_cap)
+        if recs is None:
+            recs = cache[rec_cap] = (Record * rec_cap)()
         if shard is None:
             rc = L.usac_ransac_run(self.ctx._h, ctypes.byref(p), ctypes.byref(out), _ptr(inl, ctypes.c_int32), recs,
                                    rec_cap)

@@ -12,6 +12,8 @@
 //                 (the reference's order; evaluated in parallel, bit-exactly, by launch_seqsum)
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "usac_device.hpp"
@@ -220,6 +222,14 @@ hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, 
                                 uint32_t W, float thr, const float *thrs, const uint32_t *slots, int32_t *idx,
                                 size_t idx_stride, int32_t *counts, float *sums, void *scratch, const int32_t *ok) {
     if (W == 0) return hipSuccess;
+    // one model with its sum over a few thousand points: one workgroup, one launch (the five
+    // launches below are ~5 us each at this size; USAC_INLIERS_SMALL=0 keeps them)
+    static const bool small_on = [] {
+        const char *e = getenv("USAC_INLIERS_SMALL");
+        return !e || atoi(e) != 0;
+    }();
+    if (small_on && W == 1 && !thrs && !slots && idx && sums && n <= kPolPtsMax && estimator != USAC_LINE2D)
+        return launch_inliers_small(st, estimator, pts, n, models, thr, ok, idx, counts, sums);
     const uint32_t nb = (n + kInlBlock - 1) / kInlBlock;
     uint32_t *scr = static_cast<uint32_t *>(scratch);
     const dim3 grid(nb, W);

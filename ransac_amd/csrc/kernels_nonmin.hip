@@ -1270,4 +1270,67 @@ hipError_t launch_polish_fused(hipStream_t st, int estimator, const void *pts, u
     return hipGetLastError();
 }
 
+// getInliers of ONE model over N <= kPolPtsMax points in one workgroup (pol_score + the Σerr
+// chain), for launch_inliers_batch's single-model calls with sums: one launch instead of five
+// (flags, compact, and the three launches of the Σ chain), the same list, count and sum bits.
+// ok (nullable): a failed fit's slot gets count 0 and sum 0 and its list is left alone.
+template <int EST>
+__global__ __launch_bounds__(kPolT) void k_inliers_small(const float4 *__restrict__ pts, uint32_t N,
+                                                         const float *__restrict__ model, float thr,
+                                                         const int32_t *__restrict__ ok, int32_t *__restrict__ idx,
+                                                         int32_t *__restrict__ count, float *__restrict__ sum) {
+    __shared__ __attribute__((aligned(16))) float s_e[kPolPtsMax];
+    __shared__ double s_psum[8 * 64 / kPolC];
+    __shared__ float s_R[kPolT], s_model[18], s_sum[1];
+    __shared__ uint32_t s_wc[8 * (kPolT / 64)];
+    const uint32_t t = threadIdx.x;
+    if (ok && !*ok) {
+        if (t == 0) {
+            *count = 0;
+            *sum = 0.f;
+        }
+        return;
+    }
+    PolShared sh;
+    sh.Q = nullptr;
+    sh.D = nullptr;
+    sh.E = s_e;
+    sh.part = nullptr;
+    sh.psum = s_psum;
+    sh.R = s_R;
+    sh.wc = s_wc;
+    sh.dbg = nullptr;
+    if (t == 0) {  // inl_model: the model, H^-1 for H
+        for (int k = 0; k < 9; k++) s_model[k] = model[k];
+        if (EST == USAC_HOMOGRAPHY) inv3x3(s_model, s_model + 9);
+    }
+    __syncthreads();
+    const uint32_t cnt = pol_score<EST>(pts, N, s_model, thr, idx, sh);
+    pol_seq<1, false>(s_e, 0, cnt, sh, s_sum);
+    if (t == 0) {
+        *count = (int32_t)cnt;
+        *sum = s_sum[0];
+    }
+}
+
+hipError_t launch_inliers_small(hipStream_t st, int estimator, const void *pts, uint32_t N, const float *model,
+                                float thr, const int32_t *ok, int32_t *idx, int32_t *count, float *sum) {
+    if (N > kPolPtsMax) return hipErrorInvalidValue;
+    const float4 *p = static_cast<const float4 *>(pts);
+    switch (estimator) {
+        case USAC_HOMOGRAPHY:
+            hipLaunchKernelGGL(k_inliers_small<USAC_HOMOGRAPHY>, dim3(1), dim3(kPolT), 0, st, p, N, model, thr, ok, idx, count, sum);
+            break;
+        case USAC_FUNDAMENTAL:
+            hipLaunchKernelGGL(k_inliers_small<USAC_FUNDAMENTAL>, dim3(1), dim3(kPolT), 0, st, p, N, model, thr, ok, idx, count, sum);
+            break;
+        case USAC_ESSENTIAL:
+            hipLaunchKernelGGL(k_inliers_small<USAC_ESSENTIAL>, dim3(1), dim3(kPolT), 0, st, p, N, model, thr, ok, idx, count, sum);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 }  // namespace usac

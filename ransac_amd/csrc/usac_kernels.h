@@ -202,6 +202,10 @@ hipError_t launch_inliers_batch(hipStream_t st, int estimator, const void *pts, 
                                 const int32_t *ok = nullptr);
 hipError_t launch_inliers_sums(hipStream_t st, uint32_t n, uint32_t W, const uint32_t *slots, const int32_t *counts,
                                float *sums, void *scratch);
+// one model's list, count and sum in one workgroup (kernels_nonmin.hip k_inliers_small): H, F, E
+// on n <= kPolPtsMax points; launch_inliers_batch takes it for W = 1 with sums
+hipError_t launch_inliers_small(hipStream_t st, int estimator, const void *pts, uint32_t n, const float *model,
+                                float thr, const int32_t *ok, int32_t *idx, int32_t *count, float *sum);
 size_t inliers_scratch_bytes(uint32_t n, uint32_t W);
 // the polish result block, int32 / float words: pass k's model[9], ok, count, sum at
 // kPolPass * k (pass 0's slots 12-13: the initial getInliers' count, sum), the fitted point
