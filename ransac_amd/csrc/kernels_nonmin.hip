@@ -655,7 +655,7 @@ __global__ __launch_bounds__(64) void k_dlt_finish(const float4 *__restrict__ q_
 // two distance sums as the reference's sequential chains, one lane each (they are short);
 // T1, T2; the normal matrix in the spec's order (16-point blocks in point order, blocks in
 // order: one superblock), lane = entry; fit_finish.  Bit-identical to the multi-launch path.
-constexpr uint32_t kSmallFit = 256;
+constexpr uint32_t kSmallFit = kSmallFitMax;
 static_assert(kSmallFit <= 64 * kAtaBlock, "k_fit_small sums one A^T A superblock");
 
 template <bool FUND>
@@ -806,6 +806,7 @@ hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pt
         return hipGetLastError();
     }
     float4 *q = static_cast<float4 *>(b.q);
+    if (b.skip_finish && (b.W != 1 || b.nmax <= kSmallFit || b.weights || b.prep)) return hipErrorInvalidValue;
     if (b.nmax <= kSmallFit && !b.weights && !b.prep) {  // every fit in one workgroup, one launch
         if (estimator == USAC_HOMOGRAPHY)
             hipLaunchKernelGGL(k_fit_small<false>, dim3(b.W), dim3(64), 0, st, static_cast<const float4 *>(pts), b.base,
@@ -859,13 +860,15 @@ hipError_t launch_nonminimal_batch(hipStream_t st, int estimator, const void *pt
     if (estimator == USAC_HOMOGRAPHY) {
         hipLaunchKernelGGL(k_ata_partial<false>, ga, dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial, b.p_stride,
                            sums4, dsum2, b.ws);
-        hipLaunchKernelGGL(k_dlt_finish<false>, dim3(b.W), dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial,
-                           b.p_stride, b.ws, b.model_out, b.ok);
+        if (!b.skip_finish)
+            hipLaunchKernelGGL(k_dlt_finish<false>, dim3(b.W), dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial,
+                               b.p_stride, b.ws, b.model_out, b.ok);
     } else {
         hipLaunchKernelGGL(k_ata_partial<true>, ga, dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial, b.p_stride,
                            sums4, dsum2, b.ws);
-        hipLaunchKernelGGL(k_dlt_finish<true>, dim3(b.W), dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial,
-                           b.p_stride, b.ws, b.model_out, b.ok);
+        if (!b.skip_finish)
+            hipLaunchKernelGGL(k_dlt_finish<true>, dim3(b.W), dim3(64), 0, st, q, b.q_stride, b.ns, b.n1, b.partial,
+                               b.p_stride, b.ws, b.model_out, b.ok);
     }
     return hipGetLastError();
 }
@@ -1330,6 +1333,94 @@ hipError_t launch_inliers_small(hipStream_t st, int estimator, const void *pts, 
         default:
             return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+// k_dlt_finish + k_inliers_small + k_polish_prep of one polish pass in one workgroup (the three
+// launches' operations in their order, the model kept in LDS between them)
+template <int EST>
+__global__ __launch_bounds__(kPolT) void k_finish_score(const float4 *__restrict__ q, const uint32_t *__restrict__ ns,
+                                                        uint32_t n1, const double *__restrict__ partial,
+                                                        const float *__restrict__ ws, float *__restrict__ model_out,
+                                                        int32_t *__restrict__ ok_out, const float4 *__restrict__ pts,
+                                                        uint32_t N, float thr, int32_t *__restrict__ idx,
+                                                        int32_t *__restrict__ count, float *__restrict__ sum,
+                                                        int32_t *__restrict__ res, int prep_k, int32_t best0) {
+    constexpr bool FUND = EST != USAC_HOMOGRAPHY;
+    __shared__ __attribute__((aligned(16))) float s_e[kPolPtsMax];
+    __shared__ double A[9][9], V[9][9], s_v[9], s_psum[8 * 64 / kPolC];
+    __shared__ float s_R[kPolT], s_model[18], s_sum[1], s_ws[18];
+    __shared__ uint32_t s_wc[8 * (kPolT / 64)];
+    __shared__ int32_t s_ok;
+    const uint32_t t = threadIdx.x;
+    const uint32_t n = ns ? ns[0] : n1;
+    if (t < 18) s_ws[t] = ws[t];
+    if (n > 0 && !(FUND ? n <= 8 : 2 * n <= 9) && t < 45) {  // k_dlt_finish: the superblock partials in order
+        int j, k;
+        ata_entry(t, j, k);
+        const uint32_t nblocks = (n + kAtaBlock * 64 - 1) / (kAtaBlock * 64);
+        double acc = 0.0;
+        for (uint32_t c = 0; c < nblocks; c++) acc += partial[(size_t)c * 45 + t];
+        A[j][k] = acc;
+        A[k][j] = acc;
+    }
+    __syncthreads();
+    fit_finish<FUND>(q, n, s_ws, A, V, s_v, s_model, &s_ok);
+    __syncthreads();
+    const int32_t ok = s_ok;
+    if (t == 0) {
+        if (n > 0)
+            for (int j = 0; j < 9; j++) model_out[j] = s_model[j];
+        *ok_out = ok;
+    }
+    uint32_t cnt = 0;
+    float sm = 0.f;
+    if (ok) {  // k_inliers_small
+        PolShared sh;
+        sh.Q = nullptr;
+        sh.D = nullptr;
+        sh.E = s_e;
+        sh.part = nullptr;
+        sh.psum = s_psum;
+        sh.R = s_R;
+        sh.wc = s_wc;
+        sh.dbg = nullptr;
+        if (EST == USAC_HOMOGRAPHY && t == 0) inv3x3(s_model, s_model + 9);
+        __syncthreads();
+        cnt = pol_score<EST>(pts, N, s_model, thr, idx, sh);
+        pol_seq<1, false>(s_e, 0, cnt, sh, s_sum);
+        sm = s_sum[0];
+    }
+    if (t == 0) {
+        *count = (int32_t)cnt;
+        *sum = sm;
+        if (prep_k >= 0) {  // k_polish_prep
+            const int32_t best = prep_k == 0 ? best0 : res[kPolState];
+            const int32_t prev = prep_k == 0 ? 0 : res[kPolState + 1];
+            const int32_t c = (int32_t)cnt;
+            const bool accept = ok && !((double)((float)c / (float)best) < 0.8) && c > prev;
+            reinterpret_cast<uint32_t *>(res)[kPolNs + prep_k + 1] = accept ? (uint32_t)c : 0u;
+            res[kPolState] = accept ? c : best;
+            res[kPolState + 1] = accept ? c : prev;
+        }
+    }
+}
+
+hipError_t launch_finish_score(hipStream_t st, int estimator, const NmBatch &b, const void *pts, uint32_t N,
+                               float thr, int32_t *idx, int32_t *count, float *sum, int32_t *res, int prep_k,
+                               int32_t best0) {
+    if (N > kPolPtsMax || b.W != 1 || !b.skip_finish) return hipErrorInvalidValue;
+    const float4 *q = static_cast<const float4 *>(b.q), *p = static_cast<const float4 *>(pts);
+#define FS(E)                                                                                                       \
+    hipLaunchKernelGGL(k_finish_score<E>, dim3(1), dim3(kPolT), 0, st, q, b.ns, b.n1, b.partial, b.ws, b.model_out, \
+                       b.ok, p, N, thr, idx, count, sum, res, prep_k, best0)
+    switch (estimator) {
+        case USAC_HOMOGRAPHY: FS(USAC_HOMOGRAPHY); break;
+        case USAC_FUNDAMENTAL: FS(USAC_FUNDAMENTAL); break;
+        case USAC_ESSENTIAL: FS(USAC_ESSENTIAL); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef FS
     return hipGetLastError();
 }
 

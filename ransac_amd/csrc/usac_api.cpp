@@ -791,10 +791,12 @@ hipError_t enqueue_inliers(usac_ctx *c, const float *model_dev, float thr) {
 // ns_dev (nullable): the fit's point count on the device, n then only a bound on it
 hipError_t enqueue_nonminimal(usac_ctx *c, const int32_t *idx_dev, uint32_t n, float *model_out = nullptr,
                               int32_t *ok_out = nullptr, const float *weights_dev = nullptr,
-                              const uint32_t *ns_dev = nullptr) {
+                              const uint32_t *ns_dev = nullptr, usac::NmBatch *batch_out = nullptr) {
     hipError_t e = c->nm_seq.reserve(usac::nonminimal_seq_bytes(n, 1));
     if (e != hipSuccess) return e;
     usac::NmBatch b{};
+    // batch_out: the fit stops before its finish (NmBatch::skip_finish) and the batch is handed
+    // back for launch_finish_score
     b.seq = c->nm_seq.p;
     b.base = idx_dev;
     b.n1 = n;
@@ -812,6 +814,8 @@ hipError_t enqueue_nonminimal(usac_ctx *c, const int32_t *idx_dev, uint32_t n, f
         b.weights = weights_dev;
         b.qw = c->nm_qw.p;
     }
+    b.skip_finish = batch_out != nullptr;
+    if (batch_out) *batch_out = b;
     return usac::launch_nonminimal_batch(c->stream, c->estimator, c->pts.p, b);
 }
 
@@ -3144,6 +3148,9 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         }
     };
     int k_first = 0;  // the first pass for the multi-launch path
+    // USAC_FINISH_SCORE=0: each pass's finish, scoring and acceptance as three launches
+    const char *fse = getenv("USAC_FINISH_SCORE");
+    const bool finish_score = !(fse && atoi(fse) == 0) && c->estimator != USAC_LINE2D && c->n <= usac::kPolPtsMax;
     if (fused) {
         HIP_TRY(c, hipMemcpyAsync(c->pol_pin, dres, sizeof(float) * usac::kPolWords, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(c, stream_wait(c->stream));
@@ -3174,11 +3181,23 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
         for (int k = k0; k < k1; k++) {
             float *pres = dres + usac::kPolPass * k;
             int32_t *dok = dres_i + usac::kPolPass * k + 9;
+            // the pass's finish, scoring and acceptance in one workgroup (k_finish_score) when the
+            // points fit its LDS and the fit takes the multi-launch path
+            const uint32_t nfit = k == 0 ? (uint32_t)best.inlier_number : c->n;
+            const bool fs = finish_score && nfit > usac::kSmallFitMax;
+            usac::NmBatch nb{};
             if (k == 0)
-                HIP_TRY(c, enqueue_nonminimal(c, lists[0], (uint32_t)best.inlier_number, pres, dok));
+                HIP_TRY(c, enqueue_nonminimal(c, lists[0], nfit, pres, dok, nullptr, nullptr, fs ? &nb : nullptr));
             else  // the count pass k - 1's acceptance left on the device; c->n bounds it
-                HIP_TRY(c, enqueue_nonminimal(c, lists[k], c->n, pres, dok, nullptr,
-                                              reinterpret_cast<const uint32_t *>(dres_i + usac::kPolNs + k)));
+                HIP_TRY(c, enqueue_nonminimal(c, lists[k], nfit, pres, dok, nullptr,
+                                              reinterpret_cast<const uint32_t *>(dres_i + usac::kPolNs + k),
+                                              fs ? &nb : nullptr));
+            if (fs) {
+                HIP_TRY(c, usac::launch_finish_score(c->stream, c->estimator, nb, c->pts.p, c->n, thr, lists[k + 1],
+                                                     dok + 1, pres + 11, dres_i, k + 1 < kPasses ? k : -1,
+                                                     best.inlier_number));
+                continue;
+            }
             HIP_TRY(c, usac::launch_inliers_batch(c->stream, c->estimator, c->pts.p, c->n, pres, 1, thr, nullptr,
                                                   nullptr, lists[k + 1], 0, dok + 1, pres + 11, c->inl_scratch.p, dok));
             if (k + 1 < kPasses) HIP_TRY(c, usac::launch_polish_prep(c->stream, dres_i, k, best.inlier_number));

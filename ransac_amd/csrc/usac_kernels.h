@@ -218,9 +218,19 @@ hipError_t launch_polish_prep(hipStream_t st, int32_t *res, int k, int32_t best0
 // point count is <= fit_max (<= kPolFitMax); res[kPolStop] = the passes it ran (4: all; the host runs the
 // rest the multi-launch way).  H, F, E on <= kPolPtsMax points; else hipErrorInvalidValue.
 constexpr uint32_t kPolFitMax = 4096, kPolPtsMax = 16384;
+constexpr uint32_t kSmallFitMax = 256;  // kernels_nonmin.hip kSmallFit: fits of at most this many points take k_fit_small
 struct PolLists {
     int32_t *l[5];
 };
+// One polish pass's tail in one workgroup (kernels_nonmin.hip k_finish_score): the fit's finish
+// (as k_dlt_finish, from b's partials / q / ws, after launch_nonminimal_batch with skip_finish),
+// the fitted model's getInliers over N <= kPolPtsMax points (as k_inliers_small, gated on the
+// fit's ok) into idx / count / sum, and, when prep_k >= 0, k_polish_prep(res, prep_k, best0).
+// Fundamental / essential / homography fits of more than kSmallFit points (W = 1).
+struct NmBatch;
+hipError_t launch_finish_score(hipStream_t st, int estimator, const NmBatch &b, const void *pts, uint32_t N,
+                               float thr, int32_t *idx, int32_t *count, float *sum, int32_t *res, int prep_k,
+                               int32_t best0);
 hipError_t launch_polish_fused(hipStream_t st, int estimator, const void *pts, uint32_t N, const float *model0,
                                float thr, int32_t best0, PolLists lists, int32_t *res,
                                uint32_t fit_max = kPolFitMax, uint64_t *dbg = nullptr);
@@ -270,6 +280,8 @@ struct NmBatch {
     // counts and the stage's thresholds from the previous stage's outputs, computed by the
     // gather itself (see LoPrep) and written to ns (then read by every later kernel) / thr
     const struct LoPrep *prep;
+    // the multi-launch path stops after the A^T A partials: launch_finish_score takes the finish
+    bool skip_finish;
 };
 // ns[w] = cnt[w] while chain w may continue -- it was fitted (ns_prev > 0), its fit
 // succeeded, it kept more than m inliers and (compare: after an iterative step) not fewer
