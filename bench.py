@@ -649,9 +649,11 @@ def cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank):
     # parity of that run: iterations, LO counters, model, inliers
     ref = O.ransac_run(O.HOMOGRAPHY, pts, args.threshold, 0.95, args.seed, sampler=O.SAMPLER_NAPSAC, sprt=False,
                        lo=args.lo, max_iters=max_iters)
-    roof = valu_roofline("void usac::k_score_hf<8, false>", n, B, score_ms) or {
+    # the batch scorer of this context is the matrix-core prefilter (kernels_h16.hip, the cfg2
+    # scorer): its PMC summary at N = 100k (tools/profile_round.sh h100k) prices the timed launches
+    roof = valu_roofline("void usac::k_score_h16<2, 1, 8>(", n, B, score_ms) or {
         "bound": "valu", "achieved": None, "peak": SIMD_CYCLES_S, "unit": "SIMD-cycles/s", "frac": None}
-    roof.update({"traffic": roof.get("hbm", {}).get("traffic_bytes_per_launch"), "kernel": "k_score_hf<8,false>",
+    roof.update({"traffic": roof.get("hbm", {}).get("traffic_bytes_per_launch"), "kernel": "k_score_h16<2,1,8>",
                  "kernel_ms": score_ms, "hypotheses_per_launch": B,
                  "algorithmic_bytes_per_hypothesis": bytes_per_hyp, "algorithmic_equiv_gbs": achieved,
                  "note": "score kernel of one %d-hypothesis batch at N = %d (the loop's batched verify), VALU-issue "
