@@ -734,11 +734,12 @@ def cfg3_exact_main(args, usac, synthetic, dist, torch, world, rank, local_rank)
     n = args.points
     pts, _, _ = synthetic.fundamental_points(n=n, inlier_ratio=0.3, seed=args.seed)  # quality-sorted (PROSAC)
 
-    def model(seed):
-        mdl = usac.Model(args.threshold, 7, 0.95, 7, usac.ESTIMATOR.Fundamental, usac.SAMPLER.Prosac)
-        mdl.ResetRandomGenerator(False)
+    mdl = usac.Model(args.threshold, 7, 0.95, 7, usac.ESTIMATOR.Fundamental, usac.SAMPLER.Prosac)
+    mdl.ResetRandomGenerator(False)
+    mdl.setSprt(True)
+
+    def model(seed):  # one parameter object, re-seeded per run (usac.Model.setSeed)
         mdl.setSeed(seed)
-        mdl.setSprt(True)
         return mdl
 
     ctx = usac.Context(usac.ESTIMATOR.Fundamental, pts, device=local_rank)  # one context, runs back to back
