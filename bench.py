@@ -753,7 +753,7 @@ def cfg3_exact_main(args, usac, synthetic, dist, torch, world, rank, local_rank)
         one_run(10_000 + i)
     if world > 1:
         dist.barrier()
-    iters, rejected, batches, lib_us = 0, 0, 0, 0
+    iters, rejected, batches, lib_us, rewinds = 0, 0, 0, 0, 0
     t0 = time.perf_counter()
     for step in range(args.steps):
         r = one_run(args.seed + step * world + rank)
@@ -761,6 +761,7 @@ def cfg3_exact_main(args, usac, synthetic, dist, torch, world, rank, local_rank)
         iters += out.getNumberOfMainIterations()
         rejected += out.raw["sprt_rejected"]
         batches += out.raw["batches"]
+        rewinds += out.raw["rollbacks"]
         lib_us += out.getTimeMicroSeconds()
     if world > 1:
         dist.barrier()
@@ -815,6 +816,9 @@ def cfg3_exact_main(args, usac, synthetic, dist, torch, world, rank, local_rank)
         "parity": parity,
         "run_stats": {"iterations_per_run": iters / world / args.steps, "sprt_rejected": rejected,
                       "batches": batches,
+                      # PROSAC redraws: a best update that shrinks the termination length below a
+                      # later sample's subset cuts the batch there (a new device batch follows)
+                      "prosac_rewinds": rewinds,
                       # rank 0's usac_ransac_run wall time per run (RansacOutput.getTimeMicroSeconds:
                       # argument checks to the polish's end) beside the line's per-run wall time
                       "library_ms_per_run": lib_us / 1e3 / args.steps},
