@@ -3024,11 +3024,13 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                 nrec++;
             }
             iters++;
-            if (prosac && pterm->terminationLength() != gen_term) {
-                // would any later sample of the batch be drawn differently?
+            if (prosac && pterm->terminationLength() != gen_term && j + 1 < B) {
+                // would the NEXT sample be drawn differently (prosac_sampler.hpp: a subset above the
+                // termination length takes the uniform draw)?  The subsets only grow and the length
+                // only shrinks, so the batch's samples stay valid up to the first one that would --
+                // the replay goes on through them (the run often ends there) and rewinds at it
                 const uint32_t tl = pterm->terminationLength();
-                for (uint32_t k = j + 1; k < B && !rewind; k++)
-                    rewind = (subset_at[k] > gen_term) || (subset_at[k] > tl);
+                rewind = (subset_at[j + 1] > gen_term) || (subset_at[j + 1] > tl);
                 if (rewind) break;
             }
         }
