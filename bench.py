@@ -599,9 +599,13 @@ def cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank):
         dist.all_gather(parts, t)
         return [p.numpy().tobytes() for p in parts]
 
+    # replicas: one context per rank on its own device, runs back to back on it (the points stay
+    # in HBM and the context's device NAPSAC grid is built once per cell size)
+    run_ctx = None if sharded else usac.Context(usac.ESTIMATOR.Homography, pts, device=local_rank)
+
     def one_run(seed):
         if not sharded:
-            r = usac.Ransac(model(seed), pts)
+            r = usac.Ransac(model(seed), pts, ctx=run_ctx)
             r.run()
             return r.getRansacOutput()
         r = usac.Ransac(model(seed), pts, ctx=comm_ctx)
