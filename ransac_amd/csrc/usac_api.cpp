@@ -320,6 +320,10 @@ struct usac_ctx {
     int32_t *grid_members() const { return reinterpret_cast<int32_t *>(grid_csr.as<uint32_t>() + 2 * (size_t)n); }
     uint32_t *grid_start() const { return grid_csr.as<uint32_t>() + 3 * (size_t)n; }
     int grid_cs = 0;        // cell size the grid was built for (0 = none)
+    uint64_t grid_gen = 0;  // bumped at every (re)build of the device grid
+    // the host copy of the grid (download_grid), reused while grid_gen is unchanged
+    std::shared_ptr<const usac::GridNeighbors> grid_host;
+    uint64_t grid_host_gen = ~0ull;
     int cell_size = 50;     // model.hpp:43, the device NAPSAC sampler's grid
     uint32_t grid_n_cells = 0, grid_n_elig = 0;
     DevBuf gc_err;           // graph-cut LO: residuals of the model being labelled
@@ -514,6 +518,7 @@ int host_grid(usac_ctx *c, int cs) {
     c->grid_n_cells = nc;
     c->grid_n_elig = (uint32_t)elig.size();
     c->grid_cs = cs;
+    c->grid_gen++;
     return USAC_OK;
 }
 
@@ -548,24 +553,31 @@ int ensure_grid(usac_ctx *c, int cs) {
     HIP_TRY(c, c->grid_csr.reserve(sizeof(uint32_t) * (4 * n + 1)));
     HIP_TRY(c, c->grid_elig.reserve(sizeof(int32_t) * n));
     c->grid_cs = 0;
+    c->grid_gen++;
     if (!packable) return host_grid(c, cs);
     if (!c->grid_pin && !(c->grid_pin = static_cast<uint32_t *>(PinnedPool::get().take(64, &c->grid_pin_bytes))))
         return fail(c, USAC_ERR_HIP, "pinned host allocation failed");
     HIP_TRY(c, c->grid_ws.reserve(usac::grid_workspace_bytes(c->n)));
     c->grid_cs = 0;
+    c->grid_gen++;
     HIP_TRY(c, usac::build_grid(c->stream, c->pts.as<float4>(), c->n, cs, make_int4(lo[0], lo[1], lo[2], lo[3]),
                                 make_int4(bits[0], bits[1], bits[2], bits[3]), c->m, c->grid_ws.p,
                                 c->grid_cell(), c->grid_rank(), c->grid_start(), c->grid_members(),
                                 c->grid_elig.as<int32_t>(), c->grid_pin,
                                 &c->grid_n_cells, &c->grid_n_elig));
     c->grid_cs = cs;
+    c->grid_gen++;
     return USAC_OK;
 }
 
 // the device grid as the host loop's GridNeighbors (bit-identical to building it on the host)
-int download_grid(usac_ctx *c, int cs, std::unique_ptr<usac::GridNeighbors> &out) {
+int download_grid(usac_ctx *c, int cs, std::shared_ptr<const usac::GridNeighbors> &out) {
     int rc = ensure_grid(c, cs);
     if (rc) return rc;
+    if (c->grid_host && c->grid_host_gen == c->grid_gen) {  // the same device grid: its host copy
+        out = c->grid_host;
+        return USAC_OK;
+    }
     // DMA into one pinned block, then into the host vectors (the sampler reads them at random:
     // they should be cache-warm, which DMA-written pinned memory is not)
     const size_t n = c->n, nc1 = (size_t)c->grid_n_cells + 1;
@@ -582,7 +594,10 @@ int download_grid(usac_ctx *c, int cs, std::unique_ptr<usac::GridNeighbors> &out
     HIP_TRY(c, stream_wait(c->stream));
     std::vector<uint32_t> cell(w, w + n), rank(w + n, w + 2 * n), start(w + 3 * n, w + 3 * n + nc1);
     std::vector<int32_t> members(reinterpret_cast<const int32_t *>(w + 2 * n), reinterpret_cast<const int32_t *>(w + 3 * n));
-    out.reset(new usac::GridNeighbors(std::move(cell), std::move(rank), std::move(start), std::move(members)));
+    out = std::make_shared<const usac::GridNeighbors>(std::move(cell), std::move(rank), std::move(start),
+                                                      std::move(members));
+    c->grid_host = out;
+    c->grid_host_gen = c->grid_gen;
     return USAC_OK;
 }
 
@@ -2538,7 +2553,7 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
     std::unique_ptr<usac::UniformSampler> uni;
     std::unique_ptr<usac::ProsacSampler> pro;
     std::unique_ptr<usac::ProsacTerminationCriteria> pterm;
-    std::unique_ptr<usac::GridNeighbors> grid;
+    std::shared_ptr<const usac::GridNeighbors> grid;
     std::unique_ptr<usac::NapsacSampler> nap;
     std::unique_ptr<usac::NapsacKnnSampler> napk;
     std::vector<int32_t> knn_tab;
@@ -3369,7 +3384,7 @@ struct usac_sampler {
     uint32_t n = 0, m = 0;
     std::unique_ptr<usac::UniformSampler> uni;
     std::unique_ptr<usac::ProsacSampler> pro;
-    std::unique_ptr<usac::GridNeighbors> grid;
+    std::shared_ptr<const usac::GridNeighbors> grid;
     std::unique_ptr<usac::NapsacSampler> nap;
     std::vector<int32_t> knn_tab;
     std::unique_ptr<usac::NapsacKnnSampler> napk;
@@ -3415,7 +3430,7 @@ struct usac_lo {
     std::unique_ptr<LoRansac> lo;
     std::unique_ptr<GcLo> gc;
     std::vector<int32_t> knn_tab;
-    std::unique_ptr<usac::GridNeighbors> grid;
+    std::shared_ptr<const usac::GridNeighbors> grid;
 };
 
 namespace {
