@@ -215,3 +215,37 @@ def test_prosac_sprt_mask_inlier_lists(usac, oracle, kind):
             runs.append((out.getNumberOfMainIterations(), r.records, out.raw["prosac_term_len"]))
         assert runs[0] == runs[1], seed
         assert runs[0][0] == ref["iters"] and runs[0][2] == ref["prosac_term_len"], seed
+
+
+def test_sprt_batch_copy_paths_identical(usac, oracle):
+    """PROSAC + SPRT runs with the round-5 host paths switched off one by one -- the batch's
+    counts / list / models copied behind its mask words (USAC_NO_POOL_TAIL), the pool shuffle
+    behind the first solve (USAC_NO_DEFER_POOL), the inlier lists decoded from the masks
+    (USAC_DEVICE_INLIERS), the word-run SPRT walk (USAC_SPRT_PLAIN_WALK) -- give the same runs,
+    equal to the oracle's; batches of 64 and 1024 (the split and the whole mask copy)."""
+    import os
+    for seed in (1, 2):
+        pts = _data("F", seed, True)
+        ref = oracle.ransac_run(oracle.FUNDAMENTAL, pts, 2.0, 0.95, seed, sampler=oracle.SAMPLER_PROSAC, sprt=True)
+        for batch in (64, 1024):
+            runs = []
+            for env in (None, "USAC_NO_POOL_TAIL", "USAC_NO_DEFER_POOL", "USAC_DEVICE_INLIERS", "USAC_SPRT_PLAIN_WALK"):
+                if env:
+                    os.environ[env] = "1"
+                try:
+                    m = usac.Model(2.0, 7, 0.95, 7, usac.ESTIMATOR.Fundamental, usac.SAMPLER.Prosac)
+                    m.ResetRandomGenerator(False)
+                    m.setSeed(seed)
+                    m.setSprt(True)
+                    m.batch = batch
+                    r = usac.Ransac(m, pts)
+                    r.run()
+                finally:
+                    if env:
+                        os.environ.pop(env, None)
+                o = r.getRansacOutput()
+                runs.append((o.getNumberOfMainIterations(), r.records, o.raw["sprt_rejected"],
+                             o.raw["prosac_term_len"], _bits(o.getModel()).tolist(), o.getInliers().tolist()))
+            assert all(x == runs[0] for x in runs[1:]), (seed, batch)
+            assert runs[0][0] == ref["iters"] and runs[0][3] == ref["prosac_term_len"], (seed, batch)
+            assert runs[0][5] == list(ref["inlier_idx"]), (seed, batch)
