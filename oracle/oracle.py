@@ -344,12 +344,40 @@ def e5_poly(est, sample):
 
 
 def real_roots(coeffs):
-    """real roots (ascending) of sum coeffs[i] z^i (the 5-pt solver's root finder)"""
+    """real zeros of sum coeffs[i] z^i (degree <= 10) in the order the 5-pt solver's Jenkins-Traub
+    root step finds them (usac_oracle.c jt_rpoly; five_points.cpp:143-157)"""
     a = np.ascontiguousarray(coeffs, dtype=np.float64)
     r = np.zeros(max(len(a) - 1, 1), dtype=np.float64)
     k = lib().orc_real_roots(a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), len(a) - 1,
                              r.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
     return r[:k].copy()
+
+
+def rpoly_zeros(coeffs):
+    """every zero the oracle's rpoly restatement reports (real, imaginary parts), in its order"""
+    L = lib()
+    _d = ctypes.POINTER(ctypes.c_double)
+    L.orc_rpoly_zeros.restype = ctypes.c_int
+    L.orc_rpoly_zeros.argtypes = [_d, ctypes.c_int, _d, _d]
+    a = np.ascontiguousarray(coeffs, dtype=np.float64)
+    zr = np.zeros(10)
+    zi = np.zeros(10)
+    k = max(L.orc_rpoly_zeros(a.ctypes.data_as(_d), len(a) - 1, zr.ctypes.data_as(_d), zi.ctypes.data_as(_d)), 0)
+    return zr[:k].copy(), zi[:k].copy()
+
+
+def jt_log(x):
+    L = lib()
+    L.orc_jt_log.restype = ctypes.c_double
+    L.orc_jt_log.argtypes = [ctypes.c_double]
+    return L.orc_jt_log(float(x))
+
+
+def jt_exp(y):
+    L = lib()
+    L.orc_jt_exp.restype = ctypes.c_double
+    L.orc_jt_exp.argtypes = [ctypes.c_double]
+    return L.orc_jt_exp(float(y))
 
 
 def cubic_roots(c0, c1, c2, c3):

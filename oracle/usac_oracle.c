@@ -1392,114 +1392,521 @@ static int null10(double A[10][10], double *v) {
     return 1;
 }
 
-/* Horner with fused multiply-adds (fma: one IEEE rounding, as v_fma_f64 on the device) */
-static double poly_eval(const double *c, int deg, double x) {
-    double r = c[deg];
-    for (int i = deg - 1; i >= 0; i--) r = fma(r, x, c[i]);
+/* ---- 5-pt root step: the reference's Jenkins-Traub zeros, in the order it finds them.
+ * Solve5PointEssential hands det M(z)'s coefficients to rpoly_ak1 (five_points.cpp:139-157;
+ * usac/estimator/essential/rpoly.cpp:7-750, the akiti.ca C++ rendering of Jenkins & Traub's
+ * RPOLY, ACM TOMS 493) and keeps the zeros whose imaginary part is exactly 0 in the order rpoly
+ * deflates them; the first of those whose E passes cheirality is the model (:239-273).  So the
+ * order is part of the result, and it is only reproducible by running the same iteration: it is
+ * restated here operation for operation (same expression shapes, no FMA contraction,
+ * correctly rounded division / sqrt).  rpoly's only library calls besides sqrt are log / exp in
+ * its scaling factor and root bound (rpoly.cpp:82,98): glibc's are not correctly rounded
+ * (measured here: exp differs from the correctly rounded value on ~7e-4 of arguments, log on
+ * ~5e-6), so the restatement uses one portable correctly rounded pair (double-double series,
+ * jt_log / jt_exp) that the device repeats bit for bit; where glibc's last bit differs, the bound
+ * `bnd` -- only the start of the fixed shifts -- differs in its last bits and the zeros agree to
+ * rounding (tests/test_oracle_essential.py pins the order and values against oracle/_ref's
+ * compiled rpoly.cpp).  Safety caps the reference lacks: non-finite coefficients give no zeros
+ * (the reference's bounded loops all fail on NaN, rpoly.cpp:214-220), and the bound's chop /
+ * Newton loops stop after 2100 / 500 trips (they converge in a few dozen for any finite input). */
+typedef struct {
+    double hi, lo;
+} jt_dd;
+
+static jt_dd jt_sum(double a, double b) { /* exact a + b */
+    const double s = a + b, bb = s - a;
+    const jt_dd r = {s, (a - (s - bb)) + (b - bb)};
     return r;
 }
-
-/* Root refinement inside a sign-changing bracket (monotone there): safeguarded Newton in the
- * manner of rtsafe, started at the secant (regula falsi) point of the bracket -- a Newton
- * step when it stays strictly inside the bracket and at least halves the previous step
- * (|2f| <= |dxold f'|), else bisection; the bracket is tightened at every evaluation.  Stops
- * on an exact zero, a Newton step below 2^-50 |x| (the root to a few ulp; its end point is
- * taken when inside the bracket), an unsplittable bracket, or 200 evaluations.  p and p' by one fused Horner pass. */
-static void poly_eval2(const double *c, int deg, double x, double *f, double *df) {
-    double v = c[deg], d = 0.0;
-    for (int j = deg - 1; j >= 0; j--) {
-        d = fma(d, x, v);
-        v = fma(v, x, c[j]);
-    }
-    *f = v;
-    *df = d;
-}
-
-static double poly_refine(const double *c, int deg, double lo, double hi, double flo, double fhi) {
-    double x = lo - flo * ((hi - lo) / (fhi - flo));
-    if (!(x > lo && x < hi)) x = 0.5 * (lo + hi);
-    double dxold = hi - lo, dx = dxold, f, df;
-    poly_eval2(c, deg, x, &f, &df);
-    for (int it = 0; it < 200; it++) {
-        if (f == 0.0) return x;
-        if ((f < 0.0) == (flo < 0.0)) {
-            lo = x;
-            flo = f;
-        } else {
-            hi = x;
-        }
-        const double step = f / df;
-        const double xn = x - step;
-        const int inside = xn > lo && xn < hi;
-        if (xn == x || fabs(step) <= 0x1p-50 * fabs(x)) return inside ? xn : x;
-        const int newton = inside && !(fabs(2.0 * f) > fabs(dxold * df));
-        dxold = dx;
-        if (newton) {
-            dx = step;
-            x = xn;
-        } else {
-            const double mid = 0.5 * (lo + hi);
-            if (!(mid > lo && mid < hi)) return mid;
-            dx = mid - x;
-            x = mid;
-        }
-        poly_eval2(c, deg, x, &f, &df);
-    }
-    return x;
-}
-
-/* root bound with IEEE operations only: the smallest r = 2^k (k >= 0) with
- * |a_n| r > sum_i |a_i| r^(i-n+1) (then no root has |z| >= r) */
-static double root_bound(const double *a, int n) {
-    double r = 1.0;
-    const double an = fabs(a[n]);
-    for (int it = 0; it < 2100; it++) {
-        double t = fabs(a[0]);
-        for (int i = 1; i < n; i++) t = t / r + fabs(a[i]);
-        if (an * r > t) break;
-        r = r * 2.0;
-    }
+static jt_dd jt_qsum(double a, double b) { /* exact a + b for |a| >= |b| */
+    const double s = a + b;
+    const jt_dd r = {s, b - (s - a)};
     return r;
 }
+static jt_dd jt_dadd(jt_dd x, jt_dd y) {
+    jt_dd s = jt_sum(x.hi, y.hi);
+    const jt_dd t = jt_sum(x.lo, y.lo);
+    s.lo += t.hi;
+    s = jt_qsum(s.hi, s.lo);
+    s.lo += t.lo;
+    return jt_qsum(s.hi, s.lo);
+}
+static jt_dd jt_dmul(jt_dd x, jt_dd y) {
+    const double p = x.hi * y.hi;
+    double e = fma(x.hi, y.hi, -p);
+    e += x.hi * y.lo + x.lo * y.hi;
+    return jt_qsum(p, e);
+}
+static jt_dd jt_inv(double k) { /* 1 / k as a double-double (k a small integer) */
+    const double h = 1.0 / k;
+    const jt_dd r = {h, fma(-h, k, 1.0) / k};
+    return r;
+}
+static const jt_dd JT_LN2 = {0x1.62e42fefa39efp-1, 0x1.abc9e3b39803fp-56};
 
-/* real roots of a[0] + a[1] z + ... + a[n] z^n, ascending (<= n) */
-static int real_roots(const double *a_in, int n, double *roots) {
-    while (n > 0 && a_in[n] == 0.0) n--;
-    if (n == 0) return 0;
-    const double R = root_bound(a_in, n);
-    /* level g works on the derivative of order n-g (degree g) and leaves exactly g points,
-     * ascending: the root of each sign-changing interval, or the interval's left end as a
-     * filler where it has none (fillers only split monotone intervals further, and keep the
-     * per-level counts fixed) */
-    double crit[10], next[10];
-    int found[10] = {0};
-    for (int g = 1; g <= n; g++) {
-        const int d = n - g;
-        double c[11];
-        for (int j = 0; j <= g; j++) {
-            double f = 1.0;
-            for (int m = j + d; m > j; m--) f *= (double)m;
-            c[j] = a_in[j + d] * f;
+/* log x correctly rounded (x > 0 finite): x = m 2^e, m in [sqrt(1/2), sqrt 2), log m = 2 atanh s,
+ * s = (m - 1) / (m + 1), the series in double-double (terms below 2^-60 in double) */
+static double jt_log(double x) {
+    if (!(x > 0.0) || isinf(x)) return x == 0.0 ? -INFINITY : (x > 0.0 ? x : NAN);
+    int e;
+    double m = frexp(x, &e);
+    if (m < 0x1.6a09e667f3bcdp-1) {
+        m *= 2.0;
+        e--;
+    }
+    const double f = m - 1.0; /* exact */
+    const jt_dd den = jt_sum(2.0, f);
+    const double sh = f / den.hi;
+    const double r = fma(-sh, den.hi, f) - sh * den.lo;
+    const jt_dd s = jt_qsum(sh, r / den.hi);
+    const jt_dd t = jt_dmul(s, s);
+    double tail = 0.0;
+    for (int k = 24; k >= 11; k--) tail = tail * t.hi + 1.0 / (double)(2 * k + 1);
+    jt_dd P = {tail, 0.0};
+    for (int k = 10; k >= 1; k--) P = jt_dadd(jt_dmul(P, t), jt_inv((double)(2 * k + 1)));
+    const jt_dd one = {1.0, 0.0};
+    P = jt_dadd(jt_dmul(P, t), one);
+    jt_dd lm = jt_dmul(s, P);
+    lm.hi *= 2.0;
+    lm.lo *= 2.0;
+    const jt_dd ed = {(double)e, 0.0};
+    const jt_dd res = jt_dadd(jt_dmul(ed, JT_LN2), lm);
+    return res.hi + res.lo;
+}
+
+/* exp y correctly rounded: y = k ln2 + r, |r| <= ln2 / 2, the Taylor series in double-double */
+static double jt_exp(double y) {
+    if (y != y) return y;
+    if (y > 709.79) return INFINITY;
+    if (y < -745.2) return 0.0;
+    const double k = nearbyint(y / JT_LN2.hi);
+    const jt_dd yk = {y, 0.0}, mk = {-k, 0.0};
+    const jt_dd r = jt_dadd(yk, jt_dmul(mk, JT_LN2));
+    double fact = 1.0, tail = 0.0;
+    double inv[28];
+    for (int n = 1; n < 28; n++) {
+        fact *= (double)n;
+        inv[n] = 1.0 / fact;
+    }
+    for (int n = 27; n >= 14; n--) tail = tail * r.hi + inv[n];
+    jt_dd P = {tail, 0.0};
+    fact = 1.0;
+    for (int n = 1; n < 14; n++) fact *= (double)n;
+    for (int n = 13; n >= 1; n--) { /* 1 / n! as a double-double: n! < 2^53 is exact */
+        const jt_dd c = jt_inv(fact);
+        P = jt_dadd(jt_dmul(P, r), c);
+        fact /= (double)n;
+    }
+    const jt_dd one = {1.0, 0.0};
+    P = jt_dadd(jt_dmul(P, r), one);
+    return ldexp(P.hi + P.lo, (int)k);
+}
+
+/* the iteration's shared scalars: rpoly passes them between its routines by pointer */
+typedef struct {
+    int N, NN; /* degree and coefficient count of p (highest power first) */
+    double p[11], K[11], qp[11], qk[11];
+    double a, b, c, d, e, f, g, h, a1, a3, a7;
+} jt_state;
+
+/* QuadSD_ak1 (rpoly.cpp:378-394): q = src / (z^2 + u z + v); the last two running values -> *ra, *rb */
+static void jt_divide(int nn, double u, double v, const double *src, double *q, double *ra, double *rb) {
+    double bb = src[0], aa = src[1] - bb * u;
+    q[0] = bb;
+    q[1] = aa;
+    for (int i = 2; i < nn; i++) {
+        const double t = src[i] - (aa * u + bb * v);
+        q[i] = t;
+        bb = aa;
+        aa = t;
+    }
+    *ra = aa;
+    *rb = bb;
+}
+
+/* calcSC_ak1 (rpoly.cpp:396-435): 3 = the quadratic almost divides K; 2 / 1 = scaled by d / c */
+static int jt_scalars(jt_state *s, double u, double v) {
+    const int N = s->N;
+    jt_divide(N, u, v, s->K, s->qk, &s->c, &s->d);
+    if (fabs(s->c) <= 100.0 * DBL_EPSILON * fabs(s->K[N - 1]) && fabs(s->d) <= 100.0 * DBL_EPSILON * fabs(s->K[N - 2]))
+        return 3;
+    s->h = v * s->b;
+    if (fabs(s->d) >= fabs(s->c)) {
+        s->e = s->a / s->d;
+        s->f = s->c / s->d;
+        s->g = u * s->b;
+        s->a3 = s->e * (s->g + s->a) + s->h * (s->b / s->d);
+        s->a1 = s->f * s->b - s->a;
+        s->a7 = s->h + (s->f + u) * s->a;
+        return 2;
+    }
+    s->e = s->a / s->c;
+    s->f = s->d / s->c;
+    s->g = s->e * u;
+    s->a3 = s->e * s->a + (s->g + s->h / s->c) * s->b;
+    s->a1 = s->b - s->a * (s->d / s->c);
+    s->a7 = s->g * s->d + s->h * s->f + s->a;
+    return 1;
+}
+
+/* nextK_ak1 (rpoly.cpp:437-475) */
+static void jt_next_k(jt_state *s, int type) {
+    const int N = s->N;
+    if (type == 3) {
+        s->K[0] = s->K[1] = 0.0;
+        for (int i = 2; i < N; i++) s->K[i] = s->qk[i - 2];
+        return;
+    }
+    const double ref = type == 1 ? s->b : s->a;
+    if (fabs(s->a1) > 10.0 * DBL_EPSILON * fabs(ref)) {
+        s->a7 /= s->a1;
+        s->a3 /= s->a1;
+        s->K[0] = s->qp[0];
+        s->K[1] = s->qp[1] - s->a7 * s->qp[0];
+        for (int i = 2; i < N; i++) s->K[i] = (s->a3 * s->qk[i - 2] - s->a7 * s->qp[i - 1]) + s->qp[i];
+    } else {
+        s->K[0] = 0.0;
+        s->K[1] = -s->a7 * s->qp[0];
+        for (int i = 2; i < N; i++) s->K[i] = s->a3 * s->qk[i - 2] - s->a7 * s->qp[i - 1];
+    }
+}
+
+/* newest_ak1 (rpoly.cpp:477-513): the next estimate (uu, vv) of the quadratic factor */
+static void jt_newest(const jt_state *s, int type, double u, double v, double *uu, double *vv) {
+    *uu = *vv = 0.0;
+    if (type == 3) return;
+    double a4, a5;
+    if (type != 2) {
+        a4 = (s->a + u * s->b) + s->h * s->f;
+        a5 = s->c + (u + v * s->f) * s->d;
+    } else {
+        a4 = (s->a + s->g) * s->f + s->h;
+        a5 = (s->f + u) * s->c + v * s->d;
+    }
+    const int N = s->N;
+    const double b1 = -s->K[N - 1] / s->p[N];
+    const double b2 = -(s->K[N - 2] + b1 * s->p[N - 1]) / s->p[N];
+    const double c1 = v * b2 * s->a1, c2 = b1 * s->a7, c3 = b1 * b1 * s->a3;
+    const double c4 = c1 - (c2 + c3);
+    const double t = (a5 - c4) + b1 * a4;
+    if (t != 0.0) {
+        *uu = u - (u * (c3 + c2) + v * (b1 * s->a1 + b2 * s->a7)) / t;
+        *vv = v * (1.0 + c4 / t);
+    }
+}
+
+/* Quad_ak1 (rpoly.cpp:700-750): zeros of a z^2 + b1 z + c, (sr, si) and (lr, li) */
+static void jt_quadratic(double a, double b1, double c, double *sr, double *si, double *lr, double *li) {
+    *sr = *si = *lr = *li = 0.0;
+    if (a == 0.0) {
+        if (b1 != 0.0) *sr = -(c / b1);
+        return;
+    }
+    if (c == 0.0) {
+        *lr = -(b1 / a);
+        return;
+    }
+    const double b = b1 / 2.0;
+    double d, e;
+    if (fabs(b) < fabs(c)) {
+        e = c >= 0.0 ? a : -a;
+        e = b * (b / fabs(c)) - e;
+        d = sqrt(fabs(e)) * sqrt(fabs(c));
+    } else {
+        e = 1.0 - (a / b) * (c / b);
+        d = sqrt(fabs(e)) * fabs(b);
+    }
+    if (e >= 0.0) {
+        if (b >= 0.0) d = -d;
+        *lr = (d - b) / a;
+        if (*lr != 0.0) *sr = (c / *lr) / a;
+    } else {
+        *lr = *sr = -(b / a);
+        *si = fabs(d / a);
+        *li = -*si;
+    }
+}
+
+/* QuadIT_ak1 (rpoly.cpp:515-607): variable-shift iteration for a quadratic factor from (uu, vv);
+ * returns 2 (both zeros found, quotient in qp) or 0 */
+static int jt_quad_iter(jt_state *s, double uu, double vv, double *szr, double *szi, double *lzr, double *lzi) {
+    const int N = s->N, NN = s->NN;
+    double u = uu, v = vv, relstp = 0.0, omp = 0.0, ui = 0.0, vi = 0.0;
+    int j = 0, tried = 0;
+    do {
+        jt_quadratic(1.0, u, v, szr, szi, lzr, lzi);
+        if (fabs(fabs(*szr) - fabs(*lzr)) > 0.01 * fabs(*lzr)) break;
+        jt_divide(NN, u, v, s->p, s->qp, &s->a, &s->b);
+        const double mp = fabs(s->a - *szr * s->b) + fabs(*szi * s->b);
+        const double zm = sqrt(fabs(v));
+        double ee = 2.0 * fabs(s->qp[0]);
+        const double t = -(*szr * s->b);
+        for (int i = 1; i < N; i++) ee = ee * zm + fabs(s->qp[i]);
+        ee = ee * zm + fabs(s->a + t);
+        ee = (9.0 * ee + 2.0 * fabs(t) - 7.0 * (fabs(s->a + t) + zm * fabs(s->b))) * DBL_EPSILON;
+        if (mp <= 20.0 * ee) return 2;
+        if (++j > 20) break;
+        if (j >= 2 && relstp <= 0.01 && mp >= omp && !tried) { /* a cluster: five fixed shifts near it */
+            relstp = relstp < DBL_EPSILON ? sqrt(DBL_EPSILON) : sqrt(relstp);
+            u -= u * relstp;
+            v += v * relstp;
+            jt_divide(NN, u, v, s->p, s->qp, &s->a, &s->b);
+            for (int i = 0; i < 5; i++) jt_next_k(s, jt_scalars(s, u, v));
+            tried = 1;
+            j = 0;
         }
-        double lo = -R, flo = poly_eval(c, g, lo);
-        for (int k = 0; k < g; k++) {
-            const double hi = k < g - 1 ? crit[k] : R;
-            const double fhi = poly_eval(c, g, hi);
-            if (hi > lo && ((flo < 0.0) != (fhi < 0.0))) {
-                next[k] = poly_refine(c, g, lo, hi, flo, fhi);
-                found[k] = 1;
-            } else {
-                next[k] = lo;
-                found[k] = 0;
+        omp = mp;
+        jt_next_k(s, jt_scalars(s, u, v));
+        jt_newest(s, jt_scalars(s, u, v), u, v, &ui, &vi);
+        if (vi != 0.0) {
+            relstp = fabs((vi - v) / vi);
+            u = ui;
+            v = vi;
+        }
+    } while (vi != 0.0);
+    return 0;
+}
+
+/* RealIT_ak1 (rpoly.cpp:609-698): variable-shift iteration for a real zero from *sx; returns 1
+ * (zero found, quotient in qp) or 0, *flag = 1 (and *sx) asks for a quadratic iteration */
+static int jt_real_iter(jt_state *s, double *sx, int *flag, double *szr, double *szi) {
+    const int N = s->N, NN = s->NN;
+    double x = *sx, t = 0.0, omp = 0.0;
+    int j = 0;
+    *flag = 0;
+    for (;;) {
+        double pv = s->p[0];
+        s->qp[0] = pv;
+        for (int i = 1; i < NN; i++) s->qp[i] = pv = pv * x + s->p[i];
+        const double mp = fabs(pv), ms = fabs(x);
+        double ee = 0.5 * fabs(s->qp[0]);
+        for (int i = 1; i < NN; i++) ee = ee * ms + fabs(s->qp[i]);
+        if (mp <= 20.0 * DBL_EPSILON * (2.0 * ee - mp)) {
+            *szr = x;
+            *szi = 0.0;
+            return 1;
+        }
+        if (++j > 10) return 0;
+        if (j >= 2 && fabs(t) <= 0.001 * fabs(x - t) && mp > omp) {
+            *flag = 1;
+            *sx = x;
+            return 0;
+        }
+        omp = mp;
+        double kv = s->K[0];
+        s->qk[0] = kv;
+        for (int i = 1; i < N; i++) s->qk[i] = kv = kv * x + s->K[i];
+        if (fabs(kv) > fabs(s->K[N - 1]) * 10.0 * DBL_EPSILON) {
+            const double tt = -(pv / kv);
+            s->K[0] = s->qp[0];
+            for (int i = 1; i < N; i++) s->K[i] = tt * s->qk[i - 1] + s->qp[i];
+        } else {
+            s->K[0] = 0.0;
+            for (int i = 1; i < N; i++) s->K[i] = s->qk[i - 1];
+        }
+        kv = s->K[0];
+        for (int i = 1; i < N; i++) kv = kv * x + s->K[i];
+        t = fabs(kv) > fabs(s->K[N - 1]) * 10.0 * DBL_EPSILON ? -(pv / kv) : 0.0;
+        x += t;
+    }
+}
+
+/* Fxshfr_ak1 (rpoly.cpp:232-376): up to l2 fixed-shift steps with the quadratic z^2 + u z + v,
+ * a variable-shift iteration once the s or v sequence converges; returns the zeros found */
+static int jt_fixed_shift(jt_state *s, int l2, double sr, double v, double u, double *szr, double *szi, double *lzr,
+                          double *lzi) {
+    const int N = s->N;
+    int iflag = 1, type;
+    double betav = 0.25, betas = 0.25, oss = sr, ovv = v, ots = 0.0, otv = 0.0, ui = 0.0, vi = 0.0, xs = 0.0;
+    double svk[11];
+    jt_divide(s->NN, u, v, s->p, s->qp, &s->a, &s->b);
+    type = jt_scalars(s, u, v);
+    for (int j = 0; j < l2; j++) {
+        int first = 1;
+        jt_next_k(s, type);
+        type = jt_scalars(s, u, v);
+        jt_newest(s, type, u, v, &ui, &vi);
+        const double vv = vi;
+        const double ss = s->K[N - 1] != 0.0 ? -(s->p[N] / s->K[N - 1]) : 0.0;
+        double tv = 1.0, ts = 1.0;
+        if (j != 0 && type != 3) {
+            if (vv != 0.0) tv = fabs((vv - ovv) / vv);
+            if (ss != 0.0) ts = fabs((ss - oss) / ss);
+            const double tvv = tv < otv ? tv * otv : 1.0;
+            const double tss = ts < ots ? ts * ots : 1.0;
+            const int vpass = tvv < betav, spass = tss < betas;
+            if (spass || vpass) {
+                memcpy(svk, s->K, sizeof(double) * (size_t)N);
+                xs = ss;
+                int stry = 0, vtry = 0;
+                for (;;) {
+                    const int linear_first = first && spass && (!vpass || tss < tvv);
+                    first = 0;
+                    if (!linear_first) {
+                        const int nz = jt_quad_iter(s, ui, vi, szr, szi, lzr, lzi);
+                        if (nz > 0) return nz;
+                        iflag = vtry = 1;
+                        betav *= 0.25;
+                        if (stry || !spass) iflag = 0;
+                        else memcpy(s->K, svk, sizeof(double) * (size_t)N);
+                    }
+                    if (iflag != 0) {
+                        const int nz = jt_real_iter(s, &xs, &iflag, szr, szi);
+                        if (nz > 0) return nz;
+                        stry = 1;
+                        betas *= 0.25;
+                        if (iflag != 0) {
+                            ui = -(xs + xs);
+                            vi = xs * xs;
+                            continue;
+                        }
+                    }
+                    memcpy(s->K, svk, sizeof(double) * (size_t)N);
+                    if (!vpass || vtry) break;
+                }
+                jt_divide(s->NN, u, v, s->p, s->qp, &s->a, &s->b);
+                type = jt_scalars(s, u, v);
             }
-            lo = hi;
-            flo = fhi;
         }
-        for (int k = 0; k < g; k++) crit[k] = next[k];
+        ovv = vv;
+        oss = ss;
+        otv = tv;
+        ots = ts;
     }
+    return 0;
+}
+
+/* rpoly_ak1 (rpoly.cpp:7-230) on a[0..deg] (ascending powers; five_points.cpp:145-148 hands rpoly
+ * the highest power first).  Writes the zeros in the order found; returns their number (deg, less
+ * the ones not found after 20 shifts; 0 for a zero leading coefficient) */
+static int jt_rpoly(const double *a, int deg, double *zr, double *zi) {
+    const double cosr = -0x1.1db8f6d6a512ap-4, sinr = 0x1.fec0b7170fff6p-1; /* cos / sin (94 pi / 180), rpoly.cpp:14-18 */
+    const double lo = DBL_MIN / DBL_EPSILON, lb2 = JT_LN2.hi;
+    if (a[deg] == 0.0) return 0;
+    for (int i = 0; i <= deg; i++)
+        if (!isfinite(a[i])) return 0;
+    jt_state s;
+    int N = deg, found = 0;
+    double xx = sqrt(0.5), yy = -xx;
+    while (a[deg - N] == 0.0) { /* zeros at the origin */
+        zr[found] = zi[found] = 0.0;
+        N--;
+        found++;
+    }
+    int NN = N + 1;
+    for (int i = 0; i < NN; i++) s.p[i] = a[deg - i];
+    while (N >= 1) {
+        if (N <= 2) {
+            if (N < 2) {
+                zr[deg - 1] = -(s.p[1] / s.p[0]);
+                zi[deg - 1] = 0.0;
+            } else {
+                jt_quadratic(s.p[0], s.p[1], s.p[2], &zr[deg - 2], &zi[deg - 2], &zr[deg - 1], &zi[deg - 1]);
+            }
+            return deg;
+        }
+        double mmax = 0.0, mmin = DBL_MAX;
+        for (int i = 0; i < NN; i++) {
+            const double x = fabs(s.p[i]);
+            if (x > mmax) mmax = x;
+            if (x != 0.0 && x < mmin) mmin = x;
+        }
+        double sc = lo / mmin;
+        if ((sc <= 1.0 && mmax >= 10.0) || (sc > 1.0 && DBL_MAX / sc >= mmax)) {
+            if (sc == 0.0) sc = DBL_MIN;
+            const int l = (int)(jt_log(sc) / lb2 + 0.5);
+            const double factor = ldexp(1.0, l); /* pow(2.0, l): exact */
+            if (factor != 1.0)
+                for (int i = 0; i < NN; i++) s.p[i] *= factor;
+        }
+        /* the lower bound of the zeros' moduli: the positive zero of |p0| z^N + ... - |pN| */
+        double pt[11];
+        for (int i = 0; i < NN; i++) pt[i] = fabs(s.p[i]);
+        pt[N] = -pt[N];
+        const int NM1 = N - 1;
+        double x = jt_exp((jt_log(-pt[N]) - jt_log(pt[0])) / (double)N);
+        if (pt[NM1] != 0.0) {
+            const double xm = -pt[N] / pt[NM1];
+            if (xm < x) x = xm;
+        }
+        double xm = x, ff = 0.0, df, dx;
+        int trips = 0;
+        do {
+            x = xm;
+            xm = 0.1 * x;
+            ff = pt[0];
+            for (int i = 1; i < NN; i++) ff = ff * xm + pt[i];
+        } while (ff > 0.0 && ++trips < 2100);
+        trips = 0;
+        do {
+            df = ff = pt[0];
+            for (int i = 1; i < N; i++) {
+                ff = x * ff + pt[i];
+                df = x * df + ff;
+            }
+            ff = x * ff + pt[N];
+            dx = ff / df;
+            x -= dx;
+        } while (fabs(dx / x) > 0.005 && ++trips < 500);
+        const double bnd = x;
+        /* K = p' / N, then five unshifted steps */
+        for (int i = 1; i < N; i++) s.K[i] = (double)(N - i) * s.p[i] / (double)N;
+        s.K[0] = s.p[0];
+        const double aa = s.p[N], bb = s.p[NM1];
+        int zerok = s.K[NM1] == 0.0;
+        for (int jj = 0; jj < 5; jj++) {
+            const double cc = s.K[NM1];
+            if (zerok) {
+                for (int j = NM1; j >= 1; j--) s.K[j] = s.K[j - 1];
+                s.K[0] = 0.0;
+                zerok = s.K[NM1] == 0.0;
+            } else {
+                const double t = -aa / cc;
+                for (int j = NM1; j >= 1; j--) s.K[j] = t * s.K[j - 1] + s.p[j];
+                s.K[0] = s.p[0];
+                zerok = fabs(s.K[NM1]) <= fabs(bb) * DBL_EPSILON * 10.0;
+            }
+        }
+        double saved[11];
+        memcpy(saved, s.K, sizeof(double) * (size_t)N);
+        s.N = N;
+        s.NN = NN;
+        int jj;
+        for (jj = 1; jj <= 20; jj++) {
+            /* a shift of modulus bnd, its amplitude rotated by 94 degrees from the last one */
+            const double xr = cosr * xx - sinr * yy;
+            yy = sinr * xx + cosr * yy;
+            xx = xr;
+            const double sr = bnd * xx, u = -(2.0 * sr);
+            double szr, szi, lzr, lzi;
+            const int nz = jt_fixed_shift(&s, 20 * jj, sr, bnd, u, &szr, &szi, &lzr, &lzi);
+            if (nz != 0) {
+                const int j = deg - N;
+                zr[j] = szr;
+                zi[j] = szi;
+                NN -= nz;
+                N = NN - 1;
+                for (int i = 0; i < NN; i++) s.p[i] = s.qp[i];
+                if (nz != 1) {
+                    zr[j + 1] = lzr;
+                    zi[j + 1] = lzi;
+                }
+                break;
+            }
+            memcpy(s.K, saved, sizeof(double) * (size_t)N);
+        }
+        if (jj > 20) return deg - N;
+    }
+    return deg;
+}
+
+/* real zeros (zero imaginary part) in rpoly's order (five_points.cpp:152-156) */
+static int real_roots(const double *a, int n, double *roots) {
+    double zr[10], zi[10];
+    const int nz = jt_rpoly(a, n, zr, zi);
     int nr = 0;
-    for (int k = 0; k < n; k++)
-        if (found[k]) roots[nr++] = crit[k];
+    for (int k = 0; k < nz; k++)
+        if (zi[k] == 0.0) roots[nr++] = zr[k];
     return nr;
 }
 
@@ -1723,8 +2130,15 @@ static inline float essential_error(const orc_est *e, unsigned int pidx) {
     return (fabsf(a1 / a2) + fabsf(b1 / b2)) / 2;
 }
 
-/* test hook: real roots of a polynomial (ascending) by the 5-pt solver's spec */
+/* test hook: the real zeros of a polynomial (ascending powers, degree <= 10) in rpoly's order */
 int orc_real_roots(const double *a, int n, double *roots) { return real_roots(a, n, roots); }
+
+/* test hook: every zero rpoly_ak1 reports (its order; returns their number) */
+int orc_rpoly_zeros(const double *a, int n, double *zr, double *zi) { return n >= 1 && n <= 10 ? jt_rpoly(a, n, zr, zi) : -1; }
+
+/* test hook: the portable correctly rounded log / exp of the restatement */
+double orc_jt_log(double x) { return jt_log(x); }
+double orc_jt_exp(double y) { return jt_exp(y); }
 
 /* test hook: the degree-10 polynomial det M(z) of an essential sample (ascending powers), the
  * input of the root step -- pinned against the reference's rpoly_ak1 (oracle/rpoly_ref.cpp) */

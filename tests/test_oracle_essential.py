@@ -3,10 +3,11 @@
 The reference's 5-point solver goes through OpenCV SVD/determinant/inv and the rpoly
 Jenkins-Traub root finder (five_points.cpp:13-274).  Two of its steps are pinned against the
 reference's own code compiled where it lies (oracle/_ref): the polynomial matrix M(z)
-(mblock.hpp) and the root step (rpoly.cpp's rpoly_ak1, on the oracle's own polynomials).  The
-OpenCV steps (null basis, determinant interpolation, triangulation SVD) are not reproducible
-here, and the oracle's restatement of them is pinned by identities: its root finder matches
-numpy on degree-10 polynomials, on exact two-view data
+(mblock.hpp) and the root step (rpoly.cpp's rpoly_ak1, restated operation for operation: the
+same zeros in the same order, which decides the selected candidate), plus a committed fixture of
+rpoly's outputs for boxes without the reference.  The OpenCV steps (null basis, determinant
+interpolation, triangulation SVD) are not reproducible here, and the oracle's restatement of
+them is pinned by identities: on exact two-view data
 the generating E is among the solver's candidates and passes its cheirality test, the
 returned E satisfies the essential-matrix constraints, and the residual equals the textbook
 point-to-epipolar-line distance.
@@ -24,22 +25,24 @@ def _dist(m, E):
 
 
 def test_real_roots_match_numpy(oracle):
+    """The root step (usac_oracle.c jt_rpoly, the reference's Jenkins-Traub rpoly_ak1 restated)
+    finds every real zero of well-separated polynomials and reports no complex one."""
     rng = np.random.default_rng(0)
     for _ in range(200):
         roots = np.sort(rng.uniform(-4, 4, size=rng.integers(1, 11)))
         if len(roots) > 1 and np.min(np.diff(roots)) < 1e-2:
             continue
         poly = np.poly(roots)[::-1] * rng.uniform(0.5, 2)
-        got = oracle.real_roots(poly)
+        got = np.sort(oracle.real_roots(poly))
         np.testing.assert_allclose(got, roots, rtol=0, atol=1e-7)
     # complex pairs are not reported
-    got = oracle.real_roots(np.poly([1.0, -2.0, 1 + 1j, 1 - 1j]).real[::-1])
+    got = np.sort(oracle.real_roots(np.poly([1.0, -2.0, 1 + 1j, 1 - 1j]).real[::-1]))
     np.testing.assert_allclose(got, [-2.0, 1.0], atol=1e-9)
 
 
 def test_real_roots_wide_range(oracle):
-    """Roots spread over six decades, both signs: none lost, full precision (the root
-    bound, filler partition points and safeguarded Newton of the spec)."""
+    """Roots spread over six decades, both signs: none lost (rpoly's scaling and its
+    lower-bound shifts), every one to ~1e-9."""
     rng = np.random.default_rng(1)
     worst, tested = 0.0, 0
     for _ in range(800):
@@ -47,11 +50,58 @@ def test_real_roots_wide_range(oracle):
         roots = np.sort(rng.choice([-1.0, 1.0], k) * 10 ** rng.uniform(-3, 3, k))
         if np.min(np.diff(roots) / np.maximum(1.0, np.abs(roots[1:]))) < 1e-3:
             continue
-        got = oracle.real_roots(np.poly(roots)[::-1])
+        got = np.sort(oracle.real_roots(np.poly(roots)[::-1]))
         assert len(got) == len(roots)
         worst = max(worst, float(np.max(np.abs(got - roots) / np.maximum(np.abs(roots), 1e-3))))
         tested += 1
-    assert tested > 600 and worst < 1e-10
+    assert tested > 600 and worst < 1e-8, worst
+
+
+def test_jt_log_exp_correctly_rounded(oracle):
+    """The restatement's portable log / exp (the two libm calls in rpoly.cpp:82,98) are the
+    correctly rounded values (checked with 60-digit decimal arithmetic); the device repeats them
+    bit for bit.  glibc's own differ on a small fraction (its exp is not correctly rounded)."""
+    import math
+    from decimal import Decimal, getcontext
+
+    getcontext().prec = 60
+
+    def cr(v):
+        f = float(v)
+        c = [math.nextafter(f, -math.inf), f, math.nextafter(f, math.inf)]
+        return min(c, key=lambda x: abs(Decimal(x) - v))
+
+    rng = np.random.default_rng(4)
+    for x in np.ldexp(rng.uniform(0.5, 1.0, 400), rng.integers(-1000, 1000, 400)):
+        assert oracle.jt_log(x) == cr(Decimal(float(x)).ln()), x
+    for y in np.r_[rng.uniform(-700, 700, 300), rng.uniform(-5, 5, 300)]:
+        assert oracle.jt_exp(y) == cr(Decimal(float(y)).exp()), y
+    assert oracle.jt_log(1.0) == 0.0 and oracle.jt_exp(0.0) == 1.0
+
+
+def test_rpoly_restatement_matches_reference_random(oracle):
+    """The restatement against the reference's rpoly_ak1 compiled where it lies (oracle/_ref):
+    20 000 random polynomials of degree 3-10 over eight decades of coefficient size give the
+    same zeros, bit for bit and in the same order, on all but a handful (measured 3 in 200 000):
+    those are the arguments where glibc's exp / log misround and the root bound's last bits
+    differ; there the degree and the order agree and the zeros agree to 1e-9."""
+    if not oracle.rpoly_ref_available():
+        pytest.skip("oracle/_ref/librpoly_ref.so not built (the reference is absent)")
+    rng = np.random.default_rng(3)
+    exact = near = 0
+    for t in range(20000):
+        n = int(rng.integers(3, 11))
+        a = (rng.uniform(size=n + 1) - 0.5) * 10.0 ** ((rng.uniform(size=n + 1) - 0.5) * 8)
+        zr, zi = oracle.rpoly_zeros(a)
+        rr, ri = oracle.rpoly_ref_zeros(a)
+        assert len(zr) == len(rr), (a, zr, rr)
+        if np.array_equal(zr, rr) and np.array_equal(zi, ri):
+            exact += 1
+            continue
+        near += 1
+        z, r = zr + 1j * zi, rr + 1j * ri
+        assert np.all(np.abs(z - r) <= 1e-9 * np.maximum(np.abs(r), 1.0)), (a, z, r)
+    assert near <= 5, near
 
 
 def test_essential_error_closed_form(oracle):
@@ -86,7 +136,9 @@ def test_five_point_candidates_contain_exact_E(oracle):
             returned += 1
             M = ms[0].reshape(3, 3).astype(np.float64)
             sv = np.linalg.svd(M, compute_uv=False)
-            assert sv[2] <= 1e-4 * sv[0] and abs(sv[0] - sv[1]) <= 1e-3 * sv[0]
+            # 1e-3: the selected zero may be a late one of rpoly's deflation order, whose value
+            # (and E) carries the deflation's larger error -- as in the reference
+            assert sv[2] <= 1e-3 * sv[0] and abs(sv[0] - sv[1]) <= 1e-3 * sv[0]
             # the returned E is the FIRST candidate passing cheirality (five_points.cpp:239-273)
             first = int(np.argmax(ok))
             assert ok.any() and np.array_equal(ms[0], cand[first])
@@ -140,61 +192,63 @@ def _residual(a, x):
 
 
 def test_e5_roots_pinned_against_reference_rpoly(oracle):
-    """the root step of the 5-point solver against the reference's own
-    rpoly_ak1 (usac/estimator/essential/rpoly.cpp:7-230, built by oracle/Makefile where it lies
-    with only the standard headers its precomp.hpp would include).  On the oracle's degree-10
-    polynomials of 10 000 cfg4 samples, the real zeros rpoly reports (zeroi == 0, the filter of
-    five_points.cpp:152-156) equal the oracle's real_roots:
-      * counts equal on >= 99.9 % of the samples; every difference is rpoly giving up after 20
-        shifts (rpoly.cpp:214-218, its degree comes back short) or a near-multiple cluster where a
-        complex pair sits within 1e-3 of the real axis (rpoly's deflation turns it into two "real"
-        zeros, or the other way round);
-      * values within rel 1e-9 on >= 99.8 % of the equal-count samples; where they differ by more,
-        the oracle's root has the smaller exact backward error (<= 1e-15: rounding level) -- rpoly's
-        deflated zeros carry the larger error.
-    The ORDER differs: rpoly returns zeros in the order it deflates them and five_points.cpp:239-273
-    keeps the first that passes cheirality, while this build's spec scans real roots ascending.  The
-    test measures how often that picks a different candidate (reported)."""
+    """the 5-point solver's root step IS the reference's rpoly_ak1
+    (usac/estimator/essential/rpoly.cpp:7-750, restated in usac_oracle.c jt_rpoly; the reference
+    compiled where it lies into oracle/_ref by oracle/Makefile).  On the oracle's degree-10
+    polynomials of 10 000 cfg4 samples the restatement reports the same zeros in the same order,
+    bit for bit, on >= 99.9 % of the samples (the rest: the root bound's last bits, where glibc's
+    exp / log misround -- same order, zeros within 1e-9); and the candidate the solver selects --
+    the first real zero in rpoly's order whose E passes cheirality (five_points.cpp:143-157,
+    239-273) -- is the one the reference's order selects on >= 99.9 % of the samples with a
+    passing candidate."""
     if not oracle.rpoly_ref_available():
         pytest.skip("oracle/_ref/librpoly_ref.so not built (the reference is absent)")
     pts, _, _ = synthetic.fundamental_points(n=50000, inlier_ratio=0.3, seed=1, normalized=True)
     est = oracle.Estimator(oracle.ESSENTIAL, pts)
     samples = oracle.uniform_samples(11, len(pts), 5, 10000)
-    n_cnt_diff, n_val, n_val_diff, n_sel, n_sel_diff, failures = 0, 0, 0, 0, 0, 0
+    n_exact, n_near, n_sel, n_sel_diff = 0, 0, 0, 0
     for s in samples:
         a = oracle.e5_poly(est, s)
+        zr, zi = oracle.rpoly_zeros(a)
+        rr, ri = oracle.rpoly_ref_zeros(a)
+        assert len(zr) == len(rr), (s, zr, rr)
+        if np.array_equal(zr, rr) and np.array_equal(zi, ri):
+            n_exact += 1
+        else:
+            n_near += 1
+            z, r = zr + 1j * zi, rr + 1j * ri
+            assert np.all(np.abs(z - r) <= 1e-9 * np.maximum(np.abs(r), 1.0)), (s, z, r)
         ours = oracle.real_roots(a)
-        zr, zi = oracle.rpoly_ref_zeros(a)
-        if len(zr) < 10:
-            failures += 1
-        real = zr[zi == 0]
-        ref = np.sort(real)
-        if len(ref) != len(ours):
-            n_cnt_diff += 1
-            if len(zr) == 10:  # a cluster: numpy's companion roots show a pair within 1e-3 of the axis
-                cr = np.roots(a[::-1])
-                near = cr[(np.abs(cr.imag) > 0) & (np.abs(cr.imag) < 1e-3 * np.maximum(1.0, np.abs(cr.real)))]
-                odd = np.setxor1d(np.round(ref, 3), np.round(ours, 3))
-                assert len(near) or len(odd) == 0, (s, ours, ref)
-            continue
-        if not len(ref):
-            continue
-        n_val += 1
-        rel = np.abs(ref - ours) / np.abs(ours)
-        if rel.max() > 1e-9:
-            n_val_diff += 1
-            k = int(np.argmax(rel))
-            ro, rr = _residual(a, ours[k]), _residual(a, ref[k])
-            assert ro <= 1e-15 and ro <= rr, (s, ours[k], ref[k], ro, rr)
-        # the selection: first cheirality-passing candidate, ascending (this spec) vs rpoly's order
+        ref = rr[ri == 0]
+        assert len(ours) == len(ref)
+        # the selection: the solver's first passing candidate against the reference order's
         cand, ok = est.e5_candidates(s)
         if len(cand) == len(ours) and ok.any():
             n_sel += 1
-            pos = [int(np.argmin(np.abs(real - r))) for r in ours]
-            first_rp = min((k for k in range(len(ours)) if ok[k]), key=lambda k: pos[k])
-            n_sel_diff += first_rp != int(np.argmax(ok))
-    print("rpoly pin: count differences %d / %d (rpoly failures %d); values > 1e-9: %d / %d; selection differs "
-          "on %d of %d samples with a passing candidate" % (n_cnt_diff, len(samples), failures, n_val_diff, n_val,
-                                                            n_sel_diff, n_sel))
-    assert n_cnt_diff <= 10 and n_val_diff <= 0.002 * n_val
-    assert n_sel > 3000
+            first = int(np.argmax(ok))
+            n_sel_diff += int(np.argmin(np.abs(ref - ours[first]))) != first
+    print("rpoly pin: %d / %d samples bit-exact, %d within 1e-9; selection differs on %d of %d samples with a "
+          "passing candidate" % (n_exact, len(samples), n_near, n_sel_diff, n_sel))
+    assert n_near <= 0.001 * len(samples) and n_sel > 3000 and n_sel_diff <= 0.001 * n_sel
+
+
+def test_rpoly_restatement_matches_golden(oracle):
+    """The same pin without the reference present: tests/golden/rpoly_ref.npz holds the
+    reference's rpoly_ak1 zeros (its order) for 400 of the solver's degree-10 polynomials and 400
+    random ones (tools/gen_rpoly_golden.py, run where oracle/_ref is built).  The restatement
+    reports the same number of zeros and the same zeros, bit for bit, on all but the rare
+    polynomials whose root bound meets a misrounded glibc exp / log (<= 2 here), and within 1e-9
+    in the same order on those."""
+    import os
+
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "rpoly_ref.npz"))
+    near = 0
+    for a, d, zr_ref, zi_ref, k in zip(g["coeffs"], g["degree"], g["zr"], g["zi"], g["nzeros"]):
+        zr, zi = oracle.rpoly_zeros(a[: d + 1])
+        assert len(zr) == k
+        if np.array_equal(zr, zr_ref[:k]) and np.array_equal(zi, zi_ref[:k]):
+            continue
+        near += 1
+        z, r = zr + 1j * zi, zr_ref[:k] + 1j * zi_ref[:k]
+        assert np.all(np.abs(z - r) <= 1e-9 * np.maximum(np.abs(r), 1.0))
+    assert near <= 2, near
