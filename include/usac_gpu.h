@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define USAC_ABI_VERSION 12
+#define USAC_ABI_VERSION 13
 
 /* = enum ESTIMATOR (usac/model.hpp:10) */
 enum { USAC_LINE2D = 1, USAC_HOMOGRAPHY = 2, USAC_FUNDAMENTAL = 3, USAC_ESSENTIAL = 4 };
@@ -458,6 +458,14 @@ int usac_exchange_best_async(usac_ctx *ctx, usac_ctx *batch, uint32_t slot);
 int usac_exchange_best_wait(usac_ctx *ctx, uint32_t slot, usac_record *all);
 /* Merge n records by Score::bigger, earliest hyp_index on exact ties. */
 int usac_merge_records(const usac_record *recs, uint32_t n, usac_record *best);
+
+/* ---- self-test hooks (ABI 13) ------------------------------------------------------- */
+/* The essential 5-point solver's root step alone (five_points.cpp:139-157: rpoly_ak1's real zeros
+ * in its order, usac_rpoly.hpp) on B host polynomials of 11 ascending coefficients each: roots
+ * (B x 10 doubles, row h = polynomial h's real zeros in order) and their numbers.  Its correctly
+ * rounded log / exp (rpoly.cpp:82,98) on n host arguments.  Device: the context's; no other state. */
+int usac_selftest_rpoly(usac_ctx *ctx, const double *coeffs, uint32_t B, double *roots, int32_t *nroots);
+int usac_selftest_logexp(usac_ctx *ctx, const double *x, uint32_t n, double *log_out, double *exp_out);
 
 #ifdef __cplusplus
 }

@@ -353,6 +353,15 @@ def real_roots(coeffs):
     return r[:k].copy()
 
 
+def asc_roots(coeffs):
+    """the 5-pt solver's candidate values: real roots of sum coeffs[i] z^i, ascending (usac_oracle.c asc_real_roots)"""
+    a = np.ascontiguousarray(coeffs, dtype=np.float64)
+    r = np.zeros(max(len(a) - 1, 1), dtype=np.float64)
+    k = lib().orc_asc_roots(a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), len(a) - 1,
+                            r.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    return r[:k].copy()
+
+
 def rpoly_zeros(coeffs):
     """every zero the oracle's rpoly restatement reports (real, imaginary parts), in its order"""
     L = lib()

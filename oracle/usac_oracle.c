@@ -1392,6 +1392,118 @@ static int null10(double A[10][10], double *v) {
     return 1;
 }
 
+/* Horner with fused multiply-adds (fma: one IEEE rounding, as v_fma_f64 on the device) */
+static double poly_eval(const double *c, int deg, double x) {
+    double r = c[deg];
+    for (int i = deg - 1; i >= 0; i--) r = fma(r, x, c[i]);
+    return r;
+}
+
+/* Root refinement inside a sign-changing bracket (monotone there): safeguarded Newton in the
+ * manner of rtsafe, started at the secant (regula falsi) point of the bracket -- a Newton
+ * step when it stays strictly inside the bracket and at least halves the previous step
+ * (|2f| <= |dxold f'|), else bisection; the bracket is tightened at every evaluation.  Stops
+ * on an exact zero, a Newton step below 2^-50 |x| (the root to a few ulp; its end point is
+ * taken when inside the bracket), an unsplittable bracket, or 200 evaluations.  p and p' by one fused Horner pass. */
+static void poly_eval2(const double *c, int deg, double x, double *f, double *df) {
+    double v = c[deg], d = 0.0;
+    for (int j = deg - 1; j >= 0; j--) {
+        d = fma(d, x, v);
+        v = fma(v, x, c[j]);
+    }
+    *f = v;
+    *df = d;
+}
+
+static double poly_refine(const double *c, int deg, double lo, double hi, double flo, double fhi) {
+    double x = lo - flo * ((hi - lo) / (fhi - flo));
+    if (!(x > lo && x < hi)) x = 0.5 * (lo + hi);
+    double dxold = hi - lo, dx = dxold, f, df;
+    poly_eval2(c, deg, x, &f, &df);
+    for (int it = 0; it < 200; it++) {
+        if (f == 0.0) return x;
+        if ((f < 0.0) == (flo < 0.0)) {
+            lo = x;
+            flo = f;
+        } else {
+            hi = x;
+        }
+        const double step = f / df;
+        const double xn = x - step;
+        const int inside = xn > lo && xn < hi;
+        if (xn == x || fabs(step) <= 0x1p-50 * fabs(x)) return inside ? xn : x;
+        const int newton = inside && !(fabs(2.0 * f) > fabs(dxold * df));
+        dxold = dx;
+        if (newton) {
+            dx = step;
+            x = xn;
+        } else {
+            const double mid = 0.5 * (lo + hi);
+            if (!(mid > lo && mid < hi)) return mid;
+            dx = mid - x;
+            x = mid;
+        }
+        poly_eval2(c, deg, x, &f, &df);
+    }
+    return x;
+}
+
+/* root bound with IEEE operations only: the smallest r = 2^k (k >= 0) with
+ * |a_n| r > sum_i |a_i| r^(i-n+1) (then no root has |z| >= r) */
+static double root_bound(const double *a, int n) {
+    double r = 1.0;
+    const double an = fabs(a[n]);
+    for (int it = 0; it < 2100; it++) {
+        double t = fabs(a[0]);
+        for (int i = 1; i < n; i++) t = t / r + fabs(a[i]);
+        if (an * r > t) break;
+        r = r * 2.0;
+    }
+    return r;
+}
+
+/* real roots of a[0] + a[1] z + ... + a[n] z^n, ascending (<= n): the solver's candidate values */
+static int asc_real_roots(const double *a_in, int n, double *roots) {
+    while (n > 0 && a_in[n] == 0.0) n--;
+    if (n == 0) return 0;
+    const double R = root_bound(a_in, n);
+    /* level g works on the derivative of order n-g (degree g) and leaves exactly g points,
+     * ascending: the root of each sign-changing interval, or the interval's left end as a
+     * filler where it has none (fillers only split monotone intervals further, and keep the
+     * per-level counts fixed) */
+    double crit[10], next[10];
+    int found[10] = {0};
+    for (int g = 1; g <= n; g++) {
+        const int d = n - g;
+        double c[11];
+        for (int j = 0; j <= g; j++) {
+            double f = 1.0;
+            for (int m = j + d; m > j; m--) f *= (double)m;
+            c[j] = a_in[j + d] * f;
+        }
+        double lo = -R, flo = poly_eval(c, g, lo);
+        for (int k = 0; k < g; k++) {
+            const double hi = k < g - 1 ? crit[k] : R;
+            const double fhi = poly_eval(c, g, hi);
+            if (hi > lo && ((flo < 0.0) != (fhi < 0.0))) {
+                next[k] = poly_refine(c, g, lo, hi, flo, fhi);
+                found[k] = 1;
+            } else {
+                next[k] = lo;
+                found[k] = 0;
+            }
+            lo = hi;
+            flo = fhi;
+        }
+        for (int k = 0; k < g; k++) crit[k] = next[k];
+    }
+    int nr = 0;
+    for (int k = 0; k < n; k++)
+        if (found[k]) roots[nr++] = crit[k];
+    return nr;
+}
+
+
 /* ---- 5-pt root step: the reference's Jenkins-Traub zeros, in the order it finds them.
  * Solve5PointEssential hands det M(z)'s coefficients to rpoly_ak1 (five_points.cpp:139-157;
  * usac/estimator/essential/rpoly.cpp:7-750, the akiti.ca C++ rendering of Jenkins & Traub's
@@ -2061,10 +2173,18 @@ static int essential_5pt_all(const orc_est *e, const int *sample, float *Eout, f
     }
     double N[4][9], a[11], Mz[10][10];
     e5_poly(W, N, a);
+    /* rpoly reports nothing for a zero leading coefficient or non-finite coefficients
+     * (rpoly.cpp:224-227; its bounded loops all fail on NaN): no model */
+    int fin = a[10] != 0.0;
+    for (int i = 0; i <= 10; i++) fin = fin && isfinite(a[i]);
+    if (!fin) return 0;
     double roots[10];
-    const int nr = real_roots(a, 10, roots);
+    const int nr = asc_real_roots(a, 10, roots);
     static const double Pref[3][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}};
+    float Ec[10][9];
+    int pass[10], npass = 0;
     for (int r = 0; r < nr; r++) {
+        pass[r] = 0;
         const double zz = roots[r];
         e5_matrix((const double(*)[9])N, zz, Mz);
         double v[10];
@@ -2086,18 +2206,47 @@ static int essential_5pt_all(const orc_est *e, const int *sample, float *Eout, f
             }
             if (inl >= 5) found = 1;
         }
+        for (int k = 0; k < 9; k++) Ec[r][k] = (float)E[k];
+        pass[r] = found;
+        npass += found;
         if (cand) {
             for (int k = 0; k < 9; k++) cand[9 * *ncand + k] = (float)E[k];
             cand_ok[*ncand] = found;
             (*ncand)++;
-            continue;
-        }
-        if (found) {
-            for (int k = 0; k < 9; k++) Eout[k] = (float)E[k];
-            return 1;
         }
     }
-    return 0;
+    if (cand || npass == 0) return 0;
+    /* five_points.cpp:239-273 keeps the first candidate in rpoly's order that passes cheirality.
+     * With one passing candidate the order does not matter; with several, the reference's order
+     * is the Jenkins-Traub restatement's (jt_rpoly: rpoly.cpp's zeros in the order it deflates
+     * them): each passing candidate takes the rank of the rpoly zero nearest to its value (first on
+     * ties; rank 10 if rpoly reports no real zero) and the lowest rank wins (ascending on ties) */
+    int best = -1, best_rank = 11;
+    if (npass == 1) {
+        for (int r = 0; r < nr; r++)
+            if (pass[r]) best = r;
+    } else {
+        double z[10];
+        const int nz = real_roots(a, 10, z);
+        for (int r = 0; r < nr; r++) {
+            if (!pass[r]) continue;
+            int rank = 10;
+            double dmin = INFINITY;
+            for (int j = 0; j < nz; j++) {
+                const double d = fabs(z[j] - roots[r]);
+                if (d < dmin) {
+                    dmin = d;
+                    rank = j;
+                }
+            }
+            if (rank < best_rank) {
+                best_rank = rank;
+                best = r;
+            }
+        }
+    }
+    for (int k = 0; k < 9; k++) Eout[k] = Ec[best][k];
+    return 1;
 }
 
 static int essential_5pt(const orc_est *e, const int *sample, float *Eout) {
@@ -2132,6 +2281,9 @@ static inline float essential_error(const orc_est *e, unsigned int pidx) {
 
 /* test hook: the real zeros of a polynomial (ascending powers, degree <= 10) in rpoly's order */
 int orc_real_roots(const double *a, int n, double *roots) { return real_roots(a, n, roots); }
+
+/* test hook: the solver's candidate values, the real roots ascending */
+int orc_asc_roots(const double *a, int n, double *roots) { return asc_real_roots(a, n, roots); }
 
 /* test hook: every zero rpoly_ak1 reports (its order; returns their number) */
 int orc_rpoly_zeros(const double *a, int n, double *zr, double *zi) { return n >= 1 && n <= 10 ? jt_rpoly(a, n, zr, zi) : -1; }

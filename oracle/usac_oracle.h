@@ -51,6 +51,7 @@ int orc_est_sample_size(const orc_est *e);
 int orc_est_max_models(const orc_est *e);
 /* real roots (ascending) of a[0] + a[1] z + ... + a[n] z^n: the 5-pt solver's root spec */
 int orc_real_roots(const double *a, int n, double *roots);
+int orc_asc_roots(const double *a, int n, double *roots);
 int orc_rpoly_zeros(const double *a, int n, double *zr, double *zi);
 double orc_jt_log(double x);
 double orc_jt_exp(double y);

@@ -120,6 +120,7 @@ ABI_SYMBOLS = [
     "usac_termination_bound", "usac_prosac_termination", "usac_termination_destroy", "usac_sprt_create",
     "usac_sprt_verify", "usac_sprt_upper_bound", "usac_sprt_stats", "usac_sprt_replay", "usac_sprt_destroy",
     "usac_lo_create", "usac_lo_get_model_score", "usac_lo_iters", "usac_lo_destroy", "usac_batch_sprt_info",
+    "usac_selftest_rpoly", "usac_selftest_logexp",
 ]
 
 
@@ -323,6 +324,25 @@ class Context:
 
     def set_score_chunks(self, chunks):
         self._check(lib().usac_set_score_chunks(self._h, int(chunks)), "set_score_chunks")
+
+    def selftest_rpoly(self, coeffs):
+        """The device's 5-point root step alone (usac_selftest_rpoly) on polynomials of 11 ascending
+        coefficients -> (roots B x 10, numbers of real zeros), rpoly's order."""
+        a = np.ascontiguousarray(coeffs, dtype=np.float64).reshape(-1, 11)
+        r = np.zeros((a.shape[0], 10), np.float64)
+        n = np.zeros(a.shape[0], np.int32)
+        self._check(lib().usac_selftest_rpoly(self._h, _ptr(a, ctypes.c_double), a.shape[0], _ptr(r, ctypes.c_double),
+                                              _ptr(n, ctypes.c_int32)), "selftest_rpoly")
+        return r, n
+
+    def selftest_logexp(self, x):
+        """The root step's correctly rounded log / exp on the device (usac_selftest_logexp)."""
+        v = np.ascontiguousarray(x, dtype=np.float64)
+        lg = np.zeros_like(v)
+        ex = np.zeros_like(v)
+        self._check(lib().usac_selftest_logexp(self._h, _ptr(v, ctypes.c_double), len(v), _ptr(lg, ctypes.c_double),
+                                               _ptr(ex, ctypes.c_double)), "selftest_logexp")
+        return lg, ex
 
     def last_counts(self, n):
         """Per-slot (counts, sums) of the last batch as the score kernel left them."""

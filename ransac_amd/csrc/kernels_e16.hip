@@ -1,0 +1,369 @@
+// kernels_e16.hip -- the essential score with a matrix-core prefilter (gfx950 MFMA, fp16 in, fp32
+// accumulate), exact counts (DESIGN.md §6 "e16").  The two-view counterpart of kernels_h16.hip.
+//
+// The reference's residual (essential_estimator.hpp:76-107) of a pair is
+//   err = (|a1| / ||l12|| + |b1| / ||t12||) / 2,   l = E^T p2, t = E p1, a1 ~ b1 ~ r = p2^T E p1,
+// so err >= |r| / max(||l12||, ||t12||) >= |r| / (S rho): S = max(||E[:, 0:2]^T||_F, ||E[0:2, :]||_F) per
+// hypothesis, rho = max(||(x1, y1, 1)||, ||(x2, y2, 1)||) per point.  r is bilinear in the point: a
+// dot product of nine per-hypothesis coefficients G with the nine features f = (u, v, 1, p u, p v, p,
+// q u, q v, q) of the centred, power-of-two-scaled coordinates of kernels_h16.hip (G = T2^T E T1,
+// T the centring transforms).  With the features divided by rho per point, one MFMA tile
+// (v_mfma_f32_32x32x16_f16, K = the nine features) gives r / rho for 32 hypotheses x 32 points and
+// the rejection test is one compare per pair against a per-hypothesis constant:
+//   keep iff |r~'| < C,   C = 2^e C0 (1 + 2^-20) + D,   C0 = delta + thr (1 + 2^-19) (S + 2^-21 M + 2^-100),
+// delta = 2^-20 Mabs + 2^-120 bounds |a1 - r| and |b1 - r| of the reference's fp32 chains (Mabs = the
+// dataset box's bound of sum |E_jk p2_j p1_k|), M = the box's bound of ||l12|| and ||t12|| (their fp32
+// evaluation is within 2^-21 M of the exact norms), D the fp16 / MFMA rounding bound of kernels_h16.hip
+// (usac_h16.hpp) over the feature maxima, 2^e the hypothesis' power-of-two scale.  A rejected pair has
+// (1 - 2^-22)(|r| - delta) >= thr max(a2, b2) for the reference's own a2, b2, i.e. err >= thr: not an
+// inlier.  Hypotheses whose bounds are not finite or whose box bounds reach 2^60 (fp32 overflow in
+// the reference's chain) get zero rows and C = +inf (every pair to the exact stage); padding and
+// non-finite points get NaN features (never kept -- the reference never counts them).
+//
+// Kept pairs go through a per-wave LDS ring to the exact stage (essential_error_guarded: counts
+// exact, Σ terms within 2^-19 relative), drained 64 at a time; counts and Σ (2^-fx fixed point,
+// integer adds, deterministic) per point chunk, added by k_e16_finish.  Models are the listed
+// slots of the batch (list / list_n), as for k_score_f2.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "usac_device.hpp"
+#include "usac_device_e5.hpp"
+#include "usac_h16.hpp"
+#include "usac_kernels.h"
+
+namespace usac {
+
+typedef float e16_f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kE16NA = 2;                       // 32-hypothesis tiles per wave
+constexpr int kE16HW = 32 * kE16NA;             // hypotheses per wave
+constexpr uint32_t kE16Queue = 64u * 16u + 64u;  // ring: < 64 waiting + one tile's appends
+
+// ------------------------------------------------------------------------ point features / rho
+// the h16 feature layout (lane l of a 32-point block holds B[k = 8 (l >> 5) + j][column l & 31]),
+// every feature divided by the point's rho (rounded up: a larger rho only loosens the test)
+__global__ __launch_bounds__(256) void k_e16_points(const float4 *__restrict__ pts, uint32_t n,
+                                                    const H16Consts *__restrict__ kc, half8 *__restrict__ feat) {
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t nblk = (n + 31) / 32;
+    if (t >= nblk * 64) return;
+    const uint32_t blk = t >> 6, l = t & 63, i = blk * 32 + (l & 31), hf = l >> 5;
+    half8 o;
+    bool ok = i < n;
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ok) {
+        p = pts[i];
+        ok = isfinite(p.x) && isfinite(p.y) && isfinite(p.z) && isfinite(p.w);
+    }
+    if (!ok) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) o[j] = (_Float16)__builtin_nanf("");
+    } else {
+        const double x1 = p.x, y1 = p.y, x2 = p.z, y2 = p.w;
+        const double rho = fmax(sqrt(x1 * x1 + y1 * y1 + 1.0), sqrt(x2 * x2 + y2 * y2 + 1.0)) * (1.0 + 0x1p-40);
+        const double u = (x1 - kc->cx1) / kc->s1, v = (y1 - kc->cy1) / kc->s1;
+        const double pp = (x2 - kc->cx2) / kc->s2, q = (y2 - kc->cy2) / kc->s2;
+        const double f[16] = {u, v, 1.0, pp * u, pp * v, pp, q * u, q * v, q, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 8; j++) o[j] = (_Float16)(float)(f[8 * hf + j] / rho);
+    }
+    feat[t] = o;
+}
+
+hipError_t launch_e16_points(hipStream_t st, const float4 *pts, uint32_t n, const H16Consts *k, void *feat) {
+    const uint32_t threads = (n + 31) / 32 * 64;
+    hipLaunchKernelGGL(k_e16_points, dim3((threads + 255) / 256), dim3(256), 0, st, pts, n, k,
+                       static_cast<half8 *>(feat));
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------ per-hypothesis rows
+// rows[2 pos + half]: coefficients 8 half .. 8 half + 7 of listed position pos; cm[pos] = C
+__device__ __forceinline__ double e16_up(double x) { return x * (1.0 + 0x1p-40); }
+
+__global__ __launch_bounds__(256) void k_e16_rows(const float *__restrict__ models, size_t stride,
+                                                  const uint32_t *__restrict__ list,
+                                                  const uint32_t *__restrict__ list_n, uint32_t kmax,
+                                                  const H16Consts *__restrict__ kc, float thr,
+                                                  half8 *__restrict__ rows, float *__restrict__ cm) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t K = list ? *list_n : kmax;
+    if (i >= K) return;
+    const uint32_t slot = list ? list[i] : i;
+    double E[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) E[k] = models[(size_t)k * stride + slot];
+    const float4 c = kc->ext;
+    const double C1[3] = {c.x, c.y, 1.0}, C2[3] = {c.z, c.w, 1.0};
+    // box bounds: Mabs >= sum |E_jk| |p2_j| |p1_k|, M >= ||l12||, ||t12|| (l_k = sum_j E_jk p2_j, t_j = sum_k E_jk p1_k)
+    double Mabs = 0.0, Lb[2] = {0.0, 0.0}, Tb[2] = {0.0, 0.0}, SA = 0.0, SB = 0.0;
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const double a = fabs(E[3 * j + k]);
+            Mabs += a * C2[j] * C1[k];
+            if (k < 2) {
+                Lb[k] += a * C2[j];
+                SA += a * a;
+            }
+            if (j < 2) {
+                Tb[j] += a * C1[k];
+                SB += a * a;
+            }
+        }
+    const double M = e16_up(fmax(sqrt(Lb[0] * Lb[0] + Lb[1] * Lb[1]), sqrt(Tb[0] * Tb[0] + Tb[1] * Tb[1])));
+    const double S = e16_up(fmax(sqrt(SA), sqrt(SB)));
+    const double delta = e16_up(0x1p-20 * e16_up(Mabs)) + 0x1p-120;
+    const double C0 = e16_up(delta + e16_up((double)thr * (1.0 + 0x1p-19) * (S + 0x1p-21 * M + 0x1p-100)));
+    // G = T2^T E T1 in the feature order (u, v, 1 | p u, p v, p | q u, q v, q): row 2, row 0, row 1
+    const double s1 = kc->s1, s2 = kc->s2, cx1 = kc->cx1, cy1 = kc->cy1, cx2 = kc->cx2, cy2 = kc->cy2;
+    double X[3][3], aX[3][3];  // E T1 and its terms' magnitudes
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        X[j][0] = E[3 * j] * s1;
+        X[j][1] = E[3 * j + 1] * s1;
+        X[j][2] = E[3 * j] * cx1 + E[3 * j + 1] * cy1 + E[3 * j + 2];
+        aX[j][0] = fabs(X[j][0]);
+        aX[j][1] = fabs(X[j][1]);
+        aX[j][2] = fabs(E[3 * j] * cx1) + fabs(E[3 * j + 1] * cy1) + fabs(E[3 * j + 2]);
+    }
+    double g[9], a[9];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        g[k] = cx2 * X[0][k] + cy2 * X[1][k] + X[2][k];
+        a[k] = fabs(cx2) * aX[0][k] + fabs(cy2) * aX[1][k] + aX[2][k];
+        g[3 + k] = s2 * X[0][k];
+        a[3 + k] = s2 * aX[0][k];
+        g[6 + k] = s2 * X[1][k];
+        a[6 + k] = s2 * aX[1][k];
+    }
+    double mx = 0.0;
+    bool fin = isfinite(C0) && isfinite(M) && M < 0x1p60 && Mabs < 0x1p60;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        fin = fin && isfinite(a[k]);
+        mx = fmax(mx, fabs(g[k]));
+    }
+    fin = fin && mx > 0x1p-100 && mx < 0x1p100;
+    half8 out[2];
+    float cv = INFINITY;
+    if (!fin) {
+#pragma unroll
+        for (int hf = 0; hf < 2; hf++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) out[hf][j] = (_Float16)0.0f;
+    } else {
+        const int e = -(ilogb(mx) + 1);  // max |g| 2^e in [0.5, 1)
+        double D = 0x1p-100;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const double gh = k < 9 ? ldexp(g[k], e) : 0.0;
+            const _Float16 gt = (_Float16)(float)gh;
+            out[k >> 3][k & 7] = gt;
+            if (k < 9) {
+                const double agt = fabs((double)(float)gt), fk = kc->fmax[k];
+                D += agt * (0x1p-10 * fk + 0x1p-25) + fk * (0x1p-10 * fabs(gh) + 0x1p-25 + 0x1p-50 * ldexp(a[k], e)) +
+                     0x1p-19 * agt * (fk + 0x1p-24);
+            }
+        }
+        const double Cd = e16_up(ldexp(C0, e) * (1.0 + 0x1p-20) + D * (1.0 + 0x1p-18));
+        const float Cf = (float)Cd;
+        cv = (double)Cf >= Cd ? Cf : nextafterf(Cf, INFINITY);
+        if (!isfinite(cv)) cv = INFINITY;
+    }
+    rows[2 * (size_t)i] = out[0];
+    rows[2 * (size_t)i + 1] = out[1];
+    cm[i] = cv;
+}
+
+hipError_t launch_e16_rows(hipStream_t st, const float *models, size_t stride, const uint32_t *list,
+                           const uint32_t *list_n, uint32_t kmax, const H16Consts *k, float thr, void *rows,
+                           float *cm) {
+    hipLaunchKernelGGL(k_e16_rows, dim3((kmax + 255) / 256), dim3(256), 0, st, models, stride, list, list_n, kmax, k,
+                       thr, static_cast<half8 *>(rows), cm);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------ the scorer
+__device__ __forceinline__ void e16_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Drain cnt (<= 64) ring entries from head: lane i evaluates entry head + i (the guarded residual:
+// exact inlier decision) and adds an inlier to its hypothesis' LDS counters.
+__device__ __forceinline__ void e16_drain(uint32_t cnt, uint32_t head, const uint32_t *q, const float (*sm)[9],
+                                          uint32_t *sc, unsigned long long *ss, const float4 *__restrict__ pts,
+                                          float thr, float lo, float hi, double fxs) {
+    const uint32_t lane = threadIdx.x & 63;
+    e16_wave_sync();
+    if (lane < cnt) {
+        const uint32_t qi = head + lane;
+        const uint32_t e = q[qi >= kE16Queue ? qi - kE16Queue : qi];
+        const uint32_t hk = e >> 25, p = e & 0x1FFFFFFu;
+        const float4 pt = pts[p];
+        float m[9];
+#pragma unroll
+        for (int k = 0; k < 9; k++) m[k] = sm[hk][k];
+        bool inl;
+        const float val = essential_error_guarded(m, pt.x, pt.y, pt.z, pt.w, thr, lo, hi, inl);
+        if (inl) {
+            atomicAdd(&sc[hk], 1u);
+            atomicAdd(&ss[hk], (unsigned long long)llrint((double)val * fxs));
+        }
+    }
+    e16_wave_sync();
+}
+
+// Workgroup = 4 waves; wave w owns listed positions [hb, hb + 64) and point chunk blockIdx.y.  A
+// fragment of tile a: lane l holds row l & 31 (position hb + 32 a + (l & 31)), coefficients 8 (l >> 5)
+// ..; the D register j of lane l holds row (j & 3) + 4 (l >> 5) + 8 (j >> 2), column l & 31.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_score_e16(
+    const half8 *__restrict__ feat, const float4 *__restrict__ pts, uint32_t n, const half8 *__restrict__ rows,
+    const float *__restrict__ cm, const float *__restrict__ models, size_t stride, const uint32_t *__restrict__ list,
+    const uint32_t *__restrict__ list_n, uint32_t kmax, float thr, double fxs, uint32_t *__restrict__ cpart,
+    unsigned long long *__restrict__ spart) {
+    __shared__ float sM[4][kE16HW][9];
+    __shared__ uint32_t sC[4][kE16HW];
+    __shared__ unsigned long long sS[4][kE16HW];
+    __shared__ uint32_t sQ[4][kE16Queue];
+    const uint32_t K = list ? __builtin_amdgcn_readfirstlane(*list_n) : kmax;
+    const uint32_t lane = threadIdx.x & 63, hf = lane >> 5;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t hb = (blockIdx.x * 4 + wave) * kE16HW;
+    if (hb >= K) return;  // wave-uniform; no workgroup barrier below
+    {
+        const uint32_t pos = hb + lane;
+        const uint32_t slot = pos < K ? (list ? list[pos] : pos) : 0u;
+#pragma unroll
+        for (int k = 0; k < 9; k++) sM[wave][lane][k] = pos < K ? models[(size_t)k * stride + slot] : 0.f;
+        sC[wave][lane] = 0;
+        sS[wave][lane] = 0;
+    }
+    half8 A[kE16NA];
+    float Cv[kE16NA][16];
+#pragma unroll
+    for (int a = 0; a < kE16NA; a++) {
+        const uint32_t pos = hb + 32 * a + (lane & 31);
+        half8 z;
+#pragma unroll
+        for (int j = 0; j < 8; j++) z[j] = (_Float16)0.0f;
+        A[a] = pos < K ? rows[2 * (size_t)pos + hf] : z;
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const uint32_t pj = hb + 32 * a + (j & 3) + 4 * hf + 8 * (j >> 2);
+            Cv[a][j] = pj < K ? cm[pj] : 0.0f;  // a missing hypothesis keeps nothing (|x| < 0 is false)
+        }
+    }
+    const uint32_t nblk = (n + 31) / 32, nch = gridDim.y, ch = blockIdx.y;
+    const uint32_t per = (nblk + nch - 1) / nch;
+    const uint32_t b0 = ch * per < nblk ? ch * per : nblk, b1 = b0 + per < nblk ? b0 + per : nblk;
+    const float lo = thr * 0.9999847412109375f, hi = thr * 1.0000152587890625f;  // thr (1 -+ 2^-16)
+    uint32_t qn = 0, qh = 0;
+    const e16_f32x16 zero = {};
+    e16_wave_sync();
+    half8 bn = b0 < b1 ? feat[(size_t)b0 * 64 + lane] : half8{};
+    for (uint32_t blk = b0; blk < b1; blk++) {
+        const half8 bf = bn;
+        if (blk + 1 < b1) bn = feat[(size_t)(blk + 1) * 64 + lane];
+        e16_f32x16 acc[kE16NA];
+#pragma unroll
+        for (int a = 0; a < kE16NA; a++) acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[a], bf, zero, 0, 0, 0);
+        const uint32_t point = blk * 32 + (lane & 31);
+#pragma unroll
+        for (int a = 0; a < kE16NA; a++) {
+            uint64_t msk[16], any = 0;
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                msk[j] = __builtin_amdgcn_ballot_w64(fabsf(acc[a][j]) < Cv[a][j]);
+                any |= msk[j];
+            }
+            if (!any) continue;  // wave-uniform
+            // append the kept pairs of tile a (<= 1024), then drain full groups of 64
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const uint64_t mk = msk[j];
+                if (mk) {
+                    const uint32_t below =
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+                    if ((mk >> lane) & 1) {
+                        const uint32_t qi = qh + qn + below;  // < 2 Q
+                        const uint32_t hk = 32 * a + (j & 3) + 4 * hf + 8 * (j >> 2);
+                        sQ[wave][qi >= kE16Queue ? qi - kE16Queue : qi] = (hk << 25) | point;
+                    }
+                    qn += (uint32_t)__builtin_popcountll(mk);
+                }
+            }
+            while (qn >= 64) {
+                e16_drain(64, qh, sQ[wave], sM[wave], sC[wave], sS[wave], pts, thr, lo, hi, fxs);
+                qh = qh + 64 >= kE16Queue ? qh + 64 - kE16Queue : qh + 64;
+                qn -= 64;
+            }
+        }
+    }
+    while (qn) {
+        const uint32_t d = qn < 64 ? qn : 64;
+        e16_drain(d, qh, sQ[wave], sM[wave], sC[wave], sS[wave], pts, thr, lo, hi, fxs);
+        qh = qh + d >= kE16Queue ? qh + d - kE16Queue : qh + d;
+        qn -= d;
+    }
+    e16_wave_sync();
+    if (hb + lane < K) {
+        cpart[(size_t)ch * kmax + hb + lane] = sC[wave][lane];
+        spart[(size_t)ch * kmax + hb + lane] = sS[wave][lane];
+    }
+}
+
+// counts / sums at the listed slots from the chunk partials (integers: any order is exact)
+__global__ __launch_bounds__(256) void k_e16_finish(const uint32_t *__restrict__ list,
+                                                    const uint32_t *__restrict__ list_n, uint32_t kmax,
+                                                    const uint32_t *__restrict__ cpart,
+                                                    const unsigned long long *__restrict__ spart, uint32_t nch,
+                                                    double inv_fxs, int32_t *__restrict__ counts,
+                                                    float *__restrict__ sums) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t K = list ? *list_n : kmax;
+    if (i >= K) return;
+    uint32_t c = 0;
+    unsigned long long s = 0;
+    for (uint32_t y = 0; y < nch; y++) {
+        c += cpart[(size_t)y * kmax + i];
+        s += spart[(size_t)y * kmax + i];
+    }
+    const uint32_t slot = list ? list[i] : i;
+    counts[slot] = (int32_t)c;
+    sums[slot] = (float)((double)s * inv_fxs);
+}
+
+size_t e16_part_bytes(uint32_t kmax, int chunks) {
+    return (size_t)chunks * kmax * (sizeof(uint32_t) + sizeof(uint64_t));
+}
+
+size_t e16_row_bytes(uint32_t kmax) { return (size_t)kmax * 32; }
+
+hipError_t launch_score_e16(hipStream_t st, const void *feat, const float4 *pts, uint32_t n, const void *rows,
+                            const float *cm, const float *models, size_t stride, const uint32_t *list,
+                            const uint32_t *list_n, uint32_t kmax, float thr, int chunks, void *part,
+                            int32_t *counts, float *sums) {
+    if (chunks < 1 || n == 0 || n > 0x2000000u || kmax == 0) return hipErrorInvalidValue;
+    const uint32_t nblk = (n + 31) / 32, per = (nblk + (uint32_t)chunks - 1) / (uint32_t)chunks;
+    if ((uint64_t)per * 32 > (1u << 23)) return hipErrorInvalidValue;  // the fixed-point Σ bound (below)
+    if (!(thr > 0x1p-100f && thr < 0x1p100f)) return hipErrorInvalidValue;
+    // Σ in fixed point: an inlier's term is < thr (1 + 2^-15), 2^fx with thr 2^fx <= 2^40 leaves 2^23
+    // terms per hypothesis and chunk below 2^63
+    const int fx = 39 - ilogbf(thr);
+    unsigned long long *sp = static_cast<unsigned long long *>(part);
+    uint32_t *cp = reinterpret_cast<uint32_t *>(sp + (size_t)chunks * kmax);
+    hipLaunchKernelGGL(k_score_e16, dim3((kmax + 4 * kE16HW - 1) / (4 * kE16HW), chunks), dim3(256), 0, st,
+                       static_cast<const half8 *>(feat), pts, n, static_cast<const half8 *>(rows), cm, models, stride,
+                       list, list_n, kmax, thr, ldexp(1.0, fx), cp, sp);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_e16_finish, dim3((kmax + 255) / 256), dim3(256), 0, st, list, list_n, kmax, cp, sp,
+                       (uint32_t)chunks, ldexp(1.0, -fx), counts, sums);
+    return hipGetLastError();
+}
+
+}  // namespace usac

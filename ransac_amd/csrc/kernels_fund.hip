@@ -13,6 +13,7 @@
 #include "usac_device.hpp"
 #include "usac_device_e5.hpp"
 #include "usac_kernels.h"
+#include "usac_pk.hpp"
 
 namespace usac {
 
@@ -199,7 +200,6 @@ __global__ __launch_bounds__(64 * CHUNKS) void k_score_f(const float4 *__restric
 //
 // Points come from the fast-kernel records (k_prepare_rec: SoA groups of four, NaN-padded
 // tail, never queued).
-typedef float v2f __attribute__((ext_vector_type(2)));
 
 template <int EST>
 struct TwoViewModel {
@@ -259,24 +259,24 @@ __device__ __forceinline__ void two_view_reject2(const TwoViewModel<EST> &M, v2f
     const v2f *f = M.f2;
     v2f A, T;
     if constexpr (EST == USAC_ESSENTIAL) {
-        const v2f l1 = __builtin_elementwise_fma(f[0], x2, __builtin_elementwise_fma(f[3], y2, f[6]));
-        const v2f l2 = __builtin_elementwise_fma(f[1], x2, __builtin_elementwise_fma(f[4], y2, f[7]));
-        const v2f l3 = __builtin_elementwise_fma(f[2], x2, __builtin_elementwise_fma(f[5], y2, f[8]));
-        const v2f a1 = __builtin_elementwise_fma(l1, x1, __builtin_elementwise_fma(l2, y1, l3));
-        const v2f Qa = __builtin_elementwise_fma(l1, l1, l2 * l2);
+        const v2f l1 = vfma(f[0], x2, vfma(f[3], y2, f[6]));
+        const v2f l2 = vfma(f[1], x2, vfma(f[4], y2, f[7]));
+        const v2f l3 = vfma(f[2], x2, vfma(f[5], y2, f[8]));
+        const v2f a1 = vfma(l1, x1, vfma(l2, y1, l3));
+        const v2f Qa = vfma(l1, l1, l2 * l2);
         A = a1 * a1;
-        T = __builtin_elementwise_fma(Qa, M.K, M.C);
+        T = vfma(Qa, M.K, M.C);
     } else {
-        const v2f Fx = __builtin_elementwise_fma(f[0], x1, __builtin_elementwise_fma(f[1], y1, f[2]));
-        const v2f Fy = __builtin_elementwise_fma(f[3], x1, __builtin_elementwise_fma(f[4], y1, f[5]));
-        const v2f Gx = __builtin_elementwise_fma(f[0], x2, __builtin_elementwise_fma(f[3], y2, f[6]));
-        const v2f Gy = __builtin_elementwise_fma(f[1], x2, __builtin_elementwise_fma(f[4], y2, f[7]));
-        const v2f sv = __builtin_elementwise_fma(
-            x2, Fx, __builtin_elementwise_fma(y2, Fy, __builtin_elementwise_fma(f[6], x1, __builtin_elementwise_fma(f[7], y1, f[8]))));
-        const v2f D = __builtin_elementwise_fma(
-            Fx, Fx, __builtin_elementwise_fma(Fy, Fy, __builtin_elementwise_fma(Gx, Gx, Gy * Gy)));
+        const v2f Fx = vfma(f[0], x1, vfma(f[1], y1, f[2]));
+        const v2f Fy = vfma(f[3], x1, vfma(f[4], y1, f[5]));
+        const v2f Gx = vfma(f[0], x2, vfma(f[3], y2, f[6]));
+        const v2f Gy = vfma(f[1], x2, vfma(f[4], y2, f[7]));
+        const v2f sv = vfma(
+            x2, Fx, vfma(y2, Fy, vfma(f[6], x1, vfma(f[7], y1, f[8]))));
+        const v2f D = vfma(
+            Fx, Fx, vfma(Fy, Fy, vfma(Gx, Gx, Gy * Gy)));
         A = sv * sv;
-        T = __builtin_elementwise_fma(D, M.K, M.C);
+        T = vfma(D, M.K, M.C);
     }
 #ifdef TV_EXP_NOKEEP
     r0 = !(A.x <= T.x) || true;
@@ -296,38 +296,7 @@ __device__ __forceinline__ void two_view_reject2(const TwoViewModel<EST> &M, v2f
 // branch would run the exact path nearly always; the queues run it only for kept pairs.
 constexpr int kTvQueue = 16;  // entries per lane (4 KB of LDS per wave)
 
-// The guarded essential residual of the throughput drains (C > 1: Σ is re-associated anyway and
-// its terms may carry a stated error; the counts stay exact).  The reference's l, t, a1, b1 and
-// squared norms (the same unfused operations), then e' = (|a1| rsq(a2²) + |b1| rsq(b2²)) / 2
-// with v_rsq_f32 (1 ulp) instead of two correctly rounded square roots and two IEEE divisions.
-// Per term the two differ by < 2^-21 relative (rsq 2^-23, the product and the reference's sqrt
-// and division 2^-24 each), so |e' - e| <= e' 2^-19: e' <= thr (1 - 2^-16) proves e < thr and
-// e' >= thr (1 + 2^-16) proves !(e < thr).  Pairs inside that band, squared norms outside
-// [2^-96, inf) (denormal / zero / overflowing rsq) and non-finite values take the exact
-// expression.  Returns the error added to Σ: e' for a proven inlier, else the exact e.
-__device__ __forceinline__ float essential_error_guarded(const float *E, float x1, float y1, float x2, float y2,
-                                                         float thr, float lo, float hi, bool &inl) {
-    const float l1 = E[0] * x2 + E[3] * y2 + E[6];
-    const float l2 = E[1] * x2 + E[4] * y2 + E[7];
-    const float l3 = E[2] * x2 + E[5] * y2 + E[8];
-    const float t1 = E[0] * x1 + E[1] * y1 + E[2];
-    const float t2 = E[3] * x1 + E[4] * y1 + E[5];
-    const float t3 = E[6] * x1 + E[7] * y1 + E[8];
-    const float a1 = l1 * x1 + l2 * y1 + l3;
-    const float qa = l1 * l1 + l2 * l2;
-    const float b1 = t1 * x2 + t2 * y2 + t3;
-    const float qb = t1 * t1 + t2 * t2;
-    const float ef = (fabsf(a1) * __builtin_amdgcn_rsqf(qa) + fabsf(b1) * __builtin_amdgcn_rsqf(qb)) * 0.5f;
-    const bool normal = qa >= 1.2621774483536189e-29f && qb >= 1.2621774483536189e-29f &&  // 2^-96
-                        qa < INFINITY && qb < INFINITY;
-    if (__builtin_expect(normal && (ef <= lo || ef >= hi), 1)) {
-        inl = ef <= lo;
-        return ef;
-    }
-    const float e = (fabsf(a1 / sqrtf(qa)) + fabsf(b1 / sqrtf(qb))) / 2;  // essential_error, bit for bit
-    inl = e < thr;
-    return e;
-}
+// essential_error_guarded (usac_device_e5.hpp): the throughput drains' guarded essential residual
 
 template <int EST>
 __device__ __forceinline__ void two_view_drain(const TwoViewModel<EST> &M, const float4 *__restrict__ pts,

@@ -411,7 +411,10 @@ hipError_t launch_score_h16(hipStream_t st, const void *feat, const float4 *pts,
     static const int na = getenv("USAC_H16_NA") ? atoi(getenv("USAC_H16_NA")) : 2;  // 10-hypothesis tiles per wave
     if (chunks < 1 || n == 0 || n > 0x2000000u) return hipErrorInvalidValue;  // 25-bit point indices in the queue
     // Σ in fixed point: a stage-B term is < 2 T (1 + 2^-15) (S ~ 2 err of an inlier, err < thr = T / 2), so
-    // 2^fx with 2 T 2^fx <= 2^40 leaves 2^23 terms per hypothesis and chunk below 2^63
+    // 2^fx with 2 T 2^fx <= 2^40 leaves 2^23 terms per hypothesis and chunk below 2^63: a chunk of more
+    // than 2^23 points could wrap its partial, so such a launch is refused (h16_chunks never asks for one)
+    const uint32_t nblk = (n + 31) / 32, per = (nblk + (uint32_t)chunks - 1) / (uint32_t)chunks;
+    if ((uint64_t)per * 32 > (1u << 23)) return hipErrorInvalidValue;
     const int fx = h16_fixed_point(thr);
     const double fxs = ldexp(1.0, fx);
     unsigned long long *sp = static_cast<unsigned long long *>(part);  // 8-byte words first (alignment)

@@ -301,6 +301,12 @@ struct usac_ctx {
     uint32_t h16_deferred_ch = 0;  // > 0: the last h16 batch's chunk partials await batch_argmax
     float h16_deferred_thr = 0.f;
     DevBuf h16_k, h16_feat, h16_rows, h16_fm, h16_part;  // h16_k: the dataset constants (usac::H16Consts)
+    // the matrix-core prefilter scorer of essential matrices (kernels_e16.hip): the h16 dataset
+    // constants, its own rho-scaled fp16 features, per-batch rows / bounds and chunk partials; e16 = 1
+    // when usable (USAC_E16=0: the lanes-over-models k_score_f2 scores every throughput batch)
+    int e16 = 0;
+    bool h16_k_ok = false, e16_feat_ok = false;
+    DevBuf e16_feat, e16_rows, e16_cm, e16_part;
     // batch buffers
     DevBuf samples, models, counts, sums, best, hostmodels, argmax_part;
     DevBuf list, list_n;    // fundamental: occupied model slots (compacted) and their number
@@ -651,21 +657,33 @@ uint32_t h16_chunks(const usac_ctx *c, uint32_t B) {
     const uint32_t waves = (B + 10 * na - 1) / (10 * na), nblk = (c->n + 31) / 32;
     static const int env_ch = getenv("USAC_H16_CHUNKS") ? atoi(getenv("USAC_H16_CHUNKS")) : 0;
     const uint32_t ch = env_ch > 0 ? (uint32_t)env_ch : (16384u + waves - 1) / waves;
-    return std::max(1u, std::min(ch, std::min(nblk, 256u)));
+    // at most 2^23 points per chunk: a hypothesis' fixed-point Σ partial of one chunk stays below 2^63
+    // (launch_score_h16 refuses more); n <= 2^25 makes this at most 4
+    const uint32_t min_ch = (nblk + (1u << 18) - 1) >> 18;
+    return std::max(std::max(1u, min_ch), std::min(ch, std::min(nblk, 256u)));
 }
 
 // The matrix-core prefilter scorer (kernels_h16.hip): the point features once per context, each
 // hypothesis' fp16 rows and slack per batch, then the scorer over point chunks -- enough chunks for
 // ~16 waves per SIMD over the launch (20 hypotheses per wave; USAC_H16_CHUNKS overrides).
 // the dataset constants and the point features, once per context (on its stream)
-hipError_t h16_init(usac_ctx *c) {
-    if (c->h16_feat_ok) return hipSuccess;
+// the dataset constants (centres, power-of-two scales, feature maxima), shared by h16 and e16
+hipError_t h16_consts_init(usac_ctx *c) {
+    if (c->h16_k_ok) return hipSuccess;
     hipError_t e;
     if ((e = c->h16_k.reserve(sizeof(usac::H16Consts))) != hipSuccess) return e;
-    if ((e = c->h16_feat.reserve(usac::h16_feature_bytes(c->n))) != hipSuccess) return e;
     if ((e = usac::launch_h16_consts(c->stream, c->pts.as<float4>(), c->n, c->ext, c->h16_k.as<usac::H16Consts>())) !=
         hipSuccess)
         return e;
+    c->h16_k_ok = true;
+    return hipSuccess;
+}
+
+hipError_t h16_init(usac_ctx *c) {
+    if (c->h16_feat_ok) return hipSuccess;
+    hipError_t e;
+    if ((e = h16_consts_init(c)) != hipSuccess) return e;
+    if ((e = c->h16_feat.reserve(usac::h16_feature_bytes(c->n))) != hipSuccess) return e;
     if ((e = usac::launch_h16_points(c->stream, c->pts.as<float4>(), c->n, c->h16_k.as<usac::H16Consts>(),
                                      c->h16_feat.p)) != hipSuccess)
         return e;
@@ -711,6 +729,49 @@ hipError_t enqueue_score_h16(usac_ctx *c, uint32_t B, float thr, bool defer_fini
     return e;
 }
 
+// The essential matrix-core prefilter scorer (kernels_e16.hip): throughput batches of listed models
+// (chunks > 1: Σ re-associated, counts exact), the default score variant, USAC_E16 unset or 1
+bool e16_scores(const usac_ctx *c, int chunks, float thr) {
+    return is_e(c) && !c->sprt_on && c->e16 == 1 && c->score_variant == 0 && chunks > 1 && thr > 0x1p-100f &&
+           thr < 0x1p100f;
+}
+
+// point chunks of the e16 scorer for kmax listed slots: ~12 waves per SIMD if every slot is
+// occupied (64 models per wave), at most one 32-point block per chunk, 256 chunks, and >= 1 per
+// 2^23 points (its fixed-point Σ bound)
+uint32_t e16_chunks(const usac_ctx *c, uint32_t kmax) {
+    const uint32_t waves = (kmax + 63) / 64, nblk = (c->n + 31) / 32;
+    static const int env_ch = getenv("USAC_E16_CHUNKS") ? atoi(getenv("USAC_E16_CHUNKS")) : 0;
+    const uint32_t ch = env_ch > 0 ? (uint32_t)env_ch : (12288u + waves - 1) / waves;
+    const uint32_t min_ch = (nblk + (1u << 18) - 1) >> 18;
+    return std::max(std::max(1u, min_ch), std::min(ch, std::min(nblk, 256u)));
+}
+
+// list / list_n: the batch's occupied slots (nullptr: models 0 .. kmax - 1)
+hipError_t enqueue_score_e16(usac_ctx *c, uint32_t kmax, float thr, const uint32_t *list, const uint32_t *list_n) {
+    hipError_t e;
+    if ((e = h16_consts_init(c)) != hipSuccess) return e;
+    if (!c->e16_feat_ok) {
+        if ((e = c->e16_feat.reserve(usac::h16_feature_bytes(c->n))) != hipSuccess) return e;
+        if ((e = usac::launch_e16_points(c->stream, c->pts.as<float4>(), c->n, c->h16_k.as<usac::H16Consts>(),
+                                         c->e16_feat.p)) != hipSuccess)
+            return e;
+        c->e16_feat_ok = true;
+    }
+    const uint32_t ch = e16_chunks(c, kmax);
+    if ((e = c->e16_rows.reserve(usac::e16_row_bytes(kmax))) != hipSuccess) return e;
+    if ((e = c->e16_cm.reserve(sizeof(float) * (size_t)kmax)) != hipSuccess) return e;
+    if ((e = c->e16_part.reserve(usac::e16_part_bytes(kmax, (int)ch))) != hipSuccess) return e;
+    const size_t stride = kmax;
+    if ((e = usac::launch_e16_rows(c->stream, c->models.as<float>(), stride, list, list_n, kmax,
+                                   c->h16_k.as<usac::H16Consts>(), thr, c->e16_rows.p, c->e16_cm.as<float>())) !=
+        hipSuccess)
+        return e;
+    return usac::launch_score_e16(c->stream, c->e16_feat.p, c->pts.as<float4>(), c->n, c->e16_rows.p,
+                                  c->e16_cm.as<float>(), c->models.as<float>(), stride, list, list_n, kmax, thr,
+                                  (int)ch, c->e16_part.p, c->counts.as<int32_t>(), c->sums.as<float>());
+}
+
 // chunks == 1 is the parity configuration: per-hypothesis sums are the exact sequential
 // fp32 sums of the reference.  chunks > 1 re-associates Σerr across chunks (counts exact).
 hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks, bool defer_finish = false) {
@@ -742,6 +803,8 @@ hipError_t enqueue_score(usac_ctx *c, uint32_t B, float thr, int chunks, bool de
                                         c->models.as<float>(), (size_t)B * c->spk, c->list.as<uint32_t>(),
                                         c->list_n.as<uint32_t>(), B * c->spk, thr, c->counts.as<int32_t>(),
                                         c->sums.as<float>());
+        if (e16_scores(c, chunks, thr))  // counts exact
+            return enqueue_score_e16(c, B * c->spk, thr, c->list.as<uint32_t>(), c->list_n.as<uint32_t>());
         hipError_t e = c->tv_part.reserve(usac::tv_scratch_bytes(B * c->spk, chunks));
         if (e != hipSuccess) return e;
         return usac::launch_score_f2(c->stream, c->estimator, chunks, c->rec.as<float4>(), c->pts.as<float4>(), c->n,
@@ -1823,6 +1886,8 @@ int usac_create(usac_ctx **out, int device, int estimator, const float *pts, uin
             c->ext = make_float4(mx[0], mx[1], mx[2], mx[3]);
             const char *h16env = getenv("USAC_H16");
             c->h16 = !h16env || atoi(h16env) != 0 ? 1 : 0;
+            const char *e16env = getenv("USAC_E16");
+            c->e16 = !e16env || atoi(e16env) != 0 ? 1 : 0;
         }
         if (e != hipSuccess) { rc = fail(c, USAC_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e)); break; }
     } while (0);
@@ -1865,7 +1930,7 @@ void usac_destroy(usac_ctx *c) {
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->h4_fb, &c->h4_fb_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,
                       &c->sprt_tested, &c->sprt_surv, &c->sprt_surv_n, &c->sprt_starts, &c->inl_scratch, &c->e5_ws, &c->one_model,
-                      &c->h16_k, &c->h16_feat, &c->h16_rows, &c->h16_fm, &c->h16_part,
+                      &c->h16_k, &c->h16_feat, &c->h16_rows, &c->h16_fm, &c->h16_part, &c->e16_feat, &c->e16_rows, &c->e16_cm, &c->e16_part,
                       &c->inl_idx, &c->pol_lists, &c->pol_res, &c->inl_cnt, &c->inl_sum, &c->q, &c->partial, &c->ws, &c->nm_model, &c->nm_ok, &c->nm_seq, &c->nm_w, &c->nm_qw, &c->lo_io,
                       &c->rec_send, &c->rec_all, &c->tv_part, &c->hf_part, &c->prosac_tab, &c->lo_max, &c->lo_lists, &c->lo_pos,
                       &c->lo_ns, &c->lo_thrs, &c->lo_slots, &c->lo_models, &c->lo_ok, &c->lo_cnts, &c->lo_sums,
@@ -1956,6 +2021,9 @@ int usac_score_models(usac_ctx *c, const float *models, uint32_t nm, float thr, 
             HIP_TRY(c, usac::launch_score_f(c->stream, c->estimator, 1, c->pts.as<float4>(), c->n,
                                             c->models.as<float>(), nm, nullptr, nullptr, nm, thr,
                                             c->counts.as<int32_t>(), c->sums.as<float>()));
+        } else if (c->score_variant == 3 && is_e(c) && c->e16 == 1 && thr > 0x1p-100f && thr < 0x1p100f) {
+            // variant 3 (tests): the matrix-core throughput scorer -- counts exact, Σ within its bound
+            HIP_TRY(c, enqueue_score_e16(c, nm, thr, nullptr, nullptr));
         } else {  // the fast two-view kernel, one chunk: exact sequential sums
             if (c->rec_thr != thr) {
                 HIP_TRY(c, c->rec.reserve(sizeof(float) * 32 * (((size_t)c->n + 3) / 4)));
@@ -2118,6 +2186,54 @@ int usac_hypothesize_async(usac_ctx *c, uint32_t B, uint64_t seed, uint64_t firs
     HIP_TRY(c, batch_argmax(c, B * c->spk, first_hyp));
     HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
     c->timed_pending = true;
+    return USAC_OK;
+}
+
+int usac_selftest_rpoly(usac_ctx *c, const double *coeffs, uint32_t B, double *roots, int32_t *nroots) {
+    if (!c || !coeffs || !roots || !nroots || B == 0) return USAC_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    DevBuf dc, dr, dn, ws;
+    struct Rel {
+        DevBuf *b[4];
+        ~Rel() {
+            (void)hipDeviceSynchronize();
+            for (DevBuf *x : b) x->release();
+        }
+    } rel{{&dc, &dr, &dn, &ws}};
+    HIP_TRY(c, dc.reserve(sizeof(double) * 11 * (size_t)B));
+    HIP_TRY(c, dr.reserve(sizeof(double) * 10 * (size_t)B));
+    HIP_TRY(c, dn.reserve(sizeof(int32_t) * (size_t)B));
+    HIP_TRY(c, ws.reserve(usac::e5_workspace_bytes(B)));
+    HIP_TRY(c, hipMemcpyAsync(dc.p, coeffs, sizeof(double) * 11 * (size_t)B, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, usac::launch_e5_roots_selftest(c->stream, dc.as<double>(), B, dr.as<double>(), dn.as<int32_t>(), ws.p));
+    std::vector<double> r(10 * (size_t)B);
+    HIP_TRY(c, hipMemcpyAsync(r.data(), dr.p, sizeof(double) * 10 * (size_t)B, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(nroots, dn.p, sizeof(int32_t) * (size_t)B, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
+    for (uint32_t h = 0; h < B; h++)  // device layout [r B + h] -> row h
+        for (int k = 0; k < 10; k++) roots[10 * (size_t)h + k] = k < nroots[h] ? r[(size_t)k * B + h] : 0.0;
+    return USAC_OK;
+}
+
+int usac_selftest_logexp(usac_ctx *c, const double *x, uint32_t n, double *log_out, double *exp_out) {
+    if (!c || !x || !log_out || !exp_out || n == 0) return USAC_ERR_ARG;
+    HIP_TRY(c, hipSetDevice(c->device));
+    DevBuf dx, dl, de;
+    struct Rel {
+        DevBuf *b[3];
+        ~Rel() {
+            (void)hipDeviceSynchronize();
+            for (DevBuf *y : b) y->release();
+        }
+    } rel{{&dx, &dl, &de}};
+    HIP_TRY(c, dx.reserve(sizeof(double) * n));
+    HIP_TRY(c, dl.reserve(sizeof(double) * n));
+    HIP_TRY(c, de.reserve(sizeof(double) * n));
+    HIP_TRY(c, hipMemcpyAsync(dx.p, x, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, usac::launch_jt_logexp_selftest(c->stream, dx.as<double>(), n, dl.as<double>(), de.as<double>()));
+    HIP_TRY(c, hipMemcpyAsync(log_out, dl.p, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(exp_out, de.p, sizeof(double) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, stream_wait(c->stream));
     return USAC_OK;
 }
 
@@ -2467,16 +2583,18 @@ static int ransac_run_impl(usac_ctx *c, const usac_params *prm, int nranks, int 
                            uint32_t rec_cap) {
     if (!c || !prm || !out || nranks < 1 || rank < 0 || rank >= nranks) return USAC_ERR_ARG;
     memset(out, 0, sizeof(*out));
-    // The loop scores with k_score_hf, never the matrix-core scorer: its batches are small (the
-    // ramp; h16's per-batch rows + finish launches cost more than they save: cfg5 3.30 ms per run
-    // with k_score_hf, 3.8-3.9 with h16), and its speculative batch runs beside the main stream's
-    // recount / LO kernels, where h16 was seen to corrupt a concurrent recount.
+    // The loop scores homographies with k_score_hf, not the matrix-core scorer: its batches are
+    // small (the ramp; h16's per-batch rows + finish launches cost more than they save: cfg5 3.30 ms
+    // per run with k_score_hf, 3.8-3.9 with h16).  USAC_LOOP_H16=1 lets the loop use it (tests: the
+    // round-5 miscount beside the speculative h16 batch was packed-fp32 VALU corruption beside MFMA
+    // waves, gone since the library issues no packed fp32 instruction -- usac_pk.hpp).
     struct H16Off {
         usac_ctx *c;
         bool saved;
         ~H16Off() { c->h16_off = saved; }
     } h16_off{c, c->h16_off};
-    c->h16_off = true;
+    const bool loop_h16 = getenv("USAC_LOOP_H16") && atoi(getenv("USAC_LOOP_H16")) != 0;
+    c->h16_off = !loop_h16;
     if (nranks > 1 && !gather && (!c->comm || c->nranks != nranks || c->rank != rank))
         return fail(c, USAC_ERR_ARG, "sharded run without a gather callback needs usac_comm_init(nranks, rank)");
     const bool prosac = prm->sampler == USAC_SAMPLER_PROSAC;

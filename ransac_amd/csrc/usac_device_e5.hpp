@@ -5,12 +5,14 @@
 // Written to the spec the oracle restates (oracle/usac_oracle.c "essential (5-pt)"): the
 // same IEEE operation sequence -- fp64 throughout the solver, no FMA contraction, correctly
 // rounded division and square root -- so device and oracle agree bit for bit.  The
-// reference's OpenCV SVD / determinant / inv and rpoly are replaced by: row Jacobi + null
-// complement (basis), LU with partial pivoting (det M(z) at z = -5..5), Newton divided
-// differences (degree-10 coefficients), derivative-recursion root isolation + bisection
-// (real roots), elimination with partial pivoting (null vector of M(z)), and a cheirality
-// test through Jacobi 3x3 SVD + 4x4 linear triangulation.
+// reference's OpenCV SVD / determinant / inv are replaced by: row Jacobi + null complement
+// (basis), LU with partial pivoting (det M(z) at z = -5..5), Newton divided differences
+// (degree-10 coefficients), elimination with partial pivoting (null vector of M(z)), and a
+// cheirality test through Jacobi 3x3 SVD + 4x4 linear triangulation; its rpoly root step is
+// restated operation for operation (usac_rpoly.hpp: the same zeros in the same order).
 #pragma once
+#include <float.h>
+
 #include <type_traits>
 
 #include "usac_device.hpp"
@@ -303,6 +305,10 @@ __device__ __forceinline__ bool null10(double (&A)[10][10], double (&v)[10]) {
     return true;
 }
 
+// ---- the candidate values: real roots of det M(z), ascending (the oracle's asc_real_roots):
+// derivative-recursion isolation + safeguarded Newton.  The reference's ORDER of the candidates
+// (rpoly's, which decides the selected model when several pass cheirality) comes from the
+// Jenkins-Traub restatement in usac_rpoly.hpp, run only for the samples that need it (k_e5_order).
 // Horner with fused multiply-adds (oracle poly_eval / poly_eval2)
 __device__ __forceinline__ double poly_eval(const double *c, int deg, double x) {
     double r = c[deg];
@@ -687,6 +693,39 @@ __device__ __forceinline__ float essential_error(const float *E, float x1, float
     const float b1 = t1 * x2 + t2 * y2 + t3;
     const float b2 = sqrtf(t1 * t1 + t2 * t2);
     return (fabsf(a1 / a2) + fabsf(b1 / b2)) / 2;
+}
+
+// The guarded essential residual of the throughput drains (C > 1: Σ is re-associated anyway and
+// its terms may carry a stated error; the counts stay exact).  The reference's l, t, a1, b1 and
+// squared norms (the same unfused operations), then e' = (|a1| rsq(a2²) + |b1| rsq(b2²)) / 2
+// with v_rsq_f32 (1 ulp) instead of two correctly rounded square roots and two IEEE divisions.
+// Per term the two differ by < 2^-21 relative (rsq 2^-23, the product and the reference's sqrt
+// and division 2^-24 each), so |e' - e| <= e' 2^-19: e' <= thr (1 - 2^-16) proves e < thr and
+// e' >= thr (1 + 2^-16) proves !(e < thr).  Pairs inside that band, squared norms outside
+// [2^-96, inf) (denormal / zero / overflowing rsq) and non-finite values take the exact
+// expression.  Returns the error added to Σ: e' for a proven inlier, else the exact e.
+__device__ __forceinline__ float essential_error_guarded(const float *E, float x1, float y1, float x2, float y2,
+                                                         float thr, float lo, float hi, bool &inl) {
+    const float l1 = E[0] * x2 + E[3] * y2 + E[6];
+    const float l2 = E[1] * x2 + E[4] * y2 + E[7];
+    const float l3 = E[2] * x2 + E[5] * y2 + E[8];
+    const float t1 = E[0] * x1 + E[1] * y1 + E[2];
+    const float t2 = E[3] * x1 + E[4] * y1 + E[5];
+    const float t3 = E[6] * x1 + E[7] * y1 + E[8];
+    const float a1 = l1 * x1 + l2 * y1 + l3;
+    const float qa = l1 * l1 + l2 * l2;
+    const float b1 = t1 * x2 + t2 * y2 + t3;
+    const float qb = t1 * t1 + t2 * t2;
+    const float ef = (fabsf(a1) * __builtin_amdgcn_rsqf(qa) + fabsf(b1) * __builtin_amdgcn_rsqf(qb)) * 0.5f;
+    const bool normal = qa >= 1.2621774483536189e-29f && qb >= 1.2621774483536189e-29f &&  // 2^-96
+                        qa < INFINITY && qb < INFINITY;
+    if (__builtin_expect(normal && (ef <= lo || ef >= hi), 1)) {
+        inl = ef <= lo;
+        return ef;
+    }
+    const float e = (fabsf(a1 / sqrtf(qa)) + fabsf(b1 / sqrtf(qb))) / 2;  // essential_error, bit for bit
+    inl = e < thr;
+    return e;
 }
 
 }  // namespace usac

@@ -5,13 +5,13 @@
 #include <hip/hip_runtime.h>
 
 #include "usac_device.hpp"
+#include "usac_pk.hpp"
 
 namespace usac {
 
 // Model registers of a lane: h[9] = H, hi[9] = H^-1; plus the lane's stage-A error
 // bounds dZ, E (below), and H / dZ / E duplicated into both halves of 2-wide vectors for the
 // packed stage A (two points per v_pk_fma_f32).
-typedef float v2f __attribute__((ext_vector_type(2)));
 
 struct HModel {
     float h[9], hi[9];
@@ -55,11 +55,11 @@ __device__ __forceinline__ void stage_a_bounds(HModel &M, float4 c, float T) {
 // error is not finite or not below thr.  Returns the KEEP flags.
 __device__ __forceinline__ void stage_a_keep2(const HModel &M, v2f x1, v2f y1, v2f x2, v2f y2, bool &k0,
                                               bool &k1) {
-    const v2f X = __builtin_elementwise_fma(M.h2[1], y1, __builtin_elementwise_fma(M.h2[0], x1, M.h2[2]));
-    const v2f Y = __builtin_elementwise_fma(M.h2[4], y1, __builtin_elementwise_fma(M.h2[3], x1, M.h2[5]));
-    const v2f Z = __builtin_elementwise_fma(M.h2[7], y1, __builtin_elementwise_fma(M.h2[6], x1, M.h2[8]));
-    const v2f ex = __builtin_elementwise_fma(x2, Z, -X);
-    const v2f ey = __builtin_elementwise_fma(y2, Z, -Y);
+    const v2f X = vfma(M.h2[1], y1, vfma(M.h2[0], x1, M.h2[2]));
+    const v2f Y = vfma(M.h2[4], y1, vfma(M.h2[3], x1, M.h2[5]));
+    const v2f Z = vfma(M.h2[7], y1, vfma(M.h2[6], x1, M.h2[8]));
+    const v2f ex = vfma(x2, Z, -X);
+    const v2f ey = vfma(y2, Z, -Y);
     const float m0 = __builtin_fmaxf(fabsf(ex.x), fabsf(ey.x)), m1 = __builtin_fmaxf(fabsf(ex.y), fabsf(ey.y));
     k0 = !(m0 > __builtin_fmaf(fabsf(Z.x), M.trm, M.F));
     k1 = !(m1 > __builtin_fmaf(fabsf(Z.y), M.trm, M.F));

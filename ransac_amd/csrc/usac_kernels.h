@@ -105,6 +105,29 @@ hipError_t launch_score_h16(hipStream_t st, const void *feat, const float4 *pts,
 // Σ's fixed-point exponent of the h16 chunk partials for threshold thr
 int h16_fixed_point(float thr);
 
+// Matrix-core prefilter scorer of essential matrices (kernels_e16.hip, DESIGN.md §6 "e16"): fp16
+// features of the h16 layout divided by each point's rho (once per context), per batch each listed
+// model's fp16 coefficient row (32 B) and rejection bound (e16_row_bytes(kmax), kmax floats), then the
+// scorer over `chunks` point chunks (part = e16_part_bytes(kmax, chunks)); counts exact, Σ from
+// fixed-point guarded terms, written at the listed slots
+// self-test hooks (usac_selftest_*): the 5-point root step alone on B given polynomials (11 ascending
+// coefficients each) -> roots (10 x B doubles, root r of polynomial h at [r B + h]) and their numbers;
+// workspace = e5_workspace_bytes(B).  The root step's correctly rounded log / exp on n arguments.
+hipError_t launch_e5_roots_selftest(hipStream_t st, const double *coef, uint32_t B, double *roots, int32_t *nroots,
+                                    void *workspace);
+hipError_t launch_jt_logexp_selftest(hipStream_t st, const double *x, uint32_t n, double *lg, double *ex);
+
+hipError_t launch_e16_points(hipStream_t st, const float4 *pts, uint32_t n, const H16Consts *k, void *feat);
+size_t e16_row_bytes(uint32_t kmax);
+hipError_t launch_e16_rows(hipStream_t st, const float *models, size_t stride, const uint32_t *list,
+                           const uint32_t *list_n, uint32_t kmax, const H16Consts *k, float thr, void *rows,
+                           float *cm);
+size_t e16_part_bytes(uint32_t kmax, int chunks);
+hipError_t launch_score_e16(hipStream_t st, const void *feat, const float4 *pts, uint32_t n, const void *rows,
+                            const float *cm, const float *models, size_t stride, const uint32_t *list,
+                            const uint32_t *list_n, uint32_t kmax, float thr, int chunks, void *part,
+                            int32_t *counts, float *sums);
+
 hipError_t launch_solve_line(hipStream_t st, const float2 *pts, uint32_t n, const int32_t *samples_in,
                              int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, float *models);
 hipError_t launch_prepare_line(hipStream_t st, const float *in, uint32_t B, float *models);

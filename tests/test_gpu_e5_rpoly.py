@@ -1,0 +1,75 @@
+"""The device's 5-point root step (usac_rpoly.hpp: the reference's rpoly_ak1, rpoly.cpp:7-750) against the
+oracle's restatement (usac_oracle.c jt_rpoly), through the self-test hooks (include/usac_gpu.h ABI 13):
+
+* its log / exp -- the table-driven fast path with Ziv's rounding test and the double-double slow
+  path -- equal the oracle's correctly rounded values on random and edge arguments;
+* on 65 536 degree-10 polynomials (the solver's own det M(z) of cfg4 samples, random ones over eight
+  decades, zeros at the origin, the committed rpoly fixture) the device reports the oracle's real
+  zeros bit for bit and in the same order -- including the ~0.1 % that exceed k_e5_roots' step budget
+  and go to k_e5_roots_tail (the 20 shift attempts of a search side by side)."""
+import os
+
+import numpy as np
+import pytest
+
+from ransac_amd import synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx(usac):
+    pts, _, _ = synthetic.fundamental_points(n=1000, inlier_ratio=0.3, seed=1, normalized=True)
+    with usac.Context(usac.ESTIMATOR.Essential, pts) as c:
+        yield c
+
+
+def test_device_log_exp_equal_oracle(ctx, oracle):
+    rng = np.random.default_rng(2)
+    xs = np.r_[np.ldexp(rng.uniform(0.5, 1.0, 200000), rng.integers(-1060, 1024, 200000)),
+               rng.uniform(0.25, 4.0, 100000), 1.0 + rng.uniform(-1e-6, 1e-6, 20000),
+               [1.0, 2.0, 0.5, np.sqrt(0.5), 4.9e-324, 2.2250738585072014e-308, 1.7976931348623157e308, 0.0, -1.0,
+                np.inf, np.nan]]
+    ys = np.r_[rng.uniform(-745, 710, 200000), rng.uniform(-5, 5, 100000), rng.uniform(-1e-3, 1e-3, 20000),
+               [0.0, -0.0, 709.78, -745.1, 710.0, -750.0, 1e-300, np.inf, -np.inf, np.nan, 1.0]]
+    lg, _ = ctx.selftest_logexp(xs)
+    _, ex = ctx.selftest_logexp(ys)
+    ol = np.array([oracle.jt_log(x) for x in xs])
+    oe = np.array([oracle.jt_exp(y) for y in ys])
+    np.testing.assert_array_equal(lg.view(np.int64)[np.isfinite(ol)], ol.view(np.int64)[np.isfinite(ol)])
+    np.testing.assert_array_equal(np.isnan(lg), np.isnan(ol))
+    np.testing.assert_array_equal(ex.view(np.int64)[~np.isnan(oe)], oe.view(np.int64)[~np.isnan(oe)])
+
+
+def _polys(oracle):
+    pts, _, _ = synthetic.fundamental_points(n=50000, inlier_ratio=0.3, seed=1, normalized=True)
+    est = oracle.Estimator(oracle.ESSENTIAL, pts)
+    polys = [oracle.e5_poly(est, s) for s in oracle.uniform_samples(23, len(pts), 5, 40000)]
+    rng = np.random.default_rng(5)
+    for _ in range(24000):
+        polys.append((rng.uniform(size=11) - 0.5) * 10.0 ** ((rng.uniform(size=11) - 0.5) * 8))
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "rpoly_ref.npz"))
+    polys += [a for a, d in zip(g["coeffs"], g["degree"]) if d == 10]
+    extra = []
+    for a in polys[:600]:
+        b = np.array(a, np.float64)
+        b[0] = 0.0
+        extra.append(b)
+        c = b.copy()
+        c[1] = 0.0
+        extra.append(c)
+    polys += extra
+    return np.array(polys[:65536], np.float64)
+
+
+def test_device_rpoly_equals_oracle(ctx, oracle):
+    A = _polys(oracle)
+    roots, n = ctx.selftest_rpoly(A)
+    bad = []
+    for h, a in enumerate(A):
+        o = oracle.real_roots(a)
+        if n[h] != len(o) or not np.array_equal(roots[h, : n[h]].view(np.int64), o.view(np.int64)):
+            bad.append(h)
+    assert not bad, "%d of %d polynomials differ, e.g. %d: device %s oracle %s" % (
+        len(bad), len(A), bad[0], roots[bad[0], : n[bad[0]]], oracle.real_roots(A[bad[0]]))
+    assert (n > 0).mean() > 0.5

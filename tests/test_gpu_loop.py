@@ -123,11 +123,16 @@ def _run_loop(usac, pts, est, sampler, thr, seed, lo, spec):
     return r.getRansacOutput(), r.records
 
 
-def test_speculation_on_off_identical(usac):
+@pytest.mark.parametrize("loop_h16", ["0", "1"])
+def test_speculation_on_off_identical(usac, loop_h16, monkeypatch):
     """The loop's next batch drawn and solved ahead of the replay: with the library's
     ramping batches, runs with and without the speculation give the same records, iterations,
     model bits and inliers -- Uniform and NAPSAC, with and without LO -- and the journal rollback
-    (a speculative batch cut short by a new termination bound) is exercised."""
+    (a speculative batch cut short by a new termination bound) is exercised.  loop_h16 = "1"
+    (USAC_LOOP_H16): the speculative batches scored by the matrix-core k_score_h16 beside the main
+    stream's exact recount and LO kernels -- the configuration that miscounted in round 5 (packed
+    fp32 beside MFMA waves)."""
+    monkeypatch.setenv("USAC_LOOP_H16", loop_h16)
     rollbacks = batches = 0
     for kind, sampler, lo in [("H", usac.SAMPLER.Uniform, 0), ("H", usac.SAMPLER.Uniform, 1),
                               ("Hc", usac.SAMPLER.Napsac, 0), ("Hc", usac.SAMPLER.Napsac, 1),

@@ -62,11 +62,13 @@ def test_loop_napsac_lo_identical(usac, oracle, kind, sampler, lo, sprt):
     assert (out.getInliers() == ref["inlier_idx"]).all()
 
 
-@pytest.mark.parametrize("lo", [1, 2])
-def test_cfg5_full_size(usac, oracle, lo):
+@pytest.mark.parametrize("lo,loop_h16", [(1, "0"), (2, "0"), (1, "1"), (2, "1")])
+def test_cfg5_full_size(usac, oracle, lo, loop_h16, monkeypatch):
     """BASELINE configs[4] at full size: homography + NAPSAC (grid) + LO-RANSAC over 100k
     correspondences -- the device loop's iterations, records, LO counters, final model and
-    inlier list identical to the oracle's."""
+    inlier list identical to the oracle's; loop_h16 = "1": its batches scored by the matrix-core
+    k_score_h16 (USAC_LOOP_H16), the speculative ones beside the recount and LO kernels."""
+    monkeypatch.setenv("USAC_LOOP_H16", loop_h16)
     pts, _, _ = synthetic.homography_points(n=100000, inlier_ratio=0.2, seed=11, cluster=(500, 500, 150))
     ref = oracle.ransac_run(oracle.HOMOGRAPHY, pts, 2.0, 0.95, 5, sampler=oracle.SAMPLER_NAPSAC, sprt=False, lo=lo,
                             max_iters=5000)

@@ -139,9 +139,10 @@ def test_five_point_candidates_contain_exact_E(oracle):
             # 1e-3: the selected zero may be a late one of rpoly's deflation order, whose value
             # (and E) carries the deflation's larger error -- as in the reference
             assert sv[2] <= 1e-3 * sv[0] and abs(sv[0] - sv[1]) <= 1e-3 * sv[0]
-            # the returned E is the FIRST candidate passing cheirality (five_points.cpp:239-273)
-            first = int(np.argmax(ok))
-            assert ok.any() and np.array_equal(ms[0], cand[first])
+            # the returned E is a passing candidate -- the only one when one passes (the order among
+            # several: test_e5_selection_follows_reference_rpoly_order)
+            hits = [k for k in range(len(cand)) if ok[k] and np.array_equal(ms[0], cand[k])]
+            assert hits and (ok.sum() > 1 or hits == [int(np.argmax(ok))])
     assert hit >= 95 and returned >= 95
 
 
@@ -192,21 +193,18 @@ def _residual(a, x):
 
 
 def test_e5_roots_pinned_against_reference_rpoly(oracle):
-    """the 5-point solver's root step IS the reference's rpoly_ak1
+    """the 5-point solver's root step follows the reference's rpoly_ak1
     (usac/estimator/essential/rpoly.cpp:7-750, restated in usac_oracle.c jt_rpoly; the reference
     compiled where it lies into oracle/_ref by oracle/Makefile).  On the oracle's degree-10
     polynomials of 10 000 cfg4 samples the restatement reports the same zeros in the same order,
     bit for bit, on >= 99.9 % of the samples (the rest: the root bound's last bits, where glibc's
-    exp / log misround -- same order, zeros within 1e-9); and the candidate the solver selects --
-    the first real zero in rpoly's order whose E passes cheirality (five_points.cpp:143-157,
-    239-273) -- is the one the reference's order selects on >= 99.9 % of the samples with a
-    passing candidate."""
+    exp / log misround -- same order, zeros within 1e-9)."""
     if not oracle.rpoly_ref_available():
         pytest.skip("oracle/_ref/librpoly_ref.so not built (the reference is absent)")
     pts, _, _ = synthetic.fundamental_points(n=50000, inlier_ratio=0.3, seed=1, normalized=True)
     est = oracle.Estimator(oracle.ESSENTIAL, pts)
     samples = oracle.uniform_samples(11, len(pts), 5, 10000)
-    n_exact, n_near, n_sel, n_sel_diff = 0, 0, 0, 0
+    n_exact = n_near = 0
     for s in samples:
         a = oracle.e5_poly(est, s)
         zr, zi = oracle.rpoly_zeros(a)
@@ -218,18 +216,49 @@ def test_e5_roots_pinned_against_reference_rpoly(oracle):
             n_near += 1
             z, r = zr + 1j * zi, rr + 1j * ri
             assert np.all(np.abs(z - r) <= 1e-9 * np.maximum(np.abs(r), 1.0)), (s, z, r)
-        ours = oracle.real_roots(a)
-        ref = rr[ri == 0]
-        assert len(ours) == len(ref)
-        # the selection: the solver's first passing candidate against the reference order's
+    print("rpoly pin: %d / %d samples bit-exact, %d within 1e-9" % (n_exact, len(samples), n_near))
+    assert n_near <= 0.001 * len(samples)
+
+
+def test_e5_selection_follows_reference_rpoly_order(oracle):
+    """five_points.cpp:239-273 returns the first candidate in rpoly's order that passes cheirality.
+    The solver's candidates are the real roots ascending (asc_real_roots); when several pass it takes
+    the one nearest the earliest rpoly zero (the restatement's order).  Against the reference's own
+    rpoly (oracle/_ref): on 10 000 cfg4 samples the selected model is the candidate the reference's
+    order selects on >= 99.9 % of the samples with several passing candidates (round 5
+    scanned ascending and differed on 14.7 % of the samples with a passing candidate)."""
+    if not oracle.rpoly_ref_available():
+        pytest.skip("oracle/_ref/librpoly_ref.so not built (the reference is absent)")
+    pts, _, _ = synthetic.fundamental_points(n=50000, inlier_ratio=0.3, seed=1, normalized=True)
+    est = oracle.Estimator(oracle.ESSENTIAL, pts)
+    n_multi = n_diff = n_one = 0
+    for s in oracle.uniform_samples(11, len(pts), 5, 10000):
         cand, ok = est.e5_candidates(s)
-        if len(cand) == len(ours) and ok.any():
-            n_sel += 1
-            first = int(np.argmax(ok))
-            n_sel_diff += int(np.argmin(np.abs(ref - ours[first]))) != first
-    print("rpoly pin: %d / %d samples bit-exact, %d within 1e-9; selection differs on %d of %d samples with a "
-          "passing candidate" % (n_exact, len(samples), n_near, n_sel_diff, n_sel))
-    assert n_near <= 0.001 * len(samples) and n_sel > 3000 and n_sel_diff <= 0.001 * n_sel
+        if ok.sum() == 0:
+            continue
+        ms = est.estimate(s)
+        assert len(ms) == 1
+        mine = [k for k in range(len(cand)) if ok[k] and np.array_equal(ms[0], cand[k])]
+        assert mine
+        a = oracle.e5_poly(est, s)
+        roots = oracle.asc_roots(a)
+        if len(roots) != len(cand):  # a candidate without a null vector (not reported): skip the mapping
+            continue
+        if ok.sum() == 1:
+            n_one += 1
+            continue
+        n_multi += 1
+        rr, ri = oracle.rpoly_ref_zeros(a)
+        ref_pick = None
+        for z in rr[ri == 0]:  # the reference: its zeros in order, the first whose candidate passes
+            k = int(np.argmin(np.abs(roots - z)))
+            if ok[k]:
+                ref_pick = k
+                break
+        n_diff += ref_pick != mine[0]
+    print("selection: %d samples with several passing candidates, %d differ from the reference's order "
+          "(%d with one)" % (n_multi, n_diff, n_one))
+    assert n_multi > 500 and n_diff <= 0.001 * n_multi
 
 
 def test_rpoly_restatement_matches_golden(oracle):
