@@ -71,9 +71,10 @@ def parse():
                     help="untimed device warm-up before the warmup steps (throughput lines): batches are run "
                          "for this long first, so the timed steps see the GPU at its sustained clocks even when "
                          "--warmup is a handful of steps (0 = off)")
-    ap.add_argument("--pipeline", type=int, default=3,
+    ap.add_argument("--pipeline", type=int, default=None,
                     help="batches in flight: one context (stream + buffers) per in-flight batch, so batch i+1's "
-                         "solve overlaps batch i's scoring")
+                         "solve overlaps batch i's scoring (default 3; essential 8: its root-order kernels are "
+                         "long and narrow, see DESIGN.md §3)")
     args = ap.parse_args()
     ess = args.estimator == "essential"
     if args.points is None:
@@ -89,6 +90,8 @@ def parse():
         args.sampler = "prosac" if fund else "uniform"
     if args.batch is None:
         args.batch = 262144 if fund and args.sprt else 65536
+    if args.pipeline is None:
+        args.pipeline = 8 if ess else 3
     return args
 
 
@@ -1012,6 +1015,10 @@ def main():
     if os.environ.get("USAC_BENCH_SAME_DEVICE"):  # rehearsal of the N > 1 path on a 1-GPU box
         local_rank = 0
     _DEV = local_rank
+    # one hardware queue per in-flight batch (HIP's default is 4 per process: more contexts would share
+    # queues and serialise behind each other's long kernels); set before the runtime initialises
+    if args.pipeline > int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4):
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.pipeline, 16))
     import torch  # noqa: F401  (torch.distributed rendezvous; loads the process's HIP runtime first)
     import torch.distributed as dist
 

@@ -13,8 +13,13 @@
 //   keep iff |r~'| < C,   C = 2^e C0 (1 + 2^-20) + D,   C0 = delta + thr (1 + 2^-19) (S + 2^-21 M + 2^-100),
 // delta = 2^-20 Mabs + 2^-120 bounds |a1 - r| and |b1 - r| of the reference's fp32 chains (Mabs = the
 // dataset box's bound of sum |E_jk p2_j p1_k|), M = the box's bound of ||l12|| and ||t12|| (their fp32
-// evaluation is within 2^-21 M of the exact norms), D the fp16 / MFMA rounding bound of kernels_h16.hip
-// (usac_h16.hpp) over the feature maxima, 2^e the hypothesis' power-of-two scale.  A rejected pair has
+// evaluation is within 2^-21 M of the exact norms), 2^e the hypothesis' power-of-two scale, and D the
+// bound of the matrix cores' rounding: coefficients and features are split into fp16 hi + lo parts and
+// two chained MFMAs add gh fh + gl fh + gh fl (the lo parts of seven coefficients ride in the spare K
+// slots of the first, the rest in the second), so the products miss only gl fl and the parts' own
+// roundings -- D = (1 + 2^-10) sum_k [2^-17 a_k fmax_k + 2^-23 (a_k + fmax_k)], a_k = |gh_k| + |gl_k| +
+// 2^-24, fmax the dataset's feature maxima (k_h16_consts) -- instead of ~2^-10 of the products with one
+// fp16 part each (twice the kept pairs on cfg4: the drain and the append, not the MFMA, are the cost).  A rejected pair has
 // (1 - 2^-22)(|r| - delta) >= thr max(a2, b2) for the reference's own a2, b2, i.e. err >= thr: not an
 // inlier.  Hypotheses whose bounds are not finite or whose box bounds reach 2^60 (fp32 overflow in
 // the reference's chain) get zero rows and C = +inf (every pair to the exact stage); padding and
@@ -38,18 +43,22 @@ typedef float e16_f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kE16NA = 2;                       // 32-hypothesis tiles per wave
 constexpr int kE16HW = 32 * kE16NA;             // hypotheses per wave
-constexpr uint32_t kE16Queue = 64u * 16u + 64u;  // ring: < 64 waiting + one tile's appends
+constexpr uint32_t kE16Queue = 2048u;  // ring (a power of two): < 64 waiting + one tile's appends (<= 1024)
 
 // ------------------------------------------------------------------------ point features / rho
-// the h16 feature layout (lane l of a 32-point block holds B[k = 8 (l >> 5) + j][column l & 31]),
-// every feature divided by the point's rho (rounded up: a larger rho only loosens the test)
+// per 32-point block two B matrices of the h16 layout (lane l holds B[k = 8 (l >> 5) + j][column l & 31]),
+// the features divided by the point's rho (rounded up: a larger rho only loosens the test) and split
+// into fp16 hi + lo parts: B1 = (fh_0 .. fh_8, fh_0 .. fh_6), B2 = (fl_0 .. fl_8, fh_7, fh_8, 0 ..);
+// feat[(2 blk + m) 64 + lane], m = 0 (B1), 1 (B2)
+size_t e16_feature_bytes(uint32_t n) { return (size_t)((n + 31) / 32) * 2048; }
+
 __global__ __launch_bounds__(256) void k_e16_points(const float4 *__restrict__ pts, uint32_t n,
                                                     const H16Consts *__restrict__ kc, half8 *__restrict__ feat) {
     const uint32_t t = blockIdx.x * 256 + threadIdx.x;
     const uint32_t nblk = (n + 31) / 32;
     if (t >= nblk * 64) return;
     const uint32_t blk = t >> 6, l = t & 63, i = blk * 32 + (l & 31), hf = l >> 5;
-    half8 o;
+    half8 o1, o2;
     bool ok = i < n;
     float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
     if (ok) {
@@ -58,17 +67,32 @@ __global__ __launch_bounds__(256) void k_e16_points(const float4 *__restrict__ p
     }
     if (!ok) {
 #pragma unroll
-        for (int j = 0; j < 8; j++) o[j] = (_Float16)__builtin_nanf("");
+        for (int j = 0; j < 8; j++) o1[j] = o2[j] = (_Float16)__builtin_nanf("");
     } else {
         const double x1 = p.x, y1 = p.y, x2 = p.z, y2 = p.w;
         const double rho = fmax(sqrt(x1 * x1 + y1 * y1 + 1.0), sqrt(x2 * x2 + y2 * y2 + 1.0)) * (1.0 + 0x1p-40);
         const double u = (x1 - kc->cx1) / kc->s1, v = (y1 - kc->cy1) / kc->s1;
         const double pp = (x2 - kc->cx2) / kc->s2, q = (y2 - kc->cy2) / kc->s2;
-        const double f[16] = {u, v, 1.0, pp * u, pp * v, pp, q * u, q * v, q, 0, 0, 0, 0, 0, 0, 0};
+        const double f[9] = {u / rho, v / rho, 1.0 / rho, pp * u / rho, pp * v / rho, pp / rho,
+                             q * u / rho, q * v / rho, q / rho};
+        _Float16 fh[9], fl[9];
 #pragma unroll
-        for (int j = 0; j < 8; j++) o[j] = (_Float16)(float)(f[8 * hf + j] / rho);
+        for (int k = 0; k < 9; k++) {
+            fh[k] = (_Float16)(float)f[k];
+            fl[k] = (_Float16)(float)(f[k] - (double)(float)fh[k]);
+        }
+        const _Float16 z = (_Float16)0.0f;
+        const _Float16 b1[16] = {fh[0], fh[1], fh[2], fh[3], fh[4], fh[5], fh[6], fh[7],
+                                 fh[8], fh[0], fh[1], fh[2], fh[3], fh[4], fh[5], fh[6]};
+        const _Float16 b2[16] = {fl[0], fl[1], fl[2], fl[3], fl[4], fl[5], fl[6], fl[7], fl[8], fh[7], fh[8], z, z, z, z, z};
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            o1[j] = b1[8 * hf + j];
+            o2[j] = b2[8 * hf + j];
+        }
     }
-    feat[t] = o;
+    feat[(2 * (size_t)blk) * 64 + l] = o1;
+    feat[(2 * (size_t)blk + 1) * 64 + l] = o2;
 }
 
 hipError_t launch_e16_points(hipStream_t st, const float4 *pts, uint32_t n, const H16Consts *k, void *feat) {
@@ -79,7 +103,8 @@ hipError_t launch_e16_points(hipStream_t st, const float4 *pts, uint32_t n, cons
 }
 
 // ------------------------------------------------------------------------ per-hypothesis rows
-// rows[2 pos + half]: coefficients 8 half .. 8 half + 7 of listed position pos; cm[pos] = C
+// rows[4 pos + 2 m + half]: A1 (m = 0: gh_0 .. gh_8, gl_0 .. gl_6) and A2 (m = 1: gh_0 .. gh_8, gl_7, gl_8,
+// 0 ..) of listed position pos, coefficients 8 half .. 8 half + 7; cm[pos] = C
 __device__ __forceinline__ double e16_up(double x) { return x * (1.0 + 0x1p-40); }
 
 __global__ __launch_bounds__(256) void k_e16_rows(const float *__restrict__ models, size_t stride,
@@ -147,34 +172,43 @@ __global__ __launch_bounds__(256) void k_e16_rows(const float *__restrict__ mode
         mx = fmax(mx, fabs(g[k]));
     }
     fin = fin && mx > 0x1p-100 && mx < 0x1p100;
-    half8 out[2];
+    half8 out[4];
     float cv = INFINITY;
     if (!fin) {
 #pragma unroll
-        for (int hf = 0; hf < 2; hf++)
+        for (int m = 0; m < 4; m++)
 #pragma unroll
-            for (int j = 0; j < 8; j++) out[hf][j] = (_Float16)0.0f;
+            for (int j = 0; j < 8; j++) out[m][j] = (_Float16)0.0f;
     } else {
         const int e = -(ilogb(mx) + 1);  // max |g| 2^e in [0.5, 1)
+        _Float16 gh[9], gl[9];
         double D = 0x1p-100;
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            const double gh = k < 9 ? ldexp(g[k], e) : 0.0;
-            const _Float16 gt = (_Float16)(float)gh;
-            out[k >> 3][k & 7] = gt;
-            if (k < 9) {
-                const double agt = fabs((double)(float)gt), fk = kc->fmax[k];
-                D += agt * (0x1p-10 * fk + 0x1p-25) + fk * (0x1p-10 * fabs(gh) + 0x1p-25 + 0x1p-50 * ldexp(a[k], e)) +
-                     0x1p-19 * agt * (fk + 0x1p-24);
-            }
+        for (int k = 0; k < 9; k++) {
+            const double gs = ldexp(g[k], e);
+            gh[k] = (_Float16)(float)gs;
+            gl[k] = (_Float16)(float)(gs - (double)(float)gh[k]);
+            const double ak = fabs((double)(float)gh[k]) + fabs((double)(float)gl[k]) + 0x1p-24, fk = kc->fmax[k];
+            D += 0x1p-17 * ak * fk + 0x1p-23 * (ak + fk) + 0x1p-50 * ldexp(a[k], e) * fk;
         }
-        const double Cd = e16_up(ldexp(C0, e) * (1.0 + 0x1p-20) + D * (1.0 + 0x1p-18));
+        const _Float16 z = (_Float16)0.0f;
+        const _Float16 a1[16] = {gh[0], gh[1], gh[2], gh[3], gh[4], gh[5], gh[6], gh[7],
+                                 gh[8], gl[0], gl[1], gl[2], gl[3], gl[4], gl[5], gl[6]};
+        const _Float16 a2[16] = {gh[0], gh[1], gh[2], gh[3], gh[4], gh[5], gh[6], gh[7], gh[8], gl[7], gl[8], z, z, z, z, z};
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            out[0][j] = a1[j];
+            out[1][j] = a1[8 + j];
+            out[2][j] = a2[j];
+            out[3][j] = a2[8 + j];
+        }
+        const double Cd = e16_up(ldexp(C0, e) * (1.0 + 0x1p-20) + D * (1.0 + 0x1p-10));
         const float Cf = (float)Cd;
         cv = (double)Cf >= Cd ? Cf : nextafterf(Cf, INFINITY);
         if (!isfinite(cv)) cv = INFINITY;
     }
-    rows[2 * (size_t)i] = out[0];
-    rows[2 * (size_t)i + 1] = out[1];
+#pragma unroll
+    for (int m = 0; m < 4; m++) rows[4 * (size_t)i + m] = out[m];
     cm[i] = cv;
 }
 
@@ -201,7 +235,7 @@ __device__ __forceinline__ void e16_drain(uint32_t cnt, uint32_t head, const uin
     e16_wave_sync();
     if (lane < cnt) {
         const uint32_t qi = head + lane;
-        const uint32_t e = q[qi >= kE16Queue ? qi - kE16Queue : qi];
+        const uint32_t e = q[qi & (kE16Queue - 1)];
         const uint32_t hk = e >> 25, p = e & 0x1FFFFFFu;
         const float4 pt = pts[p];
         float m[9];
@@ -220,7 +254,7 @@ __device__ __forceinline__ void e16_drain(uint32_t cnt, uint32_t head, const uin
 // Workgroup = 4 waves; wave w owns listed positions [hb, hb + 64) and point chunk blockIdx.y.  A
 // fragment of tile a: lane l holds row l & 31 (position hb + 32 a + (l & 31)), coefficients 8 (l >> 5)
 // ..; the D register j of lane l holds row (j & 3) + 4 (l >> 5) + 8 (j >> 2), column l & 31.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_score_e16(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_score_e16(
     const half8 *__restrict__ feat, const float4 *__restrict__ pts, uint32_t n, const half8 *__restrict__ rows,
     const float *__restrict__ cm, const float *__restrict__ models, size_t stride, const uint32_t *__restrict__ list,
     const uint32_t *__restrict__ list_n, uint32_t kmax, float thr, double fxs, uint32_t *__restrict__ cpart,
@@ -242,7 +276,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         sC[wave][lane] = 0;
         sS[wave][lane] = 0;
     }
-    half8 A[kE16NA];
+    half8 A1[kE16NA], A2[kE16NA];
     float Cv[kE16NA][16];
 #pragma unroll
     for (int a = 0; a < kE16NA; a++) {
@@ -250,7 +284,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         half8 z;
 #pragma unroll
         for (int j = 0; j < 8; j++) z[j] = (_Float16)0.0f;
-        A[a] = pos < K ? rows[2 * (size_t)pos + hf] : z;
+        A1[a] = pos < K ? rows[4 * (size_t)pos + hf] : z;
+        A2[a] = pos < K ? rows[4 * (size_t)pos + 2 + hf] : z;
 #pragma unroll
         for (int j = 0; j < 16; j++) {
             const uint32_t pj = hb + 32 * a + (j & 3) + 4 * hf + 8 * (j >> 2);
@@ -264,20 +299,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     uint32_t qn = 0, qh = 0;
     const e16_f32x16 zero = {};
     e16_wave_sync();
-    half8 bn = b0 < b1 ? feat[(size_t)b0 * 64 + lane] : half8{};
+    half8 bn1 = b0 < b1 ? feat[(2 * (size_t)b0) * 64 + lane] : half8{};
+    half8 bn2 = b0 < b1 ? feat[(2 * (size_t)b0 + 1) * 64 + lane] : half8{};
     for (uint32_t blk = b0; blk < b1; blk++) {
-        const half8 bf = bn;
-        if (blk + 1 < b1) bn = feat[(size_t)(blk + 1) * 64 + lane];
+        const half8 bf1 = bn1, bf2 = bn2;
+        if (blk + 1 < b1) {
+            bn1 = feat[(2 * (size_t)blk + 2) * 64 + lane];
+            bn2 = feat[(2 * (size_t)blk + 3) * 64 + lane];
+        }
         e16_f32x16 acc[kE16NA];
 #pragma unroll
-        for (int a = 0; a < kE16NA; a++) acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A[a], bf, zero, 0, 0, 0);
+        for (int a = 0; a < kE16NA; a++) {
+            acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1[a], bf1, zero, 0, 0, 0);
+            acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A2[a], bf2, acc[a], 0, 0, 0);
+        }
         const uint32_t point = blk * 32 + (lane & 31);
 #pragma unroll
         for (int a = 0; a < kE16NA; a++) {
+            bool kp[16];
             uint64_t msk[16], any = 0;
 #pragma unroll
             for (int j = 0; j < 16; j++) {
-                msk[j] = __builtin_amdgcn_ballot_w64(fabsf(acc[a][j]) < Cv[a][j]);
+                kp[j] = fabsf(acc[a][j]) < Cv[a][j];
+                msk[j] = __builtin_amdgcn_ballot_w64(kp[j]);
                 any |= msk[j];
             }
             if (!any) continue;  // wave-uniform
@@ -286,19 +330,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
             for (int j = 0; j < 16; j++) {
                 const uint64_t mk = msk[j];
                 if (mk) {
-                    const uint32_t below =
-                        __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
-                    if ((mk >> lane) & 1) {
-                        const uint32_t qi = qh + qn + below;  // < 2 Q
+                    if (kp[j]) {  // the compare's own lane mask: no lane test
+                        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
+                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
                         const uint32_t hk = 32 * a + (j & 3) + 4 * hf + 8 * (j >> 2);
-                        sQ[wave][qi >= kE16Queue ? qi - kE16Queue : qi] = (hk << 25) | point;
+                        sQ[wave][(qh + qn + below) & (kE16Queue - 1)] = (hk << 25) | point;
                     }
                     qn += (uint32_t)__builtin_popcountll(mk);
                 }
             }
             while (qn >= 64) {
                 e16_drain(64, qh, sQ[wave], sM[wave], sC[wave], sS[wave], pts, thr, lo, hi, fxs);
-                qh = qh + 64 >= kE16Queue ? qh + 64 - kE16Queue : qh + 64;
+                qh = (qh + 64) & (kE16Queue - 1);
                 qn -= 64;
             }
         }
@@ -306,7 +349,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
     while (qn) {
         const uint32_t d = qn < 64 ? qn : 64;
         e16_drain(d, qh, sQ[wave], sM[wave], sC[wave], sS[wave], pts, thr, lo, hi, fxs);
-        qh = qh + d >= kE16Queue ? qh + d - kE16Queue : qh + d;
+        qh = (qh + d) & (kE16Queue - 1);
         qn -= d;
     }
     e16_wave_sync();
@@ -341,7 +384,7 @@ size_t e16_part_bytes(uint32_t kmax, int chunks) {
     return (size_t)chunks * kmax * (sizeof(uint32_t) + sizeof(uint64_t));
 }
 
-size_t e16_row_bytes(uint32_t kmax) { return (size_t)kmax * 32; }
+size_t e16_row_bytes(uint32_t kmax) { return (size_t)kmax * 64; }
 
 hipError_t launch_score_e16(hipStream_t st, const void *feat, const float4 *pts, uint32_t n, const void *rows,
                             const float *cm, const float *models, size_t stride, const uint32_t *list,

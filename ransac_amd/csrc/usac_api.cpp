@@ -752,7 +752,7 @@ hipError_t enqueue_score_e16(usac_ctx *c, uint32_t kmax, float thr, const uint32
     hipError_t e;
     if ((e = h16_consts_init(c)) != hipSuccess) return e;
     if (!c->e16_feat_ok) {
-        if ((e = c->e16_feat.reserve(usac::h16_feature_bytes(c->n))) != hipSuccess) return e;
+        if ((e = c->e16_feat.reserve(usac::e16_feature_bytes(c->n))) != hipSuccess) return e;
         if ((e = usac::launch_e16_points(c->stream, c->pts.as<float4>(), c->n, c->h16_k.as<usac::H16Consts>(),
                                          c->e16_feat.p)) != hipSuccess)
             return e;
@@ -1886,8 +1886,8 @@ int usac_create(usac_ctx **out, int device, int estimator, const float *pts, uin
             c->ext = make_float4(mx[0], mx[1], mx[2], mx[3]);
             const char *h16env = getenv("USAC_H16");
             c->h16 = !h16env || atoi(h16env) != 0 ? 1 : 0;
-            const char *e16env = getenv("USAC_E16");
-            c->e16 = !e16env || atoi(e16env) != 0 ? 1 : 0;
+            const char *e16env = getenv("USAC_E16");  // opt-in until it beats k_score_f2
+            c->e16 = e16env && atoi(e16env) != 0 ? 1 : 0;
         }
         if (e != hipSuccess) { rc = fail(c, USAC_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e)); break; }
     } while (0);

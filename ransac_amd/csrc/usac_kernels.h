@@ -107,7 +107,7 @@ int h16_fixed_point(float thr);
 
 // Matrix-core prefilter scorer of essential matrices (kernels_e16.hip, DESIGN.md §6 "e16"): fp16
 // features of the h16 layout divided by each point's rho (once per context), per batch each listed
-// model's fp16 coefficient row (32 B) and rejection bound (e16_row_bytes(kmax), kmax floats), then the
+// model's fp16 coefficient rows (hi / lo, 64 B) and rejection bound (e16_row_bytes(kmax), kmax floats), then the
 // scorer over `chunks` point chunks (part = e16_part_bytes(kmax, chunks)); counts exact, Σ from
 // fixed-point guarded terms, written at the listed slots
 // self-test hooks (usac_selftest_*): the 5-point root step alone on B given polynomials (11 ascending
@@ -117,6 +117,7 @@ hipError_t launch_e5_roots_selftest(hipStream_t st, const double *coef, uint32_t
                                     void *workspace);
 hipError_t launch_jt_logexp_selftest(hipStream_t st, const double *x, uint32_t n, double *lg, double *ex);
 
+size_t e16_feature_bytes(uint32_t n);
 hipError_t launch_e16_points(hipStream_t st, const float4 *pts, uint32_t n, const H16Consts *k, void *feat);
 size_t e16_row_bytes(uint32_t kmax);
 hipError_t launch_e16_rows(hipStream_t st, const float *models, size_t stride, const uint32_t *list,

@@ -13,6 +13,12 @@ from ransac_amd import synthetic
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def e16_on(monkeypatch):
+    """the scorer is opt-in (USAC_E16=1, read at context creation)"""
+    monkeypatch.setenv("USAC_E16", "1")
+
+
 def _bound(sums_ref, counts, thr):
     c = np.maximum(counts, 0).astype(np.float64)
     return np.abs(sums_ref.astype(np.float64)) * c * 2.0 ** -23 + c * thr * 2.0 ** -18

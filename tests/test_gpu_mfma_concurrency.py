@@ -23,7 +23,8 @@ def _perturbed(M, rng, k, scale):
 
 
 @pytest.mark.parametrize("kind", ["H", "E"])
-def test_exact_recount_beside_matrix_core_batches(usac, kind):
+def test_exact_recount_beside_matrix_core_batches(usac, kind, monkeypatch):
+    monkeypatch.setenv("USAC_E16", "1")  # the essential matrix-core scorer is opt-in
     rng = np.random.default_rng(3)
     if kind == "H":
         pts, M, _ = synthetic.homography_points(n=20000, inlier_ratio=0.3, seed=12)

@@ -3,6 +3,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+os.environ["USAC_E16"] = "1"
 import ransac_amd as usac  # noqa: E402
 from ransac_amd import synthetic  # noqa: E402
 
