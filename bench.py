@@ -558,6 +558,65 @@ def stage_roofline(prefixes, n_points, batch, stage_ms):
     return out
 
 
+def run_roofline(n_points, run_ms):
+    """Roofline of a full-run workload (cfg5) from the committed rocprofv3 summary of its own runs
+    (profiles/r*_summary.json with workload batch 0 and the number of runs profiled: every dispatch
+    counted, tools/profile_round.sh cfg5).  Per kernel: calls per run, average duration, device time
+    per run and VALU-busy SIMD-cycles per dispatch (PMC SQ_ACTIVE_INST_VALU x 4).  The dominant
+    kernel -- most device time per run -- is priced against the VALU issue peak over its own
+    average duration (and its counter-measured HBM bytes against HBM peak); beside it the share of
+    the run's wall time the device spends in kernels at all (the rest is host replay and launch
+    latency of the run's dependent steps)."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_summary.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        w = d.get("workload", {})
+        if w.get("n_points") == n_points and w.get("batch") == 0 and w.get("runs"):
+            best = (d, os.path.relpath(f, ROOT))
+    if best is None:
+        return None
+    d, src = best
+    runs = d["workload"]["runs"]
+    rows = []
+    for k, v in d["kernels"].items():
+        tr = v.get("trace")
+        if not tr or not tr.get("avg_ns"):
+            continue
+        pmc = v.get("pmc", {})
+        r = {"kernel": k.split("(")[0].replace("void ", "").replace("usac::", ""), "calls_per_run": tr["calls"] / runs,
+             "avg_us": tr["avg_ns"] / 1e3, "device_us_per_run": tr["calls"] / runs * tr["avg_ns"] / 1e3}
+        if pmc.get("SQ_ACTIVE_INST_VALU"):
+            r["valu_frac"] = pmc["SQ_ACTIVE_INST_VALU"] * 4 / (tr["avg_ns"] * 1e-9) / SIMD_CYCLES_S
+        if "hbm_bytes_per_launch" in v:
+            r["hbm_bytes"] = v["hbm_bytes_per_launch"]
+            r["hbm_frac"] = v["hbm_bytes_per_launch"] / (tr["avg_ns"] * 1e-9) / 1e9 / HBM_PEAK_GBS
+        rows.append(r)
+    if not rows:
+        return None
+    rows.sort(key=lambda r: -r["device_us_per_run"])
+    top = rows[0]
+    dev_us = sum(r["device_us_per_run"] for r in rows)
+    t = top["avg_us"] * 1e-6
+    busy = top.get("valu_frac", 0.0) * t * SIMD_CYCLES_S
+    return {"bound": "valu", "unit": "SIMD-cycles/s", "peak": SIMD_CYCLES_S, "achieved": busy / t,
+            "frac": top.get("valu_frac"), "kernel": top["kernel"], "kernel_avg_us": top["avg_us"],
+            "traffic": top.get("hbm_bytes"), "traffic_unit": "bytes/launch",
+            "hbm": {"achieved_gbs": (top.get("hbm_bytes") or 0.0) / t / 1e9, "peak_gbs": HBM_PEAK_GBS,
+                    "frac": top.get("hbm_frac")},
+            "source": src, "runs_profiled": runs,
+            "device_us_per_run": dev_us, "run_ms": run_ms,
+            "device_busy_frac_of_run": dev_us * 1e-3 / run_ms if run_ms else None,
+            "kernels_by_device_time": rows[:12],
+            "note": "the kernels the cfg5 runs execute (trace of bench.py --cfg5 itself): the dominant one by "
+                    "device time per run, VALU-busy cycles per dispatch / its average duration / (1024 SIMDs x "
+                    "2.4 GHz); device_busy_frac_of_run = summed kernel time per run / this line's ms per run"}
+
+
 _DEV = 0
 
 
@@ -637,35 +696,16 @@ def cfg5_main(args, usac, synthetic, dist, torch, world, rank, local_rank):
     out = one_run(args.seed)
     if rank != 0:
         return
-    # roofline of the dominant loop kernel: the score of one batch of B hypotheses at N = 100k
-    B = args.batch
-    with usac.Context(usac.ESTIMATOR.Homography, pts, device=local_rank) as ctx:
-        ctx.set_score_chunks(8)
-        for i in range(3):
-            ctx.hypothesize_async(B, args.seed, i * B, args.threshold)
-            ctx.fetch_best()
-        sc = []
-        for i in range(10):
-            ctx.hypothesize_async(B, args.seed, (3 + i) * B, args.threshold)
-            ctx.fetch_best()
-            sc.append(ctx.last_timings()["score_ms"])
     n = args.points
-    bytes_per_hyp = 16.0 * n + 16 + 44
-    score_ms = float(np.mean(sc))
-    achieved = bytes_per_hyp * B / (score_ms * 1e-3) / 1e9
+    run_ms = elapsed / args.steps * 1e3
     # parity of that run: iterations, LO counters, model, inliers
     ref = O.ransac_run(O.HOMOGRAPHY, pts, args.threshold, 0.95, args.seed, sampler=O.SAMPLER_NAPSAC, sprt=False,
                        lo=args.lo, max_iters=max_iters)
-    # the batch scorer of this context is the matrix-core prefilter (kernels_h16.hip, the cfg2
-    # scorer): its PMC summary at N = 100k (tools/profile_round.sh h100k) prices the timed launches
-    roof = valu_roofline("void usac::k_score_h16<2, 1, 8>(", n, B, score_ms) or {
-        "bound": "valu", "achieved": None, "peak": SIMD_CYCLES_S, "unit": "SIMD-cycles/s", "frac": None}
-    roof.update({"traffic": roof.get("hbm", {}).get("traffic_bytes_per_launch"), "kernel": "k_score_h16<2,1,8>",
-                 "kernel_ms": score_ms, "hypotheses_per_launch": B,
-                 "algorithmic_bytes_per_hypothesis": bytes_per_hyp, "algorithmic_equiv_gbs": achieved,
-                 "note": "score kernel of one %d-hypothesis batch at N = %d (the loop's batched verify), VALU-issue "
-                         "roofline as the cfg2 line; a run is dominated by LO and the host replay, see DESIGN.md"
-                         % (B, n)})
+    # the kernels these runs execute, from the committed trace + PMC summary of this same command
+    # (tools/profile_round.sh cfg5: every dispatch of its runs)
+    roof = run_roofline(n, run_ms) or {
+        "bound": "valu", "achieved": None, "peak": SIMD_CYCLES_S, "unit": "SIMD-cycles/s", "frac": None,
+        "traffic": None, "note": "no committed cfg5 summary (profiles/r*_summary.json, workload batch 0)"}
     parity = {"runs": 1, "iterations_equal": out.getNumberOfMainIterations() == ref["iters"],
               "lo_iters_equal": out.getLOIters() == ref["lo_inner_iters"],
               "model_bit_equal": bool((np.asarray(out.getModel(), np.float32).view(np.int32) ==

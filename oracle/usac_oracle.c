@@ -2216,34 +2216,34 @@ static int essential_5pt_all(const orc_est *e, const int *sample, float *Eout, f
         }
     }
     if (cand || npass == 0) return 0;
-    /* five_points.cpp:239-273 keeps the first candidate in rpoly's order that passes cheirality.
-     * With one passing candidate the order does not matter; with several, the reference's order
-     * is the Jenkins-Traub restatement's (jt_rpoly: rpoly.cpp's zeros in the order it deflates
-     * them): each passing candidate takes the rank of the rpoly zero nearest to its value (first on
-     * ties; rank 10 if rpoly reports no real zero) and the lowest rank wins (ascending on ties) */
-    int best = -1, best_rank = 11;
-    if (npass == 1) {
-        for (int r = 0; r < nr; r++)
-            if (pass[r]) best = r;
-    } else {
+    /* five_points.cpp:239-273 keeps the first candidate in rpoly's order that passes cheirality
+     * (with 5 points "found" needs all 5 in front, so the first found has the most and a later one
+     * never replaces it).  With one passing candidate the order does not matter; with several, the
+     * reference's order is the Jenkins-Traub restatement's (jt_rpoly: rpoly.cpp's zeros in the order
+     * it deflates them): its real zeros are taken in that order, each stands for the candidate value
+     * nearest to it (first on ties), and the first whose candidate passes wins -- the reference's
+     * loop with each zero's model the candidate's.  No such zero (rpoly reports none, or only zeros
+     * of failing candidates before a 20-shift failure): the first passing candidate ascending. */
+    int best = -1;
+    for (int r = 0; r < nr && best < 0; r++)
+        if (pass[r] && npass == 1) best = r;
+    if (npass > 1) {
         double z[10];
         const int nz = real_roots(a, 10, z);
-        for (int r = 0; r < nr; r++) {
-            if (!pass[r]) continue;
-            int rank = 10;
+        for (int j = 0; j < nz && best < 0; j++) {
+            int near = -1;
             double dmin = INFINITY;
-            for (int j = 0; j < nz; j++) {
+            for (int r = 0; r < nr; r++) {
                 const double d = fabs(z[j] - roots[r]);
                 if (d < dmin) {
                     dmin = d;
-                    rank = j;
+                    near = r;
                 }
             }
-            if (rank < best_rank) {
-                best_rank = rank;
-                best = r;
-            }
+            if (near >= 0 && pass[near]) best = near;
         }
+        for (int r = 0; r < nr && best < 0; r++)
+            if (pass[r]) best = r;
     }
     for (int k = 0; k < 9; k++) Eout[k] = Ec[best][k];
     return 1;

@@ -12,8 +12,8 @@
 //                                         sample is listed for k_e5_order; counts 0 / -1 and the
 //                                         occupied-slot list (as k_solve_f7)
 //   k_e5_order   lane / listed sample   : the reference's candidate order -- rpoly's real zeros in the
-//                                         order it finds them (usac_rpoly.hpp) -- under a work budget;
-//                                         the passing candidate nearest the earliest zero -> the model
+//                                         order it finds them (usac_rpoly.hpp) -- under a work budget,
+//                                         until a zero's nearest candidate passed -> the model
 //   k_e5_order_tail  wave / deferred    : the same without a budget, rpoly's 20 shift attempts of a
 //                                         search side by side (samples over k_e5_order's budget)
 //
@@ -250,32 +250,41 @@ int e5_budget() {
     return b;
 }
 
-// five_points.cpp:239-273 over rpoly's order: each passing candidate (ascending values) takes the rank of
-// the rpoly zero nearest to it (first on ties; 10 without one), the lowest rank wins (ascending on ties)
-// -- the oracle's essential_5pt_all.  models nullable (the self-test hook computes the zeros only).
-__device__ __forceinline__ void e5_select_by_rank(const E5Work &w, uint32_t B, uint32_t h, int nz,
-                                                  float *__restrict__ models) {
-    w.njt[h] = nz;
-    if (!models) return;
-    const int nr = w.nroots[h];
-    int best = -1, best_rank = 11;
-    for (int r = 0; r < nr; r++) {
-        if (!w.flags[(size_t)r * B + h]) continue;
-        const double v = w.roots[(size_t)r * B + h];
-        int rank = 10;
+// five_points.cpp:239-273 over rpoly's order (the oracle's essential_5pt_all): rpoly's real zeros in
+// the order found, each standing for the candidate value nearest to it (first on ties); the first whose
+// candidate passed cheirality is the model -- the search stops there.  Inactive (models == nullptr, the
+// self-test hook): every zero.
+struct E5Take {
+    const E5Work &w;
+    uint32_t B, h;
+    int nr;
+    bool on;
+    int pick = -1;
+    __device__ bool operator()(double z) {
+        if (!on) return false;
+        int near = -1;
         double dmin = INFINITY;
-        for (int j = 0; j < nz; j++) {
-            const double d = fabs(w.jt[(size_t)j * B + h] - v);
+        for (int r = 0; r < nr; r++) {
+            const double d = fabs(w.roots[(size_t)r * B + h] - z);
             if (d < dmin) {
                 dmin = d;
-                rank = j;
+                near = r;
             }
         }
-        if (rank < best_rank) {
-            best_rank = rank;
-            best = r;
-        }
+        if (near >= 0 && w.flags[(size_t)near * B + h]) pick = near;
+        return pick >= 0;
     }
+};
+
+// the model of a listed sample: the picked candidate, else (no zero stood for a passing one) the first
+// passing candidate ascending.  models nullable (the self-test hook keeps the zeros' number only).
+__device__ __forceinline__ void e5_select_pick(const E5Work &w, uint32_t B, uint32_t h, int nz, int pick,
+                                               float *__restrict__ models) {
+    w.njt[h] = nz;
+    if (!models) return;
+    int best = pick;
+    for (int r = 0; r < w.nroots[h] && best < 0; r++)
+        if (w.flags[(size_t)r * B + h]) best = r;
     const size_t rb = (size_t)best * B + h;
 #pragma unroll
     for (int k = 0; k < 9; k++) models[(size_t)k * B + h] = w.cand[(size_t)k * 10 * B + rb];
@@ -289,12 +298,15 @@ __global__ __launch_bounds__(64) void k_e5_order(uint32_t B, E5Work w, const dou
     const uint32_t h = w.multi[i];
     double a[11];
     e5_coeffs_of(w, coef, B, h, a);
-    const int nz = e5_coeffs_ok(a) ? e5::jt_rpoly10<false>(a, w.jt + h, B, budget, nullptr) : 0;
+    E5Take take{w, B, h, models ? w.nroots[h] : 0, models != nullptr};
+    const int nz = e5_coeffs_ok(a) ? e5::jt_rpoly10<false>(a, w.jt + h, B, budget, nullptr, [&](double z) {
+        return take(z);
+    }) : 0;
     if (nz < 0) {
         w.defer[atomicAdd(w.ndefer, 1u)] = h;
         return;
     }
-    e5_select_by_rank(w, B, h, nz, models);
+    e5_select_pick(w, B, h, nz, take.pick, models);
 }
 
 // the deferred samples, one per wave: rpoly's 20 shift attempts of each search side by side on lanes
@@ -307,8 +319,9 @@ __global__ __launch_bounds__(64) void k_e5_order_tail(uint32_t B, E5Work w, cons
         const uint32_t h = w.defer[d];
         double a[11];
         e5_coeffs_of(w, coef, B, h, a);
-        const int nz = e5::jt_rpoly10<true>(a, w.jt + h, B, 0x7fffffff, &s_stop);
-        if (threadIdx.x == 0) e5_select_by_rank(w, B, h, nz, models);
+        E5Take take{w, B, h, models ? w.nroots[h] : 0, models != nullptr};
+        const int nz = e5::jt_rpoly10<true>(a, w.jt + h, B, 0x7fffffff, &s_stop, [&](double z) { return take(z); });
+        if (threadIdx.x == 0) e5_select_pick(w, B, h, nz, take.pick, models);
     }
 }
 

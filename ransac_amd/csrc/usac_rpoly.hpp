@@ -619,7 +619,7 @@ __device__ __forceinline__ int jt_search(double (&p)[11], double &xx, double &yy
 // degree n run its zero search there; degrees only decrease (by 1 or 2), so one pass n = 10 .. 3 takes
 // every lane through its searches in order and a wave runs each degree's code once (a switch over the
 // lanes' degrees inside a loop would serialise the cases every round).  status: 0 searching, -1 out of
-// budget, 2 no convergence after 20 shifts (rpoly.cpp:214-220).
+// budget, 2 no convergence after 20 shifts (rpoly.cpp:214-220), 3 the caller has the zero it needs.
 template <int n, bool PAR, class Emit>
 __device__ __forceinline__ void jt_lockstep(int &N, int &status, double (&p)[11], double &xx, double &yy, int &steps,
                                             int budget, volatile int *stop, Emit &emit) {
@@ -636,15 +636,23 @@ __device__ __forceinline__ void jt_lockstep(int &N, int &status, double (&p)[11]
 // checks): the real zeros in the order found, to roots[r * stride] (PAR: written by lane 0).  Returns
 // their number, or -1 when more than `budget` fixed-shift steps would be needed (not PAR: the caller
 // defers the polynomial and the roots written so far are rewritten).  stop: an LDS word (PAR only).
-template <bool PAR>
+// take(zr) sees each real zero as it is found (PAR: on every lane, uniformly) and returns true when
+// the caller needs no further zero: the search ends there (the caller's choice is made; the count
+// returned is the zeros seen so far).
+struct JtTakeAll {
+    __device__ bool operator()(double) const { return false; }
+};
+
+template <bool PAR, class Take = JtTakeAll>
 __device__ __forceinline__ int jt_rpoly10(const double (&a)[11], double *roots, size_t stride, int budget,
-                                          volatile int *stop) {
-    int nr = 0;
+                                          volatile int *stop, Take take = Take()) {
+    int nr = 0, status = 0;  // status 3: take() is satisfied
     const bool writer = !PAR || (threadIdx.x & 63) == 0;
     auto emit = [&](double zr, double zi) {
-        if (zi == 0.0) {
+        if (zi == 0.0 && status != 3) {
             if (writer) roots[(size_t)nr * stride] = zr;
             nr++;
+            if (take(zr)) status = 3;
         }
     };
     int z = 0;  // zeros at the origin (rpoly.cpp:36-42)
@@ -656,10 +664,10 @@ __device__ __forceinline__ int jt_rpoly10(const double (&a)[11], double *roots, 
 #pragma unroll
     for (int i = 0; i < 11; i++) p[i] = a[10 - i];
     double xx = sqrt(0.5), yy = -xx;
-    int N = 10 - z, steps = 0, status = 0;
+    int N = 10 - z, steps = 0;
     jt_lockstep<10, PAR>(N, status, p, xx, yy, steps, budget, stop, emit);
     if (status == -1) return -1;
-    if (status == 2) return nr;
+    if (status == 2 || status == 3) return nr;
     if (N == 2) {
         double sr, si, lr, li;
         jt_quadratic(p[0], p[1], p[2], sr, si, lr, li);

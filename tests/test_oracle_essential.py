@@ -222,11 +222,11 @@ def test_e5_roots_pinned_against_reference_rpoly(oracle):
 
 def test_e5_selection_follows_reference_rpoly_order(oracle):
     """five_points.cpp:239-273 returns the first candidate in rpoly's order that passes cheirality.
-    The solver's candidates are the real roots ascending (asc_real_roots); when several pass it takes
-    the one nearest the earliest rpoly zero (the restatement's order).  Against the reference's own
-    rpoly (oracle/_ref): on 10 000 cfg4 samples the selected model is the candidate the reference's
-    order selects on >= 99.9 % of the samples with several passing candidates (round 5
-    scanned ascending and differed on 14.7 % of the samples with a passing candidate)."""
+    The solver's candidates are the real roots ascending (asc_real_roots); when several pass it walks
+    the restatement's zeros in rpoly's order and takes the first whose nearest candidate passes.
+    Against the reference's own rpoly (oracle/_ref): on 10 000 cfg4 samples the selected model is the
+    candidate the reference's order selects on every sample with several passing candidates (VERDICT
+    r5: round 5 scanned ascending and differed on 14.7 % of the samples with a passing candidate)."""
     if not oracle.rpoly_ref_available():
         pytest.skip("oracle/_ref/librpoly_ref.so not built (the reference is absent)")
     pts, _, _ = synthetic.fundamental_points(n=50000, inlier_ratio=0.3, seed=1, normalized=True)
@@ -258,7 +258,7 @@ def test_e5_selection_follows_reference_rpoly_order(oracle):
         n_diff += ref_pick != mine[0]
     print("selection: %d samples with several passing candidates, %d differ from the reference's order "
           "(%d with one)" % (n_multi, n_diff, n_one))
-    assert n_multi > 500 and n_diff <= 0.001 * n_multi
+    assert n_multi > 500 and n_diff == 0
 
 
 def test_rpoly_restatement_matches_golden(oracle):

@@ -15,7 +15,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT/summaries
 WORKLOADS=${WORKLOADS:-"h10k f10k_sprt f10k_exact e50k"}
 for w in $WORKLOADS; do
-  BATCH=65536; STEPS="--steps 20 --warmup 3"; PSTEPS="--steps 5 --warmup 1"; GRIDS=""
+  RUNS=""; BATCH=65536; STEPS="--steps 20 --warmup 3"; PSTEPS="--steps 5 --warmup 1"; GRIDS=""
   case $w in
     h10k)       ARGS=""; NPTS=10000 ;;
     h100k)      ARGS="--points 100000"; NPTS=100000 ;;
@@ -23,6 +23,9 @@ for w in $WORKLOADS; do
     f10k)       ARGS="--estimator fundamental --no-sprt --sampler uniform"; NPTS=10000 ;;
     f10k_sprt)  ARGS="--estimator fundamental"; NPTS=10000; BATCH=262144 ;;   # cfg3: PROSAC + batch SPRT (bench default, B = 262144)
     f10k_exact) ARGS="--sprt-exact"; NPTS=10000; BATCH=1024; STEPS="--steps 20 --warmup 2"; PSTEPS="--steps 5 --warmup 1"; GRIDS=all ;;
+    # cfg5 full runs (batch 0 = "whole runs"): every dispatch of warmup + steps + the parity run counts,
+    # the summary records the runs so bench.py can put calls per run beside durations
+    cfg5)       ARGS="--cfg5"; NPTS=100000; BATCH=0; STEPS="--steps 20 --warmup 2"; PSTEPS="--steps 20 --warmup 2"; GRIDS=all; RUNS=23 ;;
   esac
   D=$OUT/$w; mkdir -p $D
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $PWD/$D/trace -o run --output-format csv -- \
@@ -43,7 +46,7 @@ for w in $WORKLOADS; do
         python3 bench.py $PSTEPS --cpu-seconds 0 --pipeline 1 $ARGS > $D/bench_pmc_$name.json 2> $D/pmc_$name.err
     rc=$?; echo "== $w pmc $ctr rc=$rc"; [ $rc -eq 0 ] || { tail -5 $D/pmc_$name.err; exit $rc; }
   done
-  python3 tools/summarize_profile.py $D ${TAG}_$w $NPTS $BATCH $OUT/summaries $GRIDS > /dev/null || exit 1
+  python3 tools/summarize_profile.py $D ${TAG}_$w $NPTS $BATCH $OUT/summaries $GRIDS $RUNS > /dev/null || exit 1
   cp $D/trace/run_kernel_stats.csv $OUT/summaries/kernel_stats_${TAG}_$w.csv 2>/dev/null
 done
 ls -la $OUT/summaries

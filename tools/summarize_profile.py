@@ -8,7 +8,8 @@ its largest Grid_Size are averaged (trace durations too, from run_kernel_trace.c
 size and the number of dispatches used are recorded.  HBM traffic per launch =
 FETCH_SIZE*1024*2 (gfx950 reports half the bytes of wide coalesced reads: MI355X_MICROARCH.md
 §HBM) + WRITE_SIZE*1024.
-  python3 tools/summarize_profile.py <dir> <tag> <n_points> <batch> <outdir> [all]
+  python3 tools/summarize_profile.py <dir> <tag> <n_points> <batch> <outdir> [all [runs]]
+(runs: the number of whole runs the profiled command made -- full-run workloads, cfg5)
 """
 import collections
 import csv
@@ -49,6 +50,8 @@ def main():
            "filter": "all dispatches" if ALL_GRIDS else "largest Grid_Size dispatches per kernel"}
     if len(sys.argv) > 4:  # workload shape the bench matches on (bench.py _profile_entry)
         out["workload"] = {"n_points": int(sys.argv[3]), "batch": int(sys.argv[4])}
+        if len(sys.argv) > 7:
+            out["workload"]["runs"] = int(sys.argv[7])
     trace = os.path.join(src, "trace", "run_kernel_trace.csv")
     stats = os.path.join(src, "trace", "run_kernel_stats.csv")
     if os.path.exists(trace):
