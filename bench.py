@@ -506,7 +506,7 @@ def _stage_kernels(estimator, sprt, chunks, stage):
     if stage == "solve":
         return {2: ["usac::k_solve_h4("], 3: ["usac::k_solve_f7("],
                 4: ["usac::k_e5_basis(", "usac::k_e5_dets(", "usac::k_e5_roots(", "usac::k_e5_check(",
-                    "usac::k_e5_select("]}[est]
+                    "usac::k_e5_select(", "usac::k_e5_order(", "usac::k_e5_order_tail("]}[est]
     if sprt:
         return ["void usac::k_sprt_head<%d>(" % est, "void usac::k_sprt_tail<%d>(" % est]
     if est == 2:  # the matrix-core prefilter scorer (kernels_h16.hip; USAC_H16=0: k_presort_h + k_score_hf)
@@ -518,6 +518,8 @@ def _stage_kernels(estimator, sprt, chunks, stage):
         if os.environ.get("USAC_H16_DEFER", "1") == "0":  # the chunk sums by their own kernel, not the argmax
             ks = ks + ["usac::k_h16_finish("]
         return ks
+    if est == 4 and os.environ.get("USAC_E16", "1") != "0":  # the matrix-core prefilter scorer (kernels_e16.hip)
+        return ["usac::k_e16_rows(", "usac::k_score_e16(", "usac::k_e16_finish("]
     return ["usac::k_prepare_rec(", "void usac::k_presort_tv<%d>(" % est, "void usac::k_score_f2<%d>(" % est,
             "usac::k_tv_combine("]
 
@@ -1057,8 +1059,10 @@ def main():
     _DEV = local_rank
     # one hardware queue per in-flight batch (HIP's default is 4 per process: more contexts would share
     # queues and serialise behind each other's long kernels); set before the runtime initialises
-    if args.pipeline > int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4):
-        os.environ["GPU_MAX_HW_QUEUES"] = str(min(args.pipeline, 16))
+    # (essential: a second, CU-masked stream per context for its root-order kernels)
+    queues = args.pipeline * (2 if args.estimator == "essential" else 1)
+    if queues > int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4):
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(queues, 16))
     import torch  # noqa: F401  (torch.distributed rendezvous; loads the process's HIP runtime first)
     import torch.distributed as dist
 

@@ -3,7 +3,7 @@
 //
 // The reference's residual (essential_estimator.hpp:76-107) of a pair is
 //   err = (|a1| / ||l12|| + |b1| / ||t12||) / 2,   l = E^T p2, t = E p1, a1 ~ b1 ~ r = p2^T E p1,
-// so err >= |r| / max(||l12||, ||t12||) >= |r| / (S rho): S = max(||E[:, 0:2]^T||_F, ||E[0:2, :]||_F) per
+// so err >= |r| / max(||l12||, ||t12||) >= |r| / (S rho): S = max(||E[:, 0:2]||_2, ||E[0:2, :]||_2) per
 // hypothesis, rho = max(||(x1, y1, 1)||, ||(x2, y2, 1)||) per point.  r is bilinear in the point: a
 // dot product of nine per-hypothesis coefficients G with the nine features f = (u, v, 1, p u, p v, p,
 // q u, q v, q) of the centred, power-of-two-scaled coordinates of kernels_h16.hip (G = T2^T E T1,
@@ -25,8 +25,8 @@
 // the reference's chain) get zero rows and C = +inf (every pair to the exact stage); padding and
 // non-finite points get NaN features (never kept -- the reference never counts them).
 //
-// Kept pairs go through a per-wave LDS ring to the exact stage (essential_error_guarded: counts
-// exact, Σ terms within 2^-19 relative), drained 64 at a time; counts and Σ (2^-fx fixed point,
+// Kept pairs go through per-lane LDS stacks to the exact stage (essential_error_guarded: counts
+// exact, Σ terms within 2^-19 relative), drained in rounds of one entry per lane; counts and Σ (2^-fx fixed point,
 // integer adds, deterministic) per point chunk, added by k_e16_finish.  Models are the listed
 // slots of the batch (list / list_n), as for k_score_f2.
 #include <hip/hip_runtime.h>
@@ -43,7 +43,6 @@ typedef float e16_f32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int kE16NA = 2;                       // 32-hypothesis tiles per wave
 constexpr int kE16HW = 32 * kE16NA;             // hypotheses per wave
-constexpr uint32_t kE16Queue = 2048u;  // ring (a power of two): < 64 waiting + one tile's appends (<= 1024)
 
 // ------------------------------------------------------------------------ point features / rho
 // per 32-point block two B matrices of the h16 layout (lane l holds B[k = 8 (l >> 5) + j][column l & 31]),
@@ -122,24 +121,36 @@ __global__ __launch_bounds__(256) void k_e16_rows(const float *__restrict__ mode
     const float4 c = kc->ext;
     const double C1[3] = {c.x, c.y, 1.0}, C2[3] = {c.z, c.w, 1.0};
     // box bounds: Mabs >= sum |E_jk| |p2_j| |p1_k|, M >= ||l12||, ||t12|| (l_k = sum_j E_jk p2_j, t_j = sum_k E_jk p1_k)
-    double Mabs = 0.0, Lb[2] = {0.0, 0.0}, Tb[2] = {0.0, 0.0}, SA = 0.0, SB = 0.0;
+    double Mabs = 0.0, Lb[2] = {0.0, 0.0}, Tb[2] = {0.0, 0.0};
 #pragma unroll
     for (int j = 0; j < 3; j++)
 #pragma unroll
         for (int k = 0; k < 3; k++) {
             const double a = fabs(E[3 * j + k]);
             Mabs += a * C2[j] * C1[k];
-            if (k < 2) {
-                Lb[k] += a * C2[j];
-                SA += a * a;
-            }
-            if (j < 2) {
-                Tb[j] += a * C1[k];
-                SB += a * a;
-            }
+            if (k < 2) Lb[k] += a * C2[j];
+            if (j < 2) Tb[j] += a * C1[k];
         }
     const double M = e16_up(fmax(sqrt(Lb[0] * Lb[0] + Lb[1] * Lb[1]), sqrt(Tb[0] * Tb[0] + Tb[1] * Tb[1])));
-    const double S = e16_up(fmax(sqrt(SA), sqrt(SB)));
+    // S >= the spectral norms of E[:, 0:2] (l12 = E[:, 0:2]^T p2) and E[0:2, :] (t12 = E[0:2, :] p1): the
+    // larger eigenvalue of each 2 x 2 Gram matrix, (g00 + g11) / 2 + sqrt(((g00 - g11) / 2)^2 + g01^2), is
+    // within ~40 ulp of the computed one relative to g00 + g11 <= 2 lambda, so (1 + 2^-40) covers it
+    // (round 6: Frobenius norms before -- up to sqrt 2 larger, 23 % more kept pairs on cfg4)
+    double gA[3] = {0.0, 0.0, 0.0}, gB[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        gA[0] += E[3 * j] * E[3 * j];
+        gA[1] += E[3 * j + 1] * E[3 * j + 1];
+        gA[2] += E[3 * j] * E[3 * j + 1];
+        gB[0] += E[j] * E[j];
+        gB[1] += E[3 + j] * E[3 + j];
+        gB[2] += E[j] * E[3 + j];
+    }
+    auto lmax = [](const double (&g)[3]) {
+        const double h = 0.5 * (g[0] - g[1]);
+        return e16_up(e16_up(0.5 * (g[0] + g[1]) + sqrt(h * h + g[2] * g[2])));
+    };
+    const double S = e16_up(sqrt(fmax(lmax(gA), lmax(gB))));
     const double delta = e16_up(0x1p-20 * e16_up(Mabs)) + 0x1p-120;
     const double C0 = e16_up(delta + e16_up((double)thr * (1.0 + 0x1p-19) * (S + 0x1p-21 * M + 0x1p-100)));
     // G = T2^T E T1 in the feature order (u, v, 1 | p u, p v, p | q u, q v, q): row 2, row 0, row 1
@@ -226,16 +237,17 @@ __device__ __forceinline__ void e16_wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// Drain cnt (<= 64) ring entries from head: lane i evaluates entry head + i (the guarded residual:
-// exact inlier decision) and adds an inlier to its hypothesis' LDS counters.
-__device__ __forceinline__ void e16_drain(uint32_t cnt, uint32_t head, const uint32_t *q, const float (*sm)[9],
-                                          uint32_t *sc, unsigned long long *ss, const float4 *__restrict__ pts,
-                                          float thr, float lo, float hi, double fxs) {
-    const uint32_t lane = threadIdx.x & 63;
-    e16_wave_sync();
-    if (lane < cnt) {
-        const uint32_t qi = head + lane;
-        const uint32_t e = q[qi & (kE16Queue - 1)];
+// per-lane stacks: lane l keeps the pairs of its own point column, kE16Lane entries
+// (LDS [entry][lane]: a push of all 64 lanes is one conflict-free ds_write); a tile pushes at most 16
+// per lane, so a drain round runs before a tile while any stack holds more than kE16Lane - 16, and
+// whenever >= kE16Round lanes hold an entry (a round: every lane with an entry evaluates its top one;
+// the order of the integer count / fixed-point Σ adds does not matter)
+constexpr uint32_t kE16Lane = 32u, kE16Round = 48u;
+
+__device__ __forceinline__ void e16_drain_lane(bool has, uint32_t e, const float (*sm)[9], uint32_t *sc,
+                                               unsigned long long *ss, const float4 *__restrict__ pts, float thr,
+                                               float lo, float hi, double fxs) {
+    if (has) {
         const uint32_t hk = e >> 25, p = e & 0x1FFFFFFu;
         const float4 pt = pts[p];
         float m[9];
@@ -248,7 +260,6 @@ __device__ __forceinline__ void e16_drain(uint32_t cnt, uint32_t head, const uin
             atomicAdd(&ss[hk], (unsigned long long)llrint((double)val * fxs));
         }
     }
-    e16_wave_sync();
 }
 
 // Workgroup = 4 waves; wave w owns listed positions [hb, hb + 64) and point chunk blockIdx.y.  A
@@ -262,7 +273,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     __shared__ float sM[4][kE16HW][9];
     __shared__ uint32_t sC[4][kE16HW];
     __shared__ unsigned long long sS[4][kE16HW];
-    __shared__ uint32_t sQ[4][kE16Queue];
+    __shared__ uint32_t sQ[4][kE16Lane][64];
     const uint32_t K = list ? __builtin_amdgcn_readfirstlane(*list_n) : kmax;
     const uint32_t lane = threadIdx.x & 63, hf = lane >> 5;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -296,11 +307,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     const uint32_t per = (nblk + nch - 1) / nch;
     const uint32_t b0 = ch * per < nblk ? ch * per : nblk, b1 = b0 + per < nblk ? b0 + per : nblk;
     const float lo = thr * 0.9999847412109375f, hi = thr * 1.0000152587890625f;  // thr (1 -+ 2^-16)
-    uint32_t qn = 0, qh = 0;
+    uint32_t d = 0;  // this lane's stack depth
     const e16_f32x16 zero = {};
     e16_wave_sync();
     half8 bn1 = b0 < b1 ? feat[(2 * (size_t)b0) * 64 + lane] : half8{};
     half8 bn2 = b0 < b1 ? feat[(2 * (size_t)b0 + 1) * 64 + lane] : half8{};
+    uint32_t *const q = &sQ[wave][0][lane];
     for (uint32_t blk = b0; blk < b1; blk++) {
         const half8 bf1 = bn1, bf2 = bn2;
         if (blk + 1 < b1) {
@@ -316,41 +328,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         const uint32_t point = blk * 32 + (lane & 31);
 #pragma unroll
         for (int a = 0; a < kE16NA; a++) {
-            bool kp[16];
-            uint64_t msk[16], any = 0;
+            // drain rounds until the tile's pushes fit and fewer than kE16Round lanes hold an entry
+            for (;;) {
+                const uint64_t ne = __builtin_amdgcn_ballot_w64(d > 0);
+                if (__builtin_popcountll(ne) < (int)kE16Round && __builtin_amdgcn_ballot_w64(d > kE16Lane - 16) == 0)
+                    break;
+                const bool has = d > 0;
+                d -= has ? 1u : 0u;
+                e16_wave_sync();
+                e16_drain_lane(has, q[64 * d], sM[wave], sC[wave], sS[wave], pts, thr, lo, hi, fxs);
+                e16_wave_sync();
+            }
+            // push: every lane writes the slot above its top, a kept pair keeps it
+            const uint32_t e0 = ((uint32_t)(32 * a + 4 * hf) << 25) | point;
 #pragma unroll
             for (int j = 0; j < 16; j++) {
-                kp[j] = fabsf(acc[a][j]) < Cv[a][j];
-                msk[j] = __builtin_amdgcn_ballot_w64(kp[j]);
-                any |= msk[j];
-            }
-            if (!any) continue;  // wave-uniform
-            // append the kept pairs of tile a (<= 1024), then drain full groups of 64
-#pragma unroll
-            for (int j = 0; j < 16; j++) {
-                const uint64_t mk = msk[j];
-                if (mk) {
-                    if (kp[j]) {  // the compare's own lane mask: no lane test
-                        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32),
-                                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
-                        const uint32_t hk = 32 * a + (j & 3) + 4 * hf + 8 * (j >> 2);
-                        sQ[wave][(qh + qn + below) & (kE16Queue - 1)] = (hk << 25) | point;
-                    }
-                    qn += (uint32_t)__builtin_popcountll(mk);
-                }
-            }
-            while (qn >= 64) {
-                e16_drain(64, qh, sQ[wave], sM[wave], sC[wave], sS[wave], pts, thr, lo, hi, fxs);
-                qh = (qh + 64) & (kE16Queue - 1);
-                qn -= 64;
+                q[64 * d] = e0 + ((uint32_t)((j & 3) + 8 * (j >> 2)) << 25);
+                d += fabsf(acc[a][j]) < Cv[a][j] ? 1u : 0u;
             }
         }
     }
-    while (qn) {
-        const uint32_t d = qn < 64 ? qn : 64;
-        e16_drain(d, qh, sQ[wave], sM[wave], sC[wave], sS[wave], pts, thr, lo, hi, fxs);
-        qh = (qh + d) & (kE16Queue - 1);
-        qn -= d;
+    for (;;) {
+        if (__builtin_amdgcn_ballot_w64(d > 0) == 0) break;
+        const bool has = d > 0;
+        d -= has ? 1u : 0u;
+        e16_wave_sync();
+        e16_drain_lane(has, q[64 * d], sM[wave], sC[wave], sS[wave], pts, thr, lo, hi, fxs);
+        e16_wave_sync();
     }
     e16_wave_sync();
     if (hb + lane < K) {

@@ -400,7 +400,8 @@ __global__ __launch_bounds__(64) void k_e5_select(uint32_t B, E5Work w, float *_
 
 hipError_t launch_solve_e5(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
                            int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, float *models,
-                           int32_t *counts, uint32_t *list, uint32_t *list_n, void *workspace) {
+                           int32_t *counts, uint32_t *list, uint32_t *list_n, void *workspace, hipStream_t thin,
+                           hipEvent_t ev_in, hipEvent_t ev_out) {
     const E5Work w = e5_carve(workspace, B);
     hipError_t e = hipMemsetAsync(list_n, 0, sizeof(uint32_t), st);
     if (e == hipSuccess) e = hipMemsetAsync(w.npairs, 0, sizeof(uint32_t), st);
@@ -413,9 +414,22 @@ hipError_t launch_solve_e5(hipStream_t st, const float4 *pts, uint32_t n, const 
     hipLaunchKernelGGL(k_e5_roots, g1, dim3(64), 0, st, B, w);
     hipLaunchKernelGGL(k_e5_check, g10, dim3(64), 0, st, pts, B, 10 * B, w);
     hipLaunchKernelGGL(k_e5_select, g1, dim3(64), 0, st, B, w, models, counts, list, list_n);
-    hipLaunchKernelGGL(k_e5_order, g1, dim3(64), 0, st, B, w, nullptr, e5_budget(), models);
-    hipLaunchKernelGGL(k_e5_order_tail, dim3(std::min(1024u, (B + 63) / 64)), dim3(64), 0, st, B, w, nullptr, models);
-    return hipGetLastError();
+    // the order kernels hold one ~260-register wave per SIMD for hundreds of microseconds: on a CU-masked
+    // stream they keep off most of the chip, where the other batches' wide kernels run
+    hipStream_t os = st;
+    if (thin && ev_in && ev_out) {
+        if ((e = hipEventRecord(ev_in, st)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(thin, ev_in, 0)) != hipSuccess) return e;
+        os = thin;
+    }
+    hipLaunchKernelGGL(k_e5_order, g1, dim3(64), 0, os, B, w, nullptr, e5_budget(), models);
+    hipLaunchKernelGGL(k_e5_order_tail, dim3(std::min(1024u, (B + 63) / 64)), dim3(64), 0, os, B, w, nullptr, models);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (os != st) {
+        if ((e = hipEventRecord(ev_out, os)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(st, ev_out, 0)) != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 // self-test hooks: rpoly's zeros (k_e5_order's schedule: budget, deferral, tail) of given polynomials;

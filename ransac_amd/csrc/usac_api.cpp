@@ -155,6 +155,39 @@ struct StreamPool {
         std::lock_guard<std::mutex> g(mu);
         streams.emplace(dev, s);
     }
+    // streams restricted to a few CUs spread over the device (hipExtStreamCreateWithCUMask), pooled
+    // apart; cus <= 0 or >= the device's CU count: none (nullptr)
+    std::multimap<int, hipStream_t> masked;
+    hipError_t masked_stream(int cus, hipStream_t *s) {
+        *s = nullptr;
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        {
+            std::lock_guard<std::mutex> g(mu);
+            auto it = masked.find(dev);
+            if (it != masked.end()) {
+                *s = it->second;
+                masked.erase(it);
+                return hipSuccess;
+            }
+        }
+        int ncu = 0;
+        hipError_t e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e != hipSuccess) return e;
+        if (cus <= 0 || cus >= ncu) return hipSuccess;
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int k = 0; k < cus; k++) {
+            const int cu = (int)((long long)k * ncu / cus);
+            mask[cu / 32] |= 1u << (cu % 32);
+        }
+        return hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data());
+    }
+    void give_back_masked(hipStream_t s) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        std::lock_guard<std::mutex> g(mu);
+        masked.emplace(dev, s);
+    }
     void give_back(hipEvent_t ev) {
         int dev = 0;
         (void)hipGetDevice(&dev);
@@ -362,6 +395,8 @@ struct usac_ctx {
     size_t lo_best_pin_bytes = 0;
     // the loop's next batch drawn and run ahead of the current batch's replay (usac_ransac_run)
     hipStream_t spec_stream = nullptr;
+    hipStream_t thin_stream = nullptr;  // CU-masked: the essential solver's root-order kernels
+    hipEvent_t thin_ev[2] = {nullptr, nullptr};
     hipEvent_t spec_ev = nullptr;
     // per block parity: the stage's outputs in the host block (main), its Σ (side); round end
     hipEvent_t lo_ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -619,9 +654,18 @@ hipError_t enqueue_solve(usac_ctx *c, const int32_t *samples_dev, uint32_t B, ui
     if (is_e(c)) {
         hipError_t e = c->e5_ws.reserve(usac::e5_workspace_bytes(B));
         if (e != hipSuccess) return e;
+        // USAC_E5_THIN_CUS = k > 0: the root-order kernels on a stream masked to k CUs (default 0: the
+        // context stream -- measured faster once every context has its own hardware queue)
+        static const int thin_cus = getenv("USAC_E5_THIN_CUS") ? atoi(getenv("USAC_E5_THIN_CUS")) : 0;
+        if (thin_cus > 0 && !c->thin_stream) {
+            if ((e = StreamPool::get().masked_stream(thin_cus, &c->thin_stream)) != hipSuccess) return e;
+            for (auto &ev : c->thin_ev)
+                if (!ev && (e = StreamPool::get().event(&ev)) != hipSuccess) return e;
+        }
         return usac::launch_solve_e5(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, ds,
                                      first_hyp, c->models.as<float>(), c->counts.as<int32_t>(),
-                                     c->list.as<uint32_t>(), c->list_n.as<uint32_t>(), c->e5_ws.p);
+                                     c->list.as<uint32_t>(), c->list_n.as<uint32_t>(), c->e5_ws.p, c->thin_stream,
+                                     c->thin_ev[0], c->thin_ev[1]);
     }
     if (is_f(c))
         return usac::launch_solve_f7(c->stream, c->pts.as<float4>(), c->n, samples_dev, samples_out, B, ds,
@@ -1886,8 +1930,8 @@ int usac_create(usac_ctx **out, int device, int estimator, const float *pts, uin
             c->ext = make_float4(mx[0], mx[1], mx[2], mx[3]);
             const char *h16env = getenv("USAC_H16");
             c->h16 = !h16env || atoi(h16env) != 0 ? 1 : 0;
-            const char *e16env = getenv("USAC_E16");  // opt-in until it beats k_score_f2
-            c->e16 = e16env && atoi(e16env) != 0 ? 1 : 0;
+            const char *e16env = getenv("USAC_E16");  // USAC_E16=0: k_score_f2 for every essential batch
+            c->e16 = !e16env || atoi(e16env) != 0 ? 1 : 0;
         }
         if (e != hipSuccess) { rc = fail(c, USAC_ERR_HIP, std::string("hipMemcpy: ") + hipGetErrorString(e)); break; }
     } while (0);
@@ -1910,6 +1954,7 @@ void usac_destroy(usac_ctx *c) {
     if (c->xstream) (void)hipStreamSynchronize(c->xstream);
     if (c->lo_stream) (void)hipStreamSynchronize(c->lo_stream);
     if (c->spec_stream) (void)hipStreamSynchronize(c->spec_stream);
+    if (c->thin_stream) (void)hipStreamSynchronize(c->thin_stream);
     if (c->comm) ncclCommDestroy(c->comm);
     if (c->pol_pin) PinnedPool::get().give_back(c->pol_pin, c->pol_pin_bytes);
     if (c->x_pin) PinnedPool::get().give_back(c->x_pin, c->x_pin_bytes);
@@ -1926,6 +1971,9 @@ void usac_destroy(usac_ctx *c) {
     if (c->lo_best_pin) PinnedPool::get().give_back(c->lo_best_pin, c->lo_best_pin_bytes);
     if (c->spec_ev) StreamPool::get().give_back(c->spec_ev);
     if (c->spec_stream) StreamPool::get().give_back(c->spec_stream);
+    if (c->thin_stream) StreamPool::get().give_back_masked(c->thin_stream);
+    for (auto &ev : c->thin_ev)
+        if (ev) StreamPool::get().give_back(ev);
     if (c->grid_pin) PinnedPool::get().give_back(c->grid_pin, c->grid_pin_bytes);
     for (DevBuf *b : {&c->pts, &c->rec, &c->perm, &c->samples, &c->models, &c->counts, &c->sums, &c->best, &c->hostmodels,
                       &c->argmax_part, &c->list, &c->list_n, &c->h4_fb, &c->h4_fb_n, &c->pool_idx, &c->pool_pts, &c->masks, &c->sprt_pts,

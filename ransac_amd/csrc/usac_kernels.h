@@ -173,9 +173,12 @@ hipError_t launch_score_f2(hipStream_t st, int estimator, int chunks, const floa
 size_t tv_scratch_bytes(uint32_t kmax, int chunks);
 // essential 5-point (kernels_ess.hip): one slot per sample (models [9][B], counts 0 / -1,
 // list / list_n); workspace = e5_workspace_bytes(B)
+// thin (nullable): a CU-masked stream for the root-order kernels (k_e5_order / k_e5_order_tail: one
+// register-heavy wave per SIMD for long), ordered against st by ev_in / ev_out
 hipError_t launch_solve_e5(hipStream_t st, const float4 *pts, uint32_t n, const int32_t *samples_in,
                            int32_t *samples_out, uint32_t B, DevSampler ds, uint64_t first_hyp, float *models,
-                           int32_t *counts, uint32_t *list, uint32_t *list_n, void *workspace);
+                           int32_t *counts, uint32_t *list, uint32_t *list_n, void *workspace,
+                           hipStream_t thin = nullptr, hipEvent_t ev_in = nullptr, hipEvent_t ev_out = nullptr);
 size_t e5_workspace_bytes(uint32_t B);
 
 // SPRT parity support (kernels_sprt.hip): points permuted into pool order, and per-model

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(autouse=True)
 def e16_on(monkeypatch):
-    """the scorer is opt-in (USAC_E16=1, read at context creation)"""
+    """the scorer is the default (USAC_E16 unset or 1, read at context creation); pinned on here"""
     monkeypatch.setenv("USAC_E16", "1")
 
 

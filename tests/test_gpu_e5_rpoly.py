@@ -6,7 +6,7 @@ oracle's restatement (usac_oracle.c jt_rpoly), through the self-test hooks (incl
 * on 65 536 degree-10 polynomials (the solver's own det M(z) of cfg4 samples, random ones over eight
   decades, zeros at the origin, the committed rpoly fixture) the device reports the oracle's real
   zeros bit for bit and in the same order -- including the ~0.1 % that exceed k_e5_roots' step budget
-  and go to k_e5_roots_tail (the 20 shift attempts of a search side by side)."""
+  and go to k_e5_order_tail (the 20 shift attempts of a search side by side)."""
 import os
 
 import numpy as np

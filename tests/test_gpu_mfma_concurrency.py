@@ -24,7 +24,7 @@ def _perturbed(M, rng, k, scale):
 
 @pytest.mark.parametrize("kind", ["H", "E"])
 def test_exact_recount_beside_matrix_core_batches(usac, kind, monkeypatch):
-    monkeypatch.setenv("USAC_E16", "1")  # the essential matrix-core scorer is opt-in
+    monkeypatch.setenv("USAC_E16", "1")  # the essential matrix-core scorer (the default), pinned on
     rng = np.random.default_rng(3)
     if kind == "H":
         pts, M, _ = synthetic.homography_points(n=20000, inlier_ratio=0.3, seed=12)
