@@ -73,8 +73,8 @@ def parse():
                          "--warmup is a handful of steps (0 = off)")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="batches in flight: one context (stream + buffers) per in-flight batch, so batch i+1's "
-                         "solve overlaps batch i's scoring (default 3; essential 8: its root-order kernels are "
-                         "long and narrow, see DESIGN.md §3)")
+                         "solve overlaps batch i's scoring (default 3; essential 12 at N = 1, else 8: its "
+                         "root-order kernels are long and narrow, DESIGN.md §6)")
     args = ap.parse_args()
     ess = args.estimator == "essential"
     if args.points is None:
@@ -90,8 +90,8 @@ def parse():
         args.sampler = "prosac" if fund else "uniform"
     if args.batch is None:
         args.batch = 262144 if fund and args.sprt else 65536
-    if args.pipeline is None:
-        args.pipeline = 8 if ess else 3
+    if args.pipeline is None:  # essential: 12 in flight at N = 1 (the N > 1 exchange ring holds 8)
+        args.pipeline = (12 if args.gpus == 1 else 8) if ess else 3
     return args
 
 
@@ -1062,7 +1062,7 @@ def main():
     # (essential: a second, CU-masked stream per context for its root-order kernels)
     queues = args.pipeline * (2 if args.estimator == "essential" else 1)
     if queues > int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4):
-        os.environ["GPU_MAX_HW_QUEUES"] = str(min(queues, 16))
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(queues, 32))
     import torch  # noqa: F401  (torch.distributed rendezvous; loads the process's HIP runtime first)
     import torch.distributed as dist
 
@@ -1088,7 +1088,8 @@ def main():
     dlt_mode = 0 if args.dlt == "thin" else 1
     est_id = usac.ESTIMATOR.Fundamental if fund else usac.ESTIMATOR.Essential if ess else usac.ESTIMATOR.Homography
     P = max(1, args.pipeline)
-    assert P <= usac.Context.XRING, "at most %d batches in flight (exchange ring)" % usac.Context.XRING
+    # the N > 1 exchange keeps one ring slot per batch in flight
+    assert world == 1 or P <= usac.Context.XRING, "at most %d batches in flight (exchange ring)" % usac.Context.XRING
     ctxs = [usac.Context(est_id, pts, device=local_rank) for _ in range(P)]
     for c in ctxs:
         c.set_dlt_mode(dlt_mode)
