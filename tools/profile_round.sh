@@ -33,7 +33,7 @@ for w in $WORKLOADS; do
   rc=$?; echo "== $w trace rc=$rc"; [ $rc -eq 0 ] || { tail -5 $D/trace.err; exit $rc; }
   PASSES=(FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
           "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVES")
-  if [ $w = h10k ] || [ $w = h100k ]; then  # the matrix-core scorer (kernels_h16.hip): MFMA busy, LDS / SALU issue
+  if [ $w = h10k ] || [ $w = h100k ] || [ $w = e50k ]; then  # the matrix-core scorers (h16 / e16): MFMA busy, LDS / SALU issue
     PASSES+=("SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE")
   fi
   if [ $w = h10k ]; then
