@@ -237,18 +237,19 @@ __device__ __forceinline__ void e16_wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// per-lane stacks: lane l keeps the pairs of its own point column, kE16Lane entries
-// (LDS [entry][lane]: a push of all 64 lanes is one conflict-free ds_write); a tile pushes at most 16
-// per lane, so a drain round runs before a tile while any stack holds more than kE16Lane - 16, and
-// whenever >= kE16Round lanes hold an entry (a round: every lane with an entry evaluates its top one;
-// the order of the integer count / fixed-point Σ adds does not matter)
-constexpr uint32_t kE16Lane = 32u, kE16Round = 48u;
+// per-lane stacks of tile masks: for each tile lane l pushes one entry -- the 16-bit mask of the
+// tile's hypotheses its point kept (built one compare + one add-with-carry per hypothesis), the
+// tile and the block -- if any was kept (LDS [entry][lane]: a push of all 64 lanes is one
+// conflict-free ds_write_b64).  A drain round: every lane with an entry evaluates one kept pair of
+// its top entry (the lowest mask bit) and clears it, popping the entry when its mask empties; rounds
+// run before a tile while >= kE16Round lanes hold an entry or a stack is full (a tile pushes at most
+// one).  The order of the integer count / fixed-point Σ adds does not matter.
+constexpr uint32_t kE16Lane = 8u, kE16Round = 48u;
 
-__device__ __forceinline__ void e16_drain_lane(bool has, uint32_t e, const float (*sm)[9], uint32_t *sc,
+__device__ __forceinline__ void e16_drain_lane(bool has, uint32_t hk, uint32_t p, const float (*sm)[9], uint32_t *sc,
                                                unsigned long long *ss, const float4 *__restrict__ pts, float thr,
                                                float lo, float hi, double fxs) {
     if (has) {
-        const uint32_t hk = e >> 25, p = e & 0x1FFFFFFu;
         const float4 pt = pts[p];
         float m[9];
 #pragma unroll
@@ -262,6 +263,27 @@ __device__ __forceinline__ void e16_drain_lane(bool has, uint32_t e, const float
     }
 }
 
+// one drain round over the lanes' top entries (every lane calls; q = this lane's column)
+__device__ __forceinline__ void e16_round(uint32_t &d, uint2 *q, uint32_t lane, uint32_t hf, const float (*sm)[9],
+                                          uint32_t *sc, unsigned long long *ss, const float4 *__restrict__ pts,
+                                          float thr, float lo, float hi, double fxs) {
+    const bool has = d > 0;
+    uint32_t hk = 0, p = 0;
+    e16_wave_sync();
+    if (has) {
+        const uint2 e = q[64 * (d - 1)];
+        const uint32_t m = e.x & 0xFFFFu, a = e.x >> 16;
+        const uint32_t b = (uint32_t)__builtin_ctz(m), j = 15u - b;  // bit 15 - j <-> hypothesis row j
+        const uint32_t rest = m & (m - 1u);
+        if (rest) q[64 * (d - 1)].x = rest | (a << 16);
+        else d--;
+        hk = 32 * a + (j & 3) + 4 * hf + 8 * (j >> 2);
+        p = e.y * 32 + (lane & 31);
+    }
+    e16_drain_lane(has, hk, p, sm, sc, ss, pts, thr, lo, hi, fxs);
+    e16_wave_sync();
+}
+
 // Workgroup = 4 waves; wave w owns listed positions [hb, hb + 64) and point chunk blockIdx.y.  A
 // fragment of tile a: lane l holds row l & 31 (position hb + 32 a + (l & 31)), coefficients 8 (l >> 5)
 // ..; the D register j of lane l holds row (j & 3) + 4 (l >> 5) + 8 (j >> 2), column l & 31.
@@ -273,7 +295,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     __shared__ float sM[4][kE16HW][9];
     __shared__ uint32_t sC[4][kE16HW];
     __shared__ unsigned long long sS[4][kE16HW];
-    __shared__ uint32_t sQ[4][kE16Lane][64];
+    __shared__ uint2 sQ[4][kE16Lane][64];
     const uint32_t K = list ? __builtin_amdgcn_readfirstlane(*list_n) : kmax;
     const uint32_t lane = threadIdx.x & 63, hf = lane >> 5;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -312,7 +334,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     e16_wave_sync();
     half8 bn1 = b0 < b1 ? feat[(2 * (size_t)b0) * 64 + lane] : half8{};
     half8 bn2 = b0 < b1 ? feat[(2 * (size_t)b0 + 1) * 64 + lane] : half8{};
-    uint32_t *const q = &sQ[wave][0][lane];
+    uint2 *const q = &sQ[wave][0][lane];
     for (uint32_t blk = b0; blk < b1; blk++) {
         const half8 bf1 = bn1, bf2 = bn2;
         if (blk + 1 < b1) {
@@ -325,37 +347,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
             acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A1[a], bf1, zero, 0, 0, 0);
             acc[a] = __builtin_amdgcn_mfma_f32_32x32x16_f16(A2[a], bf2, acc[a], 0, 0, 0);
         }
-        const uint32_t point = blk * 32 + (lane & 31);
 #pragma unroll
         for (int a = 0; a < kE16NA; a++) {
-            // drain rounds until the tile's pushes fit and fewer than kE16Round lanes hold an entry
+            // drain rounds until fewer than kE16Round lanes hold an entry and no stack is full
             for (;;) {
                 const uint64_t ne = __builtin_amdgcn_ballot_w64(d > 0);
-                if (__builtin_popcountll(ne) < (int)kE16Round && __builtin_amdgcn_ballot_w64(d > kE16Lane - 16) == 0)
+                if (__builtin_popcountll(ne) < (int)kE16Round && __builtin_amdgcn_ballot_w64(d >= kE16Lane) == 0)
                     break;
-                const bool has = d > 0;
-                d -= has ? 1u : 0u;
-                e16_wave_sync();
-                e16_drain_lane(has, q[64 * d], sM[wave], sC[wave], sS[wave], pts, thr, lo, hi, fxs);
-                e16_wave_sync();
+                e16_round(d, q, lane, hf, sM[wave], sC[wave], sS[wave], pts, thr, lo, hi, fxs);
             }
-            // push: every lane writes the slot above its top, a kept pair keeps it
-            const uint32_t e0 = ((uint32_t)(32 * a + 4 * hf) << 25) | point;
+            // the tile's keep mask (bit 15 - j: hypothesis row j), pushed when not empty
+            uint32_t m = 0;
 #pragma unroll
             for (int j = 0; j < 16; j++) {
-                q[64 * d] = e0 + ((uint32_t)((j & 3) + 8 * (j >> 2)) << 25);
-                d += fabsf(acc[a][j]) < Cv[a][j] ? 1u : 0u;
+                // kept iff |r~'| < C iff |r~'| - C < 0 (exact in sign with denormals kept; a NaN feature
+                // gives a positive NaN: not kept, as the compare); its sign bit shifted into m by one
+                // v_alignbit: m = (m << 1) | sign
+                const float t = fabsf(acc[a][j]) - Cv[a][j];
+                m = __builtin_amdgcn_alignbit(m, __float_as_uint(t), 31);
             }
+            q[64 * d] = make_uint2(m | ((uint32_t)a << 16), blk);
+            d += m != 0 ? 1u : 0u;
         }
     }
-    for (;;) {
-        if (__builtin_amdgcn_ballot_w64(d > 0) == 0) break;
-        const bool has = d > 0;
-        d -= has ? 1u : 0u;
-        e16_wave_sync();
-        e16_drain_lane(has, q[64 * d], sM[wave], sC[wave], sS[wave], pts, thr, lo, hi, fxs);
-        e16_wave_sync();
-    }
+    while (__builtin_amdgcn_ballot_w64(d > 0) != 0)
+        e16_round(d, q, lane, hf, sM[wave], sC[wave], sS[wave], pts, thr, lo, hi, fxs);
     e16_wave_sync();
     if (hb + lane < K) {
         cpart[(size_t)ch * kmax + hb + lane] = sC[wave][lane];
