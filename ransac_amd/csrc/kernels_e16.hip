@@ -25,8 +25,9 @@
 // the reference's chain) get zero rows and C = +inf (every pair to the exact stage); padding and
 // non-finite points get NaN features (never kept -- the reference never counts them).
 //
-// Kept pairs go through per-lane LDS stacks to the exact stage (essential_error_guarded: counts
-// exact, Σ terms within 2^-19 relative), drained in rounds of one entry per lane; counts and Σ (2^-fx fixed point,
+// The test builds each lane's 16-bit keep mask of a tile from sign bits (|r~'| - C < 0); non-empty masks
+// go onto per-lane LDS stacks and their pairs to the exact stage (essential_error_guarded: counts
+// exact, Σ terms within 2^-19 relative), one pair per lane per drain round; counts and Σ (2^-fx fixed point,
 // integer adds, deterministic) per point chunk, added by k_e16_finish.  Models are the listed
 // slots of the batch (list / list_n), as for k_score_f2.
 #include <hip/hip_runtime.h>
