@@ -288,7 +288,7 @@ __device__ __forceinline__ void e16_round(uint32_t &d, uint2 *q, uint32_t lane, 
 // Workgroup = 4 waves; wave w owns listed positions [hb, hb + 64) and point chunk blockIdx.y.  A
 // fragment of tile a: lane l holds row l & 31 (position hb + 32 a + (l & 31)), coefficients 8 (l >> 5)
 // ..; the D register j of lane l holds row (j & 3) + 4 (l >> 5) + 8 (j >> 2), column l & 31.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_score_e16(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_score_e16(
     const half8 *__restrict__ feat, const float4 *__restrict__ pts, uint32_t n, const half8 *__restrict__ rows,
     const float *__restrict__ cm, const float *__restrict__ models, size_t stride, const uint32_t *__restrict__ list,
     const uint32_t *__restrict__ list_n, uint32_t kmax, float thr, double fxs, uint32_t *__restrict__ cpart,
@@ -297,6 +297,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     __shared__ uint32_t sC[4][kE16HW];
     __shared__ unsigned long long sS[4][kE16HW];
     __shared__ uint2 sQ[4][kE16Lane][64];
+    __shared__ float sCv[4][kE16NA][2][16];  // the tiles' constants C by lane half (read per tile)
     const uint32_t K = list ? __builtin_amdgcn_readfirstlane(*list_n) : kmax;
     const uint32_t lane = threadIdx.x & 63, hf = lane >> 5;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -311,7 +312,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         sS[wave][lane] = 0;
     }
     half8 A1[kE16NA], A2[kE16NA];
-    float Cv[kE16NA][16];
 #pragma unroll
     for (int a = 0; a < kE16NA; a++) {
         const uint32_t pos = hb + 32 * a + (lane & 31);
@@ -320,10 +320,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         for (int j = 0; j < 8; j++) z[j] = (_Float16)0.0f;
         A1[a] = pos < K ? rows[4 * (size_t)pos + hf] : z;
         A2[a] = pos < K ? rows[4 * (size_t)pos + 2 + hf] : z;
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const uint32_t pj = hb + 32 * a + (j & 3) + 4 * hf + 8 * (j >> 2);
-            Cv[a][j] = pj < K ? cm[pj] : 0.0f;  // a missing hypothesis keeps nothing (|x| < 0 is false)
+        if ((lane & 31) < 16) {
+            const uint32_t j = lane & 15, pj = hb + 32 * a + (j & 3) + 4 * hf + 8 * (j >> 2);
+            sCv[wave][a][hf][j] = pj < K ? cm[pj] : 0.0f;  // a missing hypothesis keeps nothing
         }
     }
     const uint32_t nblk = (n + 31) / 32, nch = gridDim.y, ch = blockIdx.y;
@@ -357,14 +356,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
                     break;
                 e16_round(d, q, lane, hf, sM[wave], sC[wave], sS[wave], pts, thr, lo, hi, fxs);
             }
-            // the tile's keep mask (bit 15 - j: hypothesis row j), pushed when not empty
+            // the tile's keep mask (bit 15 - j: hypothesis row j), pushed when not empty; C read from LDS
+            // each tile (a broadcast read: 16 registers fewer, a fifth wave per SIMD)
+            __asm__ volatile("" ::: "memory");
+            float Cv[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) Cv[j] = sCv[wave][a][hf][j];
             uint32_t m = 0;
 #pragma unroll
             for (int j = 0; j < 16; j++) {
                 // kept iff |r~'| < C iff |r~'| - C < 0 (exact in sign with denormals kept; a NaN feature
                 // gives a positive NaN: not kept, as the compare); its sign bit shifted into m by one
                 // v_alignbit: m = (m << 1) | sign
-                const float t = fabsf(acc[a][j]) - Cv[a][j];
+                const float t = fabsf(acc[a][j]) - Cv[j];
                 m = __builtin_amdgcn_alignbit(m, __float_as_uint(t), 31);
             }
             q[64 * d] = make_uint2(m | ((uint32_t)a << 16), blk);

@@ -7,7 +7,8 @@
 //   k_e5_roots   lane / sample          : Newton divided differences -> degree-10 coefficients
 //                                         -> the candidate values (real roots, ascending);
 //                                         (sample, root) pairs appended to a list
-//   k_e5_check   lane / listed pair     : null vector of M(z), E, cheirality over the sample
+//   k_e5_null    lane / listed pair     : null vector of M(z) (x, y)
+//   k_e5_check   lane / listed pair     : E, cheirality over the sample
 //   k_e5_select  lane / sample          : 0 passing candidates: count -1; 1: that model; >= 2: the
 //                                         sample is listed for k_e5_order; counts 0 / -1 and the
 //                                         occupied-slot list (as k_solve_f7)
@@ -25,7 +26,8 @@
 // Workspace (e5_workspace_bytes(B)): samples int32[5][B], N double[36][B], dets double[11][B],
 // roots double[10][B], nroots int32[B], pair list uint32[10B] + counter, candidate E
 // float[9][10B], flags int32[10B], order list uint32[B] + counter, deferred list uint32[B] +
-// counter, rpoly zeros double[10][B], their numbers int32[B].
+// counter, rpoly zeros double[10][B], their numbers int32[B], the pairs' null vectors double[2][10B]
+// and found flags int32[10B].
 #include <hip/hip_runtime.h>
 
 #include "usac_device.hpp"
@@ -50,6 +52,8 @@ struct E5Work {
     uint32_t *defer, *ndefer;  // ... over k_e5_order's budget (k_e5_order_tail)
     double *jt;                // rpoly's real zeros of the listed samples, [r B + h]
     int32_t *njt;              // their numbers
+    double *xy;                // per listed pair: the null vector's x, y ([i], [10 B + i]; k_e5_null)
+    int32_t *xyok;             // ... found (null10)
 };
 
 __host__ __device__ inline size_t e5_align(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -72,7 +76,9 @@ __host__ __device__ inline E5Work e5_carve(void *base, uint32_t B) {
     w.defer = reinterpret_cast<uint32_t *>(p + off); off += e5_align(sizeof(uint32_t) * (size_t)B);
     w.ndefer = reinterpret_cast<uint32_t *>(p + off); off += e5_align(sizeof(uint32_t));
     w.jt = reinterpret_cast<double *>(p + off); off += e5_align(sizeof(double) * 10 * (size_t)B);
-    w.njt = reinterpret_cast<int32_t *>(p + off);
+    w.njt = reinterpret_cast<int32_t *>(p + off); off += e5_align(sizeof(int32_t) * (size_t)B);
+    w.xy = reinterpret_cast<double *>(p + off); off += e5_align(sizeof(double) * 20 * (size_t)B);
+    w.xyok = reinterpret_cast<int32_t *>(p + off);
     return w;
 }
 
@@ -83,7 +89,8 @@ size_t e5_workspace_bytes(uint32_t B) {
            e5_align(sizeof(uint32_t)) + e5_align(sizeof(float) * 90 * (size_t)B) +
            e5_align(sizeof(int32_t) * 10 * (size_t)B) + 2 * (e5_align(sizeof(uint32_t) * (size_t)B) +
            e5_align(sizeof(uint32_t))) + e5_align(sizeof(double) * 10 * (size_t)B) +
-           e5_align(sizeof(int32_t) * (size_t)B);
+           e5_align(sizeof(int32_t) * (size_t)B) + e5_align(sizeof(double) * 20 * (size_t)B) +
+           e5_align(sizeof(int32_t) * 10 * (size_t)B);
 }
 
 __global__ __launch_bounds__(64) void k_e5_basis(const float4 *__restrict__ pts, uint32_t n,
@@ -325,8 +332,12 @@ __global__ __launch_bounds__(64) void k_e5_order_tail(uint32_t B, E5Work w, cons
     }
 }
 
-__global__ __launch_bounds__(64) void k_e5_check(const float4 *__restrict__ pts, uint32_t B, uint32_t maxpairs,
-                                                 E5Work w) {
+// the candidate's null vector (five_points.cpp:181-190): M(z) and its elimination, the register-
+// heavy half of the candidate check, as its own kernel (two waves per SIMD, as k_e5_dets) so that
+// k_e5_check -- E, its SVD and the cheirality test -- runs at several waves per SIMD
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_e5_null(uint32_t B,
+                                                                                         uint32_t maxpairs,
+                                                                                         E5Work w) {
     const uint32_t i = blockIdx.x * 64 + threadIdx.x;
     const uint32_t np = *w.npairs;
     if (i >= np || i >= maxpairs) return;
@@ -337,8 +348,26 @@ __global__ __launch_bounds__(64) void k_e5_check(const float4 *__restrict__ pts,
     const double zz = w.roots[(size_t)r * B + h];
     double M[10][10], v[10];
     e5::matrix(N, zz, M);
-    if (!e5::null10(M, v)) return;
-    const double x = v[7], y = v[8];
+    const bool ok = e5::null10(M, v);
+    w.xyok[i] = ok ? 1 : 0;
+    if (ok) {
+        w.xy[i] = v[7];
+        w.xy[(size_t)10 * B + i] = v[8];
+    }
+}
+
+__global__ __launch_bounds__(64) void k_e5_check(const float4 *__restrict__ pts, uint32_t B, uint32_t maxpairs,
+                                                 E5Work w) {
+    const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+    const uint32_t np = *w.npairs;
+    if (i >= np || i >= maxpairs) return;
+    if (!w.xyok[i]) return;
+    const uint32_t rb = w.pairs[i];
+    const uint32_t r = rb / B, h = rb - r * B;
+    double N[4][9];
+    e5_load_basis(w, B, h, N);
+    const double zz = w.roots[(size_t)r * B + h];
+    const double x = w.xy[i], y = w.xy[(size_t)10 * B + i];
     double E[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) E[k] = N[0][k] * x + N[1][k] * y + N[2][k] * zz + N[3][k];
@@ -412,6 +441,7 @@ hipError_t launch_solve_e5(hipStream_t st, const float4 *pts, uint32_t n, const 
     hipLaunchKernelGGL(k_e5_basis, g1, dim3(64), 0, st, pts, n, samples_in, samples_out, B, ds, first_hyp, w);
     hipLaunchKernelGGL(k_e5_dets, g11, dim3(64), 0, st, B, w);
     hipLaunchKernelGGL(k_e5_roots, g1, dim3(64), 0, st, B, w);
+    hipLaunchKernelGGL(k_e5_null, g10, dim3(64), 0, st, B, 10 * B, w);
     hipLaunchKernelGGL(k_e5_check, g10, dim3(64), 0, st, pts, B, 10 * B, w);
     hipLaunchKernelGGL(k_e5_select, g1, dim3(64), 0, st, B, w, models, counts, list, list_n);
     // the order kernels hold one ~260-register wave per SIMD for hundreds of microseconds: on a CU-masked
