@@ -505,8 +505,8 @@ def _stage_kernels(estimator, sprt, chunks, stage):
     est = {"fundamental": 3, "essential": 4}.get(estimator, 2)
     if stage == "solve":
         return {2: ["usac::k_solve_h4("], 3: ["usac::k_solve_f7("],
-                4: ["usac::k_e5_basis(", "usac::k_e5_dets(", "usac::k_e5_roots(", "usac::k_e5_check(",
-                    "usac::k_e5_select(", "usac::k_e5_order(", "usac::k_e5_order_tail("]}[est]
+                4: ["usac::k_e5_basis(", "usac::k_e5_dets(", "usac::k_e5_roots(", "usac::k_e5_null(",
+                    "usac::k_e5_check(", "usac::k_e5_select(", "usac::k_e5_order(", "usac::k_e5_order_tail("]}[est]
     if sprt:
         return ["void usac::k_sprt_head<%d>(" % est, "void usac::k_sprt_tail<%d>(" % est]
     if est == 2:  # the matrix-core prefilter scorer (kernels_h16.hip; USAC_H16=0: k_presort_h + k_score_hf)
