@@ -9,8 +9,9 @@
 // kernel differ, 19-36 k lanes, all in lanes 48-63; none beside fp32 / fp64 VALU kernels or alone).
 // That was the round-5 "recount beside k_score_h16" miscount: the compiler's SLP
 // vectoriser had packed the exact residual of k_inl_flags.  The library therefore issues no packed
-// fp32 instruction: it is built with -fno-slp-vectorize -fno-vectorize and the pair arithmetic below
-// is two scalar operations (USAC_PACKED_F32=1 restores the packed form, for A/B timing only).
+// fp32 instruction: the backend's packed-fp32-ops feature is off (Makefile), so neither the
+// vectorisers nor these helpers can produce one, and the pair arithmetic below is written as two
+// scalar operations (USAC_PACKED_F32=1 keeps the vector-typed form, for A/B only).
 #include <hip/hip_runtime.h>
 
 namespace usac {

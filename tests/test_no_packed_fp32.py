@@ -24,7 +24,7 @@ def test_no_packed_fp32_in_code_objects(tmp_path):
     subprocess.run([OBJDUMP, "--offloading", str(local)], cwd=tmp_path, check=True, capture_output=True)
     objs = glob.glob(str(tmp_path / "lib.so.*gfx950*"))
     assert objs, "no gfx950 code object in the library"
-    pat = re.compile(r"\bv_pk_(fma|mul|add)_f32\b")
+    pat = re.compile(r"\bv_pk_((fma|mul|add)_f32|mov_b32)\b")  # the packed-fp32 family (Makefile: -packed-fp32-ops)
     n_instr = 0
     for o in objs:
         dis = subprocess.run([OBJDUMP, "-d", o], check=True, capture_output=True, text=True).stdout
