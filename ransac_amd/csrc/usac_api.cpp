@@ -393,6 +393,8 @@ struct usac_ctx {
     DevBuf lo_best;                  // the round's best count on the device (the graphs read it)
     int32_t *lo_best_pin = nullptr;  // its pinned host word
     size_t lo_best_pin_bytes = 0;
+    void *rec_pin = nullptr;  // usac_fetch_best's pinned staging (a pageable D2H copy is staged by the runtime)
+    size_t rec_pin_bytes = 0;
     // the loop's next batch drawn and run ahead of the current batch's replay (usac_ransac_run)
     hipStream_t spec_stream = nullptr;
     hipStream_t thin_stream = nullptr;  // CU-masked: the essential solver's root-order kernels
@@ -1969,6 +1971,7 @@ void usac_destroy(usac_ctx *c) {
         if (ev) StreamPool::get().give_back(ev);
     if (c->lo_stream) StreamPool::get().give_back(c->lo_stream);
     if (c->lo_best_pin) PinnedPool::get().give_back(c->lo_best_pin, c->lo_best_pin_bytes);
+    if (c->rec_pin) PinnedPool::get().give_back(c->rec_pin, c->rec_pin_bytes);
     if (c->spec_ev) StreamPool::get().give_back(c->spec_ev);
     if (c->spec_stream) StreamPool::get().give_back(c->spec_stream);
     if (c->thin_stream) StreamPool::get().give_back_masked(c->thin_stream);
@@ -2298,8 +2301,11 @@ int usac_last_counts(usac_ctx *c, int32_t *counts, float *sums, uint32_t n) {
 
 int usac_fetch_best(usac_ctx *c, usac_record *best) {
     if (!c || !best) return USAC_ERR_ARG;
-    HIP_TRY(c, hipMemcpyAsync(best, c->best.p, sizeof(usac_record), hipMemcpyDeviceToHost, c->stream));
+    if (!c->rec_pin && !(c->rec_pin = PinnedPool::get().take(sizeof(usac_record), &c->rec_pin_bytes)))
+        return fail(c, USAC_ERR_HIP, "pinned host allocation failed");
+    HIP_TRY(c, hipMemcpyAsync(c->rec_pin, c->best.p, sizeof(usac_record), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, stream_wait(c->stream));
+    memcpy(best, c->rec_pin, sizeof(usac_record));
     return USAC_OK;
 }
 
