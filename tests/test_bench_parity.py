@@ -121,3 +121,26 @@ def test_rccl_report_refuses_a_short_communicator():
     assert e.value.code == 4
     with pytest.raises(SystemExit):  # two ranks on one device
         bench.rccl_report(_FakeCommCtx(2, 0, 0), "rccl_allgather", _FakeDist([(2, 0, 0), (2, 1, 0)]), 2, 0)
+
+
+def test_cfg5_roofline_prices_a_kernel_its_runs_execute():
+    """the cfg5 line's roofline comes from the committed trace + PMC summary of
+    `bench.py --cfg5` itself (tools/profile_round.sh cfg5: workload batch 0, every dispatch of the
+    profiled runs), so the kernel it names is one those runs executed -- not the throughput batches'
+    matrix-core scorer, which usac_ransac_run does not use."""
+    import glob
+    import json
+    import os
+
+    r = bench.run_roofline(100000, 3.5)
+    assert r is not None, "no committed cfg5 summary (profiles/r*_summary.json, workload batch 0)"
+    src = json.load(open(os.path.join(ROOT, r["source"])))
+    assert src["workload"]["batch"] == 0 and src["workload"]["runs"] > 0
+    traced = {bench._kname_key(k) for k in src["kernels"]}
+    assert any(bench._kname_key(form % r["kernel"]) in traced for form in ("void usac::%s(", "usac::%s(")), r["kernel"]
+    assert "k_score_h16" not in r["kernel"]
+    assert 0.0 < r["frac"] <= 1.0 and r["kernels_by_device_time"][0]["kernel"] == r["kernel"]
+    # the summary's calls per run follow from its dispatch counts
+    for row in r["kernels_by_device_time"]:
+        assert row["calls_per_run"] > 0 and row["device_us_per_run"] > 0
+    assert glob.glob(os.path.join(ROOT, "profiles", "r*_cfg5_summary.json"))
