@@ -73,7 +73,7 @@ def parse():
                          "--warmup is a handful of steps (0 = off)")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="batches in flight: one context (stream + buffers) per in-flight batch, so batch i+1's "
-                         "solve overlaps batch i's scoring (default 3; essential 12 at N = 1, else 8: its "
+                         "solve overlaps batch i's scoring (default 3; essential 16 at N = 1, else 8: its "
                          "root-order kernels are long and narrow, DESIGN.md §6)")
     args = ap.parse_args()
     ess = args.estimator == "essential"
@@ -90,8 +90,8 @@ def parse():
         args.sampler = "prosac" if fund else "uniform"
     if args.batch is None:
         args.batch = 262144 if fund and args.sprt else 65536
-    if args.pipeline is None:  # essential: 12 in flight at N = 1 (the N > 1 exchange ring holds 8)
-        args.pipeline = (12 if args.gpus == 1 else 8) if ess else 3
+    if args.pipeline is None:  # essential: 16 in flight at N = 1 (the N > 1 exchange ring holds 8)
+        args.pipeline = (16 if args.gpus == 1 else 8) if ess else 3
     return args
 
 
