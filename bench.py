@@ -1148,7 +1148,9 @@ def main():
             best = c.fetch_best()
             if world > 1:
                 best = usac.merge_records(allgather(best))
-        t = c.last_timings()
+        # the in-pipeline HIP-event times of every fourth batch (three hipEventElapsedTime calls and
+        # their Python wrapping are host time inside the loop, and the 0.11 ms cfg2 steps feel it)
+        t = c.last_timings() if (i - args.warmup) % 4 == 0 else None
         return best, t
 
     def run(first_step, count, sink):
@@ -1185,9 +1187,10 @@ def main():
     first_box = []  # the first timed batch's merged record (checked against the oracle afterwards)
 
     def keep(rec, t):
-        score_ms.append(t["score_ms"])
-        solve_ms.append(t["solve_ms"])
-        batch_ms.append(t["batch_ms"])
+        if t is not None:
+            score_ms.append(t["score_ms"])
+            solve_ms.append(t["solve_ms"])
+            batch_ms.append(t["batch_ms"])
         if not first_box:
             first_box.append(rec)
         b = best_box[0]
