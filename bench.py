@@ -1099,6 +1099,8 @@ def main():
         elif napsac:  # grid neighbours built on the device at context setup (not timed)
             c.set_device_sampler(usac.SAMPLER.Napsac)
     ctx = ctxs[0]
+    for c in ctxs[1:]:  # in-pipeline timings from ctxs[0]'s batches (finish)
+        c.set_timing(False)
     exchange = "none"
     if world > 1:  # the per-batch best-record exchange: RCCL all-gather on the context stream
         uid = [usac.Context.comm_unique_id() if rank == 0 else None]
@@ -1148,9 +1150,10 @@ def main():
             best = c.fetch_best()
             if world > 1:
                 best = usac.merge_records(allgather(best))
-        # the in-pipeline HIP-event times of every fourth batch (three hipEventElapsedTime calls and
-        # their Python wrapping are host time inside the loop, and the 0.11 ms cfg2 steps feel it)
-        t = c.last_timings() if (i - args.warmup) % 4 == 0 else None
+        # the in-pipeline HIP-event times of the first context's batches only (the others record no
+        # events: four event records, three elapsed-time queries and their Python wrapping per batch
+        # are host time inside the loop, and the 0.11 ms cfg2 steps feel it)
+        t = c.last_timings() if i % P == 0 else None
         return best, t
 
     def run(first_step, count, sink):
@@ -1194,7 +1197,7 @@ def main():
         if not first_box:
             first_box.append(rec)
         b = best_box[0]
-        if b is None or usac.merge_records([rec, b]).hyp_index == rec.hyp_index:
+        if b is None or not usac.record_better(b, rec):  # usac_merge_records([rec, b]) in Python
             best_box[0] = rec
 
     t0 = time.perf_counter()
@@ -1277,9 +1280,10 @@ def main():
                     "measured bytes) is a small fraction of HBM peak; algorithmic_equiv_gbs = SURVEY §8(d) bytes "
                     "(16 B x N per hypothesis) / kernel time, a re-read-equivalent rate, not a roofline fraction",
             "score_kernel_ms": avg_score_ms,
-            "solve_kernel_ms": avg_solve_ms, "kernel_ms_in_pipeline": float(np.mean(score_ms)),
-            "solve_kernel_ms_in_pipeline": float(np.mean(solve_ms)),
-            "batch_device_ms_in_pipeline": float(np.mean(batch_ms))})
+            # (the first context's timed batches; None when none of them fell in the timed steps)
+            "solve_kernel_ms": avg_solve_ms, "kernel_ms_in_pipeline": float(np.mean(score_ms)) if score_ms else None,
+            "solve_kernel_ms_in_pipeline": float(np.mean(solve_ms)) if solve_ms else None,
+            "batch_device_ms_in_pipeline": float(np.mean(batch_ms)) if batch_ms else None})
         smp_name = {"prosac": "Prosac (reference subset schedule, T_N = 200000)",
                     "napsac": "Napsac (grid neighbours, cell 50, built on the device)"}.get(args.sampler, "Uniform")
         out = {

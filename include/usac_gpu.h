@@ -59,7 +59,7 @@
 extern "C" {
 #endif
 
-#define USAC_ABI_VERSION 13
+#define USAC_ABI_VERSION 14
 
 /* = enum ESTIMATOR (usac/model.hpp:10) */
 enum { USAC_LINE2D = 1, USAC_HOMOGRAPHY = 2, USAC_FUNDAMENTAL = 3, USAC_ESSENTIAL = 4 };
@@ -212,6 +212,10 @@ int usac_sync(usac_ctx *ctx);
 /* Device time of the last async batch's kernels, measured with HIP events on the
  * context stream: [0] whole batch, [1] score kernel, [2] solve kernel (ms). */
 int usac_last_timings(usac_ctx *ctx, float *ms3);
+/* ABI 14: on = 0 stops usac_hypothesize_async recording those HIP events on this context (four
+ * event records of host time per batch; usac_last_timings then keeps returning the last timed
+ * batch's values); on = 1 (the default) records them again. */
+int usac_set_timing(usac_ctx *ctx, int on);
 /* Score-kernel split factor (point chunks per hypothesis tile, 1 = exact sequential sums):
  * 1, 2, 4, 8, 16; any of 1..128 for the fundamental / essential estimators (their chunks are
  * separate workgroups, combined in chunk order; default 96). */

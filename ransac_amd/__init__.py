@@ -120,7 +120,7 @@ ABI_SYMBOLS = [
     "usac_termination_bound", "usac_prosac_termination", "usac_termination_destroy", "usac_sprt_create",
     "usac_sprt_verify", "usac_sprt_upper_bound", "usac_sprt_stats", "usac_sprt_replay", "usac_sprt_destroy",
     "usac_lo_create", "usac_lo_get_model_score", "usac_lo_iters", "usac_lo_destroy", "usac_batch_sprt_info",
-    "usac_selftest_rpoly", "usac_selftest_logexp",
+    "usac_selftest_rpoly", "usac_selftest_logexp", "usac_set_timing",
 ]
 
 
@@ -169,6 +169,7 @@ def lib():
         "usac_fetch_best": (ctypes.c_int, [_vp, _P(Record)]),
         "usac_sync": (ctypes.c_int, [_vp]),
         "usac_last_timings": (ctypes.c_int, [_vp, f32p]),
+        "usac_set_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
         "usac_std_termination": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32,
                                                    ctypes.c_float, ctypes.c_uint32]),
         "usac_ransac_run": (ctypes.c_int, [_vp, _P(_Params), _P(_RunOutput), i32p, _P(Record), ctypes.c_uint32]),
@@ -511,6 +512,10 @@ class Context:
     def sync(self):
         self._check(lib().usac_sync(self._h), "sync")
 
+    def set_timing(self, on):
+        """usac_set_timing (ABI 14): record the batches' HIP events (default) or not."""
+        self._check(lib().usac_set_timing(self._h, 1 if on else 0), "set_timing")
+
     def last_timings(self):
         ms = np.zeros(3, dtype=np.float32)
         self._check(lib().usac_last_timings(self._h, _ptr(ms, ctypes.c_float)), "last_timings")
@@ -554,6 +559,20 @@ class Context:
         allr = (Record * self.nranks)()
         self._check(lib().usac_exchange_best_wait(self._h, slot, allr), "exchange_best_wait")
         return list(allr)
+
+
+def record_better(a, b):
+    """usac_merge_records' order in Python (usac_api.cpp rec_better): a valid record beats an invalid
+    one, then more inliers, then the larger Σ score (Score::bigger), then the earlier hypothesis."""
+    if not a.valid:
+        return False
+    if not b.valid:
+        return True
+    if a.inliers != b.inliers:
+        return a.inliers > b.inliers
+    if a.score != b.score:
+        return a.score > b.score
+    return a.hyp_index < b.hyp_index
 
 
 def merge_records(records):

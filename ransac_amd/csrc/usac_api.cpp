@@ -428,6 +428,7 @@ struct usac_ctx {
     bool batch_valid = false;  // counts / sums hold a batch's scores (usac_last_counts)
     uint32_t sprt_S = 0;       // model slots of the last batch-SPRT launch (usac_batch_sprt_info)
     bool timed_pending = false;
+    bool timing_on = true;  // usac_set_timing
     std::string err;
 };
 
@@ -2228,15 +2229,16 @@ int usac_hypothesize_async(usac_ctx *c, uint32_t B, uint64_t seed, uint64_t firs
     int rc = ensure_batch(c, B);
     if (rc) return rc;
     HIP_TRY(c, hipSetDevice(c->device));
-    HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
+    const bool tm = c->timing_on;
+    if (tm) HIP_TRY(c, hipEventRecord(c->ev[0], c->stream));
     HIP_TRY(c, enqueue_solve(c, nullptr, B, seed, first_hyp, nullptr, h16_solver_thr(c, c->chunks, thr)));
-    HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
+    if (tm) HIP_TRY(c, hipEventRecord(c->ev[1], c->stream));
     HIP_TRY(c, enqueue_score(c, B, thr, c->chunks, h16_defer()));
     c->batch_valid = true;
-    HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
+    if (tm) HIP_TRY(c, hipEventRecord(c->ev[2], c->stream));
     HIP_TRY(c, batch_argmax(c, B * c->spk, first_hyp));
-    HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
-    c->timed_pending = true;
+    if (tm) HIP_TRY(c, hipEventRecord(c->ev[3], c->stream));
+    c->timed_pending = tm;
     return USAC_OK;
 }
 
@@ -2312,6 +2314,12 @@ int usac_fetch_best(usac_ctx *c, usac_record *best) {
 int usac_sync(usac_ctx *c) {
     if (!c) return USAC_ERR_ARG;
     HIP_TRY(c, stream_wait(c->stream));
+    return USAC_OK;
+}
+
+int usac_set_timing(usac_ctx *c, int on) {
+    if (!c) return USAC_ERR_ARG;
+    c->timing_on = on != 0;
     return USAC_OK;
 }
 

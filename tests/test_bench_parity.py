@@ -144,3 +144,21 @@ def test_cfg5_roofline_prices_a_kernel_its_runs_execute():
     for row in r["kernels_by_device_time"]:
         assert row["calls_per_run"] > 0 and row["device_us_per_run"] > 0
     assert glob.glob(os.path.join(ROOT, "profiles", "r*_cfg5_summary.json"))
+
+
+def test_record_better_equals_merge_records(usac):
+    """bench.py keeps the timed batches' best with usac.record_better (no ctypes round trip per
+    step); it must order records exactly as the library's usac_merge_records (host-only code)."""
+    rng = np.random.default_rng(4)
+    recs = []
+    for _ in range(400):
+        r = usac.Record()
+        r.hyp_index = int(rng.integers(0, 50))
+        r.inliers = int(rng.integers(-1, 4))
+        r.score = float(np.float32(rng.choice([0.5, 1.0, 1.5])))
+        r.valid = int(rng.random() < 0.85)
+        recs.append(r)
+    for a, b in zip(recs[::2], recs[1::2]):
+        m = usac.merge_records([b, a])  # b unless a is better
+        w = a if usac.record_better(a, b) else b
+        assert (m.hyp_index, m.inliers, m.score, m.valid) == (w.hyp_index, w.inliers, w.score, w.valid)
