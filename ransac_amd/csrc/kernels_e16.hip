@@ -264,13 +264,14 @@ __device__ __forceinline__ void e16_drain_lane(bool has, uint32_t hk, uint32_t p
     }
 }
 
-// one drain round over the lanes' top entries (every lane calls; q = this lane's column)
+// one drain round over the lanes' top entries (every lane calls; q = this lane's column).  No
+// barrier: a lane's stack is its own (a wave's LDS operations complete in order), the models are
+// read-only after the kernel's first barrier and the counters take LDS atomics
 __device__ __forceinline__ void e16_round(uint32_t &d, uint2 *q, uint32_t lane, uint32_t hf, const float (*sm)[9],
                                           uint32_t *sc, unsigned long long *ss, const float4 *__restrict__ pts,
                                           float thr, float lo, float hi, double fxs) {
     const bool has = d > 0;
     uint32_t hk = 0, p = 0;
-    e16_wave_sync();
     if (has) {
         const uint2 e = q[64 * (d - 1)];
         const uint32_t m = e.x & 0xFFFFu, a = e.x >> 16;
@@ -282,7 +283,6 @@ __device__ __forceinline__ void e16_round(uint32_t &d, uint2 *q, uint32_t lane, 
         p = e.y * 32 + (lane & 31);
     }
     e16_drain_lane(has, hk, p, sm, sc, ss, pts, thr, lo, hi, fxs);
-    e16_wave_sync();
 }
 
 // Workgroup = 4 waves; wave w owns listed positions [hb, hb + 64) and point chunk blockIdx.y.  A
