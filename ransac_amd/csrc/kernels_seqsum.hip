@@ -206,11 +206,16 @@ __global__ __launch_bounds__(256) void k_seq_link(const typename Op<F64>::V *__r
     const uint32_t S = (n + L - 1) / L;
     const double *psum = reinterpret_cast<const double *>(scratch + w * sstride);
     const float *R = reinterpret_cast<const float *>(scratch + w * sstride + sizeof(double) * kSegMax * NCH);
+    static_assert(kCand == 256, "thread = candidate");
+    // every row's load in flight at once (the scratch holds kSegMax rows; rows >= S are read and
+    // dropped): a strided loop here was one dependent round trip per row, ~14 us per link
+    float r[kSegMax];
+#pragma unroll
+    for (uint32_t j = 0; j < kSegMax; j++) r[j] = R[((size_t)j * NCH + q) * kCand + threadIdx.x];
     if (threadIdx.x < S) sp[threadIdx.x] = psum[threadIdx.x * NCH + q];
-    for (uint32_t i = threadIdx.x; i < S * kCand; i += 256) {
-        const uint32_t j = i / kCand, c = i % kCand;
-        sR[j][c] = R[((size_t)j * NCH + q) * kCand + c];
-    }
+#pragma unroll
+    for (uint32_t j = 0; j < kSegMax; j++)
+        if (j < S) sR[j][threadIdx.x] = r[j];
     __syncthreads();
     if (threadIdx.x >= 64) return;
     const typename Op<F64>::V *__restrict__ v = vals + w * vstride;
