@@ -146,14 +146,23 @@ __global__ __launch_bounds__(256) void k_norm_dist(const float4 *__restrict__ q_
     const float mx1 = sums4[4 * w + 0] / (float)n, my1 = sums4[4 * w + 1] / (float)n;
     const float mx2 = sums4[4 * w + 2] / (float)n, my2 = sums4[4 * w + 3] / (float)n;
     double a0 = 0.0, a1 = 0.0;
-    for (uint32_t i = j * L + threadIdx.x; i < e; i += 256) {
-        const float4 p = q[i];
-        const float xm1 = p.x - mx1, ym1 = p.y - my1;
-        const float xm2 = p.z - mx2, ym2 = p.w - my2;
-        const double d1 = sqrt((double)(xm1 * xm1 + ym1 * ym1)), d2 = sqrt((double)(xm2 * xm2 + ym2 * ym2));
-        sq[i] = make_double2(d1, d2);
-        a0 += d1;
-        a1 += d2;
+    for (uint32_t i0 = j * L + threadIdx.x; i0 < e; i0 += 4 * 256) {  // four points' loads in flight
+        float4 pv[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (i0 + 256 * u < e) pv[u] = q[i0 + 256 * u];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = i0 + 256 * u;
+            if (i >= e) break;
+            const float4 p = pv[u];
+            const float xm1 = p.x - mx1, ym1 = p.y - my1;
+            const float xm2 = p.z - mx2, ym2 = p.w - my2;
+            const double d1 = sqrt((double)(xm1 * xm1 + ym1 * ym1)), d2 = sqrt((double)(xm2 * xm2 + ym2 * ym2));
+            sq[i] = make_double2(d1, d2);
+            a0 += d1;
+            a1 += d2;
+        }
     }
     red[0][threadIdx.x] = a0;
     red[1][threadIdx.x] = a1;

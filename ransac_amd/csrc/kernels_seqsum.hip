@@ -45,9 +45,20 @@ __global__ __launch_bounds__(256) void k_seq_psum(const typename Op<F64>::V *__r
     double acc[NCH];
 #pragma unroll
     for (int q = 0; q < NCH; q++) acc[q] = 0.0;
-    for (uint32_t k = j * L + threadIdx.x; k < e; k += 256)
+    for (uint32_t k0 = j * L + threadIdx.x; k0 < e; k0 += 4 * 256) {  // four elements' loads in flight
+        typename Op<F64>::V x[4][NCH];
 #pragma unroll
-        for (int q = 0; q < NCH; q++) acc[q] += Op<F64>::wide(v[(size_t)k * NCH + q]);
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+            for (int q = 0; q < NCH; q++) {
+                const uint32_t k = k0 + 256 * u;
+                x[u][q] = k < e ? v[(size_t)k * NCH + q] : typename Op<F64>::V(0);
+            }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+            for (int q = 0; q < NCH; q++) acc[q] += Op<F64>::wide(x[u][q]);
+    }
 #pragma unroll
     for (int q = 0; q < NCH; q++) red[q][threadIdx.x] = acc[q];
     __syncthreads();
