@@ -1,6 +1,6 @@
 #!/bin/bash
 # round-6 head after the seqsum load fixes: each config default bench line and rocprof stats of
-# cfg2 / cfg4 / cfg5 (the GPU suite and smoke at the same build: tools/r6/gpu_r6t.sh)
+# cfg2 / cfg4 / cfg5 (the GPU suite and smoke at the same build: tools/r6/gpu_r6s5.sh)
 set -o pipefail
 O=gpurun_out/r6final3; mkdir -p $O
 export TMPDIR=/tmp

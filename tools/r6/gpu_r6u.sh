@@ -1,11 +1,16 @@
 #!/bin/bash
-# cfg5 line forms on one box: the default command (100 timed runs after 10 warm-up runs) and the
-# 20 / 2 form of the round's earlier tables, interleaved twice
+# cfg4: batches in flight beyond 8 (N = 1) and hardware queues
 set -o pipefail
 O=gpurun_out/r6u; mkdir -p $O
-for r in 1 2; do
-  timeout -k 10 200 python -u bench.py --cfg5 --cpu-seconds 0 > $O/cfg5_default_$r.json 2> $O/cfg5_default_$r.err || { echo "cfg5 default failed"; exit 1; }
-  timeout -k 10 200 python -u bench.py --cfg5 --steps 20 --warmup 2 --cpu-seconds 0 > $O/cfg5_s20_$r.json 2> $O/cfg5_s20_$r.err || { echo "cfg5 s20 failed"; exit 1; }
-  timeout -k 10 200 python -u bench.py --cfg5 --steps 20 --warmup 10 --cpu-seconds 0 > $O/cfg5_s20w10_$r.json 2> $O/cfg5_s20w10_$r.err || { echo "cfg5 s20w10 failed"; exit 1; }
-  for v in default s20 s20w10; do python3 -c "import json;d=json.load(open('$O/cfg5_${v}_$r.json'));print('$v', d['steps'], d['warmup'], d['ms_per_step'], all(d['parity'].values()))"; done
-done
+run() {  # name, env..., -- bench args
+  local n=$1; shift
+  env "$@" > $O/$n.json 2> $O/$n.err || { echo "bench $n failed"; tail -5 $O/$n.err; exit 1; }
+  python3 -c "import json;d=json.load(open('$O/$n.json'));print('$n', round(d['value']/1e6,2), round(d['ms_per_step'],4), d.get('parity',{}).get('ok'))"
+}
+B="timeout -k 10 200 python -u bench.py --estimator essential --steps 30 --warmup 5 --cpu-seconds 0"
+run p8 $B --pipeline 8
+run p12 $B --pipeline 12
+run p16 $B --pipeline 16
+run p12_q24 GPU_MAX_HW_QUEUES=24 $B --pipeline 12
+run p16_q32 GPU_MAX_HW_QUEUES=32 $B --pipeline 16
+run p8b $B --pipeline 8
