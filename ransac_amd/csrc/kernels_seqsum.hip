@@ -138,19 +138,22 @@ __global__ __launch_bounds__(kCand) void k_seq_seg(const typename Op<F64>::V *__
 }
 
 // The same segment ends with the chains split over the waves: workgroup (segment j, fit b) of
-// kCand * NCH threads, thread t runs chain q = t / kCand (wave-uniform) from candidate
-// c = t % kCand -- one dependent chain per lane instead of NCH interleaved ones, NCH times the
-// waves to hide its latency.  The chunk is staged transposed ([chain][element]) so a wave reads
-// its chain's next elements with 16-byte broadcast reads.  Same starts, same ops, same ends.
-template <int NCH, bool F64>
-__global__ __launch_bounds__(kCand *NCH) void k_seq_seg_split(const typename Op<F64>::V *__restrict__ vals,
-                                                              size_t vstride, const uint32_t *__restrict__ ns,
-                                                              uint32_t n1, const uint32_t *__restrict__ slots,
-                                                              char *scratch, size_t sstride) {
+// kCand * NCH / CPL threads, thread t runs chain q = t / (kCand / CPL) (wave-uniform) from the
+// CPL candidates c + u kCand / CPL, c = t % (kCand / CPL) -- CPL independent dependent chains
+// per lane, every element read once from LDS for all of them.  The chunk is staged transposed
+// ([chain][element]) so a wave reads its chain's next elements with 16-byte broadcast reads.
+// Same starts, same ops, same ends.
+template <int NCH, bool F64, int CPL>
+__global__ __launch_bounds__(kCand *NCH / CPL) void k_seq_seg_split(const typename Op<F64>::V *__restrict__ vals,
+                                                                    size_t vstride, const uint32_t *__restrict__ ns,
+                                                                    uint32_t n1, const uint32_t *__restrict__ slots,
+                                                                    char *scratch, size_t sstride) {
     typedef typename Op<F64>::V V;
-    constexpr uint32_t kT = kCand * NCH;                 // threads
+    constexpr uint32_t kLanes = kCand / CPL;             // threads per chain
+    static_assert(kLanes % 64 == 0, "a chain's threads are whole waves");
+    constexpr uint32_t kT = kLanes * NCH;                // threads
     constexpr uint32_t kChunk = 1024;                    // elements per LDS chunk
-    constexpr uint32_t kPer = kChunk * NCH / kT;         // values per thread per chunk (4)
+    constexpr uint32_t kPer = kChunk * NCH / kT;         // values per thread per chunk (4 CPL)
     constexpr uint32_t kVec = 16 / sizeof(V);            // elements per 16-byte read
     typedef V Vv __attribute__((ext_vector_type(kVec)));
     __shared__ __attribute__((aligned(16))) V sv[2][NCH][kChunk + kVec];  // rows padded 16 B: no bank conflicts
@@ -164,7 +167,7 @@ __global__ __launch_bounds__(kCand *NCH) void k_seq_seg_split(const typename Op<
     const V *__restrict__ v = vals + w * vstride + (size_t)b * NCH;
     const uint32_t tot = (e - b) * NCH;
     const uint32_t t = threadIdx.x;
-    const uint32_t q = __builtin_amdgcn_readfirstlane(t / kCand), c = t % kCand;
+    const uint32_t q = __builtin_amdgcn_readfirstlane(t / kLanes), c = t % kLanes;
     V pre[kPer];
     auto fetch = [&](uint32_t ch) {
 #pragma unroll
@@ -176,7 +179,12 @@ __global__ __launch_bounds__(kCand *NCH) void k_seq_seg_split(const typename Op<
     fetch(0);
     for (uint32_t i = t; i < j * NCH; i += kT) sp[i] = psum[i];
     __syncthreads();
-    float s = cand_start(centre(sp, j, NCH, q), c);
+    float s[CPL];
+    {
+        const float ctr = centre(sp, j, NCH, q);
+#pragma unroll
+        for (int u = 0; u < CPL; u++) s[u] = cand_start(ctr, c + kLanes * u);
+    }
     const uint32_t nch = (e - b + kChunk - 1) / kChunk;
     for (uint32_t ch = 0; ch < nch; ch++) {
 #pragma unroll
@@ -196,11 +204,18 @@ __global__ __launch_bounds__(kCand *NCH) void k_seq_seg_split(const typename Op<
 #pragma unroll
             for (uint32_t u = 0; u < 8 / kVec; u++)
 #pragma unroll
-                for (uint32_t z = 0; z < kVec; z++) s = Op<F64>::step(s, x[u][z]);
+                for (uint32_t z = 0; z < kVec; z++)
+#pragma unroll
+                    for (int a = 0; a < CPL; a++) s[a] = Op<F64>::step(s[a], x[u][z]);
         }
-        for (; k < m; k++) s = Op<F64>::step(s, buf[k]);
+        for (; k < m; k++) {
+            const V x = buf[k];
+#pragma unroll
+            for (int a = 0; a < CPL; a++) s[a] = Op<F64>::step(s[a], x);
+        }
     }
-    R[((size_t)j * NCH + q) * kCand + c] = s;
+#pragma unroll
+    for (int a = 0; a < CPL; a++) R[((size_t)j * NCH + q) * kCand + c + kLanes * a] = s[a];
 }
 
 // link: workgroup (chain q, fit b); the four waves stage the chain's candidate ends into
@@ -271,6 +286,17 @@ static bool seg_split() {
     }();
     return on;
 }
+// candidates per lane of the split kernel: 2 for the fp32 chains (the four coordinate means:
+// 15.9 -> 12.8 us per fit batch), 1 for the fp64-addend ones (21.3 / 21.2 us with 1 / 2, 27.8
+// with 4); USAC_SEQ_CPL = 1, 2 or 4 sets both, for A/B
+static int seg_cpl(bool f64) {
+    static const int cpl = [] {
+        const char *e = getenv("USAC_SEQ_CPL");
+        const int v = e ? atoi(e) : 0;
+        return v == 1 || v == 2 || v == 4 ? v : 0;
+    }();
+    return cpl ? cpl : f64 ? 1 : 2;
+}
 
 hipError_t launch_seqsum(hipStream_t st, int nch, bool f64, const void *vals, size_t vstride, const uint32_t *ns,
                          uint32_t n1, uint32_t W, const uint32_t *slots, void *scratch, size_t sstride,
@@ -284,9 +310,15 @@ hipError_t launch_seqsum(hipStream_t st, int nch, bool f64, const void *vals, si
         const V_ *v_ = static_cast<const V_ *>(vals);                                                               \
         if (!have_psum)                                                                                             \
             hipLaunchKernelGGL((k_seq_psum<N, D>), gs, dim3(256), 0, st, v_, vstride, ns, n1, slots, scr, sstride); \
-        if (N > 1 && seg_split())                                                                                   \
-            hipLaunchKernelGGL((k_seq_seg_split<N, D>), gs, dim3(kCand * N), 0, st, v_, vstride, ns, n1, slots, scr,   \
-                               sstride);                                                                            \
+        if (N > 1 && seg_split() && seg_cpl(D) == 4)                                                                 \
+            hipLaunchKernelGGL((k_seq_seg_split<N, D, 4>), gs, dim3(kCand * N / 4), 0, st, v_, vstride, ns, n1, slots, \
+                               scr, sstride);                                                                       \
+        else if (N > 1 && seg_split() && seg_cpl(D) == 2)                                                            \
+            hipLaunchKernelGGL((k_seq_seg_split<N, D, 2>), gs, dim3(kCand * N / 2), 0, st, v_, vstride, ns, n1, slots, \
+                               scr, sstride);                                                                       \
+        else if (N > 1 && seg_split())                                                                              \
+            hipLaunchKernelGGL((k_seq_seg_split<N, D, 1>), gs, dim3(kCand * N), 0, st, v_, vstride, ns, n1, slots,     \
+                               scr, sstride);                                                                       \
         else                                                                                                        \
             hipLaunchKernelGGL((k_seq_seg<N, D>), gs, dim3(kCand), 0, st, v_, vstride, ns, n1, slots, scr, sstride);  \
         hipLaunchKernelGGL((k_seq_link<N, D>), gl, dim3(256), 0, st, v_, vstride, ns, n1, slots, scr, sstride, out); \
