@@ -96,7 +96,6 @@ __global__ __launch_bounds__(kInlThreads) void k_inl_flags(const void *__restric
                                                            uint32_t *__restrict__ scratch,
                                                            const int32_t *__restrict__ ok) {
     typedef typename std::conditional<EST == USAC_LINE2D, float2, float4>::type P;
-    __shared__ float sm[18];
     __shared__ uint32_t wsum[kInlThreads / 64];
     // the points' loads go out first: they do not depend on the model, whose slot, ok word and
     // parameters are three dependent loads of their own
@@ -107,12 +106,14 @@ __global__ __launch_bounds__(kInlThreads) void k_inl_flags(const void *__restric
         if (i < n) pv[u] = static_cast<const P *>(pts)[i];
     }
     const uint32_t w = inl_slot(slots, blockIdx.y);
-    if (ok && !ok[w]) return;  // a failed fit: k_inl_compact skips the slot too
-    inl_model<EST>(models + 9 * (size_t)w, sm);
-    const float t = thrs ? thrs[w] : thr;
+    // the model, its threshold and its ok word: independent (uniform) loads, all in flight; every
+    // lane derives H^-1 itself (the same operations as one lane would: no LDS round trip, no barrier)
     float m[18];
 #pragma unroll
-    for (int k = 0; k < 18; k++) m[k] = sm[k];
+    for (int k = 0; k < 9; k++) m[k] = models[9 * (size_t)w + k];
+    const float t = thrs ? thrs[w] : thr;
+    if (ok && !ok[w]) return;  // a failed fit: k_inl_compact skips the slot too
+    if constexpr (EST == USAC_HOMOGRAPHY) inv3x3(m, m + 9);
     float *all_e = reinterpret_cast<float *>(scratch + w * inl_stride(n) + inl_all_offset(n));
     uint32_t cnt = 0;
 #pragma unroll
@@ -153,12 +154,12 @@ __global__ __launch_bounds__(kInlThreads) void k_inl_compact(const void *__restr
         const uint32_t i = blockIdx.x * kInlBlock + u * kInlThreads + threadIdx.x;
         e[u] = i < n ? all_e[i] : 0.f;
     }
+    const float t = thrs ? thrs[ws] : thr;  // in flight with the ok word
     if (ok && !ok[ws]) {  // a failed fit: its list is left as it was (workgroup-uniform) and its
         // count reads 0, so the Σ pass over this slot (launch_seqsum) sums nothing
         if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) totals[ws] = 0;
         return;
     }
-    const float t = thrs ? thrs[ws] : thr;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint64_t bal[kInlPer];
 #pragma unroll
