@@ -297,6 +297,18 @@ static int seg_cpl(bool f64) {
     }();
     return cpl ? cpl : f64 ? 1 : 2;
 }
+// one-chain sums (Σerr) through the split kernel with this many candidates per lane
+// (USAC_SEQ1_CPL = 1, 2 or 4; unset or 0: k_seq_seg).  One per lane runs as fast as k_seq_seg
+// (6.7 / 6.8 us) with half its LDS; the cfg5 / cfg3-exact lines split both ways over two boxes
+// (DESIGN §7 round 6), so k_seq_seg stays the default
+static int seg1_cpl() {
+    static const int cpl = [] {
+        const char *e = getenv("USAC_SEQ1_CPL");
+        const int v = e ? atoi(e) : 0;
+        return v == 1 || v == 2 || v == 4 ? v : 0;
+    }();
+    return cpl;
+}
 
 hipError_t launch_seqsum(hipStream_t st, int nch, bool f64, const void *vals, size_t vstride, const uint32_t *ns,
                          uint32_t n1, uint32_t W, const uint32_t *slots, void *scratch, size_t sstride,
@@ -310,7 +322,16 @@ hipError_t launch_seqsum(hipStream_t st, int nch, bool f64, const void *vals, si
         const V_ *v_ = static_cast<const V_ *>(vals);                                                               \
         if (!have_psum)                                                                                             \
             hipLaunchKernelGGL((k_seq_psum<N, D>), gs, dim3(256), 0, st, v_, vstride, ns, n1, slots, scr, sstride); \
-        if (N > 1 && seg_split() && seg_cpl(D) == 4)                                                                 \
+        if (N == 1 && seg1_cpl() == 2)                                                                              \
+            hipLaunchKernelGGL((k_seq_seg_split<N, D, 2>), gs, dim3(kCand * N / 2), 0, st, v_, vstride, ns, n1, slots, \
+                               scr, sstride);                                                                       \
+        else if (N == 1 && seg1_cpl() == 4)                                                                         \
+            hipLaunchKernelGGL((k_seq_seg_split<N, D, 4>), gs, dim3(kCand * N / 4), 0, st, v_, vstride, ns, n1, slots, \
+                               scr, sstride);                                                                       \
+        else if (N == 1 && seg1_cpl() == 1)                                                                         \
+            hipLaunchKernelGGL((k_seq_seg_split<N, D, 1>), gs, dim3(kCand * N), 0, st, v_, vstride, ns, n1, slots,     \
+                               scr, sstride);                                                                       \
+        else if (N > 1 && seg_split() && seg_cpl(D) == 4)                                                                 \
             hipLaunchKernelGGL((k_seq_seg_split<N, D, 4>), gs, dim3(kCand * N / 4), 0, st, v_, vstride, ns, n1, slots, \
                                scr, sstride);                                                                       \
         else if (N > 1 && seg_split() && seg_cpl(D) == 2)                                                            \
